@@ -1,0 +1,533 @@
+// pybind11 / torch bindings of the native layer (module `pytorchdistributed_amd._C`).
+//
+// Kernel bindings validate shapes, dtypes and devices on the host BEFORE launching (a bad launch on
+// a shared MI355X box can reset the node), run on the current HIP stream of the tensor's device,
+// and raise on any HIP error.  Runtime bindings (TCP store, bucket reducer, host ring) are CPU-only.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "pda_kernels.h"
+#include "runtime.h"
+
+namespace py = pybind11;
+using at::Tensor;
+
+namespace {
+
+#define CHECK_HIP_OK(expr)                                                                  \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    TORCH_CHECK(_e == hipSuccess, "HIP error in " #expr ": ", hipGetErrorString(_e));      \
+  } while (0)
+
+hipStream_t stream_of(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_bf16(const Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16");
+}
+void check_f32(const Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be float32");
+}
+bool is_bf16(const Tensor& t) { return t.scalar_type() == at::kBFloat16; }
+void check_f32_or_bf16(const Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, name, " must be fp32 or bf16");
+}
+void check_aligned16(const Tensor& t, const char* name) {
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+const pda::bf16_t* bp(const Tensor& t) { return reinterpret_cast<const pda::bf16_t*>(t.data_ptr()); }
+pda::bf16_t* bpm(const Tensor& t) { return reinterpret_cast<pda::bf16_t*>(t.data_ptr()); }
+const float* fopt(const c10::optional<Tensor>& t) { return t.has_value() ? t->data_ptr<float>() : nullptr; }
+
+// ------------------------------------------------------------------ optimizers
+void sgd_step(Tensor master, c10::optional<Tensor> param_bf16, Tensor grad, Tensor mom, double lr, double momentum,
+              double dampening, double wd, bool nesterov, bool first, double gscale,
+              c10::optional<Tensor> gscale_t, c10::optional<Tensor> lr_t) {
+  check_f32(master, "master");
+  check_f32_or_bf16(grad, "grad");
+  TORCH_CHECK(grad.numel() == master.numel(), "grad/master size mismatch");
+  if (momentum != 0.0) {
+    check_f32(mom, "momentum_buffer");
+    TORCH_CHECK(mom.numel() == master.numel());
+  }
+  if (param_bf16) {
+    check_bf16(*param_bf16, "param_bf16");
+    TORCH_CHECK(param_bf16->numel() == master.numel());
+  }
+  for (auto* t : {&master, &grad}) check_aligned16(*t, "optimizer buffer");
+  c10::DeviceGuard g(master.device());
+  CHECK_HIP_OK(pda::sgd_step(master.data_ptr<float>(), param_bf16 ? bpm(*param_bf16) : nullptr, grad.data_ptr(),
+                             is_bf16(grad), momentum != 0.0 ? mom.data_ptr<float>() : nullptr, master.numel(),
+                             (float)lr, (float)momentum, (float)dampening, (float)wd, nesterov, first, (float)gscale,
+                             fopt(gscale_t), fopt(lr_t), stream_of(master)));
+}
+
+void adam_step(Tensor master, c10::optional<Tensor> param_bf16, Tensor grad, Tensor m, Tensor v, double lr,
+               double beta1, double beta2, double eps, double wd, bool adamw, int64_t step, double gscale,
+               c10::optional<Tensor> gscale_t, c10::optional<Tensor> lr_t) {
+  check_f32(master, "master");
+  check_f32_or_bf16(grad, "grad");
+  check_f32(m, "exp_avg");
+  check_f32(v, "exp_avg_sq");
+  TORCH_CHECK(grad.numel() == master.numel() && m.numel() == master.numel() && v.numel() == master.numel());
+  if (param_bf16) {
+    check_bf16(*param_bf16, "param_bf16");
+    TORCH_CHECK(param_bf16->numel() == master.numel());
+  }
+  TORCH_CHECK(step >= 1, "adam step must be >= 1");
+  c10::DeviceGuard g(master.device());
+  CHECK_HIP_OK(pda::adam_step(master.data_ptr<float>(), param_bf16 ? bpm(*param_bf16) : nullptr, grad.data_ptr(),
+                              is_bf16(grad), m.data_ptr<float>(), v.data_ptr<float>(), master.numel(), (float)lr,
+                              (float)beta1, (float)beta2, (float)eps, (float)wd, adamw, step, (float)gscale,
+                              fopt(gscale_t), fopt(lr_t), stream_of(master)));
+}
+
+// returns [norm, clip_coef] on device
+Tensor grad_norm(Tensor grad, double pre, double max_norm) {
+  check_f32_or_bf16(grad, "grad");
+  c10::DeviceGuard g(grad.device());
+  auto opts = grad.options().dtype(at::kFloat);
+  Tensor partial = at::empty({pda::grad_norm_partials()}, opts);
+  Tensor out = at::empty({2}, opts);
+  CHECK_HIP_OK(pda::grad_norm(grad.data_ptr(), is_bf16(grad), grad.numel(), (float)pre, (float)max_norm,
+                              partial.data_ptr<float>(), out.data_ptr<float>(), stream_of(grad)));
+  return out;
+}
+
+void cast_scale(Tensor src, Tensor dst, double scale, c10::optional<Tensor> scale_t) {
+  check_f32_or_bf16(src, "src");
+  check_f32_or_bf16(dst, "dst");
+  TORCH_CHECK(src.numel() == dst.numel());
+  c10::DeviceGuard g(src.device());
+  CHECK_HIP_OK(pda::cast_scale(src.data_ptr(), is_bf16(src), dst.data_ptr(), is_bf16(dst), src.numel(), (float)scale,
+                               fopt(scale_t), stream_of(src)));
+}
+
+// ------------------------------------------------------------------ cross entropy
+std::vector<Tensor> ce_fwd(Tensor logits, Tensor target, int64_t ignore_index, double smoothing) {
+  check_f32_or_bf16(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2, "logits must be [M, C]");
+  const int64_t M = logits.size(0), C = logits.size(1);
+  check_gpu(target, "target");
+  const bool prob = target.is_floating_point();
+  if (prob) {
+    TORCH_CHECK(target.scalar_type() == at::kFloat && target.sizes() == logits.sizes(), "prob target must be fp32 [M,C]");
+  } else {
+    TORCH_CHECK(target.scalar_type() == at::kLong && target.numel() == M, "index target must be int64 [M]");
+  }
+  c10::DeviceGuard g(logits.device());
+  auto opts = logits.options().dtype(at::kFloat);
+  Tensor loss = at::empty({M}, opts), lse = at::empty({M}, opts);
+  CHECK_HIP_OK(pda::cross_entropy_fwd(logits.data_ptr(), is_bf16(logits), M, C,
+                                      prob ? nullptr : target.data_ptr<int64_t>(),
+                                      prob ? target.data_ptr<float>() : nullptr, ignore_index, (float)smoothing,
+                                      loss.data_ptr<float>(), lse.data_ptr<float>(), stream_of(logits)));
+  return {loss, lse};
+}
+
+Tensor ce_bwd(Tensor logits, Tensor target, Tensor lse, Tensor gscale_t, double gscale, int64_t ignore_index,
+              double smoothing) {
+  check_f32_or_bf16(logits, "logits");
+  const int64_t M = logits.size(0), C = logits.size(1);
+  const bool prob = target.is_floating_point();
+  check_f32(lse, "lse");
+  check_f32(gscale_t, "gscale");
+  c10::DeviceGuard g(logits.device());
+  Tensor d = at::empty_like(logits);
+  CHECK_HIP_OK(pda::cross_entropy_bwd(logits.data_ptr(), is_bf16(logits), M, C,
+                                      prob ? nullptr : target.data_ptr<int64_t>(),
+                                      prob ? target.data_ptr<float>() : nullptr, ignore_index, (float)smoothing,
+                                      lse.data_ptr<float>(), gscale_t.data_ptr<float>(), (float)gscale, d.data_ptr(),
+                                      stream_of(logits)));
+  return d;
+}
+
+// ------------------------------------------------------------------ batch norm (channels-last)
+void bn_param_ptrs(const c10::optional<Tensor>& t, const float** f, const pda::bf16_t** b, int64_t C) {
+  *f = nullptr;
+  *b = nullptr;
+  if (!t.has_value()) return;
+  check_f32_or_bf16(*t, "bn affine parameter");
+  TORCH_CHECK(t->numel() == C);
+  if (is_bf16(*t)) *b = bp(*t);
+  else *f = t->data_ptr<float>();
+}
+
+std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma,
+                                 c10::optional<Tensor> beta, c10::optional<Tensor> running_mean,
+                                 c10::optional<Tensor> running_var, double momentum, double eps, bool relu) {
+  check_bf16(x, "x");
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "channels must be a multiple of 8");
+  if (res) {
+    check_bf16(*res, "residual");
+    TORCH_CHECK(res->sizes() == x.sizes());
+  }
+  const float *gf, *bfp;
+  const pda::bf16_t *gb, *bb;
+  bn_param_ptrs(gamma, &gf, &gb, C);
+  bn_param_ptrs(beta, &bfp, &bb, C);
+  if (running_mean) {
+    check_f32(*running_mean, "running_mean");
+    check_f32(*running_var, "running_var");
+  }
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty_like(x);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({C}, fo), invstd = at::empty({C}, fo);
+  Tensor ws = at::empty({pda::bn_workspace_floats(M, C)}, fo);
+  CHECK_HIP_OK(pda::bn_fwd_train(bp(x), res ? bp(*res) : nullptr, bpm(y), M, C, gf, gb, bfp, bb,
+                                 running_mean ? running_mean->data_ptr<float>() : nullptr,
+                                 running_var ? running_var->data_ptr<float>() : nullptr, (float)momentum, (float)eps,
+                                 relu, mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr<float>(),
+                                 stream_of(x)));
+  return {y, mean, invstd};
+}
+
+Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
+                   Tensor running_mean, Tensor running_var, double eps, bool relu) {
+  check_bf16(x, "x");
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "channels must be a multiple of 8");
+  if (res) check_bf16(*res, "residual");
+  const float *gf, *bfp;
+  const pda::bf16_t *gb, *bb;
+  bn_param_ptrs(gamma, &gf, &gb, C);
+  bn_param_ptrs(beta, &bfp, &bb, C);
+  check_f32(running_mean, "running_mean");
+  check_f32(running_var, "running_var");
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty_like(x);
+  Tensor ws = at::empty({2 * C}, x.options().dtype(at::kFloat));
+  CHECK_HIP_OK(pda::bn_fwd_eval(bp(x), res ? bp(*res) : nullptr, bpm(y), M, C, gf, gb, bfp, bb,
+                                running_mean.data_ptr<float>(), running_var.data_ptr<float>(), (float)eps, relu,
+                                ws.data_ptr<float>(), stream_of(x)));
+  return y;
+}
+
+std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor mean, Tensor invstd,
+                           c10::optional<Tensor> gamma, bool relu, bool want_dres) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes());
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  if (relu) {
+    TORCH_CHECK(y.has_value(), "relu backward needs the saved output");
+    check_bf16(*y, "y");
+  }
+  check_f32(mean, "mean");
+  check_f32(invstd, "invstd");
+  const float* gf;
+  const pda::bf16_t* gb;
+  bn_param_ptrs(gamma, &gf, &gb, C);
+  c10::DeviceGuard g(x.device());
+  Tensor dx = at::empty_like(x);
+  Tensor dres = want_dres ? at::empty_like(x) : Tensor();
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor dgamma = at::empty({C}, fo), dbeta = at::empty({C}, fo);
+  Tensor ws = at::empty({pda::bn_workspace_floats(M, C)}, fo);
+  CHECK_HIP_OK(pda::bn_bwd(bp(dy), bp(x), relu ? bp(*y) : nullptr, M, C, mean.data_ptr<float>(),
+                           invstd.data_ptr<float>(), gf, gb, relu, bpm(dx), want_dres ? bpm(dres) : nullptr,
+                           dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), ws.data_ptr<float>(), stream_of(x)));
+  return {dx, dres, dgamma, dbeta};
+}
+
+// ------------------------------------------------------------------ pooling (NHWC)
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4, "x must be [N,H,W,C]");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && k * k <= 255);
+  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty({N, P, Q, C}, x.options());
+  Tensor idx = at::empty({N, P, Q, C}, x.options().dtype(at::kByte));
+  CHECK_HIP_OK(pda::maxpool2d_fwd(bp(x), bpm(y), idx.data_ptr<uint8_t>(), N, H, W, C, P, Q, k, s, pad, stream_of(x)));
+  return {y, idx};
+}
+
+Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64_t s, int64_t pad) {
+  check_bf16(dy, "dy");
+  check_gpu(idx, "idx");
+  TORCH_CHECK(idx.sizes() == dy.sizes());
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  c10::DeviceGuard g(dy.device());
+  Tensor dx = at::empty({N, H, W, C}, dy.options());
+  CHECK_HIP_OK(pda::maxpool2d_bwd(bp(dy), idx.data_ptr<uint8_t>(), bpm(dx), N, H, W, C, P, Q, k, s, pad,
+                                  stream_of(dy)));
+  return dx;
+}
+
+Tensor avgpool_fwd(Tensor x, bool out_bf16) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0);
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty({N, C}, x.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  CHECK_HIP_OK(pda::avgpool_global_fwd(bp(x), y.data_ptr(), out_bf16, N, HW, C, stream_of(x)));
+  return y;
+}
+
+Tensor avgpool_bwd(Tensor dy, int64_t H, int64_t W) {
+  check_f32_or_bf16(dy, "dy");
+  const int N = dy.size(0), C = dy.size(1);
+  c10::DeviceGuard g(dy.device());
+  Tensor dx = at::empty({N, H, W, C}, dy.options().dtype(at::kBFloat16));
+  CHECK_HIP_OK(pda::avgpool_global_bwd(dy.data_ptr(), is_bf16(dy), bpm(dx), N, H * W, C, stream_of(dy)));
+  return dx;
+}
+
+// ------------------------------------------------------------------ synthetic data
+void fill_random(Tensor t, int64_t seed, int64_t offset, int64_t kind, double a, double b) {
+  check_f32_or_bf16(t, "tensor");
+  c10::DeviceGuard g(t.device());
+  CHECK_HIP_OK(pda::fill_random(t.data_ptr(), is_bf16(t) ? 1 : 0, t.numel(), (uint64_t)seed, (uint64_t)offset,
+                                (int)kind, (float)a, (float)b, stream_of(t)));
+}
+void fill_randint(Tensor t, int64_t seed, int64_t offset, int64_t low, int64_t high) {
+  check_gpu(t, "tensor");
+  TORCH_CHECK(t.scalar_type() == at::kLong && high > low);
+  c10::DeviceGuard g(t.device());
+  CHECK_HIP_OK(pda::fill_randint(t.data_ptr<int64_t>(), t.numel(), (uint64_t)seed, (uint64_t)offset, low, high,
+                                 stream_of(t)));
+}
+
+// ------------------------------------------------------------------ GEMM / conv
+// C = A * B with A(m,k) = A[m*lda+k] (a_kmajor) or A[k*lda+m]; B(k,n) = B[n*ldb+k] (b_kmajor) or B[k*ldb+n].
+void gemm(Tensor A, bool a_kmajor, int64_t lda, Tensor B, bool b_kmajor, int64_t ldb, Tensor C, int64_t ldc,
+          int64_t M, int64_t N, int64_t K, c10::optional<Tensor> bias, bool relu, bool allow_split) {
+  check_bf16(A, "A");
+  check_bf16(B, "B");
+  check_f32_or_bf16(C, "C");
+  TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "gemm needs K and N multiples of 8 (got K=", K, ", N=", N, ")");
+  TORCH_CHECK(a_kmajor || M % 8 == 0, "M-major A needs M % 8 == 0");
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0, "leading dims must be 16-byte multiples");
+  // bounds: the largest element each operand touches
+  TORCH_CHECK((a_kmajor ? (M - 1) * lda + K : (K - 1) * lda + M) <= A.numel(), "A too small");
+  TORCH_CHECK((b_kmajor ? (N - 1) * ldb + K : (K - 1) * ldb + N) <= B.numel(), "B too small");
+  TORCH_CHECK((M - 1) * ldc + N <= C.numel(), "C too small");
+  for (auto* t : {&A, &B, &C}) check_aligned16(*t, "gemm operand");
+  if (bias) {
+    check_f32_or_bf16(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N);
+  }
+  c10::DeviceGuard g(A.device());
+  const int64_t slab_n = pda::gemm_slab_floats(M, N, K, allow_split);
+  Tensor slab = slab_n > 0 ? at::empty({slab_n}, A.options().dtype(at::kFloat)) : Tensor();
+  CHECK_HIP_OK(pda::gemm_bf16(bp(A), a_kmajor, lda, bp(B), b_kmajor, ldb, C.data_ptr(), C.scalar_type() == at::kFloat,
+                              ldc, M, N, K, bias ? bias->data_ptr() : nullptr, bias ? !is_bf16(*bias) : false, relu,
+                              slab_n > 0 ? slab.data_ptr<float>() : nullptr, slab_n > 0, stream_of(A)));
+}
+
+void conv_check(const Tensor& x, const Tensor& w) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4, "conv tensors must be 4-D (NHWC activations, OHWI weights)");
+  TORCH_CHECK(x.size(3) % 8 == 0, "input channels must be a multiple of 8");
+  TORCH_CHECK(w.size(0) % 8 == 0, "output channels must be a multiple of 8");
+  TORCH_CHECK(w.size(3) == x.size(3), "channel mismatch");
+  TORCH_CHECK(x.numel() < (1LL << 31), "activation too large for 32-bit index math");
+}
+
+Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, c10::optional<Tensor> bias, bool relu) {
+  conv_check(x, w);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Cout = w.size(0), R = w.size(1), S = w.size(2);
+  const int P = (H + 2 * pad - dil * (R - 1) - 1) / stride + 1, Q = (W + 2 * pad - dil * (S - 1) - 1) / stride + 1;
+  TORCH_CHECK(P > 0 && Q > 0);
+  if (bias) TORCH_CHECK(bias->numel() == Cout);
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty({N, P, Q, Cout}, x.options());
+  CHECK_HIP_OK(pda::conv2d_fwd(bp(x), bp(w), bpm(y), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
+                               bias ? bias->data_ptr() : nullptr, bias ? !is_bf16(*bias) : false, relu,
+                               stream_of(x)));
+  return y;
+}
+
+Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad, int64_t dil) {
+  check_bf16(dy, "dy");
+  check_bf16(w, "w");
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), Cout = dy.size(3);
+  const int R = w.size(1), S = w.size(2), C = w.size(3);
+  TORCH_CHECK(w.size(0) == Cout && C % 8 == 0 && Cout % 8 == 0);
+  c10::DeviceGuard g(dy.device());
+  Tensor wt = at::empty({C, R, S, Cout}, w.options());
+  CHECK_HIP_OK(pda::conv_weight_transpose(bp(w), bpm(wt), Cout, R * S, C, stream_of(dy)));
+  Tensor dx = at::empty({N, H, W, C}, dy.options());
+  CHECK_HIP_OK(pda::conv2d_dgrad(bp(dy), bp(wt), bpm(dx), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
+                                 stream_of(dy)));
+  return dx;
+}
+
+Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t dil, bool out_f32) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int P = dy.size(1), Q = dy.size(2), Cout = dy.size(3);
+  TORCH_CHECK(dy.size(0) == N && C % 8 == 0 && Cout % 8 == 0);
+  c10::DeviceGuard g(dy.device());
+  Tensor dw = at::empty({Cout, R, S, C}, dy.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  const int64_t slab_n = pda::conv_slab_floats(2, N, H, W, C, Cout, R, S, P, Q);
+  Tensor slab = slab_n > 0 ? at::empty({slab_n}, dy.options().dtype(at::kFloat)) : Tensor();
+  CHECK_HIP_OK(pda::conv2d_wgrad(bp(dy), bp(x), dw.data_ptr(), out_f32, N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
+                                 slab_n > 0 ? slab.data_ptr<float>() : nullptr, stream_of(dy)));
+  return dw;
+}
+
+// ------------------------------------------------------------------ activations / SIMT GEMM
+Tensor act_fwd(Tensor x, int64_t op) {
+  check_f32_or_bf16(x, "x");
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty_like(x);
+  CHECK_HIP_OK(pda::act_fwd(x.data_ptr(), y.data_ptr(), is_bf16(x), x.numel(), (int)op, stream_of(x)));
+  return y;
+}
+
+Tensor act_bwd(Tensor dy, Tensor ref, int64_t op) {
+  check_f32_or_bf16(dy, "dy");
+  check_gpu(ref, "ref");
+  TORCH_CHECK(ref.sizes() == dy.sizes() && ref.scalar_type() == dy.scalar_type());
+  c10::DeviceGuard g(dy.device());
+  Tensor dx = at::empty_like(dy);
+  CHECK_HIP_OK(pda::act_bwd(dy.data_ptr(), ref.data_ptr(), dx.data_ptr(), is_bf16(dy), dy.numel(), (int)op,
+                            stream_of(dy)));
+  return dx;
+}
+
+Tensor relu_bwd(Tensor dy, Tensor y) { return act_bwd(dy, y, 0); }
+
+Tensor swiglu_fwd(Tensor gu) {
+  check_f32_or_bf16(gu, "gate_up");
+  const int64_t F2 = gu.size(-1);
+  TORCH_CHECK(F2 % 16 == 0, "swiglu width must be a multiple of 8");
+  const int64_t rows = gu.numel() / F2, F = F2 / 2;
+  c10::DeviceGuard g(gu.device());
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F;
+  Tensor y = at::empty(sizes, gu.options());
+  CHECK_HIP_OK(pda::swiglu_fwd(gu.data_ptr(), y.data_ptr(), is_bf16(gu), rows, F, stream_of(gu)));
+  return y;
+}
+
+Tensor swiglu_bwd(Tensor dy, Tensor gu) {
+  check_f32_or_bf16(dy, "dy");
+  check_gpu(gu, "gate_up");
+  const int64_t F2 = gu.size(-1), rows = gu.numel() / F2, F = F2 / 2;
+  TORCH_CHECK(dy.numel() == rows * F);
+  c10::DeviceGuard g(gu.device());
+  Tensor dgu = at::empty_like(gu);
+  CHECK_HIP_OK(pda::swiglu_bwd(dy.data_ptr(), gu.data_ptr(), dgu.data_ptr(), is_bf16(gu), rows, F, stream_of(gu)));
+  return dgu;
+}
+
+Tensor colsum(Tensor x) {
+  check_f32_or_bf16(x, "x");
+  const int64_t cols = x.size(-1), rows = x.numel() / cols;
+  c10::DeviceGuard g(x.device());
+  Tensor out = at::empty({cols}, x.options().dtype(at::kFloat));
+  CHECK_HIP_OK(pda::colsum(x.data_ptr(), is_bf16(x), out.data_ptr<float>(), rows, cols, stream_of(x)));
+  return out;
+}
+
+// C[M,N] (+)= A[M,K] B[K,N] with explicit element strides (any alignment / dtype fp32|bf16)
+void simt_gemm(Tensor A, int64_t sam, int64_t sak, Tensor B, int64_t sbk, int64_t sbn, Tensor C, int64_t scm,
+               int64_t scn, int64_t M, int64_t N, int64_t K, c10::optional<Tensor> bias, bool relu, double beta) {
+  for (auto* t : {&A, &B, &C}) {
+    TORCH_CHECK(t->is_cuda(), "simt_gemm operands must be GPU tensors");
+    TORCH_CHECK(t->scalar_type() == at::kFloat || t->scalar_type() == at::kBFloat16, "fp32/bf16 only");
+  }
+  auto span = [](int64_t a, int64_t sa, int64_t b, int64_t sb) { return (a - 1) * sa + (b - 1) * sb + 1; };
+  TORCH_CHECK(M > 0 && N > 0 && K > 0);
+  TORCH_CHECK(span(M, sam, K, sak) <= A.numel() && span(K, sbk, N, sbn) <= B.numel() &&
+              span(M, scm, N, scn) <= C.numel(), "simt_gemm: operand too small for the given strides");
+  if (bias) {
+    check_f32(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N);
+  }
+  c10::DeviceGuard g(A.device());
+  CHECK_HIP_OK(pda::simt_gemm(A.data_ptr(), is_bf16(A), sam, sak, B.data_ptr(), is_bf16(B), sbk, sbn, C.data_ptr(),
+                              is_bf16(C), scm, scn, M, N, K, bias ? bias->data_ptr<float>() : nullptr, relu,
+                              (float)beta, stream_of(A)));
+}
+
+// ------------------------------------------------------------------ LayerNorm / RMSNorm
+std::vector<Tensor> rownorm_fwd(Tensor x, Tensor gamma, c10::optional<Tensor> beta, double eps, bool rms) {
+  check_f32_or_bf16(x, "x");
+  check_f32_or_bf16(gamma, "gamma");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && D <= 8192, "norm width must be a multiple of 8 and <= 8192");
+  TORCH_CHECK(gamma.numel() == D);
+  if (!rms) {
+    TORCH_CHECK(beta.has_value() && beta->numel() == D && beta->scalar_type() == gamma.scalar_type());
+    check_gpu(*beta, "beta");
+  }
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty_like(x);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({rms ? 1 : rows}, fo), rstd = at::empty({rows}, fo);
+  CHECK_HIP_OK(pda::rownorm_fwd(x.data_ptr(), is_bf16(x), gamma.data_ptr(), rms ? nullptr : beta->data_ptr(),
+                                is_bf16(gamma), y.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, D,
+                                (float)eps, rms, stream_of(x)));
+  return {y, mean, rstd};
+}
+
+std::vector<Tensor> rownorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, bool rms) {
+  check_f32_or_bf16(dy, "dy");
+  check_f32_or_bf16(x, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type());
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  c10::DeviceGuard g(x.device());
+  Tensor dx = at::empty_like(x);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor dgamma = at::empty({D}, fo), dbeta = at::empty({D}, fo);
+  CHECK_HIP_OK(pda::rownorm_bwd(dy.data_ptr(), x.data_ptr(), is_bf16(x), gamma.data_ptr(), is_bf16(gamma),
+                                rms ? nullptr : mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(),
+                                dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), rows, D, rms, stream_of(x)));
+  return {dx, dgamma, dbeta};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "pytorchdistributed_amd native layer: CDNA4 HIP kernels + C++ runtime";
+  m.def("sgd_step", &sgd_step);
+  m.def("adam_step", &adam_step);
+  m.def("grad_norm", &grad_norm);
+  m.def("cast_scale", &cast_scale);
+  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("bn_fwd_train", &bn_fwd_train);
+  m.def("bn_fwd_eval", &bn_fwd_eval);
+  m.def("bn_bwd", &bn_bwd);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("fill_random", &fill_random);
+  m.def("fill_randint", &fill_randint);
+  m.def("gemm", &gemm);
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("act_fwd", &act_fwd);
+  m.def("act_bwd", &act_bwd);
+  m.def("relu_bwd", &relu_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("colsum", &colsum);
+  m.def("simt_gemm", &simt_gemm);
+  m.def("rownorm_fwd", &rownorm_fwd);
+  m.def("rownorm_bwd", &rownorm_bwd);
+  pda_rt::bind_runtime(m);
+}

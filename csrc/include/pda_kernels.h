@@ -1,0 +1,95 @@
+// Host-callable launchers of the pytorchdistributed_amd HIP kernels.  Pure HIP: no torch headers,
+// so kernel translation units compile in seconds and the bindings layer owns tensor validation.
+// Every launcher is asynchronous on `st`, performs no allocation and no synchronisation.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pda {
+typedef uint16_t bf16_t;
+
+// ---- optim.hip
+hipError_t sgd_step(float* master, bf16_t* param_bf16, const void* grad, bool grad_bf16, float* mom, int64_t n,
+                    float lr, float momentum, float dampening, float wd, bool nesterov, bool first, float gscale,
+                    const float* gscale_ptr, const float* lr_ptr, hipStream_t st);
+hipError_t adam_step(float* master, bf16_t* param_bf16, const void* grad, bool grad_bf16, float* m, float* v,
+                     int64_t n, float lr, float beta1, float beta2, float eps, float wd, bool adamw, int64_t step,
+                     float gscale, const float* gscale_ptr, const float* lr_ptr, hipStream_t st);
+int grad_norm_partials();
+hipError_t grad_norm(const void* grad, bool grad_bf16, int64_t n, float pre, float max_norm, float* partial,
+                     float* out, hipStream_t st);
+hipError_t cast_scale(const void* src, bool src_bf16, void* dst, bool dst_bf16, int64_t n, float scale,
+                      const float* scale_ptr, hipStream_t st);
+
+// ---- cross_entropy.hip
+hipError_t cross_entropy_fwd(const void* logits, bool logits_bf16, int64_t M, int64_t C, const int64_t* target_idx,
+                             const float* target_prob, int64_t ignore_index, float smoothing, float* loss, float* lse,
+                             hipStream_t st);
+hipError_t cross_entropy_bwd(const void* logits, bool logits_bf16, int64_t M, int64_t C, const int64_t* target_idx,
+                             const float* target_prob, int64_t ignore_index, float smoothing, const float* lse,
+                             const float* gscale_ptr, float gscale, void* dlogits, hipStream_t st);
+
+// ---- batchnorm.hip (x, y: [M, C] channels-last, C % 8 == 0)
+int64_t bn_workspace_floats(int64_t M, int64_t C);
+hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
+                        const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, float* running_mean,
+                        float* running_var, float momentum, float eps, bool relu, float* save_mean,
+                        float* save_invstd, float* ws, hipStream_t st);
+hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
+                       const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, const float* running_mean,
+                       const float* running_var, float eps, bool relu, float* ws, hipStream_t st);
+hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, int64_t M, int64_t C, const float* save_mean,
+                  const float* save_invstd, const float* gamma_f, const bf16_t* gamma_b, bool relu, bf16_t* dx,
+                  bf16_t* dres, float* dgamma, float* dbeta, float* ws, hipStream_t st);
+
+// ---- pool.hip (NHWC, C % 8 == 0)
+hipError_t maxpool2d_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int k,
+                         int s, int pad, hipStream_t st);
+hipError_t maxpool2d_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C, int P, int Q,
+                         int k, int s, int pad, hipStream_t st);
+hipError_t avgpool_global_fwd(const bf16_t* x, void* y, bool y_bf16, int N, int HW, int C, hipStream_t st);
+hipError_t avgpool_global_bwd(const void* dy, bool dy_bf16, bf16_t* dx, int N, int HW, int C, hipStream_t st);
+
+// ---- synth.hip
+hipError_t fill_random(void* out, int dtype /*0 f32, 1 bf16*/, int64_t n, uint64_t seed, uint64_t offset, int kind,
+                       float a, float b, hipStream_t st);
+hipError_t fill_randint(int64_t* out, int64_t n, uint64_t seed, uint64_t offset, int64_t low, int64_t high,
+                        hipStream_t st);
+
+// ---- gemm_conv.hip
+int64_t gemm_slab_floats(int64_t M, int64_t N, int64_t K, bool allow_split);
+hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
+                     void* C, bool c_f32, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
+                     bool bias_f32, bool relu, float* slab, bool allow_split, hipStream_t st);
+int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, int S, int P, int Q);
+hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int Cout, int R, int S,
+                      int P, int Q, int stride, int pad, int dil, const void* bias, bool bias_f32, bool relu,
+                      hipStream_t st);
+hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int N, int H, int W, int C, int Cout, int R,
+                        int S, int P, int Q, int stride, int pad, int dil, hipStream_t st);
+hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32, int N, int H, int W, int C,
+                        int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, float* slab,
+                        hipStream_t st);
+hipError_t conv_weight_transpose(const bf16_t* w, bf16_t* wt, int Cout, int RS, int Cin, hipStream_t st);
+
+
+// ---- act.hip (op: 0 relu, 1 gelu_tanh)
+hipError_t act_fwd(const void* x, void* y, bool bf16, int64_t n, int op, hipStream_t st);
+hipError_t act_bwd(const void* dy, const void* ref, void* dx, bool bf16, int64_t n, int op, hipStream_t st);
+hipError_t swiglu_fwd(const void* gu, void* y, bool bf16, int64_t rows, int64_t F, hipStream_t st);
+hipError_t swiglu_bwd(const void* dy, const void* gu, void* dgu, bool bf16, int64_t rows, int64_t F, hipStream_t st);
+hipError_t colsum(const void* x, bool bf16, float* out, int64_t rows, int64_t cols, hipStream_t st);
+
+// ---- simt_gemm.hip (dtype codes 0 fp32 / 1 bf16; arbitrary strides)
+hipError_t simt_gemm(const void* A, int a_dt, int64_t sam, int64_t sak, const void* B, int b_dt, int64_t sbk,
+                     int64_t sbn, void* C, int c_dt, int64_t scm, int64_t scn, int64_t M, int64_t N, int64_t K,
+                     const float* bias, bool relu, float beta, hipStream_t st);
+
+// ---- rownorm.hip (LayerNorm / RMSNorm over the last dim, D % 8 == 0, D <= 8192)
+hipError_t rownorm_fwd(const void* x, bool x_bf16, const void* gamma, const void* beta, bool p_bf16, void* y,
+                       float* mean, float* rstd, int64_t rows, int64_t D, float eps, bool rms, hipStream_t st);
+hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* gamma, bool p_bf16, const float* mean,
+                       const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, bool rms,
+                       hipStream_t st);
+
+}  // namespace pda

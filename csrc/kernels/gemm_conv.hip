@@ -1,0 +1,652 @@
+// MFMA GEMM + implicit-GEMM convolution for gfx950.
+//
+// One tiled kernel template serves every matmul-shaped op of the framework:
+//   Linear fwd / dgrad / wgrad            (plain operands, any of the 4 major-ness combinations)
+//   Conv2d fwd    C[npq, co]   = im2col(x)[npq, rsc]   * W[co, rsc]^T          (NHWC, weights OHWI)
+//   Conv2d dgrad  C[nhw, ci]   = col(dy)[nhw, rs co]   * Wt[ci, rs co]^T       (stride folded into the gather)
+//   Conv2d wgrad  C[co, rsc]   = dy[npq, co]^T         * im2col(x)[npq, rsc]   (split-K over N*P*Q)
+// The reference reaches these through cuBLAS / cuDNN (`nn.Linear` `PY1:77`, torchvision ResNet-50
+// convs `NB03:314,325-349`); here they are one CDNA4 kernel family.
+//
+// Design (cdna_hip_programming.md §3, §5, §5.5):
+//   * v_mfma_f32_16x16x32_bf16, 256 threads = 4 waves in a 2x2 grid, block tile BM x BN x 64.
+//   * Operands are staged global -> VGPR -> LDS (register staging: conv gathers need per-lane
+//     predication / zero fill), double-buffered, loads for tile k+1 issued before the MFMAs of
+//     tile k and written to LDS after them (T14), one barrier per K tile.
+//   * K-major tiles ([rows][64], 128-B rows) are read with ds_read_b128 and XOR-swizzled on the
+//     16-B chunk index by (row & 7) -> conflict-free for the MFMA fragment pattern (T2).
+//   * MN-major tiles ([64][rows]) are read with ds_read_b64_tr_b16 (T10), so transposed operands
+//     (dgrad / wgrad of Linear, dy and im2col(x) in conv wgrad) need no transpose pass; their
+//     32-B slots are XOR-swizzled by k so the 8 rows a half-wave touches hit distinct banks.
+//   * MFMA roles are swapped (A-operand = N tile) so each lane ends with 4 consecutive output
+//     columns (channels): 8-B bf16 / 16-B fp32 stores and per-channel epilogues.
+//   * Workgroup ids are remapped XCD-aware so tiles that share an A panel share an L2 (T1).
+//   * Index math uses precomputed multiply-shift division (no integer divides in the K loop).
+#include "pda_common.h"
+#include "pda_kernels.h"
+
+namespace pda {
+namespace {
+
+constexpr int NT = 256;
+constexpr int BK = 64;
+
+typedef __bf16 mfma_bf16x8 __attribute__((ext_vector_type(8)));
+
+// ------------------------------------------------------------------ fast division (n < 2^31)
+struct FastDiv {
+  uint32_t d, mul, shr;
+};
+FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  if (d <= 1) {
+    f.mul = 0;
+    f.shr = 0;
+  } else {
+    uint32_t l = 0;
+    while ((1u << l) < d) ++l;  // ceil(log2 d)
+    const uint32_t p = 31 + l;
+    f.mul = (uint32_t)(((1ull << p) + d - 1) / d);
+    f.shr = p - 32;
+  }
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return f.d == 1 ? n : (__umulhi(n, f.mul) >> f.shr);
+}
+
+__device__ __forceinline__ u16x8 zero8() {
+  u16x8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = 0;
+  return z;
+}
+
+// ------------------------------------------------------------------ operand loaders
+// A K-major loader feeds a [R][BK] tile: thread t owns k-chunk (t & 7) of rows (t >> 3) + 32 i.
+// An MN-major loader feeds a [BK][R] tile: thread t owns column chunk (t % (R/8)) of
+// k-rows t / (R/8) + (NT / (R/8)) i.  Both produce R/32 16-byte chunks per thread per tile.
+
+template <int R>
+struct PlainK {  // element (row, k) = p[row * ld + k]
+  static constexpr bool kMajor = true;
+  static constexpr int NCH = R / 32;
+  const bf16_t* p;
+  int64_t rows, K, ld;
+  struct State {
+    const bf16_t* ptr[NCH];
+    bool ok[NCH];
+    int kc;
+  };
+  __device__ void init(State& s, int64_t row0, int tid) const {
+    s.kc = (tid & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int64_t row = row0 + (tid >> 3) + 32 * i;
+      s.ok[i] = row < rows;
+      s.ptr[i] = p + (s.ok[i] ? row : 0) * ld + s.kc;
+    }
+  }
+  __device__ void fetch(const State& s, int64_t k0, u16x8 (&v)[NCH]) const {
+    const bool kok = k0 + s.kc < K;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+      v[i] = (s.ok[i] && kok) ? *reinterpret_cast<const u16x8*>(s.ptr[i] + k0) : zero8();
+  }
+};
+
+template <int R>
+struct PlainMN {  // element (k, col) = p[k * ld + col]
+  static constexpr bool kMajor = false;
+  static constexpr int NCH = R / 32;
+  static constexpr int CPR = R / 8;
+  static constexpr int KSTEP = NT / CPR;
+  const bf16_t* p;
+  int64_t K, cols, ld;
+  struct State {
+    const bf16_t* base;
+    bool ok;
+    int krow;
+  };
+  __device__ void init(State& s, int64_t col0, int tid) const {
+    const int64_t col = col0 + (tid % CPR) * 8;
+    s.ok = col < cols;
+    s.base = p + (s.ok ? col : 0);
+    s.krow = tid / CPR;
+  }
+  __device__ void fetch(const State& s, int64_t k0, u16x8 (&v)[NCH]) const {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int64_t k = k0 + s.krow + KSTEP * i;
+      v[i] = (s.ok && k < K) ? *reinterpret_cast<const u16x8*>(s.base + k * ld) : zero8();
+    }
+  }
+};
+
+struct ConvGeom {
+  int H, W, C;     // input (fwd/wgrad) or dx (dgrad) spatial dims and its channel count
+  int P, Q;        // output spatial dims
+  int R, S, st, pad, dil;
+  int Cg;          // channel count of the gathered tensor (C for fwd/wgrad, Cout for dgrad)
+  FastDiv fC, fS, fQ, fP, fW, fH;
+};
+
+// Conv fwd A operand: element (m = (n,p,q), k = (r,s,ci)) = x[n, p*st-pad+r*dil, q*st-pad+s*dil, ci]
+template <int R>
+struct ConvFwdK {
+  static constexpr bool kMajor = true;
+  static constexpr int NCH = R / 32;
+  const bf16_t* x;
+  ConvGeom g;
+  int64_t M, K;
+  struct State {
+    int nH[NCH], ih0[NCH], iw0[NCH];
+    bool ok[NCH];
+    int kc;
+  };
+  __device__ void init(State& s, int64_t row0, int tid) const {
+    s.kc = (tid & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int64_t m = row0 + (tid >> 3) + 32 * i;
+      s.ok[i] = m < M;
+      const uint32_t mm = s.ok[i] ? (uint32_t)m : 0u;
+      const uint32_t t = fdiv(mm, g.fQ);
+      const int q = (int)(mm - t * g.Q);
+      const uint32_t n = fdiv(t, g.fP);
+      const int p = (int)(t - n * g.P);
+      s.nH[i] = (int)n * g.H;
+      s.ih0[i] = p * g.st - g.pad;
+      s.iw0[i] = q * g.st - g.pad;
+    }
+  }
+  __device__ void fetch(const State& s, int64_t k0, u16x8 (&v)[NCH]) const {
+    const int64_t k = k0 + s.kc;
+    if (k >= K) {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) v[i] = zero8();
+      return;
+    }
+    const uint32_t rs = fdiv((uint32_t)k, g.fC);
+    const int ci = (int)((uint32_t)k - rs * g.C);
+    const uint32_t r = fdiv(rs, g.fS);
+    const int sidx = (int)(rs - r * g.S);
+    const int dr = (int)r * g.dil, ds = sidx * g.dil;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int ih = s.ih0[i] + dr, iw = s.iw0[i] + ds;
+      const bool ok = s.ok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const int64_t off = ((int64_t)(s.nH[i] + ih) * g.W + iw) * g.C + ci;
+      v[i] = ok ? *reinterpret_cast<const u16x8*>(x + off) : zero8();
+    }
+  }
+};
+
+// Conv dgrad A operand: element (m = (n,h,w), k = (r,s,co)) = dy[n, p, q, co] where
+// p*st - pad + r*dil = h (zero when not integral / out of range).  dy has dims [N,P,Q,Cg].
+template <int R>
+struct ConvDgradK {
+  static constexpr bool kMajor = true;
+  static constexpr int NCH = R / 32;
+  const bf16_t* dy;
+  ConvGeom g;
+  int64_t M, K;
+  struct State {
+    int nP[NCH], h[NCH], w[NCH];
+    bool ok[NCH];
+    int kc;
+  };
+  __device__ void init(State& s, int64_t row0, int tid) const {
+    s.kc = (tid & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int64_t m = row0 + (tid >> 3) + 32 * i;
+      s.ok[i] = m < M;
+      const uint32_t mm = s.ok[i] ? (uint32_t)m : 0u;
+      const uint32_t t = fdiv(mm, g.fW);
+      s.w[i] = (int)(mm - t * g.W);
+      const uint32_t n = fdiv(t, g.fH);
+      s.h[i] = (int)(t - n * g.H);
+      s.nP[i] = (int)n * g.P;
+    }
+  }
+  __device__ void fetch(const State& s, int64_t k0, u16x8 (&v)[NCH]) const {
+    const int64_t k = k0 + s.kc;
+    if (k >= K) {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) v[i] = zero8();
+      return;
+    }
+    const uint32_t rs = fdiv((uint32_t)k, g.fC);  // fC divides by Cg here
+    const int co = (int)((uint32_t)k - rs * g.Cg);
+    const uint32_t r = fdiv(rs, g.fS);
+    const int sidx = (int)(rs - r * g.S);
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int ph = s.h[i] + g.pad - (int)r * g.dil;
+      const int pw = s.w[i] + g.pad - sidx * g.dil;
+      int p = ph, q = pw;
+      bool ok = s.ok[i] && ph >= 0 && pw >= 0;
+      if (g.st != 1) {
+        p = ph / g.st;
+        q = pw / g.st;
+        ok = ok && p * g.st == ph && q * g.st == pw;
+      }
+      ok = ok && p < g.P && q < g.Q;
+      const int64_t off = ((int64_t)(s.nP[i] + p) * g.Q + q) * g.Cg + co;
+      v[i] = ok ? *reinterpret_cast<const u16x8*>(dy + off) : zero8();
+    }
+  }
+};
+
+// Conv wgrad B operand (MN-major): element (k = (n,p,q), col = (r,s,ci)) = x[n, p*st-pad+r*dil, ...]
+template <int R>
+struct ConvWgradMN {
+  static constexpr bool kMajor = false;
+  static constexpr int NCH = R / 32;
+  static constexpr int CPR = R / 8;
+  static constexpr int KSTEP = NT / CPR;
+  const bf16_t* x;
+  ConvGeom g;
+  int64_t K, cols;
+  struct State {
+    int roff, soff, ci;
+    bool ok;
+    int krow;
+  };
+  __device__ void init(State& s, int64_t col0, int tid) const {
+    const int64_t col = col0 + (tid % CPR) * 8;
+    s.ok = col < cols;
+    const uint32_t cc = s.ok ? (uint32_t)col : 0u;
+    const uint32_t rs = fdiv(cc, g.fC);
+    s.ci = (int)(cc - rs * g.C);
+    const uint32_t r = fdiv(rs, g.fS);
+    s.roff = (int)r * g.dil - g.pad;
+    s.soff = (int)(rs - r * g.S) * g.dil - g.pad;
+    s.krow = tid / CPR;
+  }
+  __device__ void fetch(const State& s, int64_t k0, u16x8 (&v)[NCH]) const {
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int64_t k = k0 + s.krow + KSTEP * i;
+      bool ok = s.ok && k < K;
+      const uint32_t kk = ok ? (uint32_t)k : 0u;
+      const uint32_t t = fdiv(kk, g.fQ);
+      const int q = (int)(kk - t * g.Q);
+      const uint32_t n = fdiv(t, g.fP);
+      const int p = (int)(t - n * g.P);
+      const int ih = p * g.st + s.roff, iw = q * g.st + s.soff;
+      ok = ok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const int64_t off = ((int64_t)((int)n * g.H + ih) * g.W + iw) * g.C + s.ci;
+      v[i] = ok ? *reinterpret_cast<const u16x8*>(x + off) : zero8();
+    }
+  }
+};
+
+// ------------------------------------------------------------------ LDS images
+// K-major [R][64] bf16: 128-B rows, 16-B chunk index XOR (row & 7).
+__device__ __forceinline__ int kmaj_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+// MN-major [64][R] bf16: 32-B slots XOR-swizzled by k (see header).
+template <int R>
+__device__ __forceinline__ int mn_off(int k, int m) {
+  if constexpr (R == 128) {
+    const int h = (k & 3) | (((k >> 3) & 1) << 2);
+    return k * 256 + ((((m >> 4) ^ h) & 7) << 5) + ((m & 15) << 1);
+  } else {
+    const int h = ((k >> 1) & 1) | (((k >> 3) & 1) << 1);
+    return k * 128 + ((((m >> 4) ^ h) & 3) << 5) + ((m & 15) << 1);
+  }
+}
+
+template <class L, int R>
+__device__ __forceinline__ void stage_write(char* tile, const typename L::State& s, const u16x8 (&v)[R / 32], int tid) {
+  if constexpr (L::kMajor) {
+    const int chunk = tid & 7;
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      *reinterpret_cast<u16x8*>(tile + kmaj_off(row, chunk)) = v[i];
+    }
+  } else {
+    constexpr int CPR = R / 8, KSTEP = NT / CPR;
+    const int m = (tid % CPR) * 8;
+#pragma unroll
+    for (int i = 0; i < R / 32; ++i) {
+      const int k = tid / CPR + KSTEP * i;
+      *reinterpret_cast<u16x8*>(tile + mn_off<R>(k, m)) = v[i];
+    }
+  }
+}
+
+// Fragment for one 16-row group starting at `row0`, k-substep kk (0 or 32):
+// lane l holds (row0 + (l & 15), kk + 8 (l >> 4) + j), j = 0..7.
+template <bool KMAJ, int R>
+__device__ __forceinline__ mfma_bf16x8 read_frag(const char* tile, int row0, int kk, int lane) {
+  if constexpr (KMAJ) {
+    const int row = row0 + (lane & 15);
+    const int chunk = (kk >> 3) + (lane >> 4);
+    return *reinterpret_cast<const mfma_bf16x8*>(tile + kmaj_off(row, chunk));
+  } else {
+    const int i = lane & 15, g = lane >> 4;
+    const int k1 = kk + 8 * g + (i >> 2);
+    const int m = row0 + 4 * (i & 3);
+    typedef short s16x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+    const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + mn_off<R>(k1, m)));
+    const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(tile + mn_off<R>(k1 + 4, m)));
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    s16x8 f;
+    f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+    f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+    return __builtin_bit_cast(mfma_bf16x8, f);
+  }
+}
+
+struct Epi {
+  void* C;           // output base
+  int64_t ldc;
+  int c_f32;         // 1: fp32 output, 0: bf16 output
+  const void* bias;  // per-column bias or null
+  int bias_f32;
+  int relu;
+  float* slab;       // split-K fp32 partial slabs [splits][M][N] (overrides C when non-null)
+};
+
+// ------------------------------------------------------------------ the kernel
+template <int BM, int BN, class LA, class LB>
+__global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K, int tiles_n,
+                                                     int ktiles_per_split, Epi epi) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntiles = gridDim.x;
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int tn = tile % tiles_n, tm = tile / tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+  const int ktiles = (int)((K + BK - 1) / BK);
+  const int kt0 = blockIdx.y * ktiles_per_split;
+  const int kt1 = min(ktiles, kt0 + ktiles_per_split);
+
+  typename LA::State sa;
+  typename LB::State sb;
+  la.init(sa, m0, tid);
+  lb.init(sb, n0, tid);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u16x8 ra[BM / 32], rb[BN / 32];
+  if (kt0 < kt1) {
+    la.fetch(sa, (int64_t)kt0 * BK, ra);
+    lb.fetch(sb, (int64_t)kt0 * BK, rb);
+    stage_write<LA, BM>(smem, sa, ra, tid);
+    stage_write<LB, BN>(smem + A_BYTES, sb, rb, tid);
+  }
+  __syncthreads();
+
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int buf = (kt - kt0) & 1;
+    char* As = smem + buf * (A_BYTES + B_BYTES);
+    char* Bs = As + A_BYTES;
+    const bool more = kt + 1 < kt1;
+    if (more) {
+      la.fetch(sa, (int64_t)(kt + 1) * BK, ra);
+      lb.fetch(sb, (int64_t)(kt + 1) * BK, rb);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      mfma_bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = read_frag<LA::kMajor, BM>(As, wm * WM + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = read_frag<LB::kMajor, BN>(Bs, wn * WN + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      char* An = smem + (buf ^ 1) * (A_BYTES + B_BYTES);
+      stage_write<LA, BM>(An, sa, ra, tid);
+      stage_write<LB, BN>(An + A_BYTES, sb, rb, tid);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: acc[i][j][r] = C[m0 + wm*WM + 16 i + (lane & 15)][n0 + wn*WN + 16 j + 4 (lane >> 4) + r]
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int64_t m = m0 + wm * WM + 16 * i + (lane & 15);
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int64_t n = n0 + wn * WN + 16 * j + 4 * (lane >> 4);
+      if (n >= N) continue;
+      f32x4 v = acc[i][j];
+      if (epi.slab) {
+        float* dst = epi.slab + (int64_t)blockIdx.y * M * N + m * N + n;
+        *reinterpret_cast<f32x4*>(dst) = v;
+        continue;
+      }
+      if (epi.bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          v[r] += epi.bias_f32 ? ((const float*)epi.bias)[n + r] : bf2f(((const bf16_t*)epi.bias)[n + r]);
+      }
+      if (epi.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (epi.c_f32) {
+        *reinterpret_cast<f32x4*>((float*)epi.C + m * epi.ldc + n) = v;
+      } else {
+        u16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = f2bf(v[r]);
+        *reinterpret_cast<u16x4*>((bf16_t*)epi.C + m * epi.ldc + n) = o;
+      }
+    }
+  }
+}
+
+// Split-K reduction: out[m, n] = act(sum_s slab[s, m, n] + bias[n])
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t M,
+                                                            int64_t N, Epi epi) {
+  const int64_t total4 = M * N / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total4; t += stride) {
+    f32x4 v = *reinterpret_cast<const f32x4*>(slab + t * 4);
+    for (int s = 1; s < splits; ++s) {
+      const f32x4 u = *reinterpret_cast<const f32x4*>(slab + (int64_t)s * M * N + t * 4);
+      v += u;
+    }
+    const int64_t m = (t * 4) / N, n = (t * 4) % N;
+    if (epi.bias) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        v[r] += epi.bias_f32 ? ((const float*)epi.bias)[n + r] : bf2f(((const bf16_t*)epi.bias)[n + r]);
+    }
+    if (epi.relu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+    }
+    if (epi.c_f32) {
+      *reinterpret_cast<f32x4*>((float*)epi.C + m * epi.ldc + n) = v;
+    } else {
+      u16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = f2bf(v[r]);
+      *reinterpret_cast<u16x4*>((bf16_t*)epi.C + m * epi.ldc + n) = o;
+    }
+  }
+}
+
+// Weight transpose for conv dgrad: wt[ci][r][s][co] = w[co][r][s][ci]
+__global__ void __launch_bounds__(256) conv_wt_transpose_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
+                                                                int Cout, int RS, int Cin) {
+  __shared__ bf16_t tile[32][33];
+  const int rs = blockIdx.z;
+  const int co0 = blockIdx.y * 32, ci0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int yy = ty; yy < 32; yy += 8) {
+    const int co = co0 + yy, ci = ci0 + tx;
+    tile[yy][tx] = (co < Cout && ci < Cin) ? w[((int64_t)co * RS + rs) * Cin + ci] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int yy = ty; yy < 32; yy += 8) {
+    const int ci = ci0 + yy, co = co0 + tx;
+    if (co < Cout && ci < Cin) wt[((int64_t)ci * RS + rs) * Cout + co] = tile[tx][yy];
+  }
+}
+
+// ------------------------------------------------------------------ host-side dispatch
+struct Plan {
+  int bn;           // 64 or 128
+  int tiles_m, tiles_n, splits, ktiles_per_split;
+};
+
+Plan plan_gemm(int64_t M, int64_t N, int64_t K, bool allow_split, int target_blocks) {
+  Plan p;
+  p.bn = N <= 64 ? 64 : 128;
+  p.tiles_m = (int)((M + 127) / 128);
+  p.tiles_n = (int)((N + p.bn - 1) / p.bn);
+  const int ktiles = (int)((K + BK - 1) / BK);
+  p.splits = 1;
+  const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
+  if (allow_split && tiles < target_blocks) {
+    int s = (int)(target_blocks / tiles);
+    const int max_s = ktiles / 4 > 1 ? ktiles / 4 : 1;  // keep >= 4 K-tiles per split
+    if (s > max_s) s = max_s;
+    if (s > 64) s = 64;
+    p.splits = s < 1 ? 1 : s;
+  }
+  p.ktiles_per_split = (ktiles + p.splits - 1) / p.splits;
+  p.splits = (ktiles + p.ktiles_per_split - 1) / p.ktiles_per_split;
+  if (p.splits < 1) p.splits = 1;
+  return p;
+}
+
+template <int BN, class LA, class LB>
+hipError_t launch(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, const Plan& p, Epi epi,
+                  float* slab, hipStream_t st) {
+  const int ntiles = p.tiles_m * p.tiles_n;
+  Epi e = epi;
+  if (p.splits > 1) e.slab = slab;
+  gemm_kernel<128, BN, LA, LB><<<dim3(ntiles, p.splits), NT, 0, st>>>(la, lb, M, N, K, p.tiles_n,
+                                                                       p.ktiles_per_split, e);
+  PDA_CHECK_HIP(hipGetLastError());
+  if (p.splits > 1) {
+    int64_t g = (M * N / 4 + 255) / 256;
+    if (g > 8192) g = 8192;
+    splitk_reduce_kernel<<<(int)(g < 1 ? 1 : g), 256, 0, st>>>(slab, p.splits, M, N, epi);
+    PDA_CHECK_HIP(hipGetLastError());
+  }
+  return hipSuccess;
+}
+
+template <template <int> class TA, template <int> class TB, class MakeA, class MakeB>
+hipError_t dispatch_bn(int64_t M, int64_t N, int64_t K, const Plan& p, Epi epi, float* slab, hipStream_t st,
+                       MakeA make_a, MakeB make_b) {
+  if (p.bn == 64) return launch<64>(make_a(TA<128>{}), make_b(TB<64>{}), M, N, K, p, epi, slab, st);
+  return launch<128>(make_a(TA<128>{}), make_b(TB<128>{}), M, N, K, p, epi, slab, st);
+}
+
+ConvGeom make_geom(int H, int W, int C, int P, int Q, int R, int S, int st, int pad, int dil, int Cg) {
+  ConvGeom g;
+  g.H = H; g.W = W; g.C = C; g.P = P; g.Q = Q; g.R = R; g.S = S; g.st = st; g.pad = pad; g.dil = dil; g.Cg = Cg;
+  g.fC = make_fastdiv((uint32_t)Cg);
+  g.fS = make_fastdiv((uint32_t)S);
+  g.fQ = make_fastdiv((uint32_t)Q);
+  g.fP = make_fastdiv((uint32_t)P);
+  g.fW = make_fastdiv((uint32_t)W);
+  g.fH = make_fastdiv((uint32_t)H);
+  return g;
+}
+
+}  // namespace
+
+int64_t gemm_slab_floats(int64_t M, int64_t N, int64_t K, bool allow_split) {
+  Plan p = plan_gemm(M, N, K, allow_split, 512);
+  return p.splits > 1 ? (int64_t)p.splits * M * N : 0;
+}
+
+// C[M,N] = A[M,K] * B[K,N].  a_kmajor: A(m,k)=A[m*lda+k] else A[k*lda+m];
+// b_kmajor: B(k,n)=B[n*ldb+k] else B[k*ldb+n].  K, N must be multiples of 8 (N of 4 for the store).
+hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
+                     void* C, bool c_f32, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
+                     bool bias_f32, bool relu, float* slab, bool allow_split, hipStream_t st) {
+  Plan p = plan_gemm(M, N, K, allow_split && slab != nullptr, 512);
+  Epi epi{C, ldc, c_f32 ? 1 : 0, bias, bias_f32 ? 1 : 0, relu ? 1 : 0, nullptr};
+  auto mk_ak = [&](auto t) { t.p = A; t.rows = M; t.K = K; t.ld = lda; return t; };
+  auto mk_amn = [&](auto t) { t.p = A; t.K = K; t.cols = M; t.ld = lda; return t; };
+  auto mk_bk = [&](auto t) { t.p = B; t.rows = N; t.K = K; t.ld = ldb; return t; };
+  auto mk_bmn = [&](auto t) { t.p = B; t.K = K; t.cols = N; t.ld = ldb; return t; };
+  if (a_kmajor && b_kmajor) return dispatch_bn<PlainK, PlainK>(M, N, K, p, epi, slab, st, mk_ak, mk_bk);
+  if (a_kmajor) return dispatch_bn<PlainK, PlainMN>(M, N, K, p, epi, slab, st, mk_ak, mk_bmn);
+  if (b_kmajor) return dispatch_bn<PlainMN, PlainK>(M, N, K, p, epi, slab, st, mk_amn, mk_bk);
+  return dispatch_bn<PlainMN, PlainMN>(M, N, K, p, epi, slab, st, mk_amn, mk_bmn);
+}
+
+int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, int S, int P, int Q) {
+  if (mode != 2) return 0;  // only wgrad splits K
+  const int64_t M = Cout, Nn = (int64_t)R * S * C, K = (int64_t)N * P * Q;
+  Plan p = plan_gemm(M, Nn, K, true, 512);
+  return p.splits > 1 ? (int64_t)p.splits * M * Nn : 0;
+}
+
+// y[N,P,Q,Cout] = conv(x[N,H,W,C], w[Cout,R,S,C]) (+bias, relu)
+hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int Cout, int R, int S,
+                      int P, int Q, int stride, int pad, int dil, const void* bias, bool bias_f32, bool relu,
+                      hipStream_t st) {
+  const int64_t M = (int64_t)N * P * Q, Nn = Cout, K = (int64_t)R * S * C;
+  Plan p = plan_gemm(M, Nn, K, false, 512);
+  Epi epi{y, Cout, 0, bias, bias_f32 ? 1 : 0, relu ? 1 : 0, nullptr};
+  ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
+  auto mk_a = [&](auto t) { t.x = x; t.g = g; t.M = M; t.K = K; return t; };
+  auto mk_b = [&](auto t) { t.p = w; t.rows = Nn; t.K = K; t.ld = K; return t; };
+  return dispatch_bn<ConvFwdK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
+}
+
+// dx[N,H,W,C] = dgrad(dy[N,P,Q,Cout], wt[C,R,S,Cout])
+hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int N, int H, int W, int C, int Cout, int R,
+                        int S, int P, int Q, int stride, int pad, int dil, hipStream_t st) {
+  const int64_t M = (int64_t)N * H * W, Nn = C, K = (int64_t)R * S * Cout;
+  Plan p = plan_gemm(M, Nn, K, false, 512);
+  Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
+  ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, Cout);
+  auto mk_a = [&](auto t) { t.dy = dy; t.g = g; t.M = M; t.K = K; return t; };
+  auto mk_b = [&](auto t) { t.p = wt; t.rows = Nn; t.K = K; t.ld = K; return t; };
+  return dispatch_bn<ConvDgradK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
+}
+
+// dw[Cout, R*S*C] = dy[NPQ, Cout]^T * im2col(x)[NPQ, R*S*C]   (fp32 or bf16 output)
+hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32, int N, int H, int W, int C,
+                        int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, float* slab,
+                        hipStream_t st) {
+  const int64_t M = Cout, Nn = (int64_t)R * S * C, K = (int64_t)N * P * Q;
+  Plan p = plan_gemm(M, Nn, K, slab != nullptr, 512);
+  Epi epi{dw, Nn, dw_f32 ? 1 : 0, nullptr, 0, 0, nullptr};
+  ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
+  auto mk_a = [&](auto t) { t.p = dy; t.K = K; t.cols = M; t.ld = Cout; return t; };
+  auto mk_b = [&](auto t) { t.x = x; t.g = g; t.K = K; t.cols = Nn; return t; };
+  return dispatch_bn<PlainMN, ConvWgradMN>(M, Nn, K, p, epi, slab, st, mk_a, mk_b);
+}
+
+hipError_t conv_weight_transpose(const bf16_t* w, bf16_t* wt, int Cout, int RS, int Cin, hipStream_t st) {
+  dim3 grid((Cin + 31) / 32, (Cout + 31) / 32, RS);
+  conv_wt_transpose_kernel<<<grid, 256, 0, st>>>(w, wt, Cout, RS, Cin);
+  return hipGetLastError();
+}
+
+}  // namespace pda

@@ -1,0 +1,178 @@
+// Pooling over channels-last activations (SURVEY §2.5 K06 MaxPool2d 3x3/s2/p1 `NB03:333`,
+// K07 AdaptiveAvgPool2d(1) `NB03:341`).
+//
+// MaxPool saves the in-window argmax as one byte per output element (the window is at most 255
+// positions), so the backward is a gather over the <= ceil(k/s)^2 windows that cover each input
+// pixel: no atomics, no [N,H,W,C] index tensor.  Each lane owns 8 channels (16-B accesses).
+#include "pda_common.h"
+#include "pda_kernels.h"
+
+namespace pda {
+namespace {
+
+constexpr int kThreads = 256;
+
+inline int ew_grid(int64_t n) {
+  int64_t g = (n + kThreads - 1) / kThreads;
+  if (g > 16384) g = 16384;
+  return g < 1 ? 1 : (int)g;
+}
+
+__global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                               uint8_t* __restrict__ idx, int N, int H, int W, int C,
+                                                               int P, int Q, int k, int s, int pad) {
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * P * Q * cv;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int c8 = (int)(t % cv);
+    int64_t pix = t / cv;
+    const int q = (int)(pix % Q);
+    pix /= Q;
+    const int p = (int)(pix % P);
+    const int n = (int)(pix / P);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      best[j] = -INFINITY;
+      bi[j] = 0;
+    }
+    for (int kh = 0; kh < k; ++kh) {
+      const int h = p * s - pad + kh;
+      if (h < 0 || h >= H) continue;
+      for (int kw = 0; kw < k; ++kw) {
+        const int w = q * s - pad + kw;
+        if (w < 0 || w >= W) continue;
+        float v[8];
+        load8(x + (((int64_t)n * H + h) * W + w) * C + c8 * 8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (v[j] > best[j] || (v[j] != v[j])) {  // NaN propagates like torch
+            best[j] = v[j];
+            bi[j] = (uint8_t)(kh * k + kw);
+          }
+      }
+    }
+    store8(y + t * 8, best);
+    uint64_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) packed |= (uint64_t)bi[j] << (8 * j);
+    *reinterpret_cast<uint64_t*>(idx + t * 8) = packed;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) maxpool_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                               const uint8_t* __restrict__ idx,
+                                                               bf16_t* __restrict__ dx, int N, int H, int W, int C,
+                                                               int P, int Q, int k, int s, int pad) {
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * H * W * cv;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int c8 = (int)(t % cv);
+    int64_t pix = t / cv;
+    const int w = (int)(pix % W);
+    pix /= W;
+    const int h = (int)(pix % H);
+    const int n = (int)(pix / H);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    // outputs p with p*s - pad <= h <= p*s - pad + k - 1
+    const int p_lo = max(0, (h + pad - k + s) / s), p_hi = min(P - 1, (h + pad) / s);
+    const int q_lo = max(0, (w + pad - k + s) / s), q_hi = min(Q - 1, (w + pad) / s);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int kh = h - (p * s - pad);
+      if (kh < 0 || kh >= k) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int kw = w - (q * s - pad);
+        if (kw < 0 || kw >= k) continue;
+        const int64_t o = (((int64_t)n * P + p) * Q + q) * C + c8 * 8;
+        const uint64_t packed = *reinterpret_cast<const uint64_t*>(idx + o);
+        float g[8];
+        load8(dy + o, g);
+        const uint8_t me = (uint8_t)(kh * k + kw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if ((uint8_t)(packed >> (8 * j)) == me) acc[j] += g[j];
+      }
+    }
+    store8(dx + t * 8, acc);
+  }
+}
+
+// Global average pool: x [N, HW, C] -> y [N, C]
+template <typename O>
+__global__ void __launch_bounds__(kThreads) avgpool_fwd_kernel(const bf16_t* __restrict__ x, O* __restrict__ y, int N,
+                                                               int HW, int C) {
+  const int cv = C / 8;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * cv) return;
+  const int n = (int)(t / cv), c8 = (int)(t % cv);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  const bf16_t* base = x + (int64_t)n * HW * C + c8 * 8;
+  for (int i = 0; i < HW; ++i) {
+    float v[8];
+    load8(base + (int64_t)i * C, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+  const float r = 1.f / (float)HW;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] *= r;
+  store8(y + (int64_t)n * C + c8 * 8, acc);
+}
+
+template <typename G>
+__global__ void __launch_bounds__(kThreads) avgpool_bwd_kernel(const G* __restrict__ dy, bf16_t* __restrict__ dx,
+                                                               int N, int HW, int C) {
+  const int cv = C / 8;
+  const int64_t total = (int64_t)N * HW * cv;
+  const float r = 1.f / (float)HW;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int c8 = (int)(t % cv);
+    const int n = (int)(t / cv / HW);
+    float g[8];
+    load8(dy + (int64_t)n * C + c8 * 8, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] *= r;
+    store8(dx + t * 8, g);
+  }
+}
+
+}  // namespace
+
+hipError_t maxpool2d_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int k,
+                         int s, int pad, hipStream_t st) {
+  const int64_t total = (int64_t)N * P * Q * (C / 8);
+  maxpool_fwd_kernel<<<ew_grid(total), kThreads, 0, st>>>(x, y, idx, N, H, W, C, P, Q, k, s, pad);
+  return hipGetLastError();
+}
+
+hipError_t maxpool2d_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C, int P, int Q,
+                         int k, int s, int pad, hipStream_t st) {
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  maxpool_bwd_kernel<<<ew_grid(total), kThreads, 0, st>>>(dy, idx, dx, N, H, W, C, P, Q, k, s, pad);
+  return hipGetLastError();
+}
+
+hipError_t avgpool_global_fwd(const bf16_t* x, void* y, bool y_bf16, int N, int HW, int C, hipStream_t st) {
+  const int64_t total = (int64_t)N * (C / 8);
+  const int grid = (int)((total + kThreads - 1) / kThreads);
+  if (y_bf16) avgpool_fwd_kernel<bf16_t><<<grid, kThreads, 0, st>>>(x, (bf16_t*)y, N, HW, C);
+  else avgpool_fwd_kernel<float><<<grid, kThreads, 0, st>>>(x, (float*)y, N, HW, C);
+  return hipGetLastError();
+}
+
+hipError_t avgpool_global_bwd(const void* dy, bool dy_bf16, bf16_t* dx, int N, int HW, int C, hipStream_t st) {
+  const int64_t total = (int64_t)N * HW * (C / 8);
+  if (dy_bf16) avgpool_bwd_kernel<bf16_t><<<ew_grid(total), kThreads, 0, st>>>((const bf16_t*)dy, dx, N, HW, C);
+  else avgpool_bwd_kernel<float><<<ew_grid(total), kThreads, 0, st>>>((const float*)dy, dx, N, HW, C);
+  return hipGetLastError();
+}
+
+}  // namespace pda

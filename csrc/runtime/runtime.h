@@ -1,0 +1,127 @@
+// Native host runtime of pytorchdistributed_amd (SURVEY §2.3 N02 TCPStore/rendezvous, N03 DDP
+// Reducer, §5.8 host ring transport).  CPU-only C++; no HIP or torch dependency.
+#pragma once
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace pda_rt {
+
+// ------------------------------------------------------------------ sockets
+int tcp_listen(const std::string& host, int port, int* bound_port);
+int tcp_connect(const std::string& host, int port, double timeout_s);
+void send_all(int fd, const void* buf, size_t n);
+void recv_all(int fd, void* buf, size_t n);
+
+// ------------------------------------------------------------------ TCP key-value store
+// Rendezvous store with torch c10d Store semantics (set/get/add/wait/check/delete/compare_set).
+// Rank 0 (or the launcher) hosts the server; every rank owns one client connection.
+class StoreServer {
+ public:
+  StoreServer(const std::string& host, int port);
+  ~StoreServer();
+  int port() const { return port_; }
+  void stop();
+
+ private:
+  void loop();
+  int listen_fd_ = -1, port_ = 0;
+  int wake_[2] = {-1, -1};
+  std::thread thread_;
+  std::atomic<bool> stop_{false};
+};
+
+class StoreClient {
+ public:
+  StoreClient(const std::string& host, int port, double timeout_s);
+  ~StoreClient();
+  void set(const std::string& key, const std::string& value);
+  pybind11::bytes get(const std::string& key);
+  int64_t add(const std::string& key, int64_t delta);
+  bool check(const std::vector<std::string>& keys);
+  void wait(const std::vector<std::string>& keys, double timeout_s);
+  bool delete_key(const std::string& key);
+  int64_t num_keys();
+  pybind11::bytes compare_set(const std::string& key, const std::string& expected, const std::string& desired);
+  void set_timeout(double t) { timeout_s_ = t; }
+  double timeout() const { return timeout_s_; }
+
+ private:
+  std::string request(const std::string& msg, double timeout_s);
+  int fd_ = -1;
+  double timeout_s_;
+  std::mutex mu_;
+};
+
+// ------------------------------------------------------------------ DDP bucket reducer
+// Assigns parameters to gradient buckets (reverse registration order ~ backward order, a small first
+// bucket so communication starts early, per-dtype buckets, cap in bytes) and tracks readiness.
+// Buckets are released strictly in index order so every rank issues collectives in the same order.
+class BucketReducer {
+ public:
+  BucketReducer(const std::vector<int64_t>& numels, const std::vector<int64_t>& elem_sizes,
+                const std::vector<int>& dtype_ids, int64_t bucket_cap_bytes, int64_t first_bucket_bytes,
+                int64_t align_elems, const std::vector<int64_t>& order);
+  int num_buckets() const { return (int)buckets_.size(); }
+  std::vector<int64_t> bucket_params(int b) const { return buckets_.at(b).params; }
+  std::vector<int64_t> bucket_offsets(int b) const { return buckets_.at(b).offsets; }
+  int64_t bucket_numel(int b) const { return buckets_.at(b).numel; }
+  int bucket_dtype(int b) const { return buckets_.at(b).dtype; }
+  int param_bucket(int64_t p) const { return param_bucket_.at(p); }
+  void prepare();
+  std::vector<int> mark_ready(int64_t p);
+  std::vector<int> flush_unready();  // mark every unready parameter ready (unused params), return buckets
+  bool all_launched() const { return next_launch_ == (int)buckets_.size(); }
+  std::vector<int64_t> unready_params() const;
+  std::vector<int64_t> ready_order() const { return ready_order_; }
+
+ private:
+  struct Bucket {
+    std::vector<int64_t> params, offsets;
+    int64_t numel = 0;
+    int dtype = 0;
+    int pending = 0;
+  };
+  std::vector<Bucket> buckets_;
+  std::vector<int> param_bucket_;
+  std::vector<char> ready_;
+  std::vector<int64_t> ready_order_;
+  int next_launch_ = 0;
+};
+
+// ------------------------------------------------------------------ host ring transport
+// The ring algorithm of the reference's DDP chapter (`02 DDP基本概念/02_ddp.ipynb` raw lines
+// 33-47: N-1 scatter-reduce steps then N-1 all-gather steps), executable over TCP for CPU tensors.
+class HostRing {
+ public:
+  HostRing(int rank, int world);
+  ~HostRing();
+  std::string listen(const std::string& host);
+  void connect(const std::string& right_host, int right_port, double timeout_s);
+  void allreduce_f32(uintptr_t data, int64_t n);
+  void allreduce_f64(uintptr_t data, int64_t n);
+  void broadcast(uintptr_t data, int64_t bytes, int root);
+  void allgather(uintptr_t in, uintptr_t out, int64_t bytes);
+  void barrier();
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+
+ private:
+  template <typename T>
+  void allreduce(T* data, int64_t n);
+  void sendrecv(const void* sbuf, size_t sn, void* rbuf, size_t rn);
+  int rank_, world_;
+  int listen_fd_ = -1, right_fd_ = -1, left_fd_ = -1;
+};
+
+void bind_runtime(pybind11::module& m);
+
+}  // namespace pda_rt

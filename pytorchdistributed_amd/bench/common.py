@@ -1,0 +1,50 @@
+"""Shared benchmark plumbing: distributed setup from the torchrun / pda-run env contract and the
+timed-window protocol (barrier + synchronize on both sides, MAX over ranks)."""
+from __future__ import annotations
+
+import json
+import os
+
+import torch
+import torch.distributed as dist
+
+from .. import distributed as pdist
+from ..utils.timing import StepTimer
+
+
+def setup(n_gpus: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if n_gpus != world and world > 1:
+        raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
+    use_gpu = torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(local)
+    if world > 1 and not dist.is_initialized():
+        pdist.init_process_group("nccl" if use_gpu else "gloo", rank=rank, world_size=world,
+                                 device_id=local if use_gpu else None)
+    device = torch.device("cuda", local) if use_gpu else torch.device("cpu")
+    return rank, world, local, device
+
+
+def timed(step_fn, steps: int, warmup: int) -> float:
+    """Run ``warmup`` untimed steps, then time exactly ``steps``; returns max-over-ranks seconds."""
+    for _ in range(warmup):
+        step_fn()
+    t = StepTimer()
+    t.start()
+    for _ in range(steps):
+        step_fn()
+    secs = t.stop()
+    return t.max_over_ranks(secs)
+
+
+def emit(record: dict, rank: int):
+    if rank == 0:
+        print(json.dumps(record), flush=True)
+
+
+def teardown():
+    if dist.is_initialized():
+        pdist.destroy_process_group()

@@ -1,0 +1,77 @@
+"""Headline benchmark: ResNet-50 DDP images/sec on 1/2/4/8 MI355X (BASELINE.json metric / config 2).
+
+Model: ResNet-50 v1.5 random init, bf16 parameters + fp32 masters (fused SGD, momentum 0.9, wd 5e-5);
+data: synthetic ImageNet-shape batches (224x224, 1000 classes) generated on device every step;
+parallelism: one process per GPU, gradients all-reduced by the bucketed DDP over RCCL, overlapped with
+backward.  Weak scaling: the per-GPU batch is fixed.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+
+import torch
+
+from ..data.device import DeviceSyntheticImages
+from ..models.resnet import resnet50
+from ..ops import cross_entropy
+from ..optim import SGD
+from ..parallel.ddp import DistributedDataParallel
+from .common import emit, setup, teardown, timed
+
+METRIC = "images/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X; scaling efficiency"
+
+
+def build(batch: int, image: int, device, rank: int, dtype=torch.bfloat16, bucket_mb=None):
+    torch.manual_seed(0)
+    model = resnet50(device=device, dtype=dtype)
+    model = DistributedDataParallel(model, device_ids=[device.index] if device.type == "cuda" else None,
+                                    bucket_cap_mb=bucket_mb)
+    opt = SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=5e-5)
+    data = DeviceSyntheticImages(batch, image, 1000, device=device, dtype=dtype, seed=1234, rank=rank)
+
+    def step():
+        x, y = data.next()
+        opt.zero_grad(set_to_none=True)
+        out = model(x)
+        loss = cross_entropy(out, y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    return model, opt, step
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("PDA_BENCH_BATCH", "256")),
+                    help="per-GPU batch")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--bucket-mb", type=float, default=None)
+    a = ap.parse_args(argv)
+    rank, world, local, device = setup(a.gpus)
+    if device.type == "cpu":  # plumbing-only run on a machine without a GPU
+        a.batch, a.image = min(a.batch, 2), min(a.image, 64)
+    _, _, step = build(a.batch, a.image, device, rank, bucket_mb=a.bucket_mb)
+    secs = timed(step, a.steps, a.warmup)
+    ms = secs / a.steps * 1e3
+    imgs = a.batch * world * a.steps / secs
+    emit({
+        "metric": METRIC, "value": round(imgs, 2), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16" if device.type == "cuda" else "bf16-cpu-plumbing",
+        "data": "synthetic (on-device Philox, ImageNet shape 224x224x3, 1000 classes), random-init weights",
+        "config": {"model": "resnet50", "global_batch": a.batch * world, "per_gpu_batch": a.batch,
+                   "image_size": a.image, "seq_len": None, "parallelism": f"dp{world}",
+                   "optimizer": "SGD(momentum=0.9, wd=5e-5), fp32 master weights"},
+        "notes": "reference publishes no number for this metric (BASELINE.json published={}); NB03 parity "
+                 "numbers are produced by pytorchdistributed_amd.bench.nb03",
+    }, rank)
+    teardown()
+
+
+if __name__ == "__main__":
+    main()

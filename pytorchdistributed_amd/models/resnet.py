@@ -1,0 +1,148 @@
+"""ResNet-50 v1.5, channels-last, built on the framework's native layers.
+
+Reference: torchvision ``ResNet(Bottleneck, [3, 4, 6, 3], 1000)`` used in
+`03 模型并行/03_model_parallel.ipynb` (raw lines 107-110, 314: 25,557,032 parameters; the model/pipeline
+parallel variants at raw lines 325-349 and 538-561).  torchvision is not available on the target, so
+the architecture is re-built here: same layer names (``conv1``, ``bn1``, ``layer1..4``, ``fc``, blocks
+``conv1..3`` / ``bn1..3`` / ``downsample``), same parameter count, stride on the 3x3 conv (v1.5).
+
+Differences by design (MI355X-first):
+* activations are ``[N, H, W, C]`` and conv weights OHWI; the stem accepts 3-channel input and pads
+  it to 8 channels on device (implicit-GEMM gathers want 16-byte channel vectors);
+* BN+ReLU and BN+residual-add+ReLU are single fused kernels (``bn(x, residual=..., relu=True)``).
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+import torch.nn as tnn
+import torch.nn.functional as F
+
+from .. import nn as pnn
+from .. import ops
+
+
+class Bottleneck(tnn.Module):
+    expansion = 4
+
+    def __init__(self, inplanes, planes, stride=1, downsample=False, device=None, dtype=None):
+        super().__init__()
+        kw = dict(device=device, dtype=dtype)
+        width = planes
+        self.conv1 = pnn.Conv2d(inplanes, width, 1, **kw)
+        self.bn1 = pnn.BatchNorm2d(width, **kw)
+        self.conv2 = pnn.Conv2d(width, width, 3, stride=stride, padding=1, **kw)
+        self.bn2 = pnn.BatchNorm2d(width, **kw)
+        self.conv3 = pnn.Conv2d(width, planes * 4, 1, **kw)
+        self.bn3 = pnn.BatchNorm2d(planes * 4, **kw)
+        if downsample:
+            self.downsample = tnn.Sequential(pnn.Conv2d(inplanes, planes * 4, 1, stride=stride, **kw),
+                                             pnn.BatchNorm2d(planes * 4, **kw))
+        else:
+            self.downsample = None
+
+    def forward(self, x):
+        out = self.bn1(self.conv1(x), relu=True)
+        out = self.bn2(self.conv2(out), relu=True)
+        if self.downsample is not None:
+            idn = self.downsample[1](self.downsample[0](x))
+        else:
+            idn = x
+        return self.bn3(self.conv3(out), residual=idn, relu=True)
+
+
+class Stem(tnn.Module):
+    def __init__(self, device=None, dtype=None):
+        super().__init__()
+        self.conv1 = pnn.Conv2d(3, 64, 7, stride=2, padding=3, device=device, dtype=dtype)
+        self.bn1 = pnn.BatchNorm2d(64, device=device, dtype=dtype)
+        self.maxpool = pnn.MaxPool2d(3, 2, 1)
+
+    def forward(self, x):
+        if x.dim() == 4 and x.shape[1] == 3 and x.shape[-1] != 3:  # NCHW input -> NHWC
+            x = x.permute(0, 2, 3, 1)
+        if x.is_cuda and x.shape[-1] % 8 != 0:
+            x = F.pad(x, (0, 8 - x.shape[-1] % 8))
+        x = x.contiguous()
+        return self.maxpool(self.bn1(self.conv1(x), relu=True))
+
+
+class ResNet(tnn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, device=None, dtype=None):
+        super().__init__()
+        kw = dict(device=device, dtype=dtype)
+        self.stem = Stem(**kw)
+        inplanes = 64
+        for i, (planes, n) in enumerate(zip((64, 128, 256, 512), layers)):
+            stride = 1 if i == 0 else 2
+            blocks = []
+            for j in range(n):
+                blocks.append(Bottleneck(inplanes, planes, stride if j == 0 else 1, downsample=(j == 0), **kw))
+                inplanes = planes * 4
+            setattr(self, f"layer{i + 1}", tnn.Sequential(*blocks))
+        self.fc = pnn.Linear(512 * 4, num_classes, **kw)
+
+    # torchvision-compatible aliases for the stem layers
+    @property
+    def conv1(self):
+        return self.stem.conv1
+
+    @property
+    def bn1(self):
+        return self.stem.bn1
+
+    def features(self, x):
+        x = self.stem(x)
+        x = self.layer1(x)
+        x = self.layer2(x)
+        x = self.layer3(x)
+        return self.layer4(x)
+
+    def forward(self, x):
+        x = self.features(x)
+        x = ops.global_avg_pool2d(x)
+        return self.fc(x)
+
+    def stage_modules(self) -> List[tnn.Module]:
+        """Ordered top-level stages (used by model/pipeline parallel splits, `NB03:325-349`)."""
+        return [self.stem, self.layer1, self.layer2, self.layer3, self.layer4, _Head(self.fc)]
+
+
+class _Head(tnn.Module):
+    def __init__(self, fc):
+        super().__init__()
+        self.fc = fc
+
+    def forward(self, x):
+        return self.fc(ops.global_avg_pool2d(x))
+
+
+def resnet50(num_classes=1000, device=None, dtype=None) -> ResNet:
+    return ResNet((3, 4, 6, 3), num_classes, device=device, dtype=dtype)
+
+
+def num_parameters(model: tnn.Module) -> int:
+    return sum(p.numel() for p in model.parameters())
+
+
+def to_torchvision_state_dict(model: ResNet) -> dict:
+    """Convert to torchvision key/layout conventions (OIHW conv weights, ``conv1``/``bn1`` at top level)."""
+    out = {}
+    for k, v in model.state_dict().items():
+        if k.startswith("stem."):
+            k = k[len("stem."):]
+        if v.dim() == 4:
+            v = v.permute(0, 3, 1, 2).contiguous()
+        out[k] = v
+    return out
+
+
+def from_torchvision_state_dict(model: ResNet, sd: dict):
+    mine = {}
+    for k, v in sd.items():
+        key = ("stem." + k) if (k.startswith("conv1") or k.startswith("bn1")) else k
+        if v.dim() == 4:
+            v = v.permute(0, 2, 3, 1).contiguous()
+        mine[key] = v
+    return model.load_state_dict(mine)

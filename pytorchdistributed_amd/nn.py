@@ -1,0 +1,135 @@
+"""``nn.Module`` layers over :mod:`pytorchdistributed_amd.ops`.
+
+Image layers are channels-last: activations ``[N, H, W, C]``, conv weights ``[C_out, R, S, C_in]``.
+Parameter initialisation follows torch's defaults (kaiming-uniform(a=sqrt(5)) for conv / linear,
+ones / zeros for norms) so parameter counts and init statistics match the reference's torch models.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as tnn
+
+from . import ops
+
+
+def _kaiming_uniform_(w: torch.Tensor, fan_in: int):
+    bound = 1.0 / math.sqrt(fan_in) * math.sqrt(3.0) * math.sqrt(2.0 / (1 + 5))
+    with torch.no_grad():
+        w.uniform_(-bound, bound)
+    return w
+
+
+class Linear(tnn.Module):
+    def __init__(self, in_features, out_features, bias=True, relu=False, device=None, dtype=None):
+        super().__init__()
+        self.in_features, self.out_features, self.relu = in_features, out_features, relu
+        self.weight = tnn.Parameter(torch.empty(out_features, in_features, device=device, dtype=dtype))
+        self.bias = tnn.Parameter(torch.empty(out_features, device=device, dtype=dtype)) if bias else None
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        _kaiming_uniform_(self.weight, self.in_features)
+        if self.bias is not None:
+            b = 1.0 / math.sqrt(self.in_features) if self.in_features > 0 else 0
+            with torch.no_grad():
+                self.bias.uniform_(-b, b)
+
+    def forward(self, x):
+        return ops.linear(x, self.weight, self.bias, self.relu)
+
+    def extra_repr(self):
+        return f"in_features={self.in_features}, out_features={self.out_features}, bias={self.bias is not None}"
+
+
+class Conv2d(tnn.Module):
+    """Channels-last conv; ``weight`` is OHWI."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1, bias=False,
+                 device=None, dtype=None):
+        super().__init__()
+        k = kernel_size
+        self.in_channels, self.out_channels, self.kernel_size = in_channels, out_channels, k
+        self.stride, self.padding, self.dilation = stride, padding, dilation
+        self.weight = tnn.Parameter(torch.empty(out_channels, k, k, in_channels, device=device, dtype=dtype))
+        self.bias = tnn.Parameter(torch.zeros(out_channels, device=device, dtype=dtype)) if bias else None
+        _kaiming_uniform_(self.weight, in_channels * k * k)
+
+    def forward(self, x, relu=False):
+        return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, relu)
+
+    def extra_repr(self):
+        return (f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, stride={self.stride}, "
+                f"padding={self.padding}")
+
+
+class BatchNorm2d(tnn.Module):
+    """BatchNorm over the channel (last) dim; running statistics stay fp32 whatever the param dtype."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, device=None, dtype=None):
+        super().__init__()
+        self.num_features, self.eps, self.momentum = num_features, eps, momentum
+        if affine:
+            self.weight = tnn.Parameter(torch.ones(num_features, device=device, dtype=dtype))
+            self.bias = tnn.Parameter(torch.zeros(num_features, device=device, dtype=dtype))
+        else:
+            self.weight = self.bias = None
+        self.register_buffer("running_mean", torch.zeros(num_features, device=device))
+        self.register_buffer("running_var", torch.ones(num_features, device=device))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long, device=device))
+
+    def _apply(self, fn, recurse=True):
+        # keep running stats in fp32 when the module is cast to bf16
+        rm, rv = self.running_mean, self.running_var
+        super()._apply(fn, recurse)
+        if self.running_mean.dtype != torch.float32:
+            self.running_mean = fn(rm).float()
+            self.running_var = fn(rv).float()
+        return self
+
+    def forward(self, x, residual=None, relu=False):
+        if self.training:
+            self.num_batches_tracked.add_(1)
+        return ops.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
+                              self.momentum, self.eps, residual=residual, relu=relu)
+
+
+class ReLU(tnn.Module):
+    def forward(self, x):
+        return ops.relu(x)
+
+
+class MaxPool2d(tnn.Module):
+    def __init__(self, kernel_size=3, stride=2, padding=1):
+        super().__init__()
+        self.k, self.s, self.p = kernel_size, stride, padding
+
+    def forward(self, x):
+        return ops.max_pool2d(x, self.k, self.s, self.p)
+
+
+class GlobalAvgPool2d(tnn.Module):
+    def forward(self, x):
+        return ops.global_avg_pool2d(x)
+
+
+class LayerNorm(tnn.Module):
+    def __init__(self, dim, eps=1e-5, device=None, dtype=None):
+        super().__init__()
+        self.eps = eps
+        self.weight = tnn.Parameter(torch.ones(dim, device=device, dtype=dtype))
+        self.bias = tnn.Parameter(torch.zeros(dim, device=device, dtype=dtype))
+
+    def forward(self, x):
+        return ops.layer_norm(x, self.weight, self.bias, self.eps)
+
+
+class RMSNorm(tnn.Module):
+    def __init__(self, dim, eps=1e-5, device=None, dtype=None):
+        super().__init__()
+        self.eps = eps
+        self.weight = tnn.Parameter(torch.ones(dim, device=device, dtype=dtype))
+
+    def forward(self, x):
+        return ops.rms_norm(x, self.weight, self.eps)

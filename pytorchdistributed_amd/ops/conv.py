@@ -1,0 +1,58 @@
+"""2-D convolution, channels-last (reference: torchvision ResNet-50 convs
+`03 模型并行/03_model_parallel.ipynb` raw lines 314, 325-349, reached through cuDNN).
+
+GPU: implicit-GEMM MFMA kernels (`csrc/kernels/gemm_conv.hip`) for forward, data-gradient (the
+stride is folded into the gather, weights transposed to [C_in, R, S, C_out] on the fly) and
+weight-gradient (split-K over N*P*Q with a deterministic slab reduction).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .._native import C
+
+
+def _ref_conv(x, w, stride, padding, dilation, bias=None):
+    y = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), bias, stride, padding, dilation)
+    return y.permute(0, 2, 3, 1).contiguous()
+
+
+class _Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias, stride, padding, dilation, relu):
+        x = x.contiguous()
+        w = w.contiguous()
+        y = C().conv_fwd(x, w, stride, padding, dilation, bias, relu)
+        ctx.save_for_backward(x, w, y if relu else None)
+        ctx.cfg = (stride, padding, dilation, relu, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        stride, padding, dilation, relu, has_bias = ctx.cfg
+        dy = dy.contiguous()
+        if relu:
+            dy = C().relu_bwd(dy, y)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation)
+        if ctx.needs_input_grad[1]:
+            dw = C().conv_wgrad(dy, x, w.shape[1], w.shape[2], stride, padding, dilation, w.dtype == torch.float32)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.reshape(-1, dy.shape[-1]).sum(0, dtype=torch.float32).to(dy.dtype)
+        return dx, dw, db, None, None, None, None
+
+
+def conv2d(x: torch.Tensor, weight: torch.Tensor, bias=None, stride: int = 1, padding: int = 0, dilation: int = 1,
+           relu: bool = False) -> torch.Tensor:
+    """``y[N,P,Q,Co] = conv(x[N,H,W,Ci], weight[Co,R,S,Ci])`` (+bias, optional fused ReLU)."""
+    if x.is_cuda:
+        if weight.shape[-1] != x.shape[-1]:  # stem: input channels padded to a multiple of 8
+            weight = F.pad(weight, (0, x.shape[-1] - weight.shape[-1]))
+        return _Conv2dFn.apply(x, weight, bias, stride, padding, dilation, relu)
+    if weight.shape[-1] != x.shape[-1]:
+        x = x[..., : weight.shape[-1]]
+    y = _ref_conv(x, weight, stride, padding, dilation, bias)
+    return torch.relu(y) if relu else y

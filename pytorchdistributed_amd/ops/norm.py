@@ -1,0 +1,96 @@
+"""Normalisation ops.
+
+* :func:`batch_norm` — training/eval BatchNorm over channels-last activations with fused residual add
+  and ReLU (reference ResNet-50 BN ×53, `03_model_parallel.ipynb` raw line 314).
+* :func:`layer_norm`, :func:`rms_norm` — row norms for GPT-2 / Llama-3 (K19, K20).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .._native import C
+
+
+class _BatchNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu):
+        x = x.contiguous()
+        if residual is not None:
+            residual = residual.contiguous()
+        if training:
+            y, mean, invstd = C().bn_fwd_train(x, residual, gamma, beta, running_mean, running_var, momentum, eps,
+                                               relu)
+        else:
+            y = C().bn_fwd_eval(x, residual, gamma, beta, running_mean, running_var, eps, relu)
+            mean = running_mean
+            invstd = torch.rsqrt(running_var + eps)
+        ctx.save_for_backward(x, y if relu else None, mean, invstd, gamma)
+        ctx.cfg = (relu, residual is not None, training)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, invstd, gamma = ctx.saved_tensors
+        relu, has_res, training = ctx.cfg
+        if not training:
+            raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
+        dx, dres, dgamma, dbeta = C().bn_bwd(dy.contiguous(), x, y, mean, invstd, gamma, relu, has_res)
+        dg = dgamma.to(gamma.dtype) if gamma is not None and ctx.needs_input_grad[1] else None
+        db = dbeta.to(gamma.dtype if gamma is not None else dbeta.dtype) if ctx.needs_input_grad[2] else None
+        return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None
+
+
+def _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu):
+    C_ = x.shape[-1]
+    xf = x.reshape(-1, C_)
+    g = gamma.float() if gamma is not None else None
+    b = beta.float() if beta is not None else None
+    y = F.batch_norm(xf.float(), running_mean, running_var, g, b, training, momentum, eps)
+    y = y.reshape(x.shape)
+    if residual is not None:
+        y = y + residual.float()
+    if relu:
+        y = torch.relu(y)
+    return y.to(x.dtype)
+
+
+def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True, momentum=0.1, eps=1e-5,
+               residual=None, relu=False):
+    """BatchNorm over the last (channel) dim of ``x`` (any leading dims), then ``+residual``, then ReLU."""
+    if x.is_cuda and x.dtype == torch.bfloat16:
+        return _BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
+                                  relu)
+    return _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu)
+
+
+class _RowNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, eps, rms):
+        x = x.contiguous()
+        y, mean, rstd = C().rownorm_fwd(x, gamma.contiguous(), beta, eps, rms)
+        ctx.save_for_backward(x, gamma, mean, rstd)
+        ctx.rms = rms
+        ctx.has_beta = beta is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, mean, rstd = ctx.saved_tensors
+        dx, dg, db = C().rownorm_bwd(dy.contiguous(), x, gamma, mean, rstd, ctx.rms)
+        return dx, dg.to(gamma.dtype), (db.to(gamma.dtype) if ctx.has_beta else None), None, None
+
+
+def layer_norm(x, weight, bias, eps=1e-5):
+    if x.is_cuda and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192:
+        return _RowNormFn.apply(x, weight, bias, eps, False)
+    return F.layer_norm(x.float(), (x.shape[-1],), weight.float(), bias.float() if bias is not None else None,
+                        eps).to(x.dtype)
+
+
+def rms_norm(x, weight, eps=1e-6):
+    if x.is_cuda and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192:
+        return _RowNormFn.apply(x, weight, None, eps, True)
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * weight.float()
+    return y.to(x.dtype)

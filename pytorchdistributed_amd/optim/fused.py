@@ -1,0 +1,221 @@
+"""Implementation of the fused optimizers (see package docstring)."""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+
+from .._native import C
+from ..parallel.flat import FlatGroup, flat_group_of
+
+
+class _FusedBase(torch.optim.Optimizer):
+    """Common machinery: per-group flat-path detection, fp32 masters, gradient scale / clip input."""
+
+    _state_names: tuple = ()
+
+    def __init__(self, params, defaults, master_weights: Optional[bool] = None):
+        super().__init__(params, defaults)
+        self.master_weights = master_weights
+        self._flat: Dict[int, dict] = {}  # group index -> flat state
+        self.grad_scale: Optional[torch.Tensor] = None  # device scalar multiplied into every gradient
+
+    # --------------------------------------------------------------- flat path
+    def _flat_for(self, gi: int, group) -> Optional[dict]:
+        params = [p for p in group["params"]]
+        if not params or not params[0].is_cuda:
+            return None
+        fg = flat_group_of(params[0])
+        if fg is None or not fg.covers(params):
+            return None
+        st = self._flat.get(gi)
+        if st is None or st["fg"] is not fg:
+            # low-precision parameters always get an fp32 master; fp32 ones only on request
+            need_master = fg.dtype != torch.float32 or bool(self.master_weights)
+            master = fg.param_buffer.float().clone() if need_master else fg.param_buffer
+            st = {"fg": fg, "master": master, "bf16": fg.param_buffer if fg.dtype == torch.bfloat16 and need_master
+                  else None, "step": 0}
+            for name in self._state_names:
+                st[name] = torch.zeros(fg.numel, dtype=torch.float32, device=fg.device)
+            self._flat[gi] = st
+            # expose per-parameter views as regular optimizer state (checkpoint layout = torch's)
+            for p, off in zip(fg.params, fg.offsets):
+                s = self.state[p]
+                for name in self._state_names:
+                    s[name] = st[name][off: off + p.numel()].view_as(p)
+                if need_master:
+                    s["master_param"] = master[off: off + p.numel()].view_as(p)
+        return st
+
+    def zero_grad(self, set_to_none: bool = True):
+        super().zero_grad(set_to_none=set_to_none)
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            st = self._flat_for(gi, group)
+            if st is not None:
+                fg: FlatGroup = st["fg"]
+                if any(p.grad is None for p in fg.params):
+                    fg.attach_grads()  # grads were set to None without a backward: the flat buffer holds them
+                st["step"] += 1
+                self._flat_update(st, group, fg.grad_buffer)
+                continue
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                self._param_update(p, group)
+        return loss
+
+    # subclasses implement these
+    def _flat_update(self, st, group, grad):
+        raise NotImplementedError
+
+    def _param_update(self, p, group):
+        raise NotImplementedError
+
+    def _gscale_args(self):
+        return (1.0, self.grad_scale)
+
+
+class SGD(_FusedBase):
+    _state_names = ("momentum_buffer",)
+
+    def __init__(self, params, lr=1e-3, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False,
+                 master_weights: Optional[bool] = None):
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay, nesterov=nesterov)
+        super().__init__(params, defaults, master_weights)
+
+    def _flat_update(self, st, group, grad):
+        gs, gs_t = self._gscale_args()
+        C().sgd_step(st["master"], st["bf16"], grad, st["momentum_buffer"], group["lr"], group["momentum"],
+                     group["dampening"], group["weight_decay"], group["nesterov"], st["step"] == 1, gs, gs_t, None)
+
+    def _param_update(self, p, group):
+        s = self.state[p]
+        lr, mom, damp, wd, nest = (group[k] for k in ("lr", "momentum", "dampening", "weight_decay", "nesterov"))
+        if p.is_cuda and p.dtype in (torch.float32, torch.bfloat16) and p.is_contiguous():
+            first = "step" not in s
+            s["step"] = s.get("step", 0) + 1
+            if p.dtype == torch.float32:
+                master, pb = p, None
+            else:
+                if "master_param" not in s:
+                    s["master_param"] = p.detach().float().clone()
+                master, pb = s["master_param"], p
+            if "momentum_buffer" not in s:
+                s["momentum_buffer"] = torch.zeros_like(master)
+            gs, gs_t = self._gscale_args()
+            C().sgd_step(master, pb, p.grad.contiguous(), s["momentum_buffer"], lr, mom, damp, wd, nest, first, gs,
+                         gs_t, None)
+            return
+        # reference math (torch.optim.SGD semantics)
+        g = p.grad.float()
+        if self.grad_scale is not None:
+            g = g * self.grad_scale.to(g.device)
+        if wd != 0:
+            g = g + wd * p.float()
+        if mom != 0:
+            buf = s.get("momentum_buffer")
+            if buf is None:
+                buf = g.clone()
+            else:
+                buf.mul_(mom).add_(g, alpha=1 - damp)
+            s["momentum_buffer"] = buf
+            g = g + mom * buf if nest else buf
+        p.add_((-lr * g).to(p.dtype))
+
+
+class Adam(_FusedBase):
+    _state_names = ("exp_avg", "exp_avg_sq")
+    _decoupled = False
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0,
+                 master_weights: Optional[bool] = None):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults, master_weights)
+
+    def _flat_update(self, st, group, grad):
+        b1, b2 = group["betas"]
+        gs, gs_t = self._gscale_args()
+        C().adam_step(st["master"], st["bf16"], grad, st["exp_avg"], st["exp_avg_sq"], group["lr"], b1, b2,
+                      group["eps"], group["weight_decay"], self._decoupled, st["step"], gs, gs_t, None)
+
+    def _param_update(self, p, group):
+        s = self.state[p]
+        b1, b2 = group["betas"]
+        lr, eps, wd = group["lr"], group["eps"], group["weight_decay"]
+        s["step"] = s.get("step", 0) + 1
+        t = s["step"]
+        if p.is_cuda and p.dtype in (torch.float32, torch.bfloat16) and p.is_contiguous():
+            if p.dtype == torch.float32:
+                master, pb = p, None
+            else:
+                if "master_param" not in s:
+                    s["master_param"] = p.detach().float().clone()
+                master, pb = s["master_param"], p
+            for n in self._state_names:
+                if n not in s:
+                    s[n] = torch.zeros_like(master)
+            gs, gs_t = self._gscale_args()
+            C().adam_step(master, pb, p.grad.contiguous(), s["exp_avg"], s["exp_avg_sq"], lr, b1, b2, eps, wd,
+                          self._decoupled, t, gs, gs_t, None)
+            return
+        g = p.grad.float()
+        if self.grad_scale is not None:
+            g = g * self.grad_scale.to(g.device)
+        pf = p.float()
+        if self._decoupled:
+            pf = pf * (1 - lr * wd)
+        elif wd != 0:
+            g = g + wd * pf
+        for n in self._state_names:
+            if n not in s:
+                s[n] = torch.zeros_like(pf)
+        m, v = s["exp_avg"], s["exp_avg_sq"]
+        m.mul_(b1).add_(g, alpha=1 - b1)
+        v.mul_(b2).addcmul_(g, g, value=1 - b2)
+        denom = (v.sqrt() / math.sqrt(1 - b2 ** t)).add_(eps)
+        pf = pf - (lr / (1 - b1 ** t)) * m / denom
+        p.copy_(pf.to(p.dtype))
+
+
+class AdamW(Adam):
+    _decoupled = True
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
+                 master_weights: Optional[bool] = None):
+        super().__init__(params, lr, betas, eps, weight_decay, master_weights)
+
+
+@torch.no_grad()
+def clip_grad_norm_(parameters, max_norm: float, optimizer: Optional[_FusedBase] = None) -> torch.Tensor:
+    """Total-norm gradient clipping without a host sync.
+
+    With a fused optimizer the clip coefficient is handed over as its device-side ``grad_scale`` (the
+    gradients are not rewritten); otherwise gradients are scaled in place.  Returns the norm (device).
+    """
+    params = [p for p in parameters if p.grad is not None]
+    if not params:
+        return torch.zeros(())
+    fg = flat_group_of(params[0])
+    if params[0].is_cuda and fg is not None and fg.covers(params):
+        out = C().grad_norm(fg.grad_buffer, 1.0, float(max_norm))
+    elif params[0].is_cuda:
+        sq = torch.stack([C().grad_norm(p.grad.contiguous(), 1.0, 0.0)[0] ** 2 for p in params]).sum()
+        norm = sq.sqrt()
+        out = torch.stack([norm, torch.clamp(max_norm / (norm + 1e-6), max=1.0)])
+    else:
+        norm = torch.norm(torch.stack([p.grad.float().norm() for p in params]))
+        out = torch.stack([norm, torch.clamp(max_norm / (norm + 1e-6), max=1.0)])
+    if optimizer is not None and isinstance(optimizer, _FusedBase):
+        optimizer.grad_scale = out[1:2].float()
+    else:
+        for p in params:
+            p.grad.mul_(out[1].to(p.grad.dtype))
+    return out[0]

@@ -1,0 +1,3 @@
+"""Parallelism wrappers."""
+from .ddp import DistributedDataParallel, DDP  # noqa: F401
+from .flat import FlatGroup  # noqa: F401

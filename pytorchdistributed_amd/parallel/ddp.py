@@ -1,0 +1,198 @@
+"""DistributedDataParallel (reference
+``DDP(model, device_ids=[gpu_id])`` at `02 DDP基本概念/ddp_gpus.py:35` and `ddp_gpus_torchrun.py:33`).
+
+MI355X-first design:
+* parameters and gradients live in flat per-dtype buffers (:class:`~.flat.FlatGroup`) laid out in
+  bucket order, so a bucket is a contiguous slice that is all-reduced in place and the fused
+  optimizer updates the whole model in one launch;
+* bucket assignment and readiness tracking are native C++ (``_C.BucketReducer``): buckets are
+  released strictly in index order, so all ranks issue RCCL collectives in the same order;
+* each ready bucket is all-reduced asynchronously (RCCL runs on its own HIP stream, ordered after the
+  producing backward kernels by an event) so communication overlaps the rest of backward; the
+  autograd final callback makes the compute stream wait on every bucket before the optimizer;
+* bucket sizing for xGMI: RCCL rings are per-link bound (7 links x ~153 GB/s per GPU), so buckets
+  default to 32 MB (every peer gets >= 4 MB per ring step) with a small 2 MB first bucket to start
+  communicating early in backward;
+* averaging uses ``ReduceOp.AVG`` on RCCL (no extra pass); on gloo / the native host ring the sum is
+  divided in place.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as tnn
+
+from .. import _native
+from .. import distributed as pdist
+from .flat import FlatGroup, flatten_buffers
+
+_DTYPE_IDS = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}
+
+
+def _mb(env, default):
+    return float(os.environ.get(env, default))
+
+
+class DistributedDataParallel(tnn.Module):
+    def __init__(self, module: tnn.Module, device_ids: Optional[List[int]] = None, output_device=None,
+                 broadcast_buffers: bool = True, process_group=None, bucket_cap_mb: Optional[float] = None,
+                 first_bucket_mb: Optional[float] = None, find_unused_parameters: bool = False,
+                 gradient_as_bucket_view: bool = True, static_graph: bool = False):
+        super().__init__()
+        self.module = module
+        self.device_ids = device_ids
+        self.process_group = process_group
+        self.broadcast_buffers = broadcast_buffers
+        self.find_unused_parameters = find_unused_parameters
+        self.world = pdist.get_world_size(process_group)
+        self.rank = pdist.get_rank(process_group)
+        self.backend = pdist.backend() if dist.is_initialized() else None
+        self.require_backward_grad_sync = True
+        bucket_cap_mb = bucket_cap_mb if bucket_cap_mb is not None else _mb("PDA_BUCKET_MB", 32)
+        first_bucket_mb = first_bucket_mb if first_bucket_mb is not None else _mb("PDA_FIRST_BUCKET_MB", 2)
+
+        params = [p for p in module.parameters() if p.requires_grad]
+        self._params = params
+        # ---- native bucket assignment
+        C = _native.C()
+        self.reducer = C.BucketReducer([p.numel() for p in params], [p.element_size() for p in params],
+                                       [_DTYPE_IDS.get(p.dtype, 9) for p in params], int(bucket_cap_mb * 2 ** 20),
+                                       int(first_bucket_mb * 2 ** 20), 8, [])
+        nb = self.reducer.num_buckets
+        # ---- flat storage in bucket order, one group per dtype
+        by_dtype: Dict[int, list] = {}
+        for b in range(nb):
+            by_dtype.setdefault(self.reducer.bucket_dtype(b), []).append(b)
+        self.groups: Dict[int, FlatGroup] = {}
+        self.bucket_slices: List[tuple] = [None] * nb  # (group, start, numel)
+        for dt, blist in by_dtype.items():
+            gparams, goffs, start = [], [], 0
+            for b in blist:
+                for pi, off in zip(self.reducer.bucket_params(b), self.reducer.bucket_offsets(b)):
+                    gparams.append(params[pi])
+                    goffs.append(start + off)
+                self.bucket_slices[b] = (dt, start, self.reducer.bucket_numel(b))
+                start += self.reducer.bucket_numel(b)
+            self.groups[dt] = FlatGroup(gparams, goffs, start)
+        self._param_index = {id(p): i for i, p in enumerate(params)}
+        # ---- rank-0 state broadcast (X04) as one collective per flat buffer
+        self._buffer_flats = flatten_buffers(module)
+        if self.world > 1:
+            with torch.no_grad():
+                for g in self.groups.values():
+                    self._bcast(g.param_buffer)
+                for flat in self._buffer_flats.values():
+                    self._bcast(flat)
+        for g in self.groups.values():
+            g.attach_grads()
+        # ---- autograd hooks
+        self._works: List = []
+        self._callback_queued = False
+        self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
+        self.reducer.prepare()
+
+    # ------------------------------------------------------------------ communication
+    def _use_ring(self):
+        return self.backend == "ring"
+
+    def _bcast(self, t: torch.Tensor):
+        if self._use_ring() and t.device.type == "cpu":
+            pdist.host_ring().broadcast(t.data_ptr(), t.numel() * t.element_size(), 0)
+        else:
+            dist.broadcast(t, 0, group=self.process_group)
+
+    def _bucket_view(self, b: int) -> torch.Tensor:
+        dt, start, n = self.bucket_slices[b]
+        return self.groups[dt].grad_buffer[start: start + n]
+
+    def _launch(self, b: int):
+        t = self._bucket_view(b)
+        if self.world == 1:
+            return
+        if self._use_ring() and t.device.type == "cpu" and t.dtype in (torch.float32, torch.float64):
+            pdist.ring_all_reduce(t, average=True)
+            return
+        if self.backend == "nccl":
+            self._works.append((dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.process_group,
+                                                async_op=True), None))
+        else:
+            self._works.append((dist.all_reduce(t, group=self.process_group, async_op=True), t))
+
+    def _make_hook(self, i: int):
+        def hook(p: torch.Tensor):
+            if not self.require_backward_grad_sync:
+                return
+            g = self.groups[_DTYPE_IDS.get(p.dtype, 9)]
+            gi = g.index[id(p)]
+            view = g.grad_view(gi)
+            if p.grad is not None and p.grad.data_ptr() != view.data_ptr():
+                view.copy_(p.grad)
+                p.grad = view
+            if not self._callback_queued:
+                self._callback_queued = True
+                torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+            for b in self.reducer.mark_ready(i):
+                self._launch(b)
+        return hook
+
+    def _finalize(self):
+        self._callback_queued = False
+        if not self.reducer.all_launched():
+            unready = self.reducer.unready_params()
+            if not self.find_unused_parameters:
+                self.reducer.prepare()
+                self._works.clear()
+                raise RuntimeError(
+                    f"DDP: {len(unready)} parameter(s) received no gradient this iteration "
+                    f"(e.g. index {unready[:8]}); pass find_unused_parameters=True")
+            for pi in unready:
+                p = self._params[pi]
+                g = self.groups[_DTYPE_IDS.get(p.dtype, 9)]
+                g.grad_view(g.index[id(p)]).zero_()
+            for b in self.reducer.flush_unready():
+                self._launch(b)
+        for work, t in self._works:
+            work.wait()
+            if t is not None:
+                t.div_(self.world)
+        self._works.clear()
+        for g in self.groups.values():
+            g.attach_grads()
+        self.reducer.prepare()
+
+    # ------------------------------------------------------------------ module API
+    def forward(self, *args, **kwargs):
+        if self.broadcast_buffers and self.world > 1 and self.module.training and self._buffer_flats:
+            with torch.no_grad():
+                for flat in self._buffer_flats.values():
+                    self._bcast(flat)
+        return self.module(*args, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        """Accumulate gradients locally (no all-reduce) inside the context."""
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+
+    def zero_grad(self, set_to_none: bool = True):
+        for g in self.groups.values():
+            g.zero_grad()
+
+    def bucket_info(self):
+        """[(dtype_id, numel, bytes)] per bucket, in launch order."""
+        out = []
+        for b in range(self.reducer.num_buckets):
+            dt, _, n = self.bucket_slices[b]
+            out.append((dt, n, n * self.groups[dt].grad_buffer.element_size()))
+        return out
+
+
+DDP = DistributedDataParallel

@@ -1,0 +1,87 @@
+"""Worker functions for multi-process CPU tests (importable by spawned children)."""
+import os
+
+import torch
+import torch.nn.functional as F
+
+
+def collectives(rank, world, outdir):
+    import pytorchdistributed_amd.distributed as pd
+
+    pd.init_process_group("ring")
+    t = torch.full((5,), float(rank + 1))
+    pd.all_reduce(t)
+    r = torch.arange(11, dtype=torch.float32) * (rank + 1)
+    pd.ring_all_reduce(r)
+    b = torch.full((3,), float(rank))
+    pd.host_ring().broadcast(b.data_ptr(), b.numel() * 4, 1)
+    g = torch.zeros(world * 2)
+    mine = torch.tensor([rank, rank * 10.0])
+    pd.host_ring().allgather(mine.data_ptr(), g.data_ptr(), 8)
+    pd.barrier()
+    torch.save({"t": t, "r": r, "b": b, "g": g}, os.path.join(outdir, f"{rank}.pt"))
+    pd.destroy_process_group()
+
+
+def ddp_mlp(rank, world, backend, outdir, steps):
+    """DDP on an MLP: after `steps` SGD steps the params must equal single-process full-batch training."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.models.mlp import MnistMLP
+    from pytorchdistributed_amd.optim import SGD
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+
+    pd.init_process_group(backend)
+    torch.manual_seed(123 + rank)  # different init per rank: DDP must broadcast rank 0's state
+    model = MnistMLP((16, 32, 24, 10))
+    ddp = DistributedDataParallel(model, bucket_cap_mb=0.001, first_bucket_mb=0.0005)
+    opt = SGD(ddp.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(7)
+    X = torch.randn(steps, world * 4, 16, generator=g)
+    Y = torch.randint(0, 10, (steps, world * 4), generator=g)
+    for s in range(steps):
+        xs = X[s, rank * 4:(rank + 1) * 4]
+        ys = Y[s, rank * 4:(rank + 1) * 4]
+        opt.zero_grad()
+        loss = F.cross_entropy(ddp(xs), ys)
+        loss.backward()
+        opt.step()
+    torch.save({k: v.clone() for k, v in model.state_dict().items()}, os.path.join(outdir, f"{rank}.pt"))
+    torch.save({"nb": ddp.reducer.num_buckets}, os.path.join(outdir, f"meta{rank}.pt"))
+    pd.destroy_process_group()
+
+
+def reference_ddp_demo(rank, world, max_epochs, batch_size, outdir):
+    """The reference's ddp_gpus.py main() (Linear(20,1), SGD, F.cross_entropy on float targets) on gloo."""
+    import contextlib
+    import io
+
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.data import DistributedSampler, MyTrainDataset
+    from pytorchdistributed_amd.models.mlp import linear_20_1
+    from pytorchdistributed_amd.train import Trainer
+    from torch.utils.data import DataLoader
+
+    pd.init_process_group("gloo")
+    ds = MyTrainDataset(2048)
+    dl = DataLoader(ds, batch_size=batch_size, pin_memory=False, shuffle=False, sampler=DistributedSampler(ds))
+    model = linear_20_1()
+    opt = torch.optim.SGD(model.parameters(), lr=1e-3)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        tr = Trainer(model, dl, opt, gpu_id=rank, loss_fn=F.cross_entropy)
+        tr.train(max_epochs)
+    with open(os.path.join(outdir, f"{rank}.log"), "w") as f:
+        f.write(buf.getvalue())
+    torch.save({"loss": tr.last_loss, "w": model.weight.detach().clone()}, os.path.join(outdir, f"{rank}.pt"))
+    pd.destroy_process_group()
+
+
+def failing_worker(rank, world):
+    import pytorchdistributed_amd.distributed as pd
+
+    pd.init_process_group("gloo")
+    if rank == 1:
+        raise ValueError("boom from rank 1")
+    import time
+
+    time.sleep(60)

@@ -1,0 +1,150 @@
+"""Multi-process CPU tests: launcher, native store, host ring, DDP, reference parity."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+import _workers
+from pytorchdistributed_amd.launch import ProcessRaisedException, spawn
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_collectives_ring_and_gloo(tmp_path, world):
+    spawn(_workers.collectives, args=(world, str(tmp_path)), nprocs=world, timeout=120)
+    tot = world * (world + 1) / 2
+    for r in range(world):
+        d = torch.load(tmp_path / f"{r}.pt", weights_only=True)
+        assert torch.allclose(d["t"], torch.full((5,), tot))
+        assert torch.allclose(d["r"], torch.arange(11, dtype=torch.float32) * tot)
+        assert torch.allclose(d["b"], torch.full((3,), 1.0))
+        assert torch.allclose(d["g"], torch.tensor([[q, q * 10.0] for q in range(world)]).flatten())
+
+
+@pytest.mark.parametrize("backend", ["gloo", "ring"])
+def test_ddp_matches_single_process(tmp_path, backend):
+    world, steps = 2, 3
+    spawn(_workers.ddp_mlp, args=(world, backend, str(tmp_path), steps), nprocs=world, timeout=120)
+    s0 = torch.load(tmp_path / "0.pt", weights_only=True)
+    s1 = torch.load(tmp_path / "1.pt", weights_only=True)
+    meta = torch.load(tmp_path / "meta0.pt", weights_only=True)
+    assert meta["nb"] > 1  # small caps -> several buckets exercised
+    # single-process full-batch reference from rank 0's initial weights
+    import torch.nn.functional as F
+    from pytorchdistributed_amd.models.mlp import MnistMLP
+
+    torch.manual_seed(123)
+    ref = MnistMLP((16, 32, 24, 10))
+    opt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(7)
+    X = torch.randn(steps, world * 4, 16, generator=g)
+    Y = torch.randint(0, 10, (steps, world * 4), generator=g)
+    for s in range(steps):
+        opt.zero_grad()
+        F.cross_entropy(ref(X[s]), Y[s]).backward()
+        opt.step()
+    for k, v in ref.state_dict().items():
+        assert torch.allclose(s0[k], v, atol=1e-5), k
+        assert torch.equal(s0[k], s1[k]), k
+
+
+def test_reference_ddp_demo_parity(tmp_path):
+    """Reference W2 (`ddp_gpus.py`): 2048 samples, bs 32, W=2 -> `Steps: 32`; C=1 soft-target CE -> loss 0."""
+    spawn(_workers.reference_ddp_demo, args=(2, 2, 32, str(tmp_path)), nprocs=2, timeout=120)
+    for r in range(2):
+        log = (tmp_path / f"{r}.log").read_text().strip().splitlines()
+        assert log == [f"[GPU: {r}] Epoch: {e} | Batchsize: 32 | Steps: 32" for e in range(2)]
+        d = torch.load(tmp_path / f"{r}.pt", weights_only=True)
+        assert d["loss"].abs().item() == 0.0
+
+
+def test_spawn_propagates_child_exception():
+    with pytest.raises(ProcessRaisedException) as ei:
+        spawn(_workers.failing_worker, args=(2,), nprocs=2, timeout=60)
+    assert "boom from rank 1" in str(ei.value)
+
+
+def _run(args, env=None, timeout=120):
+    e = dict(os.environ)
+    e["PYTHONPATH"] = ROOT + os.pathsep + e.get("PYTHONPATH", "")
+    if env:
+        e.update(env)
+    return subprocess.run([sys.executable, "-m", "pytorchdistributed_amd.run"] + args, cwd=ROOT, env=e,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_pda_run_env_contract(tmp_path):
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import os, json\n"
+        "keys=['RANK','LOCAL_RANK','WORLD_SIZE','LOCAL_WORLD_SIZE','MASTER_ADDR','MASTER_PORT','GROUP_RANK']\n"
+        f"open(os.path.join({str(tmp_path)!r}, 'env'+os.environ['RANK']), 'w').write(json.dumps({{k: os.environ[k] for k in keys}}))\n")
+    r = _run(["--standalone", "--nproc-per-node", "3", str(script)])
+    assert r.returncode == 0, r.stderr
+    import json
+
+    envs = [json.loads((tmp_path / f"env{i}").read_text()) for i in range(3)]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2"]
+    assert all(e["WORLD_SIZE"] == "3" and e["LOCAL_WORLD_SIZE"] == "3" for e in envs)
+
+
+def test_pda_run_tears_down_on_failure(tmp_path):
+    script = tmp_path / "w.py"
+    script.write_text("import os, time, sys\nif os.environ['RANK']=='1': sys.exit(3)\ntime.sleep(60)\n")
+    r = _run(["--standalone", "--nproc-per-node", "2", "--grace", "2", str(script)], timeout=40)
+    assert r.returncode == 3
+
+
+def test_pda_run_simulated_two_nodes_ddp(tmp_path):
+    """--nnodes=2 simulated on one host: 2 launchers x 2 workers, DDP all-reduce over gloo."""
+    script = tmp_path / "w.py"
+    script.write_text(
+        "import os, torch\n"
+        "import pytorchdistributed_amd.distributed as pd\n"
+        "pd.init_process_group('gloo')\n"
+        "t = torch.ones(3) * (pd.get_rank() + 1)\n"
+        "pd.all_reduce(t)\n"
+        f"open(os.path.join({str(tmp_path)!r}, 'o'+str(pd.get_rank())), 'w').write(str(t[0].item()))\n"
+        "pd.destroy_process_group()\n")
+    from pytorchdistributed_amd.distributed import free_port
+
+    port = str(free_port())
+    common = ["--nnodes", "2", "--nproc-per-node", "2", "--master-port", port]
+    e = dict(os.environ)
+    e["PYTHONPATH"] = ROOT
+    p1 = subprocess.Popen([sys.executable, "-m", "pytorchdistributed_amd.run"] + common + ["--node-rank", "1", str(script)],
+                          cwd=ROOT, env=e)
+    r0 = _run(common + ["--node-rank", "0", str(script)], timeout=120)
+    assert p1.wait(timeout=120) == 0
+    assert r0.returncode == 0, r0.stderr
+    assert [float((tmp_path / f"o{i}").read_text()) for i in range(4)] == [10.0] * 4
+
+
+def test_pda_run_max_restarts_resumes_from_snapshot(tmp_path):
+    """Crash injected at step 5 on rank 1; the launcher restarts the group and training resumes."""
+    snap = tmp_path / "snap.pt"
+    script = tmp_path / "train.py"
+    script.write_text(
+        "import os, torch, torch.nn.functional as F\n"
+        "from torch.utils.data import DataLoader\n"
+        "import pytorchdistributed_amd.distributed as pd\n"
+        "from pytorchdistributed_amd.data import DistributedSampler, MyTrainDataset\n"
+        "from pytorchdistributed_amd.train import Trainer\n"
+        "from pytorchdistributed_amd.models.mlp import linear_20_1\n"
+        "pd.init_process_group('gloo')\n"
+        "ds = MyTrainDataset(256)\n"
+        "dl = DataLoader(ds, batch_size=32, sampler=DistributedSampler(ds))\n"
+        "m = linear_20_1()\n"
+        "opt = torch.optim.SGD(m.parameters(), lr=1e-3)\n"
+        f"tr = Trainer(m, dl, opt, gpu_id=pd.get_rank(), save_every=1, snapshot_path={str(snap)!r}, loss_fn=F.mse_loss)\n"
+        "tr.train(3)\n"
+        f"open({str(tmp_path / 'done')!r} + os.environ['RANK'], 'w').write(os.environ['PDA_RESTART_COUNT'] + ' ' + str(tr.epochs_run))\n"
+        "pd.destroy_process_group()\n")
+    r = _run(["--standalone", "--nproc-per-node", "2", "--max-restarts", "1", "--grace", "2", str(script)],
+             env={"PDA_FAULT": "1:5:crash"}, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Resuming training from snapshot at Epoch 1" in r.stdout
+    assert (tmp_path / "done0").read_text() == "1 1"

@@ -1,0 +1,335 @@
+"""Numerics of every HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+Run on the MI355X box: ``python -m pytest tests -m gpu``.  All tests here are single-process.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def C():
+    from pytorchdistributed_amd._native import C as _C
+
+    return _C()
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def bf(x):
+    return x.to(DEV, torch.bfloat16).contiguous()
+
+
+# ----------------------------------------------------------------------------- GEMM
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 200, 136), (1024, 1000, 2048), (77, 64, 520),
+                                   (4096, 256, 64), (16, 8, 8)])
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_layouts(M, N, K, ak, bk):
+    if not ak and M % 8:
+        pytest.skip("M-major A needs M % 8 == 0")
+    torch.manual_seed(0)
+    A = torch.randn(M, K)
+    B = torch.randn(K, N)
+    a_store = bf(A) if ak else bf(A.t().contiguous())
+    b_store = bf(B.t().contiguous()) if bk else bf(B)
+    lda = K if ak else M
+    ldb = K if bk else N
+    out = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    C().gemm(a_store, ak, lda, b_store, bk, ldb, out, N, M, N, K, None, False, True)
+    ref = A.to(torch.bfloat16).float() @ B.to(torch.bfloat16).float()
+    assert rel_err(out.cpu(), ref) < 1e-5
+
+
+def test_gemm_identity_asymmetric():
+    # A = I with an asymmetric B catches a transposed C write (cdna guide §3)
+    n = 64
+    A = torch.eye(n)
+    B = torch.arange(n * n, dtype=torch.float32).reshape(n, n) % 97
+    out = torch.empty(n, n, device=DEV)
+    C().gemm(bf(A), True, n, bf(B.t().contiguous()), True, n, out, n, n, n, n, None, False, False)
+    assert torch.equal(out.cpu(), B.to(torch.bfloat16).float())
+
+
+def test_gemm_bias_relu_bf16_out():
+    M, N, K = 257, 136, 96
+    A, W, b = torch.randn(M, K), torch.randn(N, K), torch.randn(N)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C().gemm(bf(A), True, K, bf(W), True, K, out, N, M, N, K, b.to(DEV), True, False)
+    ref = torch.relu(A.to(torch.bfloat16).float() @ W.to(torch.bfloat16).float().t() + b)
+    assert rel_err(out.cpu(), ref) < 1e-2
+
+
+# ----------------------------------------------------------------------------- conv
+CONV_CASES = [
+    # N, H, W, C, Cout, k, stride, pad
+    (2, 16, 16, 64, 64, 1, 1, 0),
+    (2, 16, 16, 64, 128, 3, 1, 1),
+    (2, 15, 15, 128, 64, 3, 2, 1),
+    (2, 16, 16, 256, 512, 1, 2, 0),
+    (2, 32, 32, 8, 64, 7, 2, 3),
+    (3, 7, 7, 512, 2048, 1, 1, 0),
+    (1, 9, 11, 24, 40, 3, 1, 1),
+]
+
+
+def _conv_ref(x, w, stride, pad):
+    return F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), None, stride, pad).permute(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(case):
+    N, H, W, Cin, Cout, k, s, p = case
+    torch.manual_seed(1)
+    x = torch.randn(N, H, W, Cin).to(torch.bfloat16).float().requires_grad_()
+    w = (torch.randn(Cout, k, k, Cin) / math.sqrt(Cin * k * k)).to(torch.bfloat16).float().requires_grad_()
+    y = _conv_ref(x, w, s, p)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    yg = C().conv_fwd(bf(x.detach()), bf(w.detach()), s, p, 1, None, False)
+    assert yg.shape == y.shape
+    assert rel_err(yg.cpu(), y.detach()) < 1e-2
+    dx = C().conv_dgrad(bf(dy), bf(w.detach()), H, W, s, p, 1)
+    assert rel_err(dx.cpu(), x.grad) < 1e-2
+    dw = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, 1, True)
+    assert rel_err(dw.cpu(), w.grad) < 1e-3
+    dwb = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, 1, False)
+    assert rel_err(dwb.cpu(), w.grad) < 1e-2
+
+
+# ----------------------------------------------------------------------------- batch norm
+@pytest.mark.parametrize("shape", [(4, 8, 8, 64), (2, 7, 7, 2048), (3, 5, 5, 200), (2, 56, 56, 256)])
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+def test_batchnorm_train(shape, relu, res):
+    torch.manual_seed(2)
+    Cc = shape[-1]
+    x = (torch.randn(shape) * 3 + 1.5).to(torch.bfloat16).float()
+    r = torch.randn(shape).to(torch.bfloat16).float() if res else None
+    g = torch.rand(Cc) + 0.5
+    b = torch.randn(Cc)
+    rm, rv = torch.zeros(Cc), torch.ones(Cc)
+    xr = x.clone().requires_grad_()
+    gr, br = g.clone().requires_grad_(), b.clone().requires_grad_()
+    rr = r.clone().requires_grad_() if res else None
+    y = F.batch_norm(xr.reshape(-1, Cc), rm, rv, gr, br, True, 0.1, 1e-5).reshape(shape)
+    if res:
+        y = y + rr
+    if relu:
+        y = torch.relu(y)
+    dy = torch.randn(shape).to(torch.bfloat16).float()
+    y.backward(dy)
+
+    rmg, rvg = torch.zeros(Cc, device=DEV), torch.ones(Cc, device=DEV)
+    yg, mean, invstd = C().bn_fwd_train(bf(x), bf(r) if res else None, g.to(DEV), b.to(DEV), rmg, rvg, 0.1, 1e-5,
+                                        relu)
+    assert rel_err(yg.cpu(), y.detach()) < 1e-2
+    assert rel_err(rmg.cpu(), rm) < 1e-4 and rel_err(rvg.cpu(), rv) < 1e-4
+    dx, dres, dgamma, dbeta = C().bn_bwd(bf(dy), bf(x), yg, mean, invstd, g.to(DEV), relu, res)
+    assert rel_err(dx.cpu(), xr.grad) < 2e-2
+    assert rel_err(dgamma.cpu(), gr.grad) < 1e-2
+    assert rel_err(dbeta.cpu(), br.grad) < 1e-2
+    if res:
+        assert rel_err(dres.cpu(), rr.grad) < 1e-2
+
+
+def test_batchnorm_eval():
+    x = torch.randn(2, 4, 4, 64)
+    g, b = torch.rand(64) + 0.5, torch.randn(64)
+    rm, rv = torch.randn(64), torch.rand(64) + 0.5
+    y = C().bn_fwd_eval(bf(x), None, g.to(DEV), b.to(DEV), rm.to(DEV), rv.to(DEV), 1e-5, True)
+    ref = torch.relu(F.batch_norm(x.to(torch.bfloat16).float().reshape(-1, 64), rm, rv, g, b, False, 0.1, 1e-5))
+    assert rel_err(y.cpu(), ref.reshape(x.shape)) < 1e-2
+
+
+# ----------------------------------------------------------------------------- pooling
+def test_maxpool_fwd_bwd():
+    torch.manual_seed(3)
+    x = torch.randn(2, 17, 16, 64).to(torch.bfloat16).float().requires_grad_()
+    y = F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    yg, idx = C().maxpool_fwd(bf(x.detach()), 3, 2, 1)
+    assert torch.equal(yg.cpu().float(), y.detach())
+    dx = C().maxpool_bwd(bf(dy), idx, 17, 16, 3, 2, 1)
+    assert rel_err(dx.cpu(), x.grad) < 1e-2
+
+
+def test_avgpool_fwd_bwd():
+    x = torch.randn(3, 7, 7, 128)
+    y = C().avgpool_fwd(bf(x), False)
+    assert rel_err(y.cpu(), x.to(torch.bfloat16).float().mean((1, 2))) < 1e-4
+    dy = torch.randn(3, 128)
+    dx = C().avgpool_bwd(dy.to(DEV), 7, 7)
+    assert rel_err(dx.cpu(), (dy / 49)[:, None, None, :].expand(3, 7, 7, 128)) < 1e-2
+
+
+# ----------------------------------------------------------------------------- cross entropy
+@pytest.mark.parametrize("M,Cc,dtype", [(64, 1000, torch.float32), (33, 1000, torch.bfloat16), (8, 50257, torch.bfloat16),
+                                        (32, 1, torch.float32)])
+@pytest.mark.parametrize("kind", ["index", "prob", "smooth"])
+def test_cross_entropy(M, Cc, dtype, kind):
+    from pytorchdistributed_amd.ops import cross_entropy
+
+    torch.manual_seed(4)
+    logits = (torch.randn(M, Cc) * 3).to(dtype).float()
+    if kind == "prob":
+        tgt = torch.rand(M, Cc) if Cc > 1 else torch.rand(M, 1)
+        ls = 0.0
+    else:
+        tgt = torch.randint(0, Cc, (M,))
+        if M > 3:
+            tgt[3] = -100
+        ls = 0.1 if kind == "smooth" else 0.0
+    lr = logits.clone().requires_grad_()
+    ref = F.cross_entropy(lr, tgt, label_smoothing=ls)
+    ref.backward()
+    lg = logits.to(DEV, dtype).requires_grad_()
+    out = cross_entropy(lg, tgt.to(DEV), label_smoothing=ls)
+    out.backward()
+    assert abs(out.item() - ref.item()) < 1e-3 * max(1.0, abs(ref.item()))
+    assert rel_err(lg.grad.cpu(), lr.grad) < (1e-4 if dtype == torch.float32 else 2e-2) or lr.grad.norm() < 1e-12
+
+
+# ----------------------------------------------------------------------------- optimizers
+def test_sgd_flat_matches_torch():
+    torch.manual_seed(5)
+    p0 = torch.randn(1003)
+    grads = [torch.randn(1003) for _ in range(3)]
+    ref = p0.clone().requires_grad_()
+    opt = torch.optim.SGD([ref], lr=0.1, momentum=0.9, weight_decay=1e-3, nesterov=True)
+    master = p0.clone().to(DEV)
+    mom = torch.zeros(1003, device=DEV)
+    pb = torch.empty(1003, device=DEV, dtype=torch.bfloat16)
+    for i, g in enumerate(grads):
+        ref.grad = g.clone()
+        opt.step()
+        C().sgd_step(master, pb, g.to(DEV), mom, 0.1, 0.9, 0.0, 1e-3, True, i == 0, 1.0, None, None)
+    assert rel_err(master.cpu(), ref.detach()) < 1e-6
+    assert rel_err(pb.cpu(), ref.detach()) < 1e-2
+
+
+@pytest.mark.parametrize("adamw", [False, True])
+def test_adam_matches_torch(adamw):
+    torch.manual_seed(6)
+    p0 = torch.randn(517)
+    ref = p0.clone().requires_grad_()
+    cls = torch.optim.AdamW if adamw else torch.optim.Adam
+    opt = cls([ref], lr=1e-2, betas=(0.9, 0.99), eps=1e-8, weight_decay=0.01)
+    master = p0.clone().to(DEV)
+    m, v = torch.zeros(517, device=DEV), torch.zeros(517, device=DEV)
+    for t in range(1, 4):
+        g = torch.randn(517).to(torch.bfloat16).float()
+        ref.grad = g.clone()
+        opt.step()
+        C().adam_step(master, None, g.to(DEV, torch.bfloat16), m, v, 1e-2, 0.9, 0.99, 1e-8, 0.01, adamw, t,
+                      1.0, None, None)
+    assert rel_err(master.cpu(), ref.detach()) < 1e-5
+
+
+def test_grad_norm():
+    g = torch.randn(10001)
+    out = C().grad_norm(g.to(DEV, torch.bfloat16), 0.5, 1.0).cpu()
+    n = g.to(torch.bfloat16).float().norm() * 0.5
+    assert abs(out[0].item() - n.item()) / n.item() < 1e-4
+    assert abs(out[1].item() - min(1.0, 1.0 / (n.item() + 1e-6))) < 1e-5
+
+
+# ----------------------------------------------------------------------------- norms / activations / simt
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("D", [64, 1024, 1600, 4096])
+def test_rownorm(rms, D):
+    from pytorchdistributed_amd.ops import layer_norm, rms_norm
+
+    torch.manual_seed(7)
+    x = (torch.randn(37, D) * 2 + 0.3).to(torch.bfloat16).float()
+    g = torch.rand(D) + 0.5
+    b = torch.randn(D)
+    xr = x.clone().requires_grad_()
+    gr, br = g.clone().requires_grad_(), b.clone().requires_grad_()
+    if rms:
+        y = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * gr
+    else:
+        y = F.layer_norm(xr, (D,), gr, br, 1e-5)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xg = x.to(DEV, torch.bfloat16).requires_grad_()
+    gg = g.to(DEV).requires_grad_()
+    bg = b.to(DEV).requires_grad_()
+    yg = rms_norm(xg, gg, 1e-6) if rms else layer_norm(xg, gg, bg, 1e-5)
+    yg.backward(dy.to(DEV, torch.bfloat16))
+    assert rel_err(yg.cpu(), y.detach()) < 1e-2
+    assert rel_err(xg.grad.cpu(), xr.grad) < 2e-2
+    assert rel_err(gg.grad.cpu(), gr.grad) < 2e-2
+    if not rms:
+        assert rel_err(bg.grad.cpu(), br.grad) < 2e-2
+
+
+def test_activations():
+    from pytorchdistributed_amd.ops import gelu_tanh, relu, swiglu
+
+    x = torch.randn(33, 64)
+    for fn, ref in [(relu, torch.relu), (gelu_tanh, lambda t: F.gelu(t, approximate="tanh"))]:
+        xr = x.clone().requires_grad_()
+        y = ref(xr)
+        y.backward(torch.ones_like(y))
+        xg = x.to(DEV).requires_grad_()
+        yg = fn(xg)
+        yg.backward(torch.ones_like(yg))
+        assert rel_err(yg.cpu(), y.detach()) < 1e-5
+        assert rel_err(xg.grad.cpu(), xr.grad) < 1e-5
+    gu = torch.randn(5, 128)
+    gr = gu.clone().requires_grad_()
+    g_, u_ = gr.chunk(2, -1)
+    y = F.silu(g_) * u_
+    y.backward(torch.ones_like(y))
+    gg = gu.to(DEV).requires_grad_()
+    yg = swiglu(gg)
+    yg.backward(torch.ones_like(yg))
+    assert rel_err(yg.cpu(), y.detach()) < 1e-5
+    assert rel_err(gg.grad.cpu(), gr.grad) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 1, 20), (16, 20, 10), (100, 37, 333)])
+def test_simt_gemm_fp32(M, N, K):
+    A, B = torch.randn(M, K), torch.randn(K, N)
+    out = torch.empty(M, N, device=DEV)
+    C().simt_gemm(A.to(DEV), K, 1, B.to(DEV), N, 1, out, N, 1, M, N, K, None, False, 0.0)
+    assert rel_err(out.cpu(), A @ B) < 1e-5
+
+
+def test_linear_op_all_paths():
+    from pytorchdistributed_amd.ops import linear
+
+    for dtype, fin, fout in [(torch.bfloat16, 64, 136), (torch.float32, 20, 1), (torch.bfloat16, 10, 20)]:
+        torch.manual_seed(8)
+        x = torch.randn(50, fin).to(dtype).float()
+        w = (torch.randn(fout, fin) * 0.1).to(dtype).float()
+        b = torch.randn(fout).to(dtype).float()
+        xr, wr, br = (t.clone().requires_grad_() for t in (x, w, b))
+        y = torch.relu(F.linear(xr, wr, br))
+        y.backward(torch.ones_like(y))
+        xg, wg, bg = (t.to(DEV, dtype).requires_grad_() for t in (x, w, b))
+        yg = linear(xg, wg, bg, relu=True)
+        yg.backward(torch.ones_like(yg))
+        tol = 1e-5 if dtype == torch.float32 else 2e-2
+        for a, r in [(yg, y), (xg.grad, xr.grad), (wg.grad, wr.grad), (bg.grad, br.grad)]:
+            assert rel_err(a.cpu(), r.detach()) < tol
+
+
+def test_synth_fill_statistics():
+    t = torch.empty(1 << 20, device=DEV)
+    C().fill_random(t, 7, 0, 1, 0.0, 1.0)
+    assert abs(t.mean().item()) < 0.01 and abs(t.std().item() - 1) < 0.01
+    t2 = torch.empty(1 << 20, device=DEV)
+    C().fill_random(t2, 7, 0, 1, 0.0, 1.0)
+    assert torch.equal(t, t2)
+    i = torch.empty(100000, device=DEV, dtype=torch.long)
+    C().fill_randint(i, 1, 0, 0, 1000)
+    assert i.min().item() >= 0 and i.max().item() < 1000
