@@ -169,7 +169,7 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optio
                                  c10::optional<Tensor> running_var, double momentum, double eps, bool relu) {
   check_bf16(x, "x");
   const int64_t C = x.size(-1), M = x.numel() / C;
-  TORCH_CHECK(C % 8 == 0, "channels must be a multiple of 8");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "channels must be a multiple of 8 and <= 2048");
   if (res) {
     check_bf16(*res, "residual");
     TORCH_CHECK(res->sizes() == x.sizes());
@@ -199,7 +199,7 @@ Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> ga
                    Tensor running_mean, Tensor running_var, double eps, bool relu) {
   check_bf16(x, "x");
   const int64_t C = x.size(-1), M = x.numel() / C;
-  TORCH_CHECK(C % 8 == 0, "channels must be a multiple of 8");
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "channels must be a multiple of 8 and <= 2048");
   if (res) check_bf16(*res, "residual");
   const float *gf, *bfp;
   const pda::bf16_t *gb, *bb;
@@ -217,11 +217,13 @@ Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> ga
 }
 
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor mean, Tensor invstd,
-                           c10::optional<Tensor> gamma, bool relu, bool want_dres) {
+                           c10::optional<Tensor> gamma, bool relu, bool want_dres, c10::optional<Tensor> dgamma_out,
+                           c10::optional<Tensor> dbeta_out) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   TORCH_CHECK(dy.sizes() == x.sizes());
   const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "channels must be a multiple of 8 and <= 2048");
   if (relu) {
     TORCH_CHECK(y.has_value(), "relu backward needs the saved output");
     check_bf16(*y, "y");
@@ -234,12 +236,20 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor 
   c10::DeviceGuard g(x.device());
   Tensor dx = at::empty_like(x);
   Tensor dres = want_dres ? at::empty_like(x) : Tensor();
-  auto fo = x.options().dtype(at::kFloat);
-  Tensor dgamma = at::empty({C}, fo), dbeta = at::empty({C}, fo);
-  Tensor ws = at::empty({pda::bn_workspace_floats(M, C)}, fo);
+  // parameter gradients are produced directly in the parameter dtype (no cast kernels)
+  const auto pdt = gamma.has_value() ? gamma->scalar_type() : at::kFloat;
+  Tensor dgamma = dgamma_out.has_value() ? *dgamma_out : at::empty({C}, x.options().dtype(pdt));
+  Tensor dbeta = dbeta_out.has_value() ? *dbeta_out : at::empty({C}, x.options().dtype(pdt));
+  TORCH_CHECK(dgamma.numel() == C && dbeta.numel() == C && dgamma.scalar_type() == pdt && dbeta.scalar_type() == pdt);
+  check_gpu(dgamma, "dgamma");
+  check_gpu(dbeta, "dbeta");
+  const bool pb = pdt == at::kBFloat16;
+  Tensor ws = at::empty({pda::bn_workspace_floats(M, C)}, x.options().dtype(at::kFloat));
   CHECK_HIP_OK(pda::bn_bwd(bp(dy), bp(x), relu ? bp(*y) : nullptr, M, C, mean.data_ptr<float>(),
                            invstd.data_ptr<float>(), gf, gb, relu, bpm(dx), want_dres ? bpm(dres) : nullptr,
-                           dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), ws.data_ptr<float>(), stream_of(x)));
+                           pb ? nullptr : dgamma.data_ptr<float>(), pb ? bpm(dgamma) : nullptr,
+                           pb ? nullptr : dbeta.data_ptr<float>(), pb ? bpm(dbeta) : nullptr, ws.data_ptr<float>(),
+                           stream_of(x)));
   return {dx, dres, dgamma, dbeta};
 }
 
@@ -310,7 +320,8 @@ void gemm(Tensor A, bool a_kmajor, int64_t lda, Tensor B, bool b_kmajor, int64_t
   check_bf16(A, "A");
   check_bf16(B, "B");
   check_f32_or_bf16(C, "C");
-  TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "gemm needs K and N multiples of 8 (got K=", K, ", N=", N, ")");
+  TORCH_CHECK(N % 8 == 0, "gemm needs N multiple of 8 (got N=", N, ")");
+  TORCH_CHECK((!a_kmajor && !b_kmajor) || K % 8 == 0, "gemm with a K-major operand needs K % 8 == 0 (got K=", K, ")");
   TORCH_CHECK(a_kmajor || M % 8 == 0, "M-major A needs M % 8 == 0");
   TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0, "leading dims must be 16-byte multiples");
   // bounds: the largest element each operand touches
@@ -370,14 +381,23 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   return dx;
 }
 
-Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t dil, bool out_f32) {
+Tensor conv_wgrad(Tensor dy, Tensor x, int64_t R, int64_t S, int64_t stride, int64_t pad, int64_t dil, bool out_f32,
+                  c10::optional<Tensor> out) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int P = dy.size(1), Q = dy.size(2), Cout = dy.size(3);
   TORCH_CHECK(dy.size(0) == N && C % 8 == 0 && Cout % 8 == 0);
   c10::DeviceGuard g(dy.device());
-  Tensor dw = at::empty({Cout, R, S, C}, dy.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  Tensor dw;
+  if (out.has_value()) {  // write straight into e.g. a DDP gradient-bucket view
+    dw = *out;
+    check_gpu(dw, "out");
+    TORCH_CHECK(dw.numel() == (int64_t)Cout * R * S * C && dw.scalar_type() == (out_f32 ? at::kFloat : at::kBFloat16));
+    check_aligned16(dw, "out");
+  } else {
+    dw = at::empty({Cout, R, S, C}, dy.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  }
   const int64_t slab_n = pda::conv_slab_floats(2, N, H, W, C, Cout, R, S, P, Q);
   Tensor slab = slab_n > 0 ? at::empty({slab_n}, dy.options().dtype(at::kFloat)) : Tensor();
   CHECK_HIP_OK(pda::conv2d_wgrad(bp(dy), bp(x), dw.data_ptr(), out_f32, N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,

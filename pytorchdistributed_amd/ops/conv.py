@@ -11,6 +11,7 @@ import torch
 import torch.nn.functional as F
 
 from .._native import C
+from ..parallel.flat import grad_target
 
 
 def _ref_conv(x, w, stride, padding, dilation, bias=None):
@@ -26,6 +27,7 @@ class _Conv2dFn(torch.autograd.Function):
         y = C().conv_fwd(x, w, stride, padding, dilation, bias, relu)
         ctx.save_for_backward(x, w, y if relu else None)
         ctx.cfg = (stride, padding, dilation, relu, bias is not None)
+        ctx.wparam = w
         return y
 
     @staticmethod
@@ -39,7 +41,8 @@ class _Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation)
         if ctx.needs_input_grad[1]:
-            dw = C().conv_wgrad(dy, x, w.shape[1], w.shape[2], stride, padding, dilation, w.dtype == torch.float32)
+            dw = C().conv_wgrad(dy, x, w.shape[1], w.shape[2], stride, padding, dilation, w.dtype == torch.float32,
+                                grad_target(ctx.wparam))
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.reshape(-1, dy.shape[-1]).sum(0, dtype=torch.float32).to(dy.dtype)
         return dx, dw, db, None, None, None, None

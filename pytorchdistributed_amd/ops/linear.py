@@ -11,6 +11,7 @@ import torch
 import torch.nn.functional as F
 
 from .._native import C
+from ..parallel.flat import grad_target
 
 
 def _mfma_ok(x2, w):
@@ -47,10 +48,10 @@ def _gemm_dgrad(dy, w):
     return dx
 
 
-def _gemm_wgrad(dy, x2, out_dtype):
+def _gemm_wgrad(dy, x2, out_dtype, target=None):
     M, N = dy.shape
     K = x2.shape[1]
-    dw = torch.empty(N, K, device=dy.device, dtype=out_dtype)
+    dw = target if target is not None else torch.empty(N, K, device=dy.device, dtype=out_dtype)
     if M == 0:
         return dw.zero_()
     if dy.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and N % 8 == 0 and K % 8 == 0:
@@ -72,6 +73,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_bias = b is not None
         ctx.shape = shape
+        ctx.wparam, ctx.bparam = w, b
         return y.reshape(*shape[:-1], w.shape[0])
 
     @staticmethod
@@ -84,9 +86,11 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _gemm_dgrad(dy2, w).reshape(ctx.shape)
         if ctx.needs_input_grad[1]:
-            dw = _gemm_wgrad(dy2, x2, w.dtype)
+            dw = _gemm_wgrad(dy2, x2, w.dtype, grad_target(ctx.wparam))
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = C().colsum(dy2).to(dy2.dtype)
+            tb = grad_target(ctx.bparam)
+            db = C().colsum(dy2)
+            db = tb.copy_(db) if tb is not None else db.to(ctx.bparam.dtype)
         return dx, dw, db, None
 
 

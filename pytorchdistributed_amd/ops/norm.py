@@ -10,6 +10,7 @@ import torch
 import torch.nn.functional as F
 
 from .._native import C
+from ..parallel.flat import grad_target
 
 
 class _BatchNormFn(torch.autograd.Function):
@@ -27,6 +28,7 @@ class _BatchNormFn(torch.autograd.Function):
             invstd = torch.rsqrt(running_var + eps)
         ctx.save_for_backward(x, y if relu else None, mean, invstd, gamma)
         ctx.cfg = (relu, residual is not None, training)
+        ctx.beta = beta
         return y
 
     @staticmethod
@@ -35,9 +37,13 @@ class _BatchNormFn(torch.autograd.Function):
         relu, has_res, training = ctx.cfg
         if not training:
             raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
-        dx, dres, dgamma, dbeta = C().bn_bwd(dy.contiguous(), x, y, mean, invstd, gamma, relu, has_res)
-        dg = dgamma.to(gamma.dtype) if gamma is not None and ctx.needs_input_grad[1] else None
-        db = dbeta.to(gamma.dtype if gamma is not None else dbeta.dtype) if ctx.needs_input_grad[2] else None
+        tg = grad_target(gamma) if gamma is not None and ctx.needs_input_grad[1] else None
+        tb = grad_target(ctx.beta) if ctx.beta is not None and ctx.needs_input_grad[2] else None
+        if (tg is None) != (tb is None):
+            tg = tb = None
+        dx, dres, dgamma, dbeta = C().bn_bwd(dy.contiguous(), x, y, mean, invstd, gamma, relu, has_res, tg, tb)
+        dg = dgamma if gamma is not None and ctx.needs_input_grad[1] else None
+        db = dbeta if ctx.needs_input_grad[2] else None
         return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None
 
 

@@ -64,6 +64,21 @@ class FlatGroup:
         return len(params) == len(self.params) and all(id(p) in self.index for p in params)
 
 
+def grad_target(param: torch.Tensor) -> Optional[torch.Tensor]:
+    """Where a backward kernel should write ``param``'s gradient.
+
+    For a parameter living in a :class:`FlatGroup` whose ``.grad`` is unset, this is its slot of the
+    flat gradient buffer: the kernel writes there and autograd's AccumulateGrad adopts the returned
+    view as ``.grad`` without a copy (so DDP's bucket is filled in place).  Otherwise ``None``
+    (allocate normally; accumulation semantics are then autograd's).
+    """
+    info = getattr(param, "_pda_flat", None)
+    if info is None or param.grad is not None or not param.requires_grad:
+        return None
+    fg, off = info
+    return fg.grad_buffer[off: off + param.numel()].view_as(param)
+
+
 def flat_group_of(p: torch.Tensor) -> Optional[FlatGroup]:
     info = getattr(p, "_pda_flat", None)
     return info[0] if info is not None else None

@@ -1,0 +1,199 @@
+"""Single-process CPU unit tests: sampler parity, bucket reducer, native store,
+optimizers' reference math, model shapes / parameter counts, log format, checkpoint layout."""
+import threading
+
+import pytest
+import torch
+import torch.nn.functional as F
+from hypothesis import given, settings, strategies as st
+
+from pytorchdistributed_amd import _native
+from pytorchdistributed_amd.data import DistributedSampler, MyTrainDataset, SimpleDataset, random_image_batch
+
+
+class _Len:
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+
+@settings(max_examples=150, deadline=None)
+@given(n=st.integers(1, 300), w=st.integers(1, 9), epoch=st.integers(0, 5), shuffle=st.booleans(),
+       drop_last=st.booleans(), seed=st.integers(0, 1000))
+def test_sampler_matches_torch(n, w, epoch, shuffle, drop_last, seed):
+    if drop_last and n < w:
+        return
+    ds = _Len(n)
+    for r in range(w):
+        ours = DistributedSampler(ds, num_replicas=w, rank=r, shuffle=shuffle, seed=seed, drop_last=drop_last)
+        ref = torch.utils.data.DistributedSampler(ds, num_replicas=w, rank=r, shuffle=shuffle, seed=seed,
+                                                  drop_last=drop_last)
+        ours.set_epoch(epoch)
+        ref.set_epoch(epoch)
+        assert list(ours) == list(ref)
+        assert len(ours) == len(ref)
+
+
+def test_sampler_reference_numbers():
+    # 2048/2 -> 1024 per rank, disjoint; 10/3 padding wraps -> rank 2 gets 4 items
+    s0 = DistributedSampler(_Len(2048), 2, 0)
+    s1 = DistributedSampler(_Len(2048), 2, 1)
+    assert len(s0) == len(s1) == 1024
+    assert not (set(s0) & set(s1))
+    assert len(list(DistributedSampler(_Len(10), 3, 2, shuffle=False))) == 4
+    assert list(DistributedSampler(_Len(10), 3, 2, shuffle=False)) == [2, 5, 8, 1]
+
+
+def test_reducer_buckets_and_order():
+    C = _native.C()
+    numels = [1000, 50, 3000, 7, 2000, 64]
+    r = C.BucketReducer(numels, [2] * 6, [1] * 6, 4000, 1000, 8, [])
+    seen = []
+    for b in range(r.num_buckets):
+        ps = r.bucket_params(b)
+        seen += ps
+        offs = r.bucket_offsets(b)
+        assert all(o % 8 == 0 for o in offs)
+        assert r.bucket_numel(b) >= sum(numels[p] for p in ps)
+    assert sorted(seen) == list(range(6))
+    assert seen == [5, 4, 3, 2, 1, 0]  # reverse registration order
+    # buckets only launch in index order even if a later bucket is ready first
+    r.prepare()
+    last_bucket_params = r.bucket_params(r.num_buckets - 1)
+    launched = []
+    for p in last_bucket_params:
+        launched += r.mark_ready(p)
+    assert launched == [] or launched == [0]
+    for p in range(6):
+        if p not in last_bucket_params:
+            launched += r.mark_ready(p)
+    assert launched == list(range(r.num_buckets))
+    assert r.all_launched()
+    with pytest.raises(RuntimeError):
+        r.mark_ready(0)
+
+
+def test_reducer_dtype_split_and_flush():
+    C = _native.C()
+    r = C.BucketReducer([10, 10, 10], [4, 2, 4], [0, 1, 0], 1 << 20, 1 << 20, 8, [])
+    assert {r.bucket_dtype(b) for b in range(r.num_buckets)} == {0, 1}
+    r.prepare()
+    r.mark_ready(0)
+    assert sorted(r.unready_params()) == [1, 2]
+    assert r.flush_unready() != []
+    assert r.all_launched()
+
+
+def test_native_store_blocking_get_and_ops():
+    C = _native.C()
+    srv = C.StoreServer("127.0.0.1", 0)
+    a = C.StoreClient("127.0.0.1", srv.port, 10.0)
+    b = C.StoreClient("127.0.0.1", srv.port, 10.0)
+    out = {}
+    t = threading.Thread(target=lambda: out.setdefault("v", b.get("late")))
+    t.start()
+    a.set("late", b"value")
+    t.join(5)
+    assert out["v"] == b"value"
+    assert a.add("ctr", 2) == 2 and b.add("ctr", 3) == 5
+    assert a.compare_set("cas", b"", b"x") == b"x"
+    assert a.compare_set("cas", b"nope", b"y") == b"x"
+    assert a.check(["late", "ctr"]) and not a.check(["missing"])
+    assert a.delete_key("late") and not a.check(["late"])
+    with pytest.raises(Exception):
+        c = C.StoreClient("127.0.0.1", srv.port, 0.3)
+        c.get("never")
+    srv.stop()
+
+
+def test_fused_optim_cpu_reference_math():
+    from pytorchdistributed_amd.optim import SGD, Adam, AdamW
+
+    for ours_cls, ref_cls, kw in [(SGD, torch.optim.SGD, dict(lr=0.1, momentum=0.9, weight_decay=1e-3, nesterov=True)),
+                                  (Adam, torch.optim.Adam, dict(lr=1e-2, weight_decay=1e-2)),
+                                  (AdamW, torch.optim.AdamW, dict(lr=1e-2, weight_decay=1e-2))]:
+        torch.manual_seed(0)
+        p1 = torch.nn.Parameter(torch.randn(37))
+        p2 = torch.nn.Parameter(p1.detach().clone())
+        o1, o2 = ours_cls([p1], **kw), ref_cls([p2], **kw)
+        for _ in range(4):
+            g = torch.randn(37)
+            p1.grad, p2.grad = g.clone(), g.clone()
+            o1.step()
+            o2.step()
+        assert torch.allclose(p1, p2, atol=1e-6), ours_cls
+
+
+def test_models_param_counts_and_shapes():
+    from pytorchdistributed_amd.models import TutorialMLP, resnet50, linear_20_1
+    from pytorchdistributed_amd.models.resnet import from_torchvision_state_dict, to_torchvision_state_dict
+
+    m = resnet50()
+    assert sum(p.numel() for p in m.parameters()) == 25_557_032  # `03_model_parallel.ipynb` raw line 301
+    assert sum(p.numel() for p in TutorialMLP().parameters()) == 1165
+    assert sum(p.numel() for p in linear_20_1().parameters()) == 21
+    y = m(torch.randn(2, 3, 64, 64))  # NCHW input accepted
+    assert y.shape == (2, 1000)
+    sd = to_torchvision_state_dict(m)
+    assert sd["conv1.weight"].shape == (64, 3, 7, 7) and sd["layer1.0.conv2.weight"].shape == (64, 64, 3, 3)
+    m2 = resnet50()
+    from_torchvision_state_dict(m2, sd)
+    assert torch.equal(m2.layer3[2].conv2.weight, m.layer3[2].conv2.weight)
+
+
+def test_reference_datasets():
+    ds = MyTrainDataset(2048)
+    x, y = ds[0]
+    assert x.shape == (20,) and y.shape == (1,)
+    assert torch.equal(MyTrainDataset(16)[3][0], MyTrainDataset(16)[3][0])  # seeded: same on every rank
+    s = SimpleDataset(1000)
+    assert s[0][0].shape == (10,) and s.labels.unique().tolist() == [0]
+    xb, yb = random_image_batch(120, (128, 128), 1000)
+    assert xb.shape == (120, 3, 128, 128) and torch.equal(yb.sum(1), torch.ones(120))
+
+
+def test_reference_quirk_ce_c1_is_zero():
+    # soft-target CE with one logit -> loss 0, grad 0
+    from pytorchdistributed_amd.ops import cross_entropy
+
+    out = torch.randn(32, 1, requires_grad=True)
+    loss = cross_entropy(out, torch.rand(32, 1))
+    loss.backward()
+    assert loss.abs().item() == 0.0 and out.grad.abs().sum().item() == 0.0
+
+
+def test_epoch_log_line():
+    from pytorchdistributed_amd.utils.log import epoch_line
+
+    assert epoch_line(1, 4, 32, 32) == "[GPU: 1] Epoch: 4 | Batchsize: 32 | Steps: 32"
+
+
+def test_checkpoint_layout_loads_with_plain_torch(tmp_path):
+    from pytorchdistributed_amd.models import TutorialMLP
+    from pytorchdistributed_amd.utils.checkpoint import load_snapshot, save_snapshot
+
+    m = TutorialMLP()
+    opt = torch.optim.SGD(m.parameters(), lr=0.1)
+    path = str(tmp_path / "snap.pt")
+    save_snapshot(path, m, opt, epochs_run=3)
+    snap = torch.load(path, weights_only=True)
+    assert set(snap) >= {"MODEL_STATE", "OPTIMIZER_STATE", "EPOCHS_RUN", "RNG"}
+    assert not any(k.startswith("module.") for k in snap["MODEL_STATE"])
+    m2 = TutorialMLP()
+    assert load_snapshot(path, m2, torch.optim.SGD(m2.parameters(), lr=0.1)) == 3
+    assert torch.equal(m2.fc1.weight, m.fc1.weight)
+
+
+def test_cpu_ops_match_torch():
+    from pytorchdistributed_amd import ops
+
+    x = torch.randn(2, 9, 9, 16)
+    w = torch.randn(8, 3, 3, 16)
+    y = ops.conv2d(x, w, stride=2, padding=1)
+    ref = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), None, 2, 1).permute(0, 2, 3, 1)
+    assert torch.allclose(y, ref, atol=1e-5)
+    p = ops.max_pool2d(x)
+    assert p.shape == (2, 5, 5, 16)
+    assert torch.allclose(ops.global_avg_pool2d(x), x.mean((1, 2)))
