@@ -4,17 +4,16 @@
 // The reference's ResNet-50 (`NB03:314`, Bottleneck BN x53, `model.train()` at `NB03:381`) runs
 // torch's BN followed by separate ReLU / add kernels.  Here every BN is viewed as an [M = N*H*W, C]
 // matrix (C contiguous, a multiple of 8) and handled in two memory-bound passes per direction:
-//   forward : stats  — per-channel shifted sums (x - K_c), (x - K_c)^2 with pivot K_c = x[0, c]
-//                      (cancellation-safe when |mean| >> std), block-reduced in LDS, one fp32 atomic
-//                      per channel per workgroup into a [2, C] accumulator (zeroed by a memset node);
-//             apply  — every workgroup first turns the accumulator into per-channel scale/shift in
-//                      LDS, then streams y = relu(x * scale + shift [+ residual]); workgroup 0 also
-//                      writes the saved mean / invstd and the running statistics.
-//   backward: reduce — sum(dz), sum(dz * (x - mean)) with dz = dy * [y > 0] recomputed from the
-//                      saved output, same atomic scheme;
-//             apply  — dx = A*dz + B*x + C per channel (coefficients built in LDS), dz also emitted
-//                      for the residual branch; workgroup 0 writes dgamma / dbeta in the parameter dtype.
-// No separate "finalize" launches: each direction is memset + 2 kernels.
+//   forward : stats    — per-channel shifted sums (x - K_c), (x - K_c)^2 with pivot K_c = x[0, c]
+//                        (cancellation-safe when |mean| >> std), block-reduced in LDS, written as
+//                        per-workgroup partial slabs [nrb][C] (plain stores: no same-address atomics,
+//                        which serialise at the memory side when ~1000 workgroups hit 2C words);
+//             finalize — 64 channels x 4 row-lanes per workgroup sum the slabs (coalesced, unrolled),
+//                        produce mean / invstd / running stats and the per-channel scale, shift;
+//             apply    — y = relu(x * scale + shift [+ residual]), scale/shift staged in LDS.
+//   backward: reduce   — sum(dz), sum(dz * (x - mean)) with dz = dy * [y > 0] recomputed from the
+//                        saved output, same slab scheme; finalize -> dgamma / dbeta (parameter dtype)
+//                        and per-channel (A, B, C); apply -> dx = A*dz + B*x + C, dz for the residual.
 // Each lane owns 8 consecutive channels (16-B loads); workgroups tile rows x channel groups.
 #include "pda_common.h"
 #include "pda_kernels.h"
@@ -61,10 +60,10 @@ inline int ew_grid(int64_t nvec) {
   return g < 1 ? 1 : (int)g;
 }
 
-// Reduce per-thread 8-channel partials (a, b) over the `rpi` row-threads of a column, then one
-// atomic per channel per block.
-__device__ __forceinline__ void block_col_reduce_atomic(float (&a)[8], float (&b)[8], int tx, int ty, int cols,
-                                                        int rpi, int vcol, int C, float* acc) {
+// Reduce per-thread 8-channel partials (a, b) over the `rpi` row-threads of a column and store one
+// partial per channel per workgroup: slab_a[blockIdx.x][c], slab_b[blockIdx.x][c].
+__device__ __forceinline__ void block_col_reduce_store(float (&a)[8], float (&b)[8], int tx, int ty, int cols,
+                                                       int rpi, int vcol, int C, float* slab_a, float* slab_b) {
   __shared__ float s_a[kThreads * 8];
   __shared__ float s_b[kThreads * 8];
 #pragma unroll
@@ -82,17 +81,42 @@ __device__ __forceinline__ void block_col_reduce_atomic(float (&a)[8], float (&b
         b[j] += s_b[t * 8 + j];
       }
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      atomicAdd(acc + vcol * 8 + j, a[j]);
-      atomicAdd(acc + C + vcol * 8 + j, b[j]);
+    store8(slab_a + (int64_t)blockIdx.x * C + vcol * 8, a);
+    store8(slab_b + (int64_t)blockIdx.x * C + vcol * 8, b);
+  }
+}
+
+// Sum the [nrb][C] slabs for 64 channels per workgroup: 4 row-lanes x 64 channels, coalesced.
+__device__ __forceinline__ void slab_sum(const float* __restrict__ pa, const float* __restrict__ pb, int nrb, int C,
+                                         int c, float& sa, float& sb) {
+  __shared__ float red_a[kThreads], red_b[kThreads];
+  const int l = threadIdx.x >> 6;
+  float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
+  if (c < C) {
+    int r = l;
+    for (; r + 4 < nrb; r += 8) {
+      a0 += pa[(int64_t)r * C + c];
+      b0 += pb[(int64_t)r * C + c];
+      a1 += pa[(int64_t)(r + 4) * C + c];
+      b1 += pb[(int64_t)(r + 4) * C + c];
+    }
+    for (; r < nrb; r += 4) {
+      a0 += pa[(int64_t)r * C + c];
+      b0 += pb[(int64_t)r * C + c];
     }
   }
+  red_a[threadIdx.x] = a0 + a1;
+  red_b[threadIdx.x] = b0 + b1;
+  __syncthreads();
+  sa = red_a[threadIdx.x & 63] + red_a[64 + (threadIdx.x & 63)] + red_a[128 + (threadIdx.x & 63)] +
+       red_a[192 + (threadIdx.x & 63)];
+  sb = red_b[threadIdx.x & 63] + red_b[64 + (threadIdx.x & 63)] + red_b[128 + (threadIdx.x & 63)] +
+       red_b[192 + (threadIdx.x & 63)];
 }
 
 // ---------------------------------------------------------------- forward statistics
 __global__ void __launch_bounds__(kThreads) bn_stats_kernel(const bf16_t* __restrict__ x, int64_t M, int C, int cols,
-                                                            int rpi, int64_t rpb, float* __restrict__ acc) {
+                                                            int rpi, int64_t rpb, float* __restrict__ slab) {
   const int tx = threadIdx.x % cols, ty = threadIdx.x / cols;
   const int vcol = blockIdx.y * cols + tx;
   const bool active = ty < rpi && vcol * 8 < C;
@@ -114,48 +138,60 @@ __global__ void __launch_bounds__(kThreads) bn_stats_kernel(const bf16_t* __rest
       }
     }
   }
-  block_col_reduce_atomic(s1, s2, tx, ty, cols, rpi, vcol, C, acc);
+  block_col_reduce_store(s1, s2, tx, ty, cols, rpi, vcol, C, slab, slab + (int64_t)gridDim.x * C);
 }
 
 __device__ __forceinline__ float param_at(const float* f, const bf16_t* b, int c, float dflt) {
   return f ? f[c] : (b ? bf2f(b[c]) : dflt);
 }
 
-// ---------------------------------------------------------------- forward apply (+ finalize)
-template <bool RES, bool RELU, bool TRAIN>
-__global__ void __launch_bounds__(kThreads) bn_apply_kernel(
-    const bf16_t* __restrict__ x, const bf16_t* __restrict__ res, bf16_t* __restrict__ y, int64_t M, int C,
-    const float* __restrict__ acc, const float* __restrict__ gamma_f, const bf16_t* __restrict__ gamma_b,
-    const float* __restrict__ beta_f, const bf16_t* __restrict__ beta_b, float* __restrict__ running_mean,
-    float* __restrict__ running_var, float momentum, float eps, float* __restrict__ save_mean,
-    float* __restrict__ save_invstd) {
+// ---------------------------------------------------------------- forward finalize
+// TRAIN: statistics from the slabs; eval: from the running statistics.  Writes scale/shift [C].
+template <bool TRAIN>
+__global__ void __launch_bounds__(kThreads) bn_finalize_kernel(
+    const bf16_t* __restrict__ x, const float* __restrict__ slab, int nrb, int64_t M, int C,
+    const float* __restrict__ gamma_f, const bf16_t* __restrict__ gamma_b, const float* __restrict__ beta_f,
+    const bf16_t* __restrict__ beta_b, float* __restrict__ running_mean, float* __restrict__ running_var,
+    float momentum, float eps, float* __restrict__ save_mean, float* __restrict__ save_invstd,
+    float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  float s1 = 0.f, s2 = 0.f;
+  if (TRAIN) slab_sum(slab, slab + (int64_t)nrb * C, nrb, C, c, s1, s2);
+  if (threadIdx.x >= 64 || c >= C) return;
+  float mean, invstd;
+  if (TRAIN) {
+    const float invM = 1.f / (float)M;
+    const float m1 = s1 * invM;
+    const float var = fmaxf(s2 * invM - m1 * m1, 0.f);
+    mean = bf2f(x[c]) + m1;
+    invstd = rsqrtf(var + eps);
+    save_mean[c] = mean;
+    save_invstd[c] = invstd;
+    if (running_mean) {
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+      const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+    }
+  } else {
+    mean = running_mean[c];
+    invstd = rsqrtf(running_var[c] + eps);
+  }
+  const float g = param_at(gamma_f, gamma_b, c, 1.f), b = param_at(beta_f, beta_b, c, 0.f);
+  scale[c] = g * invstd;
+  shift[c] = b - mean * g * invstd;
+}
+
+// ---------------------------------------------------------------- forward apply
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                                            bf16_t* __restrict__ y, int64_t M, int C,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift) {
   __shared__ __attribute__((aligned(16))) float s_scale[kMaxC];
   __shared__ __attribute__((aligned(16))) float s_shift[kMaxC];
-  const float invM = 1.f / (float)M;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float mean, invstd;
-    if (TRAIN) {
-      const float piv = bf2f(x[c]);
-      const float m1 = acc[c] * invM;
-      const float var = fmaxf(acc[C + c] * invM - m1 * m1, 0.f);
-      mean = piv + m1;
-      invstd = rsqrtf(var + eps);
-      if (blockIdx.x == 0) {
-        save_mean[c] = mean;
-        save_invstd[c] = invstd;
-        if (running_mean) {
-          running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
-          const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
-          running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
-        }
-      }
-    } else {
-      mean = running_mean[c];
-      invstd = rsqrtf(running_var[c] + eps);
-    }
-    const float g = param_at(gamma_f, gamma_b, c, 1.f), b = param_at(beta_f, beta_b, c, 0.f);
-    s_scale[c] = g * invstd;
-    s_shift[c] = b - mean * g * invstd;
+    s_scale[c] = scale[c];
+    s_shift[c] = shift[c];
   }
   __syncthreads();
   const int cv = C / 8;
@@ -193,7 +229,7 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* _
                                                                  const bf16_t* __restrict__ y,
                                                                  const float* __restrict__ mean, int64_t M, int C,
                                                                  int cols, int rpi, int64_t rpb,
-                                                                 float* __restrict__ acc) {
+                                                                 float* __restrict__ slab) {
   const int tx = threadIdx.x % cols, ty = threadIdx.x / cols;
   const int vcol = blockIdx.y * cols + tx;
   const bool active = ty < rpi && vcol * 8 < C;
@@ -221,39 +257,46 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* _
       }
     }
   }
-  block_col_reduce_atomic(sa, sb, tx, ty, cols, rpi, vcol, C, acc);
+  block_col_reduce_store(sa, sb, tx, ty, cols, rpi, vcol, C, slab, slab + (int64_t)gridDim.x * C);
 }
 
-// dgamma = invstd * sum(dz (x-mean)), dbeta = sum(dz);  dx = A*dz + B*x + Cc
-template <bool RELU, bool DRES>
-__global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ y, int64_t M, int C,
-    const float* __restrict__ acc, const float* __restrict__ mean, const float* __restrict__ invstd,
-    const float* __restrict__ gamma_f, const bf16_t* __restrict__ gamma_b, float* __restrict__ dgamma_f,
-    bf16_t* __restrict__ dgamma_b, float* __restrict__ dbeta_f, bf16_t* __restrict__ dbeta_b, bf16_t* __restrict__ dx,
-    bf16_t* __restrict__ dres) {
-  __shared__ __attribute__((aligned(16))) float s_A[kMaxC];
-  __shared__ __attribute__((aligned(16))) float s_B[kMaxC];
-  __shared__ __attribute__((aligned(16))) float s_C[kMaxC];
+// dgamma = invstd * sum(dz (x-mean)), dbeta = sum(dz);  coefficients for dx = A*dz + B*x + Cc
+__global__ void __launch_bounds__(kThreads) bn_bwd_finalize_kernel(
+    const float* __restrict__ slab, int nrb, int64_t M, int C, const float* __restrict__ mean,
+    const float* __restrict__ invstd, const float* __restrict__ gamma_f, const bf16_t* __restrict__ gamma_b,
+    float* __restrict__ dgamma_f, bf16_t* __restrict__ dgamma_b, float* __restrict__ dbeta_f,
+    bf16_t* __restrict__ dbeta_b, float* __restrict__ coef) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  float sdz, sdx;
+  slab_sum(slab, slab + (int64_t)nrb * C, nrb, C, c, sdz, sdx);
+  if (threadIdx.x >= 64 || c >= C) return;
+  const float is = invstd[c], mu = mean[c];
+  const float g = param_at(gamma_f, gamma_b, c, 1.f);
+  const float dg = sdx * is;
+  if (dgamma_f) dgamma_f[c] = dg;
+  if (dgamma_b) dgamma_b[c] = f2bf(dg);
+  if (dbeta_f) dbeta_f[c] = sdz;
+  if (dbeta_b) dbeta_b[c] = f2bf(sdz);
   const float invM = 1.f / (float)M;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const float sdz = acc[c], sdx = acc[C + c];
-    const float is = invstd[c], mu = mean[c];
-    const float g = param_at(gamma_f, gamma_b, c, 1.f);
-    const float dg = sdx * is;
-    if (blockIdx.x == 0) {
-      if (dgamma_f) dgamma_f[c] = dg;
-      if (dgamma_b) dgamma_b[c] = f2bf(dg);
-      if (dbeta_f) dbeta_f[c] = sdz;
-      if (dbeta_b) dbeta_b[c] = f2bf(sdz);
-    }
-    const float A = g * is;
-    const float B = -A * is * dg * invM;
-    s_A[c] = A;
-    s_B[c] = B;
-    s_C[c] = -A * sdz * invM - B * mu;
-  }
+  const float A = g * is;
+  const float B = -A * is * dg * invM;
+  coef[c] = A;
+  coef[C + c] = B;
+  coef[2 * C + c] = -A * sdz * invM - B * mu;
+}
+
+template <bool RELU, bool DRES>
+__global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy,
+                                                                const bf16_t* __restrict__ x,
+                                                                const bf16_t* __restrict__ y, int64_t M, int C,
+                                                                const float* __restrict__ coef,
+                                                                bf16_t* __restrict__ dx, bf16_t* __restrict__ dres) {
+  __shared__ __attribute__((aligned(16))) float s_co[3 * kMaxC];
+  for (int c = threadIdx.x; c < 3 * C; c += blockDim.x) s_co[c] = coef[c];
   __syncthreads();
+  const float* s_A = s_co;
+  const float* s_B = s_co + C;
+  const float* s_C = s_co + 2 * C;
   const int cv = C / 8;
   const int64_t nvec = M * cv;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -274,27 +317,22 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(
   }
 }
 
-template <bool TRAIN>
-hipError_t launch_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int C, const float* acc,
-                        const float* gf, const bf16_t* gb, const float* bfp, const bf16_t* bb, float* rm, float* rv,
-                        float momentum, float eps, bool relu, float* save_mean, float* save_invstd, hipStream_t st) {
+hipError_t launch_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int C, const float* scale,
+                        const float* shift, bool relu, hipStream_t st) {
   const int grid = ew_grid(M * C / 8);
-#define PDA_BN_APPLY(R, L)                                                                                    \
-  bn_apply_kernel<R, L, TRAIN><<<grid, kThreads, 0, st>>>(x, res, y, M, C, acc, gf, gb, bfp, bb, rm, rv, momentum, \
-                                                          eps, save_mean, save_invstd)
-  if (res && relu) PDA_BN_APPLY(true, true);
-  else if (res) PDA_BN_APPLY(true, false);
-  else if (relu) PDA_BN_APPLY(false, true);
-  else PDA_BN_APPLY(false, false);
-#undef PDA_BN_APPLY
+  if (res && relu) bn_apply_kernel<true, true><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift);
+  else if (res) bn_apply_kernel<true, false><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift);
+  else if (relu) bn_apply_kernel<false, true><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift);
+  else bn_apply_kernel<false, false><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift);
   return hipGetLastError();
 }
 
 }  // namespace
 
+// workspace: 2 partial slabs [nrb][C] + 3 per-channel tables [C]
 int64_t bn_workspace_floats(int64_t M, int64_t C) {
-  (void)M;
-  return 2 * C;
+  BnGeom g = bn_geom(M, C);
+  return 2 * (int64_t)g.nrb * C + 3 * C;
 }
 
 hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
@@ -303,21 +341,28 @@ hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M
                         float* save_invstd, float* ws, hipStream_t st) {
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C);
-  PDA_CHECK_HIP(hipMemsetAsync(ws, 0, 2 * C * sizeof(float), st));
+  float* scale = ws + 2 * (int64_t)g.nrb * C;
+  float* shift = scale + C;
   bn_stats_kernel<<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(x, M, (int)C, g.cols, g.rpi, g.rpb, ws);
   PDA_CHECK_HIP(hipGetLastError());
-  return launch_apply<true>(x, res, y, M, (int)C, ws, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var,
-                            momentum, eps, relu, save_mean, save_invstd, st);
+  bn_finalize_kernel<true><<<(unsigned)((C + 63) / 64), kThreads, 0, st>>>(
+      x, ws, g.nrb, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum, eps, save_mean,
+      save_invstd, scale, shift);
+  PDA_CHECK_HIP(hipGetLastError());
+  return launch_apply(x, res, y, M, (int)C, scale, shift, relu, st);
 }
 
 hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
                        const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, const float* running_mean,
                        const float* running_var, float eps, bool relu, float* ws, hipStream_t st) {
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
-  (void)ws;
-  return launch_apply<false>(x, res, y, M, (int)C, nullptr, gamma_f, gamma_b, beta_f, beta_b,
-                             const_cast<float*>(running_mean), const_cast<float*>(running_var), 0.f, eps, relu,
-                             nullptr, nullptr, st);
+  float* scale = ws;
+  float* shift = ws + C;
+  bn_finalize_kernel<false><<<(unsigned)((C + 63) / 64), kThreads, 0, st>>>(
+      x, nullptr, 0, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, const_cast<float*>(running_mean),
+      const_cast<float*>(running_var), 0.f, eps, nullptr, nullptr, scale, shift);
+  PDA_CHECK_HIP(hipGetLastError());
+  return launch_apply(x, res, y, M, (int)C, scale, shift, relu, st);
 }
 
 hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, int64_t M, int64_t C, const float* save_mean,
@@ -326,7 +371,7 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, int64_t M,
                   hipStream_t st) {
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C);
-  PDA_CHECK_HIP(hipMemsetAsync(ws, 0, 2 * C * sizeof(float), st));
+  float* coef = ws + 2 * (int64_t)g.nrb * C;
   if (relu)
     bn_bwd_reduce_kernel<true><<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(dy, x, y, save_mean, M, (int)C, g.cols, g.rpi,
                                                                        g.rpb, ws);
@@ -334,15 +379,19 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, int64_t M,
     bn_bwd_reduce_kernel<false><<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(dy, x, y, save_mean, M, (int)C, g.cols,
                                                                         g.rpi, g.rpb, ws);
   PDA_CHECK_HIP(hipGetLastError());
+  bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kThreads, 0, st>>>(ws, g.nrb, M, (int)C, save_mean,
+                                                                         save_invstd, gamma_f, gamma_b, dgamma_f,
+                                                                         dgamma_b, dbeta_f, dbeta_b, coef);
+  PDA_CHECK_HIP(hipGetLastError());
   const int grid = ew_grid(M * C / 8);
-#define PDA_BN_BWD(R, D)                                                                                          \
-  bn_bwd_apply_kernel<R, D><<<grid, kThreads, 0, st>>>(dy, x, y, M, (int)C, ws, save_mean, save_invstd, gamma_f,   \
-                                                       gamma_b, dgamma_f, dgamma_b, dbeta_f, dbeta_b, dx, dres)
-  if (relu && dres) PDA_BN_BWD(true, true);
-  else if (relu) PDA_BN_BWD(true, false);
-  else if (dres) PDA_BN_BWD(false, true);
-  else PDA_BN_BWD(false, false);
-#undef PDA_BN_BWD
+  if (relu && dres)
+    bn_bwd_apply_kernel<true, true><<<grid, kThreads, 0, st>>>(dy, x, y, M, (int)C, coef, dx, dres);
+  else if (relu)
+    bn_bwd_apply_kernel<true, false><<<grid, kThreads, 0, st>>>(dy, x, y, M, (int)C, coef, dx, dres);
+  else if (dres)
+    bn_bwd_apply_kernel<false, true><<<grid, kThreads, 0, st>>>(dy, x, y, M, (int)C, coef, dx, dres);
+  else
+    bn_bwd_apply_kernel<false, false><<<grid, kThreads, 0, st>>>(dy, x, y, M, (int)C, coef, dx, dres);
   return hipGetLastError();
 }
 

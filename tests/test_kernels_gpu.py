@@ -98,9 +98,9 @@ def test_conv_fwd_dgrad_wgrad(case):
     assert rel_err(yg.cpu(), y.detach()) < 1e-2
     dx = C().conv_dgrad(bf(dy), bf(w.detach()), H, W, s, p, 1)
     assert rel_err(dx.cpu(), x.grad) < 1e-2
-    dw = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, 1, True)
+    dw = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, 1, True, None)
     assert rel_err(dw.cpu(), w.grad) < 1e-3
-    dwb = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, 1, False)
+    dwb = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, 1, False, None)
     assert rel_err(dwb.cpu(), w.grad) < 1e-2
 
 
@@ -131,7 +131,7 @@ def test_batchnorm_train(shape, relu, res):
                                         relu)
     assert rel_err(yg.cpu(), y.detach()) < 1e-2
     assert rel_err(rmg.cpu(), rm) < 1e-4 and rel_err(rvg.cpu(), rv) < 1e-4
-    dx, dres, dgamma, dbeta = C().bn_bwd(bf(dy), bf(x), yg, mean, invstd, g.to(DEV), relu, res)
+    dx, dres, dgamma, dbeta = C().bn_bwd(bf(dy), bf(x), yg, mean, invstd, g.to(DEV), relu, res, None, None)
     assert rel_err(dx.cpu(), xr.grad) < 2e-2
     assert rel_err(dgamma.cpu(), gr.grad) < 1e-2
     assert rel_err(dbeta.cpu(), br.grad) < 1e-2
