@@ -45,7 +45,9 @@ BnGeom bn_geom(int64_t M, int64_t C) {
     g.rpi = kThreads / g.cv;
     g.gy = 1;
   }
-  const int target = 1024 / g.gy > 0 ? 1024 / g.gy : 1;
+  // ~256 row blocks: one per CU is enough for these streaming reductions (each lane keeps 4 rows of
+  // loads in flight) and keeps the partial slabs small for the finalize pass.
+  const int target = 256 / g.gy > 0 ? 256 / g.gy : 1;
   int64_t rpb = (M + target - 1) / target;
   const int64_t min_rpb = (int64_t)g.rpi * 8;
   if (rpb < min_rpb) rpb = min_rpb;
@@ -86,21 +88,22 @@ __device__ __forceinline__ void block_col_reduce_store(float (&a)[8], float (&b)
   }
 }
 
-// Sum the [nrb][C] slabs for 64 channels per workgroup: 4 row-lanes x 64 channels, coalesced.
+// Sum the [nrb][C] slabs for 64 channels per workgroup: kFinThreads = 64 channels x 16 row-lanes.
+constexpr int kFinThreads = 1024;
 __device__ __forceinline__ void slab_sum(const float* __restrict__ pa, const float* __restrict__ pb, int nrb, int C,
                                          int c, float& sa, float& sb) {
-  __shared__ float red_a[kThreads], red_b[kThreads];
-  const int l = threadIdx.x >> 6;
+  __shared__ float red_a[kFinThreads], red_b[kFinThreads];
+  const int l = threadIdx.x >> 6;  // 0..15
   float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
   if (c < C) {
     int r = l;
-    for (; r + 4 < nrb; r += 8) {
+    for (; r + 16 < nrb; r += 32) {
       a0 += pa[(int64_t)r * C + c];
       b0 += pb[(int64_t)r * C + c];
-      a1 += pa[(int64_t)(r + 4) * C + c];
-      b1 += pb[(int64_t)(r + 4) * C + c];
+      a1 += pa[(int64_t)(r + 16) * C + c];
+      b1 += pb[(int64_t)(r + 16) * C + c];
     }
-    for (; r < nrb; r += 4) {
+    for (; r < nrb; r += 16) {
       a0 += pa[(int64_t)r * C + c];
       b0 += pb[(int64_t)r * C + c];
     }
@@ -108,10 +111,13 @@ __device__ __forceinline__ void slab_sum(const float* __restrict__ pa, const flo
   red_a[threadIdx.x] = a0 + a1;
   red_b[threadIdx.x] = b0 + b1;
   __syncthreads();
-  sa = red_a[threadIdx.x & 63] + red_a[64 + (threadIdx.x & 63)] + red_a[128 + (threadIdx.x & 63)] +
-       red_a[192 + (threadIdx.x & 63)];
-  sb = red_b[threadIdx.x & 63] + red_b[64 + (threadIdx.x & 63)] + red_b[128 + (threadIdx.x & 63)] +
-       red_b[192 + (threadIdx.x & 63)];
+  const int ch = threadIdx.x & 63;
+  sa = sb = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    sa += red_a[k * 64 + ch];
+    sb += red_b[k * 64 + ch];
+  }
 }
 
 // ---------------------------------------------------------------- forward statistics
@@ -127,7 +133,21 @@ __global__ void __launch_bounds__(kThreads) bn_stats_kernel(const bf16_t* __rest
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   if (active) {
     load8(x + vcol * 8, piv);  // row 0 is the pivot
-    for (int64_t r = r0 + ty; r < r1; r += rpi) {
+    int64_t r = r0 + ty;
+    for (; r + 3 * rpi < r1; r += 4 * rpi) {  // 4 independent 16-B loads in flight per lane
+      float v[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load8(x + (r + u * rpi) * C + vcol * 8, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[u][j] - piv[j];
+          s1[j] += d;
+          s2[j] += d * d;
+        }
+    }
+    for (; r < r1; r += rpi) {
       float v[8];
       load8(x + r * C + vcol * 8, v);
 #pragma unroll
@@ -148,7 +168,7 @@ __device__ __forceinline__ float param_at(const float* f, const bf16_t* b, int c
 // ---------------------------------------------------------------- forward finalize
 // TRAIN: statistics from the slabs; eval: from the running statistics.  Writes scale/shift [C].
 template <bool TRAIN>
-__global__ void __launch_bounds__(kThreads) bn_finalize_kernel(
+__global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
     const bf16_t* __restrict__ x, const float* __restrict__ slab, int nrb, int64_t M, int C,
     const float* __restrict__ gamma_f, const bf16_t* __restrict__ gamma_b, const float* __restrict__ beta_f,
     const bf16_t* __restrict__ beta_b, float* __restrict__ running_mean, float* __restrict__ running_var,
@@ -240,6 +260,7 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* _
   for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.f;
   if (active) {
     load8(mean + vcol * 8, mu);
+#pragma unroll 2
     for (int64_t r = r0 + ty; r < r1; r += rpi) {
       const int64_t off = r * C + vcol * 8;
       float g[8], xv[8];
@@ -261,7 +282,7 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* _
 }
 
 // dgamma = invstd * sum(dz (x-mean)), dbeta = sum(dz);  coefficients for dx = A*dz + B*x + Cc
-__global__ void __launch_bounds__(kThreads) bn_bwd_finalize_kernel(
+__global__ void __launch_bounds__(kFinThreads) bn_bwd_finalize_kernel(
     const float* __restrict__ slab, int nrb, int64_t M, int C, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma_f, const bf16_t* __restrict__ gamma_b,
     float* __restrict__ dgamma_f, bf16_t* __restrict__ dgamma_b, float* __restrict__ dbeta_f,
@@ -345,7 +366,7 @@ hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M
   float* shift = scale + C;
   bn_stats_kernel<<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(x, M, (int)C, g.cols, g.rpi, g.rpb, ws);
   PDA_CHECK_HIP(hipGetLastError());
-  bn_finalize_kernel<true><<<(unsigned)((C + 63) / 64), kThreads, 0, st>>>(
+  bn_finalize_kernel<true><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
       x, ws, g.nrb, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum, eps, save_mean,
       save_invstd, scale, shift);
   PDA_CHECK_HIP(hipGetLastError());
@@ -358,7 +379,7 @@ hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M,
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
   float* scale = ws;
   float* shift = ws + C;
-  bn_finalize_kernel<false><<<(unsigned)((C + 63) / 64), kThreads, 0, st>>>(
+  bn_finalize_kernel<false><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
       x, nullptr, 0, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, const_cast<float*>(running_mean),
       const_cast<float*>(running_var), 0.f, eps, nullptr, nullptr, scale, shift);
   PDA_CHECK_HIP(hipGetLastError());
@@ -379,7 +400,7 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, int64_t M,
     bn_bwd_reduce_kernel<false><<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(dy, x, y, save_mean, M, (int)C, g.cols,
                                                                         g.rpi, g.rpb, ws);
   PDA_CHECK_HIP(hipGetLastError());
-  bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kThreads, 0, st>>>(ws, g.nrb, M, (int)C, save_mean,
+  bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(ws, g.nrb, M, (int)C, save_mean,
                                                                          save_invstd, gamma_f, gamma_b, dgamma_f,
                                                                          dgamma_b, dbeta_f, dbeta_b, coef);
   PDA_CHECK_HIP(hipGetLastError());

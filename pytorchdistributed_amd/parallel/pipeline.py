@@ -1,0 +1,315 @@
+"""Multi-process pipeline parallelism (reference concept docs
+`03 模型并行/03_model_parallel.ipynb` raw lines 637-705: GPipe re-computation, 1F1B, PipeDream flush,
+interleaving; reference code: the single-process micro-batch loop at raw lines 538-561).
+
+One process per stage, activations / gradients moved with RCCL point-to-point (``send``/``recv`` over
+xGMI).  Schedules:
+
+* ``gpipe`` — all forwards, then all backwards (fill-drain);
+* ``1f1b``  — PipeDream-flush: ``S - s - 1`` warm-up forwards, then one-forward-one-backward, then the
+  cool-down backwards; peak activation memory is bounded by the stage depth instead of the number of
+  micro-batches.
+
+In the 1F1B steady state a stage's "send activation to s+1" and "receive gradient from s+1" are issued
+as ONE batched P2P group (likewise "send gradient to s-1" + "receive next activation from s-1"), so two
+neighbours never wait on each other's opposite-direction transfer (the classic blocking-P2P deadlock).
+``recompute=True`` keeps only each micro-batch's stage input and re-runs the stage forward in backward
+(GPipe re-materialisation, raw lines 637-643).  :func:`pp_dp_groups` builds the PP x DP process groups
+(e.g. 4 stages x 2 replicas: PP {0-3},{4-7}; DP {0,4},{1,5},{2,6},{3,7}) and :func:`dp_sync_grads`
+averages a stage's gradients over its DP group in flat buckets.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+import torch.nn as tnn
+from torch.utils.checkpoint import checkpoint
+
+from .. import distributed as pdist
+
+
+# ------------------------------------------------------------------ schedules (pure functions)
+def schedule_gpipe(num_stages: int, num_micro: int, stage: int) -> List[Tuple[str, int]]:
+    return [("F", i) for i in range(num_micro)] + [("B", i) for i in range(num_micro)]
+
+
+def schedule_1f1b(num_stages: int, num_micro: int, stage: int) -> List[Tuple[str, int]]:
+    warm = min(num_stages - stage - 1, num_micro)
+    out = [("F", i) for i in range(warm)]
+    steady = num_micro - warm
+    for i in range(steady):
+        out.append(("F", warm + i))
+        out.append(("B", i))
+    out += [("B", i) for i in range(steady, num_micro)]
+    return out
+
+
+SCHEDULES = {"gpipe": schedule_gpipe, "1f1b": schedule_1f1b}
+
+
+def check_schedule(fn, num_stages: int, num_micro: int) -> bool:
+    """Simulate every stage's action list with unbounded send buffers; True iff it completes."""
+    acts = [list(fn(num_stages, num_micro, s)) for s in range(num_stages)]
+    done_f = [set() for _ in range(num_stages)]
+    done_b = [set() for _ in range(num_stages)]
+    pos = [0] * num_stages
+    progress = True
+    while progress:
+        progress = False
+        for s in range(num_stages):
+            if pos[s] >= len(acts[s]):
+                continue
+            kind, mb = acts[s][pos[s]]
+            if kind == "F":
+                ok = s == 0 or mb in done_f[s - 1]
+            else:
+                ok = mb in done_f[s] and (s == num_stages - 1 or mb in done_b[s + 1])
+            if ok:
+                (done_f if kind == "F" else done_b)[s].add(mb)
+                pos[s] += 1
+                progress = True
+    return all(p == len(a) for p, a in zip(pos, acts))
+
+
+# ------------------------------------------------------------------ process groups
+def pp_dp_groups(pp: int, dp: int):
+    """Returns (pp_group, dp_group, stage, dp_rank, pp_ranks) for this rank; rank = dp_rank * pp + stage."""
+    rank, world = pdist.get_rank(), pdist.get_world_size()
+    assert world == pp * dp, f"world {world} != pp {pp} x dp {dp}"
+    pp_group = dp_group = None
+    my_pp_ranks = None
+    for d in range(dp):
+        ranks = [d * pp + s for s in range(pp)]
+        g = dist.new_group(ranks)
+        if rank in ranks:
+            pp_group, my_pp_ranks = g, ranks
+    for s in range(pp):
+        ranks = [d * pp + s for d in range(dp)]
+        g = dist.new_group(ranks)
+        if rank in ranks:
+            dp_group = g
+    return pp_group, dp_group, rank % pp, rank // pp, my_pp_ranks
+
+
+@torch.no_grad()
+def dp_sync_grads(module: tnn.Module, group, bucket_mb: float = 64.0):
+    """Average ``module``'s gradients over ``group`` with coalesced all-reduces (one per bucket)."""
+    if group is None or dist.get_world_size(group) == 1:
+        return
+    grads = [p.grad for p in module.parameters() if p.grad is not None]
+    if not grads:
+        return
+    nccl = dist.get_backend(group) == "nccl"
+    cap = int(bucket_mb * 2 ** 20)
+    bucket: List[torch.Tensor] = []
+    size = 0
+
+    def flush():
+        if not bucket:
+            return
+        flat = torch.cat([g.reshape(-1) for g in bucket])
+        if nccl:
+            dist.all_reduce(flat, op=dist.ReduceOp.AVG, group=group)
+        else:
+            dist.all_reduce(flat, group=group)
+            flat.div_(dist.get_world_size(group))
+        off = 0
+        for g in bucket:
+            g.copy_(flat[off: off + g.numel()].view_as(g))
+            off += g.numel()
+
+    for g in grads:
+        if size + g.numel() * g.element_size() > cap and bucket:
+            flush()
+            bucket, size = [], 0
+        bucket.append(g)
+        size += g.numel() * g.element_size()
+    flush()
+
+
+# ------------------------------------------------------------------ the pipeline engine
+class Pipeline:
+    """Drive one pipeline stage.
+
+    ``stage_module``: this rank's stage; ``ranks``: global ranks of the pipeline in stage order;
+    ``loss_fn(output, target)`` is applied on the last stage per micro-batch.
+    """
+
+    def __init__(self, stage_module: tnn.Module, ranks: Sequence[int], num_microbatches: int,
+                 schedule: str = "1f1b", loss_fn: Optional[Callable] = None, recompute: bool = False,
+                 group=None, device=None):
+        self.module = stage_module
+        self.ranks = list(ranks)
+        self.S = len(self.ranks)
+        self.rank = pdist.get_rank()
+        self.stage = self.ranks.index(self.rank)
+        self.M = num_microbatches
+        self.schedule_name = schedule
+        self.loss_fn = loss_fn
+        self.recompute = recompute
+        self.group = group
+        self.device = device or next(stage_module.parameters()).device
+        self.prev = self.ranks[self.stage - 1] if self.stage > 0 else None
+        self.next = self.ranks[self.stage + 1] if self.stage < self.S - 1 else None
+        self._fwd_meta = None  # (shape, dtype) received from prev
+        self._bwd_meta = None  # (shape, dtype) of our output (grad received from next)
+
+    @property
+    def is_first(self):
+        return self.stage == 0
+
+    @property
+    def is_last(self):
+        return self.stage == self.S - 1
+
+    # ---------------- shape handshake (once) and p2p helpers
+    def _send_meta(self, t: torch.Tensor, dst: int):
+        meta = torch.zeros(10, dtype=torch.long, device=self.device)
+        meta[0] = t.dim()
+        meta[1] = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[t.dtype]
+        meta[2: 2 + t.dim()] = torch.tensor(t.shape, dtype=torch.long)
+        dist.send(meta, dst, group=self.group)
+
+    def _recv_meta(self, src: int):
+        meta = torch.zeros(10, dtype=torch.long, device=self.device)
+        dist.recv(meta, src, group=self.group)
+        nd = int(meta[0])
+        dtype = [torch.float32, torch.bfloat16, torch.float16][int(meta[1])]
+        return tuple(int(v) for v in meta[2: 2 + nd]), dtype
+
+    def _p2p(self, send: Optional[Tuple[torch.Tensor, int]] = None, recv: Optional[Tuple[torch.Tensor, int]] = None):
+        ops = []
+        if send is not None:
+            ops.append(dist.P2POp(dist.isend, send[0].contiguous(), send[1], group=self.group))
+        if recv is not None:
+            ops.append(dist.P2POp(dist.irecv, recv[0], recv[1], group=self.group))
+        if ops:
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+
+    def _empty(self, meta):
+        shape, dtype = meta
+        return torch.empty(shape, dtype=dtype, device=self.device)
+
+    # ---------------- compute
+    def _forward(self, x: torch.Tensor):
+        if self.recompute and torch.is_grad_enabled():
+            return checkpoint(self.module, x, use_reentrant=False)
+        return self.module(x)
+
+    def step(self, inputs: Optional[torch.Tensor] = None, targets: Optional[torch.Tensor] = None):
+        """Run one optimisation step's forward+backward over ``num_microbatches``; returns the mean loss
+        on the last stage (None elsewhere).  Gradients accumulate into the stage parameters."""
+        M = self.M
+        in_mb = list(inputs.chunk(M)) if (self.is_first and inputs is not None) else [None] * M
+        tg_mb = list(targets.chunk(M)) if (self.is_last and targets is not None) else [None] * M
+        acts_in: List[Optional[torch.Tensor]] = [None] * M
+        acts_out: List[Optional[torch.Tensor]] = [None] * M
+        losses = []
+
+        # first-step handshakes so receivers can allocate buffers
+        def ensure_fwd_meta():
+            if self._fwd_meta is None and not self.is_first:
+                self._fwd_meta = self._recv_meta(self.prev)
+
+        def recv_forward(i):
+            if self.is_first:
+                x = in_mb[i].to(self.device)
+                return x
+            ensure_fwd_meta()
+            buf = self._empty(self._fwd_meta)
+            self._p2p(recv=(buf, self.prev))
+            return buf.requires_grad_()
+
+        def run_forward(i, x):
+            if not self.is_first:
+                x.requires_grad_()
+            acts_in[i] = x
+            y = self._forward(x)
+            if self.is_last:
+                loss = self.loss_fn(y, tg_mb[i].to(self.device)) / M if self.loss_fn else y.float().mean() / M
+                losses.append(loss.detach())
+                acts_out[i] = loss
+                return None
+            acts_out[i] = y
+            if self._bwd_meta is None:
+                self._bwd_meta = (tuple(y.shape), y.dtype)
+                self._send_meta(y, self.next)
+            return y
+
+        def run_backward(i, dy):
+            out = acts_out[i]
+            if self.is_last:
+                out.backward()
+            else:
+                torch.autograd.backward(out, dy)
+            dx = acts_in[i].grad if not self.is_first else None
+            acts_in[i] = acts_out[i] = None
+            return dx
+
+        sched = self.schedule_name
+        if sched == "gpipe":
+            for i in range(M):
+                y = run_forward(i, recv_forward(i))
+                if y is not None:
+                    self._p2p(send=(y.detach(), self.next))
+            for i in range(M):
+                dy = None
+                if not self.is_last:
+                    dy = self._empty(self._bwd_meta)
+                    self._p2p(recv=(dy, self.next))
+                dx = run_backward(i, dy)
+                if not self.is_first:
+                    self._p2p(send=(dx, self.prev))
+        elif sched == "1f1b":
+            warm = min(self.S - self.stage - 1, M)
+            steady = M - warm
+            for i in range(warm):
+                y = run_forward(i, recv_forward(i))
+                if y is not None:
+                    self._p2p(send=(y.detach(), self.next))
+            x = recv_forward(warm) if steady > 0 else None
+            for j in range(steady):
+                fi = warm + j
+                y = run_forward(fi, x)
+                dy = None
+                if not self.is_last:
+                    dy = self._empty(self._bwd_meta)
+                    self._p2p(send=(y.detach(), self.next), recv=(dy, self.next))  # send fwd + recv bwd
+                dx = run_backward(j, dy)
+                if j == steady - 1:
+                    if not self.is_first:
+                        self._p2p(send=(dx, self.prev))
+                else:
+                    if self.is_first:
+                        x = recv_forward(fi + 1)
+                    else:
+                        ensure_fwd_meta()
+                        x = self._empty(self._fwd_meta)
+                        self._p2p(send=(dx, self.prev), recv=(x, self.prev))  # send bwd + recv fwd
+            for i in range(steady, M):
+                dy = None
+                if not self.is_last:
+                    dy = self._empty(self._bwd_meta)
+                    self._p2p(recv=(dy, self.next))
+                dx = run_backward(i, dy)
+                if not self.is_first:
+                    self._p2p(send=(dx, self.prev))
+        else:
+            raise ValueError(f"unknown schedule {sched!r}")
+        if self.is_last:
+            return torch.stack(losses).sum()
+        return None
+
+
+def partition_layers(num_layers: int, num_stages: int) -> List[Tuple[int, int]]:
+    """Contiguous [start, end) layer ranges, balanced (earlier stages get the remainder)."""
+    base, rem = divmod(num_layers, num_stages)
+    out, s = [], 0
+    for i in range(num_stages):
+        n = base + (1 if i < rem else 0)
+        out.append((s, s + n))
+        s += n
+    return out

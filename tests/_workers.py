@@ -85,3 +85,87 @@ def failing_worker(rank, world):
     import time
 
     time.sleep(60)
+
+
+def _tiny_stack(n_layers=4, d=16, seed=0):
+    import torch.nn as nn
+
+    torch.manual_seed(seed)
+    layers = []
+    for _ in range(n_layers):
+        layers += [nn.Linear(d, d), nn.LayerNorm(d), nn.GELU()]
+    return nn.Sequential(*layers)
+
+
+def pipeline_worker(rank, world, pp, dp, schedule, recompute, outdir):
+    """PP x DP on gloo: stage grads after one pipeline step must equal the single-process grads."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.pipeline import Pipeline, dp_sync_grads, partition_layers, pp_dp_groups
+
+    pd.init_process_group("gloo")
+    pp_group, dp_group, stage, dp_rank, ranks = pp_dp_groups(pp, dp)
+    full = _tiny_stack(4)
+    blocks = [full[3 * i: 3 * i + 3] for i in range(4)]
+    lo, hi = partition_layers(4, pp)[stage]
+    stage_mod = torch.nn.Sequential(*blocks[lo:hi])
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(dp * 8, 16, generator=g)
+    Y = torch.randn(dp * 8, 16, generator=g)
+    xs, ys = X[dp_rank * 8:(dp_rank + 1) * 8], Y[dp_rank * 8:(dp_rank + 1) * 8]
+    pipe = Pipeline(stage_mod, ranks, num_microbatches=4, schedule=schedule, loss_fn=F.mse_loss,
+                    recompute=recompute, device=torch.device("cpu"))
+    loss = pipe.step(xs, ys)
+    dp_sync_grads(stage_mod, dp_group)
+    torch.save({"grads": {n: p.grad.clone() for n, p in stage_mod.named_parameters()}, "lo": lo,
+                "loss": loss}, os.path.join(outdir, f"{rank}.pt"))
+    pd.destroy_process_group()
+
+
+class _Block(torch.nn.Module):
+    def __init__(self, d=16):
+        super().__init__()
+        self.ln = torch.nn.LayerNorm(d)
+        self.fc1 = torch.nn.Linear(d, 3 * d)
+        self.fc2 = torch.nn.Linear(3 * d, d)
+
+    def forward(self, x):
+        return x + self.fc2(F.gelu(self.fc1(self.ln(x))))
+
+
+class _Net(torch.nn.Module):
+    def __init__(self, d=16, n=3):
+        super().__init__()
+        self.inp = torch.nn.Linear(8, d)
+        self.blocks = torch.nn.ModuleList([_Block(d) for _ in range(n)])
+        self.head = torch.nn.Linear(d, 4)
+
+    def forward(self, x):
+        h = self.inp(x)
+        for b in self.blocks:
+            h = b(h)
+        return self.head(h)
+
+
+def fsdp_worker(rank, world, outdir):
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.optim import AdamW
+    from pytorchdistributed_amd.parallel.fsdp import FullyShardedDataParallel
+
+    pd.init_process_group("gloo")
+    torch.manual_seed(0)
+    net = _Net()
+    model = FullyShardedDataParallel(net, unit_types=(_Block,))
+    opt = AdamW(model.parameters(), lr=1e-2, weight_decay=0.1)
+    g = torch.Generator().manual_seed(3)
+    for step in range(3):
+        X = torch.randn(world * 4, 8, generator=g)
+        Y = torch.randint(0, 4, (world * 4,), generator=g)
+        xs, ys = X[rank * 4:(rank + 1) * 4], Y[rank * 4:(rank + 1) * 4]
+        opt.zero_grad()
+        F.cross_entropy(model(xs), ys).backward()
+        opt.step()
+    sd = model.full_state_dict()
+    model.save_sharded(os.path.join(outdir, "ckpt"))
+    if rank == 0:
+        torch.save(sd, os.path.join(outdir, "full.pt"))
+    pd.destroy_process_group()
