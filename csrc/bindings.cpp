@@ -115,7 +115,7 @@ void cast_scale(Tensor src, Tensor dst, double scale, c10::optional<Tensor> scal
 }
 
 // ------------------------------------------------------------------ cross entropy
-std::vector<Tensor> ce_fwd(Tensor logits, Tensor target, int64_t ignore_index, double smoothing) {
+std::vector<Tensor> ce_fwd(Tensor logits, Tensor target, int64_t ignore_index, double smoothing, int64_t num_valid) {
   check_f32_or_bf16(logits, "logits");
   TORCH_CHECK(logits.dim() == 2, "logits must be [M, C]");
   const int64_t M = logits.size(0), C = logits.size(1);
@@ -129,7 +129,8 @@ std::vector<Tensor> ce_fwd(Tensor logits, Tensor target, int64_t ignore_index, d
   c10::DeviceGuard g(logits.device());
   auto opts = logits.options().dtype(at::kFloat);
   Tensor loss = at::empty({M}, opts), lse = at::empty({M}, opts);
-  CHECK_HIP_OK(pda::cross_entropy_fwd(logits.data_ptr(), is_bf16(logits), M, C,
+  const int64_t Cv = num_valid > 0 ? std::min<int64_t>(num_valid, C) : C;
+  CHECK_HIP_OK(pda::cross_entropy_fwd(logits.data_ptr(), is_bf16(logits), M, C, Cv,
                                       prob ? nullptr : target.data_ptr<int64_t>(),
                                       prob ? target.data_ptr<float>() : nullptr, ignore_index, (float)smoothing,
                                       loss.data_ptr<float>(), lse.data_ptr<float>(), stream_of(logits)));
@@ -137,7 +138,7 @@ std::vector<Tensor> ce_fwd(Tensor logits, Tensor target, int64_t ignore_index, d
 }
 
 Tensor ce_bwd(Tensor logits, Tensor target, Tensor lse, Tensor gscale_t, double gscale, int64_t ignore_index,
-              double smoothing) {
+              double smoothing, int64_t num_valid) {
   check_f32_or_bf16(logits, "logits");
   const int64_t M = logits.size(0), C = logits.size(1);
   const bool prob = target.is_floating_point();
@@ -145,7 +146,8 @@ Tensor ce_bwd(Tensor logits, Tensor target, Tensor lse, Tensor gscale_t, double 
   check_f32(gscale_t, "gscale");
   c10::DeviceGuard g(logits.device());
   Tensor d = at::empty_like(logits);
-  CHECK_HIP_OK(pda::cross_entropy_bwd(logits.data_ptr(), is_bf16(logits), M, C,
+  const int64_t Cv = num_valid > 0 ? std::min<int64_t>(num_valid, C) : C;
+  CHECK_HIP_OK(pda::cross_entropy_bwd(logits.data_ptr(), is_bf16(logits), M, C, Cv,
                                       prob ? nullptr : target.data_ptr<int64_t>(),
                                       prob ? target.data_ptr<float>() : nullptr, ignore_index, (float)smoothing,
                                       lse.data_ptr<float>(), gscale_t.data_ptr<float>(), (float)gscale, d.data_ptr(),
@@ -517,6 +519,120 @@ std::vector<Tensor> rownorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, 
   return {dx, dgamma, dbeta};
 }
 
+// ------------------------------------------------------------------ flash attention
+void attn_check(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16, name, " must be a bf16 GPU tensor");
+  TORCH_CHECK(t.dim() == 4 && t.stride(3) == 1, name, " must be [B, T, H, D] with contiguous D");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0, name,
+              " strides must be multiples of 8 elements");
+  check_aligned16(t, name);
+}
+
+void rope_tables(pda::AttnParams& p, const c10::optional<Tensor>& cs, const c10::optional<Tensor>& sn, int T, int D) {
+  p.rope_cos = p.rope_sin = nullptr;
+  if (!cs.has_value()) return;
+  check_f32(*cs, "rope cos");
+  check_f32(*sn, "rope sin");
+  TORCH_CHECK(cs->numel() >= (int64_t)T * D / 2 && sn->numel() == cs->numel(), "rope tables must be [>=T, D/2]");
+  p.rope_cos = cs->data_ptr<float>();
+  p.rope_sin = sn->data_ptr<float>();
+}
+
+std::vector<Tensor> attn_fwd(Tensor q, Tensor k, Tensor v, double scale, bool causal, c10::optional<Tensor> rope_cos,
+                             c10::optional<Tensor> rope_sin) {
+  attn_check(q, "q");
+  attn_check(k, "k");
+  attn_check(v, "v");
+  const int B = q.size(0), T = q.size(1), Hq = q.size(2), D = q.size(3), Hkv = k.size(2);
+  TORCH_CHECK(D == 64 || D == 128, "head dim must be 64 or 128");
+  TORCH_CHECK(k.size(0) == B && k.size(1) == T && k.size(3) == D && v.sizes() == k.sizes());
+  TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0, "query heads must be a multiple of kv heads");
+  c10::DeviceGuard g(q.device());
+  Tensor o = at::empty({B, T, Hq, D}, q.options());
+  Tensor lse = at::empty({B, Hq, T}, q.options().dtype(at::kFloat));
+  pda::AttnParams p{};
+  p.q = bp(q); p.k = bp(k); p.v = bp(v); p.o = bpm(o); p.lse = lse.data_ptr<float>();
+  p.q_sb = q.stride(0); p.q_st = q.stride(1); p.q_sh = q.stride(2);
+  p.k_sb = k.stride(0); p.k_st = k.stride(1); p.k_sh = k.stride(2);
+  p.v_sb = v.stride(0); p.v_st = v.stride(1); p.v_sh = v.stride(2);
+  p.o_sb = o.stride(0); p.o_st = o.stride(1); p.o_sh = o.stride(2);
+  p.B = B; p.T = T; p.Hq = Hq; p.Hkv = Hkv; p.D = D; p.causal = causal ? 1 : 0; p.scale = (float)scale;
+  rope_tables(p, rope_cos, rope_sin, T, D);
+  CHECK_HIP_OK(pda::attention_fwd(p, stream_of(q)));
+  return {o, lse};
+}
+
+// Writes dq/dk/dv into the given tensors (any [B,T,H,D] strides, e.g. slices of a fused dQKV buffer).
+void attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor dq, Tensor dk, Tensor dv,
+              double scale, bool causal, c10::optional<Tensor> rope_cos, c10::optional<Tensor> rope_sin) {
+  for (auto* t : {&dout, &q, &k, &v, &o, &dq, &dk, &dv}) attn_check(*t, "attention tensor");
+  TORCH_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && dq.sizes() == q.sizes());
+  TORCH_CHECK(dk.sizes() == k.sizes() && dv.sizes() == v.sizes());
+  check_f32(lse, "lse");
+  const int B = q.size(0), T = q.size(1), Hq = q.size(2), D = q.size(3), Hkv = k.size(2);
+  TORCH_CHECK(D == 64 || D == 128);
+  c10::DeviceGuard g(q.device());
+  Tensor delta = at::empty({B, Hq, T}, q.options().dtype(at::kFloat));
+  pda::AttnParams p{};
+  p.q = bp(q); p.k = bp(k); p.v = bp(v); p.o = bpm(o); p.lse = lse.data_ptr<float>();
+  p.q_sb = q.stride(0); p.q_st = q.stride(1); p.q_sh = q.stride(2);
+  p.k_sb = k.stride(0); p.k_st = k.stride(1); p.k_sh = k.stride(2);
+  p.v_sb = v.stride(0); p.v_st = v.stride(1); p.v_sh = v.stride(2);
+  p.o_sb = o.stride(0); p.o_st = o.stride(1); p.o_sh = o.stride(2);
+  p.B = B; p.T = T; p.Hq = Hq; p.Hkv = Hkv; p.D = D; p.causal = causal ? 1 : 0; p.scale = (float)scale;
+  p.dout = bp(dout); p.do_sb = dout.stride(0); p.do_st = dout.stride(1); p.do_sh = dout.stride(2);
+  p.delta = delta.data_ptr<float>();
+  p.dq = bpm(dq); p.dq_sb = dq.stride(0); p.dq_st = dq.stride(1); p.dq_sh = dq.stride(2);
+  p.dk = bpm(dk); p.dk_sb = dk.stride(0); p.dk_st = dk.stride(1); p.dk_sh = dk.stride(2);
+  p.dv = bpm(dv); p.dv_sb = dv.stride(0); p.dv_st = dv.stride(1); p.dv_sh = dv.stride(2);
+  rope_tables(p, rope_cos, rope_sin, T, D);
+  CHECK_HIP_OK(pda::attention_bwd(p, stream_of(q)));
+}
+
+// ------------------------------------------------------------------ embedding / rope
+Tensor embedding_fwd(Tensor idx, Tensor table) {
+  check_gpu(idx, "idx");
+  check_bf16(table, "table");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && table.dim() == 2 && table.size(1) % 8 == 0);
+  c10::DeviceGuard g(table.device());
+  auto sizes = idx.sizes().vec();
+  sizes.push_back(table.size(1));
+  Tensor out = at::empty(sizes, table.options());
+  CHECK_HIP_OK(pda::embedding_fwd(idx.data_ptr<int64_t>(), bp(table), bpm(out), idx.numel(), table.size(1),
+                                  stream_of(table)));
+  return out;
+}
+
+// returns the table gradient in `out_dtype` (fp32 accumulate); writes into `out` when given
+Tensor embedding_bwd(Tensor idx, Tensor dy, int64_t V, c10::optional<Tensor> out) {
+  check_gpu(idx, "idx");
+  check_bf16(dy, "dy");
+  const int64_t D = dy.size(-1);
+  c10::DeviceGuard g(dy.device());
+  Tensor acc = at::zeros({V, D}, dy.options().dtype(at::kFloat));
+  CHECK_HIP_OK(pda::embedding_bwd(idx.data_ptr<int64_t>(), bp(dy), acc.data_ptr<float>(), idx.numel(), D,
+                                  stream_of(dy)));
+  Tensor res = out.has_value() ? *out : at::empty({V, D}, dy.options());
+  TORCH_CHECK(res.numel() == V * D);
+  CHECK_HIP_OK(pda::cast_scale(acc.data_ptr(), false, res.data_ptr(), is_bf16(res), V * D, 1.f, nullptr,
+                               stream_of(dy)));
+  return res;
+}
+
+Tensor rope(Tensor x_in, Tensor cs, Tensor sn, bool inverse) {
+  Tensor x = x_in.contiguous();
+  attn_check(x, "x");
+  check_f32(cs, "cos");
+  check_f32(sn, "sin");
+  const int B = x.size(0), T = x.size(1), H = x.size(2), D = x.size(3);
+  TORCH_CHECK(D % 16 == 0 && cs.numel() >= (int64_t)T * D / 2);
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty_like(x);
+  CHECK_HIP_OK(pda::rope_apply(bp(x), bpm(y), cs.data_ptr<float>(), sn.data_ptr<float>(), B, T, H, D, x.stride(0),
+                               x.stride(1), x.stride(2), inverse, stream_of(x)));
+  return y;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -549,5 +665,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("simt_gemm", &simt_gemm);
   m.def("rownorm_fwd", &rownorm_fwd);
   m.def("rownorm_bwd", &rownorm_bwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
+  m.def("rope", &rope);
   pda_rt::bind_runtime(m);
 }

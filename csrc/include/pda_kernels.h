@@ -8,6 +8,24 @@
 namespace pda {
 typedef uint16_t bf16_t;
 
+// attention tensors are [B, T, H, D] with element strides (sb, st, sh) and a contiguous head dim
+struct AttnParams {
+  const bf16_t *q, *k, *v;
+  bf16_t* o;
+  float* lse;  // [B, Hq, T] (natural log)
+  int64_t q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh;
+  int B, T, Hq, Hkv, D, causal;
+  float scale;
+  // optional fused rotary embedding (rotate-half convention) of q and k: tables [T, D/2]
+  const float *rope_cos, *rope_sin;
+  // backward
+  const bf16_t* dout;
+  int64_t do_sb, do_st, do_sh;
+  float* delta;  // [B, Hq, T] workspace
+  bf16_t *dq, *dk, *dv;
+  int64_t dq_sb, dq_st, dq_sh, dk_sb, dk_st, dk_sh, dv_sb, dv_st, dv_sh;
+};
+
 // ---- optim.hip
 hipError_t sgd_step(float* master, bf16_t* param_bf16, const void* grad, bool grad_bf16, float* mom, int64_t n,
                     float lr, float momentum, float dampening, float wd, bool nesterov, bool first, float gscale,
@@ -22,10 +40,12 @@ hipError_t cast_scale(const void* src, bool src_bf16, void* dst, bool dst_bf16, 
                       const float* scale_ptr, hipStream_t st);
 
 // ---- cross_entropy.hip
-hipError_t cross_entropy_fwd(const void* logits, bool logits_bf16, int64_t M, int64_t C, const int64_t* target_idx,
+hipError_t cross_entropy_fwd(const void* logits, bool logits_bf16, int64_t M, int64_t C, int64_t Cv,
+                             const int64_t* target_idx,
                              const float* target_prob, int64_t ignore_index, float smoothing, float* loss, float* lse,
                              hipStream_t st);
-hipError_t cross_entropy_bwd(const void* logits, bool logits_bf16, int64_t M, int64_t C, const int64_t* target_idx,
+hipError_t cross_entropy_bwd(const void* logits, bool logits_bf16, int64_t M, int64_t C, int64_t Cv,
+                             const int64_t* target_idx,
                              const float* target_prob, int64_t ignore_index, float smoothing, const float* lse,
                              const float* gscale_ptr, float gscale, void* dlogits, hipStream_t st);
 
@@ -92,5 +112,15 @@ hipError_t rownorm_fwd(const void* x, bool x_bf16, const void* gamma, const void
 hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* gamma, bool p_bf16, const float* mean,
                        const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, bool rms,
                        hipStream_t st);
+
+// ---- attention.hip (flash attention fwd / bwd, D in {64, 128}, GQA, causal or not)
+hipError_t attention_fwd(const AttnParams& p, hipStream_t st);
+hipError_t attention_bwd(const AttnParams& p, hipStream_t st);
+
+// ---- embed.hip
+hipError_t embedding_fwd(const int64_t* idx, const bf16_t* table, bf16_t* out, int64_t n, int64_t D, hipStream_t st);
+hipError_t embedding_bwd(const int64_t* idx, const bf16_t* dy, float* acc, int64_t n, int64_t D, hipStream_t st);
+hipError_t rope_apply(const bf16_t* x, bf16_t* y, const float* cos, const float* sin, int B, int T, int H, int D,
+                      int64_t sb, int64_t st_, int64_t sh, bool inverse, hipStream_t st);
 
 }  // namespace pda

@@ -1,0 +1,504 @@
+// Causal / non-causal flash attention, forward and backward, bf16 in / fp32 accumulate, GQA
+// (GPT-2 d_head 64, 16/25 heads, T=1024; Llama-3 d_head 128, 32 Q / 8 KV heads).
+//
+// Layout: q/k/v are [B, T, H, D] with arbitrary batch / time / head strides (so the q, k, v slices of a
+// fused QKV projection are consumed in place) and a contiguous head dim; outputs likewise.
+//
+// MFMA structure (v_mfma_f32_16x16x32_bf16, wave64; cdna_hip_programming.md §3 "accumulator tile as
+// the next MFMA's operand"):
+//  * S = Q K^T is computed with K as the A operand and Q as the B operand, so each lane ends up owning
+//    ONE query row (lane & 15) and 4 consecutive keys per 16-key sub-tile: row max / sum need only two
+//    cross-lane shuffles and the O rescale is a per-lane scalar.
+//  * P (bf16) feeds P*V directly from registers as the B operand, with the key order inside each 32-key
+//    k-step permuted to match the S layout; V is the A operand, read with ds_read_b64_tr_b16 (T10) from
+//    an LDS image swizzled per 32-B slot so the 8 rows a half-wave reads hit distinct banks.
+//  * K tiles for the row-wise reads use a 16-B-chunk XOR swizzle (T2) -> conflict-free ds_read_b128.
+// Backward = FA2 with recomputation, split into a dQ kernel (query-stationary) and a dK/dV kernel
+// (key-stationary, looping over the query heads of its GQA group), so no atomics are needed.
+#include "pda_common.h"
+#include "pda_kernels.h"
+
+namespace pda {
+namespace {
+
+typedef __bf16 mbf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int NT = 256;
+constexpr int BQ = 64, BKV = 64;
+constexpr float LOG2E = 1.4426950408889634f;
+
+// ---------------------------------------------------------------- LDS images (rows of D bf16)
+// row image (for ds_read_b128 of 8 consecutive columns of one row)
+template <int D>
+__device__ __forceinline__ int row_off(int row, int chunk) {
+  if constexpr (D == 128) return row * 256 + ((chunk ^ (row & 15)) << 4);
+  else return row * 128 + ((chunk ^ (row & 7)) << 4);
+}
+// transposed-read image (for ds_read_b64_tr_b16 of 4 consecutive rows x 16 columns)
+template <int D>
+__device__ __forceinline__ int tr_off(int row, int col) {
+  if constexpr (D == 128) return row * 256 + ((((col >> 4) ^ (row & 7)) & 7) << 5) + ((col & 15) << 1);
+  else return row * 128 + ((((col >> 4) ^ ((row >> 1) & 3)) & 3) << 5) + ((col & 15) << 1);
+}
+
+__device__ __forceinline__ u16x8 ld16(const bf16_t* p) { return *reinterpret_cast<const u16x8*>(p); }
+__device__ __forceinline__ u16x8 zero16() {
+  u16x8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = 0;
+  return z;
+}
+
+// Stage a [64 rows][D] tile of X (rows row0.., row stride `rs` elements) into LDS images, optionally
+// applying the rotary embedding of row position gr (rotate-half: pairs (d, d + D/2)).
+template <int D, bool ROW, bool TR>
+__device__ __forceinline__ void stage_tile(const bf16_t* __restrict__ X, int64_t rs, int row0, int T, char* row_img,
+                                           char* tr_img, const float* __restrict__ rc = nullptr,
+                                           const float* __restrict__ rsn = nullptr) {
+  constexpr int CPR = D / 8;  // 16-B chunks per row
+  if (rc == nullptr) {
+#pragma unroll
+    for (int i = 0; i < (64 * CPR) / NT; ++i) {
+      const int c = threadIdx.x + NT * i;
+      const int r = c / CPR, ch = c % CPR;
+      const int gr = row0 + r;
+      const u16x8 v = gr < T ? ld16(X + (int64_t)gr * rs + ch * 8) : zero16();
+      if (ROW) *reinterpret_cast<u16x8*>(row_img + row_off<D>(r, ch)) = v;
+      if (TR) *reinterpret_cast<u16x8*>(tr_img + tr_off<D>(r, ch * 8)) = v;
+    }
+    return;
+  }
+  constexpr int HALF = CPR / 2;
+#pragma unroll
+  for (int i = 0; i < (64 * HALF) / NT; ++i) {
+    const int c = threadIdx.x + NT * i;
+    const int r = c / HALF, ch = c % HALF;
+    const int gr = row0 + r;
+    u16x8 a = zero16(), b = zero16();
+    if (gr < T) {
+      a = ld16(X + (int64_t)gr * rs + ch * 8);
+      b = ld16(X + (int64_t)gr * rs + (ch + HALF) * 8);
+      const float* cr = rc + (int64_t)gr * (D / 2) + ch * 8;
+      const float* sr = rsn + (int64_t)gr * (D / 2) + ch * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x1 = bf2f(a[j]), x2 = bf2f(b[j]);
+        a[j] = f2bf(x1 * cr[j] - x2 * sr[j]);
+        b[j] = f2bf(x2 * cr[j] + x1 * sr[j]);
+      }
+    }
+    if (ROW) {
+      *reinterpret_cast<u16x8*>(row_img + row_off<D>(r, ch)) = a;
+      *reinterpret_cast<u16x8*>(row_img + row_off<D>(r, ch + HALF)) = b;
+    }
+    if (TR) {
+      *reinterpret_cast<u16x8*>(tr_img + tr_off<D>(r, ch * 8)) = a;
+      *reinterpret_cast<u16x8*>(tr_img + tr_off<D>(r, (ch + HALF) * 8)) = b;
+    }
+  }
+}
+
+// Rotate register fragments f[ks] / f[ks + KS/2] (columns 32 ks + 8 g + j) of sequence position `row`.
+template <int KS, int D>
+__device__ __forceinline__ void rope_frags(mbf16x8 (&f)[KS], const float* rc, const float* rsn, int row, int T,
+                                           int lane) {
+  if (rc == nullptr || row >= T) return;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < KS / 2; ++ks) {
+    const int d = 32 * ks + 8 * g;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float cs = rc[(int64_t)row * (D / 2) + d + j], sn = rsn[(int64_t)row * (D / 2) + d + j];
+      const float x1 = (float)f[ks][j], x2 = (float)f[ks + KS / 2][j];
+      f[ks][j] = (__bf16)(x1 * cs - x2 * sn);
+      f[ks + KS / 2][j] = (__bf16)(x2 * cs + x1 * sn);
+    }
+  }
+}
+
+// Gradient w.r.t. the pre-rotation input for an accumulator pair acc[dt] / acc[dt + DT/2]
+// (lane holds columns 16 dt + 4 g + r of sequence position `row`).
+template <int DT, int D>
+__device__ __forceinline__ void rope_grad_acc(f32x4 (&acc)[DT], const float* rc, const float* rsn, int row, int T,
+                                              int lane) {
+  if (rc == nullptr || row >= T) return;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int dt = 0; dt < DT / 2; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int d = 16 * dt + 4 * g + r;
+      const float cs = rc[(int64_t)row * (D / 2) + d], sn = rsn[(int64_t)row * (D / 2) + d];
+      const float g1 = acc[dt][r], g2 = acc[dt + DT / 2][r];
+      acc[dt][r] = g1 * cs + g2 * sn;
+      acc[dt + DT / 2][r] = g2 * cs - g1 * sn;
+    }
+}
+
+// A/B fragment from a row image: lane l -> row (row0 + (l & 15)), columns 32 ks + 8 (l >> 4) + j
+template <int D>
+__device__ __forceinline__ mbf16x8 frag_row(const char* img, int row0, int ks, int lane) {
+  const int r = row0 + (lane & 15);
+  return *reinterpret_cast<const mbf16x8*>(img + row_off<D>(r, ks * 4 + (lane >> 4)));
+}
+
+// A fragment via transposed reads: lane l -> column (col0 + (l & 15)) of rows
+// {k0 + 4g + q} (elements 0..3) and {k0 + 16 + 4g + q} (elements 4..7), g = l >> 4, i.e. the key
+// order produced by an S / dS accumulator pair (sub-tiles 2c, 2c+1) with k0 = 32 c.
+template <int D>
+__device__ __forceinline__ mbf16x8 frag_tr(const char* img, int k0, int col0, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const int row = k0 + 4 * g + (i >> 2);
+  const int col = col0 + 4 * (i & 3);
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + tr_off<D>(row, col)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + tr_off<D>(row + 16, col)));
+  s16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return __builtin_bit_cast(mbf16x8, f);
+}
+
+// Pack two S-layout accumulators (sub-tiles 2c, 2c+1) into a bf16 B/A fragment with permuted key order.
+__device__ __forceinline__ mbf16x8 pack_p(const f32x4& a, const f32x4& b) {
+  mbf16x8 f;
+  f[0] = (__bf16)a[0]; f[1] = (__bf16)a[1]; f[2] = (__bf16)a[2]; f[3] = (__bf16)a[3];
+  f[4] = (__bf16)b[0]; f[5] = (__bf16)b[1]; f[6] = (__bf16)b[2]; f[7] = (__bf16)b[3];
+  return f;
+}
+
+__device__ __forceinline__ mbf16x8 load_frag_global(const bf16_t* base, int64_t rs, int row, int T, int ks,
+                                                    int lane) {
+  if (row >= T) {
+    s16x8 z;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) z[j] = 0;
+    return __builtin_bit_cast(mbf16x8, z);
+  }
+  return *reinterpret_cast<const mbf16x8*>(base + (int64_t)row * rs + 32 * ks + 8 * (lane >> 4));
+}
+
+__device__ __forceinline__ f32x4 mfma(const mbf16x8& a, const mbf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------- forward
+template <int D>
+__global__ void __launch_bounds__(NT, 2) attn_fwd_kernel(AttnParams p) {
+  constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG];
+  char* Ks = smem;
+  char* Vs = smem + IMG;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int hk = h / (p.Hq / p.Hkv);
+  const int T = p.T;
+  const int qrow = qt * BQ + w * 16 + (lane & 15);
+  const bf16_t* qb = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* vb = p.v + b * p.v_sb + hk * p.v_sh;
+  mbf16x8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) qf[ks] = load_frag_global(qb, p.q_st, qrow, T, ks, lane);
+  rope_frags<KS, D>(qf, p.rope_cos, p.rope_sin, qrow, T, lane);
+  const float c = p.scale * LOG2E;
+  float m = -INFINITY, l = 0.f;
+  f32x4 o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kv_end = p.causal ? min(T, (qt + 1) * BQ) : T;
+  for (int kv0 = 0; kv0 < kv_end; kv0 += BKV) {
+    __syncthreads();
+    stage_tile<D, true, false>(kb, p.k_st, kv0, T, Ks, nullptr, p.rope_cos, p.rope_sin);
+    stage_tile<D, false, true>(vb, p.v_st, kv0, T, nullptr, Vs);
+    __syncthreads();
+    f32x4 s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) s[t] = mfma(frag_row<D>(Ks, 16 * t, ks, lane), qf[ks], s[t]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kv = kv0 + 16 * t + 4 * g + r;
+        float v = s[t][r] * c;
+        if (kv >= T || (p.causal && kv > qrow)) v = -INFINITY;
+        s[t][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m, mx);
+    const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m - m_new);
+    float rs = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = (m_new == -INFINITY) ? 0.f : exp2f(s[t][r] - m_new);
+        s[t][r] = e;
+        rs += e;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l = l * alpha + rs;
+    m = m_new;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const mbf16x8 pf = pack_p(s[2 * cc], s[2 * cc + 1]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] = mfma(frag_tr<D>(Vs, 32 * cc, 16 * dt, lane), pf, o[dt]);
+    }
+  }
+  if (qrow < T) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16_t* ob = p.o + b * p.o_sb + (int64_t)qrow * p.o_st + h * p.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      u16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][r] * inv);
+      *reinterpret_cast<u16x4*>(ob + 16 * dt + 4 * g) = v;
+    }
+    if (g == 0) p.lse[((int64_t)b * p.Hq + h) * T + qrow] = (m + log2f(l)) / LOG2E;
+  }
+}
+
+// ---------------------------------------------------------------- backward: delta = rowsum(dO * O)
+template <int D>
+__global__ void __launch_bounds__(NT) attn_bwd_delta_kernel(AttnParams p) {
+  constexpr int TPR = D / 8;  // threads per row
+  const int64_t rows = (int64_t)p.B * p.Hq * p.T;
+  const int64_t row = (int64_t)blockIdx.x * (NT / TPR) + threadIdx.x / TPR;
+  const int part = threadIdx.x % TPR;
+  float acc = 0.f;
+  if (row < rows) {
+    const int t = (int)(row % p.T);
+    const int h = (int)((row / p.T) % p.Hq);
+    const int b = (int)(row / ((int64_t)p.T * p.Hq));
+    float a[8], o[8];
+    load8(p.dout + b * p.do_sb + (int64_t)t * p.do_st + h * p.do_sh + part * 8, a);
+    load8(p.o + b * p.o_sb + (int64_t)t * p.o_st + h * p.o_sh + part * 8, o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += a[j] * o[j];
+  }
+#pragma unroll
+  for (int off = TPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (row < rows && part == 0) p.delta[row] = acc;
+}
+
+// ---------------------------------------------------------------- backward: dQ (query-stationary)
+template <int D>
+__global__ void __launch_bounds__(NT, 2) attn_bwd_dq_kernel(AttnParams p) {
+  constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[3 * IMG];
+  char* Kr = smem;
+  char* Kt = smem + IMG;
+  char* Vr = smem + 2 * IMG;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int hk = h / (p.Hq / p.Hkv);
+  const int T = p.T;
+  const int qrow = qt * BQ + w * 16 + (lane & 15);
+  const bf16_t* qb = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* dob = p.dout + b * p.do_sb + h * p.do_sh;
+  const bf16_t* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* vb = p.v + b * p.v_sb + hk * p.v_sh;
+  mbf16x8 qf[KS], df[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    qf[ks] = load_frag_global(qb, p.q_st, qrow, T, ks, lane);
+    df[ks] = load_frag_global(dob, p.do_st, qrow, T, ks, lane);
+  }
+  rope_frags<KS, D>(qf, p.rope_cos, p.rope_sin, qrow, T, lane);
+  const int64_t rowid = ((int64_t)b * p.Hq + h) * T + qrow;
+  const float lse2 = qrow < T ? p.lse[rowid] * LOG2E : 0.f;
+  const float dl = qrow < T ? p.delta[rowid] : 0.f;
+  const float c = p.scale * LOG2E;
+  f32x4 dq[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kv_end = p.causal ? min(T, (qt + 1) * BQ) : T;
+  for (int kv0 = 0; kv0 < kv_end; kv0 += BKV) {
+    __syncthreads();
+    stage_tile<D, true, true>(kb, p.k_st, kv0, T, Kr, Kt, p.rope_cos, p.rope_sin);
+    stage_tile<D, true, false>(vb, p.v_st, kv0, T, Vr, nullptr);
+    __syncthreads();
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s[t] = mfma(frag_row<D>(Kr, 16 * t, ks, lane), qf[ks], s[t]);
+        dp[t] = mfma(frag_row<D>(Vr, 16 * t, ks, lane), df[ks], dp[t]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kv = kv0 + 16 * t + 4 * g + r;
+        const bool ok = qrow < T && kv < T && !(p.causal && kv > qrow);
+        const float pr = ok ? exp2f(s[t][r] * c - lse2) : 0.f;
+        s[t][r] = pr * (dp[t][r] - dl);  // dS (unscaled)
+      }
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const mbf16x8 sf = pack_p(s[2 * cc], s[2 * cc + 1]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma(frag_tr<D>(Kt, 32 * cc, 16 * dt, lane), sf, dq[dt]);
+    }
+  }
+  rope_grad_acc<DT, D>(dq, p.rope_cos, p.rope_sin, qrow, T, lane);
+  if (qrow < T) {
+    bf16_t* out = p.dq + b * p.dq_sb + (int64_t)qrow * p.dq_st + h * p.dq_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      u16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(dq[dt][r] * p.scale);
+      *reinterpret_cast<u16x4*>(out + 16 * dt + 4 * g) = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- backward: dK, dV (key-stationary)
+template <int D>
+__global__ void __launch_bounds__(NT, 1) attn_bwd_dkdv_kernel(AttnParams p) {
+  constexpr int KS = D / 32, DT = D / 16, IMG = BQ * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + 2 * BQ * 4];
+  char* Qr = smem;
+  char* Qt = smem + IMG;
+  char* Dr = smem + 2 * IMG;
+  char* Dt = smem + 3 * IMG;
+  float* s_lse = reinterpret_cast<float*>(smem + 4 * IMG);
+  float* s_dl = s_lse + BQ;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int kt = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int T = p.T, G = p.Hq / p.Hkv;
+  const int kvrow = kt * BKV + w * 16 + (lane & 15);
+  const bf16_t* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* vb = p.v + b * p.v_sb + hk * p.v_sh;
+  mbf16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    kf[ks] = load_frag_global(kb, p.k_st, kvrow, T, ks, lane);
+    vf[ks] = load_frag_global(vb, p.v_st, kvrow, T, ks, lane);
+  }
+  rope_frags<KS, D>(kf, p.rope_cos, p.rope_sin, kvrow, T, lane);
+  const float c = p.scale * LOG2E;
+  f32x4 dk[DT], dv[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int q_begin = p.causal ? kt * BKV : 0;
+  for (int hq = hk * G; hq < (hk + 1) * G; ++hq) {
+    const bf16_t* qb = p.q + b * p.q_sb + hq * p.q_sh;
+    const bf16_t* dob = p.dout + b * p.do_sb + hq * p.do_sh;
+    const float* lse = p.lse + ((int64_t)b * p.Hq + hq) * T;
+    const float* dlt = p.delta + ((int64_t)b * p.Hq + hq) * T;
+    for (int q0 = q_begin; q0 < T; q0 += BQ) {
+      __syncthreads();
+      stage_tile<D, true, true>(qb, p.q_st, q0, T, Qr, Qt, p.rope_cos, p.rope_sin);
+      stage_tile<D, true, true>(dob, p.do_st, q0, T, Dr, Dt);
+      if (threadIdx.x < BQ) {
+        const int q = q0 + threadIdx.x;
+        s_lse[threadIdx.x] = q < T ? lse[q] * LOG2E : 0.f;
+        s_dl[threadIdx.x] = q < T ? dlt[q] : 0.f;
+      }
+      __syncthreads();
+      f32x4 s[4], dp[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          s[t] = mfma(frag_row<D>(Qr, 16 * t, ks, lane), kf[ks], s[t]);   // S^T: [q][kv = lane]
+          dp[t] = mfma(frag_row<D>(Dr, 16 * t, ks, lane), vf[ks], dp[t]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = 16 * t + 4 * g + r;
+          const int q = q0 + qi;
+          const bool ok = q < T && kvrow < T && !(p.causal && kvrow > q);
+          const float pr = ok ? exp2f(s[t][r] * c - s_lse[qi]) : 0.f;
+          s[t][r] = pr;
+          dp[t][r] = pr * (dp[t][r] - s_dl[qi]);  // dS
+        }
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        const mbf16x8 pf = pack_p(s[2 * cc], s[2 * cc + 1]);
+        const mbf16x8 sf = pack_p(dp[2 * cc], dp[2 * cc + 1]);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          dv[dt] = mfma(frag_tr<D>(Dt, 32 * cc, 16 * dt, lane), pf, dv[dt]);
+          dk[dt] = mfma(frag_tr<D>(Qt, 32 * cc, 16 * dt, lane), sf, dk[dt]);
+        }
+      }
+    }
+  }
+  rope_grad_acc<DT, D>(dk, p.rope_cos, p.rope_sin, kvrow, T, lane);
+  if (kvrow < T) {
+    bf16_t* dkp = p.dk + b * p.dk_sb + (int64_t)kvrow * p.dk_st + hk * p.dk_sh;
+    bf16_t* dvp = p.dv + b * p.dv_sb + (int64_t)kvrow * p.dv_st + hk * p.dv_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      u16x4 a, v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] = f2bf(dk[dt][r] * p.scale);
+        v[r] = f2bf(dv[dt][r]);
+      }
+      *reinterpret_cast<u16x4*>(dkp + 16 * dt + 4 * g) = a;
+      *reinterpret_cast<u16x4*>(dvp + 16 * dt + 4 * g) = v;
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t attention_fwd(const AttnParams& p, hipStream_t st) {
+  if (p.D != 64 && p.D != 128) return hipErrorInvalidValue;
+  if (p.Hkv <= 0 || p.Hq % p.Hkv) return hipErrorInvalidValue;
+  dim3 grid((p.T + BQ - 1) / BQ, p.Hq, p.B);
+  if (p.D == 128) attn_fwd_kernel<128><<<grid, NT, 0, st>>>(p);
+  else attn_fwd_kernel<64><<<grid, NT, 0, st>>>(p);
+  return hipGetLastError();
+}
+
+hipError_t attention_bwd(const AttnParams& p, hipStream_t st) {
+  if (p.D != 64 && p.D != 128) return hipErrorInvalidValue;
+  if (p.Hkv <= 0 || p.Hq % p.Hkv) return hipErrorInvalidValue;
+  const int64_t rows = (int64_t)p.B * p.Hq * p.T;
+  const int rows_per_block = NT / (p.D / 8);
+  const unsigned dgrid = (unsigned)((rows + rows_per_block - 1) / rows_per_block);
+  if (p.D == 128) attn_bwd_delta_kernel<128><<<dgrid, NT, 0, st>>>(p);
+  else attn_bwd_delta_kernel<64><<<dgrid, NT, 0, st>>>(p);
+  PDA_CHECK_HIP(hipGetLastError());
+  dim3 gq((p.T + BQ - 1) / BQ, p.Hq, p.B);
+  dim3 gk((p.T + BKV - 1) / BKV, p.Hkv, p.B);
+  if (p.D == 128) {
+    attn_bwd_dq_kernel<128><<<gq, NT, 0, st>>>(p);
+    attn_bwd_dkdv_kernel<128><<<gk, NT, 0, st>>>(p);
+  } else {
+    attn_bwd_dq_kernel<64><<<gq, NT, 0, st>>>(p);
+    attn_bwd_dkdv_kernel<64><<<gk, NT, 0, st>>>(p);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace pda

@@ -53,7 +53,7 @@ __device__ __forceinline__ void block_lse(float& m, float& s, float& a, float& b
 // Forward. Class-index targets: loss = (1-eps)(lse - x_t) + eps(lse - mean_c x_c), 0 for ignored rows.
 // Probability targets:        loss = lse * sum_c p_c - sum_c p_c x_c.
 template <typename T>
-__global__ void __launch_bounds__(kThreads) ce_fwd_kernel(const T* __restrict__ logits, int64_t C,
+__global__ void __launch_bounds__(kThreads) ce_fwd_kernel(const T* __restrict__ logits, int64_t C, int64_t Cv,
                                                           const int64_t* __restrict__ tidx,
                                                           const float* __restrict__ tprob, int64_t ignore_index,
                                                           float smoothing, float* __restrict__ loss,
@@ -70,9 +70,12 @@ __global__ void __launch_bounds__(kThreads) ce_fwd_kernel(const T* __restrict__ 
       b += p;
     }
   } else if (C % 8 == 0) {
-    for (int64_t c = (int64_t)threadIdx.x * 8; c < C; c += (int64_t)blockDim.x * 8) {
+    for (int64_t c = (int64_t)threadIdx.x * 8; c < Cv; c += (int64_t)blockDim.x * 8) {
       float v[8];
       load8(row + c, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c + j >= Cv) v[j] = -INFINITY;  // vocabulary padding
       float lm = v[0];
 #pragma unroll
       for (int j = 1; j < 8; ++j) lm = fmaxf(lm, v[j]);
@@ -80,12 +83,12 @@ __global__ void __launch_bounds__(kThreads) ce_fwd_kernel(const T* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         ls += __expf(v[j] - lm);
-        a += v[j];
+        a += (c + j < Cv) ? v[j] : 0.f;
       }
       lse_merge(m, s, lm, ls);
     }
   } else {
-    for (int64_t c = threadIdx.x; c < C; c += blockDim.x) {
+    for (int64_t c = threadIdx.x; c < Cv; c += blockDim.x) {
       const float v = Elem<T>::load(row, c);
       lse_merge(m, s, v, 1.f);
       a += v;
@@ -100,11 +103,11 @@ __global__ void __launch_bounds__(kThreads) ce_fwd_kernel(const T* __restrict__ 
       l = lse * b - a;
     } else {
       const int64_t t = tidx[r];
-      if (t == ignore_index || t < 0 || t >= C) {
+      if (t == ignore_index || t < 0 || t >= Cv) {
         l = 0.f;
       } else {
         const float xt = Elem<T>::load(row, t);
-        l = (1.f - smoothing) * (lse - xt) + smoothing * (lse - a / (float)C);
+        l = (1.f - smoothing) * (lse - xt) + smoothing * (lse - a / (float)Cv);
       }
     }
     loss[r] = l;
@@ -114,7 +117,7 @@ __global__ void __launch_bounds__(kThreads) ce_fwd_kernel(const T* __restrict__ 
 // Backward: d x_c = g * (softmax_c * S - target_c), S = sum_c p_c for probability targets (1 for
 // class indices), target_c = (1-eps)[c==t] + eps/C for class indices.
 template <typename T, typename D>
-__global__ void __launch_bounds__(kThreads) ce_bwd_kernel(const T* __restrict__ logits, int64_t C,
+__global__ void __launch_bounds__(kThreads) ce_bwd_kernel(const T* __restrict__ logits, int64_t C, int64_t Cv,
                                                           const int64_t* __restrict__ tidx,
                                                           const float* __restrict__ tprob, int64_t ignore_index,
                                                           float smoothing, const float* __restrict__ lse,
@@ -139,48 +142,51 @@ __global__ void __launch_bounds__(kThreads) ce_bwd_kernel(const T* __restrict__ 
   }
   const int64_t t = tidx[r];
   const float gr = (t == ignore_index) ? 0.f : g;
-  const float off = smoothing / (float)C, hit = 1.f - smoothing;
+  const float off = smoothing / (float)Cv, hit = 1.f - smoothing;
   if (C % 8 == 0) {
     for (int64_t c = (int64_t)threadIdx.x * 8; c < C; c += (int64_t)blockDim.x * 8) {
       float v[8];
       load8(row + c, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = gr * (__expf(v[j] - L) - ((c + j == t ? hit : 0.f) + off));
+      for (int j = 0; j < 8; ++j)
+        v[j] = (c + j < Cv) ? gr * (__expf(v[j] - L) - ((c + j == t ? hit : 0.f) + off)) : 0.f;
       store8(drow + c, v);
     }
   } else {
     for (int64_t c = threadIdx.x; c < C; c += blockDim.x) {
       const float sm = __expf(Elem<T>::load(row, c) - L);
-      Elem<D>::store(drow, c, gr * (sm - ((c == t ? hit : 0.f) + off)));
+      Elem<D>::store(drow, c, c < Cv ? gr * (sm - ((c == t ? hit : 0.f) + off)) : 0.f);
     }
   }
 }
 
 }  // namespace
 
-hipError_t cross_entropy_fwd(const void* logits, bool logits_bf16, int64_t M, int64_t C, const int64_t* target_idx,
+hipError_t cross_entropy_fwd(const void* logits, bool logits_bf16, int64_t M, int64_t C, int64_t Cv,
+                             const int64_t* target_idx,
                              const float* target_prob, int64_t ignore_index, float smoothing, float* loss, float* lse,
                              hipStream_t st) {
   if (M == 0) return hipSuccess;
   if (logits_bf16)
-    ce_fwd_kernel<bf16_t><<<(unsigned)M, kThreads, 0, st>>>((const bf16_t*)logits, C, target_idx, target_prob,
+    ce_fwd_kernel<bf16_t><<<(unsigned)M, kThreads, 0, st>>>((const bf16_t*)logits, C, Cv, target_idx, target_prob,
                                                             ignore_index, smoothing, loss, lse);
   else
-    ce_fwd_kernel<float><<<(unsigned)M, kThreads, 0, st>>>((const float*)logits, C, target_idx, target_prob,
+    ce_fwd_kernel<float><<<(unsigned)M, kThreads, 0, st>>>((const float*)logits, C, Cv, target_idx, target_prob,
                                                            ignore_index, smoothing, loss, lse);
   return hipGetLastError();
 }
 
-hipError_t cross_entropy_bwd(const void* logits, bool logits_bf16, int64_t M, int64_t C, const int64_t* target_idx,
+hipError_t cross_entropy_bwd(const void* logits, bool logits_bf16, int64_t M, int64_t C, int64_t Cv,
+                             const int64_t* target_idx,
                              const float* target_prob, int64_t ignore_index, float smoothing, const float* lse,
                              const float* gscale_ptr, float gscale, void* dlogits, hipStream_t st) {
   if (M == 0) return hipSuccess;
   if (logits_bf16)
-    ce_bwd_kernel<bf16_t, bf16_t><<<(unsigned)M, kThreads, 0, st>>>((const bf16_t*)logits, C, target_idx,
+    ce_bwd_kernel<bf16_t, bf16_t><<<(unsigned)M, kThreads, 0, st>>>((const bf16_t*)logits, C, Cv, target_idx,
                                                                     target_prob, ignore_index, smoothing, lse,
                                                                     gscale_ptr, gscale, (bf16_t*)dlogits);
   else
-    ce_bwd_kernel<float, float><<<(unsigned)M, kThreads, 0, st>>>((const float*)logits, C, target_idx, target_prob,
+    ce_bwd_kernel<float, float><<<(unsigned)M, kThreads, 0, st>>>((const float*)logits, C, Cv, target_idx, target_prob,
                                                                   ignore_index, smoothing, lse, gscale_ptr, gscale,
                                                                   (float*)dlogits);
   return hipGetLastError();

@@ -1,0 +1,154 @@
+"""GPT-2 (BASELINE configs 3 — GPT-2-medium DDP — and 5 — GPT-2-XL PP4 x DP2), on the native layers.
+
+Architecture as OpenAI GPT-2: learned token + position embeddings, pre-LN blocks (LN -> fused QKV ->
+causal attention -> proj; LN -> 4x MLP with tanh-GELU), final LN, LM head tied to the token embedding.
+MI355X-specific choices: the vocabulary table is padded to a multiple of 64 rows (50257 -> 50304) so the
+LM-head GEMMs tile cleanly, and the padded logits are excluded from the softmax by the cross-entropy
+kernel (``num_valid_classes``), so the loss equals the unpadded model's; attention consumes the fused
+QKV output in place.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, replace
+from typing import List, Optional
+
+import torch
+import torch.nn as tnn
+
+from .. import nn as pnn
+from .. import ops
+
+
+@dataclass
+class GPT2Config:
+    vocab_size: int = 50257
+    n_positions: int = 1024
+    n_embd: int = 1024
+    n_layer: int = 24
+    n_head: int = 16
+    layer_norm_eps: float = 1e-5
+    pad_vocab_multiple: int = 64
+
+    @property
+    def padded_vocab(self) -> int:
+        m = self.pad_vocab_multiple
+        return (self.vocab_size + m - 1) // m * m
+
+
+PRESETS = {
+    "gpt2": GPT2Config(n_embd=768, n_layer=12, n_head=12),
+    "gpt2-medium": GPT2Config(n_embd=1024, n_layer=24, n_head=16),
+    "gpt2-large": GPT2Config(n_embd=1280, n_layer=36, n_head=20),
+    "gpt2-xl": GPT2Config(n_embd=1600, n_layer=48, n_head=25),
+}
+
+
+def config(name: str, **overrides) -> GPT2Config:
+    return replace(PRESETS[name], **overrides)
+
+
+class GPT2Block(tnn.Module):
+    def __init__(self, cfg: GPT2Config, device=None, dtype=None):
+        super().__init__()
+        d, kw = cfg.n_embd, dict(device=device, dtype=dtype)
+        self.n_head = cfg.n_head
+        self.ln_1 = pnn.LayerNorm(d, cfg.layer_norm_eps, **kw)
+        self.c_attn = pnn.Linear(d, 3 * d, **kw)
+        self.attn_proj = pnn.Linear(d, d, **kw)
+        self.ln_2 = pnn.LayerNorm(d, cfg.layer_norm_eps, **kw)
+        self.c_fc = pnn.Linear(d, 4 * d, **kw)
+        self.mlp_proj = pnn.Linear(4 * d, d, **kw)
+
+    def forward(self, x):
+        B, T, d = x.shape
+        qkv = self.c_attn(self.ln_1(x)).view(B, T, 3 * self.n_head, d // self.n_head)
+        a = ops.attention_qkv(qkv, self.n_head, self.n_head, causal=True)
+        x = x + self.attn_proj(a.reshape(B, T, d))
+        h = ops.gelu_tanh(self.c_fc(self.ln_2(x)))
+        return x + self.mlp_proj(h)
+
+
+class GPT2(tnn.Module):
+    def __init__(self, cfg: GPT2Config, device=None, dtype=None):
+        super().__init__()
+        self.cfg = cfg
+        kw = dict(device=device, dtype=dtype)
+        self.wte = tnn.Parameter(torch.empty(cfg.padded_vocab, cfg.n_embd, **kw))
+        self.wpe = tnn.Parameter(torch.empty(cfg.n_positions, cfg.n_embd, **kw))
+        self.h = tnn.ModuleList([GPT2Block(cfg, **kw) for _ in range(cfg.n_layer)])
+        self.ln_f = pnn.LayerNorm(cfg.n_embd, cfg.layer_norm_eps, **kw)
+        self.reset_parameters()
+
+    @torch.no_grad()
+    def reset_parameters(self):
+        std = 0.02
+        self.wte.normal_(0, std)
+        self.wpe.normal_(0, std / 2)
+        for blk in self.h:
+            for lin in (blk.c_attn, blk.c_fc):
+                lin.weight.normal_(0, std)
+                lin.bias.zero_()
+            for lin in (blk.attn_proj, blk.mlp_proj):  # residual projections, GPT-2 scaling
+                lin.weight.normal_(0, std / math.sqrt(2 * self.cfg.n_layer))
+                lin.bias.zero_()
+
+    def embed(self, idx):
+        T = idx.shape[1]
+        pos = torch.arange(T, device=idx.device)
+        return ops.embedding(idx, self.wte) + ops.embedding(pos, self.wpe).unsqueeze(0)
+
+    def head(self, x, targets=None):
+        logits = ops.linear(self.ln_f(x), self.wte)
+        if targets is None:
+            return logits[..., : self.cfg.vocab_size]
+        return ops.cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1),
+                                 num_valid_classes=self.cfg.vocab_size)
+
+    def forward(self, idx, targets=None):
+        x = self.embed(idx)
+        for blk in self.h:
+            x = blk(x)
+        return self.head(x, targets)
+
+    def num_params(self, exclude_padding=True) -> int:
+        n = sum(p.numel() for p in self.parameters())
+        if exclude_padding:
+            n -= (self.cfg.padded_vocab - self.cfg.vocab_size) * self.cfg.n_embd
+        return n
+
+
+class GPT2Stage(tnn.Module):
+    """Blocks [lo, hi) of a GPT-2, plus the embedding on the first stage and LN_f + LM head + loss on
+    the last (pipeline parallel, BASELINE config 5).  The last stage's forward takes (x, targets)."""
+
+    def __init__(self, cfg: GPT2Config, lo: int, hi: int, first: bool, last: bool, device=None, dtype=None):
+        super().__init__()
+        self.cfg, self.first, self.last = cfg, first, last
+        kw = dict(device=device, dtype=dtype)
+        if first:
+            self.wte = tnn.Parameter(torch.empty(cfg.padded_vocab, cfg.n_embd, **kw).normal_(0, 0.02))
+            self.wpe = tnn.Parameter(torch.empty(cfg.n_positions, cfg.n_embd, **kw).normal_(0, 0.01))
+        self.h = tnn.ModuleList([GPT2Block(cfg, **kw) for _ in range(lo, hi)])
+        if last:
+            self.ln_f = pnn.LayerNorm(cfg.n_embd, cfg.layer_norm_eps, **kw)
+            # untied head on the last stage (the embedding lives on stage 0)
+            self.lm_head = tnn.Parameter(torch.empty(cfg.padded_vocab, cfg.n_embd, **kw).normal_(0, 0.02))
+
+    def forward(self, x):
+        if self.first:
+            T = x.shape[1]
+            x = ops.embedding(x, self.wte) + ops.embedding(torch.arange(T, device=x.device), self.wpe).unsqueeze(0)
+        for blk in self.h:
+            x = blk(x)
+        if self.last:
+            x = ops.linear(self.ln_f(x), self.lm_head)
+        return x
+
+    def loss(self, logits, targets):
+        return ops.cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1),
+                                 num_valid_classes=self.cfg.vocab_size)
+
+
+def gpt2(name: str = "gpt2-medium", device=None, dtype=None, **overrides) -> GPT2:
+    return GPT2(config(name, **overrides), device=device, dtype=dtype)

@@ -1,0 +1,114 @@
+"""Llama-3 (BASELINE config 4 — Llama-3 8B FSDP full-shard on 8 x MI355X; the reference's
+``LlamaForCausalLM`` load at `03_model_parallel.ipynb` raw lines 85-89), on the native layers.
+
+Llama-3-8B: d 4096, 32 layers, 32 query / 8 KV heads (GQA) of 128, SwiGLU FFN 14336, RMSNorm
+(eps 1e-5), RoPE theta 500000, vocab 128256, untied output head.  MI355X choices: Q, K, V are one fused
+projection (one GEMM, consumed in place by attention), gate/up are one fused projection feeding the
+SwiGLU kernel, and RoPE is applied inside the attention kernels (no rotary pass over HBM).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, replace
+
+import torch
+import torch.nn as tnn
+
+from .. import nn as pnn
+from .. import ops
+
+
+@dataclass
+class LlamaConfig:
+    vocab_size: int = 128256
+    dim: int = 4096
+    n_layers: int = 32
+    n_heads: int = 32
+    n_kv_heads: int = 8
+    ffn_dim: int = 14336
+    norm_eps: float = 1e-5
+    rope_theta: float = 500000.0
+    max_seq_len: int = 8192
+
+    @property
+    def head_dim(self) -> int:
+        return self.dim // self.n_heads
+
+
+PRESETS = {
+    "llama3-8b": LlamaConfig(),
+    "llama3-70b": LlamaConfig(dim=8192, n_layers=80, n_heads=64, n_kv_heads=8, ffn_dim=28672),
+    "llama3-tiny": LlamaConfig(vocab_size=1024, dim=256, n_layers=2, n_heads=2, n_kv_heads=1, ffn_dim=512,
+                               max_seq_len=512),
+}
+
+
+def config(name: str, **overrides) -> LlamaConfig:
+    return replace(PRESETS[name], **overrides)
+
+
+class LlamaBlock(tnn.Module):
+    def __init__(self, cfg: LlamaConfig, device=None, dtype=None):
+        super().__init__()
+        kw = dict(device=device, dtype=dtype)
+        self.cfg = cfg
+        hd = cfg.head_dim
+        self.attention_norm = pnn.RMSNorm(cfg.dim, cfg.norm_eps, **kw)
+        self.wqkv = pnn.Linear(cfg.dim, (cfg.n_heads + 2 * cfg.n_kv_heads) * hd, bias=False, **kw)
+        self.wo = pnn.Linear(cfg.n_heads * hd, cfg.dim, bias=False, **kw)
+        self.ffn_norm = pnn.RMSNorm(cfg.dim, cfg.norm_eps, **kw)
+        self.w13 = pnn.Linear(cfg.dim, 2 * cfg.ffn_dim, bias=False, **kw)  # gate | up
+        self.w2 = pnn.Linear(cfg.ffn_dim, cfg.dim, bias=False, **kw)
+
+    def forward(self, x, rope):
+        B, T, d = x.shape
+        c = self.cfg
+        qkv = self.wqkv(self.attention_norm(x)).view(B, T, c.n_heads + 2 * c.n_kv_heads, c.head_dim)
+        a = ops.attention_qkv(qkv, c.n_heads, c.n_kv_heads, causal=True, rope=rope)
+        h = x + self.wo(a.reshape(B, T, d))
+        return h + self.w2(ops.swiglu(self.w13(self.ffn_norm(h))))
+
+
+class Llama(tnn.Module):
+    def __init__(self, cfg: LlamaConfig, device=None, dtype=None):
+        super().__init__()
+        self.cfg = cfg
+        kw = dict(device=device, dtype=dtype)
+        self.tok_embeddings = tnn.Parameter(torch.empty(cfg.vocab_size, cfg.dim, **kw))
+        self.layers = tnn.ModuleList([LlamaBlock(cfg, **kw) for _ in range(cfg.n_layers)])
+        self.norm = pnn.RMSNorm(cfg.dim, cfg.norm_eps, **kw)
+        self.output = pnn.Linear(cfg.dim, cfg.vocab_size, bias=False, **kw)
+        self._rope_cache = {}
+        self.reset_parameters()
+
+    @torch.no_grad()
+    def reset_parameters(self):
+        std = 0.02
+        self.tok_embeddings.normal_(0, std)
+        for blk in self.layers:
+            for lin in (blk.wqkv, blk.w13):
+                lin.weight.normal_(0, std)
+            for lin in (blk.wo, blk.w2):
+                lin.weight.normal_(0, std / math.sqrt(2 * self.cfg.n_layers))
+        self.output.weight.normal_(0, std)
+
+    def rope(self, T: int, device):
+        key = (T, str(device))
+        if key not in self._rope_cache:
+            self._rope_cache[key] = ops.rope_tables(T, self.cfg.head_dim, self.cfg.rope_theta, device=device)
+        return self._rope_cache[key]
+
+    def forward(self, idx, targets=None):
+        T = idx.shape[1]
+        rope = self.rope(T, idx.device)
+        x = ops.embedding(idx, self.tok_embeddings)
+        for blk in self.layers:
+            x = blk(x, rope)
+        logits = self.output(self.norm(x))
+        if targets is None:
+            return logits
+        return ops.cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1))
+
+
+def llama(name: str = "llama3-8b", device=None, dtype=None, **overrides) -> Llama:
+    return Llama(config(name, **overrides), device=device, dtype=dtype)

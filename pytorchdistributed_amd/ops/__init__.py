@@ -12,3 +12,4 @@ from .pool import max_pool2d, global_avg_pool2d  # noqa: F401
 from .loss import cross_entropy  # noqa: F401
 from .act import relu, gelu_tanh, swiglu  # noqa: F401
 from .synth import fill_normal_, fill_uniform_, fill_randint_  # noqa: F401
+from .attention import attention_qkv, attention_ref, embedding, rope_tables  # noqa: F401

@@ -124,6 +124,7 @@ class DistributedDataParallel(tnn.Module):
 
     def _make_hook(self, i: int):
         def hook(p: torch.Tensor):
+            p._pda_claimed = False
             if not self.require_backward_grad_sync:
                 return
             g = self.groups[_DTYPE_IDS.get(p.dtype, 9)]

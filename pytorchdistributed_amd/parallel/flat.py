@@ -75,6 +75,11 @@ def grad_target(param: torch.Tensor) -> Optional[torch.Tensor]:
     info = getattr(param, "_pda_flat", None)
     if info is None or param.grad is not None or not param.requires_grad:
         return None
+    if getattr(param, "_pda_claimed", False):
+        # used more than once in this graph (tied weights): only the first backward writes in place,
+        # the others allocate; autograd sums them before AccumulateGrad (DDP's hook clears the claim)
+        return None
+    param._pda_claimed = True
     fg, off = info
     return fg.grad_buffer[off: off + param.numel()].view_as(param)
 

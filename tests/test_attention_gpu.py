@@ -1,0 +1,108 @@
+"""Flash-attention / embedding / RoPE kernels vs fp32 PyTorch references, and small GPT-2 / Llama
+models end to end on the native path."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("B,T,Hq,Hkv,D,causal", [(2, 128, 4, 4, 64, True), (1, 200, 4, 2, 128, True),
+                                                  (2, 64, 2, 2, 128, False), (1, 256, 8, 1, 64, True),
+                                                  (1, 96, 2, 2, 64, False)])
+@pytest.mark.parametrize("use_rope", [False, True])
+def test_flash_attention_fwd_bwd(B, T, Hq, Hkv, D, causal, use_rope):
+    from pytorchdistributed_amd.ops.attention import attention_qkv, attention_ref, rope_tables
+
+    torch.manual_seed(0)
+    qkv = torch.randn(B, T, Hq + 2 * Hkv, D).to(torch.bfloat16)
+    rope = rope_tables(T, D, 10000.0) if use_rope else None
+    ref_in = qkv.float().clone().requires_grad_()
+    q, k, v = ref_in[:, :, :Hq], ref_in[:, :, Hq:Hq + Hkv], ref_in[:, :, Hq + Hkv:]
+    o_ref = attention_ref(q, k, v, causal, 1 / math.sqrt(D), rope)
+    do = torch.randn_like(o_ref)
+    o_ref.backward(do)
+    g_in = qkv.cuda().requires_grad_()
+    rope_g = tuple(t.cuda() for t in rope) if rope is not None else None
+    o = attention_qkv(g_in, Hq, Hkv, causal=causal, rope=rope_g)
+    o.backward(do.cuda().to(torch.bfloat16))
+    assert rel_err(o.cpu(), o_ref.detach()) < 2e-2
+    g = g_in.grad.cpu().float()
+    r = ref_in.grad
+    assert rel_err(g[:, :, :Hq], r[:, :, :Hq]) < 3e-2            # dq
+    assert rel_err(g[:, :, Hq:Hq + Hkv], r[:, :, Hq:Hq + Hkv]) < 3e-2  # dk
+    assert rel_err(g[:, :, Hq + Hkv:], r[:, :, Hq + Hkv:]) < 3e-2      # dv
+
+
+def test_embedding_and_rope_kernels():
+    from pytorchdistributed_amd._native import C
+    from pytorchdistributed_amd.ops import embedding
+    from pytorchdistributed_amd.ops.attention import _rope_ref, rope_tables
+
+    torch.manual_seed(1)
+    table = torch.randn(100, 64).to(torch.bfloat16)
+    idx = torch.randint(0, 100, (3, 17))
+    tg = table.cuda().requires_grad_()
+    out = embedding(idx.cuda(), tg)
+    assert torch.equal(out.cpu(), table[idx])
+    dy = torch.randn(3, 17, 64).to(torch.bfloat16)
+    out.backward(dy.cuda())
+    ref = torch.zeros(100, 64).index_add_(0, idx.reshape(-1), dy.float().reshape(-1, 64))
+    assert rel_err(tg.grad.cpu(), ref) < 1e-2
+    x = torch.randn(2, 9, 3, 64).to(torch.bfloat16)
+    cs, sn = rope_tables(9, 64)
+    y = C().rope(x.cuda(), cs.cuda(), sn.cuda(), False)
+    assert rel_err(y.cpu(), _rope_ref(x, cs, sn)) < 1e-2
+    back = C().rope(y, cs.cuda(), sn.cuda(), True)
+    assert rel_err(back.cpu(), x) < 2e-2
+
+
+def test_gpt2_small_native_vs_reference():
+    import copy
+
+    from pytorchdistributed_amd.models.gpt2 import GPT2, config
+
+    torch.manual_seed(0)
+    cfg = config("gpt2", n_layer=2, n_embd=256, n_head=4, n_positions=128, vocab_size=1000)
+    ref = GPT2(cfg, dtype=torch.bfloat16)
+    gpu = copy.deepcopy(ref).cuda()
+    idx = torch.randint(0, 1000, (2, 128))
+    tgt = torch.randint(0, 1000, (2, 128))
+    l_ref = ref(idx, tgt)
+    l_ref.backward()
+    l = gpu(idx.cuda(), tgt.cuda())
+    l.backward()
+    assert abs(l.item() - l_ref.item()) < 2e-2
+    for n in ["wte", "h.0.c_attn.weight", "h.1.mlp_proj.weight", "ln_f.weight"]:
+        g = dict(gpu.named_parameters())[n].grad.float().cpu().flatten()
+        r = dict(ref.named_parameters())[n].grad.float().flatten()
+        assert torch.nn.functional.cosine_similarity(g, r, dim=0) > 0.98, n
+
+
+def test_llama_tiny_native_vs_reference():
+    import copy
+
+    from pytorchdistributed_amd.models.llama import Llama, config
+
+    torch.manual_seed(0)
+    cfg = config("llama3-tiny", dim=256, n_heads=2, n_kv_heads=1, ffn_dim=512)
+    ref = Llama(cfg, dtype=torch.bfloat16)
+    gpu = copy.deepcopy(ref).cuda()
+    gpu._rope_cache = {}
+    idx = torch.randint(0, cfg.vocab_size, (2, 128))
+    tgt = torch.randint(0, cfg.vocab_size, (2, 128))
+    l_ref = ref(idx, tgt)
+    l_ref.backward()
+    l = gpu(idx.cuda(), tgt.cuda())
+    l.backward()
+    assert abs(l.item() - l_ref.item()) < 2e-2
+    for n in ["tok_embeddings", "layers.0.wqkv.weight", "layers.1.w13.weight", "output.weight"]:
+        g = dict(gpu.named_parameters())[n].grad.float().cpu().flatten()
+        r = dict(ref.named_parameters())[n].grad.float().flatten()
+        assert torch.nn.functional.cosine_similarity(g, r, dim=0) > 0.98, n

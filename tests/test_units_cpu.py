@@ -197,3 +197,29 @@ def test_cpu_ops_match_torch():
     p = ops.max_pool2d(x)
     assert p.shape == (2, 5, 5, 16)
     assert torch.allclose(ops.global_avg_pool2d(x), x.mean((1, 2)))
+
+
+def test_transformer_models_cpu():
+    from pytorchdistributed_amd.models.gpt2 import GPT2, GPT2Stage, config as gcfg
+    from pytorchdistributed_amd.models.llama import Llama, config as lcfg
+
+    g = GPT2(gcfg("gpt2", n_layer=2, n_embd=64, n_head=2, n_positions=32, vocab_size=100))
+    idx = torch.randint(0, 100, (2, 32))
+    loss = g(idx, idx)
+    loss.backward()
+    assert g.cfg.padded_vocab == 128 and g.wte.grad[100:].abs().sum() == 0  # padded rows get no gradient
+    assert torch.isfinite(loss)
+    full = gcfg("gpt2-medium")
+    assert GPT2(gcfg("gpt2", n_layer=1, n_embd=64, n_head=2), device="meta").num_params() > 0
+    # GPT-2 medium / XL and Llama-3-8B parameter counts (standard architectures)
+    gm = GPT2(full, device="meta")
+    assert abs(gm.num_params() - 354.8e6) / 354.8e6 < 0.01
+    gx = GPT2(gcfg("gpt2-xl"), device="meta")
+    assert abs(gx.num_params() - 1.558e9) / 1.558e9 < 0.01
+    lm = Llama(lcfg("llama3-8b"), device="meta")
+    assert abs(sum(p.numel() for p in lm.parameters()) - 8.03e9) / 8.03e9 < 0.01
+    tl = Llama(lcfg("llama3-tiny", dim=64, n_heads=2, n_kv_heads=1, ffn_dim=128))
+    out = tl(torch.randint(0, 1024, (2, 16)), torch.randint(0, 1024, (2, 16)))
+    out.backward()
+    st = GPT2Stage(gcfg("gpt2", n_layer=4, n_embd=64, n_head=2, vocab_size=100), 0, 2, True, False)
+    assert st(idx).shape == (2, 32, 64)
