@@ -1,0 +1,69 @@
+"""BASELINE config 5: GPT-2-XL pipeline-parallel 4 stages x DDP 2 (RCCL send/recv micro-batches).
+
+    python -m torch.distributed.run --nproc-per-node 8 -m pytorchdistributed_amd.bench.gpt2xl_pp --gpus 8
+World = pp x dp (default pp = min(4, world)); 1F1B schedule; per-stage gradient averaging over the DP
+group after the pipeline flush; fused AdamW per stage.
+"""
+from __future__ import annotations
+
+import argparse
+
+import torch
+
+from ..data.device import DeviceSyntheticTokens
+from ..models.gpt2 import GPT2Stage, config
+from ..optim import AdamW
+from ..parallel.pipeline import Pipeline, dp_sync_grads, partition_layers, pp_dp_groups
+from .common import emit, setup, teardown, timed
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="gpt2-xl")
+    ap.add_argument("--pp", type=int, default=None)
+    ap.add_argument("--micro", type=int, default=8, help="micro-batches per step")
+    ap.add_argument("--micro-batch", type=int, default=4)
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--schedule", default="1f1b")
+    ap.add_argument("--layers", type=int, default=None)
+    a = ap.parse_args(argv)
+    rank, world, local, device = setup(a.gpus)
+    pp = a.pp or min(4, world)
+    dp = world // pp
+    cfg = config(a.model, **({} if a.layers is None else {"n_layer": a.layers}))
+    if world > 1:
+        pp_group, dp_group, stage, dp_rank, ranks = pp_dp_groups(pp, dp)
+    else:
+        pp_group = dp_group = None
+        stage, dp_rank, ranks = 0, 0, [0]
+    lo, hi = partition_layers(cfg.n_layer, pp)[stage]
+    torch.manual_seed(stage)
+    mod = GPT2Stage(cfg, lo, hi, stage == 0, stage == pp - 1, device=device, dtype=torch.bfloat16)
+    opt = AdamW(mod.parameters(), lr=1e-4, weight_decay=0.1)
+    pipe = Pipeline(mod, ranks, a.micro, schedule=a.schedule, loss_fn=mod.loss if stage == pp - 1 else None,
+                    group=pp_group, device=device)
+    data = DeviceSyntheticTokens(a.micro * a.micro_batch, a.seq, cfg.vocab_size, device=device, rank=dp_rank)
+
+    def step():
+        x, y = data.next()
+        opt.zero_grad(set_to_none=True)
+        pipe.step(x, y)
+        dp_sync_grads(mod, dp_group)
+        opt.step()
+
+    secs = timed(step, a.steps, a.warmup)
+    toks = a.micro * a.micro_batch * a.seq * dp * a.steps / secs
+    emit({"metric": "tokens/sec (whole job) GPT-2-XL pipeline x DDP", "value": round(toks, 1),
+          "unit": "tokens/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+          "ms_per_step": round(secs / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+          "vs_baseline": None, "dtype": "bf16", "data": "synthetic tokens (on-device), random-init weights",
+          "config": {"model": a.model, "global_batch": a.micro * a.micro_batch * dp, "seq_len": a.seq,
+                     "parallelism": f"pp{pp}xdp{dp}", "schedule": a.schedule, "microbatches": a.micro}}, rank)
+    teardown()
+
+
+if __name__ == "__main__":
+    main()

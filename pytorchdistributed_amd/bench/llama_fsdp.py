@@ -1,0 +1,59 @@
+"""BASELINE config 4: Llama-3 8B FSDP full-shard, tokens/sec (whole job).
+
+    python -m torch.distributed.run --nproc-per-node 8 -m pytorchdistributed_amd.bench.llama_fsdp --gpus 8
+Units = transformer blocks (436 MB bf16 all-gather per block in forward and again in backward, one
+reduce-scatter per block), prefetch of the next block's all-gather, fused AdamW on the fp32 shards.
+"""
+from __future__ import annotations
+
+import argparse
+
+import torch
+
+from ..data.device import DeviceSyntheticTokens
+from ..models.llama import Llama, LlamaBlock, config
+from ..optim import AdamW
+from ..parallel.fsdp import FullyShardedDataParallel
+from .common import emit, setup, teardown, timed
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--batch", type=int, default=1, help="per-GPU sequences")
+    ap.add_argument("--seq", type=int, default=4096)
+    ap.add_argument("--layers", type=int, default=None, help="override depth (smoke runs only)")
+    a = ap.parse_args(argv)
+    rank, world, local, device = setup(a.gpus)
+    over = {} if a.layers is None else {"n_layers": a.layers}
+    torch.manual_seed(0)
+    model = Llama(config(a.model, **over), device=device, dtype=torch.bfloat16)
+    n_params = sum(p.numel() for p in model.parameters())
+    fsdp = FullyShardedDataParallel(model, unit_types=(LlamaBlock,))
+    opt = AdamW(fsdp.parameters(), lr=3e-4, weight_decay=0.1)
+    data = DeviceSyntheticTokens(a.batch, a.seq, model.cfg.vocab_size, device=device, rank=rank)
+
+    def step():
+        x, y = data.next()
+        opt.zero_grad(set_to_none=True)
+        loss = fsdp(x, y)
+        loss.backward()
+        opt.step()
+
+    secs = timed(step, a.steps, a.warmup)
+    toks = a.batch * a.seq * world * a.steps / secs
+    emit({"metric": "tokens/sec (whole job) Llama-3 FSDP full-shard", "value": round(toks, 1),
+          "unit": "tokens/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+          "ms_per_step": round(secs / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+          "vs_baseline": None, "dtype": "bf16", "data": "synthetic tokens (on-device), random-init weights",
+          "config": {"model": a.model + ("" if a.layers is None else f"-{a.layers}L"),
+                     "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": f"fsdp{world}",
+                     "params": n_params}}, rank)
+    teardown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,106 @@
+"""Reproduction of the reference's own benchmark (`03 模型并行/03_model_parallel.ipynb` raw lines 369-624;
+numbers in BASELINE.md): ResNet-50, ``train(model)`` = 3 Adam steps on fresh 120 x 3x128x128 batches
+with one-hot soft targets, timed with ``timeit.repeat(number=1, repeat=10)``.
+
+Modes:
+* ``parity`` — the reference's methodology: CPU data generation + pageable host->device copies inside
+  the timed call, a new Adam optimizer per call; we add a final device synchronize (the reference
+  stops its timer with kernels still queued) so the number is honest.
+* ``clean``  — data generated on device, optimizer reused, HIP-event/synchronize bracketed.
+Variants: ``single`` (1 device), ``mp`` (layer split, stem..layer2 on dev0, rest on dev1), ``pp``
+(micro-batch pipeline, ``--split-size``), ``sweep`` (pp over the reference's split sizes).
+Precision: bf16 compute with fp32 master weights (the reference ran fp32/TF32 on A100).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import timeit
+
+import numpy as np
+import torch
+
+from ..data.datasets import random_image_batch
+from ..data.device import DeviceSyntheticImages
+from ..models.resnet import resnet50
+from ..ops import cross_entropy
+from ..optim import Adam
+from ..parallel.model_parallel import ModelParallelResNet50, PipelineParallelResNet50
+
+REFERENCE_S = {"single": 0.248, "mp": 0.272, "pp20": 0.454,
+               "sweep": {1: 4.88, 3: 1.84, 5: 1.16, 8: 0.81, 10: 0.71, 12: 0.62, 20: 0.47, 40: 0.33, 60: 0.29}}
+SPLITS = [1, 3, 5, 8, 10, 12, 20, 40, 60]
+
+
+def make_model(kind, devs, split=20):
+    if kind == "single":
+        return resnet50(device=devs[0], dtype=torch.bfloat16), devs[0]
+    base = resnet50(dtype=torch.bfloat16)
+    if kind == "mp":
+        return ModelParallelResNet50(base, devices=devs), devs[1]
+    return PipelineParallelResNet50(base, devices=devs, split_size=split), devs[1]
+
+
+def run(kind, devs, mode, split=20, repeat=10, batch=120, size=128):
+    model, out_dev = make_model(kind, devs, split)
+    in_dev = devs[0]
+    dev_data = DeviceSyntheticImages(batch, size, 1000, device=in_dev, seed=0) if mode == "clean" else None
+    opt_holder = {}
+
+    def train():
+        model.train()
+        opt = Adam(model.parameters(), lr=1e-3) if mode == "parity" else opt_holder.setdefault(
+            "o", Adam(model.parameters(), lr=1e-3))
+        for _ in range(3):
+            if mode == "parity":
+                inputs, labels = random_image_batch(batch, (size, size), 1000)
+                x = inputs.to(in_dev).permute(0, 2, 3, 1).to(torch.bfloat16)
+                y = labels.to(out_dev)
+            else:
+                x, yi = dev_data.next()
+                y = yi.to(out_dev)
+            opt.zero_grad()
+            out = model(x)
+            loss = cross_entropy(out, y)
+            loss.backward()
+            opt.step()
+        torch.cuda.synchronize()
+
+    train()  # warm-up (the reference's first timeit repeat includes it; we exclude compile/alloc effects)
+    times = timeit.repeat(train, number=1, repeat=repeat)
+    return float(np.mean(times)), float(np.std(times))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="single,mp,pp")
+    ap.add_argument("--mode", default="parity", choices=["parity", "clean"])
+    ap.add_argument("--devices", default=None, help="comma list, e.g. 0,1 (default: 0,1 if 2 GPUs else 0,0)")
+    ap.add_argument("--split-size", type=int, default=20)
+    ap.add_argument("--repeat", type=int, default=10)
+    ap.add_argument("--sweep", action="store_true")
+    a = ap.parse_args(argv)
+    n = torch.cuda.device_count()
+    devs = [int(d) for d in a.devices.split(",")] if a.devices else ([0, 1] if n >= 2 else [0, 0])
+    devs = [torch.device("cuda", d) for d in devs]
+    results = {}
+    for v in a.variants.split(","):
+        m, s = run(v, devs, a.mode, a.split_size, a.repeat)
+        key = "pp20" if v == "pp" and a.split_size == 20 else v
+        ref = REFERENCE_S.get(key)
+        results[v] = {"mean_s": round(m, 4), "std_s": round(s, 4), "img_per_s": round(360 / m, 1),
+                      "reference_s_A100": ref, "speedup_vs_reference": round(ref / m, 2) if ref else None}
+    if a.sweep:
+        sw = {}
+        for sp in SPLITS:
+            m, s = run("pp", devs, a.mode, sp, a.repeat)
+            ref = REFERENCE_S["sweep"][sp]
+            sw[sp] = {"mean_s": round(m, 4), "std_s": round(s, 4), "reference_s_A100": ref,
+                      "speedup_vs_reference": round(ref / m, 2)}
+        results["sweep"] = sw
+    print(json.dumps({"benchmark": "NB03 ResNet-50 train() (3 Adam steps x 120 imgs @128px)", "mode": a.mode,
+                      "devices": [str(d) for d in devs], "dtype": "bf16 (fp32 masters)", "results": results}))
+
+
+if __name__ == "__main__":
+    main()

@@ -86,8 +86,6 @@ class PipelineParallelResNet50(ModelParallelResNet50):
 
     def forward(self, x):
         splits = x.split(self.split_size, dim=0)
-        n = x.shape[0]
-        out = None
         s0, s1 = self._stream(self.dev0), self._stream(self.dev1)
         if s0 is None or s1 is None:  # CPU devices: sequential reference semantics
             outs = [self.head(self.seq2(self.seq1(s.to(self.dev0)).to(self.dev1))) for s in splits]
@@ -104,20 +102,15 @@ class PipelineParallelResNet50(ModelParallelResNet50):
                 ev = torch.cuda.Event()
                 ev.record(s0)
                 handoff.append((a, ev))
-        start = 0
+        outs = []
         with torch.cuda.stream(s1):
             for a, ev in handoff:
                 s1.wait_event(ev)
                 a1 = a.to(self.dev1, non_blocking=True)
-                y = self.head(self.seq2(a1))
-                if out is None:
-                    out = torch.empty((n,) + tuple(y.shape[1:]), device=self.dev1, dtype=y.dtype)
-                    out = out.clone()  # keep autograd happy for the slice writes below
-                out = out.index_copy(0, torch.arange(start, start + y.shape[0], device=self.dev1), y)
-                start += y.shape[0]
+                outs.append(self.head(self.seq2(a1)))
         cur0.wait_stream(s0)
         cur1.wait_stream(s1)
-        return out
+        return torch.cat(outs)
 
 
 def auto_place(model: tnn.Module, max_memory: Optional[Dict] = None, devices: Optional[Sequence] = None,
