@@ -42,23 +42,29 @@ def test_resnet50_native_matches_reference():
     with torch.no_grad():
         assert rel_err(gpu(x.to("cuda", torch.bfloat16)).cpu(), ref(x.to(torch.bfloat16))) < 5e-2
     # backward, block by block (a composed check without the chaotic amplification of 50 random layers):
-    # a downsampling bottleneck and a strided one, fp32 reference vs the native bf16 path
+    # a downsampling bottleneck and a strided one.  Oracle: fp32 reference; the bound is set by the same
+    # block run in bf16 on the CPU reference ops (batch-statistics BN backward over tiny maps loses ~6 %
+    # to bf16 rounding alone), so the native path must be no worse than 1.5x plain bf16 rounding.
     for bi, blk_ref in [(0, ref.layer1[0]), (1, ref.layer2[0]), (2, ref.layer4[0])]:
         blk_ref = blk_ref.float().train()
         blk_gpu = copy.deepcopy(blk_ref).to("cuda", torch.bfloat16)
+        blk_b16 = copy.deepcopy(blk_ref).to(torch.bfloat16)
         cin = blk_ref.conv1.in_channels
         hw = {0: 16, 1: 16, 2: 8}[bi]
         xin = torch.randn(4, hw, hw, cin).to(torch.bfloat16).float().requires_grad_()
         out_r = blk_ref(xin)
         dy = torch.randn_like(out_r).to(torch.bfloat16).float()
         out_r.backward(dy)
+        xb = xin.detach().to(torch.bfloat16).requires_grad_()
+        blk_b16(xb).backward(dy.to(torch.bfloat16))
         xg = xin.detach().to("cuda", torch.bfloat16).requires_grad_()
         out_g = blk_gpu(xg)
         out_g.backward(dy.to("cuda", torch.bfloat16))
         assert rel_err(out_g.cpu(), out_r.detach()) < 3e-2
-        assert rel_err(xg.grad.cpu(), xin.grad) < 5e-2
-        for (n, pr), (_, pg) in zip(blk_ref.named_parameters(), blk_gpu.named_parameters()):
-            assert rel_err(pg.grad.cpu(), pr.grad) < 5e-2, (bi, n)
+        assert rel_err(xg.grad.cpu(), xin.grad) < max(2e-2, 1.5 * rel_err(xb.grad, xin.grad)), bi
+        for (n, pr), (_, pg), (_, pb) in zip(blk_ref.named_parameters(), blk_gpu.named_parameters(),
+                                             blk_b16.named_parameters()):
+            assert rel_err(pg.grad.cpu(), pr.grad) < max(2e-2, 1.5 * rel_err(pb.grad, pr.grad)), (bi, n)
 
 
 def test_ddp_fused_sgd_step_single_rank():

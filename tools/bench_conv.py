@@ -1,0 +1,100 @@
+"""Per-shape TFLOP/s of the native MFMA GEMM / implicit-GEMM conv kernels vs the vendor libraries
+(hipBLASLt through torch.matmul, MIOpen through F.conv2d channels-last) on the ResNet-50 bs-256
+layer shapes.  Prints one JSON line per (shape, op).
+
+    python tools/bench_conv.py [--batch 256] [--iters 20] [--torch]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+
+import torch
+import torch.nn.functional as F
+
+from pytorchdistributed_amd._native import C
+
+# (H, Cin, Cout, R, stride) for every distinct ResNet-50 conv (input spatial size H)
+RESNET_CONVS = [
+    (224, 8, 64, 7, 2),
+    (56, 64, 64, 1, 1), (56, 64, 64, 3, 1), (56, 64, 256, 1, 1), (56, 256, 64, 1, 1),
+    (56, 256, 128, 1, 1), (56, 128, 128, 3, 2), (28, 128, 512, 1, 1), (56, 256, 512, 1, 2),
+    (28, 512, 128, 1, 1), (28, 128, 128, 3, 1),
+    (28, 512, 256, 1, 1), (28, 256, 256, 3, 2), (14, 256, 1024, 1, 1), (28, 512, 1024, 1, 2),
+    (14, 1024, 256, 1, 1), (14, 256, 256, 3, 1),
+    (14, 1024, 512, 1, 1), (14, 512, 512, 3, 2), (7, 512, 2048, 1, 1), (14, 1024, 2048, 1, 2),
+    (7, 2048, 512, 1, 1), (7, 512, 512, 3, 1),
+]
+# how many times each shape appears in one ResNet-50 forward
+COUNT = [1, 1, 3, 4, 2, 1, 1, 4, 1, 3, 3, 1, 1, 6, 1, 5, 5, 1, 1, 3, 1, 2, 2]
+
+
+def time_fn(fn, iters):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--torch", action="store_true", help="also time MIOpen / hipBLASLt")
+    a = ap.parse_args()
+    c = C()
+    dev = "cuda"
+    for M, N, K in [(4096, 4096, 4096), (8192, 8192, 8192)]:
+        A = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+        B = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ms = time_fn(lambda: c.gemm(A, True, K, B, True, K, out, N, M, N, K, None, False, False), a.iters)
+        rec = {"op": "gemm", "shape": [M, N, K], "ms": round(ms, 4), "tflops": round(2 * M * N * K / ms / 1e9, 1)}
+        if a.torch:
+            mt = time_fn(lambda: torch.matmul(A, B.t()), a.iters)
+            rec["torch_ms"] = round(mt, 4)
+            rec["torch_tflops"] = round(2 * M * N * K / mt / 1e9, 1)
+        print(json.dumps(rec), flush=True)
+    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    tot_t = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    for (H, Ci, Co, R, st), cnt in zip(RESNET_CONVS, COUNT):
+        pad = R // 2
+        P = (H + 2 * pad - R) // st + 1
+        x = torch.randn(a.batch, H, H, Ci, device=dev, dtype=torch.bfloat16)
+        w = torch.randn(Co, R, R, Ci, device=dev, dtype=torch.bfloat16) * 0.05
+        dy = torch.randn(a.batch, P, P, Co, device=dev, dtype=torch.bfloat16)
+        dwo = torch.empty(Co, R, R, Ci, device=dev, dtype=torch.float32)
+        flops = 2.0 * a.batch * P * P * Co * R * R * Ci
+        fns = {"fwd": lambda: c.conv_fwd(x, w, st, pad, 1, None, False),
+               "dgrad": lambda: c.conv_dgrad(dy, w, H, H, st, pad, 1),
+               "wgrad": lambda: c.conv_wgrad(dy, x, R, R, st, pad, 1, True, dwo)}
+        rec = {"op": "conv", "H": H, "Cin": Ci, "Cout": Co, "R": R, "stride": st, "count": cnt}
+        for k, fn in fns.items():
+            ms = time_fn(fn, a.iters)
+            tot[k] += ms * cnt
+            rec[k + "_ms"] = round(ms, 4)
+            rec[k + "_tflops"] = round(flops / ms / 1e9, 1)
+        if a.torch:
+            xt = x.permute(0, 3, 1, 2)
+            wt = w.permute(0, 3, 1, 2)
+            dyt = dy.permute(0, 3, 1, 2)
+            tf = {"fwd": lambda: F.conv2d(xt, wt, None, st, pad),
+                  "dgrad": lambda: torch.nn.grad.conv2d_input(xt.shape, wt, dyt, st, pad),
+                  "wgrad": lambda: torch.nn.grad.conv2d_weight(xt, wt.shape, dyt, st, pad)}
+            for k, fn in tf.items():
+                ms = time_fn(fn, a.iters)
+                tot_t[k] += ms * cnt
+                rec["torch_" + k + "_ms"] = round(ms, 4)
+        print(json.dumps(rec), flush=True)
+    print(json.dumps({"op": "total_per_step_ms", "ours": {k: round(v, 3) for k, v in tot.items()},
+                      "torch": {k: round(v, 3) for k, v in tot_t.items()} if a.torch else None}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
