@@ -376,7 +376,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   TORCH_CHECK(w.size(0) == Cout && C % 8 == 0 && Cout % 8 == 0);
   c10::DeviceGuard g(dy.device());
   Tensor wt = at::empty({C, R, S, Cout}, w.options());
-  CHECK_HIP_OK(pda::conv_weight_transpose(bp(w), bpm(wt), Cout, R * S, C, stream_of(dy)));
+  CHECK_HIP_OK(pda::conv_weight_transpose(bp(w), bpm(wt), Cout, R, S, C, stride, pad, dil, stream_of(dy)));
   Tensor dx = at::empty({N, H, W, C}, dy.options());
   CHECK_HIP_OK(pda::conv2d_dgrad(bp(dy), bp(wt), bpm(dx), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
                                  stream_of(dy)));
@@ -458,7 +458,14 @@ Tensor colsum(Tensor x) {
   const int64_t cols = x.size(-1), rows = x.numel() / cols;
   c10::DeviceGuard g(x.device());
   Tensor out = at::empty({cols}, x.options().dtype(at::kFloat));
-  CHECK_HIP_OK(pda::colsum(x.data_ptr(), is_bf16(x), out.data_ptr<float>(), rows, cols, stream_of(x)));
+  if (cols % 8 != 0 || !x.is_contiguous()) {
+    Tensor xc = x.contiguous();
+    CHECK_HIP_OK(pda::colsum_unaligned(xc.data_ptr(), is_bf16(x), out.data_ptr<float>(), rows, cols, stream_of(x)));
+    return out;
+  }
+  Tensor ws = at::empty({pda::colreduce_ws_floats(rows, cols, 1)}, x.options().dtype(at::kFloat));
+  CHECK_HIP_OK(pda::colsum(x.data_ptr(), is_bf16(x), out.data_ptr<float>(), rows, cols, ws.data_ptr<float>(),
+                           stream_of(x)));
   return out;
 }
 
@@ -513,9 +520,11 @@ std::vector<Tensor> rownorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, 
   Tensor dx = at::empty_like(x);
   auto fo = x.options().dtype(at::kFloat);
   Tensor dgamma = at::empty({D}, fo), dbeta = at::empty({D}, fo);
+  Tensor ws = at::empty({pda::colreduce_ws_floats(rows, D, rms ? 1 : 2)}, fo);
   CHECK_HIP_OK(pda::rownorm_bwd(dy.data_ptr(), x.data_ptr(), is_bf16(x), gamma.data_ptr(), is_bf16(gamma),
                                 rms ? nullptr : mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(),
-                                dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), rows, D, rms, stream_of(x)));
+                                dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), rows, D, rms, ws.data_ptr<float>(),
+                                stream_of(x)));
   return {dx, dgamma, dbeta};
 }
 

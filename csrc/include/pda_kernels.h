@@ -91,7 +91,9 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int N, i
 hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32, int N, int H, int W, int C,
                         int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, float* slab,
                         hipStream_t st);
-hipError_t conv_weight_transpose(const bf16_t* w, bf16_t* wt, int Cout, int RS, int Cin, hipStream_t st);
+// wt = w transposed to [Cin][taps][Cout], phase-packed for the stride-decomposed dgrad
+hipError_t conv_weight_transpose(const bf16_t* w, bf16_t* wt, int Cout, int R, int S, int Cin, int stride, int pad,
+                                 int dil, hipStream_t st);
 
 
 // ---- act.hip (op: 0 relu, 1 gelu_tanh)
@@ -99,7 +101,7 @@ hipError_t act_fwd(const void* x, void* y, bool bf16, int64_t n, int op, hipStre
 hipError_t act_bwd(const void* dy, const void* ref, void* dx, bool bf16, int64_t n, int op, hipStream_t st);
 hipError_t swiglu_fwd(const void* gu, void* y, bool bf16, int64_t rows, int64_t F, hipStream_t st);
 hipError_t swiglu_bwd(const void* dy, const void* gu, void* dgu, bool bf16, int64_t rows, int64_t F, hipStream_t st);
-hipError_t colsum(const void* x, bool bf16, float* out, int64_t rows, int64_t cols, hipStream_t st);
+hipError_t colsum_unaligned(const void* x, bool bf16, float* out, int64_t rows, int64_t cols, hipStream_t st);
 
 // ---- simt_gemm.hip (dtype codes 0 fp32 / 1 bf16; arbitrary strides)
 hipError_t simt_gemm(const void* A, int a_dt, int64_t sam, int64_t sak, const void* B, int b_dt, int64_t sbk,
@@ -111,7 +113,10 @@ hipError_t rownorm_fwd(const void* x, bool x_bf16, const void* gamma, const void
                        float* mean, float* rstd, int64_t rows, int64_t D, float eps, bool rms, hipStream_t st);
 hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* gamma, bool p_bf16, const float* mean,
                        const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, bool rms,
-                       hipStream_t st);
+                       float* ws, hipStream_t st);
+// column sums via slab partials (cols % 8 == 0); ws holds colreduce_ws_floats(rows, cols, 1) floats
+hipError_t colsum(const void* x, bool bf16, float* out, int64_t rows, int64_t cols, float* ws, hipStream_t st);
+int64_t colreduce_ws_floats(int64_t rows, int64_t D, int nout);
 
 // ---- attention.hip (flash attention fwd / bwd, D in {64, 128}, GQA, causal or not)
 hipError_t attention_fwd(const AttnParams& p, hipStream_t st);

@@ -154,7 +154,7 @@ hipError_t swiglu_bwd(const void* dy, const void* gu, void* dgu, bool bf16, int6
   return hipGetLastError();
 }
 
-hipError_t colsum(const void* x, bool bf16, float* out, int64_t rows, int64_t cols, hipStream_t st) {
+hipError_t colsum_unaligned(const void* x, bool bf16, float* out, int64_t rows, int64_t cols, hipStream_t st) {
   PDA_CHECK_HIP(hipMemsetAsync(out, 0, cols * sizeof(float), st));
   const int64_t rpb = 256;
   dim3 grid((unsigned)((cols + kThreads - 1) / kThreads), (unsigned)((rows + rpb - 1) / rpb));

@@ -240,6 +240,66 @@ struct ConvDgradK {
   }
 };
 
+// Conv dgrad A operand, stride-decomposed (dil == 1 or stride == 1): the rows of one launch are the
+// dx pixels of ONE output phase (h = hh*st + ph, w = ww*st + pw), and K runs over only the taps that
+// reach that phase (r = r0 + ri*st) — no zero taps are gathered, unlike the folded form above (a
+// stride-2 3x3 dgrad wastes 3/4 of its MFMA work there).  p = hh + base_r - ri*step_r (step_r = dil
+// for stride 1, 1 otherwise); likewise q.  dy has dims [N,P,Q,Cg]; k = (ri, si, co).
+struct PhaseGeom {
+  int Hh, Wh, Sv;
+  int base_r, step_r, base_s, step_s;
+  FastDiv fWh, fHh, fSv;
+};
+
+template <int R>
+struct ConvDgradPhaseK {
+  static constexpr bool kMajor = true;
+  static constexpr int NCH = R / 32;
+  const bf16_t* dy;
+  ConvGeom g;
+  PhaseGeom ph;
+  int64_t M, K;
+  struct State {
+    int nP[NCH], hh[NCH], ww[NCH];
+    bool ok[NCH];
+    int kc;
+  };
+  __device__ void init(State& s, int64_t row0, int tid) const {
+    s.kc = (tid & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int64_t m = row0 + (tid >> 3) + 32 * i;
+      s.ok[i] = m < M;
+      const uint32_t mm = s.ok[i] ? (uint32_t)m : 0u;
+      const uint32_t t = fdiv(mm, ph.fWh);
+      s.ww[i] = (int)(mm - t * ph.Wh);
+      const uint32_t n = fdiv(t, ph.fHh);
+      s.hh[i] = (int)(t - n * ph.Hh);
+      s.nP[i] = (int)n * g.P;
+    }
+  }
+  __device__ void fetch(const State& s, int64_t k0, u16x8 (&v)[NCH]) const {
+    const int64_t k = k0 + s.kc;
+    if (k >= K) {
+#pragma unroll
+      for (int i = 0; i < NCH; ++i) v[i] = zero8();
+      return;
+    }
+    const uint32_t t = fdiv((uint32_t)k, g.fC);  // fC divides by Cg (= Cout) here
+    const int co = (int)((uint32_t)k - t * g.Cg);
+    const uint32_t ri = fdiv(t, ph.fSv);
+    const int si = (int)(t - ri * ph.Sv);
+    const int dr = ph.base_r - (int)ri * ph.step_r, ds = ph.base_s - si * ph.step_s;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int p = s.hh[i] + dr, q = s.ww[i] + ds;
+      const bool ok = s.ok[i] && (unsigned)p < (unsigned)g.P && (unsigned)q < (unsigned)g.Q;
+      const int64_t off = ((int64_t)(s.nP[i] + p) * g.Q + q) * g.Cg + co;
+      v[i] = ok ? *reinterpret_cast<const u16x8*>(dy + off) : zero8();
+    }
+  }
+};
+
 // Conv wgrad B operand (MN-major): element (k = (n,p,q), col = (r,s,ci)) = x[n, p*st-pad+r*dil, ...]
 template <int R>
 struct ConvWgradMN {
@@ -352,7 +412,19 @@ struct Epi {
   int bias_f32;
   int relu;
   float* slab;       // split-K fp32 partial slabs [splits][M][N] (overrides C when non-null)
+  // row remap (dgrad phase launches): row m = (n, hh, ww) of a [N, Hh, Wh] phase grid is written to
+  // C row (n*H + hh*st + ph)*W + ww*st + pw
+  int rm_on, rm_Hh, rm_Wh, rm_st, rm_ph, rm_pw, rm_H, rm_W;
 };
+
+__device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
+  if (!e.rm_on) return m;
+  const int64_t t = m / e.rm_Wh;
+  const int ww = (int)(m - t * e.rm_Wh);
+  const int64_t n = t / e.rm_Hh;
+  const int hh = (int)(t - n * e.rm_Hh);
+  return (n * e.rm_H + (int64_t)hh * e.rm_st + e.rm_ph) * e.rm_W + (int64_t)ww * e.rm_st + e.rm_pw;
+}
 
 // ------------------------------------------------------------------ the kernel
 template <int BM, int BN, class LA, class LB>
@@ -429,6 +501,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
   for (int i = 0; i < TM; ++i) {
     const int64_t m = m0 + wm * WM + 16 * i + (lane & 15);
     if (m >= M) continue;
+    const int64_t crow = epi_row(epi, m);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int64_t n = n0 + wn * WN + 16 * j + 4 * (lane >> 4);
@@ -449,12 +522,12 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
         for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
       }
       if (epi.c_f32) {
-        *reinterpret_cast<f32x4*>((float*)epi.C + m * epi.ldc + n) = v;
+        *reinterpret_cast<f32x4*>((float*)epi.C + crow * epi.ldc + n) = v;
       } else {
         u16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = f2bf(v[r]);
-        *reinterpret_cast<u16x4*>((bf16_t*)epi.C + m * epi.ldc + n) = o;
+        *reinterpret_cast<u16x4*>((bf16_t*)epi.C + crow * epi.ldc + n) = o;
       }
     }
   }
@@ -492,34 +565,72 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
-// Weight transpose for conv dgrad: wt[ci][r][s][co] = w[co][r][s][ci]
+// Stride phases of a dgrad with dilation 1 (or stride 1): phase ph of the rows takes the taps
+// r = r0 + ri*st, ri < Rv, with r0 = (ph + pad) mod st.
+struct TapPhase {
+  int r0, n;     // first tap, tap count
+  int cum;       // taps of all earlier phases
+  int base;      // p = hh + base - ri*step
+};
+__host__ __device__ inline TapPhase tap_phase(int ph, int R, int st, int pad, int dil) {
+  TapPhase t;
+  if (st == 1) {
+    t.r0 = 0; t.n = R; t.cum = 0; t.base = pad;  // p = h + pad - r*dil
+    return t;
+  }
+  t.cum = 0;
+  for (int q = 0; q <= ph; ++q) {
+    const int r0 = (q + pad) % st;
+    const int n = r0 < R ? (R - r0 + st - 1) / st : 0;
+    if (q < ph) t.cum += n;
+    else { t.r0 = r0; t.n = n; t.base = (q + pad - r0) / st; }
+  }
+  return t;
+}
+
+// Weight transpose for conv dgrad, phase-packed: for every (ph, pw) phase block (row-major) the taps
+// it uses are stored as wt[ci][ri][si][co] (for stride 1 this is simply wt[ci][r][s][co]).
+// blockIdx.z = source tap (r, s).  `packed` = 0 keeps the plain [ci][r][s][co] layout (folded path).
 __global__ void __launch_bounds__(256) conv_wt_transpose_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
-                                                                int Cout, int RS, int Cin) {
+                                                                int Cout, int R, int S, int Cin, int st, int pad,
+                                                                int packed) {
   __shared__ bf16_t tile[32][33];
-  const int rs = blockIdx.z;
+  const int rs = blockIdx.z, r = rs / S, sx = rs % S;
+  int64_t base = 0;
+  int T = R * S, t = rs;
+  if (packed && st > 1) {
+    const int ph = ((r - pad) % st + st) % st, pw = ((sx - pad) % st + st) % st;
+    const TapPhase a = tap_phase(ph, R, st, pad, 1), b = tap_phase(pw, S, st, pad, 1);
+    base = ((int64_t)a.cum * S + (int64_t)a.n * b.cum) * Cin * Cout;
+    T = a.n * b.n;
+    t = ((r - a.r0) / st) * b.n + (sx - b.r0) / st;
+  }
   const int co0 = blockIdx.y * 32, ci0 = blockIdx.x * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
   for (int yy = ty; yy < 32; yy += 8) {
     const int co = co0 + yy, ci = ci0 + tx;
-    tile[yy][tx] = (co < Cout && ci < Cin) ? w[((int64_t)co * RS + rs) * Cin + ci] : (bf16_t)0;
+    tile[yy][tx] = (co < Cout && ci < Cin) ? w[((int64_t)co * R * S + rs) * Cin + ci] : (bf16_t)0;
   }
   __syncthreads();
   for (int yy = ty; yy < 32; yy += 8) {
     const int ci = ci0 + yy, co = co0 + tx;
-    if (co < Cout && ci < Cin) wt[((int64_t)ci * RS + rs) * Cout + co] = tile[tx][yy];
+    if (co < Cout && ci < Cin) wt[base + ((int64_t)ci * T + t) * Cout + co] = tile[tx][yy];
   }
 }
 
 // ------------------------------------------------------------------ host-side dispatch
 struct Plan {
-  int bn;           // 64 or 128
+  int bm, bn;       // 64 or 128 each
   int tiles_m, tiles_n, splits, ktiles_per_split;
 };
 
-Plan plan_gemm(int64_t M, int64_t N, int64_t K, bool allow_split, int target_blocks) {
+// target_blocks: workgroups wanted in flight (>= 2 per CU); split-K is only used when the output
+// tiles alone cannot fill the chip, with >= 4 K tiles per split and at most max_splits slabs.
+Plan plan_gemm(int64_t M, int64_t N, int64_t K, bool allow_split, int target_blocks, int max_splits = 64) {
   Plan p;
+  p.bm = M <= 64 ? 64 : 128;
   p.bn = N <= 64 ? 64 : 128;
-  p.tiles_m = (int)((M + 127) / 128);
+  p.tiles_m = (int)((M + p.bm - 1) / p.bm);
   p.tiles_n = (int)((N + p.bn - 1) / p.bn);
   const int ktiles = (int)((K + BK - 1) / BK);
   p.splits = 1;
@@ -528,23 +639,26 @@ Plan plan_gemm(int64_t M, int64_t N, int64_t K, bool allow_split, int target_blo
     int s = (int)(target_blocks / tiles);
     const int max_s = ktiles / 4 > 1 ? ktiles / 4 : 1;  // keep >= 4 K-tiles per split
     if (s > max_s) s = max_s;
-    if (s > 64) s = 64;
+    if (s > max_splits) s = max_splits;
     p.splits = s < 1 ? 1 : s;
   }
-  p.ktiles_per_split = (ktiles + p.splits - 1) / p.splits;
-  p.splits = (ktiles + p.ktiles_per_split - 1) / p.ktiles_per_split;
+  p.ktiles_per_split = ktiles > 0 ? (ktiles + p.splits - 1) / p.splits : 0;
+  p.splits = p.ktiles_per_split > 0 ? (ktiles + p.ktiles_per_split - 1) / p.ktiles_per_split : 1;
   if (p.splits < 1) p.splits = 1;
   return p;
 }
 
-template <int BN, class LA, class LB>
+// conv wgrad: M = Cout, N = R*S*C are small, K = N*P*Q is huge -> deep split-K
+Plan plan_wgrad(int64_t M, int64_t N, int64_t K, bool allow_split) { return plan_gemm(M, N, K, allow_split, 1024, 256); }
+
+template <int BM, int BN, class LA, class LB>
 hipError_t launch(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, const Plan& p, Epi epi,
                   float* slab, hipStream_t st) {
   const int ntiles = p.tiles_m * p.tiles_n;
   Epi e = epi;
   if (p.splits > 1) e.slab = slab;
-  gemm_kernel<128, BN, LA, LB><<<dim3(ntiles, p.splits), NT, 0, st>>>(la, lb, M, N, K, p.tiles_n,
-                                                                       p.ktiles_per_split, e);
+  gemm_kernel<BM, BN, LA, LB><<<dim3(ntiles, p.splits), NT, 0, st>>>(la, lb, M, N, K, p.tiles_n,
+                                                                     p.ktiles_per_split, e);
   PDA_CHECK_HIP(hipGetLastError());
   if (p.splits > 1) {
     int64_t g = (M * N / 4 + 255) / 256;
@@ -558,8 +672,12 @@ hipError_t launch(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, c
 template <template <int> class TA, template <int> class TB, class MakeA, class MakeB>
 hipError_t dispatch_bn(int64_t M, int64_t N, int64_t K, const Plan& p, Epi epi, float* slab, hipStream_t st,
                        MakeA make_a, MakeB make_b) {
-  if (p.bn == 64) return launch<64>(make_a(TA<128>{}), make_b(TB<64>{}), M, N, K, p, epi, slab, st);
-  return launch<128>(make_a(TA<128>{}), make_b(TB<128>{}), M, N, K, p, epi, slab, st);
+  if (p.bm == 64) {
+    if (p.bn == 64) return launch<64, 64>(make_a(TA<64>{}), make_b(TB<64>{}), M, N, K, p, epi, slab, st);
+    return launch<64, 128>(make_a(TA<64>{}), make_b(TB<128>{}), M, N, K, p, epi, slab, st);
+  }
+  if (p.bn == 64) return launch<128, 64>(make_a(TA<128>{}), make_b(TB<64>{}), M, N, K, p, epi, slab, st);
+  return launch<128, 128>(make_a(TA<128>{}), make_b(TB<128>{}), M, N, K, p, epi, slab, st);
 }
 
 ConvGeom make_geom(int H, int W, int C, int P, int Q, int R, int S, int st, int pad, int dil, int Cg) {
@@ -573,6 +691,8 @@ ConvGeom make_geom(int H, int W, int C, int P, int Q, int R, int S, int st, int 
   g.fH = make_fastdiv((uint32_t)H);
   return g;
 }
+
+bool dgrad_phased(int stride, int dil) { return stride == 1 || dil == 1; }
 
 }  // namespace
 
@@ -601,7 +721,7 @@ hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* 
 int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, int S, int P, int Q) {
   if (mode != 2) return 0;  // only wgrad splits K
   const int64_t M = Cout, Nn = (int64_t)R * S * C, K = (int64_t)N * P * Q;
-  Plan p = plan_gemm(M, Nn, K, true, 512);
+  Plan p = plan_wgrad(M, Nn, K, true);
   return p.splits > 1 ? (int64_t)p.splits * M * Nn : 0;
 }
 
@@ -618,16 +738,49 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H,
   return dispatch_bn<ConvFwdK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
 }
 
-// dx[N,H,W,C] = dgrad(dy[N,P,Q,Cout], wt[C,R,S,Cout])
+// dx[N,H,W,C] = dgrad(dy[N,P,Q,Cout], wt): one launch per stride phase with only the taps that reach
+// it (wt phase-packed by conv_weight_transpose); folded single launch when stride > 1 and dil > 1.
 hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int N, int H, int W, int C, int Cout, int R,
                         int S, int P, int Q, int stride, int pad, int dil, hipStream_t st) {
-  const int64_t M = (int64_t)N * H * W, Nn = C, K = (int64_t)R * S * Cout;
-  Plan p = plan_gemm(M, Nn, K, false, 512);
-  Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
   ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, Cout);
-  auto mk_a = [&](auto t) { t.dy = dy; t.g = g; t.M = M; t.K = K; return t; };
-  auto mk_b = [&](auto t) { t.p = wt; t.rows = Nn; t.K = K; t.ld = K; return t; };
-  return dispatch_bn<ConvDgradK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
+  if (!dgrad_phased(stride, dil)) {
+    const int64_t M = (int64_t)N * H * W, Nn = C, K = (int64_t)R * S * Cout;
+    Plan p = plan_gemm(M, Nn, K, false, 512);
+    Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
+    auto mk_a = [&](auto t) { t.dy = dy; t.g = g; t.M = M; t.K = K; return t; };
+    auto mk_b = [&](auto t) { t.p = wt; t.rows = Nn; t.K = K; t.ld = K; return t; };
+    return dispatch_bn<ConvDgradK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
+  }
+  const int nph = stride;  // phases per dim (1 for stride 1)
+  for (int ph = 0; ph < nph; ++ph) {
+    const TapPhase a = tap_phase(ph, R, stride, pad, dil);
+    const int Hh = stride == 1 ? H : (H - ph + stride - 1) / stride;
+    for (int pw = 0; pw < nph; ++pw) {
+      const TapPhase b = tap_phase(pw, S, stride, pad, dil);
+      const int Wh = stride == 1 ? W : (W - pw + stride - 1) / stride;
+      if (Hh <= 0 || Wh <= 0) continue;
+      PhaseGeom pg;
+      pg.Hh = Hh; pg.Wh = Wh; pg.Sv = b.n > 0 ? b.n : 1;
+      pg.base_r = a.base; pg.step_r = stride == 1 ? dil : 1;
+      pg.base_s = b.base; pg.step_s = stride == 1 ? dil : 1;
+      pg.fWh = make_fastdiv((uint32_t)Wh);
+      pg.fHh = make_fastdiv((uint32_t)Hh);
+      pg.fSv = make_fastdiv((uint32_t)pg.Sv);
+      const int64_t M = (int64_t)N * Hh * Wh, Nn = C, K = (int64_t)a.n * b.n * Cout;
+      const bf16_t* wph = wt + ((int64_t)a.cum * S + (int64_t)a.n * b.cum) * C * Cout;
+      Plan p = plan_gemm(M, Nn, K, false, 512);
+      Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
+      if (stride > 1) {
+        epi.rm_on = 1; epi.rm_Hh = Hh; epi.rm_Wh = Wh; epi.rm_st = stride; epi.rm_ph = ph; epi.rm_pw = pw;
+        epi.rm_H = H; epi.rm_W = W;
+      }
+      auto mk_a = [&](auto t) { t.dy = dy; t.g = g; t.ph = pg; t.M = M; t.K = K; return t; };
+      auto mk_b = [&](auto t) { t.p = wph; t.rows = Nn; t.K = K; t.ld = K > 0 ? K : 8; return t; };
+      const hipError_t e = dispatch_bn<ConvDgradPhaseK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
+      if (e != hipSuccess) return e;
+    }
+  }
+  return hipSuccess;
 }
 
 // dw[Cout, R*S*C] = dy[NPQ, Cout]^T * im2col(x)[NPQ, R*S*C]   (fp32 or bf16 output)
@@ -635,7 +788,7 @@ hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32
                         int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, float* slab,
                         hipStream_t st) {
   const int64_t M = Cout, Nn = (int64_t)R * S * C, K = (int64_t)N * P * Q;
-  Plan p = plan_gemm(M, Nn, K, slab != nullptr, 512);
+  Plan p = plan_wgrad(M, Nn, K, slab != nullptr);
   Epi epi{dw, Nn, dw_f32 ? 1 : 0, nullptr, 0, 0, nullptr};
   ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
   auto mk_a = [&](auto t) { t.p = dy; t.K = K; t.cols = M; t.ld = Cout; return t; };
@@ -643,9 +796,10 @@ hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32
   return dispatch_bn<PlainMN, ConvWgradMN>(M, Nn, K, p, epi, slab, st, mk_a, mk_b);
 }
 
-hipError_t conv_weight_transpose(const bf16_t* w, bf16_t* wt, int Cout, int RS, int Cin, hipStream_t st) {
-  dim3 grid((Cin + 31) / 32, (Cout + 31) / 32, RS);
-  conv_wt_transpose_kernel<<<grid, 256, 0, st>>>(w, wt, Cout, RS, Cin);
+hipError_t conv_weight_transpose(const bf16_t* w, bf16_t* wt, int Cout, int R, int S, int Cin, int stride, int pad,
+                                 int dil, hipStream_t st) {
+  dim3 grid((Cin + 31) / 32, (Cout + 31) / 32, R * S);
+  conv_wt_transpose_kernel<<<grid, 256, 0, st>>>(w, wt, Cout, R, S, Cin, stride, pad, dgrad_phased(stride, dil) ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -1,43 +1,56 @@
 // Row normalisations for the transformer configs (SURVEY §2.5 K19 LayerNorm — GPT-2, K20 RMSNorm —
-// Llama-3).  x: [rows, D] (fp32 or bf16, D % 8 == 0, D <= 8192), gamma/beta: [D].
-// One 256-thread workgroup per row (ROWS_PER_BLOCK rows in sequence for the backward so the
-// gamma/beta gradient is accumulated in registers and flushed with one fp32 atomic per column per
-// workgroup).  The row lives in registers between the statistics and the normalisation (one HBM read).
+// Llama-3) and the column reductions they need.  x: [rows, D] (fp32 or bf16, D % 8 == 0, D <= 8192),
+// gamma/beta: [D].
+//
+// Layout on CDNA4: one 64-lane wavefront per row (4 rows per 256-thread workgroup), so every row
+// reduction is a register/DPP shuffle reduction with no LDS and no barrier; lane l owns the 8-wide
+// column vectors l, l+64, ... (VPL = ceil(D/512) of them, a template parameter).  The row stays in
+// registers between the statistics and the output pass when VPL <= 4 (D <= 2048: GPT-2 medium/XL);
+// wider rows re-read the (L2-resident) row instead of spilling.
+//
+// Parameter gradients (dgamma = sum_r dy*xhat, dbeta = sum_r dy) are NOT accumulated with atomics
+// from the row kernel (2K-deep same-address contention): a column-strip kernel writes per-slab
+// partials and a finalize kernel sums the slabs — the same slab scheme as the BatchNorm kernels.
 #include "pda_common.h"
 #include "pda_kernels.h"
+
+#include <type_traits>
 
 namespace pda {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kMaxV = 4;  // 8-element vectors per thread: D <= 256*8*4 = 8192
-constexpr int kBwdRows = 8;
+constexpr int kRowsPerBlock = kThreads / 64;
 
-template <typename T, typename P, bool RMS>
+template <typename T, typename P, bool RMS, int VPL>
 __global__ void __launch_bounds__(kThreads) rownorm_fwd_kernel(const T* __restrict__ x, const P* __restrict__ gamma,
                                                                const P* __restrict__ beta, T* __restrict__ y,
                                                                float* __restrict__ mean_out,
-                                                               float* __restrict__ rstd_out, int64_t D, float eps) {
-  __shared__ float scratch[16];
-  const int64_t row = blockIdx.x;
+                                                               float* __restrict__ rstd_out, int64_t rows, int64_t D,
+                                                               float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= rows) return;
   const T* xr = x + row * D;
-  float v[kMaxV][8];
+  float v[VPL][8];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < kMaxV; ++i) {
-    const int64_t c = ((int64_t)i * kThreads + threadIdx.x) * 8;
+  for (int i = 0; i < VPL; ++i) {
+    const int64_t c = ((int64_t)i * 64 + lane) * 8;
     if (c < D) {
       load8(xr + c, v[i]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) s += v[i][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
     }
   }
-  float mean = 0.f;
-  if (!RMS) mean = block_sum(s, scratch) / (float)D;
+  const float mean = RMS ? 0.f : wave_sum(s) / (float)D;
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < kMaxV; ++i) {
-    const int64_t c = ((int64_t)i * kThreads + threadIdx.x) * 8;
+  for (int i = 0; i < VPL; ++i) {
+    const int64_t c = ((int64_t)i * 64 + lane) * 8;
     if (c < D) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -46,10 +59,10 @@ __global__ void __launch_bounds__(kThreads) rownorm_fwd_kernel(const T* __restri
       }
     }
   }
-  const float rstd = rsqrtf(block_sum(q, scratch) / (float)D + eps);
+  const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
 #pragma unroll
-  for (int i = 0; i < kMaxV; ++i) {
-    const int64_t c = ((int64_t)i * kThreads + threadIdx.x) * 8;
+  for (int i = 0; i < VPL; ++i) {
+    const int64_t c = ((int64_t)i * 64 + lane) * 8;
     if (c < D) {
       float g[8], b[8], o[8];
       load8(gamma + c, g);
@@ -59,7 +72,7 @@ __global__ void __launch_bounds__(kThreads) rownorm_fwd_kernel(const T* __restri
       store8(y + row * D + c, o);
     }
   }
-  if (threadIdx.x == 0) {
+  if (lane == 0) {
     if (!RMS) mean_out[row] = mean;
     rstd_out[row] = rstd;
   }
@@ -67,112 +80,248 @@ __global__ void __launch_bounds__(kThreads) rownorm_fwd_kernel(const T* __restri
 
 // dx = rstd * (g*dy - mean(g*dy) - xhat * mean(g*dy*xhat))        (LayerNorm)
 // dx = rstd * (g*dy - xhat * mean(g*dy*xhat))                      (RMSNorm)
-template <typename T, typename P, bool RMS>
-__global__ void __launch_bounds__(kThreads) rownorm_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
-                                                               const P* __restrict__ gamma,
-                                                               const float* __restrict__ mean_in,
-                                                               const float* __restrict__ rstd_in,
-                                                               T* __restrict__ dx, float* __restrict__ dgamma,
-                                                               float* __restrict__ dbeta, int64_t rows, int64_t D) {
-  __shared__ float scratch[16];
-  float dg[kMaxV][8], db[kMaxV][8];
+template <typename T, typename P, bool RMS, int VPL>
+__global__ void __launch_bounds__(kThreads) rownorm_bwd_dx_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                                  const P* __restrict__ gamma,
+                                                                  const float* __restrict__ mean_in,
+                                                                  const float* __restrict__ rstd_in,
+                                                                  T* __restrict__ dx, int64_t rows, int64_t D) {
+  constexpr bool kKeep = VPL <= 4;
+  constexpr int KV = kKeep ? VPL : 1;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float mean = RMS ? 0.f : mean_in[row], rstd = rstd_in[row];
+  const T* xr = x + row * D;
+  const T* dyr = dy + row * D;
+  float xh[KV][8], gd[KV][8];
+  float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-  for (int i = 0; i < kMaxV; ++i)
+  for (int i = 0; i < VPL; ++i) {
+    const int64_t c = ((int64_t)i * 64 + lane) * 8;
+    if (c < D) {
+      float xv[8], d[8], g[8];
+      load8(xr + c, xv);
+      load8(dyr + c, d);
+      load8(gamma + c, g);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dg[i][j] = db[i][j] = 0.f;
-  for (int rr = 0; rr < kBwdRows; ++rr) {
-    const int64_t row = (int64_t)blockIdx.x * kBwdRows + rr;
-    if (row >= rows) break;
-    const float mean = RMS ? 0.f : mean_in[row], rstd = rstd_in[row];
-    float xh[kMaxV][8], gd[kMaxV][8];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < kMaxV; ++i) {
-      const int64_t c = ((int64_t)i * kThreads + threadIdx.x) * 8;
-      if (c < D) {
-        float xv[8], d[8], g[8];
-        load8(x + row * D + c, xv);
-        load8(dy + row * D + c, d);
-        load8(gamma + c, g);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xh[i][j] = (xv[j] - mean) * rstd;
-          gd[i][j] = g[j] * d[j];
-          s1 += gd[i][j];
-          s2 += gd[i][j] * xh[i][j];
-          dg[i][j] += d[j] * xh[i][j];
-          db[i][j] += d[j];
+      for (int j = 0; j < 8; ++j) {
+        const float h = (xv[j] - mean) * rstd, q = g[j] * d[j];
+        s1 += q;
+        s2 += q * h;
+        if constexpr (kKeep) {
+          xh[i][j] = h;
+          gd[i][j] = q;
         }
       }
     }
-    const float m1 = RMS ? 0.f : block_sum(s1, scratch) / (float)D;
-    const float m2 = block_sum(s2, scratch) / (float)D;
+  }
+  const float m1 = RMS ? 0.f : wave_sum(s1) / (float)D;
+  const float m2 = wave_sum(s2) / (float)D;
 #pragma unroll
-    for (int i = 0; i < kMaxV; ++i) {
-      const int64_t c = ((int64_t)i * kThreads + threadIdx.x) * 8;
-      if (c < D) {
-        float o[8];
+  for (int i = 0; i < VPL; ++i) {
+    const int64_t c = ((int64_t)i * 64 + lane) * 8;
+    if (c < D) {
+      float o[8];
+      if constexpr (kKeep) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rstd * (gd[i][j] - m1 - xh[i][j] * m2);
-        store8(dx + row * D + c, o);
-      }
-    }
-  }
+      } else {
+        float xv[8], d[8], g[8];
+        load8(xr + c, xv);
+        load8(dyr + c, d);
+        load8(gamma + c, g);
 #pragma unroll
-  for (int i = 0; i < kMaxV; ++i) {
-    const int64_t c = ((int64_t)i * kThreads + threadIdx.x) * 8;
-    if (c < D) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        atomicAdd(dgamma + c + j, dg[i][j]);
-        if (!RMS) atomicAdd(dbeta + c + j, db[i][j]);
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[j] * d[j] - m1 - (xv[j] - mean) * rstd * m2);
       }
+      store8(dx + row * D + c, o);
     }
   }
 }
 
+// ------------------------------------------------------------------ column-strip reductions
+// Block = 64 column vectors (512 columns) x 4 row lanes; blockIdx.y = row slab.  Each block writes
+// its slab partial(s) to ws[k][slab][col]; colreduce_finalize sums the slabs.
+constexpr int kStripCols = 512;
+
+template <typename T, bool LN_GRAD, bool RMS>
+__global__ void __launch_bounds__(kThreads) colstrip_partial_kernel(const T* __restrict__ a, const T* __restrict__ x,
+                                                                    const float* __restrict__ mean_in,
+                                                                    const float* __restrict__ rstd_in,
+                                                                    float* __restrict__ ws, int64_t rows, int64_t D,
+                                                                    int64_t rows_per_slab, int nslab) {
+  __shared__ float red[2][4][kStripCols + 4];
+  const int cv = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * kStripCols + cv * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_slab;
+  const int64_t r1 = min(rows, r0 + rows_per_slab);
+  float acc0[8], acc1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc0[j] = acc1[j] = 0.f;
+  if (c < D) {
+    for (int64_t r = r0 + rl; r < r1; r += 4) {
+      float d[8];
+      load8(a + r * D + c, d);
+      if constexpr (LN_GRAD) {
+        float xv[8];
+        load8(x + r * D + c, xv);
+        const float mean = RMS ? 0.f : mean_in[r], rstd = rstd_in[r];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          acc0[j] += d[j] * (xv[j] - mean) * rstd;
+          acc1[j] += d[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc0[j] += d[j];
+      }
+    }
+  }
+  constexpr int NOUT = (LN_GRAD && !RMS) ? 2 : 1;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[0][rl][cv * 8 + j] = acc0[j];
+    if (NOUT == 2) red[1][rl][cv * 8 + j] = acc1[j];
+  }
+  __syncthreads();
+  // 256 threads finalize 512 columns x NOUT outputs
+  for (int t = threadIdx.x; t < kStripCols * NOUT; t += kThreads) {
+    const int k = t / kStripCols, col = t % kStripCols;
+    const int64_t gc = (int64_t)blockIdx.x * kStripCols + col;
+    if (gc >= D) continue;
+    const float s = red[k][0][col] + red[k][1][col] + red[k][2][col] + red[k][3][col];
+    ws[((int64_t)k * nslab + blockIdx.y) * D + gc] = s;
+  }
+}
+
+// out_k[col] = sum_s ws[k][s][col] (+ out_k[col] if accumulate)
+__global__ void __launch_bounds__(kThreads) colreduce_finalize_kernel(const float* __restrict__ ws, int nslab,
+                                                                      int64_t D, int nout, float* __restrict__ out0,
+                                                                      float* __restrict__ out1) {
+  const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (t >= D * nout) return;
+  const int k = (int)(t / D);
+  const int64_t col = t % D;
+  const float* p = ws + (int64_t)k * nslab * D + col;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int s = 0;
+  for (; s + 4 <= nslab; s += 4) {
+    s0 += p[(int64_t)s * D];
+    s1 += p[(int64_t)(s + 1) * D];
+    s2 += p[(int64_t)(s + 2) * D];
+    s3 += p[(int64_t)(s + 3) * D];
+  }
+  for (; s < nslab; ++s) s0 += p[(int64_t)s * D];
+  (k == 0 ? out0 : out1)[col] = (s0 + s1) + (s2 + s3);
+}
+
+int plan_slabs(int64_t rows, int64_t D) {
+  const int64_t strips = (D + kStripCols - 1) / kStripCols;
+  int64_t nslab = 1024 / strips;                 // ~4 workgroups per CU
+  const int64_t max_by_rows = (rows + 31) / 32;  // >= 32 rows (8 per row lane) per slab
+  if (nslab > max_by_rows) nslab = max_by_rows;
+  if (nslab < 1) nslab = 1;
+  return (int)nslab;
+}
+
+template <typename F>
+void dispatch_vpl(int64_t D, F&& f) {
+  const int64_t vpl = (D + 511) / 512;
+  if (vpl <= 1) f(std::integral_constant<int, 1>{});
+  else if (vpl <= 2) f(std::integral_constant<int, 2>{});
+  else if (vpl <= 4) f(std::integral_constant<int, 4>{});
+  else if (vpl <= 8) f(std::integral_constant<int, 8>{});
+  else f(std::integral_constant<int, 16>{});
+}
+
 }  // namespace
+
+int64_t colreduce_ws_floats(int64_t rows, int64_t D, int nout) { return (int64_t)nout * plan_slabs(rows, D) * D; }
 
 hipError_t rownorm_fwd(const void* x, bool x_bf16, const void* gamma, const void* beta, bool p_bf16, void* y,
                        float* mean, float* rstd, int64_t rows, int64_t D, float eps, bool rms, hipStream_t st) {
   if (rows == 0) return hipSuccess;
-  const unsigned grid = (unsigned)rows;
-#define ARGS_F(T, P) (const T*)x, (const P*)gamma, (const P*)beta, (T*)y, mean, rstd, D, eps
-  if (rms) {
-    if (x_bf16 && p_bf16) rownorm_fwd_kernel<bf16_t, bf16_t, true><<<grid, kThreads, 0, st>>>(ARGS_F(bf16_t, bf16_t));
-    else if (x_bf16) rownorm_fwd_kernel<bf16_t, float, true><<<grid, kThreads, 0, st>>>(ARGS_F(bf16_t, float));
-    else if (p_bf16) rownorm_fwd_kernel<float, bf16_t, true><<<grid, kThreads, 0, st>>>(ARGS_F(float, bf16_t));
-    else rownorm_fwd_kernel<float, float, true><<<grid, kThreads, 0, st>>>(ARGS_F(float, float));
-  } else {
-    if (x_bf16 && p_bf16) rownorm_fwd_kernel<bf16_t, bf16_t, false><<<grid, kThreads, 0, st>>>(ARGS_F(bf16_t, bf16_t));
-    else if (x_bf16) rownorm_fwd_kernel<bf16_t, float, false><<<grid, kThreads, 0, st>>>(ARGS_F(bf16_t, float));
-    else if (p_bf16) rownorm_fwd_kernel<float, bf16_t, false><<<grid, kThreads, 0, st>>>(ARGS_F(float, bf16_t));
-    else rownorm_fwd_kernel<float, float, false><<<grid, kThreads, 0, st>>>(ARGS_F(float, float));
-  }
-#undef ARGS_F
+  const unsigned grid = (unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock);
+  dispatch_vpl(D, [&](auto vc) {
+    constexpr int V = decltype(vc)::value;
+#define L(T, P, R) \
+  rownorm_fwd_kernel<T, P, R, V><<<grid, kThreads, 0, st>>>((const T*)x, (const P*)gamma, (const P*)beta, (T*)y, mean, rstd, rows, D, eps)
+    if (rms) {
+      if (x_bf16 && p_bf16) L(bf16_t, bf16_t, true);
+      else if (x_bf16) L(bf16_t, float, true);
+      else if (p_bf16) L(float, bf16_t, true);
+      else L(float, float, true);
+    } else {
+      if (x_bf16 && p_bf16) L(bf16_t, bf16_t, false);
+      else if (x_bf16) L(bf16_t, float, false);
+      else if (p_bf16) L(float, bf16_t, false);
+      else L(float, float, false);
+    }
+#undef L
+  });
   return hipGetLastError();
 }
 
 hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* gamma, bool p_bf16, const float* mean,
                        const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, bool rms,
-                       hipStream_t st) {
-  if (rows == 0) return hipSuccess;
-  PDA_CHECK_HIP(hipMemsetAsync(dgamma, 0, D * sizeof(float), st));
-  if (!rms) PDA_CHECK_HIP(hipMemsetAsync(dbeta, 0, D * sizeof(float), st));
-  const unsigned grid = (unsigned)((rows + kBwdRows - 1) / kBwdRows);
-#define ARGS_B(T, P) (const T*)dy, (const T*)x, (const P*)gamma, mean, rstd, (T*)dx, dgamma, dbeta, rows, D
-  if (rms) {
-    if (x_bf16 && p_bf16) rownorm_bwd_kernel<bf16_t, bf16_t, true><<<grid, kThreads, 0, st>>>(ARGS_B(bf16_t, bf16_t));
-    else if (x_bf16) rownorm_bwd_kernel<bf16_t, float, true><<<grid, kThreads, 0, st>>>(ARGS_B(bf16_t, float));
-    else if (p_bf16) rownorm_bwd_kernel<float, bf16_t, true><<<grid, kThreads, 0, st>>>(ARGS_B(float, bf16_t));
-    else rownorm_bwd_kernel<float, float, true><<<grid, kThreads, 0, st>>>(ARGS_B(float, float));
-  } else {
-    if (x_bf16 && p_bf16) rownorm_bwd_kernel<bf16_t, bf16_t, false><<<grid, kThreads, 0, st>>>(ARGS_B(bf16_t, bf16_t));
-    else if (x_bf16) rownorm_bwd_kernel<bf16_t, float, false><<<grid, kThreads, 0, st>>>(ARGS_B(bf16_t, float));
-    else if (p_bf16) rownorm_bwd_kernel<float, bf16_t, false><<<grid, kThreads, 0, st>>>(ARGS_B(float, bf16_t));
-    else rownorm_bwd_kernel<float, float, false><<<grid, kThreads, 0, st>>>(ARGS_B(float, float));
+                       float* ws, hipStream_t st) {
+  if (rows == 0) {
+    PDA_CHECK_HIP(hipMemsetAsync(dgamma, 0, D * sizeof(float), st));
+    if (!rms) PDA_CHECK_HIP(hipMemsetAsync(dbeta, 0, D * sizeof(float), st));
+    return hipSuccess;
   }
-#undef ARGS_B
+  const unsigned grid = (unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock);
+  dispatch_vpl(D, [&](auto vc) {
+    constexpr int V = decltype(vc)::value;
+#define L(T, P, R) \
+  rownorm_bwd_dx_kernel<T, P, R, V><<<grid, kThreads, 0, st>>>((const T*)dy, (const T*)x, (const P*)gamma, mean, rstd, (T*)dx, rows, D)
+    if (rms) {
+      if (x_bf16 && p_bf16) L(bf16_t, bf16_t, true);
+      else if (x_bf16) L(bf16_t, float, true);
+      else if (p_bf16) L(float, bf16_t, true);
+      else L(float, float, true);
+    } else {
+      if (x_bf16 && p_bf16) L(bf16_t, bf16_t, false);
+      else if (x_bf16) L(bf16_t, float, false);
+      else if (p_bf16) L(float, bf16_t, false);
+      else L(float, float, false);
+    }
+#undef L
+  });
+  PDA_CHECK_HIP(hipGetLastError());
+  const int nslab = plan_slabs(rows, D);
+  const int64_t rps = (rows + nslab - 1) / nslab;
+  dim3 pg((unsigned)((D + kStripCols - 1) / kStripCols), (unsigned)nslab);
+#define P(T, R) \
+  colstrip_partial_kernel<T, true, R><<<pg, kThreads, 0, st>>>((const T*)dy, (const T*)x, mean, rstd, ws, rows, D, rps, nslab)
+  if (x_bf16) {
+    if (rms) P(bf16_t, true); else P(bf16_t, false);
+  } else {
+    if (rms) P(float, true); else P(float, false);
+  }
+#undef P
+  PDA_CHECK_HIP(hipGetLastError());
+  const int nout = rms ? 1 : 2;
+  colreduce_finalize_kernel<<<(unsigned)((D * nout + kThreads - 1) / kThreads), kThreads, 0, st>>>(ws, nslab, D, nout,
+                                                                                                  dgamma, dbeta);
+  return hipGetLastError();
+}
+
+// Column sums of a [rows, cols] matrix (bias gradients): out[c] = sum_r x[r, c] (fp32 out), cols % 8 == 0.
+hipError_t colsum(const void* x, bool bf16, float* out, int64_t rows, int64_t cols, float* ws, hipStream_t st) {
+  if (rows == 0) return hipMemsetAsync(out, 0, cols * sizeof(float), st);
+  const int nslab = plan_slabs(rows, cols);
+  const int64_t rps = (rows + nslab - 1) / nslab;
+  dim3 pg((unsigned)((cols + kStripCols - 1) / kStripCols), (unsigned)nslab);
+  if (bf16)
+    colstrip_partial_kernel<bf16_t, false, false><<<pg, kThreads, 0, st>>>((const bf16_t*)x, nullptr, nullptr, nullptr,
+                                                                           ws, rows, cols, rps, nslab);
+  else
+    colstrip_partial_kernel<float, false, false><<<pg, kThreads, 0, st>>>((const float*)x, nullptr, nullptr, nullptr,
+                                                                          ws, rows, cols, rps, nslab);
+  PDA_CHECK_HIP(hipGetLastError());
+  colreduce_finalize_kernel<<<(unsigned)((cols + kThreads - 1) / kThreads), kThreads, 0, st>>>(ws, nslab, cols, 1, out,
+                                                                                               nullptr);
   return hipGetLastError();
 }
 

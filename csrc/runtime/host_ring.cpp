@@ -188,6 +188,16 @@ void bind_runtime(pybind11::module& m) {
       .def("barrier", &HostRing::barrier)
       .def_property_readonly("rank", &HostRing::rank)
       .def_property_readonly("world", &HostRing::world);
+  py::class_<Watchdog>(m, "Watchdog")
+      .def(py::init<double, int, const std::string&, int, double>(), py::arg("timeout"), py::arg("rank"),
+           py::arg("action") = "abort", py::arg("exit_code") = 17, py::arg("poll") = 0.5)
+      .def("arm", &Watchdog::arm, py::arg("desc"), py::arg("timeout") = -1.0)
+      .def("disarm", &Watchdog::disarm)
+      .def("pending", &Watchdog::pending)
+      .def("expired", &Watchdog::expired)
+      .def_property_readonly("armed_total", &Watchdog::armed_total)
+      .def_property_readonly("timeout", &Watchdog::timeout)
+      .def("stop", &Watchdog::stop, py::call_guard<py::gil_scoped_release>());
 }
 
 }  // namespace pda_rt

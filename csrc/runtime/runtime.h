@@ -122,6 +122,42 @@ class HostRing {
   int listen_fd_ = -1, right_fd_ = -1, left_fd_ = -1;
 };
 
+// ------------------------------------------------------------------ collective watchdog
+// Per-process native thread (no GIL) that enforces a deadline on every armed collective; on expiry it
+// reports all pending operations and aborts / exits the rank (see watchdog.cpp).
+class Watchdog {
+ public:
+  Watchdog(double timeout_s, int rank, const std::string& action, int exit_code, double poll_s);
+  ~Watchdog();
+  int64_t arm(const std::string& desc, double timeout_s);
+  bool disarm(int64_t id);
+  std::vector<std::string> pending() const;
+  std::vector<std::string> expired() const;
+  int64_t armed_total() const;
+  double timeout() const { return timeout_s_; }
+  void stop();
+
+ private:
+  struct Ticket {
+    std::string desc;
+    double start = 0, deadline = 0;
+    bool reported = false;
+  };
+  void loop();
+  double timeout_s_;
+  int rank_;
+  std::string action_;
+  int exit_code_;
+  double poll_s_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::map<int64_t, Ticket> tickets_;
+  std::vector<std::string> expired_;
+  int64_t next_id_ = 1, armed_total_ = 0;
+  bool stop_ = false;
+  std::thread thread_;
+};
+
 void bind_runtime(pybind11::module& m);
 
 }  // namespace pda_rt

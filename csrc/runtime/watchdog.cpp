@@ -1,0 +1,120 @@
+// Collective watchdog (SURVEY §5.3 "a communicator watchdog thread per process enforces a timeout
+// per outstanding collective").  The reference has no timeouts at all (torchrun defaults, `NB02:287`);
+// a rank that stops participating leaves every other rank blocked inside RCCL forever.
+//
+// The watchdog is a native thread that never takes the Python GIL, so it keeps running while the
+// main thread is blocked in a collective wait.  Callers arm a ticket (description + deadline) when
+// they launch a collective and disarm it when the collective completed.  When a ticket outlives its
+// deadline the thread prints every pending ticket of this rank to stderr and then either
+//   * raises SIGABRT (default: Python's faulthandler, enabled by the framework, dumps every thread's
+//     stack, the launcher sees the abnormal exit and tears the job down), or
+//   * _exit(code), or
+//   * only records the expiry (report mode, used by tests and by callers that poll `expired()`).
+#include <chrono>
+#include <csignal>
+#include <cstdio>
+#include <stdexcept>
+#include <unistd.h>
+
+#include "runtime.h"
+
+namespace pda_rt {
+
+namespace {
+double now_s() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+
+Watchdog::Watchdog(double timeout_s, int rank, const std::string& action, int exit_code, double poll_s)
+    : timeout_s_(timeout_s), rank_(rank), action_(action), exit_code_(exit_code), poll_s_(poll_s) {
+  if (action_ != "abort" && action_ != "exit" && action_ != "report")
+    throw std::invalid_argument("Watchdog action must be abort | exit | report");
+  thread_ = std::thread([this] { loop(); });
+}
+
+Watchdog::~Watchdog() { stop(); }
+
+void Watchdog::stop() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (stop_) return;
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (thread_.joinable()) thread_.join();
+}
+
+int64_t Watchdog::arm(const std::string& desc, double timeout_s) {
+  std::lock_guard<std::mutex> g(mu_);
+  const int64_t id = next_id_++;
+  const double t = timeout_s > 0 ? timeout_s : timeout_s_;
+  tickets_[id] = Ticket{desc, now_s(), now_s() + t};
+  ++armed_total_;
+  return id;
+}
+
+bool Watchdog::disarm(int64_t id) {
+  std::lock_guard<std::mutex> g(mu_);
+  return tickets_.erase(id) > 0;
+}
+
+std::vector<std::string> Watchdog::pending() const {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<std::string> out;
+  const double t = now_s();
+  for (auto& kv : tickets_) {
+    char buf[64];
+    snprintf(buf, sizeof(buf), " (%.1fs)", t - kv.second.start);
+    out.push_back(kv.second.desc + buf);
+  }
+  return out;
+}
+
+std::vector<std::string> Watchdog::expired() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return expired_;
+}
+
+int64_t Watchdog::armed_total() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return armed_total_;
+}
+
+void Watchdog::loop() {
+  std::unique_lock<std::mutex> lk(mu_);
+  while (!stop_) {
+    cv_.wait_for(lk, std::chrono::duration<double>(poll_s_));
+    if (stop_) break;
+    const double t = now_s();
+    bool fire = false;
+    for (auto& kv : tickets_) {
+      if (t > kv.second.deadline && !kv.second.reported) {
+        kv.second.reported = true;
+        expired_.push_back(kv.second.desc);
+        fire = true;
+      }
+    }
+    if (!fire) continue;
+    fprintf(stderr, "[pda watchdog] rank %d: collective timeout; %zu pending operation(s):\n", rank_,
+            tickets_.size());
+    for (auto& kv : tickets_)
+      fprintf(stderr, "[pda watchdog] rank %d:   #%lld %s pending %.1fs (deadline %.1fs)\n", rank_,
+              (long long)kv.first, kv.second.desc.c_str(), t - kv.second.start, kv.second.deadline - kv.second.start);
+    fflush(stderr);
+    if (action_ == "report") continue;
+    if (action_ == "exit") {
+      fprintf(stderr, "[pda watchdog] rank %d: exiting with code %d\n", rank_, exit_code_);
+      fflush(stderr);
+      _exit(exit_code_);
+    }
+    fprintf(stderr, "[pda watchdog] rank %d: aborting (SIGABRT)\n", rank_);
+    fflush(stderr);
+    lk.unlock();
+    std::raise(SIGABRT);
+    lk.lock();
+  }
+}
+
+}  // namespace pda_rt

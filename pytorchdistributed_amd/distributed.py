@@ -159,6 +159,9 @@ def init_process_group(
     _STATE["backend"] = "ring" if want_ring else backend
     if want_ring:
         host_ring()
+    from .parallel import debug as _debug
+
+    _debug.maybe_enable()  # PDA_DEBUG=collectives: cross-rank fingerprint check before every collective
     return dist.group.WORLD
 
 

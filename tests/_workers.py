@@ -169,3 +169,43 @@ def fsdp_worker(rank, world, outdir):
     if rank == 0:
         torch.save(sd, os.path.join(outdir, "full.pt"))
     pd.destroy_process_group()
+
+
+def debug_checker_worker(rank, world, mode, outdir):
+    """PDA_DEBUG=collectives: matching collectives pass; a size/op mismatch or a missing collective is
+    reported on every rank before anything hangs."""
+    os.environ["PDA_DEBUG"] = "collectives"
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel import debug
+
+    pd.init_process_group("gloo")
+    ck = debug._CHECKER
+    ck.timeout_s = 3.0
+    res = {"enabled": ck is not None}
+    import torch.distributed as dist
+
+    t = torch.ones(4)
+    dist.all_reduce(t)
+    dist.broadcast(t, 0)
+    res["ok_checked"] = ck.checked
+    try:
+        if mode == "size":
+            dist.all_reduce(torch.ones(4 if rank == 0 else 5))
+        elif mode == "op":
+            if rank == 0:
+                dist.all_reduce(torch.ones(4))
+            else:
+                dist.broadcast(torch.ones(4), 0)
+        elif mode == "missing":
+            if rank == 0:
+                dist.all_reduce(torch.ones(4))
+        res["error"] = None
+    except debug.CollectiveMismatchError as e:
+        res["error"] = str(e)
+    with open(os.path.join(outdir, f"{rank}.json"), "w") as fh:
+        import json
+
+        json.dump(res, fh)
+    debug.disable_collective_checks()
+    if mode != "missing":
+        pd.destroy_process_group()

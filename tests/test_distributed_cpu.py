@@ -148,3 +148,45 @@ def test_pda_run_max_restarts_resumes_from_snapshot(tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     assert "Resuming training from snapshot at Epoch 1" in r.stdout
     assert (tmp_path / "done0").read_text() == "1 1"
+
+
+@pytest.mark.parametrize("mode", ["size", "op", "missing"])
+def test_debug_collectives_checker(tmp_path, mode):
+    import json
+
+    spawn(_workers.debug_checker_worker, args=(2, mode, str(tmp_path)), nprocs=2, timeout=120)
+    res = [json.loads((tmp_path / f"{r}.json").read_text()) for r in range(2)]
+    assert all(r["enabled"] and r["ok_checked"] == 2 for r in res)
+    if mode == "missing":
+        assert "rank 1 did not reach collective #3" in res[0]["error"]
+        return
+    for r in res:
+        assert r["error"] and "collective mismatch at #3" in r["error"]
+        assert "rank 0: all_reduce" in r["error"]
+        assert ("[5]" in r["error"]) if mode == "size" else ("rank 1: broadcast" in r["error"])
+
+
+def test_watchdog_aborts_hung_rank(tmp_path):
+    code = ("import time; from pytorchdistributed_amd.utils import watchdog as w; import os;"
+            "os.environ['PDA_COLLECTIVE_TIMEOUT_S']='0.3';"
+            "from pytorchdistributed_amd.config import set_config; set_config(None);"
+            "w.arm('all_reduce bucket 3 (32 MB)'); time.sleep(30)")
+    p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=60)
+    assert p.returncode != 0
+    assert "[pda watchdog] rank 0" in p.stderr and "all_reduce bucket 3 (32 MB)" in p.stderr
+    assert "time.sleep" in p.stderr or "File" in p.stderr  # faulthandler stack dump of the hung thread
+
+
+def test_watchdog_report_mode():
+    import time
+
+    from pytorchdistributed_amd import _native
+
+    wd = _native.C().Watchdog(0.2, 0, "report", 17, 0.05)
+    t = wd.arm("bucket 0")
+    ok = wd.arm("quick", 10.0)
+    assert wd.disarm(ok)
+    time.sleep(0.5)
+    assert wd.expired() == ["bucket 0"] and len(wd.pending()) == 1
+    assert wd.disarm(t) and wd.pending() == []
+    wd.stop()

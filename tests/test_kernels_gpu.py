@@ -77,30 +77,36 @@ CONV_CASES = [
     (2, 32, 32, 8, 64, 7, 2, 3),
     (3, 7, 7, 512, 2048, 1, 1, 0),
     (1, 9, 11, 24, 40, 3, 1, 1),
+    (8, 28, 28, 64, 64, 1, 1, 0),       # deep split-K wgrad, 64-row tiles
+    (2, 14, 14, 64, 128, 3, 2, 1),      # even size, stride-2 phases
+    (2, 13, 10, 32, 48, 3, 3, 1),       # stride 3: 9 phases, some with no taps
+    (2, 12, 12, 32, 64, 3, 1, 2, 2),    # dilation 2 (stride-1 phased dgrad)
+    (2, 13, 13, 32, 64, 3, 2, 2, 2),    # dilation 2 + stride 2: folded dgrad
 ]
 
 
-def _conv_ref(x, w, stride, pad):
-    return F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), None, stride, pad).permute(0, 2, 3, 1)
+def _conv_ref(x, w, stride, pad, dil=1):
+    return F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), None, stride, pad, dil).permute(0, 2, 3, 1)
 
 
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_fwd_dgrad_wgrad(case):
-    N, H, W, Cin, Cout, k, s, p = case
+    N, H, W, Cin, Cout, k, s, p = case[:8]
+    d = case[8] if len(case) > 8 else 1
     torch.manual_seed(1)
     x = torch.randn(N, H, W, Cin).to(torch.bfloat16).float().requires_grad_()
     w = (torch.randn(Cout, k, k, Cin) / math.sqrt(Cin * k * k)).to(torch.bfloat16).float().requires_grad_()
-    y = _conv_ref(x, w, s, p)
+    y = _conv_ref(x, w, s, p, d)
     dy = torch.randn_like(y).to(torch.bfloat16).float()
     y.backward(dy)
-    yg = C().conv_fwd(bf(x.detach()), bf(w.detach()), s, p, 1, None, False)
+    yg = C().conv_fwd(bf(x.detach()), bf(w.detach()), s, p, d, None, False)
     assert yg.shape == y.shape
     assert rel_err(yg.cpu(), y.detach()) < 1e-2
-    dx = C().conv_dgrad(bf(dy), bf(w.detach()), H, W, s, p, 1)
+    dx = C().conv_dgrad(bf(dy), bf(w.detach()), H, W, s, p, d)
     assert rel_err(dx.cpu(), x.grad) < 1e-2
-    dw = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, 1, True, None)
+    dw = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, d, True, None)
     assert rel_err(dw.cpu(), w.grad) < 1e-3
-    dwb = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, 1, False, None)
+    dwb = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, d, False, None)
     assert rel_err(dwb.cpu(), w.grad) < 1e-2
 
 
@@ -243,12 +249,12 @@ def test_grad_norm():
 
 # ----------------------------------------------------------------------------- norms / activations / simt
 @pytest.mark.parametrize("rms", [False, True])
-@pytest.mark.parametrize("D", [64, 1024, 1600, 4096])
-def test_rownorm(rms, D):
+@pytest.mark.parametrize("D,rows", [(64, 37), (1024, 37), (1024, 2500), (1600, 37), (4096, 300), (8192, 130)])
+def test_rownorm(rms, D, rows):
     from pytorchdistributed_amd.ops import layer_norm, rms_norm
 
     torch.manual_seed(7)
-    x = (torch.randn(37, D) * 2 + 0.3).to(torch.bfloat16).float()
+    x = (torch.randn(rows, D) * 2 + 0.3).to(torch.bfloat16).float()
     g = torch.rand(D) + 0.5
     b = torch.randn(D)
     xr = x.clone().requires_grad_()
@@ -269,6 +275,15 @@ def test_rownorm(rms, D):
     assert rel_err(gg.grad.cpu(), gr.grad) < 2e-2
     if not rms:
         assert rel_err(bg.grad.cpu(), br.grad) < 2e-2
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 8), (37, 64), (5000, 1024), (300, 1600), (64, 50304), (33, 5)])
+def test_colsum(rows, cols):
+    x = torch.randn(rows, cols)
+    for dt in (torch.float32, torch.bfloat16):
+        xd = x.to(dt)
+        out = C().colsum(xd.to(DEV)).cpu()
+        assert rel_err(out, xd.float().sum(0)) < 1e-5
 
 
 def test_activations():
@@ -321,6 +336,27 @@ def test_linear_op_all_paths():
         tol = 1e-5 if dtype == torch.float32 else 2e-2
         for a, r in [(yg, y), (xg.grad, xr.grad), (wg.grad, wr.grad), (bg.grad, br.grad)]:
             assert rel_err(a.cpu(), r.detach()) < tol
+
+
+@pytest.mark.parametrize("mode", ["native", "blas"])
+def test_linear_gemm_backends(mode, monkeypatch):
+    """Plain bf16 Linear through the native MFMA kernel and through hipBLASLt, fwd + bwd vs fp32."""
+    from pytorchdistributed_amd.ops import linear
+
+    monkeypatch.setenv("PDA_GEMM", mode)
+    torch.manual_seed(9)
+    x = torch.randn(300, 256).to(torch.bfloat16).float()
+    w = (torch.randn(136, 256) * 0.05).to(torch.bfloat16).float()
+    b = torch.randn(136).to(torch.bfloat16).float()
+    xr, wr, br = (t.clone().requires_grad_() for t in (x, w, b))
+    y = F.linear(xr, wr, br)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    xg, wg, bg = (t.to(DEV, torch.bfloat16).requires_grad_() for t in (x, w, b))
+    yg = linear(xg, wg, bg)
+    yg.backward(dy.to(DEV, torch.bfloat16))
+    for a, r in [(yg, y), (xg.grad, xr.grad), (wg.grad, wr.grad), (bg.grad, br.grad)]:
+        assert rel_err(a.cpu(), r.detach()) < 2e-2
 
 
 def test_synth_fill_statistics():
