@@ -187,14 +187,14 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optio
   c10::DeviceGuard g(x.device());
   Tensor y = at::empty_like(x);
   auto fo = x.options().dtype(at::kFloat);
-  Tensor mean = at::empty({C}, fo), invstd = at::empty({C}, fo);
+  Tensor mean = at::empty({C}, fo), invstd = at::empty({C}, fo), ss = at::empty({2, C}, fo);
   Tensor ws = at::empty({pda::bn_workspace_floats(M, C)}, fo);
   CHECK_HIP_OK(pda::bn_fwd_train(bp(x), res ? bp(*res) : nullptr, bpm(y), M, C, gf, gb, bfp, bb,
                                  running_mean ? running_mean->data_ptr<float>() : nullptr,
                                  running_var ? running_var->data_ptr<float>() : nullptr, (float)momentum, (float)eps,
-                                 relu, mean.data_ptr<float>(), invstd.data_ptr<float>(), ws.data_ptr<float>(),
-                                 stream_of(x)));
-  return {y, mean, invstd};
+                                 relu, mean.data_ptr<float>(), invstd.data_ptr<float>(), ss.data_ptr<float>(),
+                                 ws.data_ptr<float>(), stream_of(x)));
+  return {y, mean, invstd, ss};
 }
 
 Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
@@ -218,17 +218,21 @@ Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> ga
   return y;
 }
 
-std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor mean, Tensor invstd,
-                           c10::optional<Tensor> gamma, bool relu, bool want_dres, c10::optional<Tensor> dgamma_out,
-                           c10::optional<Tensor> dbeta_out) {
+std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::optional<Tensor> ss, Tensor mean,
+                           Tensor invstd, c10::optional<Tensor> gamma, bool relu, bool want_dres,
+                           c10::optional<Tensor> dgamma_out, c10::optional<Tensor> dbeta_out) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   TORCH_CHECK(dy.sizes() == x.sizes());
   const int64_t C = x.size(-1), M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "channels must be a multiple of 8 and <= 2048");
   if (relu) {
-    TORCH_CHECK(y.has_value(), "relu backward needs the saved output");
-    check_bf16(*y, "y");
+    TORCH_CHECK(y.has_value() || ss.has_value(), "relu backward needs the saved output or scale/shift");
+    if (y.has_value()) check_bf16(*y, "y");
+    else {
+      check_f32(*ss, "ss");
+      TORCH_CHECK(ss->numel() == 2 * C);
+    }
   }
   check_f32(mean, "mean");
   check_f32(invstd, "invstd");
@@ -247,7 +251,8 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor 
   check_gpu(dbeta, "dbeta");
   const bool pb = pdt == at::kBFloat16;
   Tensor ws = at::empty({pda::bn_workspace_floats(M, C)}, x.options().dtype(at::kFloat));
-  CHECK_HIP_OK(pda::bn_bwd(bp(dy), bp(x), relu ? bp(*y) : nullptr, M, C, mean.data_ptr<float>(),
+  const float* ssp = (relu && !y.has_value()) ? ss->data_ptr<float>() : nullptr;
+  CHECK_HIP_OK(pda::bn_bwd(bp(dy), bp(x), (relu && y.has_value()) ? bp(*y) : nullptr, ssp, M, C, mean.data_ptr<float>(),
                            invstd.data_ptr<float>(), gf, gb, relu, bpm(dx), want_dres ? bpm(dres) : nullptr,
                            pb ? nullptr : dgamma.data_ptr<float>(), pb ? bpm(dgamma) : nullptr,
                            pb ? nullptr : dbeta.data_ptr<float>(), pb ? bpm(dbeta) : nullptr, ws.data_ptr<float>(),

@@ -54,14 +54,16 @@ int64_t bn_workspace_floats(int64_t M, int64_t C);
 hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
                         const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, float* running_mean,
                         float* running_var, float momentum, float eps, bool relu, float* save_mean,
-                        float* save_invstd, float* ws, hipStream_t st);
+                        float* save_invstd, float* save_ss, float* ws, hipStream_t st);
 hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
                        const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, const float* running_mean,
                        const float* running_var, float eps, bool relu, float* ws, hipStream_t st);
-hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, int64_t M, int64_t C, const float* save_mean,
-                  const float* save_invstd, const float* gamma_f, const bf16_t* gamma_b, bool relu, bf16_t* dx,
-                  bf16_t* dres, float* dgamma_f, bf16_t* dgamma_b, float* dbeta_f, bf16_t* dbeta_b, float* ws,
-                  hipStream_t st);
+// relu: the mask comes from y when given, else from x * ss[0:C] + ss[C:2C] (scale/shift saved by
+// bn_fwd_train; BN+ReLU without residual never materialises y for the backward)
+hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* ss, int64_t M, int64_t C,
+                  const float* save_mean, const float* save_invstd, const float* gamma_f, const bf16_t* gamma_b,
+                  bool relu, bf16_t* dx, bf16_t* dres, float* dgamma_f, bf16_t* dgamma_b, float* dbeta_f,
+                  bf16_t* dbeta_b, float* ws, hipStream_t st);
 
 // ---- pool.hip (NHWC, C % 8 == 0)
 hipError_t maxpool2d_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int k,

@@ -45,11 +45,12 @@ BnGeom bn_geom(int64_t M, int64_t C) {
     g.rpi = kThreads / g.cv;
     g.gy = 1;
   }
-  // ~256 row blocks: one per CU is enough for these streaming reductions (each lane keeps 4 rows of
-  // loads in flight) and keeps the partial slabs small for the finalize pass.
-  const int target = 256 / g.gy > 0 ? 256 / g.gy : 1;
+  // ~1024 row blocks (4 workgroups per CU, 8 outstanding 16-B loads per lane: ~64 KB in flight per
+  // CU, what HBM3E latency x bandwidth asks for); >= 64 rows per block keeps the partial slabs that
+  // the finalize pass sums small for the wide (C = 2048) layers.
+  const int target = 1024 / g.gy > 0 ? 1024 / g.gy : 1;
   int64_t rpb = (M + target - 1) / target;
-  const int64_t min_rpb = (int64_t)g.rpi * 8;
+  const int64_t min_rpb = (int64_t)g.rpi * 8 > 64 ? (int64_t)g.rpi * 8 : 64;
   if (rpb < min_rpb) rpb = min_rpb;
   g.rpb = rpb;
   g.nrb = (int)((M + rpb - 1) / rpb);
@@ -134,12 +135,12 @@ __global__ void __launch_bounds__(kThreads) bn_stats_kernel(const bf16_t* __rest
   if (active) {
     load8(x + vcol * 8, piv);  // row 0 is the pivot
     int64_t r = r0 + ty;
-    for (; r + 3 * rpi < r1; r += 4 * rpi) {  // 4 independent 16-B loads in flight per lane
-      float v[4][8];
+    for (; r + 7 * rpi < r1; r += 8 * rpi) {  // 8 independent 16-B loads in flight per lane
+      float v[8][8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) load8(x + (r + u * rpi) * C + vcol * 8, v[u]);
+      for (int u = 0; u < 8; ++u) load8(x + (r + u * rpi) * C + vcol * 8, v[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < 8; ++u)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float d = v[u][j] - piv[j];
@@ -243,10 +244,27 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16_t* __rest
 }
 
 // ---------------------------------------------------------------- backward reduction
-template <bool RELU>
+// MASK: 0 no ReLU; 1 ReLU mask from the saved output y; 2 ReLU mask recomputed from x and the
+// forward's per-channel scale/shift (BN+ReLU without residual: y is never saved or re-read).
+template <int MASK>
+__device__ __forceinline__ void relu_mask(float (&g)[8], const bf16_t* __restrict__ y, const float (&xv)[8],
+                                          const float* __restrict__ sc, const float* __restrict__ sh, int64_t off,
+                                          int c0) {
+  if constexpr (MASK == 1) {
+    const u16x8 yr = *reinterpret_cast<const u16x8*>(y + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = bf2f(yr[j]) > 0.f ? g[j] : 0.f;
+  } else if constexpr (MASK == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = xv[j] * sc[c0 + j] + sh[c0 + j] > 0.f ? g[j] : 0.f;
+  }
+}
+
+template <int MASK>
 __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy,
                                                                  const bf16_t* __restrict__ x,
                                                                  const bf16_t* __restrict__ y,
+                                                                 const float* __restrict__ ss,
                                                                  const float* __restrict__ mean, int64_t M, int C,
                                                                  int cols, int rpi, int64_t rpb,
                                                                  float* __restrict__ slab) {
@@ -255,22 +273,37 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* _
   const bool active = ty < rpi && vcol * 8 < C;
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
   const int64_t r1 = min(r0 + rpb, M);
+  const int c0 = vcol * 8;
   float sa[8], sb[8], mu[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.f;
   if (active) {
-    load8(mean + vcol * 8, mu);
-#pragma unroll 2
-    for (int64_t r = r0 + ty; r < r1; r += rpi) {
-      const int64_t off = r * C + vcol * 8;
+    load8(mean + c0, mu);
+    int64_t r = r0 + ty;
+    for (; r + 3 * rpi < r1; r += 4 * rpi) {  // 4 rows x 2 tensors = 8 loads in flight per lane
+      float g[4][8], xv[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t off = (r + u * rpi) * C + c0;
+        load8(dy + off, g[u]);
+        load8(x + off, xv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        relu_mask<MASK>(g[u], y, xv[u], ss, ss + C, (r + u * rpi) * C + c0, c0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sa[j] += g[u][j];
+          sb[j] += g[u][j] * (xv[u][j] - mu[j]);
+        }
+      }
+    }
+    for (; r < r1; r += rpi) {
+      const int64_t off = r * C + c0;
       float g[8], xv[8];
       load8(dy + off, g);
       load8(x + off, xv);
-      if (RELU) {
-        u16x8 yr = *reinterpret_cast<const u16x8*>(y + off);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = bf2f(yr[j]) > 0.f ? g[j] : 0.f;
-      }
+      relu_mask<MASK>(g, y, xv, ss, ss + C, off, c0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         sa[j] += g[j];
@@ -306,14 +339,17 @@ __global__ void __launch_bounds__(kFinThreads) bn_bwd_finalize_kernel(
   coef[2 * C + c] = -A * sdz * invM - B * mu;
 }
 
-template <bool RELU, bool DRES>
+template <int MASK, bool DRES>
 __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy,
                                                                 const bf16_t* __restrict__ x,
-                                                                const bf16_t* __restrict__ y, int64_t M, int C,
+                                                                const bf16_t* __restrict__ y,
+                                                                const float* __restrict__ ss, int64_t M, int C,
                                                                 const float* __restrict__ coef,
                                                                 bf16_t* __restrict__ dx, bf16_t* __restrict__ dres) {
-  __shared__ __attribute__((aligned(16))) float s_co[3 * kMaxC];
+  __shared__ __attribute__((aligned(16))) float s_co[5 * kMaxC];
   for (int c = threadIdx.x; c < 3 * C; c += blockDim.x) s_co[c] = coef[c];
+  if (MASK == 2)
+    for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) s_co[3 * C + c] = ss[c];
   __syncthreads();
   const float* s_A = s_co;
   const float* s_B = s_co + C;
@@ -326,11 +362,7 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16_t* __
     float g[8], xv[8];
     load8(dy + v * 8, g);
     load8(x + v * 8, xv);
-    if (RELU) {
-      u16x8 yr = *reinterpret_cast<const u16x8*>(y + v * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = bf2f(yr[j]) > 0.f ? g[j] : 0.f;
-    }
+    relu_mask<MASK>(g, y, xv, s_co + 3 * C, s_co + 4 * C, v * 8, c0);
     if (DRES) store8(dres + v * 8, g);
 #pragma unroll
     for (int j = 0; j < 8; ++j) xv[j] = s_A[c0 + j] * g[j] + s_B[c0 + j] * xv[j] + s_C[c0 + j];
@@ -359,10 +391,10 @@ int64_t bn_workspace_floats(int64_t M, int64_t C) {
 hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
                         const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, float* running_mean,
                         float* running_var, float momentum, float eps, bool relu, float* save_mean,
-                        float* save_invstd, float* ws, hipStream_t st) {
+                        float* save_invstd, float* save_ss, float* ws, hipStream_t st) {
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C);
-  float* scale = ws + 2 * (int64_t)g.nrb * C;
+  float* scale = save_ss ? save_ss : ws + 2 * (int64_t)g.nrb * C;
   float* shift = scale + C;
   bn_stats_kernel<<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(x, M, (int)C, g.cols, g.rpi, g.rpb, ws);
   PDA_CHECK_HIP(hipGetLastError());
@@ -386,33 +418,34 @@ hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M,
   return launch_apply(x, res, y, M, (int)C, scale, shift, relu, st);
 }
 
-hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, int64_t M, int64_t C, const float* save_mean,
-                  const float* save_invstd, const float* gamma_f, const bf16_t* gamma_b, bool relu, bf16_t* dx,
-                  bf16_t* dres, float* dgamma_f, bf16_t* dgamma_b, float* dbeta_f, bf16_t* dbeta_b, float* ws,
-                  hipStream_t st) {
+hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* ss, int64_t M, int64_t C,
+                  const float* save_mean, const float* save_invstd, const float* gamma_f, const bf16_t* gamma_b,
+                  bool relu, bf16_t* dx, bf16_t* dres, float* dgamma_f, bf16_t* dgamma_b, float* dbeta_f,
+                  bf16_t* dbeta_b, float* ws, hipStream_t st) {
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
+  if (relu && !y && !ss) return hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C);
   float* coef = ws + 2 * (int64_t)g.nrb * C;
-  if (relu)
-    bn_bwd_reduce_kernel<true><<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(dy, x, y, save_mean, M, (int)C, g.cols, g.rpi,
-                                                                       g.rpb, ws);
+  const int mask = !relu ? 0 : (y ? 1 : 2);
+  const dim3 rg(g.nrb, g.gy);
+  if (mask == 0)
+    bn_bwd_reduce_kernel<0><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
+  else if (mask == 1)
+    bn_bwd_reduce_kernel<1><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
   else
-    bn_bwd_reduce_kernel<false><<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(dy, x, y, save_mean, M, (int)C, g.cols,
-                                                                        g.rpi, g.rpb, ws);
+    bn_bwd_reduce_kernel<2><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
   PDA_CHECK_HIP(hipGetLastError());
   bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(ws, g.nrb, M, (int)C, save_mean,
                                                                          save_invstd, gamma_f, gamma_b, dgamma_f,
                                                                          dgamma_b, dbeta_f, dbeta_b, coef);
   PDA_CHECK_HIP(hipGetLastError());
   const int grid = ew_grid(M * C / 8);
-  if (relu && dres)
-    bn_bwd_apply_kernel<true, true><<<grid, kThreads, 0, st>>>(dy, x, y, M, (int)C, coef, dx, dres);
-  else if (relu)
-    bn_bwd_apply_kernel<true, false><<<grid, kThreads, 0, st>>>(dy, x, y, M, (int)C, coef, dx, dres);
-  else if (dres)
-    bn_bwd_apply_kernel<false, true><<<grid, kThreads, 0, st>>>(dy, x, y, M, (int)C, coef, dx, dres);
-  else
-    bn_bwd_apply_kernel<false, false><<<grid, kThreads, 0, st>>>(dy, x, y, M, (int)C, coef, dx, dres);
+#define BWD_APPLY(MK, DR) \
+  bn_bwd_apply_kernel<MK, DR><<<grid, kThreads, 0, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres)
+  if (mask == 0) { if (dres) BWD_APPLY(0, true); else BWD_APPLY(0, false); }
+  else if (mask == 1) { if (dres) BWD_APPLY(1, true); else BWD_APPLY(1, false); }
+  else { if (dres) BWD_APPLY(2, true); else BWD_APPLY(2, false); }
+#undef BWD_APPLY
   return hipGetLastError();
 }
 

@@ -648,8 +648,15 @@ Plan plan_gemm(int64_t M, int64_t N, int64_t K, bool allow_split, int target_blo
   return p;
 }
 
-// conv wgrad: M = Cout, N = R*S*C are small, K = N*P*Q is huge -> deep split-K
-Plan plan_wgrad(int64_t M, int64_t N, int64_t K, bool allow_split) { return plan_gemm(M, N, K, allow_split, 1024, 256); }
+// conv wgrad: M = Cout, N = R*S*C are small, K = N*P*Q is huge -> deep split-K, ~4 workgroups per CU,
+// with the fp32 partial slabs (written and re-read once) capped at 16 MB so the split traffic stays
+// small next to the operands.
+Plan plan_wgrad(int64_t M, int64_t N, int64_t K, bool allow_split) {
+  int64_t cap = ((int64_t)16 << 20) / (M * N * 4);
+  if (cap > 1024) cap = 1024;
+  if (cap < 1) cap = 1;
+  return plan_gemm(M, N, K, allow_split, 1024, (int)cap);
+}
 
 template <int BM, int BN, class LA, class LB>
 hipError_t launch(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, const Plan& p, Epi epi,

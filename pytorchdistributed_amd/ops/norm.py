@@ -19,21 +19,25 @@ class _BatchNormFn(torch.autograd.Function):
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()
+        ss = None
         if training:
-            y, mean, invstd = C().bn_fwd_train(x, residual, gamma, beta, running_mean, running_var, momentum, eps,
-                                               relu)
+            y, mean, invstd, ss = C().bn_fwd_train(x, residual, gamma, beta, running_mean, running_var, momentum,
+                                                   eps, relu)
         else:
             y = C().bn_fwd_eval(x, residual, gamma, beta, running_mean, running_var, eps, relu)
             mean = running_mean
             invstd = torch.rsqrt(running_var + eps)
-        ctx.save_for_backward(x, y if relu else None, mean, invstd, gamma)
+        # BN+ReLU without a residual: the backward recomputes the ReLU mask from x and the saved
+        # per-channel scale/shift, so y is neither kept alive nor re-read (one fewer HBM pass)
+        keep_y = relu and residual is not None
+        ctx.save_for_backward(x, y if keep_y else None, ss if (relu and not keep_y) else None, mean, invstd, gamma)
         ctx.cfg = (relu, residual is not None, training)
         ctx.beta = beta
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, mean, invstd, gamma = ctx.saved_tensors
+        x, y, ss, mean, invstd, gamma = ctx.saved_tensors
         relu, has_res, training = ctx.cfg
         if not training:
             raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
@@ -41,7 +45,7 @@ class _BatchNormFn(torch.autograd.Function):
         tb = grad_target(ctx.beta) if ctx.beta is not None and ctx.needs_input_grad[2] else None
         if (tg is None) != (tb is None):
             tg = tb = None
-        dx, dres, dgamma, dbeta = C().bn_bwd(dy.contiguous(), x, y, mean, invstd, gamma, relu, has_res, tg, tb)
+        dx, dres, dgamma, dbeta = C().bn_bwd(dy.contiguous(), x, y, ss, mean, invstd, gamma, relu, has_res, tg, tb)
         dg = dgamma if gamma is not None and ctx.needs_input_grad[1] else None
         db = dbeta if ctx.needs_input_grad[2] else None
         return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None

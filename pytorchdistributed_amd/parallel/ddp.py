@@ -14,7 +14,11 @@ MI355X-first design:
   default to 32 MB (every peer gets >= 4 MB per ring step) with a small 2 MB first bucket to start
   communicating early in backward (SURVEY §5.8);
 * averaging uses ``ReduceOp.AVG`` on RCCL (no extra pass); on gloo / the native host ring the sum is
-  divided in place.
+  divided in place;
+* every bucket collective is armed on the native collective watchdog and disarmed once
+  its work completed; ``comm_stats()`` reports bytes, calls and the EXPOSED communication time — HIP
+  events around the compute stream's wait on the bucket all-reduces, i.e. the part of communication
+  not hidden behind backward (SURVEY §5.1 overlap ratio).
 """
 from __future__ import annotations
 
@@ -28,6 +32,8 @@ import torch.nn as tnn
 
 from .. import _native
 from .. import distributed as pdist
+from ..utils import timing as _timing
+from ..utils import watchdog as _watchdog
 from .flat import FlatGroup, flatten_buffers
 
 _DTYPE_IDS = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}
@@ -54,6 +60,10 @@ class DistributedDataParallel(tnn.Module):
         self.require_backward_grad_sync = True
         bucket_cap_mb = bucket_cap_mb if bucket_cap_mb is not None else _mb("PDA_BUCKET_MB", 32)
         first_bucket_mb = first_bucket_mb if first_bucket_mb is not None else _mb("PDA_FIRST_BUCKET_MB", 2)
+        self.track_comm = bool(os.environ.get("PDA_METRICS_DIR")) or os.environ.get("PDA_TRACK_COMM") == "1"
+        self._stats = {"comm_bytes": 0, "comm_calls": 0}
+        self._exposed_events: List = []
+        self._tickets: List = []
 
         params = [p for p in module.parameters() if p.requires_grad]
         self._params = params
@@ -113,14 +123,32 @@ class DistributedDataParallel(tnn.Module):
         t = self._bucket_view(b)
         if self.world == 1:
             return
+        nbytes = t.numel() * t.element_size()
+        self._stats["comm_bytes"] += nbytes
+        self._stats["comm_calls"] += 1
         if self._use_ring() and t.device.type == "cpu" and t.dtype in (torch.float32, torch.float64):
-            pdist.ring_all_reduce(t, average=True)
+            with _watchdog.watch(f"ddp host-ring all_reduce bucket {b} ({nbytes / 2**20:.1f} MB)"):
+                pdist.ring_all_reduce(t, average=True)
             return
-        if self.backend == "nccl":
-            self._works.append((dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.process_group,
-                                                async_op=True), None))
-        else:
-            self._works.append((dist.all_reduce(t, group=self.process_group, async_op=True), t))
+        ticket = _watchdog.arm(f"ddp all_reduce bucket {b} ({nbytes / 2**20:.1f} MB, {t.dtype})")
+        with _timing.range(f"ddp.all_reduce.b{b}"):
+            if self.backend == "nccl":
+                work = dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
+                self._works.append((work, None))
+            else:
+                work = dist.all_reduce(t, group=self.process_group, async_op=True)
+                self._works.append((work, t))
+        self._tickets.append((ticket, work))
+
+    def _sweep_tickets(self, force: bool = False):
+        """Disarm the watchdog tickets of completed collectives (RCCL works complete asynchronously)."""
+        keep = []
+        for ticket, work in self._tickets:
+            if force or work.is_completed():
+                _watchdog.disarm(ticket)
+            else:
+                keep.append((ticket, work))
+        self._tickets = keep
 
     def _make_hook(self, i: int):
         def hook(p: torch.Tensor):
@@ -156,17 +184,40 @@ class DistributedDataParallel(tnn.Module):
                 g.grad_view(g.index[id(p)]).zero_()
             for b in self.reducer.flush_unready():
                 self._launch(b)
+        ev = None
+        if self.track_comm and self._works and torch.cuda.is_available() and self.backend == "nccl":
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         for work, t in self._works:
             work.wait()
             if t is not None:
                 t.div_(self.world)
+        if ev is not None:
+            ev[1].record()
+            self._exposed_events.append(ev)
         self._works.clear()
+        if self.backend != "nccl":
+            self._sweep_tickets(force=True)  # gloo waits were blocking: all done
         for g in self.groups.values():
             g.attach_grads()
         self.reducer.prepare()
 
     # ------------------------------------------------------------------ module API
+    def comm_stats(self, reset: bool = True) -> dict:
+        """Bytes / calls of gradient all-reduce since the last reset and, when tracking is on
+        (``PDA_METRICS_DIR`` or ``PDA_TRACK_COMM=1``), the exposed communication time in ms."""
+        out = dict(self._stats)
+        if self._exposed_events:
+            self._exposed_events[-1][1].synchronize()
+            out["exposed_comm_ms"] = sum(a.elapsed_time(b) for a, b in self._exposed_events)
+        if reset:
+            self._stats = {"comm_bytes": 0, "comm_calls": 0}
+            self._exposed_events = []
+        return out
+
     def forward(self, *args, **kwargs):
+        if self._tickets:
+            self._sweep_tickets()
         if self.broadcast_buffers and self.world > 1 and self.module.training and self._buffer_flats:
             with torch.no_grad():
                 for flat in self._buffer_flats.values():

@@ -111,7 +111,8 @@ def test_conv_fwd_dgrad_wgrad(case):
 
 
 # ----------------------------------------------------------------------------- batch norm
-@pytest.mark.parametrize("shape", [(4, 8, 8, 64), (2, 7, 7, 2048), (3, 5, 5, 200), (2, 56, 56, 256)])
+@pytest.mark.parametrize("shape", [(4, 8, 8, 64), (2, 7, 7, 2048), (3, 5, 5, 200), (2, 56, 56, 256),
+                                   (64, 28, 28, 64)])
 @pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
 def test_batchnorm_train(shape, relu, res):
     torch.manual_seed(2)
@@ -133,16 +134,19 @@ def test_batchnorm_train(shape, relu, res):
     y.backward(dy)
 
     rmg, rvg = torch.zeros(Cc, device=DEV), torch.ones(Cc, device=DEV)
-    yg, mean, invstd = C().bn_fwd_train(bf(x), bf(r) if res else None, g.to(DEV), b.to(DEV), rmg, rvg, 0.1, 1e-5,
-                                        relu)
+    yg, mean, invstd, ss = C().bn_fwd_train(bf(x), bf(r) if res else None, g.to(DEV), b.to(DEV), rmg, rvg, 0.1,
+                                            1e-5, relu)
     assert rel_err(yg.cpu(), y.detach()) < 1e-2
     assert rel_err(rmg.cpu(), rm) < 1e-4 and rel_err(rvg.cpu(), rv) < 1e-4
-    dx, dres, dgamma, dbeta = C().bn_bwd(bf(dy), bf(x), yg, mean, invstd, g.to(DEV), relu, res, None, None)
-    assert rel_err(dx.cpu(), xr.grad) < 2e-2
-    assert rel_err(dgamma.cpu(), gr.grad) < 1e-2
-    assert rel_err(dbeta.cpu(), br.grad) < 1e-2
-    if res:
-        assert rel_err(dres.cpu(), rr.grad) < 1e-2
+    # the ReLU mask from the saved output, and (no residual) recomputed from x and scale/shift
+    for use_y in ([True, False] if relu and not res else [True]):
+        dx, dres, dgamma, dbeta = C().bn_bwd(bf(dy), bf(x), yg if use_y else None, None if use_y else ss, mean,
+                                             invstd, g.to(DEV), relu, res, None, None)
+        assert rel_err(dx.cpu(), xr.grad) < 2e-2
+        assert rel_err(dgamma.cpu(), gr.grad) < 1e-2
+        assert rel_err(dbeta.cpu(), br.grad) < 1e-2
+        if res:
+            assert rel_err(dres.cpu(), rr.grad) < 1e-2
 
 
 def test_batchnorm_eval():

@@ -8,11 +8,14 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
+import sys
 
 import torch
 import torch.nn.functional as F
 
-from pytorchdistributed_amd._native import C
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pytorchdistributed_amd._native import C  # noqa: E402
 
 # (H, Cin, Cout, R, stride) for every distinct ResNet-50 conv (input spatial size H)
 RESNET_CONVS = [
