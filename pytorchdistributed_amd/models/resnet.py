@@ -69,6 +69,8 @@ class Stem(tnn.Module):
 
 
 class ResNet(tnn.Module):
+    nhwc = True  # activations are channels-last end to end (utils.summary reports NCHW shapes)
+
     def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, device=None, dtype=None):
         super().__init__()
         kw = dict(device=device, dtype=dtype)
