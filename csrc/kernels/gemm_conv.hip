@@ -56,17 +56,30 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
   return f.d == 1 ? n : (__umulhi(n, f.mul) >> f.shr);
 }
 
-__device__ __forceinline__ u16x8 zero8() {
-  u16x8 z;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) z[j] = 0;
-  return z;
-}
-
 // ------------------------------------------------------------------ operand loaders
-// A K-major loader feeds a [R][BK] tile: thread t owns k-chunk (t & 7) of rows (t >> 3) + 32 i.
-// An MN-major loader feeds a [BK][R] tile: thread t owns column chunk (t % (R/8)) of
-// k-rows t / (R/8) + (NT / (R/8)) i.  Both produce R/32 16-byte chunks per thread per tile.
+// Operands go global -> LDS directly with `global_load_lds_dwordx4` (no VGPR staging, no ds_write):
+// the LDS destination of one wave instruction is a wave-uniform base + lane x 16 B, so the swizzled
+// LDS images below are produced by choosing, per lane, WHICH global 16-B chunk it fetches.  Round i
+// of thread t always lands at tile byte i*4096 + t*16.  Invalid (padding / out-of-range) lanes fetch
+// from a zero page, which makes the gathers of the implicit-GEMM convolutions branch-free.
+//   K-major tile [R][64]:  thread t fills row (t >> 3) + 32 i, logical k-chunk (t & 7) ^ ((t >> 3) & 7)
+//   MN-major tile [64][R]: thread t fills k-row t / (R/8) + KSTEP i, column mn_col<R>(t)
+// Loaders return R/32 source pointers per thread per K tile.
+
+__device__ __attribute__((aligned(64))) bf16_t g_zero_page[32];
+
+__device__ __forceinline__ int kmaj_chunk(int tid) { return (tid & 7) ^ ((tid >> 3) & 7); }
+
+template <int R>
+__device__ __forceinline__ int mn_swz(int k) {
+  if constexpr (R == 128) return (k & 3) | (((k >> 3) & 1) << 2);
+  else return ((k >> 1) & 1) | (((k >> 3) & 1) << 1);
+}
+template <int R>
+__device__ __forceinline__ int mn_col(int tid) {
+  const int p = tid % (R / 8), k = tid / (R / 8);
+  return ((((p >> 1) ^ mn_swz<R>(k)) & (R / 16 - 1)) << 4) + (p & 1) * 8;
+}
 
 template <int R>
 struct PlainK {  // element (row, k) = p[row * ld + k]
@@ -80,7 +93,7 @@ struct PlainK {  // element (row, k) = p[row * ld + k]
     int kc;
   };
   __device__ void init(State& s, int64_t row0, int tid) const {
-    s.kc = (tid & 7) * 8;
+    s.kc = kmaj_chunk(tid) * 8;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int64_t row = row0 + (tid >> 3) + 32 * i;
@@ -88,11 +101,10 @@ struct PlainK {  // element (row, k) = p[row * ld + k]
       s.ptr[i] = p + (s.ok[i] ? row : 0) * ld + s.kc;
     }
   }
-  __device__ void fetch(const State& s, int64_t k0, u16x8 (&v)[NCH]) const {
+  __device__ void src(const State& s, int64_t k0, const bf16_t* (&q)[NCH]) const {
     const bool kok = k0 + s.kc < K;
 #pragma unroll
-    for (int i = 0; i < NCH; ++i)
-      v[i] = (s.ok[i] && kok) ? *reinterpret_cast<const u16x8*>(s.ptr[i] + k0) : zero8();
+    for (int i = 0; i < NCH; ++i) q[i] = (s.ok[i] && kok) ? s.ptr[i] + k0 : g_zero_page;
   }
 };
 
@@ -100,8 +112,7 @@ template <int R>
 struct PlainMN {  // element (k, col) = p[k * ld + col]
   static constexpr bool kMajor = false;
   static constexpr int NCH = R / 32;
-  static constexpr int CPR = R / 8;
-  static constexpr int KSTEP = NT / CPR;
+  static constexpr int KSTEP = NT / (R / 8);
   const bf16_t* p;
   int64_t K, cols, ld;
   struct State {
@@ -110,16 +121,16 @@ struct PlainMN {  // element (k, col) = p[k * ld + col]
     int krow;
   };
   __device__ void init(State& s, int64_t col0, int tid) const {
-    const int64_t col = col0 + (tid % CPR) * 8;
+    const int64_t col = col0 + mn_col<R>(tid);
     s.ok = col < cols;
     s.base = p + (s.ok ? col : 0);
-    s.krow = tid / CPR;
+    s.krow = tid / (R / 8);
   }
-  __device__ void fetch(const State& s, int64_t k0, u16x8 (&v)[NCH]) const {
+  __device__ void src(const State& s, int64_t k0, const bf16_t* (&q)[NCH]) const {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int64_t k = k0 + s.krow + KSTEP * i;
-      v[i] = (s.ok && k < K) ? *reinterpret_cast<const u16x8*>(s.base + k * ld) : zero8();
+      q[i] = (s.ok && k < K) ? s.base + k * ld : g_zero_page;
     }
   }
 };
@@ -146,7 +157,7 @@ struct ConvFwdK {
     int kc;
   };
   __device__ void init(State& s, int64_t row0, int tid) const {
-    s.kc = (tid & 7) * 8;
+    s.kc = kmaj_chunk(tid) * 8;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int64_t m = row0 + (tid >> 3) + 32 * i;
@@ -161,30 +172,27 @@ struct ConvFwdK {
       s.iw0[i] = q * g.st - g.pad;
     }
   }
-  __device__ void fetch(const State& s, int64_t k0, u16x8 (&v)[NCH]) const {
+  __device__ void src(const State& s, int64_t k0, const bf16_t* (&q)[NCH]) const {
     const int64_t k = k0 + s.kc;
-    if (k >= K) {
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) v[i] = zero8();
-      return;
-    }
-    const uint32_t rs = fdiv((uint32_t)k, g.fC);
-    const int ci = (int)((uint32_t)k - rs * g.C);
+    const bool kok = k < K;
+    const uint32_t kk = kok ? (uint32_t)k : 0u;
+    const uint32_t rs = fdiv(kk, g.fC);
+    const int ci = (int)(kk - rs * g.C);
     const uint32_t r = fdiv(rs, g.fS);
     const int sidx = (int)(rs - r * g.S);
     const int dr = (int)r * g.dil, ds = sidx * g.dil;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int ih = s.ih0[i] + dr, iw = s.iw0[i] + ds;
-      const bool ok = s.ok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const bool ok = kok && s.ok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
       const int64_t off = ((int64_t)(s.nH[i] + ih) * g.W + iw) * g.C + ci;
-      v[i] = ok ? *reinterpret_cast<const u16x8*>(x + off) : zero8();
+      q[i] = ok ? x + off : g_zero_page;
     }
   }
 };
 
-// Conv dgrad A operand: element (m = (n,h,w), k = (r,s,co)) = dy[n, p, q, co] where
-// p*st - pad + r*dil = h (zero when not integral / out of range).  dy has dims [N,P,Q,Cg].
+// Conv dgrad A operand, folded form (stride > 1 with dilation > 1 only): element (m = (n,h,w),
+// k = (r,s,co)) = dy[n, p, q, co] where p*st - pad + r*dil = h (zero when not integral / out of range).
 template <int R>
 struct ConvDgradK {
   static constexpr bool kMajor = true;
@@ -198,7 +206,7 @@ struct ConvDgradK {
     int kc;
   };
   __device__ void init(State& s, int64_t row0, int tid) const {
-    s.kc = (tid & 7) * 8;
+    s.kc = kmaj_chunk(tid) * 8;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int64_t m = row0 + (tid >> 3) + 32 * i;
@@ -211,31 +219,23 @@ struct ConvDgradK {
       s.nP[i] = (int)n * g.P;
     }
   }
-  __device__ void fetch(const State& s, int64_t k0, u16x8 (&v)[NCH]) const {
+  __device__ void src(const State& s, int64_t k0, const bf16_t* (&q)[NCH]) const {
     const int64_t k = k0 + s.kc;
-    if (k >= K) {
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) v[i] = zero8();
-      return;
-    }
-    const uint32_t rs = fdiv((uint32_t)k, g.fC);  // fC divides by Cg here
-    const int co = (int)((uint32_t)k - rs * g.Cg);
+    const bool kok = k < K;
+    const uint32_t kk = kok ? (uint32_t)k : 0u;
+    const uint32_t rs = fdiv(kk, g.fC);  // fC divides by Cg here
+    const int co = (int)(kk - rs * g.Cg);
     const uint32_t r = fdiv(rs, g.fS);
     const int sidx = (int)(rs - r * g.S);
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int ph = s.h[i] + g.pad - (int)r * g.dil;
       const int pw = s.w[i] + g.pad - sidx * g.dil;
-      int p = ph, q = pw;
-      bool ok = s.ok[i] && ph >= 0 && pw >= 0;
-      if (g.st != 1) {
-        p = ph / g.st;
-        q = pw / g.st;
-        ok = ok && p * g.st == ph && q * g.st == pw;
-      }
-      ok = ok && p < g.P && q < g.Q;
-      const int64_t off = ((int64_t)(s.nP[i] + p) * g.Q + q) * g.Cg + co;
-      v[i] = ok ? *reinterpret_cast<const u16x8*>(dy + off) : zero8();
+      const int p = ph / g.st, qq = pw / g.st;
+      const bool ok = kok && s.ok[i] && ph >= 0 && pw >= 0 && p * g.st == ph && qq * g.st == pw && p < g.P &&
+                      qq < g.Q;
+      const int64_t off = ((int64_t)(s.nP[i] + p) * g.Q + qq) * g.Cg + co;
+      q[i] = ok ? dy + off : g_zero_page;
     }
   }
 };
@@ -265,7 +265,7 @@ struct ConvDgradPhaseK {
     int kc;
   };
   __device__ void init(State& s, int64_t row0, int tid) const {
-    s.kc = (tid & 7) * 8;
+    s.kc = kmaj_chunk(tid) * 8;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int64_t m = row0 + (tid >> 3) + 32 * i;
@@ -278,24 +278,21 @@ struct ConvDgradPhaseK {
       s.nP[i] = (int)n * g.P;
     }
   }
-  __device__ void fetch(const State& s, int64_t k0, u16x8 (&v)[NCH]) const {
+  __device__ void src(const State& s, int64_t k0, const bf16_t* (&q)[NCH]) const {
     const int64_t k = k0 + s.kc;
-    if (k >= K) {
-#pragma unroll
-      for (int i = 0; i < NCH; ++i) v[i] = zero8();
-      return;
-    }
-    const uint32_t t = fdiv((uint32_t)k, g.fC);  // fC divides by Cg (= Cout) here
-    const int co = (int)((uint32_t)k - t * g.Cg);
+    const bool kok = k < K;
+    const uint32_t kk = kok ? (uint32_t)k : 0u;
+    const uint32_t t = fdiv(kk, g.fC);  // fC divides by Cg (= Cout) here
+    const int co = (int)(kk - t * g.Cg);
     const uint32_t ri = fdiv(t, ph.fSv);
     const int si = (int)(t - ri * ph.Sv);
     const int dr = ph.base_r - (int)ri * ph.step_r, ds = ph.base_s - si * ph.step_s;
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
-      const int p = s.hh[i] + dr, q = s.ww[i] + ds;
-      const bool ok = s.ok[i] && (unsigned)p < (unsigned)g.P && (unsigned)q < (unsigned)g.Q;
-      const int64_t off = ((int64_t)(s.nP[i] + p) * g.Q + q) * g.Cg + co;
-      v[i] = ok ? *reinterpret_cast<const u16x8*>(dy + off) : zero8();
+      const int p = s.hh[i] + dr, qq = s.ww[i] + ds;
+      const bool ok = kok && s.ok[i] && (unsigned)p < (unsigned)g.P && (unsigned)qq < (unsigned)g.Q;
+      const int64_t off = ((int64_t)(s.nP[i] + p) * g.Q + qq) * g.Cg + co;
+      q[i] = ok ? dy + off : g_zero_page;
     }
   }
 };
@@ -305,8 +302,7 @@ template <int R>
 struct ConvWgradMN {
   static constexpr bool kMajor = false;
   static constexpr int NCH = R / 32;
-  static constexpr int CPR = R / 8;
-  static constexpr int KSTEP = NT / CPR;
+  static constexpr int KSTEP = NT / (R / 8);
   const bf16_t* x;
   ConvGeom g;
   int64_t K, cols;
@@ -316,7 +312,7 @@ struct ConvWgradMN {
     int krow;
   };
   __device__ void init(State& s, int64_t col0, int tid) const {
-    const int64_t col = col0 + (tid % CPR) * 8;
+    const int64_t col = col0 + mn_col<R>(tid);
     s.ok = col < cols;
     const uint32_t cc = s.ok ? (uint32_t)col : 0u;
     const uint32_t rs = fdiv(cc, g.fC);
@@ -324,22 +320,22 @@ struct ConvWgradMN {
     const uint32_t r = fdiv(rs, g.fS);
     s.roff = (int)r * g.dil - g.pad;
     s.soff = (int)(rs - r * g.S) * g.dil - g.pad;
-    s.krow = tid / CPR;
+    s.krow = tid / (R / 8);
   }
-  __device__ void fetch(const State& s, int64_t k0, u16x8 (&v)[NCH]) const {
+  __device__ void src(const State& s, int64_t k0, const bf16_t* (&q)[NCH]) const {
 #pragma unroll
     for (int i = 0; i < NCH; ++i) {
       const int64_t k = k0 + s.krow + KSTEP * i;
       bool ok = s.ok && k < K;
       const uint32_t kk = ok ? (uint32_t)k : 0u;
       const uint32_t t = fdiv(kk, g.fQ);
-      const int q = (int)(kk - t * g.Q);
+      const int qq = (int)(kk - t * g.Q);
       const uint32_t n = fdiv(t, g.fP);
       const int p = (int)(t - n * g.P);
-      const int ih = p * g.st + s.roff, iw = q * g.st + s.soff;
+      const int ih = p * g.st + s.roff, iw = qq * g.st + s.soff;
       ok = ok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
       const int64_t off = ((int64_t)((int)n * g.H + ih) * g.W + iw) * g.C + s.ci;
-      v[i] = ok ? *reinterpret_cast<const u16x8*>(x + off) : zero8();
+      q[i] = ok ? x + off : g_zero_page;
     }
   }
 };
@@ -360,24 +356,16 @@ __device__ __forceinline__ int mn_off(int k, int m) {
   }
 }
 
-template <class L, int R>
-__device__ __forceinline__ void stage_write(char* tile, const typename L::State& s, const u16x8 (&v)[R / 32], int tid) {
-  if constexpr (L::kMajor) {
-    const int chunk = tid & 7;
+// One K tile of an operand: NCH global_load_lds_dwordx4 per thread (see "operand loaders").
+template <class L>
+__device__ __forceinline__ void glds_tile(const L& ld, const typename L::State& st, int64_t k0, char* tile, int wid) {
+  const bf16_t* q[L::NCH];
+  ld.src(st, k0, q);
 #pragma unroll
-    for (int i = 0; i < R / 32; ++i) {
-      const int row = (tid >> 3) + 32 * i;
-      *reinterpret_cast<u16x8*>(tile + kmaj_off(row, chunk)) = v[i];
-    }
-  } else {
-    constexpr int CPR = R / 8, KSTEP = NT / CPR;
-    const int m = (tid % CPR) * 8;
-#pragma unroll
-    for (int i = 0; i < R / 32; ++i) {
-      const int k = tid / CPR + KSTEP * i;
-      *reinterpret_cast<u16x8*>(tile + mn_off<R>(k, m)) = v[i];
-    }
-  }
+  for (int i = 0; i < L::NCH; ++i)
+    __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)q[i],
+                                     (void __attribute__((address_space(3)))*)(tile + i * 4096 + wid * 1024), 16, 0,
+                                     0);
 }
 
 // Fragment for one 16-row group starting at `row0`, k-substep kk (0 or 32):
@@ -457,23 +445,23 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  u16x8 ra[BM / 32], rb[BN / 32];
+  // Two LDS buffers: the DMA of tile t+1 runs while tile t is multiplied; one vmcnt(0) + barrier per
+  // K tile retires it (cdna_hip_programming.md §5 "glds vs register staging").
   if (kt0 < kt1) {
-    la.fetch(sa, (int64_t)kt0 * BK, ra);
-    lb.fetch(sb, (int64_t)kt0 * BK, rb);
-    stage_write<LA, BM>(smem, sa, ra, tid);
-    stage_write<LB, BN>(smem + A_BYTES, sb, rb, tid);
+    glds_tile(la, sa, (int64_t)kt0 * BK, smem, wid);
+    glds_tile(lb, sb, (int64_t)kt0 * BK, smem + A_BYTES, wid);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   for (int kt = kt0; kt < kt1; ++kt) {
     const int buf = (kt - kt0) & 1;
     char* As = smem + buf * (A_BYTES + B_BYTES);
     char* Bs = As + A_BYTES;
-    const bool more = kt + 1 < kt1;
-    if (more) {
-      la.fetch(sa, (int64_t)(kt + 1) * BK, ra);
-      lb.fetch(sb, (int64_t)(kt + 1) * BK, rb);
+    if (kt + 1 < kt1) {
+      char* An = smem + (buf ^ 1) * (A_BYTES + B_BYTES);
+      glds_tile(la, sa, (int64_t)(kt + 1) * BK, An, wid);
+      glds_tile(lb, sb, (int64_t)(kt + 1) * BK, An + A_BYTES, wid);
     }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 32) {
@@ -488,11 +476,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      char* An = smem + (buf ^ 1) * (A_BYTES + B_BYTES);
-      stage_write<LA, BM>(An, sa, ra, tid);
-      stage_write<LB, BN>(An + A_BYTES, sb, rb, tid);
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 

@@ -115,8 +115,11 @@ def spawn(fn: Callable, args: Sequence = (), nprocs: int = 1, join: bool = True,
 def run_workers(cmd: List[str], nproc_per_node: int, nnodes: int = 1, node_rank: int = 0,
                 master_addr: str = "127.0.0.1", master_port: int = 29500, max_restarts: int = 0,
                 monitor_interval: float = 0.1, extra_env: Optional[Dict[str, str]] = None,
-                grace: float = 10.0) -> int:
-    """Launch ``cmd`` once per local rank, supervise, tear down on failure; returns the exit code."""
+                grace: float = 10.0, profile_dir: Optional[str] = None) -> int:
+    """Launch ``cmd`` once per local rank, supervise, tear down on failure; returns the exit code.
+
+    ``profile_dir``: wrap every rank in ``rocprofv3 --kernel-trace --stats`` writing
+    ``<profile_dir>/rank<r>/`` (the program itself follows ``--``)."""
     server = None
     if node_rank == 0:
         server = pdist.start_store_server("0.0.0.0", master_port)
@@ -140,7 +143,12 @@ def run_workers(cmd: List[str], nproc_per_node: int, nnodes: int = 1, node_rank:
                 env["TORCHELASTIC_RESTART_COUNT"] = str(attempt)
                 if extra_env:
                     env.update(extra_env)
-                procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+                rcmd = cmd
+                if profile_dir:
+                    rank = node_rank * nproc_per_node + lr
+                    rcmd = ["rocprofv3", "--kernel-trace", "--stats", "-d", os.path.join(profile_dir, f"rank{rank}"),
+                            "-o", "trace", "--output-format", "csv", "--"] + list(cmd)
+                procs.append(subprocess.Popen(rcmd, env=env, start_new_session=True))
             rc = _supervise(procs, monitor_interval, grace)
             if rc == 0:
                 return 0
