@@ -86,3 +86,24 @@ def test_run_cli_flags_reach_workers(tmp_path):
         env = json.load(open(out + str(r)))
         assert env == {"PDA_METRICS_DIR": "/tmp/m", "PDA_DEBUG": "collectives", "PDA_COLLECTIVE_TIMEOUT_S": "30.0",
                        "RANK": str(r), "WORLD_SIZE": "2"}
+
+
+def test_examples_run_on_cpu(tmp_path):
+    """Chapter examples 01 / 02 (both launch flavours) and BASELINE config 1 run end to end on CPU."""
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="")
+    out = subprocess.run([sys.executable, "examples/01_data_parallel.py"], cwd=ROOT, env=env, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0 and "Outside: input size [32, 10] output_size [32, 5]" in out.stdout
+    out = subprocess.run([sys.executable, "examples/02_ddp_gpus.py", "--max_epochs", "1"], cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and "Batchsize: 32 | Steps: 32" in out.stdout
+    out = subprocess.run([sys.executable, "-m", "pytorchdistributed_amd.run", "--standalone", "--nproc-per-node", "2",
+                          "examples/02_ddp_gpus_torchrun.py", "--max_epochs", "1"], cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.count("Steps: 32") == 2
+    out = subprocess.run([sys.executable, "-m", "pytorchdistributed_amd.run", "--standalone", "--nproc-per-node", "2",
+                          "-m", "pytorchdistributed_amd.bench.mnist_ddp", "--steps", "5", "--warmup", "1",
+                          "--backend", "ring"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["n_ranks"] == 2 and rec["value"] > 0
