@@ -10,6 +10,10 @@
 #include "pda_kernels.h"
 #include "runtime.h"
 
+namespace pda_rt {
+void bind_runtime(pybind11::module& m);
+}
+
 namespace py = pybind11;
 using at::Tensor;
 

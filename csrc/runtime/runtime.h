@@ -1,9 +1,7 @@
 // Native host runtime of pytorchdistributed_amd (SURVEY §2.3 N02 TCPStore/rendezvous, N03 DDP
-// Reducer, §5.8 host ring transport).  CPU-only C++; no HIP or torch dependency.
+// Reducer, §5.8 host ring transport, §5.3 watchdog).  Plain C++17 + POSIX: no HIP, torch or Python
+// dependency (bindings live in bind_runtime.cpp), so it builds into the sanitizer self-test.
 #pragma once
-#include <pybind11/pybind11.h>
-#include <pybind11/stl.h>
-
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -44,13 +42,13 @@ class StoreClient {
   StoreClient(const std::string& host, int port, double timeout_s);
   ~StoreClient();
   void set(const std::string& key, const std::string& value);
-  pybind11::bytes get(const std::string& key);
+  std::string get(const std::string& key);
   int64_t add(const std::string& key, int64_t delta);
   bool check(const std::vector<std::string>& keys);
   void wait(const std::vector<std::string>& keys, double timeout_s);
   bool delete_key(const std::string& key);
   int64_t num_keys();
-  pybind11::bytes compare_set(const std::string& key, const std::string& expected, const std::string& desired);
+  std::string compare_set(const std::string& key, const std::string& expected, const std::string& desired);
   void set_timeout(double t) { timeout_s_ = t; }
   double timeout() const { return timeout_s_; }
 
@@ -158,6 +156,5 @@ class Watchdog {
   std::thread thread_;
 };
 
-void bind_runtime(pybind11::module& m);
 
 }  // namespace pda_rt

@@ -376,15 +376,10 @@ void StoreClient::set(const std::string& key, const std::string& value) {
   request(m, timeout_s_);
 }
 
-pybind11::bytes StoreClient::get(const std::string& key) {
+std::string StoreClient::get(const std::string& key) {
   std::string m(1, (char)GET);
   put_str(m, key);
-  std::string v;
-  {
-    pybind11::gil_scoped_release nogil;
-    v = request(m, timeout_s_);
-  }
-  return pybind11::bytes(v);
+  return request(m, timeout_s_);
 }
 
 int64_t StoreClient::add(const std::string& key, int64_t delta) {
@@ -408,7 +403,6 @@ void StoreClient::wait(const std::vector<std::string>& keys, double timeout_s) {
   std::string m(1, (char)WAIT);
   put_u32(m, (uint32_t)keys.size());
   for (auto& k : keys) put_str(m, k);
-  pybind11::gil_scoped_release nogil;
   request(m, timeout_s > 0 ? timeout_s : timeout_s_);
 }
 
@@ -426,13 +420,13 @@ int64_t StoreClient::num_keys() {
   return v;
 }
 
-pybind11::bytes StoreClient::compare_set(const std::string& key, const std::string& expected,
-                                         const std::string& desired) {
+std::string StoreClient::compare_set(const std::string& key, const std::string& expected,
+                                     const std::string& desired) {
   std::string m(1, (char)CAS);
   put_str(m, key);
   put_str(m, expected);
   put_str(m, desired);
-  return pybind11::bytes(request(m, timeout_s_));
+  return request(m, timeout_s_);
 }
 
 }  // namespace pda_rt

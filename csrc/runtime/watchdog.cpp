@@ -85,7 +85,11 @@ int64_t Watchdog::armed_total() const {
 void Watchdog::loop() {
   std::unique_lock<std::mutex> lk(mu_);
   while (!stop_) {
-    cv_.wait_for(lk, std::chrono::duration<double>(poll_s_));
+    // system_clock: wait_for(steady) lowers to pthread_cond_clockwait, which GCC 11's ThreadSanitizer
+    // does not intercept (false "double lock" reports); the poll period does not need a steady clock
+    cv_.wait_until(lk, std::chrono::system_clock::now() +
+                           std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                               std::chrono::duration<double>(poll_s_)));
     if (stop_) break;
     const double t = now_s();
     bool fire = false;
