@@ -377,7 +377,8 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, c1
   return y;
 }
 
-Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad, int64_t dil) {
+Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad, int64_t dil,
+                  c10::optional<Tensor> addend) {
   check_bf16(dy, "dy");
   check_bf16(w, "w");
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), Cout = dy.size(3);
@@ -387,8 +388,12 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   Tensor wt = at::empty({C, R, S, Cout}, w.options());
   CHECK_HIP_OK(pda::conv_weight_transpose(bp(w), bpm(wt), Cout, R, S, C, stride, pad, dil, stream_of(dy)));
   Tensor dx = at::empty({N, H, W, C}, dy.options());
+  if (addend.has_value()) {
+    check_bf16(*addend, "addend");
+    TORCH_CHECK(addend->sizes() == dx.sizes(), "addend must have dx's shape");
+  }
   CHECK_HIP_OK(pda::conv2d_dgrad(bp(dy), bp(wt), bpm(dx), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
-                                 stream_of(dy)));
+                                 addend.has_value() ? bp(*addend) : nullptr, stream_of(dy)));
   return dx;
 }
 

@@ -403,6 +403,9 @@ struct Epi {
   // row remap (dgrad phase launches): row m = (n, hh, ww) of a [N, Hh, Wh] phase grid is written to
   // C row (n*H + hh*st + ph)*W + ww*st + pw
   int rm_on, rm_Hh, rm_Wh, rm_st, rm_ph, rm_pw, rm_H, rm_W;
+  // optional bf16 addend with C's layout (gradient accumulation fused into the store: conv1's dgrad
+  // adds the residual-branch gradient of a bottleneck instead of a separate add kernel)
+  const bf16_t* addend;
 };
 
 __device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
@@ -504,6 +507,11 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
       if (epi.relu) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (epi.addend) {
+        const u16x4 a = *reinterpret_cast<const u16x4*>(epi.addend + crow * epi.ldc + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += bf2f(a[r]);
       }
       if (epi.c_f32) {
         *reinterpret_cast<f32x4*>((float*)epi.C + crow * epi.ldc + n) = v;
@@ -733,12 +741,13 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H,
 // dx[N,H,W,C] = dgrad(dy[N,P,Q,Cout], wt): one launch per stride phase with only the taps that reach
 // it (wt phase-packed by conv_weight_transpose); folded single launch when stride > 1 and dil > 1.
 hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int N, int H, int W, int C, int Cout, int R,
-                        int S, int P, int Q, int stride, int pad, int dil, hipStream_t st) {
+                        int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend, hipStream_t st) {
   ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, Cout);
   if (!dgrad_phased(stride, dil)) {
     const int64_t M = (int64_t)N * H * W, Nn = C, K = (int64_t)R * S * Cout;
     Plan p = plan_gemm(M, Nn, K, false, 512);
     Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
+    epi.addend = addend;
     auto mk_a = [&](auto t) { t.dy = dy; t.g = g; t.M = M; t.K = K; return t; };
     auto mk_b = [&](auto t) { t.p = wt; t.rows = Nn; t.K = K; t.ld = K; return t; };
     return dispatch_bn<ConvDgradK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
@@ -762,6 +771,7 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int N, i
       const bf16_t* wph = wt + ((int64_t)a.cum * S + (int64_t)a.n * b.cum) * C * Cout;
       Plan p = plan_gemm(M, Nn, K, false, 512);
       Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
+      epi.addend = addend;
       if (stride > 1) {
         epi.rm_on = 1; epi.rm_Hh = Hh; epi.rm_Wh = Wh; epi.rm_st = stride; epi.rm_ph = ph; epi.rm_pw = pw;
         epi.rm_H = H; epi.rm_W = W;

@@ -21,6 +21,7 @@ import torch.nn.functional as F
 
 from .. import nn as pnn
 from .. import ops
+from ..ops.grad_join import GradJoin
 
 
 class Bottleneck(tnn.Module):
@@ -43,13 +44,15 @@ class Bottleneck(tnn.Module):
             self.downsample = None
 
     def forward(self, x):
-        out = self.bn1(self.conv1(x), relu=True)
+        # x feeds conv1 and the shortcut: its two gradients are summed inside conv1's (or the
+        # downsample conv's) dgrad store instead of by a separate autograd add (ops/grad_join.py)
+        join = GradJoin(2) if (x.is_cuda and x.requires_grad and torch.is_grad_enabled()) else None
+        out = self.bn1(self.conv1(x, grad_join=join), relu=True)
         out = self.bn2(self.conv2(out), relu=True)
         if self.downsample is not None:
-            idn = self.downsample[1](self.downsample[0](x))
-        else:
-            idn = x
-        return self.bn3(self.conv3(out), residual=idn, relu=True)
+            idn = self.downsample[1](self.downsample[0](x, grad_join=join))
+            return self.bn3(self.conv3(out), residual=idn, relu=True)
+        return self.bn3(self.conv3(out), residual=x, relu=True, residual_join=join)
 
 
 class Stem(tnn.Module):

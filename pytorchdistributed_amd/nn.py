@@ -56,8 +56,8 @@ class Conv2d(tnn.Module):
         self.bias = tnn.Parameter(torch.zeros(out_channels, device=device, dtype=dtype)) if bias else None
         _kaiming_uniform_(self.weight, in_channels * k * k)
 
-    def forward(self, x, relu=False):
-        return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, relu)
+    def forward(self, x, relu=False, grad_join=None):
+        return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, relu, grad_join)
 
     def extra_repr(self):
         return (f"{self.in_channels}, {self.out_channels}, kernel_size={self.kernel_size}, stride={self.stride}, "
@@ -88,11 +88,11 @@ class BatchNorm2d(tnn.Module):
             self.running_var = fn(rv).float()
         return self
 
-    def forward(self, x, residual=None, relu=False):
+    def forward(self, x, residual=None, relu=False, residual_join=None):
         if self.training:
             self.num_batches_tracked.add_(1)
         return ops.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
-                              self.momentum, self.eps, residual=residual, relu=relu)
+                              self.momentum, self.eps, residual=residual, relu=relu, residual_join=residual_join)
 
 
 class ReLU(tnn.Module):

@@ -21,13 +21,14 @@ def _ref_conv(x, w, stride, padding, dilation, bias=None):
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, stride, padding, dilation, relu):
+    def forward(ctx, x, w, bias, stride, padding, dilation, relu, join):
         x = x.contiguous()
         w = w.contiguous()
         y = C().conv_fwd(x, w, stride, padding, dilation, bias, relu)
         ctx.save_for_backward(x, w, y if relu else None)
         ctx.cfg = (stride, padding, dilation, relu, bias is not None)
         ctx.wparam = w
+        ctx.join = join
         return y
 
     @staticmethod
@@ -39,22 +40,29 @@ class _Conv2dFn(torch.autograd.Function):
             dy = C().relu_bwd(dy, y)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation)
+            join = ctx.join
+            if join is not None and not join.is_last():
+                join.stash(C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation, None))
+            else:
+                addend = join.take() if join is not None else None
+                dx = C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation, addend)
         if ctx.needs_input_grad[1]:
             dw = C().conv_wgrad(dy, x, w.shape[1], w.shape[2], stride, padding, dilation, w.dtype == torch.float32,
                                 grad_target(ctx.wparam))
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.reshape(-1, dy.shape[-1]).sum(0, dtype=torch.float32).to(dy.dtype)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias=None, stride: int = 1, padding: int = 0, dilation: int = 1,
-           relu: bool = False) -> torch.Tensor:
-    """``y[N,P,Q,Co] = conv(x[N,H,W,Ci], weight[Co,R,S,Ci])`` (+bias, optional fused ReLU)."""
+           relu: bool = False, grad_join=None) -> torch.Tensor:
+    """``y[N,P,Q,Co] = conv(x[N,H,W,Ci], weight[Co,R,S,Ci])`` (+bias, optional fused ReLU).
+    ``grad_join`` (:class:`~.grad_join.GradJoin`): x's gradient from other consumers is added inside
+    the dgrad kernel's store when this conv is the last of them to run backward."""
     if x.is_cuda:
         if weight.shape[-1] != x.shape[-1]:  # stem: input channels padded to a multiple of 8
             weight = F.pad(weight, (0, x.shape[-1] - weight.shape[-1]))
-        return _Conv2dFn.apply(x, weight, bias, stride, padding, dilation, relu)
+        return _Conv2dFn.apply(x, weight, bias, stride, padding, dilation, relu, grad_join)
     if weight.shape[-1] != x.shape[-1]:
         x = x[..., : weight.shape[-1]]
     y = _ref_conv(x, weight, stride, padding, dilation, bias)

@@ -15,7 +15,7 @@ from ..parallel.flat import grad_target
 
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu):
+    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu, join):
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()
@@ -33,6 +33,7 @@ class _BatchNormFn(torch.autograd.Function):
         ctx.save_for_backward(x, y if keep_y else None, ss if (relu and not keep_y) else None, mean, invstd, gamma)
         ctx.cfg = (relu, residual is not None, training)
         ctx.beta = beta
+        ctx.join = join
         return y
 
     @staticmethod
@@ -48,7 +49,9 @@ class _BatchNormFn(torch.autograd.Function):
         dx, dres, dgamma, dbeta = C().bn_bwd(dy.contiguous(), x, y, ss, mean, invstd, gamma, relu, has_res, tg, tb)
         dg = dgamma if gamma is not None and ctx.needs_input_grad[1] else None
         db = dbeta if ctx.needs_input_grad[2] else None
-        return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None
+        if has_res and ctx.join is not None:
+            dres = ctx.join.contribute(dres)  # usually stashed for the consumer conv's dgrad epilogue
+        return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None, None
 
 
 def _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu):
@@ -66,11 +69,12 @@ def _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, trainin
 
 
 def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True, momentum=0.1, eps=1e-5,
-               residual=None, relu=False):
-    """BatchNorm over the last (channel) dim of ``x`` (any leading dims), then ``+residual``, then ReLU."""
+               residual=None, relu=False, residual_join=None):
+    """BatchNorm over the last (channel) dim of ``x`` (any leading dims), then ``+residual``, then ReLU.
+    ``residual_join``: the residual's gradient is handed to the join instead of autograd's add."""
     if x.is_cuda and x.dtype == torch.bfloat16:
         return _BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
-                                  relu)
+                                  relu, residual_join)
     return _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu)
 
 

@@ -102,8 +102,11 @@ def test_conv_fwd_dgrad_wgrad(case):
     yg = C().conv_fwd(bf(x.detach()), bf(w.detach()), s, p, d, None, False)
     assert yg.shape == y.shape
     assert rel_err(yg.cpu(), y.detach()) < 1e-2
-    dx = C().conv_dgrad(bf(dy), bf(w.detach()), H, W, s, p, d)
+    dx = C().conv_dgrad(bf(dy), bf(w.detach()), H, W, s, p, d, None)
     assert rel_err(dx.cpu(), x.grad) < 1e-2
+    add = torch.randn(N, H, W, Cin).to(torch.bfloat16)
+    dx2 = C().conv_dgrad(bf(dy), bf(w.detach()), H, W, s, p, d, add.to(DEV))  # fused gradient accumulation
+    assert rel_err(dx2.cpu(), x.grad + add.float()) < 1e-2
     dw = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, d, True, None)
     assert rel_err(dw.cpu(), w.grad) < 1e-3
     dwb = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, d, False, None)

@@ -223,3 +223,25 @@ def test_transformer_models_cpu():
     out.backward()
     st = GPT2Stage(gcfg("gpt2", n_layer=4, n_embd=64, n_head=2, vocab_size=100), 0, 2, True, False)
     assert st(idx).shape == (2, 32, 64)
+
+
+def test_grad_join_sums_consumers_without_autograd_add():
+    from pytorchdistributed_amd.ops.grad_join import GradJoin
+
+    class Scale(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, k, join):
+            ctx.k, ctx.join = k, join
+            return x * k
+
+        @staticmethod
+        def backward(ctx, g):
+            return ctx.join.contribute(g * ctx.k), None, None
+
+    for consumers in (2, 3):
+        x = torch.randn(5, requires_grad=True)
+        j = GradJoin(consumers)
+        ks = [2.0, -3.0, 0.5][:consumers]
+        sum(Scale.apply(x, k, j) for k in ks).sum().backward()
+        assert torch.allclose(x.grad, torch.full((5,), sum(ks)))
+        assert j.pending is None and j.arrived == 0
