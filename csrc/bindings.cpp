@@ -642,17 +642,21 @@ Tensor embedding_bwd(Tensor idx, Tensor dy, int64_t V, c10::optional<Tensor> out
   return res;
 }
 
-Tensor rope(Tensor x_in, Tensor cs, Tensor sn, bool inverse) {
-  Tensor x = x_in.contiguous();
+// rotate-half RoPE of x [B, T, H, D] (any B/T/H strides, contiguous D); writes a new contiguous tensor
+// or `out` (same shape, its own strides, e.g. a head slice of a fused QKV gradient)
+Tensor rope(Tensor x, Tensor cs, Tensor sn, bool inverse, c10::optional<Tensor> out) {
   attn_check(x, "x");
   check_f32(cs, "cos");
   check_f32(sn, "sin");
   const int B = x.size(0), T = x.size(1), H = x.size(2), D = x.size(3);
   TORCH_CHECK(D % 16 == 0 && cs.numel() >= (int64_t)T * D / 2);
   c10::DeviceGuard g(x.device());
-  Tensor y = at::empty_like(x);
+  Tensor y = out.has_value() ? *out : at::empty({B, T, H, D}, x.options());
+  attn_check(y, "out");
+  TORCH_CHECK(y.sizes() == x.sizes(), "rope: out shape mismatch");
   CHECK_HIP_OK(pda::rope_apply(bp(x), bpm(y), cs.data_ptr<float>(), sn.data_ptr<float>(), B, T, H, D, x.stride(0),
-                               x.stride(1), x.stride(2), inverse, stream_of(x)));
+                               x.stride(1), x.stride(2), y.stride(0), y.stride(1), y.stride(2), inverse,
+                               stream_of(x)));
   return y;
 }
 

@@ -129,6 +129,7 @@ hipError_t attention_bwd(const AttnParams& p, hipStream_t st);
 hipError_t embedding_fwd(const int64_t* idx, const bf16_t* table, bf16_t* out, int64_t n, int64_t D, hipStream_t st);
 hipError_t embedding_bwd(const int64_t* idx, const bf16_t* dy, float* acc, int64_t n, int64_t D, hipStream_t st);
 hipError_t rope_apply(const bf16_t* x, bf16_t* y, const float* cos, const float* sin, int B, int T, int H, int D,
-                      int64_t sb, int64_t st_, int64_t sh, bool inverse, hipStream_t st);
+                      int64_t sb, int64_t st_, int64_t sh, int64_t yb, int64_t yt, int64_t yh, bool inverse,
+                      hipStream_t st);
 
 }  // namespace pda

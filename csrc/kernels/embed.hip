@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(kThreads) embedding_bwd_kernel(const int64_t* 
 __global__ void __launch_bounds__(kThreads) rope_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                         const float* __restrict__ cs, const float* __restrict__ sn,
                                                         int B, int T, int H, int D, int64_t sb, int64_t st_,
-                                                        int64_t sh, float sign) {
+                                                        int64_t sh, int64_t yb, int64_t yt, int64_t yh, float sign) {
   const int half = D / 2, hv = half / 8;
   const int64_t total = (int64_t)B * T * H * hv;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -59,6 +59,7 @@ __global__ void __launch_bounds__(kThreads) rope_kernel(const bf16_t* __restrict
     const int pos = (int)(r % T);
     const int b = (int)(r / T);
     const int64_t base = b * sb + pos * st_ + h * sh + c * 8;
+    const int64_t ybase = b * yb + pos * yt + h * yh + c * 8;
     float a[8], bb[8];
     load8(x + base, a);
     load8(x + base + half, bb);
@@ -71,8 +72,8 @@ __global__ void __launch_bounds__(kThreads) rope_kernel(const bf16_t* __restrict
       a[j] = x1 * cr[j] - x2 * s;
       bb[j] = x2 * cr[j] + x1 * s;
     }
-    store8(y + base, a);
-    store8(y + base + half, bb);
+    store8(y + ybase, a);
+    store8(y + ybase + half, bb);
   }
 }
 
@@ -95,9 +96,10 @@ hipError_t embedding_bwd(const int64_t* idx, const bf16_t* dy, float* acc, int64
 }
 
 hipError_t rope_apply(const bf16_t* x, bf16_t* y, const float* cos, const float* sin, int B, int T, int H, int D,
-                      int64_t sb, int64_t st_, int64_t sh, bool inverse, hipStream_t st) {
+                      int64_t sb, int64_t st_, int64_t sh, int64_t yb, int64_t yt, int64_t yh, bool inverse,
+                      hipStream_t st) {
   rope_kernel<<<grid_for((int64_t)B * T * H * (D / 16)), kThreads, 0, st>>>(x, y, cos, sin, B, T, H, D, sb, st_, sh,
-                                                                            inverse ? -1.f : 1.f);
+                                                                            yb, yt, yh, inverse ? -1.f : 1.f);
   return hipGetLastError();
 }
 

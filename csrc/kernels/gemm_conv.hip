@@ -525,19 +525,42 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
   }
 }
 
-// Split-K reduction: out[m, n] = act(sum_s slab[s, m, n] + bias[n])
+// Split-K reduction: out[m, n] = act(sum_s slab[s, m, n] + bias[n]).  A workgroup is (256 / L) output
+// float4s x L split lanes; each lane keeps 8 slab loads in flight and the L partials meet in LDS, so
+// a small output with a deep split (conv wgrad of 64 x 64 with ~1000 slabs) still spreads over
+// many CUs instead of serialising 1000 dependent loads per thread.
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t M,
-                                                            int64_t N, Epi epi) {
+                                                            int64_t N, int lanes_log2, Epi epi) {
+  __shared__ f32x4 red[256];
+  const int L = 1 << lanes_log2;
+  const int lane = threadIdx.x & (L - 1), o = threadIdx.x >> lanes_log2;
   const int64_t total4 = M * N / 4;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total4; t += stride) {
-    f32x4 v = *reinterpret_cast<const f32x4*>(slab + t * 4);
-    for (int s = 1; s < splits; ++s) {
-      const f32x4 u = *reinterpret_cast<const f32x4*>(slab + (int64_t)s * M * N + t * 4);
-      v += u;
+  const int64_t t = (int64_t)blockIdx.x * (256 >> lanes_log2) + o;
+  const int64_t sstride = M * N;
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (t < total4) {
+    const float* p = slab + t * 4;
+    f32x4 a[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int s = lane;
+    for (; s + 7 * L < splits; s += 8 * L) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += *reinterpret_cast<const f32x4*>(p + (int64_t)(s + u * L) * sstride);
     }
-    const int64_t m = (t * 4) / N, n = (t * 4) % N;
-    if (epi.bias) {
+    for (; s < splits; s += L) a[0] += *reinterpret_cast<const f32x4*>(p + (int64_t)s * sstride);
+    acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  }
+  if (L > 1) {
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (lane != 0) return;
+    for (int l = 1; l < L; ++l) acc += red[threadIdx.x + l];
+  }
+  if (t >= total4) return;
+  f32x4 v = acc;
+  const int64_t m = (t * 4) / N, n = (t * 4) % N;
+  if (epi.bias) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         v[r] += epi.bias_f32 ? ((const float*)epi.bias)[n + r] : bf2f(((const bf16_t*)epi.bias)[n + r]);
@@ -554,7 +577,6 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
       for (int r = 0; r < 4; ++r) o[r] = f2bf(v[r]);
       *reinterpret_cast<u16x4*>((bf16_t*)epi.C + m * epi.ldc + n) = o;
     }
-  }
 }
 
 // Stride phases of a dgrad with dilation 1 (or stride 1): phase ph of the rows takes the taps
@@ -661,9 +683,11 @@ hipError_t launch(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, c
                                                                      p.ktiles_per_split, e);
   PDA_CHECK_HIP(hipGetLastError());
   if (p.splits > 1) {
-    int64_t g = (M * N / 4 + 255) / 256;
-    if (g > 8192) g = 8192;
-    splitk_reduce_kernel<<<(int)(g < 1 ? 1 : g), 256, 0, st>>>(slab, p.splits, M, N, epi);
+    int ll = 0;  // split lanes per output: ~16 slabs per lane, at most 16 lanes
+    while (ll < 4 && (p.splits >> ll) > 16) ++ll;
+    const int64_t per_block = 256 >> ll;
+    const int64_t g = (M * N / 4 + per_block - 1) / per_block;
+    splitk_reduce_kernel<<<(unsigned)g, 256, 0, st>>>(slab, p.splits, M, N, ll, epi);
     PDA_CHECK_HIP(hipGetLastError());
   }
   return hipSuccess;

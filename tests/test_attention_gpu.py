@@ -57,10 +57,29 @@ def test_embedding_and_rope_kernels():
     assert rel_err(tg.grad.cpu(), ref) < 1e-2
     x = torch.randn(2, 9, 3, 64).to(torch.bfloat16)
     cs, sn = rope_tables(9, 64)
-    y = C().rope(x.cuda(), cs.cuda(), sn.cuda(), False)
+    y = C().rope(x.cuda(), cs.cuda(), sn.cuda(), False, None)
     assert rel_err(y.cpu(), _rope_ref(x, cs, sn)) < 1e-2
-    back = C().rope(y, cs.cuda(), sn.cuda(), True)
+    back = C().rope(y, cs.cuda(), sn.cuda(), True, None)
     assert rel_err(back.cpu(), x) < 2e-2
+    # strided input (head slice of a fused buffer) written into a strided output slice
+    big = torch.randn(2, 9, 5, 64).to(torch.bfloat16)
+    out = torch.zeros(2, 9, 7, 64, dtype=torch.bfloat16).cuda()
+    C().rope(big.cuda()[:, :, 1:4], cs.cuda(), sn.cuda(), False, out[:, :, 2:5])
+    assert rel_err(out[:, :, 2:5].cpu(), _rope_ref(big[:, :, 1:4], cs, sn)) < 1e-2
+    assert out[:, :, :2].abs().sum().item() == 0 and out[:, :, 5:].abs().sum().item() == 0
+
+
+def test_attention_kernel_inline_rope():
+    """The kernels' in-load rotary path (rope_cos/rope_sin arguments) against the reference."""
+    from pytorchdistributed_amd._native import C
+    from pytorchdistributed_amd.ops.attention import attention_ref, rope_tables
+
+    torch.manual_seed(3)
+    q, k, v = (torch.randn(1, 128, h, 64).to(torch.bfloat16) for h in (4, 2, 2))
+    cs, sn = rope_tables(128, 64)
+    o, _ = C().attn_fwd(q.cuda(), k.cuda(), v.cuda(), 0.125, True, cs.cuda(), sn.cuda())
+    ref = attention_ref(q.float(), k.float(), v.float(), True, 0.125, (cs, sn))
+    assert rel_err(o.cpu(), ref) < 2e-2
 
 
 def test_gpt2_small_native_vs_reference():
