@@ -609,6 +609,12 @@ void attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, T
   p.dk = bpm(dk); p.dk_sb = dk.stride(0); p.dk_st = dk.stride(1); p.dk_sh = dk.stride(2);
   p.dv = bpm(dv); p.dv_sb = dv.stride(0); p.dv_st = dv.stride(1); p.dv_sh = dv.stride(2);
   rope_tables(p, rope_cos, rope_sin, T, D);
+  const int64_t wsn = pda::attention_bwd_ws_floats(B, T, Hq, Hkv, D, rope_cos.has_value());
+  Tensor ws;
+  if (wsn > 0) {
+    ws = at::empty({wsn}, q.options().dtype(at::kFloat));
+    p.dkv_part = ws.data_ptr<float>();
+  }
   CHECK_HIP_OK(pda::attention_bwd(p, stream_of(q)));
 }
 

@@ -24,6 +24,8 @@ struct AttnParams {
   float* delta;  // [B, Hq, T] workspace
   bf16_t *dq, *dk, *dv;
   int64_t dq_sb, dq_st, dq_sh, dk_sb, dk_st, dk_sh, dv_sb, dv_st, dv_sh;
+  // GQA dK/dV partials per query head, fp32 [2][B][Hq][T][D] (only when Hq > Hkv; attn_bwd_ws_floats)
+  float* dkv_part;
 };
 
 // ---- optim.hip
@@ -124,6 +126,7 @@ int64_t colreduce_ws_floats(int64_t rows, int64_t D, int nout);
 // ---- attention.hip (flash attention fwd / bwd, D in {64, 128}, GQA, causal or not)
 hipError_t attention_fwd(const AttnParams& p, hipStream_t st);
 hipError_t attention_bwd(const AttnParams& p, hipStream_t st);
+int64_t attention_bwd_ws_floats(int B, int T, int Hq, int Hkv, int D, bool rope);
 
 // ---- embed.hip
 hipError_t embedding_fwd(const int64_t* idx, const bf16_t* table, bf16_t* out, int64_t n, int64_t D, hipStream_t st);

@@ -469,15 +469,418 @@ __global__ void __launch_bounds__(NT, 1) attn_bwd_dkdv_kernel(AttnParams p) {
   }
 }
 
+// ================================================================ v2 kernels (no in-load RoPE)
+// Same MFMA / LDS-image structure as above, plus:
+//  * register-prefetched staging (T14): the K/V (or Q/dO) tile t+1 is loaded into VGPRs while tile t
+//    is multiplied, and written to LDS between two barriers — global latency hides behind the MFMAs;
+//  * forward: each wave owns two 16-row query groups (BQ = 128 per workgroup), so every K / V fragment
+//    read from LDS feeds two MFMAs; causal masking math only on tiles that cross the diagonal, fully
+//    masked tiles are skipped per wave, heavy (late) query tiles are scheduled first;
+//  * dK/dV: one workgroup per (key tile, QUERY head) — 4x more workgroups than looping over the GQA
+//    group inside a block — writing fp32 partials that a small kernel sums over the group.
+template <int D>
+struct TileRegs {
+  static constexpr int CPR = D / 8, NCH = 64 * CPR / NT;
+  u16x8 a[NCH], b[NCH];
+};
+
+template <int D>
+__device__ __forceinline__ void fetch_tile(TileRegs<D>& tr, const bf16_t* __restrict__ A, int64_t ars,
+                                           const bf16_t* __restrict__ B, int64_t brs, int row0, int T) {
+  constexpr int CPR = TileRegs<D>::CPR;
+#pragma unroll
+  for (int i = 0; i < TileRegs<D>::NCH; ++i) {
+    const int c = threadIdx.x + NT * i;
+    const int r = c / CPR, ch = c % CPR;
+    const int gr = row0 + r;
+    tr.a[i] = gr < T ? ld16(A + (int64_t)gr * ars + ch * 8) : zero16();
+    tr.b[i] = gr < T ? ld16(B + (int64_t)gr * brs + ch * 8) : zero16();
+  }
+}
+
+// write A to (row image a_row, optional tr image a_tr) and B likewise
+template <int D>
+__device__ __forceinline__ void store_tile(const TileRegs<D>& tr, char* a_row, char* a_tr, char* b_row, char* b_tr) {
+  constexpr int CPR = TileRegs<D>::CPR;
+#pragma unroll
+  for (int i = 0; i < TileRegs<D>::NCH; ++i) {
+    const int c = threadIdx.x + NT * i;
+    const int r = c / CPR, ch = c % CPR;
+    if (a_row) *reinterpret_cast<u16x8*>(a_row + row_off<D>(r, ch)) = tr.a[i];
+    if (a_tr) *reinterpret_cast<u16x8*>(a_tr + tr_off<D>(r, ch * 8)) = tr.a[i];
+    if (b_row) *reinterpret_cast<u16x8*>(b_row + row_off<D>(r, ch)) = tr.b[i];
+    if (b_tr) *reinterpret_cast<u16x8*>(b_tr + tr_off<D>(r, ch * 8)) = tr.b[i];
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(NT, 2) attn_fwd2_kernel(AttnParams p) {
+  constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2, BQ2 = 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * IMG];
+  char* Ks = smem;
+  char* Vs = smem + IMG;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int qt = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z;  // heavy causal tiles first
+  const int hk = h / (p.Hq / p.Hkv);
+  const int T = p.T;
+  const int qbase = qt * BQ2 + w * 32;
+  const int qrow0 = qbase + (lane & 15), qrow1 = qrow0 + 16;
+  const bf16_t* qb = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* vb = p.v + b * p.v_sb + hk * p.v_sh;
+  mbf16x8 qf0[KS], qf1[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    qf0[ks] = load_frag_global(qb, p.q_st, qrow0, T, ks, lane);
+    qf1[ks] = load_frag_global(qb, p.q_st, qrow1, T, ks, lane);
+  }
+  const float c = p.scale * LOG2E;
+  float m0 = -INFINITY, l0 = 0.f, m1 = -INFINITY, l1 = 0.f;
+  f32x4 o0[DT], o1[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o0[dt] = o1[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kv_end = p.causal ? min(T, (qt + 1) * BQ2) : T;
+  const int ntiles = (kv_end + BKV - 1) / BKV;
+  TileRegs<D> tr;
+  fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, 0, T);
+  for (int j = 0; j < ntiles; ++j) {
+    const int kv0 = j * BKV;
+    __syncthreads();
+    store_tile<D>(tr, Ks, nullptr, nullptr, Vs);
+    __syncthreads();
+    if (j + 1 < ntiles) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, kv0 + BKV, T);
+    if (p.causal && kv0 > qbase + 31) continue;  // every key of this tile is in this wave's future
+    f32x4 s0[4], s1[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s0[t] = s1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const mbf16x8 kf = frag_row<D>(Ks, 16 * t, ks, lane);
+        s0[t] = mfma(kf, qf0[ks], s0[t]);
+        s1[t] = mfma(kf, qf1[ks], s1[t]);
+      }
+    }
+    const bool need_mask = kv0 + BKV > T || (p.causal && kv0 + BKV - 1 > qbase);
+    auto softmax = [&](f32x4 (&s)[4], int qrow, float& m, float& l, f32x4 (&o)[DT]) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = s[t][r] * c;
+          if (need_mask) {
+            const int kv = kv0 + 16 * t + 4 * g + r;
+            if (kv >= T || (p.causal && kv > qrow)) v = -INFINITY;
+          }
+          s[t][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m, mx);
+      const bool dead = m_new == -INFINITY;
+      const float alpha = dead ? 1.f : exp2f(m - m_new);
+      float rs = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = dead ? 0.f : exp2f(s[t][r] - m_new);
+          s[t][r] = e;
+          rs += e;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l = l * alpha + rs;
+      m = m_new;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
+    };
+    softmax(s0, qrow0, m0, l0, o0);
+    softmax(s1, qrow1, m1, l1, o1);
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const mbf16x8 p0 = pack_p(s0[2 * cc], s0[2 * cc + 1]);
+      const mbf16x8 p1 = pack_p(s1[2 * cc], s1[2 * cc + 1]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const mbf16x8 vf = frag_tr<D>(Vs, 32 * cc, 16 * dt, lane);
+        o0[dt] = mfma(vf, p0, o0[dt]);
+        o1[dt] = mfma(vf, p1, o1[dt]);
+      }
+    }
+  }
+  auto epilogue = [&](int qrow, float m, float l, const f32x4 (&o)[DT]) {
+    if (qrow >= T) return;
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16_t* ob = p.o + b * p.o_sb + (int64_t)qrow * p.o_st + h * p.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      u16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][r] * inv);
+      *reinterpret_cast<u16x4*>(ob + 16 * dt + 4 * g) = v;
+    }
+    if (g == 0) p.lse[((int64_t)b * p.Hq + h) * T + qrow] = (m + log2f(l)) / LOG2E;
+  };
+  epilogue(qrow0, m0, l0, o0);
+  epilogue(qrow1, m1, l1, o1);
+}
+
+// dQ, query-stationary, prefetched K/V tiles (16 query rows per wave, BQ = 64)
+template <int D>
+__global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
+  constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[3 * IMG];
+  char* Kr = smem;
+  char* Kt = smem + IMG;
+  char* Vr = smem + 2 * IMG;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int qt = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  const int hk = h / (p.Hq / p.Hkv);
+  const int T = p.T;
+  const int qbase = qt * BQ + w * 16;
+  const int qrow = qbase + (lane & 15);
+  const bf16_t* qb = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* dob = p.dout + b * p.do_sb + h * p.do_sh;
+  const bf16_t* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* vb = p.v + b * p.v_sb + hk * p.v_sh;
+  mbf16x8 qf[KS], df[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    qf[ks] = load_frag_global(qb, p.q_st, qrow, T, ks, lane);
+    df[ks] = load_frag_global(dob, p.do_st, qrow, T, ks, lane);
+  }
+  const int64_t rowid = ((int64_t)b * p.Hq + h) * T + qrow;
+  const float lse2 = qrow < T ? p.lse[rowid] * LOG2E : 0.f;
+  const float dl = qrow < T ? p.delta[rowid] : 0.f;
+  const float c = p.scale * LOG2E;
+  f32x4 dq[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kv_end = p.causal ? min(T, (qt + 1) * BQ) : T;
+  const int ntiles = (kv_end + BKV - 1) / BKV;
+  TileRegs<D> tr;
+  fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, 0, T);
+  for (int j = 0; j < ntiles; ++j) {
+    const int kv0 = j * BKV;
+    __syncthreads();
+    store_tile<D>(tr, Kr, Kt, Vr, nullptr);
+    __syncthreads();
+    if (j + 1 < ntiles) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, kv0 + BKV, T);
+    if (p.causal && kv0 > qbase + 15) continue;
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s[t] = mfma(frag_row<D>(Kr, 16 * t, ks, lane), qf[ks], s[t]);
+        dp[t] = mfma(frag_row<D>(Vr, 16 * t, ks, lane), df[ks], dp[t]);
+      }
+    }
+    const bool need_mask = kv0 + BKV > T || (p.causal && kv0 + BKV - 1 > qbase) || qrow >= T;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float pr = exp2f(s[t][r] * c - lse2);
+        if (need_mask) {
+          const int kv = kv0 + 16 * t + 4 * g + r;
+          if (qrow >= T || kv >= T || (p.causal && kv > qrow)) pr = 0.f;
+        }
+        s[t][r] = pr * (dp[t][r] - dl);
+      }
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const mbf16x8 sf = pack_p(s[2 * cc], s[2 * cc + 1]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma(frag_tr<D>(Kt, 32 * cc, 16 * dt, lane), sf, dq[dt]);
+    }
+  }
+  if (qrow < T) {
+    bf16_t* out = p.dq + b * p.dq_sb + (int64_t)qrow * p.dq_st + h * p.dq_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      u16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(dq[dt][r] * p.scale);
+      *reinterpret_cast<u16x4*>(out + 16 * dt + 4 * g) = v;
+    }
+  }
+}
+
+// dK / dV for one (key tile, query head): prefetched Q / dO tiles; output bf16 directly (no GQA) or
+// fp32 partials [2][B][Hq][T][D] summed over the group by attn_dkv_reduce_kernel
+template <int D>
+__global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
+  constexpr int KS = D / 32, DT = D / 16, IMG = BQ * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + 2 * BQ * 4];
+  char* Qr = smem;
+  char* Qt = smem + IMG;
+  char* Dr = smem + 2 * IMG;
+  char* Dt = smem + 3 * IMG;
+  float* s_lse = reinterpret_cast<float*>(smem + 4 * IMG);
+  float* s_dl = s_lse + BQ;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int kt = blockIdx.x, hq = blockIdx.y, b = blockIdx.z;
+  const int T = p.T, G = p.Hq / p.Hkv, hk = hq / G;
+  const int kvbase = kt * BKV + w * 16;
+  const int kvrow = kvbase + (lane & 15);
+  const bf16_t* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* vb = p.v + b * p.v_sb + hk * p.v_sh;
+  mbf16x8 kf[KS], vf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    kf[ks] = load_frag_global(kb, p.k_st, kvrow, T, ks, lane);
+    vf[ks] = load_frag_global(vb, p.v_st, kvrow, T, ks, lane);
+  }
+  const float c = p.scale * LOG2E;
+  f32x4 dk[DT], dv[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int q_begin = p.causal ? kt * BKV : 0;
+  const bf16_t* qb = p.q + b * p.q_sb + hq * p.q_sh;
+  const bf16_t* dob = p.dout + b * p.do_sb + hq * p.do_sh;
+  const float* lse = p.lse + ((int64_t)b * p.Hq + hq) * T;
+  const float* dlt = p.delta + ((int64_t)b * p.Hq + hq) * T;
+  TileRegs<D> tr;
+  float nl = 0.f, nd = 0.f;
+  auto fetch_stats = [&](int q0) {
+    if (threadIdx.x < BQ) {
+      const int q = q0 + threadIdx.x;
+      nl = q < T ? lse[q] * LOG2E : 0.f;
+      nd = q < T ? dlt[q] : 0.f;
+    }
+  };
+  if (q_begin < T) {
+    fetch_tile<D>(tr, qb, p.q_st, dob, p.do_st, q_begin, T);
+    fetch_stats(q_begin);
+  }
+  for (int q0 = q_begin; q0 < T; q0 += BQ) {
+    __syncthreads();
+    store_tile<D>(tr, Qr, Qt, Dr, Dt);
+    if (threadIdx.x < BQ) {
+      s_lse[threadIdx.x] = nl;
+      s_dl[threadIdx.x] = nd;
+    }
+    __syncthreads();
+    if (q0 + BQ < T) {
+      fetch_tile<D>(tr, qb, p.q_st, dob, p.do_st, q0 + BQ, T);
+      fetch_stats(q0 + BQ);
+    }
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        s[t] = mfma(frag_row<D>(Qr, 16 * t, ks, lane), kf[ks], s[t]);  // S^T: [q][kv = lane]
+        dp[t] = mfma(frag_row<D>(Dr, 16 * t, ks, lane), vf[ks], dp[t]);
+      }
+    }
+    const bool need_mask = q0 + BQ > T || kvbase + 15 >= T || (p.causal && kvbase + 15 > q0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qi = 16 * t + 4 * g + r;
+        float pr = exp2f(s[t][r] * c - s_lse[qi]);
+        if (need_mask) {
+          const int q = q0 + qi;
+          if (q >= T || kvrow >= T || (p.causal && kvrow > q)) pr = 0.f;
+        }
+        s[t][r] = pr;
+        dp[t][r] = pr * (dp[t][r] - s_dl[qi]);  // dS
+      }
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const mbf16x8 pf = pack_p(s[2 * cc], s[2 * cc + 1]);
+      const mbf16x8 sf = pack_p(dp[2 * cc], dp[2 * cc + 1]);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        dv[dt] = mfma(frag_tr<D>(Dt, 32 * cc, 16 * dt, lane), pf, dv[dt]);
+        dk[dt] = mfma(frag_tr<D>(Qt, 32 * cc, 16 * dt, lane), sf, dk[dt]);
+      }
+    }
+  }
+  if (kvrow >= T) return;
+  if (G == 1) {
+    bf16_t* dkp = p.dk + b * p.dk_sb + (int64_t)kvrow * p.dk_st + hk * p.dk_sh;
+    bf16_t* dvp = p.dv + b * p.dv_sb + (int64_t)kvrow * p.dv_st + hk * p.dv_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      u16x4 a, v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        a[r] = f2bf(dk[dt][r] * p.scale);
+        v[r] = f2bf(dv[dt][r]);
+      }
+      *reinterpret_cast<u16x4*>(dkp + 16 * dt + 4 * g) = a;
+      *reinterpret_cast<u16x4*>(dvp + 16 * dt + 4 * g) = v;
+    }
+    return;
+  }
+  const int64_t plane = (int64_t)p.B * p.Hq * T * D;
+  float* pk = p.dkv_part + (((int64_t)b * p.Hq + hq) * T + kvrow) * D;
+  float* pv = pk + plane;
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    f32x4 a = dk[dt] * p.scale;
+    *reinterpret_cast<f32x4*>(pk + 16 * dt + 4 * g) = a;
+    *reinterpret_cast<f32x4*>(pv + 16 * dt + 4 * g) = dv[dt];
+  }
+}
+
+// dK/dV = sum over the G query heads of a KV head of the fp32 partials (8 columns per thread)
+__global__ void __launch_bounds__(NT) attn_dkv_reduce_kernel(AttnParams p) {
+  const int D = p.D, T = p.T, G = p.Hq / p.Hkv;
+  const int64_t n8 = (int64_t)p.B * p.Hkv * T * (D / 8);
+  const int64_t plane = (int64_t)p.B * p.Hq * T * D;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * n8; i += stride) {
+    const int which = i >= n8;  // 0: dK, 1: dV
+    int64_t r = which ? i - n8 : i;
+    const int c8 = (int)(r % (D / 8));
+    r /= D / 8;
+    const int t = (int)(r % T);
+    r /= T;
+    const int hk = (int)(r % p.Hkv);
+    const int b = (int)(r / p.Hkv);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int gq = 0; gq < G; ++gq) {
+      const float* src = p.dkv_part + which * plane + (((int64_t)b * p.Hq + hk * G + gq) * T + t) * D + c8 * 8;
+      float v[8];
+      load8(src, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += v[j];
+    }
+    bf16_t* dst = which ? p.dv + b * p.dv_sb + (int64_t)t * p.dv_st + hk * p.dv_sh
+                        : p.dk + b * p.dk_sb + (int64_t)t * p.dk_st + hk * p.dk_sh;
+    store8(dst + c8 * 8, acc);
+  }
+}
+
 }  // namespace
 
 hipError_t attention_fwd(const AttnParams& p, hipStream_t st) {
   if (p.D != 64 && p.D != 128) return hipErrorInvalidValue;
   if (p.Hkv <= 0 || p.Hq % p.Hkv) return hipErrorInvalidValue;
+  if (p.rope_cos == nullptr) {
+    dim3 grid((p.T + 127) / 128, p.Hq, p.B);
+    if (p.D == 128) attn_fwd2_kernel<128><<<grid, NT, 0, st>>>(p);
+    else attn_fwd2_kernel<64><<<grid, NT, 0, st>>>(p);
+    return hipGetLastError();
+  }
   dim3 grid((p.T + BQ - 1) / BQ, p.Hq, p.B);
   if (p.D == 128) attn_fwd_kernel<128><<<grid, NT, 0, st>>>(p);
   else attn_fwd_kernel<64><<<grid, NT, 0, st>>>(p);
   return hipGetLastError();
+}
+
+int64_t attention_bwd_ws_floats(int B, int T, int Hq, int Hkv, int D, bool rope) {
+  return (!rope && Hq > Hkv) ? (int64_t)2 * B * Hq * T * D : 0;
 }
 
 hipError_t attention_bwd(const AttnParams& p, hipStream_t st) {
@@ -490,6 +893,25 @@ hipError_t attention_bwd(const AttnParams& p, hipStream_t st) {
   else attn_bwd_delta_kernel<64><<<dgrid, NT, 0, st>>>(p);
   PDA_CHECK_HIP(hipGetLastError());
   dim3 gq((p.T + BQ - 1) / BQ, p.Hq, p.B);
+  if (p.rope_cos == nullptr) {
+    dim3 gk2((p.T + BKV - 1) / BKV, p.Hq, p.B);
+    if (p.Hq > p.Hkv && p.dkv_part == nullptr) return hipErrorInvalidValue;
+    if (p.D == 128) {
+      attn_bwd_dq2_kernel<128><<<gq, NT, 0, st>>>(p);
+      attn_bwd_dkdv2_kernel<128><<<gk2, NT, 0, st>>>(p);
+    } else {
+      attn_bwd_dq2_kernel<64><<<gq, NT, 0, st>>>(p);
+      attn_bwd_dkdv2_kernel<64><<<gk2, NT, 0, st>>>(p);
+    }
+    PDA_CHECK_HIP(hipGetLastError());
+    if (p.Hq > p.Hkv) {
+      const int64_t n8 = (int64_t)2 * p.B * p.Hkv * p.T * (p.D / 8);
+      int64_t g = (n8 + NT - 1) / NT;
+      if (g > 8192) g = 8192;
+      attn_dkv_reduce_kernel<<<(unsigned)g, NT, 0, st>>>(p);
+    }
+    return hipGetLastError();
+  }
   dim3 gk((p.T + BKV - 1) / BKV, p.Hkv, p.B);
   if (p.D == 128) {
     attn_bwd_dq_kernel<128><<<gq, NT, 0, st>>>(p);
