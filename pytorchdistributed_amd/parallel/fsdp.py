@@ -73,6 +73,19 @@ class _Unit:
         self.gathered = False
         self.pending_ag = None
         self.send_buf = None
+        # compute-dtype copy of the shard, made by the forward gather and reused by the backward
+        # re-gather of the same step (one cast per step instead of two).  Invalidated at every
+        # forward entry: fused optimizers update the shard through raw pointers, which does not
+        # bump its autograd version counter.
+        self._cast = None
+
+    def _send_buffer(self) -> torch.Tensor:
+        if self._cast is None:
+            if self.shard.dtype == self.fsdp.param_dtype:
+                self._cast = self.shard.detach()
+            else:
+                self._cast = self.shard.detach().to(self.fsdp.param_dtype)
+        return self._cast
 
     # ------------------------------------------------------------ gather / reshard
     def _alloc(self):
@@ -91,7 +104,7 @@ class _Unit:
         # saved views of this buffer stay valid for backward.
         version = self.flat._version
         with torch.no_grad():
-            self.send_buf = self.shard.detach().to(self.fsdp.param_dtype)
+            self.send_buf = self._send_buffer()
             if self.fsdp.world == 1:
                 self.flat.detach().copy_(self.send_buf)
                 self.pending_ag = None
@@ -227,10 +240,12 @@ class FullyShardedDataParallel(tnn.Module):
         self._finish_rs()
         grad_full = u.flat.grad
         u.flat.grad = None
-        out = torch.empty(u.shard_numel, dtype=grad_full.dtype, device=grad_full.device)
         if self.world == 1:
-            out.copy_(grad_full)
-            work = None
+            out, work = grad_full, None
+        else:
+            out = torch.empty(u.shard_numel, dtype=grad_full.dtype, device=grad_full.device)
+        if self.world == 1:
+            pass
         elif self.nccl:
             work = dist.reduce_scatter_tensor(out, grad_full, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
         else:
@@ -266,6 +281,8 @@ class FullyShardedDataParallel(tnn.Module):
 
     # ------------------------------------------------------------ module API
     def forward(self, *args, **kwargs):
+        for u in self.units:
+            u._cast = None
         if self.root_unit is not None:
             self.root_unit.finish_gather()
             self.root_unit.bind_views()
