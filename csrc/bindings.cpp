@@ -666,6 +666,105 @@ Tensor rope(Tensor x, Tensor cs, Tensor sn, bool inverse, c10::optional<Tensor> 
   return y;
 }
 
+
+// ------------------------------------------------------------------ xGMI one-shot all-reduce
+class XgmiComm {
+ public:
+  XgmiComm(int rank, int world, int64_t capacity_bytes, int device, double timeout_s)
+      : rank_(rank), world_(world), cap_(capacity_bytes), dev_(device) {
+    TORCH_CHECK(world >= 1 && world <= pda::kXgmiMaxRanks && rank >= 0 && rank < world, "xgmi: bad rank/world");
+    c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device));
+    CHECK_HIP_OK(pda::xgmi_alloc(&data_, (size_t)cap_));
+    CHECK_HIP_OK(pda::xgmi_alloc(&flags_, flag_bytes()));
+    CHECK_HIP_OK(pda::xgmi_alloc(reinterpret_cast<void**>(&err_), 64));
+    int rate_khz = 0;
+    CHECK_HIP_OK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device));
+    timeout_ticks_ = (long long)(timeout_s * (double)rate_khz * 1000.0);
+    for (int r = 0; r < pda::kXgmiMaxRanks; ++r) {
+      peer_data_[r] = nullptr;
+      peer_flags_[r] = nullptr;
+    }
+    peer_data_[rank] = data_;
+    peer_flags_[rank] = reinterpret_cast<uint32_t*>(flags_);
+  }
+  ~XgmiComm() {
+    c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, dev_));
+    for (int r = 0; r < world_; ++r)
+      if (r != rank_) {
+        if (peer_data_[r]) (void)pda::xgmi_close_handle(peer_data_[r]);
+        if (peer_flags_[r]) (void)pda::xgmi_close_handle(peer_flags_[r]);
+      }
+    (void)pda::xgmi_free(data_);
+    (void)pda::xgmi_free(flags_);
+    (void)pda::xgmi_free(err_);
+  }
+  static size_t flag_bytes() { return (size_t)2 * pda::kXgmiMaxBlocks * pda::kXgmiMaxRanks * sizeof(uint32_t); }
+  py::bytes handles() {
+    std::string h(2 * HIP_IPC_HANDLE_SIZE, '\0');
+    CHECK_HIP_OK(pda::xgmi_get_handle(data_, &h[0]));
+    CHECK_HIP_OK(pda::xgmi_get_handle(flags_, &h[HIP_IPC_HANDLE_SIZE]));
+    return py::bytes(h);
+  }
+  void open(const std::vector<std::string>& all) {
+    TORCH_CHECK((int)all.size() == world_, "xgmi: need one handle blob per rank");
+    c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, dev_));
+    for (int r = 0; r < world_; ++r) {
+      if (r == rank_) continue;
+      TORCH_CHECK(all[r].size() == 2 * HIP_IPC_HANDLE_SIZE, "xgmi: bad handle blob");
+      void* d = nullptr;
+      void* f = nullptr;
+      CHECK_HIP_OK(pda::xgmi_open_handle(all[r].data(), &d));
+      CHECK_HIP_OK(pda::xgmi_open_handle(all[r].data() + HIP_IPC_HANDLE_SIZE, &f));
+      peer_data_[r] = d;
+      peer_flags_[r] = reinterpret_cast<uint32_t*>(f);
+    }
+    opened_ = true;
+  }
+  // in-place all-reduce of a contiguous fp32 / bf16 tensor on this communicator's device
+  void allreduce(Tensor t, bool average) {
+    TORCH_CHECK(opened_ || world_ == 1, "xgmi: open() the peer handles first");
+    check_gpu(t, "t");
+    TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, "xgmi: fp32 / bf16 only");
+    const int64_t n = t.numel(), bytes = n * t.element_size();
+    TORCH_CHECK(n % 8 == 0 && bytes <= cap_, "xgmi: numel must be a multiple of 8 and fit the exchange buffer");
+    c10::DeviceGuard g(t.device());
+    auto st = stream_of(t);
+    CHECK_HIP_OK(hipMemcpyAsync(data_, t.data_ptr(), (size_t)bytes, hipMemcpyDeviceToDevice, st));
+    pda::XgmiArgs a{};
+    for (int r = 0; r < pda::kXgmiMaxRanks; ++r) {
+      a.data[r] = peer_data_[r];
+      a.flags[r] = peer_flags_[r];
+    }
+    a.out = t.data_ptr();
+    a.n = n;
+    a.rank = rank_;
+    a.world = world_;
+    a.scale = average ? 1.f / (float)world_ : 1.f;
+    a.epoch = ++epoch_;
+    a.timeout_ticks = timeout_ticks_;
+    a.err = err_;
+    CHECK_HIP_OK(pda::xgmi_allreduce(a, t.scalar_type() == at::kBFloat16, st));
+  }
+  int error() {
+    int e = 0;
+    CHECK_HIP_OK(hipMemcpy(&e, err_, sizeof(int), hipMemcpyDeviceToHost));
+    return e;
+  }
+  int64_t capacity() const { return cap_; }
+
+ private:
+  int rank_, world_;
+  int64_t cap_;
+  int dev_;
+  void* data_ = nullptr;
+  void* flags_ = nullptr;
+  int* err_ = nullptr;
+  void* peer_data_[pda::kXgmiMaxRanks];
+  uint32_t* peer_flags_[pda::kXgmiMaxRanks];
+  uint32_t epoch_ = 0;
+  long long timeout_ticks_ = 0;
+  bool opened_ = false;
+};
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -703,5 +802,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("rope", &rope);
+  py::class_<XgmiComm>(m, "XgmiComm")
+      .def(py::init<int, int, int64_t, int, double>(), py::arg("rank"), py::arg("world"), py::arg("capacity_bytes"),
+           py::arg("device"), py::arg("timeout") = 10.0)
+      .def("handles", &XgmiComm::handles)
+      .def("open", &XgmiComm::open)
+      .def("allreduce", &XgmiComm::allreduce, py::arg("t"), py::arg("average") = false)
+      .def("error", &XgmiComm::error)
+      .def_property_readonly("capacity", &XgmiComm::capacity);
   pda_rt::bind_runtime(m);
 }

@@ -28,6 +28,27 @@ struct AttnParams {
   float* dkv_part;
 };
 
+// ---- xgmi.hip (one-shot all-reduce over IPC-mapped peer buffers)
+constexpr int kXgmiMaxRanks = 8;
+constexpr int kXgmiMaxBlocks = 128;
+struct XgmiArgs {
+  void* data[kXgmiMaxRanks];       // exchange buffer of every rank (own + IPC-mapped peers)
+  uint32_t* flags[kXgmiMaxRanks];  // flag array of every rank: [2 phases][kXgmiMaxBlocks][kXgmiMaxRanks]
+  void* out;
+  int64_t n;                       // elements, multiple of 8
+  int rank, world;
+  float scale;
+  uint32_t epoch;
+  long long timeout_ticks;         // wall_clock64 ticks before a spin gives up
+  int* err;
+};
+hipError_t xgmi_alloc(void** p, size_t bytes);
+hipError_t xgmi_free(void* p);
+hipError_t xgmi_get_handle(void* p, char* out64);
+hipError_t xgmi_open_handle(const char* in64, void** p);
+hipError_t xgmi_close_handle(void* p);
+hipError_t xgmi_allreduce(const XgmiArgs& a, bool bf16, hipStream_t st);
+
 // ---- optim.hip
 hipError_t sgd_step(float* master, bf16_t* param_bf16, const void* grad, bool grad_bf16, float* mom, int64_t n,
                     float lr, float momentum, float dampening, float wd, bool nesterov, bool first, float gscale,

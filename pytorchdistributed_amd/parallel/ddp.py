@@ -43,6 +43,19 @@ def _mb(env, default):
     return float(os.environ.get(env, default))
 
 
+class _EventWork:
+    """Work handle of a side-stream collective: wait() orders the current stream after it."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+
+    def is_completed(self):
+        return self.event.query()
+
+
 class DistributedDataParallel(tnn.Module):
     def __init__(self, module: tnn.Module, device_ids: Optional[List[int]] = None, output_device=None,
                  broadcast_buffers: bool = True, process_group=None, bucket_cap_mb: Optional[float] = None,
@@ -104,6 +117,15 @@ class DistributedDataParallel(tnn.Module):
         self._callback_queued = False
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
         self.reducer.prepare()
+        # ---- optional one-shot xGMI all-reduce for buckets (PDA_ALLREDUCE=ipc, single node, RCCL world)
+        self.xgmi = None
+        if self.world > 1 and self.backend == "nccl" and process_group is None:
+            from . import xgmi as _xgmi
+
+            if _xgmi.ipc_requested() and _xgmi.single_node():
+                cap = max(b[2] for b in self.bucket_info())
+                self.xgmi = _xgmi.XgmiAllReduce(capacity_mb=cap / 2 ** 20 + 1)
+                self._ipc_stream = torch.cuda.Stream(self.xgmi.device)
 
     # ------------------------------------------------------------------ communication
     def _use_ring(self):
@@ -129,6 +151,17 @@ class DistributedDataParallel(tnn.Module):
         if self._use_ring() and t.device.type == "cpu" and t.dtype in (torch.float32, torch.float64):
             with _watchdog.watch(f"ddp host-ring all_reduce bucket {b} ({nbytes / 2**20:.1f} MB)"):
                 pdist.ring_all_reduce(t, average=True)
+            return
+        if self.xgmi is not None and self.xgmi.fits(t):
+            # one-shot IPC all-reduce on a side stream, ordered after the kernels that produced the bucket
+            ready = torch.cuda.Event()
+            ready.record()
+            with torch.cuda.stream(self._ipc_stream), _timing.range(f"ddp.xgmi_all_reduce.b{b}"):
+                self._ipc_stream.wait_event(ready)
+                self.xgmi(t, average=True)
+                done = torch.cuda.Event()
+                done.record(self._ipc_stream)
+            self._works.append((_EventWork(done), None))
             return
         ticket = _watchdog.arm(f"ddp all_reduce bucket {b} ({nbytes / 2**20:.1f} MB, {t.dtype})")
         with _timing.range(f"ddp.all_reduce.b{b}"):

@@ -209,3 +209,29 @@ def debug_checker_worker(rank, world, mode, outdir):
     debug.disable_collective_checks()
     if mode != "missing":
         pd.destroy_process_group()
+
+
+def xgmi_worker(rank, world, outdir):
+    """2 processes on cuda:0; store/gloo only for the handle exchange."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.xgmi import XgmiAllReduce
+
+    torch.cuda.set_device(0)
+    pd.init_process_group("gloo")
+    comm = XgmiAllReduce(capacity_mb=8, device=torch.device("cuda", 0), timeout_s=20.0)
+    for it, (n, dt) in enumerate([(8, torch.float32), (1000, torch.float32), (4096 * 129, torch.bfloat16),
+                                  (1 << 20, torch.float32), (8, torch.bfloat16), (3 * (1 << 20), torch.bfloat16)]):
+        g = torch.Generator().manual_seed(100 + it)
+        base = [torch.randn(n, generator=g) for _ in range(world)]
+        t = base[rank].to("cuda", dt)
+        comm(t, average=(it % 2 == 1))
+        torch.cuda.synchronize()
+        comm.check()
+        ref = sum(b.to(dt).float() for b in base)
+        if it % 2 == 1:
+            ref = ref / world
+        err = ((t.float().cpu() - ref).norm() / ref.norm()).item()
+        assert err < (1e-6 if dt == torch.float32 else 1e-2), (it, err)
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+        f.write("ok")
+    pd.destroy_process_group()

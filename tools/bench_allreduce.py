@@ -1,0 +1,59 @@
+"""All-reduce bandwidth sweep over bucket sizes: RCCL (torch.distributed
+"nccl") vs the one-shot xGMI IPC kernel, bf16, per size: time, algorithm bandwidth and bus bandwidth
+(2(N-1)/N x bytes / time).  Run on one node:
+
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_allreduce.py
+"""
+import json
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import pytorchdistributed_amd.distributed as pd  # noqa: E402
+from pytorchdistributed_amd.parallel.xgmi import XgmiAllReduce  # noqa: E402
+
+SIZES_MB = [0.25, 1, 2, 4, 8, 16, 32, 64, 128]
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    ms = torch.tensor([s.elapsed_time(e) / iters], device="cuda")
+    dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+    return ms.item()
+
+
+def main():
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    pd.init_process_group("nccl", device_id=local)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    xg = XgmiAllReduce(capacity_mb=max(SIZES_MB) + 1)
+    for mb in SIZES_MB:
+        n = int(mb * 2 ** 20 / 2) // 8 * 8
+        t = torch.randn(n, device="cuda", dtype=torch.bfloat16)
+        rec = {"size_mb": mb, "world": world}
+        for name, fn in [("rccl", lambda: dist.all_reduce(t)), ("xgmi_oneshot", lambda: xg(t))]:
+            ms = timeit(fn)
+            alg = n * 2 / (ms * 1e-3) / 1e9
+            rec[name] = {"ms": round(ms, 4), "alg_GBps": round(alg, 1),
+                         "bus_GBps": round(alg * 2 * (world - 1) / world, 1)}
+        if rank == 0:
+            print(json.dumps(rec), flush=True)
+    xg.check()
+    pd.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
