@@ -484,6 +484,56 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
   }
 
   // epilogue: acc[i][j][r] = C[m0 + wm*WM + 16 i + (lane & 15)][n0 + wn*WN + 16 j + 4 (lane >> 4) + r]
+  if (!epi.slab && !epi.c_f32) {
+    // bf16 output: stage the tile through LDS (row stride BN + 8 elements keeps both the 8-B fragment
+    // writes and the 16-B row reads bank-conflict free), then write whole 16-B chunks of rows —
+    // coalesced stores (and addend loads) instead of 16 rows x 32 B per wave instruction.  The K loop
+    // ended with a barrier, so every wave is done reading the operand tiles.
+    constexpr int SROW = BN + 8;
+    static_assert(BM * SROW * 2 <= 2 * (A_BYTES + B_BYTES), "staging tile must fit the operand LDS");
+    bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int r = wm * WM + 16 * i + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int cc = wn * WN + 16 * j + 4 * (lane >> 4);
+        f32x4 v = acc[i][j];
+        if (epi.bias) {
+          const int64_t n = n0 + cc;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (n + q < N)
+              v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
+        }
+        if (epi.relu) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+        }
+        u16x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
+        *reinterpret_cast<u16x4*>(stg + r * SROW + cc) = o;
+      }
+    }
+    __syncthreads();
+    constexpr int CPR = BN / 8;
+#pragma unroll
+    for (int c = tid; c < BM * CPR; c += NT) {
+      const int r = c / CPR, ch = c % CPR;
+      const int64_t m = m0 + r, n = n0 + ch * 8;
+      if (m >= M || n >= N) continue;
+      const int64_t crow = epi_row(epi, m);
+      u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * SROW + ch * 8);
+      if (epi.addend) {
+        const u16x8 a = *reinterpret_cast<const u16x8*>(epi.addend + crow * epi.ldc + n);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + bf2f(a[q]));
+      }
+      *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int64_t m = m0 + wm * WM + 16 * i + (lane & 15);
@@ -513,14 +563,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] += bf2f(a[r]);
       }
-      if (epi.c_f32) {
-        *reinterpret_cast<f32x4*>((float*)epi.C + crow * epi.ldc + n) = v;
-      } else {
-        u16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = f2bf(v[r]);
-        *reinterpret_cast<u16x4*>((bf16_t*)epi.C + crow * epi.ldc + n) = o;
-      }
+      *reinterpret_cast<f32x4*>((float*)epi.C + crow * epi.ldc + n) = v;
     }
   }
 }
