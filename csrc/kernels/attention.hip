@@ -35,7 +35,7 @@ constexpr float LOG2E = 1.4426950408889634f;
 template <int D>
 __device__ __forceinline__ int row_off(int row, int chunk) {
   if constexpr (D == 128) return row * 256 + ((chunk ^ (row & 15)) << 4);
-  else return row * 128 + ((chunk ^ (row & 7)) << 4);
+  else return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);  // 128-B rows: key on row pairs (16-row reads)
 }
 // transposed-read image (for ds_read_b64_tr_b16 of 4 consecutive rows x 16 columns)
 template <int D>

@@ -62,13 +62,13 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
 // LDS images below are produced by choosing, per lane, WHICH global 16-B chunk it fetches.  Round i
 // of thread t always lands at tile byte i*4096 + t*16.  Invalid (padding / out-of-range) lanes fetch
 // from a zero page, which makes the gathers of the implicit-GEMM convolutions branch-free.
-//   K-major tile [R][64]:  thread t fills row (t >> 3) + 32 i, logical k-chunk (t & 7) ^ ((t >> 3) & 7)
+//   K-major tile [R][64]:  thread t fills row (t >> 3) + 32 i, logical k-chunk (t & 7) ^ ((t >> 4) & 7)
 //   MN-major tile [64][R]: thread t fills k-row t / (R/8) + KSTEP i, column mn_col<R>(t)
 // Loaders return R/32 source pointers per thread per K tile.
 
 __device__ __attribute__((aligned(64))) bf16_t g_zero_page[32];
 
-__device__ __forceinline__ int kmaj_chunk(int tid) { return (tid & 7) ^ ((tid >> 3) & 7); }
+__device__ __forceinline__ int kmaj_chunk(int tid) { return (tid & 7) ^ ((tid >> 4) & 7); }
 
 template <int R>
 __device__ __forceinline__ int mn_swz(int k) {
@@ -341,8 +341,11 @@ struct ConvWgradMN {
 };
 
 // ------------------------------------------------------------------ LDS images
-// K-major [R][64] bf16: 128-B rows, 16-B chunk index XOR (row & 7).
-__device__ __forceinline__ int kmaj_off(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+// K-major [R][64] bf16: 128-B rows, 16-B chunk index XOR ((row >> 1) & 7).  A ds_read_b128 lane group
+// reads one chunk of 16 consecutive rows; rows r and r+2 share a bank base (128-B rows = half a bank
+// row), so the XOR key must differ across the 8 row PAIRS — (row & 7) repeats after 8 rows and made
+// rows r, r+8 collide (measured 16 % bank-conflict cycles, SQ_LDS_BANK_CONFLICT).
+__device__ __forceinline__ int kmaj_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
 // MN-major [64][R] bf16: 32-B slots XOR-swizzled by k (see header).
 template <int R>
@@ -705,15 +708,15 @@ Plan plan_gemm(int64_t M, int64_t N, int64_t K, bool allow_split, int target_blo
   return p;
 }
 
-// conv wgrad: M = Cout, N = R*S*C are small, K = N*P*Q is huge -> deep split-K, ~4 workgroups per CU,
-// with the fp32 partial slabs (written and re-read once) capped at 16 MB so the split traffic stays
-// small next to the operands — but always allowing 4 splits: a big-output layer (7x7 3x3 512: 144
-// tiles) needs them to fill 256 CUs (measured: 1 split 0.24 ms, 3-4 splits 0.10 ms).
+// conv wgrad: M = Cout, N = R*S*C are small, K = N*P*Q is huge -> deep split-K.  Aim for 2 workgroups
+// per CU (one workgroup per CU leaves every SIMD with a single wave: SQ_WAIT_ANY doubled on the
+// 14x14 3x3 256 layer at 252 workgroups), with the fp32 partial slabs (written + re-read once)
+// capped at 48 MB but always allowing 4 splits.
 Plan plan_wgrad(int64_t M, int64_t N, int64_t K, bool allow_split) {
-  int64_t cap = ((int64_t)16 << 20) / (M * N * 4);
+  int64_t cap = ((int64_t)48 << 20) / (M * N * 4);
   if (cap > 1024) cap = 1024;
   if (cap < 4) cap = 4;
-  return plan_gemm(M, N, K, allow_split, 1024, (int)cap);
+  return plan_gemm(M, N, K, allow_split, 512, (int)cap);
 }
 
 template <int BM, int BN, class LA, class LB>
