@@ -75,7 +75,7 @@ def main():
         dwo = torch.empty(Co, R, R, Ci, device=dev, dtype=torch.float32)
         flops = 2.0 * a.batch * P * P * Co * R * R * Ci
         fns = {"fwd": lambda: c.conv_fwd(x, w, st, pad, 1, None, False),
-               "dgrad": lambda: c.conv_dgrad(dy, w, H, H, st, pad, 1),
+               "dgrad": lambda: c.conv_dgrad(dy, w, H, H, st, pad, 1, None),
                "wgrad": lambda: c.conv_wgrad(dy, x, R, R, st, pad, 1, True, dwo)}
         rec = {"op": "conv", "H": H, "Cin": Ci, "Cout": Co, "R": R, "stride": st, "count": cnt}
         for k, fn in fns.items():
