@@ -5,12 +5,11 @@
 // torch's BN followed by separate ReLU / add kernels.  Here every BN is viewed as an [M = N*H*W, C]
 // matrix (C contiguous, a multiple of 8) and handled in two memory-bound passes per direction:
 //   forward : stats    — per-channel shifted sums (x - K_c), (x - K_c)^2 with pivot K_c = x[0, c]
-//                        (cancellation-safe when |mean| >> std), block-reduced in LDS, then added
-//                        into kAccRows = 32 partial rows (workgroup b -> row b mod 32): ~1000
-//                        workgroups hitting the same 2C words serialise at the memory side, 32-deep
-//                        contention does not, and the finalize pass only sums 32 rows;
-//             finalize — 64 channels x 16 row-lanes per workgroup sum the partial rows, produce
-//                        mean / invstd / running stats and the per-channel scale, shift;
+//                        (cancellation-safe when |mean| >> std), block-reduced in LDS, written as
+//                        per-workgroup partial slabs [nrb][C] (plain stores: no same-address atomics,
+//                        which serialise at the memory side when hundreds of workgroups hit 2C words);
+//             finalize — 64 channels x 16 row-lanes per workgroup sum the slabs (coalesced, unrolled),
+//                        produce mean / invstd / running stats and the per-channel scale, shift;
 //             apply    — y = relu(x * scale + shift [+ residual]), scale/shift staged in LDS.
 //   backward: reduce   — sum(dz), sum(dz * (x - mean)) with dz = dy * [y > 0] recomputed from the
 //                        saved output, same slab scheme; finalize -> dgamma / dbeta (parameter dtype)
@@ -24,7 +23,6 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kMaxC = 2048;  // per-channel tables staged in LDS by the apply kernels
-constexpr int kAccRows = 32; // partial-sum rows the reductions accumulate into (atomics, zeroed per call)
 
 struct BnGeom {
   int cv;       // 8-channel vectors per row
@@ -47,10 +45,12 @@ BnGeom bn_geom(int64_t M, int64_t C) {
     g.rpi = kThreads / g.cv;
     g.gy = 1;
   }
-  // ~1024 row blocks (4 workgroups per CU, 8 outstanding 16-B loads per lane: ~64 KB in flight per
-  // CU, what HBM3E latency x bandwidth asks for); >= 64 rows per block keeps the partial slabs that
-  // the finalize pass sums small for the wide (C = 2048) layers.
-  const int target = 1024 / g.gy > 0 ? 1024 / g.gy : 1;
+  // ~512 row blocks (2 workgroups per CU, 8 outstanding 16-B loads per lane) — enough bytes in flight
+  // for HBM3E, while the finalize pass (one workgroup per 64 channels) only sums 512 slab rows;
+  // >= 64 rows per block keeps the slabs small for the wide (C = 2048) layers.  (Measured: 1024
+  // blocks made finalize ~2x slower; atomic accumulation into 32 shared rows instead of slabs made
+  // the reductions 1.3 ms/step slower at bs 256.)
+  const int target = 512 / g.gy > 0 ? 512 / g.gy : 1;
   int64_t rpb = (M + target - 1) / target;
   const int64_t min_rpb = (int64_t)g.rpi * 8 > 64 ? (int64_t)g.rpi * 8 : 64;
   if (rpb < min_rpb) rpb = min_rpb;
@@ -86,15 +86,8 @@ __device__ __forceinline__ void block_col_reduce_store(float (&a)[8], float (&b)
         b[j] += s_b[t * 8 + j];
       }
     }
-    // hierarchical partials: workgroup b adds into row (b mod kAccRows) — kAccRows-deep same-address
-    // contention at most, and the finalize pass sums only kAccRows rows
-    float* pa = slab_a + (int64_t)(blockIdx.x % kAccRows) * C + vcol * 8;
-    float* pb = slab_b + (int64_t)(blockIdx.x % kAccRows) * C + vcol * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      atomicAdd(pa + j, a[j]);
-      atomicAdd(pb + j, b[j]);
-    }
+    store8(slab_a + (int64_t)blockIdx.x * C + vcol * 8, a);
+    store8(slab_b + (int64_t)blockIdx.x * C + vcol * 8, b);
   }
 }
 
@@ -168,7 +161,7 @@ __global__ void __launch_bounds__(kThreads) bn_stats_kernel(const bf16_t* __rest
       }
     }
   }
-  block_col_reduce_store(s1, s2, tx, ty, cols, rpi, vcol, C, slab, slab + (int64_t)kAccRows * C);
+  block_col_reduce_store(s1, s2, tx, ty, cols, rpi, vcol, C, slab, slab + (int64_t)gridDim.x * C);
 }
 
 __device__ __forceinline__ float param_at(const float* f, const bf16_t* b, int c, float dflt) {
@@ -320,7 +313,7 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* _
       }
     }
   }
-  block_col_reduce_store(sa, sb, tx, ty, cols, rpi, vcol, C, slab, slab + (int64_t)kAccRows * C);
+  block_col_reduce_store(sa, sb, tx, ty, cols, rpi, vcol, C, slab, slab + (int64_t)gridDim.x * C);
 }
 
 // dgamma = invstd * sum(dz (x-mean)), dbeta = sum(dz);  coefficients for dx = A*dz + B*x + Cc
@@ -393,8 +386,8 @@ hipError_t launch_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M
 
 // workspace: 2 partial slabs [nrb][C] + 3 per-channel tables [C]
 int64_t bn_workspace_floats(int64_t M, int64_t C) {
-  (void)M;
-  return 2 * (int64_t)kAccRows * C + 3 * C;
+  BnGeom g = bn_geom(M, C);
+  return 2 * (int64_t)g.nrb * C + 3 * C;
 }
 
 hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
@@ -403,13 +396,12 @@ hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M
                         float* save_invstd, float* save_ss, float* ws, hipStream_t st) {
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C);
-  float* scale = save_ss ? save_ss : ws + 2 * (int64_t)kAccRows * C;
+  float* scale = save_ss ? save_ss : ws + 2 * (int64_t)g.nrb * C;
   float* shift = scale + C;
-  PDA_CHECK_HIP(hipMemsetAsync(ws, 0, 2 * (size_t)kAccRows * C * sizeof(float), st));
   bn_stats_kernel<<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(x, M, (int)C, g.cols, g.rpi, g.rpb, ws);
   PDA_CHECK_HIP(hipGetLastError());
   bn_finalize_kernel<true><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
-      x, ws, kAccRows, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum, eps, save_mean,
+      x, ws, g.nrb, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum, eps, save_mean,
       save_invstd, scale, shift);
   PDA_CHECK_HIP(hipGetLastError());
   return launch_apply(x, res, y, M, (int)C, scale, shift, relu, st);
@@ -435,9 +427,8 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const floa
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
   if (relu && !y && !ss) return hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C);
-  float* coef = ws + 2 * (int64_t)kAccRows * C;
+  float* coef = ws + 2 * (int64_t)g.nrb * C;
   const int mask = !relu ? 0 : (y ? 1 : 2);
-  PDA_CHECK_HIP(hipMemsetAsync(ws, 0, 2 * (size_t)kAccRows * C * sizeof(float), st));
   const dim3 rg(g.nrb, g.gy);
   if (mask == 0)
     bn_bwd_reduce_kernel<0><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
@@ -446,7 +437,7 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const floa
   else
     bn_bwd_reduce_kernel<2><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
   PDA_CHECK_HIP(hipGetLastError());
-  bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(ws, kAccRows, M, (int)C, save_mean,
+  bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(ws, g.nrb, M, (int)C, save_mean,
                                                                          save_invstd, gamma_f, gamma_b, dgamma_f,
                                                                          dgamma_b, dbeta_f, dbeta_b, coef);
   PDA_CHECK_HIP(hipGetLastError());
