@@ -25,6 +25,8 @@
 #include "pda_common.h"
 #include "pda_kernels.h"
 
+#include <cstdlib>
+
 namespace pda {
 namespace {
 
@@ -571,6 +573,142 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
   }
 }
 
+// ------------------------------------------------------------------ big-tile kernel (K-major x K-major)
+// 256 x 128 output tile, 8 waves (4 along M x 2 along N, 64 x 64 each — the same per-wave work as the
+// 128-tile kernel), THREE LDS stages of 48 KB (144 KB of the CU's 160 KB): the DMA of tile t+2 is in
+// flight while tile t is multiplied, retired by a counted `s_waitcnt vmcnt(N)` (never 0 inside the
+// loop) and a raw `s_barrier` — `__syncthreads()` would drain every outstanding LDS-DMA with
+// vmcnt(0) (cdna_hip_programming.md, "Pipelining across barriers").  The two 256-thread halves of the
+// workgroup each stage one 128-row half of A and one 64-row half of B with the ordinary 256-thread
+// loaders, so every loader / LDS image of the 128-tile kernel is reused unchanged.
+// Used for the large-M, N >= 128 GEMMs of conv fwd / dgrad / Linear when they yield >= 256 tiles.
+constexpr int BIG_NT = 512;
+constexpr int BIG_A_HALF = 128 * BK * 2, BIG_B_HALF = 64 * BK * 2;
+constexpr int BIG_STAGE = 2 * BIG_A_HALF + 2 * BIG_B_HALF;
+constexpr int BIG_LDS = 3 * BIG_STAGE;
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else static_assert(N == 0 || N == 6, "add the literal");
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <class LA, class LB>
+__global__ void __launch_bounds__(BIG_NT, 1) gemm_big_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K,
+                                                            int tiles_n, Epi epi) {
+  static_assert(LA::kMajor && LB::kMajor && LA::NCH == 4 && LB::NCH == 2, "K-major 128-row A / 64-row B loaders");
+  constexpr int BM = 256, BN = 128, TM = 4, TN = 4;
+  constexpr int LPT = LA::NCH + LB::NCH;  // glds per thread per K tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = tid >> 8, gtid = tid & 255, gwid = wid & 3;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntiles = gridDim.x;
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int tn = tile % tiles_n, tm = tile / tiles_n;
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int nk = (int)((K + BK - 1) / BK);
+
+  typename LA::State sa;
+  typename LB::State sb;
+  la.init(sa, m0 + 128 * grp, gtid);
+  lb.init(sb, n0 + 64 * grp, gtid);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int t) {
+    char* base = smem + (t % 3) * BIG_STAGE;
+    glds_tile(la, sa, (int64_t)t * BK, base + grp * BIG_A_HALF, gwid);
+    glds_tile(lb, sb, (int64_t)t * BK, base + 2 * BIG_A_HALF + grp * BIG_B_HALF, gwid);
+  };
+  if (nk > 0) issue(0);
+  if (nk > 1) {
+    issue(1);
+    wait_vm<LPT>();
+  } else {
+    wait_vm<0>();
+  }
+  raw_barrier();
+  for (int t = 0; t < nk; ++t) {
+    if (t + 2 < nk) issue(t + 2);
+    const char* base = smem + (t % 3) * BIG_STAGE;
+    const char* As = base + (wm >> 1) * BIG_A_HALF;
+    const char* Bs = base + 2 * BIG_A_HALF + wn * BIG_B_HALF;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      mfma_bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = read_frag<true, 128>(As, (wm & 1) * 64 + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = read_frag<true, 64>(Bs, 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (t + 2 < nk) wait_vm<LPT>();  // tile t+1 landed, tile t+2 still in flight
+    else wait_vm<0>();
+    raw_barrier();
+  }
+
+  // epilogue (bf16 output only — the launcher routes fp32 / split-K work to the 128-tile kernel):
+  // stage the tile through LDS, then coalesced 16-B row stores (+ addend)
+  constexpr int SROW = BN + 8;
+  static_assert(BM * SROW * 2 <= BIG_LDS, "staging tile must fit");
+  bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * 64 + 16 * i + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cc = wn * 64 + 16 * j + 4 * (lane >> 4);
+      f32x4 v = acc[i][j];
+      if (epi.bias) {
+        const int64_t n = n0 + cc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (n + q < N)
+            v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
+      }
+      if (epi.relu) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+      }
+      u16x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
+      *reinterpret_cast<u16x4*>(stg + r * SROW + cc) = o;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int c = tid; c < BM * CPR; c += BIG_NT) {
+    const int r = c / CPR, ch = c % CPR;
+    const int64_t m = m0 + r, n = n0 + ch * 8;
+    if (m >= M || n >= N) continue;
+    const int64_t crow = epi_row(epi, m);
+    u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * SROW + ch * 8);
+    if (epi.addend) {
+      const u16x8 a = *reinterpret_cast<const u16x8*>(epi.addend + crow * epi.ldc + n);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + bf2f(a[q]));
+    }
+    *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
+  }
+}
+
 // Split-K reduction: out[m, n] = act(sum_s slab[s, m, n] + bias[n]).  A workgroup is (256 / L) output
 // float4s x L split lanes; each lane keeps 8 slab loads in flight and the L partials meet in LDS, so
 // a small output with a deep split (conv wgrad of 64 x 64 with ~1000 slabs) still spreads over
@@ -739,9 +877,38 @@ hipError_t launch(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, c
   return hipSuccess;
 }
 
+// The 256 x 128 three-stage kernel pays off when the GEMM has plenty of tiles to fill the chip;
+// PDA_GEMM_BIG=0 disables it (A/B against the 128-tile kernel).
+bool use_big(int64_t M, int64_t N, const Plan& p, const Epi& epi) {
+  static const int enabled = [] {
+    const char* e = getenv("PDA_GEMM_BIG");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  if (!enabled || p.splits > 1 || epi.c_f32 || epi.slab) return false;
+  const int64_t tiles = ((M + 255) / 256) * ((N + 127) / 128);
+  return N >= 128 && tiles >= 256;
+}
+
+template <class LA, class LB>
+hipError_t launch_big(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st) {
+  static bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_big_kernel<LA, LB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, BIG_LDS);
+    return true;
+  }();
+  (void)attr;
+  const int tiles_n = (int)((N + 127) / 128);
+  const int ntiles = (int)((M + 255) / 256) * tiles_n;
+  gemm_big_kernel<LA, LB><<<ntiles, BIG_NT, BIG_LDS, st>>>(la, lb, M, N, K, tiles_n, epi);
+  return hipGetLastError();
+}
+
 template <template <int> class TA, template <int> class TB, class MakeA, class MakeB>
 hipError_t dispatch_bn(int64_t M, int64_t N, int64_t K, const Plan& p, Epi epi, float* slab, hipStream_t st,
                        MakeA make_a, MakeB make_b) {
+  if constexpr (TA<128>::kMajor && TB<64>::kMajor) {
+    if (use_big(M, N, p, epi)) return launch_big(make_a(TA<128>{}), make_b(TB<64>{}), M, N, K, epi, st);
+  }
   if (p.bm == 64) {
     if (p.bn == 64) return launch<64, 64>(make_a(TA<64>{}), make_b(TB<64>{}), M, N, K, p, epi, slab, st);
     return launch<64, 128>(make_a(TA<64>{}), make_b(TB<128>{}), M, N, K, p, epi, slab, st);

@@ -58,6 +58,16 @@ def test_gemm_identity_asymmetric():
     assert torch.equal(out.cpu(), B.to(torch.bfloat16).float())
 
 
+def test_gemm_big_tile_path():
+    """M x N large enough for the 256x128 three-stage kernel, bias + ReLU epilogue, ragged edges."""
+    M, N, K = 8200, 1032, 520
+    A, W, b = torch.randn(M, K), torch.randn(N, K) * 0.05, torch.randn(N)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C().gemm(bf(A), True, K, bf(W), True, K, out, N, M, N, K, b.to(DEV), True, False)
+    ref = torch.relu(A.to(torch.bfloat16).float() @ W.to(torch.bfloat16).float().t() + b)
+    assert rel_err(out.cpu(), ref) < 1e-2
+
+
 def test_gemm_bias_relu_bf16_out():
     M, N, K = 257, 136, 96
     A, W, b = torch.randn(M, K), torch.randn(N, K), torch.randn(N)
@@ -82,6 +92,9 @@ CONV_CASES = [
     (2, 13, 10, 32, 48, 3, 3, 1),       # stride 3: 9 phases, some with no taps
     (2, 12, 12, 32, 64, 3, 1, 2, 2),    # dilation 2 (stride-1 phased dgrad)
     (2, 13, 13, 32, 64, 3, 2, 2, 2),    # dilation 2 + stride 2: folded dgrad
+    (16, 56, 56, 64, 256, 1, 1, 0),     # >= 256 tiles: 256x128 three-stage kernel (fwd)
+    (16, 56, 56, 256, 64, 1, 1, 0),     # ... and for the dgrad (with and without the fused addend)
+    (8, 57, 57, 128, 128, 3, 1, 1),     # big tiles with ragged M and 3x3 gathers
 ]
 
 
