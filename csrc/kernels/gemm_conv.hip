@@ -877,16 +877,19 @@ hipError_t launch(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, c
   return hipSuccess;
 }
 
-// The 256 x 128 three-stage kernel pays off when the GEMM has plenty of tiles to fill the chip;
-// PDA_GEMM_BIG=0 disables it (A/B against the 128-tile kernel).
-bool use_big(int64_t M, int64_t N, const Plan& p, const Epi& epi) {
-  static const int enabled = [] {
+// The 256 x 128 three-stage kernel only pays off on long-K GEMMs with many tiles (8192^3: 0.96 vs
+// 0.88 PF/s); on every ResNet-50 conv shape and at 4096^3 the 128-tile kernel (2 workgroups/CU, more
+// tiles in flight) measured equal or faster (profiles/r1_conv_gemm_microbench_v6*.jsonl), so it is
+// selected for K >= 2048 with >= 512 tiles.  PDA_GEMM_BIG=0 disables it, =1 forces it where legal.
+bool use_big(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) {
+  static const int mode = [] {
     const char* e = getenv("PDA_GEMM_BIG");
-    return (e && e[0] == '0') ? 0 : 1;
+    return e ? (e[0] == '0' ? 0 : 2) : 1;
   }();
-  if (!enabled || p.splits > 1 || epi.c_f32 || epi.slab) return false;
+  if (mode == 0 || p.splits > 1 || epi.c_f32 || epi.slab || N < 128) return false;
   const int64_t tiles = ((M + 255) / 256) * ((N + 127) / 128);
-  return N >= 128 && tiles >= 256;
+  if (mode == 2) return tiles >= 1;
+  return K >= 2048 && tiles >= 512;
 }
 
 template <class LA, class LB>
@@ -907,7 +910,7 @@ template <template <int> class TA, template <int> class TB, class MakeA, class M
 hipError_t dispatch_bn(int64_t M, int64_t N, int64_t K, const Plan& p, Epi epi, float* slab, hipStream_t st,
                        MakeA make_a, MakeB make_b) {
   if constexpr (TA<128>::kMajor && TB<64>::kMajor) {
-    if (use_big(M, N, p, epi)) return launch_big(make_a(TA<128>{}), make_b(TB<64>{}), M, N, K, epi, st);
+    if (use_big(M, N, K, p, epi)) return launch_big(make_a(TA<128>{}), make_b(TB<64>{}), M, N, K, epi, st);
   }
   if (p.bm == 64) {
     if (p.bn == 64) return launch<64, 64>(make_a(TA<64>{}), make_b(TB<64>{}), M, N, K, p, epi, slab, st);

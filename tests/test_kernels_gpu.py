@@ -59,8 +59,8 @@ def test_gemm_identity_asymmetric():
 
 
 def test_gemm_big_tile_path():
-    """M x N large enough for the 256x128 three-stage kernel, bias + ReLU epilogue, ragged edges."""
-    M, N, K = 8200, 1032, 520
+    """Long-K GEMM with >= 512 tiles: the 256x128 three-stage kernel, bias + ReLU epilogue, ragged edges."""
+    M, N, K = 16400, 1032, 2056
     A, W, b = torch.randn(M, K), torch.randn(N, K) * 0.05, torch.randn(N)
     out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
     C().gemm(bf(A), True, K, bf(W), True, K, out, N, M, N, K, b.to(DEV), True, False)
