@@ -201,6 +201,36 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optio
   return {y, mean, invstd, ss};
 }
 
+std::vector<Tensor> bn_fwd_train_sums(Tensor x, Tensor sums, Tensor shift, c10::optional<Tensor> res,
+                                      c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
+                                      c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
+                                      double momentum, double eps, bool relu) {
+  check_bf16(x, "x");
+  check_f32(sums, "sums");
+  check_f32(shift, "shift");
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && sums.numel() == 2 * C && shift.numel() == C);
+  if (res) {
+    check_bf16(*res, "residual");
+    TORCH_CHECK(res->sizes() == x.sizes());
+  }
+  const float *gf, *bfp;
+  const pda::bf16_t *gb, *bb;
+  bn_param_ptrs(gamma, &gf, &gb, C);
+  bn_param_ptrs(beta, &bfp, &bb, C);
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty_like(x);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({C}, fo), invstd = at::empty({C}, fo), ss = at::empty({2, C}, fo);
+  CHECK_HIP_OK(pda::bn_fwd_train_sums(bp(x), res ? bp(*res) : nullptr, bpm(y), M, C, sums.data_ptr<float>(),
+                                      shift.data_ptr<float>(), gf, gb, bfp, bb,
+                                      running_mean ? running_mean->data_ptr<float>() : nullptr,
+                                      running_var ? running_var->data_ptr<float>() : nullptr, (float)momentum,
+                                      (float)eps, relu, mean.data_ptr<float>(), invstd.data_ptr<float>(),
+                                      ss.data_ptr<float>(), stream_of(x)));
+  return {y, mean, invstd, ss};
+}
+
 Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
                    Tensor running_mean, Tensor running_var, double eps, bool relu) {
   check_bf16(x, "x");
@@ -372,9 +402,34 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, c1
   c10::DeviceGuard g(x.device());
   Tensor y = at::empty({N, P, Q, Cout}, x.options());
   CHECK_HIP_OK(pda::conv2d_fwd(bp(x), bp(w), bpm(y), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
-                               bias ? bias->data_ptr() : nullptr, bias ? !is_bf16(*bias) : false, relu,
-                               stream_of(x)));
+                               bias ? bias->data_ptr() : nullptr, bias ? !is_bf16(*bias) : false, relu, nullptr,
+                               nullptr, stream_of(x)));
   return y;
+}
+
+// conv forward that also returns the BatchNorm sums of its output: [y, sums[2, Cout]] with
+// sums[0] = sum(y - shift), sums[1] = sum((y - shift)^2) over N*P*Q (no separate statistics pass)
+std::vector<Tensor> conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, Tensor shift) {
+  conv_check(x, w);
+  check_f32(shift, "shift");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int Cout = w.size(0), R = w.size(1), S = w.size(2);
+  TORCH_CHECK(shift.numel() == Cout);
+  const int P = (H + 2 * pad - dil * (R - 1) - 1) / stride + 1, Q = (W + 2 * pad - dil * (S - 1) - 1) / stride + 1;
+  TORCH_CHECK(P > 0 && Q > 0);
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty({N, P, Q, Cout}, x.options());
+  const int64_t M = (int64_t)N * P * Q;
+  const int64_t rows = pda::conv_fwd_stat_rows(M, Cout);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor slab = at::empty({rows, 2 * (int64_t)Cout}, fo);
+  CHECK_HIP_OK(pda::conv2d_fwd(bp(x), bp(w), bpm(y), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil, nullptr, false,
+                               false, slab.data_ptr<float>(), shift.data_ptr<float>(), stream_of(x)));
+  Tensor sums = at::empty({2, (int64_t)Cout}, fo);
+  Tensor ws = at::empty({pda::colreduce_ws_floats(rows, 2 * (int64_t)Cout, 1)}, fo);
+  CHECK_HIP_OK(pda::colsum(slab.data_ptr<float>(), false, sums.data_ptr<float>(), rows, 2 * (int64_t)Cout,
+                           ws.data_ptr<float>(), stream_of(x)));
+  return {y, sums};
 }
 
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad, int64_t dil,
@@ -786,6 +841,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("fill_randint", &fill_randint);
   m.def("gemm", &gemm);
   m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd_stats", &conv_fwd_stats);
+  m.def("bn_fwd_train_sums", &bn_fwd_train_sums);
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("act_fwd", &act_fwd);

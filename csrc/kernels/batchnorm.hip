@@ -172,8 +172,8 @@ __device__ __forceinline__ float param_at(const float* f, const bf16_t* b, int c
 // TRAIN: statistics from the slabs; eval: from the running statistics.  Writes scale/shift [C].
 template <bool TRAIN>
 __global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
-    const bf16_t* __restrict__ x, const float* __restrict__ slab, int nrb, int64_t M, int C,
-    const float* __restrict__ gamma_f, const bf16_t* __restrict__ gamma_b, const float* __restrict__ beta_f,
+    const bf16_t* __restrict__ x, const float* __restrict__ pivot, const float* __restrict__ slab, int nrb,
+    int64_t M, int C, const float* __restrict__ gamma_f, const bf16_t* __restrict__ gamma_b, const float* __restrict__ beta_f,
     const bf16_t* __restrict__ beta_b, float* __restrict__ running_mean, float* __restrict__ running_var,
     float momentum, float eps, float* __restrict__ save_mean, float* __restrict__ save_invstd,
     float* __restrict__ scale, float* __restrict__ shift) {
@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
     const float invM = 1.f / (float)M;
     const float m1 = s1 * invM;
     const float var = fmaxf(s2 * invM - m1 * m1, 0.f);
-    mean = bf2f(x[c]) + m1;
+    mean = (pivot ? pivot[c] : bf2f(x[c])) + m1;
     invstd = rsqrtf(var + eps);
     save_mean[c] = mean;
     save_invstd[c] = invstd;
@@ -401,10 +401,24 @@ hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M
   bn_stats_kernel<<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(x, M, (int)C, g.cols, g.rpi, g.rpb, ws);
   PDA_CHECK_HIP(hipGetLastError());
   bn_finalize_kernel<true><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
-      x, ws, g.nrb, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum, eps, save_mean,
+      x, nullptr, ws, g.nrb, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum, eps, save_mean,
       save_invstd, scale, shift);
   PDA_CHECK_HIP(hipGetLastError());
   return launch_apply(x, res, y, M, (int)C, scale, shift, relu, st);
+}
+
+hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* sums,
+                             const float* shift, const float* gamma_f, const bf16_t* gamma_b, const float* beta_f,
+                             const bf16_t* beta_b, float* running_mean, float* running_var, float momentum, float eps,
+                             bool relu, float* save_mean, float* save_invstd, float* save_ss, hipStream_t st) {
+  if (C > kMaxC || C % 8) return hipErrorInvalidValue;
+  float* scale = save_ss;
+  float* shift_out = save_ss + C;
+  bn_finalize_kernel<true><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
+      x, shift, sums, 1, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum, eps,
+      save_mean, save_invstd, scale, shift_out);
+  PDA_CHECK_HIP(hipGetLastError());
+  return launch_apply(x, res, y, M, (int)C, scale, shift_out, relu, st);
 }
 
 hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
@@ -414,7 +428,7 @@ hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M,
   float* scale = ws;
   float* shift = ws + C;
   bn_finalize_kernel<false><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
-      x, nullptr, 0, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, const_cast<float*>(running_mean),
+      x, nullptr, nullptr, 0, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, const_cast<float*>(running_mean),
       const_cast<float*>(running_var), 0.f, eps, nullptr, nullptr, scale, shift);
   PDA_CHECK_HIP(hipGetLastError());
   return launch_apply(x, res, y, M, (int)C, scale, shift, relu, st);

@@ -411,6 +411,10 @@ struct Epi {
   // optional bf16 addend with C's layout (gradient accumulation fused into the store: conv1's dgrad
   // adds the residual-branch gradient of a bottleneck instead of a separate add kernel)
   const bf16_t* addend;
+  // optional BatchNorm statistics of the (bf16-rounded) output: per row-tile partial sums of (y - K)
+  // and (y - K)^2 per column, written to stats[tile_m][2][N] (K = stats_shift, e.g. running mean)
+  float* stats;
+  const float* stats_shift;
 };
 
 __device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
@@ -523,6 +527,18 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
     }
     __syncthreads();
     constexpr int CPR = BN / 8;
+    static_assert(NT % CPR == 0, "a thread keeps one column chunk");
+    // column chunk of this thread is fixed (NT % CPR == 0): BN statistics accumulate in registers
+    float st1[8], st2[8], kshift[8];
+    const bool want_stats = epi.stats != nullptr;
+    {
+      const int64_t n = n0 + (tid % CPR) * 8;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        st1[q] = st2[q] = 0.f;
+        kshift[q] = (want_stats && n + q < N) ? epi.stats_shift[n + q] : 0.f;
+      }
+    }
 #pragma unroll
     for (int c = tid; c < BM * CPR; c += NT) {
       const int r = c / CPR, ch = c % CPR;
@@ -535,7 +551,46 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + bf2f(a[q]));
       }
+      if (want_stats) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float d = bf2f(v[q]) - kshift[q];
+          st1[q] += d;
+          st2[q] += d * d;
+        }
+      }
       *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
+    }
+    if (want_stats) {
+      // lanes sharing a column chunk: xor over the lane bits above log2(CPR), then the 4 waves in LDS
+#pragma unroll
+      for (int off = CPR; off < 64; off <<= 1)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          st1[q] += __shfl_xor(st1[q], off, 64);
+          st2[q] += __shfl_xor(st2[q], off, 64);
+        }
+      __syncthreads();  // staging tile no longer read
+      float* red = reinterpret_cast<float*>(smem);  // [NT/64 waves][BN][2]
+      if (lane < CPR) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          red[(wid * BN + lane * 8 + q) * 2] = st1[q];
+          red[(wid * BN + lane * 8 + q) * 2 + 1] = st2[q];
+        }
+      }
+      __syncthreads();
+      if (tid < BN && n0 + tid < N) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int w = 0; w < NT / 64; ++w) {
+          a += red[(w * BN + tid) * 2];
+          b += red[(w * BN + tid) * 2 + 1];
+        }
+        float* row = epi.stats + (int64_t)tm * 2 * N;
+        row[n0 + tid] = a;
+        row[N + n0 + tid] = b;
+      }
     }
     return;
   }
@@ -886,7 +941,7 @@ bool use_big(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) {
     const char* e = getenv("PDA_GEMM_BIG");
     return e ? (e[0] == '0' ? 0 : 2) : 1;
   }();
-  if (mode == 0 || p.splits > 1 || epi.c_f32 || epi.slab || N < 128) return false;
+  if (mode == 0 || p.splits > 1 || epi.c_f32 || epi.slab || epi.stats || N < 128) return false;
   const int64_t tiles = ((M + 255) / 256) * ((N + 127) / 128);
   if (mode == 2) return tiles >= 1;
   return K >= 2048 && tiles >= 512;
@@ -966,12 +1021,20 @@ int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, 
 }
 
 // y[N,P,Q,Cout] = conv(x[N,H,W,C], w[Cout,R,S,C]) (+bias, relu)
+int64_t conv_fwd_stat_rows(int64_t M, int64_t Cout) {
+  Plan p = plan_gemm(M, Cout, 1, false, 512);
+  return p.tiles_m;
+}
+
 hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int Cout, int R, int S,
                       int P, int Q, int stride, int pad, int dil, const void* bias, bool bias_f32, bool relu,
-                      hipStream_t st) {
+                      float* stats, const float* stats_shift, hipStream_t st) {
   const int64_t M = (int64_t)N * P * Q, Nn = Cout, K = (int64_t)R * S * C;
   Plan p = plan_gemm(M, Nn, K, false, 512);
   Epi epi{y, Cout, 0, bias, bias_f32 ? 1 : 0, relu ? 1 : 0, nullptr};
+  epi.stats = stats;
+  epi.stats_shift = stats_shift;
+
   ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
   auto mk_a = [&](auto t) { t.x = x; t.g = g; t.M = M; t.K = K; return t; };
   auto mk_b = [&](auto t) { t.p = w; t.rows = Nn; t.K = K; t.ld = K; return t; };

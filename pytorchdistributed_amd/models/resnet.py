@@ -46,13 +46,14 @@ class Bottleneck(tnn.Module):
     def forward(self, x):
         # x feeds conv1 and the shortcut: its two gradients are summed inside conv1's (or the
         # downsample conv's) dgrad store instead of by a separate autograd add (ops/grad_join.py)
+        # Every conv also reduces the batch statistics of the BN it feeds in its epilogue (bn=...).
         join = GradJoin(2) if (x.is_cuda and x.requires_grad and torch.is_grad_enabled()) else None
-        out = self.bn1(self.conv1(x, grad_join=join), relu=True)
-        out = self.bn2(self.conv2(out), relu=True)
+        out = self.bn1(self.conv1(x, grad_join=join, bn=self.bn1), relu=True)
+        out = self.bn2(self.conv2(out, bn=self.bn2), relu=True)
         if self.downsample is not None:
-            idn = self.downsample[1](self.downsample[0](x, grad_join=join))
-            return self.bn3(self.conv3(out), residual=idn, relu=True)
-        return self.bn3(self.conv3(out), residual=x, relu=True, residual_join=join)
+            idn = self.downsample[1](self.downsample[0](x, grad_join=join, bn=self.downsample[1]))
+            return self.bn3(self.conv3(out, bn=self.bn3), residual=idn, relu=True)
+        return self.bn3(self.conv3(out, bn=self.bn3), residual=x, relu=True, residual_join=join)
 
 
 class Stem(tnn.Module):
@@ -68,7 +69,7 @@ class Stem(tnn.Module):
         if x.is_cuda and x.shape[-1] % 8 != 0:
             x = F.pad(x, (0, 8 - x.shape[-1] % 8))
         x = x.contiguous()
-        return self.maxpool(self.bn1(self.conv1(x), relu=True))
+        return self.maxpool(self.bn1(self.conv1(x, bn=self.bn1), relu=True))
 
 
 class ResNet(tnn.Module):

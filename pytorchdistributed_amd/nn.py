@@ -56,7 +56,15 @@ class Conv2d(tnn.Module):
         self.bias = tnn.Parameter(torch.zeros(out_channels, device=device, dtype=dtype)) if bias else None
         _kaiming_uniform_(self.weight, in_channels * k * k)
 
-    def forward(self, x, relu=False, grad_join=None):
+    def forward(self, x, relu=False, grad_join=None, bn=None):
+        """``bn``: the BatchNorm2d this conv feeds — in training on the GPU the conv epilogue computes
+        that BN's batch statistics and ``(y, stats)`` is returned (pass ``stats`` to the BN)."""
+        if bn is not None:
+            if x.is_cuda and bn.training and self.bias is None and not relu and x.dtype == torch.bfloat16:
+                return ops.conv2d_bn_stats(x, self.weight, self.stride, self.padding, self.dilation,
+                                           bn.running_mean, grad_join)
+            return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, relu,
+                              grad_join), None
         return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, relu, grad_join)
 
     def extra_repr(self):
@@ -88,11 +96,14 @@ class BatchNorm2d(tnn.Module):
             self.running_var = fn(rv).float()
         return self
 
-    def forward(self, x, residual=None, relu=False, residual_join=None):
+    def forward(self, x, residual=None, relu=False, residual_join=None, stats=None):
         if self.training:
             self.num_batches_tracked.add_(1)
+        if isinstance(x, tuple):  # (y, stats) from Conv2d(..., bn=self)
+            x, stats = x
         return ops.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
-                              self.momentum, self.eps, residual=residual, relu=relu, residual_join=residual_join)
+                              self.momentum, self.eps, residual=residual, relu=relu, residual_join=residual_join,
+                              stats=stats)
 
 
 class ReLU(tnn.Module):

@@ -5,7 +5,7 @@ weights are ``[C_out, R, S, C_in]`` (OHWI).  Every op has exactly one GPU implem
 kernel, which raises if the extension is missing) and a PyTorch reference implementation used for
 CPU tensors (tests, the gloo plumbing config) and as the numerics oracle.
 """
-from .conv import conv2d  # noqa: F401
+from .conv import conv2d, conv2d_bn_stats  # noqa: F401
 from .linear import linear  # noqa: F401
 from .norm import batch_norm, layer_norm, rms_norm  # noqa: F401
 from .pool import max_pool2d, global_avg_pool2d  # noqa: F401

@@ -33,6 +33,10 @@ class _Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        return _Conv2dFn._backward(ctx, dy)
+
+    @staticmethod
+    def _backward(ctx, dy):
         x, w, y = ctx.saved_tensors
         stride, padding, dilation, relu, has_bias = ctx.cfg
         dy = dy.contiguous()
@@ -52,6 +56,37 @@ class _Conv2dFn(torch.autograd.Function):
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.reshape(-1, dy.shape[-1]).sum(0, dtype=torch.float32).to(dy.dtype)
         return dx, dw, db, None, None, None, None, None
+
+
+class _Conv2dStatsFn(torch.autograd.Function):
+    """Conv forward that also emits the BatchNorm sums of its output from the GEMM epilogue
+    (sum(y - K), sum((y - K)^2) per channel, K = ``shift``), so the following BatchNorm skips its
+    statistics pass over y.  Backward is the plain conv backward."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, padding, dilation, shift, join):
+        x = x.contiguous()
+        w = w.contiguous()
+        y, sums = C().conv_fwd_stats(x, w, stride, padding, dilation, shift)
+        ctx.save_for_backward(x, w, None)
+        ctx.cfg = (stride, padding, dilation, False, False)
+        ctx.wparam = w
+        ctx.join = join
+        ctx.mark_non_differentiable(sums)
+        return y, sums
+
+    @staticmethod
+    def backward(ctx, dy, _dsums):
+        dx, dw, _db, *_ = _Conv2dFn._backward(ctx, dy)
+        return dx, dw, None, None, None, None, None
+
+
+def conv2d_bn_stats(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding: int = 0, dilation: int = 1,
+                    shift: torch.Tensor = None, grad_join=None):
+    """GPU only: ``(y, sums)`` with ``sums[0] = sum(y - shift)``, ``sums[1] = sum((y - shift)^2)``."""
+    if weight.shape[-1] != x.shape[-1]:
+        weight = F.pad(weight, (0, x.shape[-1] - weight.shape[-1]))
+    return _Conv2dStatsFn.apply(x, weight, stride, padding, dilation, shift, grad_join)
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias=None, stride: int = 1, padding: int = 0, dilation: int = 1,

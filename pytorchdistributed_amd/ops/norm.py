@@ -15,12 +15,16 @@ from ..parallel.flat import grad_target
 
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu, join):
+    def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu, join,
+                sums=None, shift=None):
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()
         ss = None
-        if training:
+        if training and sums is not None:  # statistics already reduced by the producing conv's epilogue
+            y, mean, invstd, ss = C().bn_fwd_train_sums(x, sums, shift, residual, gamma, beta, running_mean,
+                                                        running_var, momentum, eps, relu)
+        elif training:
             y, mean, invstd, ss = C().bn_fwd_train(x, residual, gamma, beta, running_mean, running_var, momentum,
                                                    eps, relu)
         else:
@@ -51,7 +55,7 @@ class _BatchNormFn(torch.autograd.Function):
         db = dbeta if ctx.needs_input_grad[2] else None
         if has_res and ctx.join is not None:
             dres = ctx.join.contribute(dres)  # usually stashed for the consumer conv's dgrad epilogue
-        return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None, None
+        return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None, None, None, None
 
 
 def _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu):
@@ -69,12 +73,14 @@ def _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, trainin
 
 
 def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True, momentum=0.1, eps=1e-5,
-               residual=None, relu=False, residual_join=None):
+               residual=None, relu=False, residual_join=None, stats=None):
     """BatchNorm over the last (channel) dim of ``x`` (any leading dims), then ``+residual``, then ReLU.
-    ``residual_join``: the residual's gradient is handed to the join instead of autograd's add."""
+    ``residual_join``: the residual's gradient is handed to the join instead of autograd's add.
+    ``stats``: ``(sums, shift)`` from :func:`~.conv.conv2d_bn_stats` — skips the statistics pass."""
     if x.is_cuda and x.dtype == torch.bfloat16:
+        sums, shift = stats if stats is not None else (None, None)
         return _BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
-                                  relu, residual_join)
+                                  relu, residual_join, sums, shift)
     return _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu)
 
 

@@ -126,6 +126,31 @@ def test_conv_fwd_dgrad_wgrad(case):
     assert rel_err(dwb.cpu(), w.grad) < 1e-2
 
 
+@pytest.mark.parametrize("case", [(2, 16, 16, 64, 64, 1, 1, 0), (3, 15, 15, 32, 136, 3, 2, 1), (1, 7, 7, 64, 2048, 1, 1, 0)])
+def test_conv_fwd_epilogue_bn_sums(case):
+    """BN statistics reduced in the conv epilogue == sums over the stored bf16 output."""
+    N, H, W, Cin, Cout, k, s, p = case
+    torch.manual_seed(4)
+    x = torch.randn(N, H, W, Cin).to(torch.bfloat16)
+    w = (torch.randn(Cout, k, k, Cin) / math.sqrt(Cin * k * k)).to(torch.bfloat16)
+    shift = torch.randn(Cout) * 0.1
+    y, sums = C().conv_fwd_stats(x.to(DEV), w.to(DEV), s, p, 1, shift.to(DEV))
+    y_plain = C().conv_fwd(x.to(DEV), w.to(DEV), s, p, 1, None, False)
+    assert torch.equal(y, y_plain)
+    d = y.float().cpu().reshape(-1, Cout) - shift
+    ref = torch.stack([d.sum(0), (d * d).sum(0)])
+    assert rel_err(sums.cpu(), ref) < 1e-4
+    # BN from the epilogue sums == BN with its own statistics pass
+    g, b = torch.rand(Cout) + 0.5, torch.randn(Cout)
+    rm1, rv1 = shift.clone().to(DEV), torch.ones(Cout, device=DEV)
+    rm2, rv2 = shift.clone().to(DEV), torch.ones(Cout, device=DEV)
+    ya, ma, ia, ssa = C().bn_fwd_train_sums(y, sums, rm1.clone(), None, g.to(DEV), b.to(DEV), rm1, rv1, 0.1, 1e-5,
+                                            True)
+    yb, mb, ib, ssb = C().bn_fwd_train(y, None, g.to(DEV), b.to(DEV), rm2, rv2, 0.1, 1e-5, True)
+    assert rel_err(ma.cpu(), mb.cpu()) < 1e-4 and rel_err(ia.cpu(), ib.cpu()) < 1e-4
+    assert rel_err(ya.cpu(), yb.cpu()) < 1e-2 and rel_err(rv1.cpu(), rv2.cpu()) < 1e-4
+
+
 # ----------------------------------------------------------------------------- batch norm
 @pytest.mark.parametrize("shape", [(4, 8, 8, 64), (2, 7, 7, 2048), (3, 5, 5, 200), (2, 56, 56, 256),
                                    (64, 28, 28, 64)])
