@@ -61,8 +61,9 @@ class Conv2d(tnn.Module):
         that BN's batch statistics and ``(y, stats)`` is returned (pass ``stats`` to the BN)."""
         if bn is not None:
             if x.is_cuda and bn.training and self.bias is None and not relu and x.dtype == torch.bfloat16:
-                return ops.conv2d_bn_stats(x, self.weight, self.stride, self.padding, self.dilation,
-                                           bn.running_mean, grad_join)
+                y, sums = ops.conv2d_bn_stats(x, self.weight, self.stride, self.padding, self.dilation,
+                                              bn.running_mean, grad_join)
+                return y, (sums, bn.running_mean)
             return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, relu,
                               grad_join), None
         return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, relu, grad_join)
