@@ -8,10 +8,14 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 import torch.nn as tnn
 
 from . import ops
+
+_EPILOGUE_STATS = os.environ.get("PDA_BN_EPILOGUE_STATS", "0") == "1"
 
 
 def _kaiming_uniform_(w: torch.Tensor, fan_in: int):
@@ -57,10 +61,15 @@ class Conv2d(tnn.Module):
         _kaiming_uniform_(self.weight, in_channels * k * k)
 
     def forward(self, x, relu=False, grad_join=None, bn=None):
-        """``bn``: the BatchNorm2d this conv feeds — in training on the GPU the conv epilogue computes
-        that BN's batch statistics and ``(y, stats)`` is returned (pass ``stats`` to the BN)."""
+        """``bn``: the BatchNorm2d this conv feeds; ``(y, stats)`` is returned (pass it to the BN).  With
+        ``PDA_BN_EPILOGUE_STATS=1`` the conv epilogue reduces that BN's batch statistics (training, GPU)
+        so the BN skips its statistics pass.  Off by default: at ResNet-50 bs 256 the epilogue
+        reduction + slab column sum cost 1.6 ms/step against the 1.5 ms statistics pass it removes
+        (profiles/r1_resnet50_bs256_v7_epilogue_stats.md) — the K = 64 layer-1 convs are
+        epilogue-bound."""
         if bn is not None:
-            if x.is_cuda and bn.training and self.bias is None and not relu and x.dtype == torch.bfloat16:
+            if (_EPILOGUE_STATS and x.is_cuda and bn.training and self.bias is None and not relu
+                    and x.dtype == torch.bfloat16):
                 y, sums = ops.conv2d_bn_stats(x, self.weight, self.stride, self.padding, self.dilation,
                                               bn.running_mean, grad_join)
                 return y, (sums, bn.running_mean)
