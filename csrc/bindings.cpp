@@ -79,22 +79,23 @@ void sgd_step(Tensor master, c10::optional<Tensor> param_bf16, Tensor grad, Tens
 
 void adam_step(Tensor master, c10::optional<Tensor> param_bf16, Tensor grad, Tensor m, Tensor v, double lr,
                double beta1, double beta2, double eps, double wd, bool adamw, int64_t step, double gscale,
-               c10::optional<Tensor> gscale_t, c10::optional<Tensor> lr_t) {
+               c10::optional<Tensor> gscale_t, c10::optional<Tensor> lr_t, c10::optional<Tensor> step_t) {
   check_f32(master, "master");
   check_f32_or_bf16(grad, "grad");
   check_f32(m, "exp_avg");
+  if (step_t) check_f32(*step_t, "step");
   check_f32(v, "exp_avg_sq");
   TORCH_CHECK(grad.numel() == master.numel() && m.numel() == master.numel() && v.numel() == master.numel());
   if (param_bf16) {
     check_bf16(*param_bf16, "param_bf16");
     TORCH_CHECK(param_bf16->numel() == master.numel());
   }
-  TORCH_CHECK(step >= 1, "adam step must be >= 1");
+  TORCH_CHECK(step >= 1 || step_t, "adam step must be >= 1");
   c10::DeviceGuard g(master.device());
   CHECK_HIP_OK(pda::adam_step(master.data_ptr<float>(), param_bf16 ? bpm(*param_bf16) : nullptr, grad.data_ptr(),
                               is_bf16(grad), m.data_ptr<float>(), v.data_ptr<float>(), master.numel(), (float)lr,
                               (float)beta1, (float)beta2, (float)eps, (float)wd, adamw, step, (float)gscale,
-                              fopt(gscale_t), fopt(lr_t), stream_of(master)));
+                              fopt(gscale_t), fopt(lr_t), fopt(step_t), stream_of(master)));
 }
 
 // returns [norm, clip_coef] on device

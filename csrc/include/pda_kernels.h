@@ -55,7 +55,8 @@ hipError_t sgd_step(float* master, bf16_t* param_bf16, const void* grad, bool gr
                     const float* gscale_ptr, const float* lr_ptr, hipStream_t st);
 hipError_t adam_step(float* master, bf16_t* param_bf16, const void* grad, bool grad_bf16, float* m, float* v,
                      int64_t n, float lr, float beta1, float beta2, float eps, float wd, bool adamw, int64_t step,
-                     float gscale, const float* gscale_ptr, const float* lr_ptr, hipStream_t st);
+                     float gscale, const float* gscale_ptr, const float* lr_ptr, const float* step_ptr,
+                     hipStream_t st);
 int grad_norm_partials();
 hipError_t grad_norm(const void* grad, bool grad_bf16, int64_t n, float pre, float max_norm, float* partial,
                      float* out, hipStream_t st);

@@ -109,17 +109,28 @@ __global__ void __launch_bounds__(kThreads) swiglu_bwd_kernel(const T* __restric
   }
 }
 
-// Column sums of a [rows, cols] matrix (bias gradients): out[c] = sum_r x[r, c] (fp32 out).
+// Column sums of a [rows, cols] matrix with any column count (classifier bias gradients):
+// out[c] = sum_r x[r, c] (fp32).  A block owns 32 columns; its 8 row lanes stride over all rows and
+// are combined through LDS, so the result is deterministic and needs no pre-zeroed output (no memset
+// node when the step is captured into a HIP graph).
+constexpr int kCsCols = 32, kCsLanes = kThreads / kCsCols;
 template <typename T>
 __global__ void __launch_bounds__(kThreads) colsum_kernel(const T* __restrict__ x, float* __restrict__ out, int64_t rows,
-                                                          int64_t cols, int64_t rows_per_block) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
-  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
-  const int64_t r1 = min(rows, r0 + rows_per_block);
+                                                          int64_t cols) {
+  __shared__ float part[kCsLanes][kCsCols];
+  const int cl = threadIdx.x % kCsCols, rl = threadIdx.x / kCsCols;
+  const int64_t c = (int64_t)blockIdx.x * kCsCols + cl;
   float acc = 0.f;
-  for (int64_t r = r0; r < r1; ++r) acc += Elem<T>::load(x, r * cols + c);
-  atomicAdd(out + c, acc);
+  if (c < cols)
+    for (int64_t r = rl; r < rows; r += kCsLanes) acc += Elem<T>::load(x, r * cols + c);
+  part[rl][cl] = acc;
+  __syncthreads();
+  if (rl == 0 && c < cols) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < kCsLanes; ++i) s += part[i][cl];
+    out[c] = s;
+  }
 }
 
 }  // namespace
@@ -155,11 +166,9 @@ hipError_t swiglu_bwd(const void* dy, const void* gu, void* dgu, bool bf16, int6
 }
 
 hipError_t colsum_unaligned(const void* x, bool bf16, float* out, int64_t rows, int64_t cols, hipStream_t st) {
-  PDA_CHECK_HIP(hipMemsetAsync(out, 0, cols * sizeof(float), st));
-  const int64_t rpb = 256;
-  dim3 grid((unsigned)((cols + kThreads - 1) / kThreads), (unsigned)((rows + rpb - 1) / rpb));
-  if (bf16) colsum_kernel<bf16_t><<<grid, kThreads, 0, st>>>((const bf16_t*)x, out, rows, cols, rpb);
-  else colsum_kernel<float><<<grid, kThreads, 0, st>>>((const float*)x, out, rows, cols, rpb);
+  const unsigned grid = (unsigned)((cols + kCsCols - 1) / kCsCols);
+  if (bf16) colsum_kernel<bf16_t><<<grid, kThreads, 0, st>>>((const bf16_t*)x, out, rows, cols);
+  else colsum_kernel<float><<<grid, kThreads, 0, st>>>((const float*)x, out, rows, cols);
   return hipGetLastError();
 }
 

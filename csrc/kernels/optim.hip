@@ -81,9 +81,15 @@ __global__ void __launch_bounds__(kThreads) adam_kernel(float* __restrict__ mast
                                                         float beta2, float eps, float wd, int adamw, float bc1,
                                                         float bc2_sqrt, float gscale,
                                                         const float* __restrict__ gscale_ptr,
-                                                        const float* __restrict__ lr_ptr) {
+                                                        const float* __restrict__ lr_ptr,
+                                                        const float* __restrict__ step_ptr) {
   const float s = read_scale(gscale_ptr, gscale);
   const float lr_ = lr_ptr ? lr_ptr[0] : lr;
+  if (step_ptr) {  // step count on the device: the launch can be replayed from a HIP graph
+    const float t = step_ptr[0];
+    bc1 = 1.f - powf(beta1, t);
+    bc2_sqrt = sqrtf(1.f - powf(beta2, t));
+  }
   const float step_size = lr_ / bc1;
   const int64_t nv = n / 8;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -204,16 +210,17 @@ hipError_t sgd_step(float* master, bf16_t* param_bf16, const void* grad, bool gr
 
 hipError_t adam_step(float* master, bf16_t* param_bf16, const void* grad, bool grad_bf16, float* m, float* v,
                      int64_t n, float lr, float beta1, float beta2, float eps, float wd, bool adamw, int64_t step,
-                     float gscale, const float* gscale_ptr, const float* lr_ptr, hipStream_t st) {
+                     float gscale, const float* gscale_ptr, const float* lr_ptr, const float* step_ptr,
+                     hipStream_t st) {
   const float bc1 = 1.f - powf(beta1, (float)step);
   const float bc2_sqrt = sqrtf(1.f - powf(beta2, (float)step));
   const int g = grid_for((n + 7) / 8);
   if (grad_bf16)
     adam_kernel<bf16_t><<<g, kThreads, 0, st>>>(master, param_bf16, (const bf16_t*)grad, m, v, n, lr, beta1, beta2,
-                                                eps, wd, adamw, bc1, bc2_sqrt, gscale, gscale_ptr, lr_ptr);
+                                                eps, wd, adamw, bc1, bc2_sqrt, gscale, gscale_ptr, lr_ptr, step_ptr);
   else
     adam_kernel<float><<<g, kThreads, 0, st>>>(master, param_bf16, (const float*)grad, m, v, n, lr, beta1, beta2,
-                                               eps, wd, adamw, bc1, bc2_sqrt, gscale, gscale_ptr, lr_ptr);
+                                               eps, wd, adamw, bc1, bc2_sqrt, gscale, gscale_ptr, lr_ptr, step_ptr);
   return hipGetLastError();
 }
 

@@ -7,6 +7,8 @@ Modes:
   the timed call, a new Adam optimizer per call; we add a final device synchronize (the reference
   stops its timer with kernels still queued) so the number is honest.
 * ``clean``  — data generated on device, optimizer reused, HIP-event/synchronize bracketed.
+  ``--graph`` additionally captures the step (forward, loss, backward, Adam) into one HIP graph
+  (`utils/graphs.py`); every replay is a full optimizer step on a fresh device batch.
 Variants: ``single`` (1 device), ``mp`` (layer split, stem..layer2 on dev0, rest on dev1), ``pp``
 (micro-batch pipeline, ``--split-size``), ``sweep`` (pp over the reference's split sizes).
 Precision: bf16 compute with fp32 master weights (the reference ran fp32/TF32 on A100).
@@ -26,6 +28,7 @@ from ..models.resnet import resnet50
 from ..ops import cross_entropy
 from ..optim import Adam
 from ..parallel.model_parallel import ModelParallelResNet50, PipelineParallelResNet50
+from ..utils.graphs import GraphedStep
 
 REFERENCE_S = {"single": 0.248, "mp": 0.272, "pp20": 0.454,
                "sweep": {1: 4.88, 3: 1.84, 5: 1.16, 8: 0.81, 10: 0.71, 12: 0.62, 20: 0.47, 40: 0.33, 60: 0.29}}
@@ -41,11 +44,38 @@ def make_model(kind, devs, split=20):
     return PipelineParallelResNet50(base, devices=devs, split_size=split), devs[1]
 
 
-def run(kind, devs, mode, split=20, repeat=10, batch=120, size=128):
+def run(kind, devs, mode, split=20, repeat=10, batch=120, size=128, graph=False):
     model, out_dev = make_model(kind, devs, split)
     in_dev = devs[0]
     dev_data = DeviceSyntheticImages(batch, size, 1000, device=in_dev, seed=0) if mode == "clean" else None
     opt_holder = {}
+    if graph:
+        if mode != "clean":
+            raise ValueError("--graph needs --mode clean (parity re-creates the optimizer every call)")
+        if kind != "single" and devs[0] != devs[1]:
+            return float("nan"), float("nan")  # a HIP graph is bound to one device (see model_parallel.py)
+        opt = Adam(model.parameters(), lr=1e-3)
+
+        def step(x, y):
+            opt.zero_grad(set_to_none=True)
+            loss = cross_entropy(model(x), y)
+            loss.backward()
+            opt.step()
+            return loss
+
+        model.train()
+        x0, y0 = dev_data.next()
+        graphed = GraphedStep(step, (x0, y0.to(out_dev)), optimizer=opt)
+
+        def train_graph():
+            for _ in range(3):
+                x, yi = dev_data.next()
+                graphed(x, yi.to(out_dev))
+            torch.cuda.synchronize()
+
+        train_graph()
+        times = timeit.repeat(train_graph, number=1, repeat=repeat)
+        return float(np.mean(times)), float(np.std(times))
 
     def train():
         model.train()
@@ -79,13 +109,14 @@ def main(argv=None):
     ap.add_argument("--split-size", type=int, default=20)
     ap.add_argument("--repeat", type=int, default=10)
     ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="capture each step into a HIP graph (clean mode)")
     a = ap.parse_args(argv)
     n = torch.cuda.device_count()
     devs = [int(d) for d in a.devices.split(",")] if a.devices else ([0, 1] if n >= 2 else [0, 0])
     devs = [torch.device("cuda", d) for d in devs]
     results = {}
     for v in a.variants.split(","):
-        m, s = run(v, devs, a.mode, a.split_size, a.repeat)
+        m, s = run(v, devs, a.mode, a.split_size, a.repeat, graph=a.graph)
         key = "pp20" if v == "pp" and a.split_size == 20 else v
         ref = REFERENCE_S.get(key)
         results[v] = {"mean_s": round(m, 4), "std_s": round(s, 4), "img_per_s": round(360 / m, 1),
@@ -93,12 +124,12 @@ def main(argv=None):
     if a.sweep:
         sw = {}
         for sp in SPLITS:
-            m, s = run("pp", devs, a.mode, sp, a.repeat)
+            m, s = run("pp", devs, a.mode, sp, a.repeat, graph=a.graph)
             ref = REFERENCE_S["sweep"][sp]
             sw[sp] = {"mean_s": round(m, 4), "std_s": round(s, 4), "reference_s_A100": ref,
                       "speedup_vs_reference": round(ref / m, 2)}
         results["sweep"] = sw
-    print(json.dumps({"benchmark": "NB03 ResNet-50 train() (3 Adam steps x 120 imgs @128px)", "mode": a.mode,
+    print(json.dumps({"benchmark": "NB03 ResNet-50 train() (3 Adam steps x 120 imgs @128px)", "mode": a.mode, "graph": a.graph,
                       "devices": [str(d) for d in devs], "dtype": "bf16 (fp32 masters)", "results": results}))
 
 

@@ -20,6 +20,36 @@ class _FusedBase(torch.optim.Optimizer):
         self.master_weights = master_weights
         self._flat: Dict[int, dict] = {}  # group index -> flat state
         self.grad_scale: Optional[torch.Tensor] = None  # device scalar multiplied into every gradient
+        # step counters mirrored on the device, so the update kernels read the step (Adam bias
+        # correction) from memory and a captured step can be replayed from a HIP graph
+        self._dstep: Dict[torch.device, list] = {}  # device -> [host value, device tensor]
+
+    def _device_step(self, device: torch.device, host_step: int) -> Optional[torch.Tensor]:
+        """Device counter equal to ``host_step`` after this step's increment (None if they diverge:
+        a parameter that skipped steps keeps the exact host value instead)."""
+        ent = self._dstep.get(device)
+        if ent is None:
+            ent = self._dstep[device] = [host_step - 1, torch.full((1,), float(host_step - 1),
+                                                                  dtype=torch.float32, device=device), -1]
+        if ent[2] != self._step_calls:  # first use of this device in this step() call: advance once
+            ent[2] = self._step_calls
+            ent[0] += 1
+            ent[1].add_(1.0)
+        return ent[1] if ent[0] == host_step else None
+
+    def advance_steps(self, n: int):
+        """Account for ``n`` updates that ran without Python (HIP graph replays): bump host counters."""
+        for st in self._flat.values():
+            st["step"] += n
+        for s in self.state.values():
+            if "step" in s:
+                s["step"] += n
+        for ent in self._dstep.values():
+            ent[0] += n
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        self._dstep.clear()
 
     # --------------------------------------------------------------- flat path
     def _flat_for(self, gi: int, group) -> Optional[dict]:
@@ -57,6 +87,7 @@ class _FusedBase(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        self._step_calls = getattr(self, "_step_calls", 0) + 1
         for gi, group in enumerate(self.param_groups):
             st = self._flat_for(gi, group)
             if st is not None:
@@ -144,7 +175,8 @@ class Adam(_FusedBase):
         b1, b2 = group["betas"]
         gs, gs_t = self._gscale_args()
         C().adam_step(st["master"], st["bf16"], grad, st["exp_avg"], st["exp_avg_sq"], group["lr"], b1, b2,
-                      group["eps"], group["weight_decay"], self._decoupled, st["step"], gs, gs_t, None)
+                      group["eps"], group["weight_decay"], self._decoupled, st["step"], gs, gs_t, None,
+                      self._device_step(grad.device, st["step"]))
 
     def _param_update(self, p, group):
         s = self.state[p]
@@ -164,7 +196,7 @@ class Adam(_FusedBase):
                     s[n] = torch.zeros_like(master)
             gs, gs_t = self._gscale_args()
             C().adam_step(master, pb, p.grad.contiguous(), s["exp_avg"], s["exp_avg_sq"], lr, b1, b2, eps, wd,
-                          self._decoupled, t, gs, gs_t, None)
+                          self._decoupled, t, gs, gs_t, None, self._device_step(p.device, t))
             return
         g = p.grad.float()
         if self.grad_scale is not None:

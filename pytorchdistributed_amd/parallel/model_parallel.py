@@ -77,17 +77,26 @@ class PipelineParallelResNet50(ModelParallelResNet50):
         self.split_size = split_size
         self._streams = {}
 
-    def _stream(self, dev):
+    def _stream(self, stage, dev):
+        """One stream per stage (also when both stages share a device, so their micro-batches overlap)."""
         if dev.type != "cuda":
             return None
-        if dev not in self._streams:
-            self._streams[dev] = torch.cuda.Stream(dev)
-        return self._streams[dev]
+        if stage not in self._streams:
+            self._streams[stage] = torch.cuda.Stream(dev)
+        return self._streams[stage]
 
     def forward(self, x):
         splits = x.split(self.split_size, dim=0)
-        s0, s1 = self._stream(self.dev0), self._stream(self.dev1)
-        if s0 is None or s1 is None:  # CPU devices: sequential reference semantics
+        s0, s1 = self._stream(0, self.dev0), self._stream(1, self.dev1)
+        capturing = s0 is not None and torch.cuda.is_current_stream_capturing()
+        if capturing and self.dev0 != self.dev1:
+            raise RuntimeError("HIP-graph capture of a two-device pipeline is not supported (a graph is bound "
+                               "to one device); capture each stage on its own device instead")
+        if s0 is None or s1 is None or capturing:
+            # CPU devices: sequential reference semantics.  Under HIP-graph capture the micro-batches are
+            # issued on the capturing stream only: backward through side-stream forwards breaks
+            # hipStreamEndCapture on this ROCm stack (tools/graph_stream_repro.py, mode C), and the
+            # replayed graph has no launch gaps to hide anyway.
             outs = [self.head(self.seq2(self.seq1(s.to(self.dev0)).to(self.dev1))) for s in splits]
             return torch.cat(outs)
         # stage-0 work of micro-batch i overlaps stage-1 work of micro-batch i-1: the two devices
@@ -106,8 +115,11 @@ class PipelineParallelResNet50(ModelParallelResNet50):
         with torch.cuda.stream(s1):
             for a, ev in handoff:
                 s1.wait_event(ev)
+                a.record_stream(s1)  # produced on s0, read on s1: keep the allocator from recycling it early
                 a1 = a.to(self.dev1, non_blocking=True)
-                outs.append(self.head(self.seq2(a1)))
+                o = self.head(self.seq2(a1))
+                o.record_stream(cur1)
+                outs.append(o)
         cur0.wait_stream(s0)
         cur1.wait_stream(s1)
         return torch.cat(outs)

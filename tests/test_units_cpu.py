@@ -245,3 +245,23 @@ def test_grad_join_sums_consumers_without_autograd_add():
         sum(Scale.apply(x, k, j) for k in ks).sum().backward()
         assert torch.allclose(x.grad, torch.full((5,), sum(ks)))
         assert j.pending is None and j.arrived == 0
+
+
+def test_optimizer_device_step_counter_bookkeeping():
+    """`_device_step` advances once per step() call, tracks the host counter, refuses a parameter
+    whose host step diverged, and `advance_steps` accounts for graph replays."""
+    from pytorchdistributed_amd.optim import Adam
+
+    p = torch.nn.Parameter(torch.zeros(4))
+    opt = Adam([p])
+    dev = torch.device("cpu")
+    opt._step_calls = 1
+    t = opt._device_step(dev, 1)
+    assert t is not None and t.item() == 1.0
+    assert opt._device_step(dev, 1) is t and t.item() == 1.0  # same step() call: no second increment
+    assert opt._device_step(dev, 3) is None                    # diverged host step: host path
+    opt._step_calls = 2
+    assert opt._device_step(dev, 2).item() == 2.0
+    opt.state[p]["step"] = 2
+    opt.advance_steps(5)
+    assert opt.state[p]["step"] == 7 and opt._dstep[dev][0] == 7
