@@ -173,7 +173,8 @@ void bn_param_ptrs(const c10::optional<Tensor>& t, const float** f, const pda::b
 
 std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma,
                                  c10::optional<Tensor> beta, c10::optional<Tensor> running_mean,
-                                 c10::optional<Tensor> running_var, double momentum, double eps, bool relu) {
+                                 c10::optional<Tensor> running_var, double momentum, double eps, bool relu,
+                                 bool relu_bits) {
   check_bf16(x, "x");
   const int64_t C = x.size(-1), M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "channels must be a multiple of 8 and <= 2048");
@@ -194,18 +195,20 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optio
   auto fo = x.options().dtype(at::kFloat);
   Tensor mean = at::empty({C}, fo), invstd = at::empty({C}, fo), ss = at::empty({2, C}, fo);
   Tensor ws = at::empty({pda::bn_workspace_floats(M, C)}, fo);
+  Tensor bits = (relu && relu_bits) ? at::empty({M * C / 8}, x.options().dtype(at::kByte)) : Tensor();
   CHECK_HIP_OK(pda::bn_fwd_train(bp(x), res ? bp(*res) : nullptr, bpm(y), M, C, gf, gb, bfp, bb,
                                  running_mean ? running_mean->data_ptr<float>() : nullptr,
                                  running_var ? running_var->data_ptr<float>() : nullptr, (float)momentum, (float)eps,
                                  relu, mean.data_ptr<float>(), invstd.data_ptr<float>(), ss.data_ptr<float>(),
-                                 ws.data_ptr<float>(), stream_of(x)));
-  return {y, mean, invstd, ss};
+                                 ws.data_ptr<float>(), bits.defined() ? bits.data_ptr<uint8_t>() : nullptr,
+                                 stream_of(x)));
+  return {y, mean, invstd, ss, bits};
 }
 
 std::vector<Tensor> bn_fwd_train_sums(Tensor x, Tensor sums, Tensor shift, c10::optional<Tensor> res,
                                       c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
                                       c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
-                                      double momentum, double eps, bool relu) {
+                                      double momentum, double eps, bool relu, bool relu_bits) {
   check_bf16(x, "x");
   check_f32(sums, "sums");
   check_f32(shift, "shift");
@@ -223,13 +226,15 @@ std::vector<Tensor> bn_fwd_train_sums(Tensor x, Tensor sums, Tensor shift, c10::
   Tensor y = at::empty_like(x);
   auto fo = x.options().dtype(at::kFloat);
   Tensor mean = at::empty({C}, fo), invstd = at::empty({C}, fo), ss = at::empty({2, C}, fo);
+  Tensor bits = (relu && relu_bits) ? at::empty({M * C / 8}, x.options().dtype(at::kByte)) : Tensor();
   CHECK_HIP_OK(pda::bn_fwd_train_sums(bp(x), res ? bp(*res) : nullptr, bpm(y), M, C, sums.data_ptr<float>(),
                                       shift.data_ptr<float>(), gf, gb, bfp, bb,
                                       running_mean ? running_mean->data_ptr<float>() : nullptr,
                                       running_var ? running_var->data_ptr<float>() : nullptr, (float)momentum,
                                       (float)eps, relu, mean.data_ptr<float>(), invstd.data_ptr<float>(),
-                                      ss.data_ptr<float>(), stream_of(x)));
-  return {y, mean, invstd, ss};
+                                      ss.data_ptr<float>(), bits.defined() ? bits.data_ptr<uint8_t>() : nullptr,
+                                      stream_of(x)));
+  return {y, mean, invstd, ss, bits};
 }
 
 Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
@@ -261,9 +266,13 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::op
   TORCH_CHECK(dy.sizes() == x.sizes());
   const int64_t C = x.size(-1), M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "channels must be a multiple of 8 and <= 2048");
+  const bool bits = relu && y.has_value() && y->scalar_type() == at::kByte;
   if (relu) {
-    TORCH_CHECK(y.has_value() || ss.has_value(), "relu backward needs the saved output or scale/shift");
-    if (y.has_value()) check_bf16(*y, "y");
+    TORCH_CHECK(y.has_value() || ss.has_value(), "relu backward needs the saved output, its bit mask or scale/shift");
+    if (bits) {
+      check_gpu(*y, "relu_bits");
+      TORCH_CHECK(y->is_contiguous() && y->numel() * 8 == x.numel(), "relu bit mask must hold numel/8 bytes");
+    } else if (y.has_value()) check_bf16(*y, "y");
     else {
       check_f32(*ss, "ss");
       TORCH_CHECK(ss->numel() == 2 * C);
@@ -287,7 +296,8 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::op
   const bool pb = pdt == at::kBFloat16;
   Tensor ws = at::empty({pda::bn_workspace_floats(M, C)}, x.options().dtype(at::kFloat));
   const float* ssp = (relu && !y.has_value()) ? ss->data_ptr<float>() : nullptr;
-  CHECK_HIP_OK(pda::bn_bwd(bp(dy), bp(x), (relu && y.has_value()) ? bp(*y) : nullptr, ssp, M, C, mean.data_ptr<float>(),
+  CHECK_HIP_OK(pda::bn_bwd(bp(dy), bp(x), (relu && y.has_value() && !bits) ? bp(*y) : nullptr,
+                           bits ? y->data_ptr<uint8_t>() : nullptr, ssp, M, C, mean.data_ptr<float>(),
                            invstd.data_ptr<float>(), gf, gb, relu, bpm(dx), want_dres ? bpm(dres) : nullptr,
                            pb ? nullptr : dgamma.data_ptr<float>(), pb ? bpm(dgamma) : nullptr,
                            pb ? nullptr : dbeta.data_ptr<float>(), pb ? bpm(dbeta) : nullptr, ws.data_ptr<float>(),
@@ -841,6 +851,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("fill_random", &fill_random);
   m.def("fill_randint", &fill_randint);
   m.def("gemm", &gemm);
+  m.def("set_gemm_paths", &pda::set_gemm_paths, "force a GEMM kernel path: wide=-1 env default, 0 off, 1 auto, 2 force");
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_fwd_stats", &conv_fwd_stats);
   m.def("bn_fwd_train_sums", &bn_fwd_train_sums);

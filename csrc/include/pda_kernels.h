@@ -78,19 +78,22 @@ int64_t bn_workspace_floats(int64_t M, int64_t C);
 hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
                         const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, float* running_mean,
                         float* running_var, float momentum, float eps, bool relu, float* save_mean,
-                        float* save_invstd, float* save_ss, float* ws, hipStream_t st);
+                        float* save_invstd, float* save_ss, float* ws, uint8_t* relu_bits, hipStream_t st);
+// relu_bits (optional, with relu): [M*C/8] bytes, bit j of byte v = ReLU mask of element 8v+j
 // training forward from precomputed sums (e.g. a conv epilogue): sums[0:C] = sum(x - K), sums[C:2C] =
 // sum((x - K)^2) over the M rows, K = shift; finalize + apply only (no statistics pass over x)
 hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* sums,
                              const float* shift, const float* gamma_f, const bf16_t* gamma_b, const float* beta_f,
                              const bf16_t* beta_b, float* running_mean, float* running_var, float momentum, float eps,
-                             bool relu, float* save_mean, float* save_invstd, float* save_ss, hipStream_t st);
+                             bool relu, float* save_mean, float* save_invstd, float* save_ss, uint8_t* relu_bits,
+                             hipStream_t st);
 hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
                        const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, const float* running_mean,
                        const float* running_var, float eps, bool relu, float* ws, hipStream_t st);
-// relu: the mask comes from y when given, else from x * ss[0:C] + ss[C:2C] (scale/shift saved by
-// bn_fwd_train; BN+ReLU without residual never materialises y for the backward)
-hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* ss, int64_t M, int64_t C,
+// relu: the mask comes from relu_bits when given, else from y, else from x * ss[0:C] + ss[C:2C]
+// (scale/shift saved by bn_fwd_train; BN+ReLU without residual never materialises y for the backward)
+hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint8_t* relu_bits, const float* ss,
+                  int64_t M, int64_t C,
                   const float* save_mean, const float* save_invstd, const float* gamma_f, const bf16_t* gamma_b,
                   bool relu, bf16_t* dx, bf16_t* dres, float* dgamma_f, bf16_t* dgamma_b, float* dbeta_f,
                   bf16_t* dbeta_b, float* ws, hipStream_t st);
@@ -110,6 +113,8 @@ hipError_t fill_randint(int64_t* out, int64_t n, uint64_t seed, uint64_t offset,
                         hipStream_t st);
 
 // ---- gemm_conv.hip
+// path override for the GEMM family: wide = -1 env default (PDA_GEMM_WIDE), 0 off, 1 heuristic, 2 force
+void set_gemm_paths(int wide);
 int64_t gemm_slab_floats(int64_t M, int64_t N, int64_t K, bool allow_split);
 hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
                      void* C, bool c_f32, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,

@@ -209,7 +209,8 @@ template <bool RES, bool RELU>
 __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                             bf16_t* __restrict__ y, int64_t M, int C,
                                                             const float* __restrict__ scale,
-                                                            const float* __restrict__ shift) {
+                                                            const float* __restrict__ shift,
+                                                            uint8_t* __restrict__ bits) {
   __shared__ __attribute__((aligned(16))) float s_scale[kMaxC];
   __shared__ __attribute__((aligned(16))) float s_shift[kMaxC];
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -238,8 +239,13 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16_t* __rest
       for (int j = 0; j < 8; ++j) a[j] += r[j];
     }
     if (RELU) {
+      uint32_t m = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] = fmaxf(a[j], 0.f);
+      for (int j = 0; j < 8; ++j) {
+        m |= (a[j] > 0.f ? 1u : 0u) << j;
+        a[j] = fmaxf(a[j], 0.f);
+      }
+      if (bits) bits[v] = (uint8_t)m;  // one byte per 8 channels: the backward's ReLU mask
     }
     store8(y + v * 8, a);
   }
@@ -247,12 +253,18 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16_t* __rest
 
 // ---------------------------------------------------------------- backward reduction
 // MASK: 0 no ReLU; 1 ReLU mask from the saved output y; 2 ReLU mask recomputed from x and the
-// forward's per-channel scale/shift (BN+ReLU without residual: y is never saved or re-read).
+// forward's per-channel scale/shift (BN+ReLU without residual: y is never saved or re-read);
+// 3 ReLU mask from the bit mask written by the forward apply (BN+residual+ReLU: 1 bit instead of
+// re-reading the 16-bit output, in both backward passes).
 template <int MASK>
 __device__ __forceinline__ void relu_mask(float (&g)[8], const bf16_t* __restrict__ y, const float (&xv)[8],
                                           const float* __restrict__ sc, const float* __restrict__ sh, int64_t off,
                                           int c0) {
-  if constexpr (MASK == 1) {
+  if constexpr (MASK == 3) {
+    const uint32_t m = reinterpret_cast<const uint8_t*>(y)[off >> 3];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = (m >> j) & 1u ? g[j] : 0.f;
+  } else if constexpr (MASK == 1) {
     const u16x8 yr = *reinterpret_cast<const u16x8*>(y + off);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] = bf2f(yr[j]) > 0.f ? g[j] : 0.f;
@@ -284,15 +296,22 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* _
     int64_t r = r0 + ty;
     for (; r + 3 * rpi < r1; r += 4 * rpi) {  // 4 rows x 2 tensors = 8 loads in flight per lane
       float g[4][8], xv[4][8];
+      uint32_t mb[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t off = (r + u * rpi) * C + c0;
         load8(dy + off, g[u]);
         load8(x + off, xv[u]);
+        if constexpr (MASK == 3) mb[u] = reinterpret_cast<const uint8_t*>(y)[off >> 3];  // in flight with dy/x
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        relu_mask<MASK>(g[u], y, xv[u], ss, ss + C, (r + u * rpi) * C + c0, c0);
+        if constexpr (MASK == 3) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[u][j] = (mb[u] >> j) & 1u ? g[u][j] : 0.f;
+        } else {
+          relu_mask<MASK>(g[u], y, xv[u], ss, ss + C, (r + u * rpi) * C + c0, c0);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           sa[j] += g[u][j];
@@ -373,12 +392,12 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16_t* __
 }
 
 hipError_t launch_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int C, const float* scale,
-                        const float* shift, bool relu, hipStream_t st) {
+                        const float* shift, bool relu, uint8_t* bits, hipStream_t st) {
   const int grid = ew_grid(M * C / 8);
-  if (res && relu) bn_apply_kernel<true, true><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift);
-  else if (res) bn_apply_kernel<true, false><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift);
-  else if (relu) bn_apply_kernel<false, true><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift);
-  else bn_apply_kernel<false, false><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift);
+  if (res && relu) bn_apply_kernel<true, true><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits);
+  else if (res) bn_apply_kernel<true, false><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr);
+  else if (relu) bn_apply_kernel<false, true><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits);
+  else bn_apply_kernel<false, false><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr);
   return hipGetLastError();
 }
 
@@ -393,7 +412,7 @@ int64_t bn_workspace_floats(int64_t M, int64_t C) {
 hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
                         const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, float* running_mean,
                         float* running_var, float momentum, float eps, bool relu, float* save_mean,
-                        float* save_invstd, float* save_ss, float* ws, hipStream_t st) {
+                        float* save_invstd, float* save_ss, float* ws, uint8_t* relu_bits, hipStream_t st) {
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C);
   float* scale = save_ss ? save_ss : ws + 2 * (int64_t)g.nrb * C;
@@ -404,13 +423,14 @@ hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M
       x, nullptr, ws, g.nrb, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum, eps, save_mean,
       save_invstd, scale, shift);
   PDA_CHECK_HIP(hipGetLastError());
-  return launch_apply(x, res, y, M, (int)C, scale, shift, relu, st);
+  return launch_apply(x, res, y, M, (int)C, scale, shift, relu, relu_bits, st);
 }
 
 hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* sums,
                              const float* shift, const float* gamma_f, const bf16_t* gamma_b, const float* beta_f,
                              const bf16_t* beta_b, float* running_mean, float* running_var, float momentum, float eps,
-                             bool relu, float* save_mean, float* save_invstd, float* save_ss, hipStream_t st) {
+                             bool relu, float* save_mean, float* save_invstd, float* save_ss, uint8_t* relu_bits,
+                             hipStream_t st) {
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
   float* scale = save_ss;
   float* shift_out = save_ss + C;
@@ -418,7 +438,7 @@ hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int6
       x, shift, sums, 1, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum, eps,
       save_mean, save_invstd, scale, shift_out);
   PDA_CHECK_HIP(hipGetLastError());
-  return launch_apply(x, res, y, M, (int)C, scale, shift_out, relu, st);
+  return launch_apply(x, res, y, M, (int)C, scale, shift_out, relu, relu_bits, st);
 }
 
 hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
@@ -431,25 +451,29 @@ hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M,
       x, nullptr, nullptr, 0, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, const_cast<float*>(running_mean),
       const_cast<float*>(running_var), 0.f, eps, nullptr, nullptr, scale, shift);
   PDA_CHECK_HIP(hipGetLastError());
-  return launch_apply(x, res, y, M, (int)C, scale, shift, relu, st);
+  return launch_apply(x, res, y, M, (int)C, scale, shift, relu, nullptr, st);
 }
 
-hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* ss, int64_t M, int64_t C,
+hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint8_t* relu_bits, const float* ss,
+                  int64_t M, int64_t C,
                   const float* save_mean, const float* save_invstd, const float* gamma_f, const bf16_t* gamma_b,
                   bool relu, bf16_t* dx, bf16_t* dres, float* dgamma_f, bf16_t* dgamma_b, float* dbeta_f,
                   bf16_t* dbeta_b, float* ws, hipStream_t st) {
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
-  if (relu && !y && !ss) return hipErrorInvalidValue;
+  if (relu && !y && !ss && !relu_bits) return hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C);
   float* coef = ws + 2 * (int64_t)g.nrb * C;
-  const int mask = !relu ? 0 : (y ? 1 : 2);
+  const int mask = !relu ? 0 : (relu_bits ? 3 : (y ? 1 : 2));
+  if (mask == 3) y = reinterpret_cast<const bf16_t*>(relu_bits);  // the mask kernels index it as bytes
   const dim3 rg(g.nrb, g.gy);
   if (mask == 0)
     bn_bwd_reduce_kernel<0><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
   else if (mask == 1)
     bn_bwd_reduce_kernel<1><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
-  else
+  else if (mask == 2)
     bn_bwd_reduce_kernel<2><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
+  else
+    bn_bwd_reduce_kernel<3><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
   PDA_CHECK_HIP(hipGetLastError());
   bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(ws, g.nrb, M, (int)C, save_mean,
                                                                          save_invstd, gamma_f, gamma_b, dgamma_f,
@@ -460,7 +484,8 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const floa
   bn_bwd_apply_kernel<MK, DR><<<grid, kThreads, 0, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres)
   if (mask == 0) { if (dres) BWD_APPLY(0, true); else BWD_APPLY(0, false); }
   else if (mask == 1) { if (dres) BWD_APPLY(1, true); else BWD_APPLY(1, false); }
-  else { if (dres) BWD_APPLY(2, true); else BWD_APPLY(2, false); }
+  else if (mask == 2) { if (dres) BWD_APPLY(2, true); else BWD_APPLY(2, false); }
+  else { if (dres) BWD_APPLY(3, true); else BWD_APPLY(3, false); }
 #undef BWD_APPLY
   return hipGetLastError();
 }

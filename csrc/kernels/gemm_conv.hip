@@ -25,6 +25,8 @@
 #include "pda_common.h"
 #include "pda_kernels.h"
 
+#include <cmath>
+
 #include <cstdlib>
 
 namespace pda {
@@ -764,6 +766,168 @@ __global__ void __launch_bounds__(BIG_NT, 1) gemm_big_kernel(LA la, LB lb, int64
   }
 }
 
+// ------------------------------------------------------------------ wide-tile kernel (K-major x K-major)
+// 256 x 256 output tile, 8 waves (2 along M x 4 along N), 128 x 64 per wave (acc[8][4]).  Why: the
+// 128-tile kernel needs ~62 B/clk/CU of operand fetch at full MFMA rate (64 KB per 1024 SIMD-cycles
+// with 2 workgroups per CU) — about the L2's per-CU share — so it stalls at ~0.9 PF/s on large
+// shapes; a 256^2 tile halves the bytes per FLOP and a 128x64 wave tile halves the LDS reads per MFMA.
+// Per 64-deep K step a wave runs 8 phases of 8 MFMAs (quadrant x k-half) and reads the fragments of
+// the NEXT phase while the current one multiplies; quadrants are ordered so one operand is reused:
+//   k 0..31 : (A0,B0) (A0,B1) (A1,B1) (A1,B0)    k 32..63 : (A1,B1) (A1,B0) (A0,B0) (A0,B1)
+// which needs only two A and two B fragment sets (fa0/fa1, fb0/fb1; 24 ds_read_b128 per step, the
+// minimum).  The next K step's operands are DMA'd (global_load_lds) into the other of two 64 KB LDS
+// stages during phases 0-1 and retired by one vmcnt(0) + barrier after phase 6; phase 7's MFMAs run
+// behind the first fragment reads of the next step.  Each 256-thread half of the workgroup stages one
+// 64-row group of every 128-row operand half with the ordinary 64-row loaders (NCH = 2), so the LDS
+// images and fragment reads are those of the 128-tile kernel.
+constexpr int W_NT = 512;
+constexpr int W_HALF = 128 * BK * 2;  // one 128-row half of an operand tile (16 KB)
+constexpr int W_STAGE = 4 * W_HALF;   // A0 A1 B0 B1
+constexpr int W_SROW = 256 + 8;       // epilogue staging row (bf16 elements)
+constexpr int W_LDS = 2 * W_STAGE > 256 * W_SROW * 2 ? 2 * W_STAGE : 256 * W_SROW * 2;
+
+template <int QA, int QB>
+__device__ __forceinline__ void wide_mma(f32x4 (&acc)[8][4], const mfma_bf16x8 (&fa)[4], const mfma_bf16x8 (&fb)[2]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      acc[4 * QA + i][2 * QB + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[4 * QA + i][2 * QB + j],
+                                                                            0, 0, 0);
+}
+
+template <class LA, class LB>
+__global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K,
+                                                           int tiles_n, Epi epi) {
+  static_assert(LA::kMajor && LB::kMajor && LA::NCH == 2 && LB::NCH == 2, "K-major 64-row loaders");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = tid >> 8, gtid = tid & 255, gwid = wid & 3;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int ntiles = gridDim.x;
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int tn = tile % tiles_n, tm = tile / tiles_n;
+  const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
+  const int nk = (int)((K + BK - 1) / BK);
+
+  typename LA::State sa0, sa1;
+  typename LB::State sb0, sb1;
+  la.init(sa0, m0 + 64 * grp, gtid);
+  la.init(sa1, m0 + 128 + 64 * grp, gtid);
+  lb.init(sb0, n0 + 64 * grp, gtid);
+  lb.init(sb1, n0 + 128 + 64 * grp, gtid);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue_a = [&](int t) {
+    char* b = smem + (t & 1) * W_STAGE + grp * (W_HALF / 2);
+    glds_tile(la, sa0, (int64_t)t * BK, b, gwid);
+    glds_tile(la, sa1, (int64_t)t * BK, b + W_HALF, gwid);
+  };
+  auto issue_b = [&](int t) {
+    char* b = smem + (t & 1) * W_STAGE + 2 * W_HALF + grp * (W_HALF / 2);
+    glds_tile(lb, sb0, (int64_t)t * BK, b, gwid);
+    glds_tile(lb, sb1, (int64_t)t * BK, b + W_HALF, gwid);
+  };
+  // fragments: A rows of this wave's half (wr), B rows (= output columns) of its 64-column slice
+  const int a_off = wr * W_HALF, b_off = 2 * W_HALF + (wc >> 1) * W_HALF, b_row = (wc & 1) * 64;
+  auto rd_a = [&](const char* st, int qa, int kk, mfma_bf16x8 (&f)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = read_frag<true, 128>(st + a_off, 64 * qa + 16 * i, kk, lane);
+  };
+  auto rd_b = [&](const char* st, int qb, int kk, mfma_bf16x8 (&f)[2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) f[j] = read_frag<true, 128>(st + b_off, b_row + 32 * qb + 16 * j, kk, lane);
+  };
+
+  mfma_bf16x8 fa0[4], fa1[4], fb0[2], fb1[2];
+  if (nk > 0) {
+    issue_a(0);
+    issue_b(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    rd_a(smem, 0, 0, fa0);
+    rd_b(smem, 0, 0, fb0);
+  }
+  for (int t = 0; t < nk; ++t) {
+    const char* cs = smem + (t & 1) * W_STAGE;
+    const bool more = t + 1 < nk;
+    // k 0..31
+    if (more) issue_a(t + 1);
+    rd_b(cs, 1, 0, fb1);
+    wide_mma<0, 0>(acc, fa0, fb0);
+    if (more) issue_b(t + 1);
+    rd_a(cs, 1, 0, fa1);
+    wide_mma<0, 1>(acc, fa0, fb1);
+    wide_mma<1, 1>(acc, fa1, fb1);
+    rd_a(cs, 1, 32, fa0);
+    rd_b(cs, 1, 32, fb1);
+    wide_mma<1, 0>(acc, fa1, fb0);
+    // k 32..63
+    rd_b(cs, 0, 32, fb0);
+    wide_mma<1, 1>(acc, fa0, fb1);
+    rd_a(cs, 0, 32, fa1);
+    wide_mma<1, 0>(acc, fa0, fb0);
+    wide_mma<0, 0>(acc, fa1, fb0);
+    if (more) {
+      // next step's operands landed (own DMAs, then everyone's); this stage is no longer read
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const char* ns = smem + ((t + 1) & 1) * W_STAGE;
+      rd_a(ns, 0, 0, fa0);
+      rd_b(ns, 0, 0, fb0);
+    }
+    wide_mma<0, 1>(acc, fa1, fb1);
+  }
+  __syncthreads();  // every wave is done with the operand stages before they become the staging tile
+
+  // epilogue (bf16 output): bias / relu in registers, stage through LDS, coalesced 16-B row stores
+  bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = wr * 128 + 16 * i + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int cc = wc * 64 + 16 * j + 4 * (lane >> 4);
+      f32x4 v = acc[i][j];
+      if (epi.bias) {
+        const int64_t n = n0 + cc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (n + q < N)
+            v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
+      }
+      if (epi.relu) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+      }
+      u16x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
+      *reinterpret_cast<u16x4*>(stg + r * W_SROW + cc) = o;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = 256 / 8;
+  for (int c = tid; c < 256 * CPR; c += W_NT) {
+    const int r = c / CPR, ch = c % CPR;
+    const int64_t m = m0 + r, n = n0 + ch * 8;
+    if (m >= M || n >= N) continue;
+    const int64_t crow = epi_row(epi, m);
+    u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * W_SROW + ch * 8);
+    if (epi.addend) {
+      const u16x8 a = *reinterpret_cast<const u16x8*>(epi.addend + crow * epi.ldc + n);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + bf2f(a[q]));
+    }
+    *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
+  }
+}
+
 // Split-K reduction: out[m, n] = act(sum_s slab[s, m, n] + bias[n]).  A workgroup is (256 / L) output
 // float4s x L split lanes; each lane keeps 8 slab loads in flight and the L partials meet in LDS, so
 // a small output with a deep split (conv wgrad of 64 x 64 with ~1000 slabs) still spreads over
@@ -961,9 +1125,56 @@ hipError_t launch_big(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t 
   return hipGetLastError();
 }
 
+// 256 x 256 wide-tile kernel: bf16 output, no split-K / statistics, N >= 256.  PDA_GEMM_WIDE=0
+// disables it, =1 forces it wherever legal; by default it is chosen when its tile count keeps the
+// chip's 256 CUs about as busy as the 128-tile kernel's (see wide_pays).
+int g_wide_override = -1;  // set_gemm_paths(): tests / benchmarks force a path at run time
+
+int wide_mode() {
+  static const int mode = [] {
+    const char* e = getenv("PDA_GEMM_WIDE");
+    return e ? (e[0] == '0' ? 0 : 2) : 1;
+  }();
+  return g_wide_override >= 0 ? g_wide_override : mode;
+}
+
+bool wide_pays(int64_t M, int64_t N) {
+  // A wide tile does 4x a 128-tile's work ~1.35x more efficiently per CU (measured on the ResNet-50
+  // conv shapes and 4096^3, profiles/r1_conv_gemm_microbench_v7_wide.jsonl); compare the two
+  // configurations' wave-quantised times over 256 CUs (1 wide / 2 narrow workgroups per CU).
+  const double wt = (double)((M + 255) / 256) * ((N + 255) / 256);
+  const double nt = (double)((M + 127) / 128) * ((N + 127) / 128);
+  const double w_time = std::ceil(wt / 256.0) * 4.0 / 1.35, n_time = std::ceil(nt / 512.0) * 2.0;
+  return w_time < n_time;
+}
+
+bool use_wide(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) {
+  const int mode = wide_mode();
+  if (mode == 0 || p.splits > 1 || epi.c_f32 || epi.slab || epi.stats || N < 256 || K < 64) return false;
+  if (mode == 2) return true;
+  return wide_pays(M, N);
+}
+
+template <class LA, class LB>
+hipError_t launch_wide(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st) {
+  static bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_wide_kernel<LA, LB>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, W_LDS);
+    return true;
+  }();
+  (void)attr;
+  const int tiles_n = (int)((N + 255) / 256);
+  const int ntiles = (int)((M + 255) / 256) * tiles_n;
+  gemm_wide_kernel<LA, LB><<<ntiles, W_NT, W_LDS, st>>>(la, lb, M, N, K, tiles_n, epi);
+  return hipGetLastError();
+}
+
 template <template <int> class TA, template <int> class TB, class MakeA, class MakeB>
 hipError_t dispatch_bn(int64_t M, int64_t N, int64_t K, const Plan& p, Epi epi, float* slab, hipStream_t st,
                        MakeA make_a, MakeB make_b) {
+  if constexpr (TA<64>::kMajor && TB<64>::kMajor) {
+    if (use_wide(M, N, K, p, epi)) return launch_wide(make_a(TA<64>{}), make_b(TB<64>{}), M, N, K, epi, st);
+  }
   if constexpr (TA<128>::kMajor && TB<64>::kMajor) {
     if (use_big(M, N, K, p, epi)) return launch_big(make_a(TA<128>{}), make_b(TB<64>{}), M, N, K, epi, st);
   }
@@ -990,6 +1201,8 @@ ConvGeom make_geom(int H, int W, int C, int P, int Q, int R, int S, int st, int 
 bool dgrad_phased(int stride, int dil) { return stride == 1 || dil == 1; }
 
 }  // namespace
+
+void set_gemm_paths(int wide) { g_wide_override = wide; }
 
 int64_t gemm_slab_floats(int64_t M, int64_t N, int64_t K, bool allow_split) {
   Plan p = plan_gemm(M, N, K, allow_split, 512);

@@ -20,21 +20,24 @@ class _BatchNormFn(torch.autograd.Function):
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()
-        ss = None
+        ss = bits = None
+        # BN+residual+ReLU: the forward also writes the ReLU mask as bits (1/16 of y), read by both
+        # backward passes instead of the 16-bit output
+        want_bits = relu and residual is not None
         if training and sums is not None:  # statistics already reduced by the producing conv's epilogue
-            y, mean, invstd, ss = C().bn_fwd_train_sums(x, sums, shift, residual, gamma, beta, running_mean,
-                                                        running_var, momentum, eps, relu)
+            y, mean, invstd, ss, bits = C().bn_fwd_train_sums(x, sums, shift, residual, gamma, beta, running_mean,
+                                                              running_var, momentum, eps, relu, want_bits)
         elif training:
-            y, mean, invstd, ss = C().bn_fwd_train(x, residual, gamma, beta, running_mean, running_var, momentum,
-                                                   eps, relu)
+            y, mean, invstd, ss, bits = C().bn_fwd_train(x, residual, gamma, beta, running_mean, running_var,
+                                                         momentum, eps, relu, want_bits)
         else:
             y = C().bn_fwd_eval(x, residual, gamma, beta, running_mean, running_var, eps, relu)
             mean = running_mean
             invstd = torch.rsqrt(running_var + eps)
         # BN+ReLU without a residual: the backward recomputes the ReLU mask from x and the saved
         # per-channel scale/shift, so y is neither kept alive nor re-read (one fewer HBM pass)
-        keep_y = relu and residual is not None
-        ctx.save_for_backward(x, y if keep_y else None, ss if (relu and not keep_y) else None, mean, invstd, gamma)
+        ctx.save_for_backward(x, bits if want_bits else None, ss if (relu and not want_bits) else None, mean, invstd,
+                              gamma)
         ctx.cfg = (relu, residual is not None, training)
         ctx.beta = beta
         ctx.join = join
@@ -42,7 +45,7 @@ class _BatchNormFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, ss, mean, invstd, gamma = ctx.saved_tensors
+        x, bits, ss, mean, invstd, gamma = ctx.saved_tensors
         relu, has_res, training = ctx.cfg
         if not training:
             raise NotImplementedError("backward through eval-mode BatchNorm is not supported")
@@ -50,7 +53,8 @@ class _BatchNormFn(torch.autograd.Function):
         tb = grad_target(ctx.beta) if ctx.beta is not None and ctx.needs_input_grad[2] else None
         if (tg is None) != (tb is None):
             tg = tb = None
-        dx, dres, dgamma, dbeta = C().bn_bwd(dy.contiguous(), x, y, ss, mean, invstd, gamma, relu, has_res, tg, tb)
+        dx, dres, dgamma, dbeta = C().bn_bwd(dy.contiguous(), x, bits, ss, mean, invstd, gamma, relu, has_res, tg,
+                                             tb)
         dg = dgamma if gamma is not None and ctx.needs_input_grad[1] else None
         db = dbeta if ctx.needs_input_grad[2] else None
         if has_res and ctx.join is not None:

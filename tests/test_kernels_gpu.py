@@ -68,6 +68,42 @@ def test_gemm_big_tile_path():
     assert rel_err(out.cpu(), ref) < 1e-2
 
 
+@pytest.fixture
+def force_wide():
+    C().set_gemm_paths(2)
+    yield
+    C().set_gemm_paths(-1)
+
+
+@pytest.mark.parametrize("M,N,K", [(700, 520, 200), (256, 256, 64), (1100, 296, 2056), (4096, 4096, 512)])
+def test_gemm_wide_tile_path(M, N, K, force_wide):
+    """256x256 wide-tile kernel (forced): ragged M/N/K, bias + ReLU epilogue, bf16 output."""
+    torch.manual_seed(5)
+    A, W, b = torch.randn(M, K), torch.randn(N, K) * 0.05, torch.randn(N)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    C().gemm(bf(A), True, K, bf(W), True, K, out, N, M, N, K, b.to(DEV), True, True)
+    ref = torch.relu(A.to(torch.bfloat16).float() @ W.to(torch.bfloat16).float().t() + b)
+    assert rel_err(out.cpu(), ref) < 1e-2
+
+
+@pytest.mark.parametrize("case", [(4, 15, 15, 64, 256, 3, 1, 1), (4, 14, 14, 256, 512, 3, 2, 1),
+                                  (3, 9, 9, 512, 272, 1, 1, 0)])
+def test_conv_wide_tile_path(case, force_wide):
+    """Conv fwd and (phased, row-remapped, addend-fused) dgrad through the wide-tile kernel."""
+    N, H, W, Cin, Cout, k, s, p = case
+    torch.manual_seed(6)
+    x = torch.randn(N, H, W, Cin).to(torch.bfloat16).float().requires_grad_()
+    w = (torch.randn(Cout, k, k, Cin) / math.sqrt(Cin * k * k)).to(torch.bfloat16).float().requires_grad_()
+    y = _conv_ref(x, w, s, p)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    yg = C().conv_fwd(bf(x.detach()), bf(w.detach()), s, p, 1, None, False)
+    assert rel_err(yg.cpu(), y.detach()) < 1e-2
+    add = torch.randn(N, H, W, Cin).to(torch.bfloat16)
+    dx = C().conv_dgrad(bf(dy), bf(w.detach()), H, W, s, p, 1, add.to(DEV))
+    assert rel_err(dx.cpu(), x.grad + add.float()) < 1e-2
+
+
 def test_gemm_bias_relu_bf16_out():
     M, N, K = 257, 136, 96
     A, W, b = torch.randn(M, K), torch.randn(N, K), torch.randn(N)
@@ -144,9 +180,9 @@ def test_conv_fwd_epilogue_bn_sums(case):
     g, b = torch.rand(Cout) + 0.5, torch.randn(Cout)
     rm1, rv1 = shift.clone().to(DEV), torch.ones(Cout, device=DEV)
     rm2, rv2 = shift.clone().to(DEV), torch.ones(Cout, device=DEV)
-    ya, ma, ia, ssa = C().bn_fwd_train_sums(y, sums, rm1.clone(), None, g.to(DEV), b.to(DEV), rm1, rv1, 0.1, 1e-5,
-                                            True)
-    yb, mb, ib, ssb = C().bn_fwd_train(y, None, g.to(DEV), b.to(DEV), rm2, rv2, 0.1, 1e-5, True)
+    ya, ma, ia, ssa, _ = C().bn_fwd_train_sums(y, sums, rm1.clone(), None, g.to(DEV), b.to(DEV), rm1, rv1, 0.1,
+                                               1e-5, True, False)
+    yb, mb, ib, ssb, _ = C().bn_fwd_train(y, None, g.to(DEV), b.to(DEV), rm2, rv2, 0.1, 1e-5, True, False)
     assert rel_err(ma.cpu(), mb.cpu()) < 1e-4 and rel_err(ia.cpu(), ib.cpu()) < 1e-4
     assert rel_err(ya.cpu(), yb.cpu()) < 1e-2 and rel_err(rv1.cpu(), rv2.cpu()) < 1e-4
 
@@ -175,13 +211,20 @@ def test_batchnorm_train(shape, relu, res):
     y.backward(dy)
 
     rmg, rvg = torch.zeros(Cc, device=DEV), torch.ones(Cc, device=DEV)
-    yg, mean, invstd, ss = C().bn_fwd_train(bf(x), bf(r) if res else None, g.to(DEV), b.to(DEV), rmg, rvg, 0.1,
-                                            1e-5, relu)
+    yg, mean, invstd, ss, bits = C().bn_fwd_train(bf(x), bf(r) if res else None, g.to(DEV), b.to(DEV), rmg, rvg,
+                                                  0.1, 1e-5, relu, relu)
     assert rel_err(yg.cpu(), y.detach()) < 1e-2
     assert rel_err(rmg.cpu(), rm) < 1e-4 and rel_err(rvg.cpu(), rv) < 1e-4
-    # the ReLU mask from the saved output, and (no residual) recomputed from x and scale/shift
-    for use_y in ([True, False] if relu and not res else [True]):
-        dx, dres, dgamma, dbeta = C().bn_bwd(bf(dy), bf(x), yg if use_y else None, None if use_y else ss, mean,
+    if relu:  # bit j of byte v is the ReLU mask of element 8v+j
+        want = (yg.reshape(-1, 8).cpu().float() > 0).to(torch.int32)
+        got = torch.stack([(bits.cpu().to(torch.int32) >> j) & 1 for j in range(8)], 1)
+        assert torch.equal(got, want)
+    # the ReLU mask from the saved output, from its bit mask, and (no residual) recomputed from x and
+    # the saved scale/shift
+    modes = ["y"] + (["bits"] if relu else []) + (["ss"] if relu and not res else [])
+    for mode in modes:
+        saved = {"y": yg, "bits": bits, "ss": None}[mode]
+        dx, dres, dgamma, dbeta = C().bn_bwd(bf(dy), bf(x), saved, ss if mode == "ss" else None, mean,
                                              invstd, g.to(DEV), relu, res, None, None)
         assert rel_err(dx.cpu(), xr.grad) < 2e-2
         assert rel_err(dgamma.cpu(), gr.grad) < 1e-2
@@ -280,7 +323,7 @@ def test_adam_matches_torch(adamw):
         ref.grad = g.clone()
         opt.step()
         C().adam_step(master, None, g.to(DEV, torch.bfloat16), m, v, 1e-2, 0.9, 0.99, 1e-8, 0.01, adamw, t,
-                      1.0, None, None)
+                      1.0, None, None, None)
     assert rel_err(master.cpu(), ref.detach()) < 1e-5
 
 

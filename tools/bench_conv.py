@@ -50,10 +50,12 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--torch", action="store_true", help="also time MIOpen / hipBLASLt")
+    ap.add_argument("--wide", type=int, default=-1, help="wide-tile GEMM path: -1 env, 0 off, 1 auto, 2 force")
     a = ap.parse_args()
     c = C()
+    c.set_gemm_paths(a.wide)
     dev = "cuda"
-    for M, N, K in [(4096, 4096, 4096), (8192, 8192, 8192)]:
+    for M, N, K in [(4096, 4096, 4096), (8192, 8192, 8192), (50176, 256, 2304), (12544, 512, 4608)]:
         A = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
         B = torch.randn(N, K, device=dev, dtype=torch.bfloat16)
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
