@@ -851,7 +851,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("fill_random", &fill_random);
   m.def("fill_randint", &fill_randint);
   m.def("gemm", &gemm);
-  m.def("set_gemm_paths", &pda::set_gemm_paths, "force a GEMM kernel path: wide=-1 env default, 0 off, 1 auto, 2 force");
+  m.def("set_gemm_paths", &pda::set_gemm_paths, "force a GEMM kernel path: wide=-1 env default, 0 off, 1 auto, 2 force",
+        pybind11::arg("wide"), pybind11::arg("variant") = -1);
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_fwd_stats", &conv_fwd_stats);
   m.def("bn_fwd_train_sums", &bn_fwd_train_sums);

@@ -110,4 +110,16 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / nxcd;
 }
 
+// Grouped tile order: consecutive tile ids walk GM rows of tiles before moving one column right, so
+// the workgroups in flight on one XCD (consecutive ids after xcd_remap) share GM A-panels and a few
+// B-panels instead of one A-panel and a whole row of B-panels (L2 / MALL traffic on wide GEMMs).
+__device__ __forceinline__ void grouped_tile(int tile, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+  const int per_group = gm * tiles_n;
+  const int g = tile / per_group, first = g * gm;
+  const int rows = min(tiles_m - first, gm);
+  const int r = tile - g * per_group;
+  tm = first + r % rows;
+  tn = r / rows;
+}
+
 }  // namespace pda

@@ -205,14 +205,46 @@ __global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
 }
 
 // ---------------------------------------------------------------- forward apply
+// LDS tables are sized by C (dynamic shared memory): a fixed kMaxC table (16-40 KB) capped residency
+// at 4 workgroups per CU for the backward apply, too few bytes in flight for HBM3E.
+template <bool RES, bool RELU>
+__device__ __forceinline__ void bn_apply_vec(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
+                                             bf16_t* __restrict__ y, uint8_t* __restrict__ bits, int64_t v, int c0,
+                                             const float* s_scale, const float* s_shift, const float (&a_in)[8],
+                                             const float (&r)[8]) {
+  float a[8];
+  const f32x4 sc0 = *reinterpret_cast<const f32x4*>(s_scale + c0), sc1 = *reinterpret_cast<const f32x4*>(s_scale + c0 + 4);
+  const f32x4 sh0 = *reinterpret_cast<const f32x4*>(s_shift + c0), sh1 = *reinterpret_cast<const f32x4*>(s_shift + c0 + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    a[j] = a_in[j] * sc0[j] + sh0[j];
+    a[j + 4] = a_in[j + 4] * sc1[j] + sh1[j];
+  }
+  if (RES) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] += r[j];
+  }
+  if (RELU) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      m |= (a[j] > 0.f ? 1u : 0u) << j;
+      a[j] = fmaxf(a[j], 0.f);
+    }
+    if (bits) bits[v] = (uint8_t)m;  // one byte per 8 channels: the backward's ReLU mask
+  }
+  store8(y + v * 8, a);
+}
+
 template <bool RES, bool RELU>
 __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ res,
                                                             bf16_t* __restrict__ y, int64_t M, int C,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift,
                                                             uint8_t* __restrict__ bits) {
-  __shared__ __attribute__((aligned(16))) float s_scale[kMaxC];
-  __shared__ __attribute__((aligned(16))) float s_shift[kMaxC];
+  extern __shared__ __attribute__((aligned(16))) float s_tab[];  // [2][C]
+  float* s_scale = s_tab;
+  float* s_shift = s_tab + C;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     s_scale[c] = scale[c];
     s_shift[c] = shift[c];
@@ -221,33 +253,23 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16_t* __rest
   const int cv = C / 8;
   const int64_t nvec = M * cv;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
-    const int c0 = (int)(v % cv) * 8;
-    float a[8];
-    load8(x + v * 8, a);
-    const f32x4 sc0 = *reinterpret_cast<const f32x4*>(s_scale + c0), sc1 = *reinterpret_cast<const f32x4*>(s_scale + c0 + 4);
-    const f32x4 sh0 = *reinterpret_cast<const f32x4*>(s_shift + c0), sh1 = *reinterpret_cast<const f32x4*>(s_shift + c0 + 4);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      a[j] = a[j] * sc0[j] + sh0[j];
-      a[j + 4] = a[j + 4] * sc1[j] + sh1[j];
-    }
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; v + stride < nvec; v += 2 * stride) {  // two vectors (2-3 loads each) in flight per lane
+    float a0[8], a1[8], r0[8], r1[8];
+    load8(x + v * 8, a0);
+    load8(x + (v + stride) * 8, a1);
     if (RES) {
-      float r[8];
-      load8(res + v * 8, r);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] += r[j];
+      load8(res + v * 8, r0);
+      load8(res + (v + stride) * 8, r1);
     }
-    if (RELU) {
-      uint32_t m = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        m |= (a[j] > 0.f ? 1u : 0u) << j;
-        a[j] = fmaxf(a[j], 0.f);
-      }
-      if (bits) bits[v] = (uint8_t)m;  // one byte per 8 channels: the backward's ReLU mask
-    }
-    store8(y + v * 8, a);
+    bn_apply_vec<RES, RELU>(x, res, y, bits, v, (int)(v % cv) * 8, s_scale, s_shift, a0, r0);
+    bn_apply_vec<RES, RELU>(x, res, y, bits, v + stride, (int)((v + stride) % cv) * 8, s_scale, s_shift, a1, r1);
+  }
+  if (v < nvec) {
+    float a0[8], r0[8];
+    load8(x + v * 8, a0);
+    if (RES) load8(res + v * 8, r0);
+    bn_apply_vec<RES, RELU>(x, res, y, bits, v, (int)(v % cv) * 8, s_scale, s_shift, a0, r0);
   }
 }
 
@@ -361,43 +383,60 @@ __global__ void __launch_bounds__(kFinThreads) bn_bwd_finalize_kernel(
 }
 
 template <int MASK, bool DRES>
+__device__ __forceinline__ void bn_bwd_apply_vec(const bf16_t* __restrict__ y, const float* s_co, int C, int64_t v,
+                                                 int c0, float (&g)[8], float (&xv)[8], bf16_t* __restrict__ dx,
+                                                 bf16_t* __restrict__ dres) {
+  relu_mask<MASK>(g, y, xv, s_co + 3 * C, s_co + 4 * C, v * 8, c0);
+  if (DRES) store8(dres + v * 8, g);
+  const float* s_A = s_co;
+  const float* s_B = s_co + C;
+  const float* s_C = s_co + 2 * C;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) xv[j] = s_A[c0 + j] * g[j] + s_B[c0 + j] * xv[j] + s_C[c0 + j];
+  store8(dx + v * 8, xv);
+}
+
+template <int MASK, bool DRES>
 __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy,
                                                                 const bf16_t* __restrict__ x,
                                                                 const bf16_t* __restrict__ y,
                                                                 const float* __restrict__ ss, int64_t M, int C,
                                                                 const float* __restrict__ coef,
                                                                 bf16_t* __restrict__ dx, bf16_t* __restrict__ dres) {
-  __shared__ __attribute__((aligned(16))) float s_co[5 * kMaxC];
+  extern __shared__ __attribute__((aligned(16))) float s_co[];  // [5][C]: A, B, Cc, scale, shift
   for (int c = threadIdx.x; c < 3 * C; c += blockDim.x) s_co[c] = coef[c];
   if (MASK == 2)
     for (int c = threadIdx.x; c < 2 * C; c += blockDim.x) s_co[3 * C + c] = ss[c];
   __syncthreads();
-  const float* s_A = s_co;
-  const float* s_B = s_co + C;
-  const float* s_C = s_co + 2 * C;
   const int cv = C / 8;
   const int64_t nvec = M * cv;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
-    const int c0 = (int)(v % cv) * 8;
-    float g[8], xv[8];
-    load8(dy + v * 8, g);
-    load8(x + v * 8, xv);
-    relu_mask<MASK>(g, y, xv, s_co + 3 * C, s_co + 4 * C, v * 8, c0);
-    if (DRES) store8(dres + v * 8, g);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) xv[j] = s_A[c0 + j] * g[j] + s_B[c0 + j] * xv[j] + s_C[c0 + j];
-    store8(dx + v * 8, xv);
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; v + stride < nvec; v += 2 * stride) {  // two vectors in flight per lane
+    float g0[8], x0[8], g1[8], x1[8];
+    load8(dy + v * 8, g0);
+    load8(x + v * 8, x0);
+    load8(dy + (v + stride) * 8, g1);
+    load8(x + (v + stride) * 8, x1);
+    bn_bwd_apply_vec<MASK, DRES>(y, s_co, C, v, (int)(v % cv) * 8, g0, x0, dx, dres);
+    bn_bwd_apply_vec<MASK, DRES>(y, s_co, C, v + stride, (int)((v + stride) % cv) * 8, g1, x1, dx, dres);
+  }
+  if (v < nvec) {
+    float g0[8], x0[8];
+    load8(dy + v * 8, g0);
+    load8(x + v * 8, x0);
+    bn_bwd_apply_vec<MASK, DRES>(y, s_co, C, v, (int)(v % cv) * 8, g0, x0, dx, dres);
   }
 }
 
 hipError_t launch_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int C, const float* scale,
                         const float* shift, bool relu, uint8_t* bits, hipStream_t st) {
   const int grid = ew_grid(M * C / 8);
-  if (res && relu) bn_apply_kernel<true, true><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits);
-  else if (res) bn_apply_kernel<true, false><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr);
-  else if (relu) bn_apply_kernel<false, true><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits);
-  else bn_apply_kernel<false, false><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr);
+  const size_t lds = 2 * (size_t)C * sizeof(float);
+  if (res && relu) bn_apply_kernel<true, true><<<grid, kThreads, lds, st>>>(x, res, y, M, C, scale, shift, bits);
+  else if (res) bn_apply_kernel<true, false><<<grid, kThreads, lds, st>>>(x, res, y, M, C, scale, shift, nullptr);
+  else if (relu) bn_apply_kernel<false, true><<<grid, kThreads, lds, st>>>(x, res, y, M, C, scale, shift, bits);
+  else bn_apply_kernel<false, false><<<grid, kThreads, lds, st>>>(x, res, y, M, C, scale, shift, nullptr);
   return hipGetLastError();
 }
 
@@ -480,8 +519,9 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint
                                                                          dgamma_b, dbeta_f, dbeta_b, coef);
   PDA_CHECK_HIP(hipGetLastError());
   const int grid = ew_grid(M * C / 8);
+  const size_t lds = 5 * (size_t)C * sizeof(float);
 #define BWD_APPLY(MK, DR) \
-  bn_bwd_apply_kernel<MK, DR><<<grid, kThreads, 0, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres)
+  bn_bwd_apply_kernel<MK, DR><<<grid, kThreads, lds, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres)
   if (mask == 0) { if (dres) BWD_APPLY(0, true); else BWD_APPLY(0, false); }
   else if (mask == 1) { if (dres) BWD_APPLY(1, true); else BWD_APPLY(1, false); }
   else if (mask == 2) { if (dres) BWD_APPLY(2, true); else BWD_APPLY(2, false); }

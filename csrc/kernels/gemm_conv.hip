@@ -441,7 +441,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
   const int wm = wid >> 1, wn = wid & 1;
   const int ntiles = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, ntiles);
-  const int tn = tile % tiles_n, tm = tile / tiles_n;
+  int tm, tn;
+  grouped_tile(tile, ntiles / tiles_n, tiles_n, 8, tm, tn);
   const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
 
   const int ktiles = (int)((K + BK - 1) / BK);
@@ -786,17 +787,26 @@ constexpr int W_STAGE = 4 * W_HALF;   // A0 A1 B0 B1
 constexpr int W_SROW = 256 + 8;       // epilogue staging row (bf16 elements)
 constexpr int W_LDS = 2 * W_STAGE > 256 * W_SROW * 2 ? 2 * W_STAGE : 256 * W_SROW * 2;
 
-template <int QA, int QB>
+// VAR (schedule experiments, selected at run time): bit 0 = s_setprio(1) around each MFMA cluster,
+// bit 1 = interleave each MFMA with one of the next phase's ds_reads (sched_group_barrier).
+template <int QA, int QB, int VAR>
 __device__ __forceinline__ void wide_mma(f32x4 (&acc)[8][4], const mfma_bf16x8 (&fa)[4], const mfma_bf16x8 (&fb)[2]) {
+  if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j) {
       acc[4 * QA + i][2 * QB + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[4 * QA + i][2 * QB + j],
                                                                             0, 0, 0);
+      if constexpr (VAR & 2) {
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);    // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // then one DS read
+      }
+    }
+  if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
 }
 
-template <class LA, class LB>
+template <class LA, class LB, int VAR>
 __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K,
                                                            int tiles_n, Epi epi) {
   static_assert(LA::kMajor && LB::kMajor && LA::NCH == 2 && LB::NCH == 2, "K-major 64-row loaders");
@@ -806,7 +816,8 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
   const int wr = wid >> 2, wc = wid & 3;
   const int ntiles = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, ntiles);
-  const int tn = tile % tiles_n, tm = tile / tiles_n;
+  int tm, tn;
+  grouped_tile(tile, ntiles / tiles_n, tiles_n, 8, tm, tn);
   const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
   const int nk = (int)((K + BK - 1) / BK);
 
@@ -859,20 +870,20 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
     // k 0..31
     if (more) issue_a(t + 1);
     rd_b(cs, 1, 0, fb1);
-    wide_mma<0, 0>(acc, fa0, fb0);
+    wide_mma<0, 0, VAR>(acc, fa0, fb0);
     if (more) issue_b(t + 1);
     rd_a(cs, 1, 0, fa1);
-    wide_mma<0, 1>(acc, fa0, fb1);
-    wide_mma<1, 1>(acc, fa1, fb1);
+    wide_mma<0, 1, VAR>(acc, fa0, fb1);
+    wide_mma<1, 1, VAR>(acc, fa1, fb1);
     rd_a(cs, 1, 32, fa0);
     rd_b(cs, 1, 32, fb1);
-    wide_mma<1, 0>(acc, fa1, fb0);
+    wide_mma<1, 0, VAR>(acc, fa1, fb0);
     // k 32..63
     rd_b(cs, 0, 32, fb0);
-    wide_mma<1, 1>(acc, fa0, fb1);
+    wide_mma<1, 1, VAR>(acc, fa0, fb1);
     rd_a(cs, 0, 32, fa1);
-    wide_mma<1, 0>(acc, fa0, fb0);
-    wide_mma<0, 0>(acc, fa1, fb0);
+    wide_mma<1, 0, VAR>(acc, fa0, fb0);
+    wide_mma<0, 0, VAR>(acc, fa1, fb0);
     if (more) {
       // next step's operands landed (own DMAs, then everyone's); this stage is no longer read
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -881,7 +892,7 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
       rd_a(ns, 0, 0, fa0);
       rd_b(ns, 0, 0, fb0);
     }
-    wide_mma<0, 1>(acc, fa1, fb1);
+    wide_mma<0, 1, VAR>(acc, fa1, fb1);
   }
   __syncthreads();  // every wave is done with the operand stages before they become the staging tile
 
@@ -1155,18 +1166,30 @@ bool use_wide(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) {
   return wide_pays(M, N);
 }
 
-template <class LA, class LB>
-hipError_t launch_wide(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st) {
+int g_wide_variant = 3;  // setprio + MFMA/ds_read interleave: best or tied on every measured shape
+
+template <class LA, class LB, int VAR>
+hipError_t launch_wide_v(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st) {
   static bool attr = [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_wide_kernel<LA, LB>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_wide_kernel<LA, LB, VAR>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, W_LDS);
     return true;
   }();
   (void)attr;
   const int tiles_n = (int)((N + 255) / 256);
   const int ntiles = (int)((M + 255) / 256) * tiles_n;
-  gemm_wide_kernel<LA, LB><<<ntiles, W_NT, W_LDS, st>>>(la, lb, M, N, K, tiles_n, epi);
+  gemm_wide_kernel<LA, LB, VAR><<<ntiles, W_NT, W_LDS, st>>>(la, lb, M, N, K, tiles_n, epi);
   return hipGetLastError();
+}
+
+template <class LA, class LB>
+hipError_t launch_wide(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st) {
+  switch (g_wide_variant) {
+    case 1: return launch_wide_v<LA, LB, 1>(la, lb, M, N, K, epi, st);
+    case 2: return launch_wide_v<LA, LB, 2>(la, lb, M, N, K, epi, st);
+    case 3: return launch_wide_v<LA, LB, 3>(la, lb, M, N, K, epi, st);
+    default: return launch_wide_v<LA, LB, 0>(la, lb, M, N, K, epi, st);
+  }
 }
 
 template <template <int> class TA, template <int> class TB, class MakeA, class MakeB>
@@ -1202,7 +1225,10 @@ bool dgrad_phased(int stride, int dil) { return stride == 1 || dil == 1; }
 
 }  // namespace
 
-void set_gemm_paths(int wide) { g_wide_override = wide; }
+void set_gemm_paths(int wide, int variant) {
+  g_wide_override = wide;
+  if (variant >= 0) g_wide_variant = variant;
+}
 
 int64_t gemm_slab_floats(int64_t M, int64_t N, int64_t K, bool allow_split) {
   Plan p = plan_gemm(M, N, K, allow_split, 512);

@@ -40,9 +40,14 @@ def main():
         t = timeit(lambda: C().bn_fwd_train(x, r, g, b, rm, rv, 0.1, 1e-5, True, True))
         res["fwd_res_relu_ms"] = round(t, 4)
         res["fwd_TBps"] = round(n * 2 * (1 + 3) / t / 1e9, 2)
+        y2 = torch.empty_like(x)
+        t = timeit(lambda: y2.copy_(x))
+        res["copy_TBps"] = round(n * 2 * 2 / t / 1e9, 2)
         for name, saved, ssv in (("y", y, None), ("bits", bits, None), ("ss", None, ss)):
             t = timeit(lambda: C().bn_bwd(dy, x, saved, ssv, mean, invstd, g, True, True, None, None))
             res[f"bwd_{name}_ms"] = round(t, 4)
+            per = {"y": 16, "bits": 12.25, "ss": 12}[name]  # bytes per element over both passes
+            res[f"bwd_{name}_TBps"] = round(n * per / t / 1e9, 2)
         print(json.dumps(res), flush=True)
 
 
