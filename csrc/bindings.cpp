@@ -171,10 +171,17 @@ void bn_param_ptrs(const c10::optional<Tensor>& t, const float** f, const pda::b
   else *f = t->data_ptr<float>();
 }
 
+int64_t* nbt_ptr(const c10::optional<Tensor>& n, const Tensor& x) {
+  if (!n || !n->defined()) return nullptr;
+  TORCH_CHECK(n->scalar_type() == at::kLong && n->numel() == 1 && n->device() == x.device(),
+              "num_batches must be a one-element int64 tensor on the input's device");
+  return n->data_ptr<int64_t>();
+}
+
 std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma,
                                  c10::optional<Tensor> beta, c10::optional<Tensor> running_mean,
                                  c10::optional<Tensor> running_var, double momentum, double eps, bool relu,
-                                 bool relu_bits) {
+                                 bool relu_bits, c10::optional<Tensor> num_batches) {
   check_bf16(x, "x");
   const int64_t C = x.size(-1), M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0 && C <= 2048, "channels must be a multiple of 8 and <= 2048");
@@ -201,14 +208,15 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optio
                                  running_var ? running_var->data_ptr<float>() : nullptr, (float)momentum, (float)eps,
                                  relu, mean.data_ptr<float>(), invstd.data_ptr<float>(), ss.data_ptr<float>(),
                                  ws.data_ptr<float>(), bits.defined() ? bits.data_ptr<uint8_t>() : nullptr,
-                                 stream_of(x)));
+                                 nbt_ptr(num_batches, x), stream_of(x)));
   return {y, mean, invstd, ss, bits};
 }
 
 std::vector<Tensor> bn_fwd_train_sums(Tensor x, Tensor sums, Tensor shift, c10::optional<Tensor> res,
                                       c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
                                       c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
-                                      double momentum, double eps, bool relu, bool relu_bits) {
+                                      double momentum, double eps, bool relu, bool relu_bits,
+                                      c10::optional<Tensor> num_batches) {
   check_bf16(x, "x");
   check_f32(sums, "sums");
   check_f32(shift, "shift");
@@ -233,7 +241,7 @@ std::vector<Tensor> bn_fwd_train_sums(Tensor x, Tensor sums, Tensor shift, c10::
                                       running_var ? running_var->data_ptr<float>() : nullptr, (float)momentum,
                                       (float)eps, relu, mean.data_ptr<float>(), invstd.data_ptr<float>(),
                                       ss.data_ptr<float>(), bits.defined() ? bits.data_ptr<uint8_t>() : nullptr,
-                                      stream_of(x)));
+                                      nbt_ptr(num_batches, x), stream_of(x)));
   return {y, mean, invstd, ss, bits};
 }
 

@@ -78,7 +78,9 @@ int64_t bn_workspace_floats(int64_t M, int64_t C);
 hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
                         const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, float* running_mean,
                         float* running_var, float momentum, float eps, bool relu, float* save_mean,
-                        float* save_invstd, float* save_ss, float* ws, uint8_t* relu_bits, hipStream_t st);
+                        float* save_invstd, float* save_ss, float* ws, uint8_t* relu_bits, int64_t* num_batches,
+                        hipStream_t st);
+// num_batches (optional): int64 counter incremented once on the stream (BN num_batches_tracked)
 // relu_bits (optional, with relu): [M*C/8] bytes, bit j of byte v = ReLU mask of element 8v+j
 // training forward from precomputed sums (e.g. a conv epilogue): sums[0:C] = sum(x - K), sums[C:2C] =
 // sum((x - K)^2) over the M rows, K = shift; finalize + apply only (no statistics pass over x)
@@ -86,7 +88,7 @@ hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int6
                              const float* shift, const float* gamma_f, const bf16_t* gamma_b, const float* beta_f,
                              const bf16_t* beta_b, float* running_mean, float* running_var, float momentum, float eps,
                              bool relu, float* save_mean, float* save_invstd, float* save_ss, uint8_t* relu_bits,
-                             hipStream_t st);
+                             int64_t* num_batches, hipStream_t st);
 hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
                        const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, const float* running_mean,
                        const float* running_var, float eps, bool relu, float* ws, hipStream_t st);

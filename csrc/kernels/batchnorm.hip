@@ -45,14 +45,14 @@ BnGeom bn_geom(int64_t M, int64_t C) {
     g.rpi = kThreads / g.cv;
     g.gy = 1;
   }
-  // ~512 row blocks (2 workgroups per CU, 8 outstanding 16-B loads per lane) — enough bytes in flight
-  // for HBM3E, while the finalize pass (one workgroup per 64 channels) only sums 512 slab rows;
-  // >= 64 rows per block keeps the slabs small for the wide (C = 2048) layers.  (Measured: 1024
-  // blocks made finalize ~2x slower; atomic accumulation into 32 shared rows instead of slabs made
-  // the reductions 1.3 ms/step slower at bs 256.)
-  const int target = 512 / g.gy > 0 ? 512 / g.gy : 1;
+  // ~1024 row blocks (4 workgroups per CU, 8 outstanding 16-B loads per lane).  Measured on the
+  // ResNet-50 shapes with HBM-cold buffers (tools/bnlab): 512 -> 1024 blocks lifts the backward
+  // reductions from ~4.9 to ~6.1 TB/s (3.7 -> 5.6 with the ReLU bit mask) and the statistics pass
+  // slightly; the finalize pass keeps up by summing the slab rows 8 loads deep per lane.  Small
+  // blocks (>= 8 row iterations of the widest layers) keep C = 2048 at ~800 blocks, not 196.
+  const int target = 1024 / g.gy > 0 ? 1024 / g.gy : 1;
   int64_t rpb = (M + target - 1) / target;
-  const int64_t min_rpb = (int64_t)g.rpi * 8 > 64 ? (int64_t)g.rpi * 8 : 64;
+  const int64_t min_rpb = (int64_t)g.rpi * 8 > 16 ? (int64_t)g.rpi * 8 : 16;
   if (rpb < min_rpb) rpb = min_rpb;
   g.rpb = rpb;
   g.nrb = (int)((M + rpb - 1) / rpb);
@@ -97,20 +97,27 @@ __device__ __forceinline__ void slab_sum(const float* __restrict__ pa, const flo
                                          int c, float& sa, float& sb) {
   __shared__ float red_a[kFinThreads], red_b[kFinThreads];
   const int l = threadIdx.x >> 6;  // 0..15
-  float a0 = 0.f, a1 = 0.f, b0 = 0.f, b1 = 0.f;
+  float a[8], b[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = b[u] = 0.f;
   if (c < C) {
+    // 8 independent loads per slab in flight per lane: the slab rows were just written (L2/MALL
+    // hits), so this pass is latency-bound — depth, not bandwidth, sets its time
     int r = l;
-    for (; r + 16 < nrb; r += 32) {
-      a0 += pa[(int64_t)r * C + c];
-      b0 += pb[(int64_t)r * C + c];
-      a1 += pa[(int64_t)(r + 16) * C + c];
-      b1 += pb[(int64_t)(r + 16) * C + c];
+    for (; r + 7 * 16 < nrb; r += 8 * 16) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a[u] += pa[(int64_t)(r + 16 * u) * C + c];
+        b[u] += pb[(int64_t)(r + 16 * u) * C + c];
+      }
     }
     for (; r < nrb; r += 16) {
-      a0 += pa[(int64_t)r * C + c];
-      b0 += pb[(int64_t)r * C + c];
+      a[0] += pa[(int64_t)r * C + c];
+      b[0] += pb[(int64_t)r * C + c];
     }
   }
+  const float a0 = (a[0] + a[1]) + (a[2] + a[3]), a1 = (a[4] + a[5]) + (a[6] + a[7]);
+  const float b0 = (b[0] + b[1]) + (b[2] + b[3]), b1 = (b[4] + b[5]) + (b[6] + b[7]);
   red_a[threadIdx.x] = a0 + a1;
   red_b[threadIdx.x] = b0 + b1;
   __syncthreads();
@@ -176,8 +183,10 @@ __global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
     int64_t M, int C, const float* __restrict__ gamma_f, const bf16_t* __restrict__ gamma_b, const float* __restrict__ beta_f,
     const bf16_t* __restrict__ beta_b, float* __restrict__ running_mean, float* __restrict__ running_var,
     float momentum, float eps, float* __restrict__ save_mean, float* __restrict__ save_invstd,
-    float* __restrict__ scale, float* __restrict__ shift) {
+    float* __restrict__ scale, float* __restrict__ shift, int64_t* __restrict__ num_batches) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  // the module's num_batches_tracked += 1 rides on this launch (one fewer kernel per BN layer)
+  if (TRAIN && num_batches && blockIdx.x == 0 && threadIdx.x == 0) *num_batches += 1;
   float s1 = 0.f, s2 = 0.f;
   if (TRAIN) slab_sum(slab, slab + (int64_t)nrb * C, nrb, C, c, s1, s2);
   if (threadIdx.x >= 64 || c >= C) return;
@@ -310,11 +319,17 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* _
   const int64_t r0 = (int64_t)blockIdx.x * rpb;
   const int64_t r1 = min(r0 + rpb, M);
   const int c0 = vcol * 8;
-  float sa[8], sb[8], mu[8];
+  float sa[8], sb[8], mu[8], rsc[8], rsh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.f;
   if (active) {
     load8(mean + c0, mu);
+    // a lane's channel group never changes: the MASK 2 scale/shift live in registers, not in
+    // per-element global loads
+    if constexpr (MASK == 2) {
+      load8(ss + c0, rsc);
+      load8(ss + C + c0, rsh);
+    }
     int64_t r = r0 + ty;
     for (; r + 3 * rpi < r1; r += 4 * rpi) {  // 4 rows x 2 tensors = 8 loads in flight per lane
       float g[4][8], xv[4][8];
@@ -331,6 +346,9 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* _
         if constexpr (MASK == 3) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) g[u][j] = (mb[u] >> j) & 1u ? g[u][j] : 0.f;
+        } else if constexpr (MASK == 2) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[u][j] = fmaf(xv[u][j], rsc[j], rsh[j]) > 0.f ? g[u][j] : 0.f;
         } else {
           relu_mask<MASK>(g[u], y, xv[u], ss, ss + C, (r + u * rpi) * C + c0, c0);
         }
@@ -451,7 +469,8 @@ int64_t bn_workspace_floats(int64_t M, int64_t C) {
 hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
                         const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, float* running_mean,
                         float* running_var, float momentum, float eps, bool relu, float* save_mean,
-                        float* save_invstd, float* save_ss, float* ws, uint8_t* relu_bits, hipStream_t st) {
+                        float* save_invstd, float* save_ss, float* ws, uint8_t* relu_bits, int64_t* num_batches,
+                        hipStream_t st) {
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C);
   float* scale = save_ss ? save_ss : ws + 2 * (int64_t)g.nrb * C;
@@ -460,7 +479,7 @@ hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M
   PDA_CHECK_HIP(hipGetLastError());
   bn_finalize_kernel<true><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
       x, nullptr, ws, g.nrb, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum, eps, save_mean,
-      save_invstd, scale, shift);
+      save_invstd, scale, shift, num_batches);
   PDA_CHECK_HIP(hipGetLastError());
   return launch_apply(x, res, y, M, (int)C, scale, shift, relu, relu_bits, st);
 }
@@ -469,13 +488,13 @@ hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int6
                              const float* shift, const float* gamma_f, const bf16_t* gamma_b, const float* beta_f,
                              const bf16_t* beta_b, float* running_mean, float* running_var, float momentum, float eps,
                              bool relu, float* save_mean, float* save_invstd, float* save_ss, uint8_t* relu_bits,
-                             hipStream_t st) {
+                             int64_t* num_batches, hipStream_t st) {
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
   float* scale = save_ss;
   float* shift_out = save_ss + C;
   bn_finalize_kernel<true><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
       x, shift, sums, 1, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum, eps,
-      save_mean, save_invstd, scale, shift_out);
+      save_mean, save_invstd, scale, shift_out, num_batches);
   PDA_CHECK_HIP(hipGetLastError());
   return launch_apply(x, res, y, M, (int)C, scale, shift_out, relu, relu_bits, st);
 }
@@ -488,7 +507,7 @@ hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M,
   float* shift = ws + C;
   bn_finalize_kernel<false><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
       x, nullptr, nullptr, 0, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, const_cast<float*>(running_mean),
-      const_cast<float*>(running_var), 0.f, eps, nullptr, nullptr, scale, shift);
+      const_cast<float*>(running_var), 0.f, eps, nullptr, nullptr, scale, shift, nullptr);
   PDA_CHECK_HIP(hipGetLastError());
   return launch_apply(x, res, y, M, (int)C, scale, shift, relu, nullptr, st);
 }

@@ -194,26 +194,43 @@ __global__ void __launch_bounds__(kThreads) colstrip_partial_kernel(const T* __r
   }
 }
 
-// out_k[col] = sum_s ws[k][s][col] (+ out_k[col] if accumulate)
-__global__ void __launch_bounds__(kThreads) colreduce_finalize_kernel(const float* __restrict__ ws, int nslab,
-                                                                      int64_t D, int nout, float* __restrict__ out0,
-                                                                      float* __restrict__ out1) {
-  const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (t >= D * nout) return;
-  const int k = (int)(t / D);
-  const int64_t col = t % D;
+// out_k[col] = sum_s ws[k][s][col].  A workgroup is 64 columns x 16 slab lanes with 8 loads in flight
+// per lane: the slabs were just written (L2 / MALL hits), so depth of outstanding loads, not bytes,
+// sets the time.  (One thread per column walking ~512 slabs 4 loads deep took ~30 us per call on the
+// GPT-2 bias / LayerNorm gradients.)
+constexpr int kFinCols = 64, kFinLanes = 16;
+__global__ void __launch_bounds__(kFinCols * kFinLanes) colreduce_finalize_kernel(const float* __restrict__ ws,
+                                                                                  int nslab, int64_t D, int nout,
+                                                                                  float* __restrict__ out0,
+                                                                                  float* __restrict__ out1) {
+  __shared__ float red[kFinLanes][kFinCols];
+  const int cl = threadIdx.x % kFinCols, lane = threadIdx.x / kFinCols;
+  const int64_t t = (int64_t)blockIdx.x * kFinCols + cl;  // output index over nout x D
+  const bool ok = t < D * nout;
+  const int k = ok ? (int)(t / D) : 0;
+  const int64_t col = ok ? t % D : 0;
   const float* p = ws + (int64_t)k * nslab * D + col;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int s = 0;
-  for (; s + 4 <= nslab; s += 4) {
-    s0 += p[(int64_t)s * D];
-    s1 += p[(int64_t)(s + 1) * D];
-    s2 += p[(int64_t)(s + 2) * D];
-    s3 += p[(int64_t)(s + 3) * D];
+  float a[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) a[u] = 0.f;
+  if (ok) {
+    int s = lane;
+    for (; s + 7 * kFinLanes < nslab; s += 8 * kFinLanes) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] += p[(int64_t)(s + u * kFinLanes) * D];
+    }
+    for (; s < nslab; s += kFinLanes) a[0] += p[(int64_t)s * D];
   }
-  for (; s < nslab; ++s) s0 += p[(int64_t)s * D];
-  (k == 0 ? out0 : out1)[col] = (s0 + s1) + (s2 + s3);
+  red[lane][cl] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (lane != 0 || !ok) return;
+  float r = 0.f;
+#pragma unroll
+  for (int l = 0; l < kFinLanes; ++l) r += red[l][cl];
+  (k == 0 ? out0 : out1)[col] = r;
 }
+
+inline unsigned fin_grid(int64_t n) { return (unsigned)((n + kFinCols - 1) / kFinCols); }
 
 int plan_slabs(int64_t rows, int64_t D) {
   const int64_t strips = (D + kStripCols - 1) / kStripCols;
@@ -302,8 +319,7 @@ hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* g
 #undef P
   PDA_CHECK_HIP(hipGetLastError());
   const int nout = rms ? 1 : 2;
-  colreduce_finalize_kernel<<<(unsigned)((D * nout + kThreads - 1) / kThreads), kThreads, 0, st>>>(ws, nslab, D, nout,
-                                                                                                  dgamma, dbeta);
+  colreduce_finalize_kernel<<<fin_grid(D * nout), kFinCols * kFinLanes, 0, st>>>(ws, nslab, D, nout, dgamma, dbeta);
   return hipGetLastError();
 }
 
@@ -320,8 +336,7 @@ hipError_t colsum(const void* x, bool bf16, float* out, int64_t rows, int64_t co
     colstrip_partial_kernel<float, false, false><<<pg, kThreads, 0, st>>>((const float*)x, nullptr, nullptr, nullptr,
                                                                           ws, rows, cols, rps, nslab);
   PDA_CHECK_HIP(hipGetLastError());
-  colreduce_finalize_kernel<<<(unsigned)((cols + kThreads - 1) / kThreads), kThreads, 0, st>>>(ws, nslab, cols, 1, out,
-                                                                                               nullptr);
+  colreduce_finalize_kernel<<<fin_grid(cols), kFinCols * kFinLanes, 0, st>>>(ws, nslab, cols, 1, out, nullptr);
   return hipGetLastError();
 }
 

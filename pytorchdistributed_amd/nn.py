@@ -107,13 +107,11 @@ class BatchNorm2d(tnn.Module):
         return self
 
     def forward(self, x, residual=None, relu=False, residual_join=None, stats=None):
-        if self.training:
-            self.num_batches_tracked.add_(1)
         if isinstance(x, tuple):  # (y, stats) from Conv2d(..., bn=self)
             x, stats = x
         return ops.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
                               self.momentum, self.eps, residual=residual, relu=relu, residual_join=residual_join,
-                              stats=stats)
+                              stats=stats, num_batches_tracked=self.num_batches_tracked)
 
 
 class ReLU(tnn.Module):

@@ -16,7 +16,7 @@ from ..parallel.flat import grad_target
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu, join,
-                sums=None, shift=None):
+                sums=None, shift=None, num_batches=None):
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()
@@ -26,10 +26,10 @@ class _BatchNormFn(torch.autograd.Function):
         want_bits = relu and residual is not None
         if training and sums is not None:  # statistics already reduced by the producing conv's epilogue
             y, mean, invstd, ss, bits = C().bn_fwd_train_sums(x, sums, shift, residual, gamma, beta, running_mean,
-                                                              running_var, momentum, eps, relu, want_bits)
+                                                              running_var, momentum, eps, relu, want_bits, num_batches)
         elif training:
             y, mean, invstd, ss, bits = C().bn_fwd_train(x, residual, gamma, beta, running_mean, running_var,
-                                                         momentum, eps, relu, want_bits)
+                                                         momentum, eps, relu, want_bits, num_batches)
         else:
             y = C().bn_fwd_eval(x, residual, gamma, beta, running_mean, running_var, eps, relu)
             mean = running_mean
@@ -59,7 +59,7 @@ class _BatchNormFn(torch.autograd.Function):
         db = dbeta if ctx.needs_input_grad[2] else None
         if has_res and ctx.join is not None:
             dres = ctx.join.contribute(dres)  # usually stashed for the consumer conv's dgrad epilogue
-        return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None, None, None, None
+        return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None, None, None, None, None
 
 
 def _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu):
@@ -77,14 +77,18 @@ def _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, trainin
 
 
 def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True, momentum=0.1, eps=1e-5,
-               residual=None, relu=False, residual_join=None, stats=None):
+               residual=None, relu=False, residual_join=None, stats=None, num_batches_tracked=None):
     """BatchNorm over the last (channel) dim of ``x`` (any leading dims), then ``+residual``, then ReLU.
     ``residual_join``: the residual's gradient is handed to the join instead of autograd's add.
-    ``stats``: ``(sums, shift)`` from :func:`~.conv.conv2d_bn_stats` — skips the statistics pass."""
+    ``stats``: ``(sums, shift)`` from :func:`~.conv.conv2d_bn_stats` — skips the statistics pass.
+    ``num_batches_tracked``: int64 counter incremented in training mode (inside the finalize kernel on
+    the native path, so it costs no launch of its own)."""
     if x.is_cuda and x.dtype == torch.bfloat16:
         sums, shift = stats if stats is not None else (None, None)
         return _BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
-                                  relu, residual_join, sums, shift)
+                                  relu, residual_join, sums, shift, num_batches_tracked if training else None)
+    if training and num_batches_tracked is not None:
+        num_batches_tracked.add_(1)
     return _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu)
 
 

@@ -180,9 +180,11 @@ def test_conv_fwd_epilogue_bn_sums(case):
     g, b = torch.rand(Cout) + 0.5, torch.randn(Cout)
     rm1, rv1 = shift.clone().to(DEV), torch.ones(Cout, device=DEV)
     rm2, rv2 = shift.clone().to(DEV), torch.ones(Cout, device=DEV)
+    nbt = torch.zeros((), dtype=torch.long, device=DEV)
     ya, ma, ia, ssa, _ = C().bn_fwd_train_sums(y, sums, rm1.clone(), None, g.to(DEV), b.to(DEV), rm1, rv1, 0.1,
-                                               1e-5, True, False)
-    yb, mb, ib, ssb, _ = C().bn_fwd_train(y, None, g.to(DEV), b.to(DEV), rm2, rv2, 0.1, 1e-5, True, False)
+                                               1e-5, True, False, nbt)
+    yb, mb, ib, ssb, _ = C().bn_fwd_train(y, None, g.to(DEV), b.to(DEV), rm2, rv2, 0.1, 1e-5, True, False, nbt)
+    assert nbt.item() == 2  # num_batches_tracked is bumped by each training finalize
     assert rel_err(ma.cpu(), mb.cpu()) < 1e-4 and rel_err(ia.cpu(), ib.cpu()) < 1e-4
     assert rel_err(ya.cpu(), yb.cpu()) < 1e-2 and rel_err(rv1.cpu(), rv2.cpu()) < 1e-4
 
@@ -212,7 +214,7 @@ def test_batchnorm_train(shape, relu, res):
 
     rmg, rvg = torch.zeros(Cc, device=DEV), torch.ones(Cc, device=DEV)
     yg, mean, invstd, ss, bits = C().bn_fwd_train(bf(x), bf(r) if res else None, g.to(DEV), b.to(DEV), rmg, rvg,
-                                                  0.1, 1e-5, relu, relu)
+                                                  0.1, 1e-5, relu, relu, None)
     assert rel_err(yg.cpu(), y.detach()) < 1e-2
     assert rel_err(rmg.cpu(), rm) < 1e-4 and rel_err(rvg.cpu(), rv) < 1e-4
     if relu:  # bit j of byte v is the ReLU mask of element 8v+j

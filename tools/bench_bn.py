@@ -35,9 +35,9 @@ def main():
         b = torch.zeros(Cc, device=dev)
         rm, rv = torch.zeros(Cc, device=dev), torch.ones(Cc, device=dev)
         n = M * Cc
-        y, mean, invstd, ss, bits = C().bn_fwd_train(x, r, g, b, rm, rv, 0.1, 1e-5, True, True)
+        y, mean, invstd, ss, bits = C().bn_fwd_train(x, r, g, b, rm, rv, 0.1, 1e-5, True, True, None)
         res = {"M": M, "C": Cc}
-        t = timeit(lambda: C().bn_fwd_train(x, r, g, b, rm, rv, 0.1, 1e-5, True, True))
+        t = timeit(lambda: C().bn_fwd_train(x, r, g, b, rm, rv, 0.1, 1e-5, True, True, None))
         res["fwd_res_relu_ms"] = round(t, 4)
         res["fwd_TBps"] = round(n * 2 * (1 + 3) / t / 1e9, 2)
         y2 = torch.empty_like(x)
