@@ -428,6 +428,25 @@ __device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
   return (n * e.rm_H + (int64_t)hh * e.rm_st + e.rm_ph) * e.rm_W + (int64_t)ww * e.rm_st + e.rm_pw;
 }
 
+// Counted vmcnt waits and a barrier that does not drain outstanding LDS-DMA (multi-stage pipelines:
+// `__syncthreads()` would wait for every global_load_lds with vmcnt(0)).  A three-stage variant of
+// the 128-tile kernel (two K tiles in flight) measured slower on every ResNet-50 shape it could
+// serve at two workgroups per CU (64-row / 64-column tiles): latency is not what bounds them.
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N == 0 || N == 4 || N == 6 || N == 8, "add the literal");
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // ------------------------------------------------------------------ the kernel
 template <int BM, int BN, class LA, class LB>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K, int tiles_n,
@@ -460,6 +479,21 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  auto mma_tile = [&](const char* As, const char* Bs) {
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      mfma_bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = read_frag<LA::kMajor, BM>(As, wm * WM + 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = read_frag<LB::kMajor, BN>(Bs, wn * WN + 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  };
   // Two LDS buffers: the DMA of tile t+1 runs while tile t is multiplied; one vmcnt(0) + barrier per
   // K tile retires it (cdna_hip_programming.md §5 "glds vs register staging").
   if (kt0 < kt1) {
@@ -478,19 +512,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
       glds_tile(la, sa, (int64_t)(kt + 1) * BK, An, wid);
       glds_tile(lb, sb, (int64_t)(kt + 1) * BK, An + A_BYTES, wid);
     }
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 32) {
-      mfma_bf16x8 af[TM], bfr[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = read_frag<LA::kMajor, BM>(As, wm * WM + 16 * i, kk, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = read_frag<LB::kMajor, BN>(Bs, wn * WN + 16 * j, kk, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
+    mma_tile(As, Bs);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -645,19 +667,6 @@ constexpr int BIG_A_HALF = 128 * BK * 2, BIG_B_HALF = 64 * BK * 2;
 constexpr int BIG_STAGE = 2 * BIG_A_HALF + 2 * BIG_B_HALF;
 constexpr int BIG_LDS = 3 * BIG_STAGE;
 
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else static_assert(N == 0 || N == 6, "add the literal");
-}
-
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
 template <class LA, class LB>
 __global__ void __launch_bounds__(BIG_NT, 1) gemm_big_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K,
                                                             int tiles_n, Epi epi) {
@@ -806,10 +815,19 @@ __device__ __forceinline__ void wide_mma(f32x4 (&acc)[8][4], const mfma_bf16x8 (
   if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
 }
 
+// Fragment of a 128-row operand half.  K-major halves are one [128][64] image; an MN-major half is
+// two [64 k][64] images (one per 256-thread group, 8 KB apart), read with ds_read_b64_tr_b16.
+template <class L>
+__device__ __forceinline__ mfma_bf16x8 wide_frag(const char* half, int row, int kk, int lane) {
+  if constexpr (L::kMajor) return read_frag<true, 128>(half, row, kk, lane);
+  else return read_frag<false, 64>(half + (row >> 6) * (W_HALF / 2), row & 63, kk, lane);
+}
+
+// blockIdx.y = K split (ktiles_per_split K tiles each); split launches write fp32 slabs.
 template <class LA, class LB, int VAR>
 __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K,
-                                                           int tiles_n, Epi epi) {
-  static_assert(LA::kMajor && LB::kMajor && LA::NCH == 2 && LB::NCH == 2, "K-major 64-row loaders");
+                                                           int tiles_n, int ktiles_per_split, Epi epi) {
+  static_assert(LA::NCH == 2 && LB::NCH == 2, "64-row / 64-column loaders");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int grp = tid >> 8, gtid = tid & 255, gwid = wid & 3;
@@ -819,7 +837,9 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
   int tm, tn;
   grouped_tile(tile, ntiles / tiles_n, tiles_n, 8, tm, tn);
   const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
-  const int nk = (int)((K + BK - 1) / BK);
+  const int ktiles = (int)((K + BK - 1) / BK);
+  const int kt0 = blockIdx.y * ktiles_per_split;
+  const int nk = min(ktiles, kt0 + ktiles_per_split);  // K-tile loop bound (exclusive)
 
   typename LA::State sa0, sa1;
   typename LB::State sb0, sb1;
@@ -848,23 +868,23 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
   const int a_off = wr * W_HALF, b_off = 2 * W_HALF + (wc >> 1) * W_HALF, b_row = (wc & 1) * 64;
   auto rd_a = [&](const char* st, int qa, int kk, mfma_bf16x8 (&f)[4]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) f[i] = read_frag<true, 128>(st + a_off, 64 * qa + 16 * i, kk, lane);
+    for (int i = 0; i < 4; ++i) f[i] = wide_frag<LA>(st + a_off, 64 * qa + 16 * i, kk, lane);
   };
   auto rd_b = [&](const char* st, int qb, int kk, mfma_bf16x8 (&f)[2]) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) f[j] = read_frag<true, 128>(st + b_off, b_row + 32 * qb + 16 * j, kk, lane);
+    for (int j = 0; j < 2; ++j) f[j] = wide_frag<LB>(st + b_off, b_row + 32 * qb + 16 * j, kk, lane);
   };
 
   mfma_bf16x8 fa0[4], fa1[4], fb0[2], fb1[2];
-  if (nk > 0) {
-    issue_a(0);
-    issue_b(0);
+  if (kt0 < nk) {
+    issue_a(kt0);
+    issue_b(kt0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    rd_a(smem, 0, 0, fa0);
-    rd_b(smem, 0, 0, fb0);
+    rd_a(smem + (kt0 & 1) * W_STAGE, 0, 0, fa0);
+    rd_b(smem + (kt0 & 1) * W_STAGE, 0, 0, fb0);
   }
-  for (int t = 0; t < nk; ++t) {
+  for (int t = kt0; t < nk; ++t) {
     const char* cs = smem + (t & 1) * W_STAGE;
     const bool more = t + 1 < nk;
     // k 0..31
@@ -895,6 +915,42 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
     wide_mma<0, 1, VAR>(acc, fa1, fb1);
   }
   __syncthreads();  // every wave is done with the operand stages before they become the staging tile
+
+  if (epi.slab || epi.c_f32) {
+    // fp32 output (split-K slab partials or an fp32 C): 16-B stores straight from the accumulators
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t m = m0 + wr * 128 + 16 * i + (lane & 15);
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
+        if (n >= N) continue;
+        f32x4 v = acc[i][j];
+        if (epi.slab) {
+          *reinterpret_cast<f32x4*>(epi.slab + (int64_t)blockIdx.y * M * N + m * N + n) = v;
+          continue;
+        }
+        const int64_t crow = epi_row(epi, m);
+        if (epi.bias) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
+        }
+        if (epi.relu) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+        }
+        if (epi.addend) {
+          const u16x4 a = *reinterpret_cast<const u16x4*>(epi.addend + crow * epi.ldc + n);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += bf2f(a[q]);
+        }
+        *reinterpret_cast<f32x4*>((float*)epi.C + crow * epi.ldc + n) = v;
+      }
+    }
+    return;
+  }
 
   // epilogue (bf16 output): bias / relu in registers, stage through LDS, coalesced 16-B row stores
   bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
@@ -1166,10 +1222,43 @@ bool use_wide(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) {
   return wide_pays(M, N);
 }
 
+// Split-K GEMMs (conv wgrad: small M x N, huge K).  The wide tile pays when it wastes little of
+// M x N: compare useful-work fractions, the wide kernel's at its measured ~1.35x per-CU advantage
+// (more for wgrad, whose MN-major operands need two ds_read_b64_tr per fragment — the wide tile's
+// 128 x 64 wave tile halves those reads per MFMA).  One 512-thread workgroup per CU means ~2x the
+// narrow plan's splits; the fp32 slabs are capped at 96 MB (the 128-tile plan's 48 MB cap starved
+// the wide launches of workgroups: 108 of 256 CUs on the 7x7 512->512 3x3 wgrad).
+int wide_split_count(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int ktiles = (int)((K + BK - 1) / BK);
+  int s = (int)(256 / tiles);  // floor: a 257th workgroup would start a second round on one CU
+  const int max_s = ktiles / 4 > 1 ? ktiles / 4 : 1;
+  int64_t cap = ((int64_t)96 << 20) / (M * N * 4);
+  if (cap < 4) cap = 4;
+  if (s > max_s) s = max_s;
+  if (s > cap) s = (int)cap;
+  return s < 1 ? 1 : s;
+}
+
+// Returns the wide split count (0: keep the 128-tile plan).
+int wide_splits(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) {
+  const int mode = wide_mode();
+  if (mode == 0 || p.splits <= 1 || epi.stats || K < 64) return 0;
+  if (mode == 1) {
+    if (M < 256 || N < 256) return 0;
+    const double useful = (double)M * N;
+    const double w = 1.35 * useful / ((double)((M + 255) / 256 * 256) * (double)((N + 255) / 256 * 256));
+    const double n = useful / ((double)((M + p.bm - 1) / p.bm * p.bm) * (double)((N + p.bn - 1) / p.bn * p.bn));
+    if (w < 1.05 * n) return 0;
+  }
+  return wide_split_count(M, N, K);
+}
+
 int g_wide_variant = 3;  // setprio + MFMA/ds_read interleave: best or tied on every measured shape
 
 template <class LA, class LB, int VAR>
-hipError_t launch_wide_v(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st) {
+hipError_t launch_wide_v(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, int splits,
+                         hipStream_t st) {
   static bool attr = [] {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_wide_kernel<LA, LB, VAR>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, W_LDS);
@@ -1178,25 +1267,47 @@ hipError_t launch_wide_v(const LA& la, const LB& lb, int64_t M, int64_t N, int64
   (void)attr;
   const int tiles_n = (int)((N + 255) / 256);
   const int ntiles = (int)((M + 255) / 256) * tiles_n;
-  gemm_wide_kernel<LA, LB, VAR><<<ntiles, W_NT, W_LDS, st>>>(la, lb, M, N, K, tiles_n, epi);
+  const int ktiles = (int)((K + BK - 1) / BK);
+  const int kps = splits > 1 ? (ktiles + splits - 1) / splits : (ktiles > 0 ? ktiles : 1);
+  gemm_wide_kernel<LA, LB, VAR><<<dim3(ntiles, splits), W_NT, W_LDS, st>>>(la, lb, M, N, K, tiles_n, kps, epi);
   return hipGetLastError();
 }
 
+// splits > 1: epi.slab receives [splits][M][N] fp32 partials, reduced (with the caller's epilogue)
+// by splitk_reduce_kernel; the effective split count is recomputed from the per-split K tiles.
 template <class LA, class LB>
-hipError_t launch_wide(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st) {
-  switch (g_wide_variant) {
-    case 1: return launch_wide_v<LA, LB, 1>(la, lb, M, N, K, epi, st);
-    case 2: return launch_wide_v<LA, LB, 2>(la, lb, M, N, K, epi, st);
-    case 3: return launch_wide_v<LA, LB, 3>(la, lb, M, N, K, epi, st);
-    default: return launch_wide_v<LA, LB, 0>(la, lb, M, N, K, epi, st);
+hipError_t launch_wide(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st,
+                       int splits = 1, float* slab = nullptr) {
+  Epi e = epi;
+  if (splits > 1) {
+    const int ktiles = (int)((K + BK - 1) / BK);
+    const int kps = (ktiles + splits - 1) / splits;
+    splits = (ktiles + kps - 1) / kps;
   }
+  if (splits > 1) e.slab = slab;
+  hipError_t r;
+  switch (g_wide_variant) {
+    case 1: r = launch_wide_v<LA, LB, 1>(la, lb, M, N, K, e, splits, st); break;
+    case 2: r = launch_wide_v<LA, LB, 2>(la, lb, M, N, K, e, splits, st); break;
+    case 3: r = launch_wide_v<LA, LB, 3>(la, lb, M, N, K, e, splits, st); break;
+    default: r = launch_wide_v<LA, LB, 0>(la, lb, M, N, K, e, splits, st); break;
+  }
+  if (r != hipSuccess || splits <= 1) return r;
+  int ll = 0;
+  while (ll < 4 && (splits >> ll) > 16) ++ll;
+  const int64_t per_block = 256 >> ll;
+  const int64_t g = (M * N / 4 + per_block - 1) / per_block;
+  splitk_reduce_kernel<<<(unsigned)g, 256, 0, st>>>(slab, splits, M, N, ll, epi);
+  return hipGetLastError();
 }
 
 template <template <int> class TA, template <int> class TB, class MakeA, class MakeB>
 hipError_t dispatch_bn(int64_t M, int64_t N, int64_t K, const Plan& p, Epi epi, float* slab, hipStream_t st,
                        MakeA make_a, MakeB make_b) {
-  if constexpr (TA<64>::kMajor && TB<64>::kMajor) {
-    if (use_wide(M, N, K, p, epi)) return launch_wide(make_a(TA<64>{}), make_b(TB<64>{}), M, N, K, epi, st);
+  if (use_wide(M, N, K, p, epi)) return launch_wide(make_a(TA<64>{}), make_b(TB<64>{}), M, N, K, epi, st);
+  if (slab) {
+    const int ws = wide_splits(M, N, K, p, epi);
+    if (ws > 0) return launch_wide(make_a(TA<64>{}), make_b(TB<64>{}), M, N, K, epi, st, ws, slab);
   }
   if constexpr (TA<128>::kMajor && TB<64>::kMajor) {
     if (use_big(M, N, K, p, epi)) return launch_big(make_a(TA<128>{}), make_b(TB<64>{}), M, N, K, epi, st);
@@ -1230,9 +1341,17 @@ void set_gemm_paths(int wide, int variant) {
   if (variant >= 0) g_wide_variant = variant;
 }
 
+// slab sizing covers both the 128-tile plan and the wide tile's (possibly deeper) split
+int64_t split_slab_floats(int64_t M, int64_t N, int64_t K, const Plan& p) {
+  if (p.splits <= 1) return 0;
+  int s = p.splits;
+  const int w = wide_split_count(M, N, K);
+  if (w > s) s = w;
+  return (int64_t)s * M * N;
+}
+
 int64_t gemm_slab_floats(int64_t M, int64_t N, int64_t K, bool allow_split) {
-  Plan p = plan_gemm(M, N, K, allow_split, 512);
-  return p.splits > 1 ? (int64_t)p.splits * M * N : 0;
+  return split_slab_floats(M, N, K, plan_gemm(M, N, K, allow_split, 512));
 }
 
 // C[M,N] = A[M,K] * B[K,N].  a_kmajor: A(m,k)=A[m*lda+k] else A[k*lda+m];
@@ -1255,8 +1374,7 @@ hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* 
 int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, int S, int P, int Q) {
   if (mode != 2) return 0;  // only wgrad splits K
   const int64_t M = Cout, Nn = (int64_t)R * S * C, K = (int64_t)N * P * Q;
-  Plan p = plan_wgrad(M, Nn, K, true);
-  return p.splits > 1 ? (int64_t)p.splits * M * Nn : 0;
+  return split_slab_floats(M, Nn, K, plan_wgrad(M, Nn, K, true));
 }
 
 // y[N,P,Q,Cout] = conv(x[N,H,W,C], w[Cout,R,S,C]) (+bias, relu)

@@ -1,0 +1,16 @@
+#!/bin/bash
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > gpurun_out/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -1 gpurun_out/$name.log
+  if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
+}
+step pytest_kern 300 python -u -m pytest tests/test_kernels_gpu.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+PDA_GEMM_STAGES=2 step conv_s2 300 python tools/bench_conv.py
+PDA_GEMM_STAGES=3 step conv_s3 300 python tools/bench_conv.py
+PDA_GEMM_STAGES=2 step bench_s2 300 python bench.py --steps 20 --warmup 5
+PDA_GEMM_STAGES=3 step bench_s3 300 python bench.py --steps 20 --warmup 5

@@ -89,7 +89,7 @@ def test_gemm_wide_tile_path(M, N, K, force_wide):
 @pytest.mark.parametrize("case", [(4, 15, 15, 64, 256, 3, 1, 1), (4, 14, 14, 256, 512, 3, 2, 1),
                                   (3, 9, 9, 512, 272, 1, 1, 0)])
 def test_conv_wide_tile_path(case, force_wide):
-    """Conv fwd and (phased, row-remapped, addend-fused) dgrad through the wide-tile kernel."""
+    """Conv fwd, (phased, row-remapped, addend-fused) dgrad and split-K wgrad through the wide tile."""
     N, H, W, Cin, Cout, k, s, p = case
     torch.manual_seed(6)
     x = torch.randn(N, H, W, Cin).to(torch.bfloat16).float().requires_grad_()
@@ -102,6 +102,28 @@ def test_conv_wide_tile_path(case, force_wide):
     add = torch.randn(N, H, W, Cin).to(torch.bfloat16)
     dx = C().conv_dgrad(bf(dy), bf(w.detach()), H, W, s, p, 1, add.to(DEV))
     assert rel_err(dx.cpu(), x.grad + add.float()) < 1e-2
+    # wgrad: MN-major operands (dy^T, im2col(x)^T) with split-K slabs through the wide tile
+    dw = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, 1, True, None)
+    assert rel_err(dw.cpu(), w.grad) < 1e-3
+    dwb = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, 1, False, None)
+    assert rel_err(dwb.cpu(), w.grad) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K,split", [(320, 384, 8192, True), (264, 512, 4160, True), (512, 256, 64, False),
+                                         (776, 264, 1032, False)])
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm_wide_layouts(M, N, K, split, ak, bk, force_wide):
+    """Wide tile with every operand major-ness (MN-major halves read with ds_read_b64_tr), fp32
+    output, and split-K fp32 slabs + reduction when ``split``."""
+    torch.manual_seed(9)
+    A = torch.randn(M, K)
+    B = torch.randn(K, N)
+    a_store = bf(A) if ak else bf(A.t().contiguous())
+    b_store = bf(B.t().contiguous()) if bk else bf(B)
+    out = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    C().gemm(a_store, ak, K if ak else M, b_store, bk, K if bk else N, out, N, M, N, K, None, False, split)
+    ref = A.to(torch.bfloat16).float() @ B.to(torch.bfloat16).float()
+    assert rel_err(out.cpu(), ref) < 1e-5
 
 
 def test_gemm_bias_relu_bf16_out():
