@@ -1,8 +1,9 @@
 """BASELINE config 5: GPT-2-XL pipeline-parallel 4 stages x DDP 2 (RCCL send/recv micro-batches).
 
     python -m torch.distributed.run --nproc-per-node 8 -m pytorchdistributed_amd.bench.gpt2xl_pp --gpus 8
-World = pp x dp (default pp = min(4, world)); 1F1B schedule; per-stage gradient averaging over the DP
-group after the pipeline flush; fused AdamW per stage.
+World = pp x dp (default pp = min(4, world)); 1F1B schedule (``--schedule interleaved --chunks v``: v
+model chunks per rank, virtual stage c*pp + stage); per-stage gradient averaging over the DP group after
+the pipeline flush; fused AdamW per stage.
 """
 from __future__ import annotations
 
@@ -27,7 +28,8 @@ def main(argv=None):
     ap.add_argument("--micro", type=int, default=8, help="micro-batches per step")
     ap.add_argument("--micro-batch", type=int, default=4)
     ap.add_argument("--seq", type=int, default=1024)
-    ap.add_argument("--schedule", default="1f1b")
+    ap.add_argument("--schedule", default="1f1b", choices=["gpipe", "1f1b", "interleaved"])
+    ap.add_argument("--chunks", type=int, default=2, help="model chunks per rank (interleaved)")
     ap.add_argument("--layers", type=int, default=None)
     a = ap.parse_args(argv)
     rank, world, local, device = setup(a.gpus)
@@ -39,12 +41,21 @@ def main(argv=None):
     else:
         pp_group = dp_group = None
         stage, dp_rank, ranks = 0, 0, [0]
-    lo, hi = partition_layers(cfg.n_layer, pp)[stage]
     torch.manual_seed(stage)
-    mod = GPT2Stage(cfg, lo, hi, stage == 0, stage == pp - 1, device=device, dtype=torch.bfloat16)
+    if a.schedule == "interleaved":
+        v = a.chunks
+        parts = partition_layers(cfg.n_layer, pp * v)
+        chunks = [GPT2Stage(cfg, *parts[c * pp + stage], c * pp + stage == 0, c * pp + stage == pp * v - 1,
+                            device=device, dtype=torch.bfloat16) for c in range(v)]
+        mod = torch.nn.ModuleList(chunks)
+        pipe = Pipeline(chunks, ranks, a.micro, schedule="interleaved",
+                        loss_fn=chunks[-1].loss if stage == pp - 1 else None, group=pp_group, device=device)
+    else:
+        lo, hi = partition_layers(cfg.n_layer, pp)[stage]
+        mod = GPT2Stage(cfg, lo, hi, stage == 0, stage == pp - 1, device=device, dtype=torch.bfloat16)
+        pipe = Pipeline(mod, ranks, a.micro, schedule=a.schedule, loss_fn=mod.loss if stage == pp - 1 else None,
+                        group=pp_group, device=device)
     opt = AdamW(mod.parameters(), lr=1e-4, weight_decay=0.1)
-    pipe = Pipeline(mod, ranks, a.micro, schedule=a.schedule, loss_fn=mod.loss if stage == pp - 1 else None,
-                    group=pp_group, device=device)
     data = DeviceSyntheticTokens(a.micro * a.micro_batch, a.seq, cfg.vocab_size, device=device, rank=dp_rank)
 
     def step():
@@ -61,7 +72,8 @@ def main(argv=None):
           "ms_per_step": round(secs / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
           "vs_baseline": None, "dtype": "bf16", "data": "synthetic tokens (on-device), random-init weights",
           "config": {"model": a.model, "global_batch": a.micro * a.micro_batch * dp, "seq_len": a.seq,
-                     "parallelism": f"pp{pp}xdp{dp}", "schedule": a.schedule, "microbatches": a.micro}}, rank)
+                     "parallelism": f"pp{pp}xdp{dp}", "schedule": a.schedule, "microbatches": a.micro,
+                     **({"chunks": a.chunks} if a.schedule == "interleaved" else {})}}, rank)
     teardown()
 
 

@@ -8,7 +8,10 @@ xGMI).  Schedules:
 * ``gpipe`` — all forwards, then all backwards (fill-drain);
 * ``1f1b``  — PipeDream-flush: ``S - s - 1`` warm-up forwards, then one-forward-one-backward, then the
   cool-down backwards; peak activation memory is bounded by the stage depth instead of the number of
-  micro-batches.
+  micro-batches;
+* ``interleaved`` — virtual-pipeline 1F1B: each rank holds ``v`` model chunks (virtual stages
+  ``c * S + s``), which divides the fill/drain bubble by ``v``; executed from a tick plan computed
+  identically on every rank (:func:`plan_interleaved`) with one batched P2P group per tick.
 
 In the 1F1B steady state a stage's "send activation to s+1" and "receive gradient from s+1" are issued
 as ONE batched P2P group (likewise "send gradient to s-1" + "receive next activation from s-1"), so two
@@ -47,6 +50,77 @@ def schedule_1f1b(num_stages: int, num_micro: int, stage: int) -> List[Tuple[str
 
 
 SCHEDULES = {"gpipe": schedule_gpipe, "1f1b": schedule_1f1b}
+
+
+def schedule_interleaved(num_stages: int, num_micro: int, stage: int, chunks: int) -> List[Tuple[str, int, int]]:
+    """Interleaved 1F1B (virtual pipeline, `NB03` raw lines 699-705): rank ``stage`` holds ``chunks``
+    model chunks; chunk ``c`` is virtual stage ``c * num_stages + stage``.  Units are
+    ``(kind, chunk, micro_batch)``.  Micro-batches advance in groups of ``num_stages`` through the
+    chunks (forward chunk 0 -> v-1, backward v-1 -> 0); each rank runs
+    ``2 (S - s - 1) + (v - 1) S`` warm-up forwards, then one-forward-one-backward, then the cool-down
+    backwards.  The bubble shrinks by ``v`` versus 1F1B at the cost of ``v`` times more P2P."""
+    S, M, v = num_stages, num_micro, chunks
+    if M % S:
+        raise ValueError(f"interleaved schedule needs num_microbatches ({M}) divisible by stages ({S})")
+    total = M * v
+
+    def unit(k, backward):
+        c = (k // S) % v
+        mb = (k // (S * v)) * S + k % S
+        return ("B" if backward else "F", v - 1 - c if backward else c, mb)
+
+    warm = min(2 * (S - stage - 1) + (v - 1) * S, total)
+    out = [unit(k, False) for k in range(warm)]
+    for j in range(total - warm):
+        out.append(unit(warm + j, False))
+        out.append(unit(j, True))
+    out += [unit(k, True) for k in range(total - warm, total)]
+    return out
+
+
+def plan_interleaved(num_stages: int, num_micro: int, chunks: int):
+    """Deterministic tick plan shared by every rank: per tick, the unit each rank runs (or None) and
+    the transfers delivered at the end of that tick, as ``(src_rank, dst_rank, kind, vstage, mb)``
+    (``kind`` "F": output of virtual stage ``vstage`` to ``vstage + 1``; "B": input gradient of
+    ``vstage`` to ``vstage - 1``).  Each tick's transfers are exchanged as ONE batched P2P group on
+    both ends, so opposite-direction and wrap-around (last rank -> rank 0) traffic cannot deadlock.
+    Raises if the unit lists cannot complete."""
+    S, v = num_stages, chunks
+    G = S * v
+    units = [schedule_interleaved(S, num_micro, s, v) for s in range(S)]
+    pos = [0] * S
+    avail = [set() for _ in range(S)]  # ("F"|"B", chunk, mb) inputs that arrived at each rank
+    fdone = [set() for _ in range(S)]
+    ticks = []
+    while any(pos[s] < len(units[s]) for s in range(S)):
+        run: List[Optional[Tuple[str, int, int]]] = [None] * S
+        xfers = []
+        for s in range(S):
+            if pos[s] >= len(units[s]):
+                continue
+            kind, c, mb = units[s][pos[s]]
+            g = c * S + s
+            if kind == "F":
+                ready = g == 0 or ("F", c, mb) in avail[s]
+            else:
+                ready = (c, mb) in fdone[s] and (g == G - 1 or ("B", c, mb) in avail[s])
+            if not ready:
+                continue
+            run[s] = (kind, c, mb)
+            pos[s] += 1
+            if kind == "F":
+                fdone[s].add((c, mb))
+                if g + 1 < G:
+                    xfers.append((s, (g + 1) % S, "F", g, mb))
+            elif g > 0:
+                xfers.append((s, (g - 1) % S, "B", g, mb))
+        if all(r is None for r in run):
+            raise RuntimeError("interleaved schedule cannot make progress")
+        for src, dst, kind, g, mb in xfers:
+            tgt = g + 1 if kind == "F" else g - 1
+            avail[dst].add((kind, tgt // S, mb))
+        ticks.append((run, xfers))
+    return ticks
 
 
 def check_schedule(fn, num_stages: int, num_micro: int) -> bool:
@@ -137,10 +211,15 @@ class Pipeline:
     ``loss_fn(output, target)`` is applied on the last stage per micro-batch.
     """
 
-    def __init__(self, stage_module: tnn.Module, ranks: Sequence[int], num_microbatches: int,
+    def __init__(self, stage_module, ranks: Sequence[int], num_microbatches: int,
                  schedule: str = "1f1b", loss_fn: Optional[Callable] = None, recompute: bool = False,
                  group=None, device=None):
-        self.module = stage_module
+        # schedule="interleaved": ``stage_module`` is the list of this rank's model chunks (chunk c =
+        # virtual stage c * len(ranks) + stage)
+        self.chunks = list(stage_module) if isinstance(stage_module, (list, tuple, tnn.ModuleList)) else None
+        if (schedule == "interleaved") != (self.chunks is not None):
+            raise ValueError("schedule='interleaved' takes a list of model chunks (and only it does)")
+        self.module = tnn.ModuleList(self.chunks) if self.chunks is not None else stage_module
         self.ranks = list(ranks)
         self.S = len(self.ranks)
         self.rank = pdist.get_rank()
@@ -199,9 +278,112 @@ class Pipeline:
             return checkpoint(self.module, x, use_reentrant=False)
         return self.module(x)
 
+    def _step_interleaved(self, inputs, targets):
+        S, M, v = self.S, self.M, len(self.chunks)
+        G = S * v
+        first = self.is_first  # rank 0 holds virtual stage 0 (chunk 0)
+        last = self.is_last    # rank S-1 holds virtual stage G-1 (chunk v-1)
+        in_mb = list(inputs.chunk(M)) if (first and inputs is not None) else [None] * M
+        tg_mb = list(targets.chunk(M)) if (last and targets is not None) else [None] * M
+        if not hasattr(self, "_plan") or self._plan_key != (S, M, v):
+            self._plan, self._plan_key = plan_interleaved(S, M, v), (S, M, v)
+            self._vmeta = {}  # virtual stage g -> (shape, dtype) of its output (known to g and g+1)
+        acts_in, acts_out, inbox = {}, {}, {}
+        losses = []
+
+        def fwd(c, x):
+            m = self.chunks[c]
+            if self.recompute and torch.is_grad_enabled():
+                return checkpoint(m, x, use_reentrant=False)
+            return m(x)
+
+        for run, xfers in self._plan:
+            out_t = {}
+            if run[self.stage] is not None:
+                kind, c, mb = run[self.stage]
+                g = c * S + self.stage
+                if kind == "F":
+                    x = in_mb[mb].to(self.device) if g == 0 else inbox.pop(("F", c, mb))
+                    if g > 0:
+                        x.requires_grad_()
+                    acts_in[(c, mb)] = x
+                    y = fwd(c, x)
+                    if g == G - 1:
+                        loss = self.loss_fn(y, tg_mb[mb].to(self.device)) / M if self.loss_fn else y.float().mean() / M
+                        losses.append(loss.detach())
+                        acts_out[(c, mb)] = loss
+                    else:
+                        acts_out[(c, mb)] = y
+                        self._vmeta[g] = (tuple(y.shape), y.dtype)
+                        out_t[("F", g, mb)] = y.detach()
+                else:
+                    out = acts_out.pop((c, mb))
+                    if g == G - 1:
+                        out.backward()
+                    else:
+                        torch.autograd.backward(out, inbox.pop(("B", c, mb)))
+                    x = acts_in.pop((c, mb))
+                    if g > 0:
+                        out_t[("B", g, mb)] = x.grad
+            # this tick's transfers: first-time forward shapes, then one batched group of tensors
+            mine = [t for t in xfers if self.stage in (t[0], t[1])]
+            meta_ops, meta_in, ops, local = [], [], [], []
+            for src, dst, kind, g, mb in mine:
+                tgt = g + 1 if kind == "F" else g - 1
+                key = (kind, tgt // S, mb)
+                if src == dst:  # S == 1: hand over within the rank
+                    local.append((key, out_t[(kind, g, mb)]))
+                    continue
+                if src == self.stage:
+                    t = out_t[(kind, g, mb)].contiguous()
+                    if kind == "F" and ("sent", g) not in self._vmeta:
+                        self._vmeta[("sent", g)] = True
+                        meta_ops.append(dist.P2POp(dist.isend, self._meta_tensor(t), self.ranks[dst], group=self.group))
+                    ops.append(dist.P2POp(dist.isend, t, self.ranks[dst], group=self.group))
+                else:
+                    if kind == "F" and g not in self._vmeta:
+                        mt = torch.zeros(10, dtype=torch.long, device=self.device)
+                        meta_ops.append(dist.P2POp(dist.irecv, mt, self.ranks[src], group=self.group))
+                        meta_in.append((g, mt))
+                    # shape of what arrives: virtual stage g's output (F) or input (B, = output of tgt)
+                    ops.append((key, src, g if kind == "F" else tgt))
+            if meta_ops:
+                for r in dist.batch_isend_irecv(meta_ops):
+                    r.wait()
+                for g, mt in meta_in:
+                    nd = int(mt[0])
+                    self._vmeta[g] = (tuple(int(q) for q in mt[2: 2 + nd]),
+                                      [torch.float32, torch.bfloat16, torch.float16][int(mt[1])])
+            p2p, recvd = [], []
+            for op in ops:
+                if isinstance(op, tuple):
+                    key, src, mg = op
+                    buf = self._empty(self._vmeta[mg])
+                    p2p.append(dist.P2POp(dist.irecv, buf, self.ranks[src], group=self.group))
+                    recvd.append((key, buf))
+                else:
+                    p2p.append(op)
+            if p2p:
+                for r in dist.batch_isend_irecv(p2p):
+                    r.wait()
+            for key, buf in recvd + local:
+                inbox[key] = buf
+        if last:
+            return torch.stack(losses).sum()
+        return None
+
+    def _meta_tensor(self, t: torch.Tensor) -> torch.Tensor:
+        meta = torch.zeros(10, dtype=torch.long, device=self.device)
+        meta[0] = t.dim()
+        meta[1] = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[t.dtype]
+        meta[2: 2 + t.dim()] = torch.tensor(t.shape, dtype=torch.long)
+        return meta
+
     def step(self, inputs: Optional[torch.Tensor] = None, targets: Optional[torch.Tensor] = None):
         """Run one optimisation step's forward+backward over ``num_microbatches``; returns the mean loss
         on the last stage (None elsewhere).  Gradients accumulate into the stage parameters."""
+        if self.schedule_name == "interleaved":
+            return self._step_interleaved(inputs, targets)
         M = self.M
         in_mb = list(inputs.chunk(M)) if (self.is_first and inputs is not None) else [None] * M
         tg_mb = list(targets.chunk(M)) if (self.is_last and targets is not None) else [None] * M

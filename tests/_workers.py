@@ -121,6 +121,31 @@ def pipeline_worker(rank, world, pp, dp, schedule, recompute, outdir):
     pd.destroy_process_group()
 
 
+def pipeline_interleaved_worker(rank, world, chunks, n_layers, n_micro, recompute, outdir):
+    """Interleaved 1F1B on gloo: rank s holds layers c*world + s (c < chunks) of an n_layers stack."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.pipeline import Pipeline
+
+    pd.init_process_group("gloo")
+    full = _tiny_stack(n_layers)
+    blocks = [full[3 * i: 3 * i + 3] for i in range(n_layers)]
+    per = n_layers // (world * chunks)  # layers per virtual stage
+    mine = [torch.nn.Sequential(*[m for b in blocks[(c * world + rank) * per:(c * world + rank + 1) * per] for m in b])
+            for c in range(chunks)]
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(n_micro * 2, 16, generator=g)
+    Y = torch.randn(n_micro * 2, 16, generator=g)
+    pipe = Pipeline(mine, list(range(world)), num_microbatches=n_micro, schedule="interleaved", loss_fn=F.mse_loss,
+                    recompute=recompute, device=torch.device("cpu"))
+    loss = pipe.step(X, Y)
+    out = {"loss": loss, "grads": {}}
+    for c, m in enumerate(mine):
+        for n, p in m.named_parameters():
+            out["grads"][f"{c}.{n}"] = p.grad.clone()
+    torch.save(out, os.path.join(outdir, f"{rank}.pt"))
+    pd.destroy_process_group()
+
+
 class _Block(torch.nn.Module):
     def __init__(self, d=16):
         super().__init__()

@@ -6,8 +6,8 @@ import torch.nn.functional as F
 
 import _workers
 from pytorchdistributed_amd.launch import spawn
-from pytorchdistributed_amd.parallel.pipeline import (check_schedule, partition_layers, schedule_1f1b,
-                                                      schedule_gpipe)
+from pytorchdistributed_amd.parallel.pipeline import (check_schedule, partition_layers, plan_interleaved,
+                                                      schedule_1f1b, schedule_gpipe, schedule_interleaved)
 
 
 @pytest.mark.parametrize("S", [1, 2, 3, 4, 8])
@@ -64,3 +64,55 @@ def test_pipeline_grads_match_single_process(tmp_path, pp, dp, schedule, recompu
         ref_stage = torch.nn.Sequential(*ref_blocks[lo:hi])
         for (n, p) in ref_stage.named_parameters():
             assert torch.allclose(d["grads"][n], p.grad, atol=1e-5, rtol=1e-4), (r, n)
+
+
+@pytest.mark.parametrize("S", [1, 2, 3, 4])
+@pytest.mark.parametrize("v", [1, 2, 3])
+@pytest.mark.parametrize("k", [1, 2, 4])
+def test_interleaved_schedule_well_formed(S, v, k):
+    M = k * S
+    for s in range(S):
+        acts = schedule_interleaved(S, M, s, v)
+        units = {(c, mb) for c in range(v) for mb in range(M)}
+        assert sorted((c, mb) for kind, c, mb in acts if kind == "F") == sorted(units)
+        assert sorted((c, mb) for kind, c, mb in acts if kind == "B") == sorted(units)
+        for c, mb in units:
+            assert acts.index(("F", c, mb)) < acts.index(("B", c, mb))
+    ticks = plan_interleaved(S, M, v)  # raises if the ranks' unit lists deadlock
+    # the fill/drain bubble (ticks beyond the 2*M*v units of work) shrinks with v in stage-time units
+    assert len(ticks) - 2 * M * v <= 2 * (S - 1) + (v - 1) * S + 2 * S
+
+
+def test_interleaved_bubble_shrinks_with_chunks():
+    S, M = 4, 16
+    stage_time = {v: len(plan_interleaved(S, M, v)) / v for v in (1, 2, 4)}
+    assert stage_time[4] < stage_time[2] < stage_time[1]
+
+
+def test_interleaved_needs_divisible_microbatches():
+    with pytest.raises(ValueError):
+        schedule_interleaved(4, 6, 0, 2)
+
+
+@pytest.mark.parametrize("world,chunks,n_layers,n_micro,recompute", [(2, 2, 4, 4, False), (2, 2, 8, 2, True),
+                                                                     (4, 2, 8, 4, False), (1, 3, 3, 2, False)])
+def test_interleaved_pipeline_grads_match_single_process(tmp_path, world, chunks, n_layers, n_micro, recompute):
+    spawn(_workers.pipeline_interleaved_worker, args=(world, chunks, n_layers, n_micro, recompute, str(tmp_path)),
+          nprocs=world, timeout=180)
+    full = _workers._tiny_stack(n_layers)
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(n_micro * 2, 16, generator=g)
+    Y = torch.randn(n_micro * 2, 16, generator=g)
+    loss = F.mse_loss(full(X), Y)
+    loss.backward()
+    per = n_layers // (world * chunks)
+    blocks = [full[3 * i: 3 * i + 3] for i in range(n_layers)]
+    for r in range(world):
+        d = torch.load(tmp_path / f"{r}.pt", weights_only=True)
+        if r == world - 1:
+            assert torch.allclose(d["loss"], loss.detach(), atol=1e-6)
+        for c in range(chunks):
+            vs = c * world + r
+            ref = torch.nn.Sequential(*[m for b in blocks[vs * per:(vs + 1) * per] for m in b])
+            for n, p in ref.named_parameters():
+                assert torch.allclose(d["grads"][f"{c}.{n}"], p.grad, atol=1e-5, rtol=1e-4), (r, c, n)
