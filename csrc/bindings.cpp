@@ -327,6 +327,19 @@ std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
   return {y, idx};
 }
 
+// x [N,H,W,Cx] bf16 (first c channels used) -> [N, ceil((H+2pad)/2), ceil((W+2pad)/2), 16]
+Tensor stem_s2d(Tensor x, int64_t c, int64_t pad) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "x must be a contiguous [N,H,W,C] tensor");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), Cx = x.size(3);
+  TORCH_CHECK(c >= 1 && c <= Cx && 4 * c <= 16, "stem_s2d: 1 <= c <= min(Cx, 4)");
+  const int U = (H + 2 * pad + 1) / 2, V = (W + 2 * pad + 1) / 2;
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty({N, U, V, 16}, x.options());
+  CHECK_HIP_OK(pda::stem_space_to_depth(bp(x), bpm(y), N, H, W, Cx, (int)c, U, V, (int)pad, stream_of(x)));
+  return y;
+}
+
 Tensor maxpool_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64_t s, int64_t pad) {
   check_bf16(dy, "dy");
   check_gpu(idx, "idx");
@@ -853,6 +866,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_bwd", &bn_bwd);
   m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("stem_s2d", &stem_s2d);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);

@@ -105,6 +105,9 @@ hipError_t maxpool2d_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H,
                          int s, int pad, hipStream_t st);
 hipError_t maxpool2d_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C, int P, int Q,
                          int k, int s, int pad, hipStream_t st);
+// stem space-to-depth: y[N, U, V, 16] from x[N, H, W, Cx] (first C <= 4 channels), 2x2 blocks, pad
+hipError_t stem_space_to_depth(const bf16_t* x, bf16_t* y, int N, int H, int W, int Cx, int C, int U, int V, int pad,
+                               hipStream_t st);
 hipError_t avgpool_global_fwd(const bf16_t* x, void* y, bool y_bf16, int N, int HW, int C, hipStream_t st);
 hipError_t avgpool_global_bwd(const void* dy, bool dy_bf16, bf16_t* dx, int N, int HW, int C, hipStream_t st);
 

@@ -175,4 +175,54 @@ hipError_t avgpool_global_bwd(const void* dy, bool dy_bf16, bf16_t* dx, int N, i
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------------ stem space-to-depth
+// y[n, u, v, (i*2 + j)*C + c] = x[n, 2u + i - pad, 2v + j - pad, c] (0 outside), channels padded with
+// zeros to Cy (16): the 7x7/2 stem conv becomes a 4x4/1 conv with 16-B channel vectors (see
+// models/resnet.py:space_to_depth_stem).  One thread per output pixel: 4 x C input loads (x's pixel
+// stride Cx may exceed C — device-side channel padding is skipped), two 16-B stores.
+__global__ void __launch_bounds__(256) stem_s2d_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y, int N,
+                                                       int H, int W, int Cx, int C, int U, int V, int pad) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)N * U * V;
+  if (t >= total) return;
+  const int v = (int)(t % V);
+  const int64_t r = t / V;
+  const int u = (int)(r % U);
+  const int n = (int)(r / U);
+  u16x8 o0, o1;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) o0[q] = o1[q] = 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int h = 2 * u + i - pad, w = 2 * v + j - pad;
+      if ((unsigned)h >= (unsigned)H || (unsigned)w >= (unsigned)W) continue;
+      const bf16_t* px = x + (((int64_t)n * H + h) * W + w) * Cx;
+      // slot (i, j, c) = (i*2 + j)*C + c; unrolled over c < 4 so every vector index is a constant
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c >= C) break;
+        const bf16_t val = px[c];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          if (k != (i * 2 + j) * C + c) continue;
+          if (k < 8) o0[k] = val;
+          else o1[k - 8] = val;
+        }
+      }
+    }
+  u16x8* dst = reinterpret_cast<u16x8*>(y + t * 16);
+  dst[0] = o0;
+  dst[1] = o1;
+}
+
+hipError_t stem_space_to_depth(const bf16_t* x, bf16_t* y, int N, int H, int W, int Cx, int C, int U, int V, int pad,
+                               hipStream_t st) {
+  if (C < 1 || 4 * C > 16) return hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * U * V;
+  stem_s2d_kernel<<<(unsigned)((total + 255) / 256), 256, 0, st>>>(x, y, N, H, W, Cx, C, U, V, pad);
+  return hipGetLastError();
+}
+
 }  // namespace pda

@@ -17,10 +17,10 @@ from ..ops.synth import fill_normal_, fill_randint_
 
 
 class DeviceSyntheticImages:
-    """Yields ``(images [B,H,W,Cpad] bf16, labels [B] int64)`` generated on ``device``."""
+    """Yields ``(images [B,H,W,pad_channels] bf16, labels [B] int64)`` generated on ``device``."""
 
     def __init__(self, batch_size: int, image_size: int = 224, num_classes: int = 1000, steps: Optional[int] = None,
-                 device="cuda", dtype=torch.bfloat16, channels: int = 3, pad_channels: int = 8, seed: int = 0,
+                 device="cuda", dtype=torch.bfloat16, channels: int = 3, pad_channels: int = 3, seed: int = 0,
                  rank: int = 0, fixed: bool = False, nchw: bool = False):
         self.B, self.S, self.K = batch_size, image_size, num_classes
         self.steps, self.device, self.dtype = steps, torch.device(device), dtype

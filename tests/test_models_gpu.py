@@ -95,3 +95,39 @@ def test_graft_smoke():
     import __graft_entry__ as g
 
     g.smoke()
+
+
+@pytest.mark.parametrize("hw", [32, 33])
+def test_stem_space_to_depth_matches_direct_conv(hw):
+    """The 4x4/1 space-to-depth stem equals the 7x7/2/pad-3 conv, forward and weight gradient."""
+    import torch.nn.functional as F
+
+    from pytorchdistributed_amd import ops
+    from pytorchdistributed_amd.models.resnet import space_to_depth_stem
+
+    torch.manual_seed(3)
+    x = torch.randn(2, hw, hw, 3).to(torch.bfloat16).float()
+    w = (torch.randn(64, 7, 7, 3) * 0.1).to(torch.bfloat16).float().requires_grad_()
+    y = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), None, 2, 3).permute(0, 2, 3, 1)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    wg = w.detach().to("cuda", torch.bfloat16).requires_grad_()
+    x2, w2 = space_to_depth_stem(x.to("cuda", torch.bfloat16), wg)
+    yg = ops.conv2d(x2, w2, None, 1, 0)[:, : (hw + 1) // 2, : (hw + 1) // 2]
+    assert yg.shape == y.shape
+    assert rel_err(yg.cpu(), y.detach()) < 1e-2
+    yg.backward(dy.to("cuda", torch.bfloat16))
+    assert rel_err(wg.grad.cpu(), w.grad) < 1e-2
+
+
+@pytest.mark.parametrize("hw,cx", [(32, 3), (33, 8)])
+def test_stem_s2d_kernel_matches_torch_layout(hw, cx):
+    from pytorchdistributed_amd._native import C
+    from pytorchdistributed_amd.models.resnet import space_to_depth_stem
+
+    x = torch.randn(2, hw, hw, cx, device="cuda").to(torch.bfloat16)
+    w = torch.randn(64, 7, 7, 3, device="cuda", dtype=torch.bfloat16)
+    ref, _ = space_to_depth_stem(x[..., :3], w)
+    got = C().stem_s2d(x, 3, 3)
+    assert got.shape == ref.shape
+    assert torch.equal(got, ref)
