@@ -212,16 +212,19 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optio
   return {y, mean, invstd, ss, bits};
 }
 
-std::vector<Tensor> bn_fwd_train_sums(Tensor x, Tensor sums, Tensor shift, c10::optional<Tensor> res,
+// training BN forward from a conv epilogue's statistics table [R, 2, C] (conv_fwd_stats), which the
+// finalize reads and leaves zeroed
+std::vector<Tensor> bn_fwd_train_sums(Tensor x, Tensor table, Tensor shift, c10::optional<Tensor> res,
                                       c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
                                       c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
                                       double momentum, double eps, bool relu, bool relu_bits,
                                       c10::optional<Tensor> num_batches) {
   check_bf16(x, "x");
-  check_f32(sums, "sums");
+  check_f32(table, "table");
   check_f32(shift, "shift");
   const int64_t C = x.size(-1), M = x.numel() / C;
-  TORCH_CHECK(C % 8 == 0 && C <= 2048 && sums.numel() == 2 * C && shift.numel() == C);
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && shift.numel() == C);
+  TORCH_CHECK(table.numel() % (2 * C) == 0 && table.numel() > 0 && table.is_contiguous(), "table must be [R, 2, C]");
   if (res) {
     check_bf16(*res, "residual");
     TORCH_CHECK(res->sizes() == x.sizes());
@@ -235,8 +238,8 @@ std::vector<Tensor> bn_fwd_train_sums(Tensor x, Tensor sums, Tensor shift, c10::
   auto fo = x.options().dtype(at::kFloat);
   Tensor mean = at::empty({C}, fo), invstd = at::empty({C}, fo), ss = at::empty({2, C}, fo);
   Tensor bits = (relu && relu_bits) ? at::empty({M * C / 8}, x.options().dtype(at::kByte)) : Tensor();
-  CHECK_HIP_OK(pda::bn_fwd_train_sums(bp(x), res ? bp(*res) : nullptr, bpm(y), M, C, sums.data_ptr<float>(),
-                                      shift.data_ptr<float>(), gf, gb, bfp, bb,
+  CHECK_HIP_OK(pda::bn_fwd_train_sums(bp(x), res ? bp(*res) : nullptr, bpm(y), M, C, table.data_ptr<float>(),
+                                      (int)(table.numel() / (2 * C)), shift.data_ptr<float>(), gf, gb, bfp, bb,
                                       running_mean ? running_mean->data_ptr<float>() : nullptr,
                                       running_var ? running_var->data_ptr<float>() : nullptr, (float)momentum,
                                       (float)eps, relu, mean.data_ptr<float>(), invstd.data_ptr<float>(),
@@ -435,33 +438,31 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, c1
   Tensor y = at::empty({N, P, Q, Cout}, x.options());
   CHECK_HIP_OK(pda::conv2d_fwd(bp(x), bp(w), bpm(y), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
                                bias ? bias->data_ptr() : nullptr, bias ? !is_bf16(*bias) : false, relu, nullptr,
-                               nullptr, stream_of(x)));
+                               nullptr, 0, stream_of(x)));
   return y;
 }
 
-// conv forward that also returns the BatchNorm sums of its output: [y, sums[2, Cout]] with
-// sums[0] = sum(y - shift), sums[1] = sum((y - shift)^2) over N*P*Q (no separate statistics pass)
-std::vector<Tensor> conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, Tensor shift) {
+// conv forward that also accumulates the BatchNorm sums of its output into `table` ([R, 2, Cout] fp32,
+// zero on entry; the BN finalize that consumes it zeroes it again): table[r][0] += sum(y - shift),
+// table[r][1] += sum((y - shift)^2) over the output tiles with tile_m % R == r (no statistics pass)
+Tensor conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, Tensor shift, Tensor table) {
   conv_check(x, w);
   check_f32(shift, "shift");
+  check_f32(table, "table");
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int Cout = w.size(0), R = w.size(1), S = w.size(2);
   TORCH_CHECK(shift.numel() == Cout);
+  TORCH_CHECK(table.numel() % (2 * (int64_t)Cout) == 0 && table.numel() > 0 && table.is_contiguous(),
+              "table must be [R, 2, Cout]");
+  TORCH_CHECK(table.device() == x.device() && shift.device() == x.device());
   const int P = (H + 2 * pad - dil * (R - 1) - 1) / stride + 1, Q = (W + 2 * pad - dil * (S - 1) - 1) / stride + 1;
   TORCH_CHECK(P > 0 && Q > 0);
   c10::DeviceGuard g(x.device());
   Tensor y = at::empty({N, P, Q, Cout}, x.options());
-  const int64_t M = (int64_t)N * P * Q;
-  const int64_t rows = pda::conv_fwd_stat_rows(M, Cout);
-  auto fo = x.options().dtype(at::kFloat);
-  Tensor slab = at::empty({rows, 2 * (int64_t)Cout}, fo);
+  const int rows = (int)(table.numel() / (2 * (int64_t)Cout));
   CHECK_HIP_OK(pda::conv2d_fwd(bp(x), bp(w), bpm(y), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil, nullptr, false,
-                               false, slab.data_ptr<float>(), shift.data_ptr<float>(), stream_of(x)));
-  Tensor sums = at::empty({2, (int64_t)Cout}, fo);
-  Tensor ws = at::empty({pda::colreduce_ws_floats(rows, 2 * (int64_t)Cout, 1)}, fo);
-  CHECK_HIP_OK(pda::colsum(slab.data_ptr<float>(), false, sums.data_ptr<float>(), rows, 2 * (int64_t)Cout,
-                           ws.data_ptr<float>(), stream_of(x)));
-  return {y, sums};
+                               false, table.data_ptr<float>(), shift.data_ptr<float>(), rows, stream_of(x)));
+  return y;
 }
 
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad, int64_t dil,

@@ -82,13 +82,14 @@ hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M
                         hipStream_t st);
 // num_batches (optional): int64 counter incremented once on the stream (BN num_batches_tracked)
 // relu_bits (optional, with relu): [M*C/8] bytes, bit j of byte v = ReLU mask of element 8v+j
-// training forward from precomputed sums (e.g. a conv epilogue): sums[0:C] = sum(x - K), sums[C:2C] =
-// sum((x - K)^2) over the M rows, K = shift; finalize + apply only (no statistics pass over x)
-hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* sums,
-                             const float* shift, const float* gamma_f, const bf16_t* gamma_b, const float* beta_f,
-                             const bf16_t* beta_b, float* running_mean, float* running_var, float momentum, float eps,
-                             bool relu, float* save_mean, float* save_invstd, float* save_ss, uint8_t* relu_bits,
-                             int64_t* num_batches, hipStream_t st);
+// training forward from a conv epilogue's statistics table [table_rows][2][C]: rows hold partial
+// sum(x - K) and sum((x - K)^2), K = shift; finalize (which re-zeroes the table) + apply only — no
+// statistics pass over x
+hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, float* table,
+                             int table_rows, const float* shift, const float* gamma_f, const bf16_t* gamma_b,
+                             const float* beta_f, const bf16_t* beta_b, float* running_mean, float* running_var,
+                             float momentum, float eps, bool relu, float* save_mean, float* save_invstd,
+                             float* save_ss, uint8_t* relu_bits, int64_t* num_batches, hipStream_t st);
 hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
                        const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, const float* running_mean,
                        const float* running_var, float eps, bool relu, float* ws, hipStream_t st);
@@ -126,12 +127,12 @@ hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* 
                      void* C, bool c_f32, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
                      bool bias_f32, bool relu, float* slab, bool allow_split, hipStream_t st);
 int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, int S, int P, int Q);
-// stats (optional): BatchNorm partial sums of the output, [conv_fwd_stat_rows(M, Cout)][2][Cout] fp32 —
-// per row-tile sum(y - K) and sum((y - K)^2) with K = stats_shift (e.g. the running mean)
+// stats (optional): BatchNorm sums of the output accumulated (atomically; must start zeroed) into a
+// [stats_rows][2][Cout] fp32 table: sum(y - K) and sum((y - K)^2) with K = stats_shift (e.g. the running
+// mean), each output tile adding into row (tile_m % stats_rows)
 hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int Cout, int R, int S,
                       int P, int Q, int stride, int pad, int dil, const void* bias, bool bias_f32, bool relu,
-                      float* stats, const float* stats_shift, hipStream_t st);
-int64_t conv_fwd_stat_rows(int64_t M, int64_t Cout);
+                      float* stats, const float* stats_shift, int stats_rows, hipStream_t st);
 // addend (optional, bf16, dx's layout): dx = dgrad + addend, fused into the store
 hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int N, int H, int W, int C, int Cout, int R,
                         int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend, hipStream_t st);

@@ -93,8 +93,11 @@ __device__ __forceinline__ void block_col_reduce_store(float (&a)[8], float (&b)
 
 // Sum the [nrb][C] slabs for 64 channels per workgroup: kFinThreads = 64 channels x 16 row-lanes.
 constexpr int kFinThreads = 1024;
-__device__ __forceinline__ void slab_sum(const float* __restrict__ pa, const float* __restrict__ pb, int nrb, int C,
-                                         int c, float& sa, float& sb) {
+// Rows are `ld` floats apart (C for the [nrb][C] slabs, 2C for a conv epilogue's [R][2][C] table).
+// CLEAR: zero every entry after reading it (the epilogue table must be zero for its next conv).
+template <bool CLEAR = false>
+__device__ __forceinline__ void slab_sum(float* __restrict__ pa, float* __restrict__ pb, int nrb, int64_t ld,
+                                         int C, int c, float& sa, float& sb) {
   __shared__ float red_a[kFinThreads], red_b[kFinThreads];
   const int l = threadIdx.x >> 6;  // 0..15
   float a[8], b[8];
@@ -107,14 +110,16 @@ __device__ __forceinline__ void slab_sum(const float* __restrict__ pa, const flo
     for (; r + 7 * 16 < nrb; r += 8 * 16) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        a[u] += pa[(int64_t)(r + 16 * u) * C + c];
-        b[u] += pb[(int64_t)(r + 16 * u) * C + c];
+        a[u] += pa[(int64_t)(r + 16 * u) * ld + c];
+        b[u] += pb[(int64_t)(r + 16 * u) * ld + c];
       }
     }
     for (; r < nrb; r += 16) {
-      a[0] += pa[(int64_t)r * C + c];
-      b[0] += pb[(int64_t)r * C + c];
+      a[0] += pa[(int64_t)r * ld + c];
+      b[0] += pb[(int64_t)r * ld + c];
     }
+    if (CLEAR)
+      for (r = l; r < nrb; r += 16) pa[(int64_t)r * ld + c] = pb[(int64_t)r * ld + c] = 0.f;
   }
   const float a0 = (a[0] + a[1]) + (a[2] + a[3]), a1 = (a[4] + a[5]) + (a[6] + a[7]);
   const float b0 = (b[0] + b[1]) + (b[2] + b[3]), b1 = (b[4] + b[5]) + (b[6] + b[7]);
@@ -177,9 +182,9 @@ __device__ __forceinline__ float param_at(const float* f, const bf16_t* b, int c
 
 // ---------------------------------------------------------------- forward finalize
 // TRAIN: statistics from the slabs; eval: from the running statistics.  Writes scale/shift [C].
-template <bool TRAIN>
+template <bool TRAIN, bool TABLE = false>
 __global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
-    const bf16_t* __restrict__ x, const float* __restrict__ pivot, const float* __restrict__ slab, int nrb,
+    const bf16_t* __restrict__ x, const float* __restrict__ pivot, float* __restrict__ slab, int nrb,
     int64_t M, int C, const float* __restrict__ gamma_f, const bf16_t* __restrict__ gamma_b, const float* __restrict__ beta_f,
     const bf16_t* __restrict__ beta_b, float* __restrict__ running_mean, float* __restrict__ running_var,
     float momentum, float eps, float* __restrict__ save_mean, float* __restrict__ save_invstd,
@@ -188,7 +193,10 @@ __global__ void __launch_bounds__(kFinThreads) bn_finalize_kernel(
   // the module's num_batches_tracked += 1 rides on this launch (one fewer kernel per BN layer)
   if (TRAIN && num_batches && blockIdx.x == 0 && threadIdx.x == 0) *num_batches += 1;
   float s1 = 0.f, s2 = 0.f;
-  if (TRAIN) slab_sum(slab, slab + (int64_t)nrb * C, nrb, C, c, s1, s2);
+  if (TRAIN) {
+    if (TABLE) slab_sum<true>(slab, slab + C, nrb, 2 * (int64_t)C, C, c, s1, s2);  // conv epilogue table
+    else slab_sum(slab, slab + (int64_t)nrb * C, nrb, C, C, c, s1, s2);
+  }
   if (threadIdx.x >= 64 || c >= C) return;
   float mean, invstd;
   if (TRAIN) {
@@ -377,13 +385,13 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* _
 
 // dgamma = invstd * sum(dz (x-mean)), dbeta = sum(dz);  coefficients for dx = A*dz + B*x + Cc
 __global__ void __launch_bounds__(kFinThreads) bn_bwd_finalize_kernel(
-    const float* __restrict__ slab, int nrb, int64_t M, int C, const float* __restrict__ mean,
+    float* __restrict__ slab, int nrb, int64_t M, int C, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma_f, const bf16_t* __restrict__ gamma_b,
     float* __restrict__ dgamma_f, bf16_t* __restrict__ dgamma_b, float* __restrict__ dbeta_f,
     bf16_t* __restrict__ dbeta_b, float* __restrict__ coef) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   float sdz, sdx;
-  slab_sum(slab, slab + (int64_t)nrb * C, nrb, C, c, sdz, sdx);
+  slab_sum(slab, slab + (int64_t)nrb * C, nrb, C, C, c, sdz, sdx);
   if (threadIdx.x >= 64 || c >= C) return;
   const float is = invstd[c], mu = mean[c];
   const float g = param_at(gamma_f, gamma_b, c, 1.f);
@@ -484,17 +492,17 @@ hipError_t bn_fwd_train(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M
   return launch_apply(x, res, y, M, (int)C, scale, shift, relu, relu_bits, st);
 }
 
-hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* sums,
-                             const float* shift, const float* gamma_f, const bf16_t* gamma_b, const float* beta_f,
-                             const bf16_t* beta_b, float* running_mean, float* running_var, float momentum, float eps,
-                             bool relu, float* save_mean, float* save_invstd, float* save_ss, uint8_t* relu_bits,
-                             int64_t* num_batches, hipStream_t st) {
-  if (C > kMaxC || C % 8) return hipErrorInvalidValue;
+hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, float* table,
+                             int table_rows, const float* shift, const float* gamma_f, const bf16_t* gamma_b,
+                             const float* beta_f, const bf16_t* beta_b, float* running_mean, float* running_var,
+                             float momentum, float eps, bool relu, float* save_mean, float* save_invstd,
+                             float* save_ss, uint8_t* relu_bits, int64_t* num_batches, hipStream_t st) {
+  if (C > kMaxC || C % 8 || table_rows < 1) return hipErrorInvalidValue;
   float* scale = save_ss;
   float* shift_out = save_ss + C;
-  bn_finalize_kernel<true><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
-      x, shift, sums, 1, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum, eps,
-      save_mean, save_invstd, scale, shift_out, num_batches);
+  bn_finalize_kernel<true, true><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
+      x, shift, table, table_rows, M, (int)C, gamma_f, gamma_b, beta_f, beta_b, running_mean, running_var, momentum,
+      eps, save_mean, save_invstd, scale, shift_out, num_batches);
   PDA_CHECK_HIP(hipGetLastError());
   return launch_apply(x, res, y, M, (int)C, scale, shift_out, relu, relu_bits, st);
 }

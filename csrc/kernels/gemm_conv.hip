@@ -413,11 +413,50 @@ struct Epi {
   // optional bf16 addend with C's layout (gradient accumulation fused into the store: conv1's dgrad
   // adds the residual-branch gradient of a bottleneck instead of a separate add kernel)
   const bf16_t* addend;
-  // optional BatchNorm statistics of the (bf16-rounded) output: per row-tile partial sums of (y - K)
-  // and (y - K)^2 per column, written to stats[tile_m][2][N] (K = stats_shift, e.g. running mean)
+  // optional BatchNorm statistics of the (bf16-rounded) output: per-tile column sums of (y - K) and
+  // (y - K)^2 (K = stats_shift, e.g. the running mean) are atomically added to row (tile_m % stats_rows)
+  // of a zero-initialised stats[stats_rows][2][N] table, which the BN finalize reads and re-zeroes.
   float* stats;
   const float* stats_shift;
+  int stats_rows;
 };
+
+// One workgroup's column partials (8 consecutive columns per thread, `cpr` column chunks per row,
+// `nt` threads): fold the lanes of a wave that share a chunk, then the waves through `red` (nt/64 x
+// 8*cpr x 2 floats of LDS that nothing else uses), then one atomic add per column and statistic.
+// The only barrier is LDS-only (lgkmcnt + s_barrier): a __syncthreads() here would also wait for the
+// tile's global stores to be acknowledged (vmcnt(0)) — measured at ~16 us per wide-tile conv, since a
+// 1-workgroup-per-CU kernel exposes every epilogue cycle.
+__device__ __forceinline__ void epi_stats_flush(const Epi& epi, float (&st1)[8], float (&st2)[8], float* red, int cpr,
+                                                int nt, int tm, int64_t n0, int64_t N) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, ncol = cpr * 8;
+  for (int off = cpr; off < 64; off <<= 1)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      st1[q] += __shfl_xor(st1[q], off, 64);
+      st2[q] += __shfl_xor(st2[q], off, 64);
+    }
+  if (lane < cpr) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      red[(wid * ncol + lane * 8 + q) * 2] = st1[q];
+      red[(wid * ncol + lane * 8 + q) * 2 + 1] = st2[q];
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (tid < ncol && n0 + tid < N) {
+    float a = 0.f, b = 0.f;
+    for (int w = 0; w < nt / 64; ++w) {
+      a += red[(w * ncol + tid) * 2];
+      b += red[(w * ncol + tid) * 2 + 1];
+    }
+    float* row = epi.stats + (int64_t)(tm % epi.stats_rows) * 2 * N;
+    unsafeAtomicAdd(row + n0 + tid, a);
+    unsafeAtomicAdd(row + N + n0 + tid, b);
+  }
+}
 
 __device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
   if (!e.rm_on) return m;
@@ -587,35 +626,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
       *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
     }
     if (want_stats) {
-      // lanes sharing a column chunk: xor over the lane bits above log2(CPR), then the 4 waves in LDS
-#pragma unroll
-      for (int off = CPR; off < 64; off <<= 1)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          st1[q] += __shfl_xor(st1[q], off, 64);
-          st2[q] += __shfl_xor(st2[q], off, 64);
-        }
-      __syncthreads();  // staging tile no longer read
-      float* red = reinterpret_cast<float*>(smem);  // [NT/64 waves][BN][2]
-      if (lane < CPR) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          red[(wid * BN + lane * 8 + q) * 2] = st1[q];
-          red[(wid * BN + lane * 8 + q) * 2 + 1] = st2[q];
-        }
-      }
-      __syncthreads();
-      if (tid < BN && n0 + tid < N) {
-        float a = 0.f, b = 0.f;
-#pragma unroll
-        for (int w = 0; w < NT / 64; ++w) {
-          a += red[(w * BN + tid) * 2];
-          b += red[(w * BN + tid) * 2 + 1];
-        }
-        float* row = epi.stats + (int64_t)tm * 2 * N;
-        row[n0 + tid] = a;
-        row[N + n0 + tid] = b;
-      }
+      static_assert(BM * SROW * 2 + (NT / 64) * BN * 2 * 4 <= 2 * (A_BYTES + B_BYTES), "stats scratch must fit");
+      epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + BM * SROW * 2), CPR, NT, tm, n0, N);
     }
     return;
   }
@@ -794,7 +806,8 @@ constexpr int W_NT = 512;
 constexpr int W_HALF = 128 * BK * 2;  // one 128-row half of an operand tile (16 KB)
 constexpr int W_STAGE = 4 * W_HALF;   // A0 A1 B0 B1
 constexpr int W_SROW = 256 + 8;       // epilogue staging row (bf16 elements)
-constexpr int W_LDS = 2 * W_STAGE > 256 * W_SROW * 2 ? 2 * W_STAGE : 256 * W_SROW * 2;
+constexpr int W_STATS_OFF = 2 * W_STAGE > 256 * W_SROW * 2 ? 2 * W_STAGE : 256 * W_SROW * 2;
+constexpr int W_LDS = W_STATS_OFF + (W_NT / 64) * 256 * 2 * 4;  // + epilogue BN-statistics scratch (16 KB)
 
 // VAR (schedule experiments, selected at run time): bit 0 = s_setprio(1) around each MFMA cluster,
 // bit 1 = interleave each MFMA with one of the next phase's ds_reads (sched_group_barrier).
@@ -980,6 +993,17 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
   }
   __syncthreads();
   constexpr int CPR = 256 / 8;
+  static_assert(W_NT % CPR == 0, "a thread keeps one column chunk");
+  const bool want_stats = epi.stats != nullptr;
+  float st1[8], st2[8], kshift[8];
+  {
+    const int64_t n = n0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      st1[q] = st2[q] = 0.f;
+      kshift[q] = (want_stats && n + q < N) ? epi.stats_shift[n + q] : 0.f;
+    }
+  }
   for (int c = tid; c < 256 * CPR; c += W_NT) {
     const int r = c / CPR, ch = c % CPR;
     const int64_t m = m0 + r, n = n0 + ch * 8;
@@ -991,8 +1015,17 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + bf2f(a[q]));
     }
+    if (want_stats) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float d = bf2f(v[q]) - kshift[q];
+        st1[q] += d;
+        st2[q] = fmaf(d, d, st2[q]);
+      }
+    }
     *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
   }
+  if (want_stats) epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + W_STATS_OFF), CPR, W_NT, tm, n0, N);
 }
 
 // Split-K reduction: out[m, n] = act(sum_s slab[s, m, n] + bias[n]).  A workgroup is (256 / L) output
@@ -1217,7 +1250,7 @@ bool wide_pays(int64_t M, int64_t N) {
 
 bool use_wide(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) {
   const int mode = wide_mode();
-  if (mode == 0 || p.splits > 1 || epi.c_f32 || epi.slab || epi.stats || N < 256 || K < 64) return false;
+  if (mode == 0 || p.splits > 1 || epi.c_f32 || epi.slab || N < 256 || K < 64) return false;
   if (mode == 2) return true;
   return wide_pays(M, N);
 }
@@ -1378,19 +1411,15 @@ int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, 
 }
 
 // y[N,P,Q,Cout] = conv(x[N,H,W,C], w[Cout,R,S,C]) (+bias, relu)
-int64_t conv_fwd_stat_rows(int64_t M, int64_t Cout) {
-  Plan p = plan_gemm(M, Cout, 1, false, 512);
-  return p.tiles_m;
-}
-
 hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int Cout, int R, int S,
                       int P, int Q, int stride, int pad, int dil, const void* bias, bool bias_f32, bool relu,
-                      float* stats, const float* stats_shift, hipStream_t st) {
+                      float* stats, const float* stats_shift, int stats_rows, hipStream_t st) {
   const int64_t M = (int64_t)N * P * Q, Nn = Cout, K = (int64_t)R * S * C;
   Plan p = plan_gemm(M, Nn, K, false, 512);
   Epi epi{y, Cout, 0, bias, bias_f32 ? 1 : 0, relu ? 1 : 0, nullptr};
   epi.stats = stats;
   epi.stats_shift = stats_shift;
+  epi.stats_rows = stats_rows > 0 ? stats_rows : 1;
 
   ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
   auto mk_a = [&](auto t) { t.x = x; t.g = g; t.M = M; t.K = K; return t; };

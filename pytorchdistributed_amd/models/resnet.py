@@ -101,7 +101,6 @@ class Stem(tnn.Module):
             x = x.permute(0, 2, 3, 1)
         if x.is_cuda and _STEM_S2D and self.conv1.weight.shape[-1] == 3:
             # (input channels beyond the weight's 3 are device-side padding: dropped by the rewrite)
-            H, W = x.shape[1], x.shape[2]
             if x.dtype == torch.bfloat16 and not x.requires_grad:
                 from .._native import C as _C
 
@@ -109,8 +108,13 @@ class Stem(tnn.Module):
                 w2 = space_to_depth_stem(None, self.conv1.weight)[1]
             else:
                 x2, w2 = space_to_depth_stem(x[..., :3], self.conv1.weight)
-            y = ops.conv2d(x2, w2, None, 1, 0)[:, : (H + 1) // 2, : (W + 1) // 2]
-            return self.maxpool(self.bn1(y.contiguous(), relu=True))
+            # (the space-to-depth image is sized so the 4x4 valid conv yields exactly ceil(H/2) x ceil(W/2))
+            bn = self.bn1
+            if pnn._EPILOGUE_STATS and bn.training and x2.dtype == torch.bfloat16:
+                table = bn.stat_table(x2.device)
+                y = ops.conv2d_bn_stats(x2, w2, 1, 0, 1, bn.running_mean, table)
+                return self.maxpool(bn((y, (table, bn.running_mean)), relu=True))
+            return self.maxpool(bn(ops.conv2d(x2, w2, None, 1, 0), relu=True))
         if x.is_cuda and x.shape[-1] % 8 != 0:
             x = F.pad(x, (0, 8 - x.shape[-1] % 8))
         x = x.contiguous()

@@ -15,7 +15,9 @@ import torch.nn as tnn
 
 from . import ops
 
-_EPILOGUE_STATS = os.environ.get("PDA_BN_EPILOGUE_STATS", "0") == "1"
+_EPILOGUE_STATS = os.environ.get("PDA_BN_EPILOGUE_STATS", "1") == "1"
+# rows of the epilogue statistics table (atomic contention vs finalize read; 32..128 measured equal)
+_STAT_ROWS = int(os.environ.get("PDA_BN_STAT_ROWS", "64"))
 
 
 def _kaiming_uniform_(w: torch.Tensor, fan_in: int):
@@ -61,18 +63,17 @@ class Conv2d(tnn.Module):
         _kaiming_uniform_(self.weight, in_channels * k * k)
 
     def forward(self, x, relu=False, grad_join=None, bn=None):
-        """``bn``: the BatchNorm2d this conv feeds; ``(y, stats)`` is returned (pass it to the BN).  With
-        ``PDA_BN_EPILOGUE_STATS=1`` the conv epilogue reduces that BN's batch statistics (training, GPU)
-        so the BN skips its statistics pass.  Off by default: at ResNet-50 bs 256 the epilogue
-        reduction + slab column sum cost 1.6 ms/step against the 1.5 ms statistics pass it removes
-        (profiles/r1_resnet50_bs256_v7_epilogue_stats.md) — the K = 64 layer-1 convs are
-        epilogue-bound."""
+        """``bn``: the BatchNorm2d this conv feeds; ``(y, stats)`` is returned (pass it to the BN).  In
+        training on the GPU (``PDA_BN_EPILOGUE_STATS=1``, default) the conv epilogue reduces that BN's
+        batch statistics (each output tile atomically adds its column sums into the BN's statistics
+        table), so the BN skips its statistics pass over y (one fewer HBM read of every BN input)."""
         if bn is not None:
             if (_EPILOGUE_STATS and x.is_cuda and bn.training and self.bias is None and not relu
                     and x.dtype == torch.bfloat16):
-                y, sums = ops.conv2d_bn_stats(x, self.weight, self.stride, self.padding, self.dilation,
-                                              bn.running_mean, grad_join)
-                return y, (sums, bn.running_mean)
+                table = bn.stat_table(x.device)
+                y = ops.conv2d_bn_stats(x, self.weight, self.stride, self.padding, self.dilation,
+                                        bn.running_mean, table, grad_join)
+                return y, (table, bn.running_mean)
             return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, relu,
                               grad_join), None
         return ops.conv2d(x, self.weight, self.bias, self.stride, self.padding, self.dilation, relu, grad_join)
@@ -96,6 +97,17 @@ class BatchNorm2d(tnn.Module):
         self.register_buffer("running_mean", torch.zeros(num_features, device=device))
         self.register_buffer("running_var", torch.ones(num_features, device=device))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long, device=device))
+
+    def stat_table(self, device) -> torch.Tensor:
+        """Zeroed [R, 2, C] fp32 table that the producing conv's epilogue accumulates this BN's batch
+        sums into (output tile t adds into row t % R, spreading the atomics over R rows) and that the
+        BN finalize reads and re-zeroes — so it is zero between uses and needs no per-step memset.
+        Not a registered buffer: never saved, broadcast or all-reduced."""
+        t = getattr(self, "_stat_table", None)
+        if t is None or t.device != torch.device(device):
+            t = torch.zeros(_STAT_ROWS, 2, self.num_features, device=device)
+            self._stat_table = t
+        return t
 
     def _apply(self, fn, recurse=True):
         # keep running stats in fp32 when the module is cast to bf16

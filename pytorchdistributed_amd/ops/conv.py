@@ -59,34 +59,35 @@ class _Conv2dFn(torch.autograd.Function):
 
 
 class _Conv2dStatsFn(torch.autograd.Function):
-    """Conv forward that also emits the BatchNorm sums of its output from the GEMM epilogue
-    (sum(y - K), sum((y - K)^2) per channel, K = ``shift``), so the following BatchNorm skips its
-    statistics pass over y.  Backward is the plain conv backward."""
+    """Conv forward whose GEMM epilogue also accumulates the BatchNorm sums of its output
+    (sum(y - K), sum((y - K)^2) per channel, K = ``shift``) into a zeroed [R, 2, C_out] table (tile t
+    adds into row t % R), so the following BatchNorm skips its statistics pass over y.  Backward is
+    the plain conv backward."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, padding, dilation, shift, join):
+    def forward(ctx, x, w, stride, padding, dilation, shift, table, join):
         x = x.contiguous()
         w = w.contiguous()
-        y, sums = C().conv_fwd_stats(x, w, stride, padding, dilation, shift)
+        y = C().conv_fwd_stats(x, w, stride, padding, dilation, shift, table)
         ctx.save_for_backward(x, w, None)
         ctx.cfg = (stride, padding, dilation, False, False)
         ctx.wparam = w
         ctx.join = join
-        ctx.mark_non_differentiable(sums)
-        return y, sums
+        return y
 
     @staticmethod
-    def backward(ctx, dy, _dsums):
+    def backward(ctx, dy):
         dx, dw, _db, *_ = _Conv2dFn._backward(ctx, dy)
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
 def conv2d_bn_stats(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding: int = 0, dilation: int = 1,
-                    shift: torch.Tensor = None, grad_join=None):
-    """GPU only: ``(y, sums)`` with ``sums[0] = sum(y - shift)``, ``sums[1] = sum((y - shift)^2)``."""
+                    shift: torch.Tensor = None, table: torch.Tensor = None, grad_join=None):
+    """GPU only: returns y and adds ``(sum(y - shift), sum((y - shift)^2))`` per channel into the rows of
+    ``table`` ([R, 2, C_out] fp32, zero on entry; the consuming BN finalize re-zeroes it)."""
     if weight.shape[-1] != x.shape[-1]:
         weight = F.pad(weight, (0, x.shape[-1] - weight.shape[-1]))
-    return _Conv2dStatsFn.apply(x, weight, stride, padding, dilation, shift, grad_join)
+    return _Conv2dStatsFn.apply(x, weight, stride, padding, dilation, shift, table, grad_join)
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias=None, stride: int = 1, padding: int = 0, dilation: int = 1,

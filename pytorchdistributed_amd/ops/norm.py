@@ -16,7 +16,7 @@ from ..parallel.flat import grad_target
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu, join,
-                sums=None, shift=None, num_batches=None):
+                table=None, shift=None, num_batches=None):
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()
@@ -24,8 +24,8 @@ class _BatchNormFn(torch.autograd.Function):
         # BN+residual+ReLU: the forward also writes the ReLU mask as bits (1/16 of y), read by both
         # backward passes instead of the 16-bit output
         want_bits = relu and residual is not None
-        if training and sums is not None:  # statistics already reduced by the producing conv's epilogue
-            y, mean, invstd, ss, bits = C().bn_fwd_train_sums(x, sums, shift, residual, gamma, beta, running_mean,
+        if training and table is not None:  # statistics accumulated by the producing conv's epilogue
+            y, mean, invstd, ss, bits = C().bn_fwd_train_sums(x, table, shift, residual, gamma, beta, running_mean,
                                                               running_var, momentum, eps, relu, want_bits, num_batches)
         elif training:
             y, mean, invstd, ss, bits = C().bn_fwd_train(x, residual, gamma, beta, running_mean, running_var,
@@ -80,13 +80,14 @@ def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=Tru
                residual=None, relu=False, residual_join=None, stats=None, num_batches_tracked=None):
     """BatchNorm over the last (channel) dim of ``x`` (any leading dims), then ``+residual``, then ReLU.
     ``residual_join``: the residual's gradient is handed to the join instead of autograd's add.
-    ``stats``: ``(sums, shift)`` from :func:`~.conv.conv2d_bn_stats` — skips the statistics pass.
+    ``stats``: ``(table, shift)`` — the statistics table filled by :func:`~.conv.conv2d_bn_stats`
+    (``BatchNorm2d.stat_table``; re-zeroed by the finalize) — skips the statistics pass.
     ``num_batches_tracked``: int64 counter incremented in training mode (inside the finalize kernel on
     the native path, so it costs no launch of its own)."""
     if x.is_cuda and x.dtype == torch.bfloat16:
-        sums, shift = stats if stats is not None else (None, None)
+        table, shift = stats if stats is not None else (None, None)
         return _BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
-                                  relu, residual_join, sums, shift, num_batches_tracked if training else None)
+                                  relu, residual_join, table, shift, num_batches_tracked if training else None)
     if training and num_batches_tracked is not None:
         num_batches_tracked.add_(1)
     return _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu)

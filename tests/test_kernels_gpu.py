@@ -184,27 +184,37 @@ def test_conv_fwd_dgrad_wgrad(case):
     assert rel_err(dwb.cpu(), w.grad) < 1e-2
 
 
-@pytest.mark.parametrize("case", [(2, 16, 16, 64, 64, 1, 1, 0), (3, 15, 15, 32, 136, 3, 2, 1), (1, 7, 7, 64, 2048, 1, 1, 0)])
-def test_conv_fwd_epilogue_bn_sums(case):
-    """BN statistics reduced in the conv epilogue == sums over the stored bf16 output."""
+@pytest.mark.parametrize("case", [(2, 16, 16, 64, 64, 1, 1, 0), (3, 15, 15, 32, 136, 3, 2, 1), (1, 7, 7, 64, 2048, 1, 1, 0),
+                                  (8, 28, 28, 64, 256, 1, 1, 0), (4, 14, 14, 256, 512, 3, 1, 1)])
+@pytest.mark.parametrize("wide", [-1, 0, 2])
+def test_conv_fwd_epilogue_bn_sums(case, wide):
+    """BN statistics accumulated by the conv epilogue (128-tile, wide-tile and auto paths) == sums over
+    the stored bf16 output; the BN finalize that consumes the table leaves it zeroed."""
     N, H, W, Cin, Cout, k, s, p = case
     torch.manual_seed(4)
     x = torch.randn(N, H, W, Cin).to(torch.bfloat16)
     w = (torch.randn(Cout, k, k, Cin) / math.sqrt(Cin * k * k)).to(torch.bfloat16)
     shift = torch.randn(Cout) * 0.1
-    y, sums = C().conv_fwd_stats(x.to(DEV), w.to(DEV), s, p, 1, shift.to(DEV))
-    y_plain = C().conv_fwd(x.to(DEV), w.to(DEV), s, p, 1, None, False)
+    rows = 5  # odd row count: tiles wrap onto rows unevenly
+    table = torch.zeros(rows, 2, Cout, device=DEV)
+    C().set_gemm_paths(wide)
+    try:
+        y = C().conv_fwd_stats(x.to(DEV), w.to(DEV), s, p, 1, shift.to(DEV), table)
+        y_plain = C().conv_fwd(x.to(DEV), w.to(DEV), s, p, 1, None, False)
+    finally:
+        C().set_gemm_paths(-1)
     assert torch.equal(y, y_plain)
     d = y.float().cpu().reshape(-1, Cout) - shift
     ref = torch.stack([d.sum(0), (d * d).sum(0)])
-    assert rel_err(sums.cpu(), ref) < 1e-4
-    # BN from the epilogue sums == BN with its own statistics pass
+    assert rel_err(table.sum(0).cpu(), ref) < 1e-4
+    # BN from the epilogue sums == BN with its own statistics pass; the finalize re-zeroes the table
     g, b = torch.rand(Cout) + 0.5, torch.randn(Cout)
     rm1, rv1 = shift.clone().to(DEV), torch.ones(Cout, device=DEV)
     rm2, rv2 = shift.clone().to(DEV), torch.ones(Cout, device=DEV)
     nbt = torch.zeros((), dtype=torch.long, device=DEV)
-    ya, ma, ia, ssa, _ = C().bn_fwd_train_sums(y, sums, rm1.clone(), None, g.to(DEV), b.to(DEV), rm1, rv1, 0.1,
+    ya, ma, ia, ssa, _ = C().bn_fwd_train_sums(y, table, rm1.clone(), None, g.to(DEV), b.to(DEV), rm1, rv1, 0.1,
                                                1e-5, True, False, nbt)
+    assert not table.any()
     yb, mb, ib, ssb, _ = C().bn_fwd_train(y, None, g.to(DEV), b.to(DEV), rm2, rv2, 0.1, 1e-5, True, False, nbt)
     assert nbt.item() == 2  # num_batches_tracked is bumped by each training finalize
     assert rel_err(ma.cpu(), mb.cpu()) < 1e-4 and rel_err(ia.cpu(), ib.cpu()) < 1e-4

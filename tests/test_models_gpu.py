@@ -113,7 +113,7 @@ def test_stem_space_to_depth_matches_direct_conv(hw):
     y.backward(dy)
     wg = w.detach().to("cuda", torch.bfloat16).requires_grad_()
     x2, w2 = space_to_depth_stem(x.to("cuda", torch.bfloat16), wg)
-    yg = ops.conv2d(x2, w2, None, 1, 0)[:, : (hw + 1) // 2, : (hw + 1) // 2]
+    yg = ops.conv2d(x2, w2, None, 1, 0)
     assert yg.shape == y.shape
     assert rel_err(yg.cpu(), y.detach()) < 1e-2
     yg.backward(dy.to("cuda", torch.bfloat16))
