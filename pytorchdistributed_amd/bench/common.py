@@ -13,18 +13,33 @@ from ..utils.timing import StepTimer
 
 
 def setup(n_gpus: int):
+    """Rank / world / local rank / device from the env contract; initialises the default group.
+
+    ``PDA_DIST_BACKEND`` overrides the backend (default ``nccl`` = RCCL on a GPU, ``gloo`` on CPU).
+    Rehearsal mode: with ``PDA_DIST_BACKEND=gloo`` more ranks than GPUs may share the visible GPUs
+    (rank r on GPU r % count) — the whole multi-rank DDP path (hooks, buckets, collectives, timing
+    protocol) runs on the native kernels of a one-GPU box; RCCL itself refuses two ranks per GPU.
+    """
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if n_gpus != world and world > 1:
         raise SystemExit(f"--gpus {n_gpus} but WORLD_SIZE={world}")
     use_gpu = torch.cuda.is_available()
+    backend = os.environ.get("PDA_DIST_BACKEND", "nccl" if use_gpu else "gloo")
+    gpu = local
     if use_gpu:
-        torch.cuda.set_device(local)
+        count = torch.cuda.device_count()
+        if local >= count:
+            if backend == "nccl":
+                raise SystemExit(f"LOCAL_RANK {local} but only {count} GPU(s) visible (RCCL needs one GPU per "
+                                 f"rank; PDA_DIST_BACKEND=gloo rehearses with shared GPUs)")
+            gpu = local % count
+        torch.cuda.set_device(gpu)
     if world > 1 and not dist.is_initialized():
-        pdist.init_process_group("nccl" if use_gpu else "gloo", rank=rank, world_size=world,
-                                 device_id=local if use_gpu else None)
-    device = torch.device("cuda", local) if use_gpu else torch.device("cpu")
+        pdist.init_process_group(backend, rank=rank, world_size=world,
+                                 device_id=gpu if use_gpu and backend == "nccl" else None)
+    device = torch.device("cuda", gpu) if use_gpu else torch.device("cpu")
     return rank, world, local, device
 
 

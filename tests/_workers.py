@@ -260,3 +260,48 @@ def xgmi_worker(rank, world, outdir):
     with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
         f.write("ok")
     pd.destroy_process_group()
+
+
+def ddp_resnet_gpu_worker(rank, world, outdir):
+    """DDP ResNet-50 on the native kernels, `world` ranks sharing cuda:0 over gloo (RCCL refuses two
+    ranks per GPU): the all-reduced bucket gradients must equal the mean of every rank's local
+    gradients (computed by a non-DDP replica with the same weights), BN buffers follow rank 0, and one
+    fused SGD step keeps the replicas identical."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.models.resnet import resnet50
+    from pytorchdistributed_amd.ops import cross_entropy
+    from pytorchdistributed_amd.optim import SGD
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    pd.init_process_group("gloo")
+    torch.manual_seed(10 + rank)  # different init per rank: DDP must broadcast rank 0's state
+    base = resnet50(device="cuda", dtype=torch.bfloat16)
+    model = DistributedDataParallel(base, device_ids=[0], bucket_cap_mb=8, first_bucket_mb=1)
+    local = resnet50(device="cuda", dtype=torch.bfloat16)  # plain replica with rank 0's broadcast state
+    local.load_state_dict(base.state_dict())
+    g = torch.Generator().manual_seed(99 + rank)
+    x = torch.randn(4, 32, 32, 3, generator=g).to("cuda", torch.bfloat16)
+    y = torch.randint(0, 1000, (4,), generator=g).to("cuda")
+    cross_entropy(model(x), y).backward()
+    cross_entropy(local(x), y).backward()
+    errs = []
+    for (n, p), (_, q) in zip(base.named_parameters(), local.named_parameters()):
+        mine = q.grad.float().clone()
+        allg = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allg, mine)
+        ref = torch.stack(allg).mean(0)
+        e = ((p.grad.float() - ref).norm() / ref.norm().clamp_min(1e-12)).item()
+        errs.append((e, n))
+    worst = max(errs)
+    assert worst[0] < 2e-2, worst
+    opt = SGD(model.parameters(), lr=0.1, momentum=0.9)
+    opt.step()
+    flat = torch.cat([p.detach().float().reshape(-1) for p in base.parameters()])
+    allf = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(allf, flat)
+    assert all(torch.equal(allf[0], f) for f in allf), "replicas diverged after the step"
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+        f.write(f"ok {worst[0]:.3e} buckets={model.reducer.num_buckets}")
+    pd.destroy_process_group()

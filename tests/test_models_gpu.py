@@ -131,3 +131,14 @@ def test_stem_s2d_kernel_matches_torch_layout(hw, cx):
     got = C().stem_s2d(x, 3, 3)
     assert got.shape == ref.shape
     assert torch.equal(got, ref)
+
+
+def test_ddp_resnet50_two_ranks_share_gpu(tmp_path):
+    """The multi-rank DDP path (hooks, native bucket reducer, bucket all-reduce, flat grads written by
+    the wgrad kernels, fused SGD) at world 2 on the one GPU of the test box, over gloo."""
+    import _workers
+    from pytorchdistributed_amd.launch import spawn
+
+    spawn(_workers.ddp_resnet_gpu_worker, args=(2, str(tmp_path)), nprocs=2, timeout=300)
+    for r in range(2):
+        assert (tmp_path / f"ok{r}").read_text().startswith("ok")
