@@ -465,8 +465,9 @@ Tensor conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t d
   return y;
 }
 
+// addend_bits: optional ReLU bit mask of the addend (numel/8 bytes): dx = dgrad + addend * mask
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad, int64_t dil,
-                  c10::optional<Tensor> addend) {
+                  c10::optional<Tensor> addend, c10::optional<Tensor> addend_bits) {
   check_bf16(dy, "dy");
   check_bf16(w, "w");
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), Cout = dy.size(3);
@@ -478,10 +479,18 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   Tensor dx = at::empty({N, H, W, C}, dy.options());
   if (addend.has_value()) {
     check_bf16(*addend, "addend");
-    TORCH_CHECK(addend->sizes() == dx.sizes(), "addend must have dx's shape");
+    TORCH_CHECK(addend->sizes() == dx.sizes() && addend->is_contiguous(), "addend must have dx's shape");
+  }
+  if (addend_bits.has_value()) {
+    TORCH_CHECK(addend.has_value(), "addend_bits without an addend");
+    check_gpu(*addend_bits, "addend_bits");
+    TORCH_CHECK(addend_bits->scalar_type() == at::kByte && addend_bits->is_contiguous() &&
+                    addend_bits->numel() * 8 == dx.numel(),
+                "addend_bits must be numel/8 contiguous bytes");
   }
   CHECK_HIP_OK(pda::conv2d_dgrad(bp(dy), bp(wt), bpm(dx), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
-                                 addend.has_value() ? bp(*addend) : nullptr, stream_of(dy)));
+                                 addend.has_value() ? bp(*addend) : nullptr,
+                                 addend_bits.has_value() ? addend_bits->data_ptr<uint8_t>() : nullptr, stream_of(dy)));
   return dx;
 }
 
@@ -879,7 +888,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_fwd_stats", &conv_fwd_stats);
   m.def("bn_fwd_train_sums", &bn_fwd_train_sums);
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"),
+        py::arg("pad"), py::arg("dil"), py::arg("addend") = py::none(), py::arg("addend_bits") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);

@@ -413,6 +413,10 @@ struct Epi {
   // optional bf16 addend with C's layout (gradient accumulation fused into the store: conv1's dgrad
   // adds the residual-branch gradient of a bottleneck instead of a separate add kernel)
   const bf16_t* addend;
+  // optional ReLU bit mask of the addend (bit j of byte v masks element 8v + j of C's layout): the
+  // addend is then dz * mask, i.e. a bottleneck's residual gradient read straight from the block's
+  // output gradient and the BN's forward bit mask, never materialised by the BN backward
+  const uint8_t* addend_bits;
   // optional BatchNorm statistics of the (bf16-rounded) output: per-tile column sums of (y - K) and
   // (y - K)^2 (K = stats_shift, e.g. the running mean) are atomically added to row (tile_m % stats_rows)
   // of a zero-initialised stats[stats_rows][2][N] table, which the BN finalize reads and re-zeroes.
@@ -456,6 +460,22 @@ __device__ __forceinline__ void epi_stats_flush(const Epi& epi, float (&st1)[8],
     unsafeAtomicAdd(row + n0 + tid, a);
     unsafeAtomicAdd(row + N + n0 + tid, b);
   }
+}
+
+// addend (optionally bit-masked) of the 8 (or 4) consecutive elements at (crow, n), n 8- (4-) aligned
+__device__ __forceinline__ void epi_addend8(const Epi& e, int64_t crow, int64_t n, float (&a)[8]) {
+  const int64_t off = crow * e.ldc + n;
+  const u16x8 v = *reinterpret_cast<const u16x8*>(e.addend + off);
+  const uint32_t mb = e.addend_bits ? e.addend_bits[off >> 3] : 0xFFu;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) a[q] = (mb >> q) & 1u ? bf2f(v[q]) : 0.f;
+}
+__device__ __forceinline__ void epi_addend4(const Epi& e, int64_t crow, int64_t n, float (&a)[4]) {
+  const int64_t off = crow * e.ldc + n;
+  const u16x4 v = *reinterpret_cast<const u16x4*>(e.addend + off);
+  const uint32_t mb = e.addend_bits ? (uint32_t)e.addend_bits[off >> 3] >> (off & 7) : 0xFu;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a[q] = (mb >> q) & 1u ? bf2f(v[q]) : 0.f;
 }
 
 __device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
@@ -611,9 +631,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
       const int64_t crow = epi_row(epi, m);
       u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * SROW + ch * 8);
       if (epi.addend) {
-        const u16x8 a = *reinterpret_cast<const u16x8*>(epi.addend + crow * epi.ldc + n);
+        float a[8];
+        epi_addend8(epi, crow, n, a);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + bf2f(a[q]));
+        for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
       }
       if (want_stats) {
 #pragma unroll
@@ -656,9 +677,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
         for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
       }
       if (epi.addend) {
-        const u16x4 a = *reinterpret_cast<const u16x4*>(epi.addend + crow * epi.ldc + n);
+        float a[4];
+        epi_addend4(epi, crow, n, a);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += bf2f(a[r]);
+        for (int r = 0; r < 4; ++r) v[r] += a[r];
       }
       *reinterpret_cast<f32x4*>((float*)epi.C + crow * epi.ldc + n) = v;
     }
@@ -780,9 +802,10 @@ __global__ void __launch_bounds__(BIG_NT, 1) gemm_big_kernel(LA la, LB lb, int64
     const int64_t crow = epi_row(epi, m);
     u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * SROW + ch * 8);
     if (epi.addend) {
-      const u16x8 a = *reinterpret_cast<const u16x8*>(epi.addend + crow * epi.ldc + n);
+      float a[8];
+      epi_addend8(epi, crow, n, a);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + bf2f(a[q]));
+      for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
     }
     *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
   }
@@ -955,9 +978,10 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
           for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
         }
         if (epi.addend) {
-          const u16x4 a = *reinterpret_cast<const u16x4*>(epi.addend + crow * epi.ldc + n);
+          float a[4];
+          epi_addend4(epi, crow, n, a);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] += bf2f(a[q]);
+          for (int q = 0; q < 4; ++q) v[q] += a[q];
         }
         *reinterpret_cast<f32x4*>((float*)epi.C + crow * epi.ldc + n) = v;
       }
@@ -1011,9 +1035,10 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
     const int64_t crow = epi_row(epi, m);
     u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * W_SROW + ch * 8);
     if (epi.addend) {
-      const u16x8 a = *reinterpret_cast<const u16x8*>(epi.addend + crow * epi.ldc + n);
+      float a[8];
+      epi_addend8(epi, crow, n, a);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + bf2f(a[q]));
+      for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
     }
     if (want_stats) {
 #pragma unroll
@@ -1430,13 +1455,15 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H,
 // dx[N,H,W,C] = dgrad(dy[N,P,Q,Cout], wt): one launch per stride phase with only the taps that reach
 // it (wt phase-packed by conv_weight_transpose); folded single launch when stride > 1 and dil > 1.
 hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int N, int H, int W, int C, int Cout, int R,
-                        int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend, hipStream_t st) {
+                        int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,
+                        const uint8_t* addend_bits, hipStream_t st) {
   ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, Cout);
   if (!dgrad_phased(stride, dil)) {
     const int64_t M = (int64_t)N * H * W, Nn = C, K = (int64_t)R * S * Cout;
     Plan p = plan_gemm(M, Nn, K, false, 512);
     Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
     epi.addend = addend;
+    epi.addend_bits = addend_bits;
     auto mk_a = [&](auto t) { t.dy = dy; t.g = g; t.M = M; t.K = K; return t; };
     auto mk_b = [&](auto t) { t.p = wt; t.rows = Nn; t.K = K; t.ld = K; return t; };
     return dispatch_bn<ConvDgradK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
@@ -1461,6 +1488,7 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int N, i
       Plan p = plan_gemm(M, Nn, K, false, 512);
       Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
       epi.addend = addend;
+      epi.addend_bits = addend_bits;
       if (stride > 1) {
         epi.rm_on = 1; epi.rm_Hh = Hh; epi.rm_Wh = Wh; epi.rm_st = stride; epi.rm_ph = ph; epi.rm_pw = pw;
         epi.rm_H = H; epi.rm_W = W;

@@ -12,6 +12,7 @@ import torch.nn.functional as F
 
 from .._native import C
 from ..parallel.flat import grad_target
+from .grad_join import MaskedGrad
 
 
 def _ref_conv(x, w, stride, padding, dilation, bias=None):
@@ -49,7 +50,10 @@ class _Conv2dFn(torch.autograd.Function):
                 join.stash(C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation, None))
             else:
                 addend = join.take() if join is not None else None
-                dx = C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation, addend)
+                bits = None
+                if isinstance(addend, MaskedGrad):  # residual gradient = dz * ReLU mask, applied in the epilogue
+                    addend, bits = addend.grad, addend.bits
+                dx = C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation, addend, bits)
         if ctx.needs_input_grad[1]:
             dw = C().conv_wgrad(dy, x, w.shape[1], w.shape[2], stride, padding, dilation, w.dtype == torch.float32,
                                 grad_target(ctx.wparam))

@@ -10,9 +10,31 @@ output — for conv1's dgrad, as the epilogue addend of the MFMA kernel.
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import Optional, Union
 
 import torch
+
+
+class MaskedGrad:
+    """A gradient held as ``grad * mask`` without materialising it: ``grad`` (bf16) and the ReLU bit
+    mask ``bits`` (uint8, bit j of byte v masks element 8v + j) written by the BN+residual+ReLU
+    forward.  A bottleneck's residual-branch gradient is exactly this (dres = dz * relu_mask), so the
+    BN backward skips writing dres and conv1's dgrad epilogue reads dz + the 1-bit mask instead
+    (one full-activation store fewer per identity block)."""
+
+    __slots__ = ("grad", "bits")
+
+    def __init__(self, grad: torch.Tensor, bits: torch.Tensor):
+        self.grad, self.bits = grad, bits
+
+    def materialize(self) -> torch.Tensor:
+        shifts = torch.arange(8, device=self.bits.device, dtype=torch.uint8)
+        mask = ((self.bits.reshape(-1, 1) >> shifts) & 1).bool().reshape(self.grad.shape)
+        return torch.where(mask, self.grad, torch.zeros((), dtype=self.grad.dtype, device=self.grad.device))
+
+
+def _dense(g):
+    return g.materialize() if isinstance(g, MaskedGrad) else g
 
 
 class GradJoin:
@@ -25,17 +47,18 @@ class GradJoin:
         """True when the calling consumer is the last one still to contribute."""
         return self.arrived == self.consumers - 1
 
-    def take(self) -> Optional[torch.Tensor]:
-        """Last contributor: the accumulated gradient of the others (None if they contributed zero)."""
+    def take(self) -> Optional[Union[torch.Tensor, MaskedGrad]]:
+        """Last contributor: the accumulated gradient of the others (None if they contributed zero);
+        a :class:`MaskedGrad` when a single masked contribution is pending."""
         p = self.pending
         self.pending = None
         self.arrived = 0  # ready for a second backward over the same graph
         return p
 
-    def stash(self, g: Optional[torch.Tensor]):
+    def stash(self, g: Optional[Union[torch.Tensor, MaskedGrad]]):
         """Non-last contributor: keep ``g`` for the last one; the caller returns None to autograd."""
         if g is not None:
-            self.pending = g if self.pending is None else self.pending + g
+            self.pending = g if self.pending is None else _dense(self.pending) + _dense(g)
         self.arrived += 1
 
     def contribute(self, g: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
@@ -45,5 +68,5 @@ class GradJoin:
             return None
         p = self.take()
         if p is None:
-            return g
-        return p if g is None else g + p
+            return _dense(g)
+        return _dense(p) if g is None else _dense(g) + _dense(p)

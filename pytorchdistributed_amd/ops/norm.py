@@ -11,6 +11,7 @@ import torch.nn.functional as F
 
 from .._native import C
 from ..parallel.flat import grad_target
+from .grad_join import MaskedGrad
 
 
 class _BatchNormFn(torch.autograd.Function):
@@ -53,11 +54,19 @@ class _BatchNormFn(torch.autograd.Function):
         tb = grad_target(ctx.beta) if ctx.beta is not None and ctx.needs_input_grad[2] else None
         if (tg is None) != (tb is None):
             tg = tb = None
-        dx, dres, dgamma, dbeta = C().bn_bwd(dy.contiguous(), x, bits, ss, mean, invstd, gamma, relu, has_res, tg,
+        dy = dy.contiguous()
+        # residual gradient of a bottleneck whose shortcut gradient joins conv1's dgrad (not the last
+        # contributor): dres = dy * relu_mask is handed over as (dy, bits) and applied in that conv's
+        # epilogue, so the backward apply kernel never stores it
+        masked = has_res and ctx.join is not None and bits is not None and not ctx.join.is_last()
+        dx, dres, dgamma, dbeta = C().bn_bwd(dy, x, bits, ss, mean, invstd, gamma, relu, has_res and not masked, tg,
                                              tb)
         dg = dgamma if gamma is not None and ctx.needs_input_grad[1] else None
         db = dbeta if ctx.needs_input_grad[2] else None
-        if has_res and ctx.join is not None:
+        if masked:
+            ctx.join.stash(MaskedGrad(dy, bits))
+            dres = None
+        elif has_res and ctx.join is not None:
             dres = ctx.join.contribute(dres)  # usually stashed for the consumer conv's dgrad epilogue
         return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None, None, None, None, None
 

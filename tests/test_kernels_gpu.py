@@ -178,6 +178,11 @@ def test_conv_fwd_dgrad_wgrad(case):
     add = torch.randn(N, H, W, Cin).to(torch.bfloat16)
     dx2 = C().conv_dgrad(bf(dy), bf(w.detach()), H, W, s, p, d, add.to(DEV))  # fused gradient accumulation
     assert rel_err(dx2.cpu(), x.grad + add.float()) < 1e-2
+    # bit-masked addend (a bottleneck's residual gradient dz * relu_mask read from dz + the 1-bit mask)
+    mask = torch.rand(N, H, W, Cin) > 0.5
+    bits = (mask.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(1).to(torch.uint8)
+    dx3 = C().conv_dgrad(bf(dy), bf(w.detach()), H, W, s, p, d, add.to(DEV), bits.to(DEV))
+    assert rel_err(dx3.cpu(), x.grad + add.float() * mask) < 1e-2
     dw = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, d, True, None)
     assert rel_err(dw.cpu(), w.grad) < 1e-3
     dwb = C().conv_wgrad(bf(dy), bf(x.detach()), k, k, s, p, d, False, None)
@@ -491,3 +496,25 @@ def test_synth_fill_statistics():
     i = torch.empty(100000, device=DEV, dtype=torch.long)
     C().fill_randint(i, 1, 0, 0, 1000)
     assert i.min().item() >= 0 and i.max().item() < 1000
+
+
+@pytest.mark.parametrize("wide", [0, 2])
+@pytest.mark.parametrize("case", [(4, 28, 28, 256, 64, 1, 1, 0), (2, 14, 14, 512, 256, 3, 1, 1)])
+def test_conv_dgrad_masked_addend_paths(case, wide):
+    """dx = dgrad + addend * mask on the 128-tile and the wide 256x256-tile epilogues (the bottleneck's
+    conv1 dgrad joining the residual gradient dz * relu_mask)."""
+    N, H, W, Cin, Cout, k, s, p = case
+    torch.manual_seed(3)
+    w = (torch.randn(Cout, k, k, Cin) / math.sqrt(Cin * k * k)).to(torch.bfloat16)
+    dy = torch.randn(N, H, W, Cout).to(torch.bfloat16)
+    add = torch.randn(N, H, W, Cin).to(torch.bfloat16)
+    mask = torch.rand(N, H, W, Cin) > 0.3
+    bits = (mask.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(1).to(torch.uint8)
+    C().set_gemm_paths(wide)
+    try:
+        dx = C().conv_dgrad(dy.to(DEV), w.to(DEV), H, W, s, p, 1, add.to(DEV), bits.to(DEV))
+        dx0 = C().conv_dgrad(dy.to(DEV), w.to(DEV), H, W, s, p, 1, None, None)
+    finally:
+        C().set_gemm_paths(-1)
+    ref = dx0.float().cpu() + add.float() * mask
+    assert rel_err(dx.cpu(), ref) < 1e-2

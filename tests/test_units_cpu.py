@@ -265,3 +265,24 @@ def test_optimizer_device_step_counter_bookkeeping():
     opt.state[p]["step"] = 2
     opt.advance_steps(5)
     assert opt.state[p]["step"] == 7 and opt._dstep[dev][0] == 7
+
+
+def test_grad_join_masked_grad():
+    """A MaskedGrad stashed in a GradJoin (bottleneck residual gradient dz * relu_mask, kept as dz + bits)
+    materialises to the dense masked gradient on every generic path."""
+    from pytorchdistributed_amd.ops.grad_join import GradJoin, MaskedGrad
+
+    torch.manual_seed(0)
+    dz = torch.randn(2, 3, 4, 8)
+    mask = torch.rand(2, 3, 4, 8) > 0.5
+    bits = (mask.reshape(-1, 8).to(torch.uint8) << torch.arange(8, dtype=torch.uint8)).sum(1).to(torch.uint8)
+    mg = MaskedGrad(dz, bits)
+    assert torch.equal(mg.materialize(), dz * mask)
+    j = GradJoin(2)
+    j.stash(mg)
+    other = torch.randn_like(dz)
+    assert torch.allclose(j.contribute(other), other + dz * mask)
+    j3 = GradJoin(3)
+    j3.stash(mg)
+    j3.stash(other)
+    assert torch.allclose(j3.take(), other + dz * mask)
