@@ -29,6 +29,30 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 constexpr int NT = 256;
 constexpr int BQ = 64, BKV = 64;
 constexpr float LOG2E = 1.4426950408889634f;
+// finite "minus infinity" for running maxima: exp2(c * (m_old - m_new)) stays exact when a row has
+// seen only masked keys so far (no inf - inf, no per-element "dead row" select)
+constexpr float NEG_BIG = -1e30f;
+
+// v_exp_f32 directly (HIP's exp2f adds a denormal-range fix-up: ldexp + compare + select per call);
+// every argument here is a max-shifted log2-domain score <= 0, where the bare instruction is exact
+// enough and underflows to 0 as wanted.
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Reductions across the lanes l ^ 16 and l ^ 32 (the 4 lanes that hold one query's keys in the S
+// accumulator layout) with the CDNA4 permlane swaps: each returns {own, partner} in some order, so a
+// max / sum of the pair is the butterfly step without an LDS round trip (ds_bpermute).
+__device__ __forceinline__ float max_x16_x32(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float sum_x16_x32(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
 
 // ---------------------------------------------------------------- LDS images (rows of D bf16)
 // row image (for ds_read_b128 of 8 consecutive columns of one row)
@@ -535,7 +559,9 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd2_kernel(AttnParams p) {
     qf1[ks] = load_frag_global(qb, p.q_st, qrow1, T, ks, lane);
   }
   const float c = p.scale * LOG2E;
-  float m0 = -INFINITY, l0 = 0.f, m1 = -INFINITY, l1 = 0.f;
+  // m: running row max of the RAW scores (scale folded into the exponent's fma); l: this lane's
+  // partial row sum (its 16 of every 64 keys) — the 4 lanes of a query are summed once at the end
+  float m0 = NEG_BIG, l0 = 0.f, m1 = NEG_BIG, l1 = 0.f;
   f32x4 o0[DT], o1[DT];
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) o0[dt] = o1[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -563,36 +589,33 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd2_kernel(AttnParams p) {
     }
     const bool need_mask = kv0 + BKV > T || (p.causal && kv0 + BKV - 1 > qbase);
     auto softmax = [&](f32x4 (&s)[4], int qrow, float& m, float& l, f32x4 (&o)[DT]) {
-      float mx = -INFINITY;
+      float mx = NEG_BIG;
+      if (need_mask) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int kv = kv0 + 16 * t + 4 * g + r;
+            if (kv >= T || (p.causal && kv > qrow)) s[t][r] = -INFINITY;
+          }
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = s[t][r] * c;
-          if (need_mask) {
-            const int kv = kv0 + 16 * t + 4 * g + r;
-            if (kv >= T || (p.causal && kv > qrow)) v = -INFINITY;
-          }
-          s[t][r] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m, mx);
-      const bool dead = m_new == -INFINITY;
-      const float alpha = dead ? 1.f : exp2f(m - m_new);
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[t][r]);
+      const float m_new = fmaxf(m, max_x16_x32(mx));
+      const float alpha = fast_exp2((m - m_new) * c);
+      const float mc = m_new * c;
       float rs = 0.f;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = dead ? 0.f : exp2f(s[t][r] - m_new);
+          const float e = fast_exp2(fmaf(s[t][r], c, -mc));
           s[t][r] = e;
           rs += e;
         }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
-      l = l * alpha + rs;
+      l = fmaf(l, alpha, rs);
       m = m_new;
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
@@ -612,6 +635,7 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd2_kernel(AttnParams p) {
     }
   }
   auto epilogue = [&](int qrow, float m, float l, const f32x4 (&o)[DT]) {
+    l = sum_x16_x32(l);  // (all lanes take part: the swaps need a full EXEC)
     if (qrow >= T) return;
     const float inv = l > 0.f ? 1.f / l : 0.f;
     bf16_t* ob = p.o + b * p.o_sb + (int64_t)qrow * p.o_st + h * p.o_sh;
@@ -622,7 +646,7 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd2_kernel(AttnParams p) {
       for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][r] * inv);
       *reinterpret_cast<u16x4*>(ob + 16 * dt + 4 * g) = v;
     }
-    if (g == 0) p.lse[((int64_t)b * p.Hq + h) * T + qrow] = (m + log2f(l)) / LOG2E;
+    if (g == 0) p.lse[((int64_t)b * p.Hq + h) * T + qrow] = (m * c + log2f(l)) / LOG2E;
   };
   epilogue(qrow0, m0, l0, o0);
   epilogue(qrow1, m1, l1, o1);
@@ -685,7 +709,7 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float pr = exp2f(s[t][r] * c - lse2);
+        float pr = fast_exp2(fmaf(s[t][r], c, -lse2));
         if (need_mask) {
           const int kv = kv0 + 16 * t + 4 * g + r;
           if (qrow >= T || kv >= T || (p.causal && kv > qrow)) pr = 0.f;
@@ -786,7 +810,7 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qi = 16 * t + 4 * g + r;
-        float pr = exp2f(s[t][r] * c - s_lse[qi]);
+        float pr = fast_exp2(fmaf(s[t][r], c, -s_lse[qi]));
         if (need_mask) {
           const int q = q0 + qi;
           if (q >= T || kvrow >= T || (p.causal && kvrow > q)) pr = 0.f;

@@ -1,0 +1,14 @@
+#!/bin/bash
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+tag=${1:-v1}
+step() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > gpurun_out/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -3 gpurun_out/$name.log | cut -c1-400
+  if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
+}
+step pytest_attn 300 python -u -m pytest tests/test_attention_gpu.py -q -x -p no:cacheprovider --timeout 120 --timeout-method thread
+step attn_$tag 240 python tools/bench_attn.py --no-torch
