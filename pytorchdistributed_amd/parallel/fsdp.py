@@ -5,19 +5,26 @@ Per *unit* (every submodule whose type is in ``unit_types`` — e.g. each transf
 root unit holding the remaining parameters):
 
 * the unit's parameters are flattened (16-byte aligned, padded to a multiple of the world size) and
-  each rank keeps ONE fp32 shard, which is the ``nn.Parameter`` the optimizer sees (fused AdamW updates
-  it in one launch per unit);
-* before the unit's forward the bf16 copy of the shard is all-gathered (RCCL over xGMI) into a
-  ``requires_grad`` flat leaf; the module's parameters become views into it, so autograd accumulates
-  the whole unit's gradient into ONE flat buffer;
+  each rank keeps ONE shard in the compute dtype, which is the ``nn.Parameter`` the optimizer sees:
+  the fused AdamW keeps the fp32 master of the shard and writes the bf16 shard in the same launch, so
+  the shard is all-gathered as is (no per-step cast kernel);
+* the module's parameters become persistent leaf tensors whose storage is a view of the unit's
+  gathered flat buffer; before the unit's forward the shard is all-gathered (RCCL over xGMI) into
+  that buffer (at world 1 the buffer IS the shard: nothing is copied);
+* every leaf's gradient lands in its slot of ONE flat gradient buffer per unit — the native
+  conv/linear/norm/embedding backward kernels write it there directly (``flat.grad_target``), any
+  other op's gradient is copied in by the leaf's post-accumulate hook — so there is no autograd
+  ``cat`` of the unit's gradients and no fp32 round trip;
 * after forward the gathered storage is released (``reshard_after_forward``) and re-gathered in place
   when the unit's backward starts (hook on the unit output), so saved views see the right bytes;
-* when the flat gradient is complete it is reduce-scattered (average) straight into the shard's grad
-  and the full buffers are freed; the next unit's all-gather is prefetched while the current unit
-  computes (forward order recorded on the first iteration, reversed for backward).
+* when the unit's last leaf gradient arrived the flat gradient is reduce-scattered (average) straight
+  into the shard's grad; the next unit's all-gather is prefetched while the current unit computes
+  (forward order recorded on the first iteration, reversed for backward).
 
-Memory per rank for Llama-3 8B: 8.03e9 x (4 B master + 8 B Adam) / 8 ~= 12 GB + gathered units in
-flight, a small fraction of the 288 GB HBM, so prefetch depth is not memory-limited.
+Memory per rank for Llama-3 8B: 8.03e9 x (2 B shard + 4 B master + 8 B Adam) / 8 ~= 14 GB, plus the
+persistent full-size gradient buffers (16 GB bf16) and the gathered units in flight: a small fraction
+of the 288 GB HBM, so neither prefetch depth nor ``reshard_after_forward=False`` (no backward
+re-gather) is memory-limited.
 Checkpoints: :meth:`full_state_dict` (rank-0 consolidated, original names) and
 :meth:`sharded_state_dict` / :meth:`load_sharded_state_dict` (``shard_{rank:05d}.pt`` + ``meta.json``).
 """
@@ -54,86 +61,108 @@ class _Unit:
             off += _round(p.numel(), ALIGN)
         W = fsdp.world
         self.numel = _round(max(off, 1), W * ALIGN)
-        # split sizes [param0, pad0, param1, pad1, ..., tail]: one SplitBackward node concatenates the
-        # whole unit's gradient (slicing each view separately would materialise a full-size zero
-        # tensor per parameter in backward)
-        self.split_sizes = []
-        for (_o, _n, _s, o, n) in self.entries:
-            self.split_sizes += [n, _round(n, ALIGN) - n]
-        self.split_sizes.append(self.numel - off)
         self.shard_numel = self.numel // W
         full = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         for (owner, name, shape, o, n) in self.entries:
             full[o: o + n].copy_(getattr(owner, name).detach().reshape(-1).float())
         r = fsdp.rank
-        self.shard = tnn.Parameter(full[r * self.shard_numel: (r + 1) * self.shard_numel].clone())
+        self.shard = tnn.Parameter(full[r * self.shard_numel: (r + 1) * self.shard_numel].to(fsdp.shard_dtype,
+                                                                                              copy=True))
+        del full
         for (owner, name, *_rest) in self.entries:
             del owner._parameters[name]
-        self.flat: Optional[torch.Tensor] = None  # gathered leaf (compute dtype)
-        self.gathered = False
+        # world 1 with a compute-dtype shard: the shard itself is the gathered buffer (no copy, never freed)
+        self.alias = W == 1 and fsdp.shard_dtype == fsdp.param_dtype
+        self.flat = self.shard.detach() if self.alias else torch.empty(self.numel, dtype=fsdp.param_dtype,
+                                                                       device=self.device)
+        # flat gradient buffer (padding stays zero; every slot is fully rewritten each backward)
+        self.grad_buffer = torch.zeros(self.numel, dtype=fsdp.param_dtype, device=self.device)
+        self.arrived = 0
+        # persistent leaf tensors (plain tensors, not registered Parameters: the optimizer sees only the
+        # shard) viewing the gathered buffer; `_pda_flat` routes native backward kernels to the grad slot
+        self.leaves: List[torch.Tensor] = []
+        for (owner, name, shape, o, n) in self.entries:
+            # (`.data =` gives the leaf the view's storage but its OWN version counter: re-filling the
+            # gathered buffer in place is not an update of the parameter as far as saved tensors go)
+            leaf = torch.empty(0, dtype=fsdp.param_dtype, device=self.device).requires_grad_(True)
+            leaf.data = self.flat[o: o + n].view(shape)
+            leaf._pda_flat = (self, o)
+            leaf.register_post_accumulate_grad_hook(self._make_leaf_hook(o, n, shape))
+            setattr(owner, name, leaf)
+            self.leaves.append(leaf)
+        self.gathered = self.alias
+        if not self.alias:
+            self.flat.untyped_storage().resize_(0)
         self.pending_ag = None
-        self.send_buf = None
-        # compute-dtype copy of the shard, made by the forward gather and reused by the backward
-        # re-gather of the same step (one cast per step instead of two).  Invalidated at every
-        # forward entry: fused optimizers update the shard through raw pointers, which does not
-        # bump its autograd version counter.
+        # compute-dtype copy of an fp32 shard, made by the forward gather and reused by the backward
+        # re-gather of the same step.  Invalidated at every forward entry: fused optimizers update the
+        # shard through raw pointers, which does not bump its autograd version counter.
         self._cast = None
 
+    def _make_leaf_hook(self, o: int, n: int, shape):
+        def hook(t: torch.Tensor):
+            slot = self.grad_buffer[o: o + n]
+            g = t.grad
+            if g is not None and g.data_ptr() != slot.data_ptr():
+                slot.view(shape).copy_(g)
+            t.grad = None  # the slot holds it; a None .grad lets the next backward write in place again
+            t._pda_claimed = False
+            t._pda_seen = True
+            self.arrived += 1
+            if self.arrived == len(self.leaves):
+                self.fsdp._grad_ready(self)
+        return hook
+
+    def flush_missing(self):
+        """Backward ended with some leaves unused: zero their slots and reduce-scatter anyway (every
+        rank runs the same graph, so the collectives still match)."""
+        if 0 < self.arrived < len(self.leaves):
+            # leaves whose hook did not fire still hold an earlier step's slot contents
+            fired = set()
+            for leaf, (_o, _n, _s, o, n) in zip(self.leaves, self.entries):
+                if getattr(leaf, "_pda_seen", False):
+                    fired.add(o)
+            for (_o, _n, _s, o, n) in self.entries:
+                if o not in fired:
+                    self.grad_buffer[o: o + n].zero_()
+            self.arrived = len(self.leaves)
+            self.fsdp._grad_ready(self)
+
     def _send_buffer(self) -> torch.Tensor:
-        if self._cast is None:
-            if self.shard.dtype == self.fsdp.param_dtype:
-                self._cast = self.shard.detach()
-            else:
-                self._cast = self.shard.detach().to(self.fsdp.param_dtype)
+        if self.shard.dtype == self.fsdp.param_dtype:
+            return self.shard.detach()
+        if self._cast is None:  # fp32 shards (shard_dtype=float32): one cast per step, reused by backward
+            self._cast = self.shard.detach().to(self.fsdp.param_dtype)
         return self._cast
 
     # ------------------------------------------------------------ gather / reshard
-    def _alloc(self):
-        if self.flat is None:
-            self.flat = torch.empty(self.numel, dtype=self.fsdp.param_dtype, device=self.device, requires_grad=True)
-            self.flat.register_post_accumulate_grad_hook(lambda t: self.fsdp._grad_ready(self))
-        elif self.flat.untyped_storage().size() == 0:
-            self.flat.untyped_storage().resize_(self.numel * self.flat.element_size())
-
     def start_gather(self):
         if self.gathered or self.pending_ag is not None:
             return
-        self._alloc()
-        # Re-filling the gathered storage is not a semantic in-place update of the parameters (the
-        # bytes are the same ones the forward saw), so the autograd version counter is restored:
-        # saved views of this buffer stay valid for backward.
-        version = self.flat._version
+        if self.flat.untyped_storage().size() == 0:
+            self.flat.untyped_storage().resize_(self.numel * self.flat.element_size())
         with torch.no_grad():
-            self.send_buf = self._send_buffer()
+            send = self._send_buffer()
             if self.fsdp.world == 1:
-                self.flat.detach().copy_(self.send_buf)
-                self.pending_ag = None
+                self.flat.copy_(send)
                 self.gathered = True
             else:
-                self.pending_ag = dist.all_gather_into_tensor(self.flat.detach(), self.send_buf,
-                                                              group=self.fsdp.group, async_op=True)
-        self._version = version
-        torch._C._autograd._unsafe_set_version_counter((self.flat,), (version,))
+                self.pending_ag = dist.all_gather_into_tensor(self.flat, send, group=self.fsdp.group,
+                                                              async_op=True)
 
     def finish_gather(self):
         if self.pending_ag is not None:
             self.pending_ag.wait()
             self.pending_ag = None
             self.gathered = True
-            torch._C._autograd._unsafe_set_version_counter((self.flat,), (self._version,))
         elif not self.gathered:
             self.start_gather()
             self.finish_gather()
-            return
-        self.send_buf = None
-
-    def bind_views(self):
-        pieces = self.flat.split(self.split_sizes)
-        for i, (owner, name, shape, o, n) in enumerate(self.entries):
-            setattr(owner, name, pieces[2 * i].view(shape))
 
     def reshard(self):
-        if self.flat is not None and self.gathered:
+        if self.alias:
+            return
+        if self.gathered:
             self.flat.untyped_storage().resize_(0)
         self.gathered = False
 
@@ -141,13 +170,18 @@ class _Unit:
 class FullyShardedDataParallel(tnn.Module):
     def __init__(self, module: tnn.Module, process_group=None, unit_types: Sequence[type] = (),
                  param_dtype: Optional[torch.dtype] = None, reshard_after_forward: bool = True,
-                 prefetch: bool = True):
+                 prefetch: bool = True, shard_dtype: Optional[torch.dtype] = None):
+        """``param_dtype``: compute dtype of the gathered parameters (default: the module's).
+        ``shard_dtype``: dtype of the sharded ``nn.Parameter`` the optimizer updates (default: the
+        compute dtype — the fused optimizers then keep fp32 masters themselves and write the shard in
+        the same launch; ``torch.float32`` keeps fp32 shards and casts them once per step)."""
         super().__init__()
         self.module = module
         self.group = process_group
         self.world = pdist.get_world_size(process_group)
         self.rank = pdist.get_rank(process_group)
         self.param_dtype = param_dtype or next(module.parameters()).dtype
+        self.shard_dtype = shard_dtype or self.param_dtype
         self.reshard_after_forward = reshard_after_forward
         self.prefetch = prefetch
         self.nccl = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
@@ -202,7 +236,6 @@ class FullyShardedDataParallel(tnn.Module):
             if not self._order_frozen:
                 self._fwd_order.append(u)
             u.finish_gather()
-            u.bind_views()
             if self.prefetch:
                 nxt = self._next_in_order(u, backward=False)
                 if nxt is not None:
@@ -238,19 +271,22 @@ class FullyShardedDataParallel(tnn.Module):
     # ------------------------------------------------------------ gradient reduce-scatter
     def _grad_ready(self, u: _Unit):
         self._finish_rs()
-        grad_full = u.flat.grad
-        u.flat.grad = None
+        grad_full = u.grad_buffer
         if self.world == 1:
+            # the shard's gradient IS the flat gradient buffer (no copy); the slots were just rewritten,
+            # so a gradient still held from an earlier backward cannot be accumulated into
+            if u.shard.grad is not None and u.shard.grad.data_ptr() == grad_full.data_ptr():
+                raise RuntimeError("FSDP at world size 1 does not accumulate gradients across backward "
+                                   "passes: call zero_grad(set_to_none=True) between steps")
             out, work = grad_full, None
         else:
             out = torch.empty(u.shard_numel, dtype=grad_full.dtype, device=grad_full.device)
-        if self.world == 1:
-            pass
-        elif self.nccl:
-            work = dist.reduce_scatter_tensor(out, grad_full, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
-        else:
-            work = dist.reduce_scatter_tensor(out, grad_full, group=self.group, async_op=True)
-        self._pending_rs = (u, work, out, grad_full)
+            if self.nccl:
+                work = dist.reduce_scatter_tensor(out, grad_full, op=dist.ReduceOp.AVG, group=self.group,
+                                                  async_op=True)
+            else:
+                work = dist.reduce_scatter_tensor(out, grad_full, group=self.group, async_op=True)
+        self._pending_rs = (u, work, out)
         if u is not self.root_unit:
             u.reshard()
         if not self._callback_queued:
@@ -260,13 +296,13 @@ class FullyShardedDataParallel(tnn.Module):
     def _finish_rs(self):
         if self._pending_rs is None:
             return
-        u, work, out, _grad_full = self._pending_rs
+        u, work, out = self._pending_rs
         self._pending_rs = None
         if work is not None:
             work.wait()
         if not self.nccl and self.world > 1:
             out.div_(self.world)
-        g = out.float()
+        g = out if out.dtype == u.shard.dtype else out.to(u.shard.dtype)
         if u.shard.grad is None:
             u.shard.grad = g
         else:
@@ -274,9 +310,14 @@ class FullyShardedDataParallel(tnn.Module):
 
     def _post_backward_final(self):
         self._callback_queued = False
+        for u in self.units:
+            u.flush_missing()
         self._finish_rs()
         for u in self.units:
             u.reshard()
+            u.arrived = 0
+            for leaf in u.leaves:
+                leaf._pda_seen = False
         self._order_frozen = True
 
     # ------------------------------------------------------------ module API
@@ -285,7 +326,6 @@ class FullyShardedDataParallel(tnn.Module):
             u._cast = None
         if self.root_unit is not None:
             self.root_unit.finish_gather()
-            self.root_unit.bind_views()
         if self._order_frozen and self.prefetch and self._fwd_order:
             self._fwd_order[0].start_gather()
         out = self.module(*args, **kwargs)
@@ -299,11 +339,12 @@ class FullyShardedDataParallel(tnn.Module):
         """All-gather every unit; returns {original name: fp32 tensor} (on every rank)."""
         out = {}
         for u, names in zip(self.units, self.names):
-            full = torch.empty(u.numel, dtype=torch.float32, device=u.device)
+            full = torch.empty(u.numel, dtype=u.shard.dtype, device=u.device)
             if self.world == 1:
                 full.copy_(u.shard)
             else:
                 dist.all_gather_into_tensor(full, u.shard.detach(), group=self.group)
+            full = full.float()
             for (owner, name, shape, o, n), full_name in zip(u.entries, names):
                 out[full_name] = full[o: o + n].view(shape).clone().cpu()
         return out

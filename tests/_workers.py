@@ -305,3 +305,45 @@ def ddp_resnet_gpu_worker(rank, world, outdir):
     with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
         f.write(f"ok {worst[0]:.3e} buckets={model.reducer.num_buckets}")
     pd.destroy_process_group()
+
+
+def fsdp_llama_gpu_worker(rank, world, outdir):
+    """FSDP (bf16 shards, fused AdamW with fp32 masters, gradients written into the units' flat buffers)
+    on a tiny Llama, `world` ranks sharing cuda:0 (gloo when world > 1): after 2 steps the consolidated
+    parameters match an unsharded replica trained on the concatenated batch."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.models.llama import Llama, LlamaBlock, config
+    from pytorchdistributed_amd.optim import AdamW
+    from pytorchdistributed_amd.parallel.fsdp import FullyShardedDataParallel
+
+    torch.cuda.set_device(0)
+    if world > 1:
+        pd.init_process_group("gloo")
+    torch.manual_seed(0)
+    cfg = config("llama3-tiny", dim=256, n_heads=2, n_kv_heads=1, ffn_dim=512)
+    ref = Llama(cfg, device="cuda", dtype=torch.bfloat16)
+    model = Llama(cfg, device="cuda", dtype=torch.bfloat16)
+    model.load_state_dict(ref.state_dict())
+    fsdp = FullyShardedDataParallel(model, unit_types=(LlamaBlock,))
+    opt = AdamW(fsdp.parameters(), lr=1e-3, weight_decay=0.1)
+    ropt = AdamW(ref.parameters(), lr=1e-3, weight_decay=0.1)
+    g = torch.Generator().manual_seed(5)
+    for _ in range(2):
+        idx = torch.randint(0, cfg.vocab_size, (world * 2, 64), generator=g).cuda()
+        tgt = torch.randint(0, cfg.vocab_size, (world * 2, 64), generator=g).cuda()
+        opt.zero_grad(set_to_none=True)
+        fsdp(idx[rank * 2:(rank + 1) * 2], tgt[rank * 2:(rank + 1) * 2]).backward()
+        opt.step()
+        ropt.zero_grad(set_to_none=True)
+        ref(idx, tgt).backward()
+        ropt.step()
+    sd = fsdp.full_state_dict()
+    worst = (0.0, "")
+    for n, p in ref.named_parameters():
+        a, b = sd[n].float(), p.detach().float().cpu()
+        worst = max(worst, (((a - b).norm() / b.norm()).item(), n))
+    assert worst[0] < 2e-2, worst
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+        f.write(f"ok {worst[0]:.3e}")
+    if world > 1:
+        pd.destroy_process_group()

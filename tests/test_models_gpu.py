@@ -142,3 +142,15 @@ def test_ddp_resnet50_two_ranks_share_gpu(tmp_path):
     spawn(_workers.ddp_resnet_gpu_worker, args=(2, str(tmp_path)), nprocs=2, timeout=300)
     for r in range(2):
         assert (tmp_path / f"ok{r}").read_text().startswith("ok")
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_fsdp_llama_tiny_matches_unsharded(tmp_path, world):
+    """FSDP on the native transformer path: world 1 (the shard aliases the gathered buffer) and world 2
+    (two ranks sharing the GPU over gloo: all-gather / reduce-scatter of bf16 shards)."""
+    import _workers
+    from pytorchdistributed_amd.launch import spawn
+
+    spawn(_workers.fsdp_llama_gpu_worker, args=(world, str(tmp_path)), nprocs=world, timeout=300)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}").read_text().startswith("ok")
