@@ -652,10 +652,11 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd2_kernel(AttnParams p) {
   epilogue(qrow1, m1, l1, o1);
 }
 
-// dQ, query-stationary, prefetched K/V tiles (16 query rows per wave, BQ = 64)
-template <int D>
+// dQ, query-stationary, prefetched K/V tiles; QG query groups of 16 rows per wave (query tile =
+// 64 * QG): every K / V fragment read from LDS feeds QG MFMAs.
+template <int D, int QG>
 __global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
-  constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2;
+  constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2, BQW = BQ * QG;
   __shared__ __attribute__((aligned(16))) char smem[3 * IMG];
   char* Kr = smem;
   char* Kt = smem + IMG;
@@ -664,26 +665,32 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
   const int qt = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int hk = h / (p.Hq / p.Hkv);
   const int T = p.T;
-  const int qbase = qt * BQ + w * 16;
-  const int qrow = qbase + (lane & 15);
+  const int qbase = qt * BQW + w * 16 * QG;  // this wave's queries: qbase + 16 qg + (lane & 15)
   const bf16_t* qb = p.q + b * p.q_sb + h * p.q_sh;
   const bf16_t* dob = p.dout + b * p.do_sb + h * p.do_sh;
   const bf16_t* kb = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* vb = p.v + b * p.v_sb + hk * p.v_sh;
-  mbf16x8 qf[KS], df[KS];
+  mbf16x8 qf[QG][KS], df[QG][KS];
+  float lse2[QG], dl[QG];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    qf[ks] = load_frag_global(qb, p.q_st, qrow, T, ks, lane);
-    df[ks] = load_frag_global(dob, p.do_st, qrow, T, ks, lane);
+  for (int qg = 0; qg < QG; ++qg) {
+    const int qrow = qbase + 16 * qg + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      qf[qg][ks] = load_frag_global(qb, p.q_st, qrow, T, ks, lane);
+      df[qg][ks] = load_frag_global(dob, p.do_st, qrow, T, ks, lane);
+    }
+    const int64_t rowid = ((int64_t)b * p.Hq + h) * T + qrow;
+    lse2[qg] = qrow < T ? p.lse[rowid] * LOG2E : 0.f;
+    dl[qg] = qrow < T ? p.delta[rowid] : 0.f;
   }
-  const int64_t rowid = ((int64_t)b * p.Hq + h) * T + qrow;
-  const float lse2 = qrow < T ? p.lse[rowid] * LOG2E : 0.f;
-  const float dl = qrow < T ? p.delta[rowid] : 0.f;
   const float c = p.scale * LOG2E;
-  f32x4 dq[DT];
+  f32x4 dq[QG][DT];
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int kv_end = p.causal ? min(T, (qt + 1) * BQ) : T;
+  for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) dq[qg][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kv_end = p.causal ? min(T, (qt + 1) * BQW) : T;
   const int ntiles = (kv_end + BKV - 1) / BKV;
   TileRegs<D> tr;
   fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, 0, T);
@@ -693,53 +700,75 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
     store_tile<D>(tr, Kr, Kt, Vr, nullptr);
     __syncthreads();
     if (j + 1 < ntiles) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, kv0 + BKV, T);
-    if (p.causal && kv0 > qbase + 15) continue;
-    f32x4 s[4], dp[4];
+    if (p.causal && kv0 > qbase + 16 * QG - 1) continue;  // every key of this tile is in this wave's future
+    f32x4 s[QG][4], dp[QG][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      s[t] = dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) s[qg][t] = dp[qg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        s[t] = mfma(frag_row<D>(Kr, 16 * t, ks, lane), qf[ks], s[t]);
-        dp[t] = mfma(frag_row<D>(Vr, 16 * t, ks, lane), df[ks], dp[t]);
-      }
-    }
-    const bool need_mask = kv0 + BKV > T || (p.causal && kv0 + BKV - 1 > qbase) || qrow >= T;
+        const mbf16x8 kf = frag_row<D>(Kr, 16 * t, ks, lane);
+        const mbf16x8 vf = frag_row<D>(Vr, 16 * t, ks, lane);
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float pr = fast_exp2(fmaf(s[t][r], c, -lse2));
-        if (need_mask) {
-          const int kv = kv0 + 16 * t + 4 * g + r;
-          if (qrow >= T || kv >= T || (p.causal && kv > qrow)) pr = 0.f;
+        for (int qg = 0; qg < QG; ++qg) {
+          s[qg][t] = mfma(kf, qf[qg][ks], s[qg][t]);
+          dp[qg][t] = mfma(vf, df[qg][ks], dp[qg][t]);
         }
-        s[t][r] = pr * (dp[t][r] - dl);
       }
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
-      const mbf16x8 sf = pack_p(s[2 * cc], s[2 * cc + 1]);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma(frag_tr<D>(Kt, 32 * cc, 16 * dt, lane), sf, dq[dt]);
     }
+    const bool need_mask = kv0 + BKV > T || (p.causal && kv0 + BKV - 1 > qbase) || qbase + 16 * QG > T;
+#pragma unroll
+    for (int qg = 0; qg < QG; ++qg) {
+      const int qrow = qbase + 16 * qg + (lane & 15);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float pr = fast_exp2(fmaf(s[qg][t][r], c, -lse2[qg]));
+          if (need_mask) {
+            const int kv = kv0 + 16 * t + 4 * g + r;
+            if (qrow >= T || kv >= T || (p.causal && kv > qrow)) pr = 0.f;
+          }
+          s[qg][t][r] = pr * (dp[qg][t][r] - dl[qg]);
+        }
+    }
+    mbf16x8 sf[2][QG];
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) sf[cc][qg] = pack_p(s[qg][2 * cc], s[qg][2 * cc + 1]);
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const mbf16x8 ktf = frag_tr<D>(Kt, 32 * cc, 16 * dt, lane);
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) dq[qg][dt] = mfma(ktf, sf[cc][qg], dq[qg][dt]);
+      }
   }
-  if (qrow < T) {
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    const int qrow = qbase + 16 * qg + (lane & 15);
+    if (qrow >= T) continue;
     bf16_t* out = p.dq + b * p.dq_sb + (int64_t)qrow * p.dq_st + h * p.dq_sh;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       u16x4 v;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = f2bf(dq[dt][r] * p.scale);
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(dq[qg][dt][r] * p.scale);
       *reinterpret_cast<u16x4*>(out + 16 * dt + 4 * g) = v;
     }
   }
 }
 
 // dK / dV for one (key tile, query head): prefetched Q / dO tiles; output bf16 directly (no GQA) or
-// fp32 partials [2][B][Hq][T][D] summed over the group by attn_dkv_reduce_kernel
-template <int D>
+// fp32 partials [2][B][Hq][T][D] summed over the group by attn_dkv_reduce_kernel.
+// KG key groups of 16 per wave (key tile = 64 * KG): every Q / dO fragment read from LDS and every
+// transposed Q / dO fragment feeds KG MFMAs, and each staged Q / dO tile serves 64 * KG keys.
+template <int D, int KG>
 __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
-  constexpr int KS = D / 32, DT = D / 16, IMG = BQ * D * 2;
+  constexpr int KS = D / 32, DT = D / 16, IMG = BQ * D * 2, BK = BKV * KG;
   __shared__ __attribute__((aligned(16))) char smem[4 * IMG + 2 * BQ * 4];
   char* Qr = smem;
   char* Qt = smem + IMG;
@@ -750,21 +779,24 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int kt = blockIdx.x, hq = blockIdx.y, b = blockIdx.z;
   const int T = p.T, G = p.Hq / p.Hkv, hk = hq / G;
-  const int kvbase = kt * BKV + w * 16;
-  const int kvrow = kvbase + (lane & 15);
+  const int kvbase = kt * BK + w * 16 * KG;  // this wave's keys: kvbase + 16 kg + (lane & 15)
   const bf16_t* kb = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* vb = p.v + b * p.v_sb + hk * p.v_sh;
-  mbf16x8 kf[KS], vf[KS];
+  mbf16x8 kf[KG][KS], vf[KG][KS];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    kf[ks] = load_frag_global(kb, p.k_st, kvrow, T, ks, lane);
-    vf[ks] = load_frag_global(vb, p.v_st, kvrow, T, ks, lane);
-  }
+  for (int kg = 0; kg < KG; ++kg)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[kg][ks] = load_frag_global(kb, p.k_st, kvbase + 16 * kg + (lane & 15), T, ks, lane);
+      vf[kg][ks] = load_frag_global(vb, p.v_st, kvbase + 16 * kg + (lane & 15), T, ks, lane);
+    }
   const float c = p.scale * LOG2E;
-  f32x4 dk[DT], dv[DT];
+  f32x4 dk[KG][DT], dv[KG][DT];
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int q_begin = p.causal ? kt * BKV : 0;
+  for (int kg = 0; kg < KG; ++kg)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) dk[kg][dt] = dv[kg][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int q_begin = p.causal ? kt * BK : 0;
   const bf16_t* qb = p.q + b * p.q_sb + hq * p.q_sh;
   const bf16_t* dob = p.dout + b * p.do_sb + hq * p.do_sh;
   const float* lse = p.lse + ((int64_t)b * p.Hq + hq) * T;
@@ -794,66 +826,94 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
       fetch_tile<D>(tr, qb, p.q_st, dob, p.do_st, q0 + BQ, T);
       fetch_stats(q0 + BQ);
     }
-    f32x4 s[4], dp[4];
+    // every query of this tile is before all of this wave's keys: nothing to add (wave-uniform)
+    if (p.causal && q0 + BQ - 1 < kvbase) continue;
+    f32x4 s[KG][4], dp[KG][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      s[t] = dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kg = 0; kg < KG; ++kg) s[kg][t] = dp[kg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        s[t] = mfma(frag_row<D>(Qr, 16 * t, ks, lane), kf[ks], s[t]);  // S^T: [q][kv = lane]
-        dp[t] = mfma(frag_row<D>(Dr, 16 * t, ks, lane), vf[ks], dp[t]);
+        const mbf16x8 qf = frag_row<D>(Qr, 16 * t, ks, lane);
+        const mbf16x8 df = frag_row<D>(Dr, 16 * t, ks, lane);
+#pragma unroll
+        for (int kg = 0; kg < KG; ++kg) {
+          s[kg][t] = mfma(qf, kf[kg][ks], s[kg][t]);  // S^T: [q][kv = lane]
+          dp[kg][t] = mfma(df, vf[kg][ks], dp[kg][t]);
+        }
       }
     }
-    const bool need_mask = q0 + BQ > T || kvbase + 15 >= T || (p.causal && kvbase + 15 > q0);
+    const bool need_mask = q0 + BQ > T || kvbase + 16 * KG - 1 >= T || (p.causal && kvbase + 16 * KG - 1 > q0);
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t) {
+      const f32x4 l4 = *reinterpret_cast<const f32x4*>(s_lse + 16 * t + 4 * g);  // 4 consecutive queries
+      const f32x4 d4 = *reinterpret_cast<const f32x4*>(s_dl + 16 * t + 4 * g);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int qi = 16 * t + 4 * g + r;
-        float pr = fast_exp2(fmaf(s[t][r], c, -s_lse[qi]));
-        if (need_mask) {
-          const int q = q0 + qi;
-          if (q >= T || kvrow >= T || (p.causal && kvrow > q)) pr = 0.f;
+        const int q = q0 + 16 * t + 4 * g + r;
+#pragma unroll
+        for (int kg = 0; kg < KG; ++kg) {
+          const int kvrow = kvbase + 16 * kg + (lane & 15);
+          float pr = fast_exp2(fmaf(s[kg][t][r], c, -l4[r]));
+          if (need_mask && (q >= T || kvrow >= T || (p.causal && kvrow > q))) pr = 0.f;
+          s[kg][t][r] = pr;
+          dp[kg][t][r] = pr * (dp[kg][t][r] - d4[r]);  // dS
         }
-        s[t][r] = pr;
-        dp[t][r] = pr * (dp[t][r] - s_dl[qi]);  // dS
+      }
+    }
+    // pack P and dS to bf16 first: the fp32 S / dP registers are dead before the dV / dK MFMAs
+    mbf16x8 pf[2][KG], sf[2][KG];
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+      for (int kg = 0; kg < KG; ++kg) {
+        pf[cc][kg] = pack_p(s[kg][2 * cc], s[kg][2 * cc + 1]);
+        sf[cc][kg] = pack_p(dp[kg][2 * cc], dp[kg][2 * cc + 1]);
       }
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
-      const mbf16x8 pf = pack_p(s[2 * cc], s[2 * cc + 1]);
-      const mbf16x8 sf = pack_p(dp[2 * cc], dp[2 * cc + 1]);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        dv[dt] = mfma(frag_tr<D>(Dt, 32 * cc, 16 * dt, lane), pf, dv[dt]);
-        dk[dt] = mfma(frag_tr<D>(Qt, 32 * cc, 16 * dt, lane), sf, dk[dt]);
+        const mbf16x8 dtf = frag_tr<D>(Dt, 32 * cc, 16 * dt, lane);
+        const mbf16x8 qtf = frag_tr<D>(Qt, 32 * cc, 16 * dt, lane);
+#pragma unroll
+        for (int kg = 0; kg < KG; ++kg) {
+          dv[kg][dt] = mfma(dtf, pf[cc][kg], dv[kg][dt]);
+          dk[kg][dt] = mfma(qtf, sf[cc][kg], dk[kg][dt]);
+        }
       }
     }
   }
-  if (kvrow >= T) return;
-  if (G == 1) {
-    bf16_t* dkp = p.dk + b * p.dk_sb + (int64_t)kvrow * p.dk_st + hk * p.dk_sh;
-    bf16_t* dvp = p.dv + b * p.dv_sb + (int64_t)kvrow * p.dv_st + hk * p.dv_sh;
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg) {
+    const int kvrow = kvbase + 16 * kg + (lane & 15);
+    if (kvrow >= T) continue;
+    if (G == 1) {
+      bf16_t* dkp = p.dk + b * p.dk_sb + (int64_t)kvrow * p.dk_st + hk * p.dk_sh;
+      bf16_t* dvp = p.dv + b * p.dv_sb + (int64_t)kvrow * p.dv_st + hk * p.dv_sh;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        u16x4 a, v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a[r] = f2bf(dk[kg][dt][r] * p.scale);
+          v[r] = f2bf(dv[kg][dt][r]);
+        }
+        *reinterpret_cast<u16x4*>(dkp + 16 * dt + 4 * g) = a;
+        *reinterpret_cast<u16x4*>(dvp + 16 * dt + 4 * g) = v;
+      }
+      continue;
+    }
+    const int64_t plane = (int64_t)p.B * p.Hq * T * D;
+    float* pk = p.dkv_part + (((int64_t)b * p.Hq + hq) * T + kvrow) * D;
+    float* pv = pk + plane;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      u16x4 a, v;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        a[r] = f2bf(dk[dt][r] * p.scale);
-        v[r] = f2bf(dv[dt][r]);
-      }
-      *reinterpret_cast<u16x4*>(dkp + 16 * dt + 4 * g) = a;
-      *reinterpret_cast<u16x4*>(dvp + 16 * dt + 4 * g) = v;
+      f32x4 a = dk[kg][dt] * p.scale;
+      *reinterpret_cast<f32x4*>(pk + 16 * dt + 4 * g) = a;
+      *reinterpret_cast<f32x4*>(pv + 16 * dt + 4 * g) = dv[kg][dt];
     }
-    return;
-  }
-  const int64_t plane = (int64_t)p.B * p.Hq * T * D;
-  float* pk = p.dkv_part + (((int64_t)b * p.Hq + hq) * T + kvrow) * D;
-  float* pv = pk + plane;
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) {
-    f32x4 a = dk[dt] * p.scale;
-    *reinterpret_cast<f32x4*>(pk + 16 * dt + 4 * g) = a;
-    *reinterpret_cast<f32x4*>(pv + 16 * dt + 4 * g) = dv[dt];
   }
 }
 
@@ -918,14 +978,14 @@ hipError_t attention_bwd(const AttnParams& p, hipStream_t st) {
   PDA_CHECK_HIP(hipGetLastError());
   dim3 gq((p.T + BQ - 1) / BQ, p.Hq, p.B);
   if (p.rope_cos == nullptr) {
-    dim3 gk2((p.T + BKV - 1) / BKV, p.Hq, p.B);
+    dim3 gq2((p.T + 2 * BQ - 1) / (2 * BQ), p.Hq, p.B);
     if (p.Hq > p.Hkv && p.dkv_part == nullptr) return hipErrorInvalidValue;
-    if (p.D == 128) {
-      attn_bwd_dq2_kernel<128><<<gq, NT, 0, st>>>(p);
-      attn_bwd_dkdv2_kernel<128><<<gk2, NT, 0, st>>>(p);
+    if (p.D == 128) {  // (two key groups per wave would exceed the 256-VGPR budget at D = 128)
+      attn_bwd_dq2_kernel<128, 1><<<gq, NT, 0, st>>>(p);
+      attn_bwd_dkdv2_kernel<128, 1><<<dim3((p.T + BKV - 1) / BKV, p.Hq, p.B), NT, 0, st>>>(p);
     } else {
-      attn_bwd_dq2_kernel<64><<<gq, NT, 0, st>>>(p);
-      attn_bwd_dkdv2_kernel<64><<<gk2, NT, 0, st>>>(p);
+      attn_bwd_dq2_kernel<64, 2><<<gq2, NT, 0, st>>>(p);
+      attn_bwd_dkdv2_kernel<64, 2><<<dim3((p.T + 2 * BKV - 1) / (2 * BKV), p.Hq, p.B), NT, 0, st>>>(p);
     }
     PDA_CHECK_HIP(hipGetLastError());
     if (p.Hq > p.Hkv) {

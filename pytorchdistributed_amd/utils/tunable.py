@@ -35,8 +35,11 @@ def use_tuned_gemms(tag: str) -> str:
         return "tune"
     if not os.path.exists(path):
         return "off"
+    import tempfile
+
     tunable.enable(True)
     tunable.tuning_enable(False)
-    tunable.write_file_on_exit(False)
+    # results are only read; anything torch writes back at exit goes to a scratch file, never the table
+    tunable.set_filename(os.path.join(tempfile.gettempdir(), f"pda_tunableop_{tag}_{os.getpid()}.csv"))
     tunable.read_file(path)
     return "table"

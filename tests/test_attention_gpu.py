@@ -15,7 +15,8 @@ def rel_err(a, b):
 
 @pytest.mark.parametrize("B,T,Hq,Hkv,D,causal", [(2, 128, 4, 4, 64, True), (1, 200, 4, 2, 128, True),
                                                   (2, 64, 2, 2, 128, False), (1, 256, 8, 1, 64, True),
-                                                  (1, 96, 2, 2, 64, False)])
+                                                  (1, 96, 2, 2, 64, False), (1, 200, 4, 2, 64, True),
+                                                  (2, 72, 2, 1, 64, True), (1, 330, 2, 2, 64, False)])
 @pytest.mark.parametrize("use_rope", [False, True])
 def test_flash_attention_fwd_bwd(B, T, Hq, Hkv, D, causal, use_rope):
     from pytorchdistributed_amd.ops.attention import attention_qkv, attention_ref, rope_tables
