@@ -537,9 +537,10 @@ __device__ __forceinline__ void store_tile(const TileRegs<D>& tr, char* a_row, c
   }
 }
 
-template <int D>
+// QG query groups of 16 rows per wave (query tile = 64 * QG): each K / V fragment read feeds QG MFMAs.
+template <int D, int QG>
 __global__ void __launch_bounds__(NT, 2) attn_fwd2_kernel(AttnParams p) {
-  constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2, BQ2 = 128;
+  constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2, BQW = 64 * QG;
   __shared__ __attribute__((aligned(16))) char smem[2 * IMG];
   char* Ks = smem;
   char* Vs = smem + IMG;
@@ -547,25 +548,28 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd2_kernel(AttnParams p) {
   const int qt = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z;  // heavy causal tiles first
   const int hk = h / (p.Hq / p.Hkv);
   const int T = p.T;
-  const int qbase = qt * BQ2 + w * 32;
-  const int qrow0 = qbase + (lane & 15), qrow1 = qrow0 + 16;
+  const int qbase = qt * BQW + w * 16 * QG;  // this wave's queries: qbase + 16 qg + (lane & 15)
   const bf16_t* qb = p.q + b * p.q_sb + h * p.q_sh;
   const bf16_t* kb = p.k + b * p.k_sb + hk * p.k_sh;
   const bf16_t* vb = p.v + b * p.v_sb + hk * p.v_sh;
-  mbf16x8 qf0[KS], qf1[KS];
+  mbf16x8 qf[QG][KS];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    qf0[ks] = load_frag_global(qb, p.q_st, qrow0, T, ks, lane);
-    qf1[ks] = load_frag_global(qb, p.q_st, qrow1, T, ks, lane);
-  }
+  for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[qg][ks] = load_frag_global(qb, p.q_st, qbase + 16 * qg + (lane & 15), T, ks, lane);
   const float c = p.scale * LOG2E;
   // m: running row max of the RAW scores (scale folded into the exponent's fma); l: this lane's
   // partial row sum (its 16 of every 64 keys) — the 4 lanes of a query are summed once at the end
-  float m0 = NEG_BIG, l0 = 0.f, m1 = NEG_BIG, l1 = 0.f;
-  f32x4 o0[DT], o1[DT];
+  float m[QG], l[QG];
+  f32x4 o[QG][DT];
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt) o0[dt] = o1[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int kv_end = p.causal ? min(T, (qt + 1) * BQ2) : T;
+  for (int qg = 0; qg < QG; ++qg) {
+    m[qg] = NEG_BIG;
+    l[qg] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[qg][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int kv_end = p.causal ? min(T, (qt + 1) * BQW) : T;
   const int ntiles = (kv_end + BKV - 1) / BKV;
   TileRegs<D> tr;
   fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, 0, T);
@@ -575,20 +579,23 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd2_kernel(AttnParams p) {
     store_tile<D>(tr, Ks, nullptr, nullptr, Vs);
     __syncthreads();
     if (j + 1 < ntiles) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, kv0 + BKV, T);
-    if (p.causal && kv0 > qbase + 31) continue;  // every key of this tile is in this wave's future
-    f32x4 s0[4], s1[4];
+    if (p.causal && kv0 > qbase + 16 * QG - 1) continue;  // every key of this tile is in this wave's future
+    f32x4 s[QG][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      s0[t] = s1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) s[qg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const mbf16x8 kf = frag_row<D>(Ks, 16 * t, ks, lane);
-        s0[t] = mfma(kf, qf0[ks], s0[t]);
-        s1[t] = mfma(kf, qf1[ks], s1[t]);
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) s[qg][t] = mfma(kf, qf[qg][ks], s[qg][t]);
       }
     }
     const bool need_mask = kv0 + BKV > T || (p.causal && kv0 + BKV - 1 > qbase);
-    auto softmax = [&](f32x4 (&s)[4], int qrow, float& m, float& l, f32x4 (&o)[DT]) {
+#pragma unroll
+    for (int qg = 0; qg < QG; ++qg) {
+      const int qrow = qbase + 16 * qg + (lane & 15);
       float mx = NEG_BIG;
       if (need_mask) {
 #pragma unroll
@@ -596,60 +603,59 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd2_kernel(AttnParams p) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int kv = kv0 + 16 * t + 4 * g + r;
-            if (kv >= T || (p.causal && kv > qrow)) s[t][r] = -INFINITY;
+            if (kv >= T || (p.causal && kv > qrow)) s[qg][t][r] = -INFINITY;
           }
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[t][r]);
-      const float m_new = fmaxf(m, max_x16_x32(mx));
-      const float alpha = fast_exp2((m - m_new) * c);
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[qg][t][r]);
+      const float m_new = fmaxf(m[qg], max_x16_x32(mx));
+      const float alpha = fast_exp2((m[qg] - m_new) * c);
       const float mc = m_new * c;
       float rs = 0.f;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = fast_exp2(fmaf(s[t][r], c, -mc));
-          s[t][r] = e;
+          const float e = fast_exp2(fmaf(s[qg][t][r], c, -mc));
+          s[qg][t][r] = e;
           rs += e;
         }
-      l = fmaf(l, alpha, rs);
-      m = m_new;
+      l[qg] = fmaf(l[qg], alpha, rs);
+      m[qg] = m_new;
 #pragma unroll
-      for (int dt = 0; dt < DT; ++dt) o[dt] *= alpha;
-    };
-    softmax(s0, qrow0, m0, l0, o0);
-    softmax(s1, qrow1, m1, l1, o1);
+      for (int dt = 0; dt < DT; ++dt) o[qg][dt] *= alpha;
+    }
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
-      const mbf16x8 p0 = pack_p(s0[2 * cc], s0[2 * cc + 1]);
-      const mbf16x8 p1 = pack_p(s1[2 * cc], s1[2 * cc + 1]);
+      mbf16x8 pf[QG];
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) pf[qg] = pack_p(s[qg][2 * cc], s[qg][2 * cc + 1]);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const mbf16x8 vf = frag_tr<D>(Vs, 32 * cc, 16 * dt, lane);
-        o0[dt] = mfma(vf, p0, o0[dt]);
-        o1[dt] = mfma(vf, p1, o1[dt]);
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) o[qg][dt] = mfma(vf, pf[qg], o[qg][dt]);
       }
     }
   }
-  auto epilogue = [&](int qrow, float m, float l, const f32x4 (&o)[DT]) {
-    l = sum_x16_x32(l);  // (all lanes take part: the swaps need a full EXEC)
-    if (qrow >= T) return;
-    const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    const int qrow = qbase + 16 * qg + (lane & 15);
+    const float lsum = sum_x16_x32(l[qg]);  // (all lanes take part: the swaps need a full EXEC)
+    if (qrow >= T) continue;
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
     bf16_t* ob = p.o + b * p.o_sb + (int64_t)qrow * p.o_st + h * p.o_sh;
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       u16x4 v;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[dt][r] * inv);
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[qg][dt][r] * inv);
       *reinterpret_cast<u16x4*>(ob + 16 * dt + 4 * g) = v;
     }
-    if (g == 0) p.lse[((int64_t)b * p.Hq + h) * T + qrow] = (m * c + log2f(l)) / LOG2E;
-  };
-  epilogue(qrow0, m0, l0, o0);
-  epilogue(qrow1, m1, l1, o1);
+    if (g == 0) p.lse[((int64_t)b * p.Hq + h) * T + qrow] = (m[qg] * c + log2f(lsum)) / LOG2E;
+  }
 }
 
 // dQ, query-stationary, prefetched K/V tiles; QG query groups of 16 rows per wave (query tile =
@@ -946,15 +952,33 @@ __global__ void __launch_bounds__(NT) attn_dkv_reduce_kernel(AttnParams p) {
   }
 }
 
+// query groups per wave of the forward kernel (PDA_ATTN_FWD_QG=1|2 overrides).  Measured
+// (profiles/r1_attn_microbench_v3.jsonl): D = 64 293 vs 273 TFLOP/s with 2 groups; D = 128 ties
+// (357 / 360), and 1 group keeps the D = 128 kernel free of spills.
+int attn_fwd_groups(int D) {
+  static const int env = [] {
+    const char* e = getenv("PDA_ATTN_FWD_QG");
+    return e ? atoi(e) : 0;
+  }();
+  if (env == 1 || env == 2) return env;
+  return D == 128 ? 1 : 2;
+}
+
 }  // namespace
 
 hipError_t attention_fwd(const AttnParams& p, hipStream_t st) {
   if (p.D != 64 && p.D != 128) return hipErrorInvalidValue;
   if (p.Hkv <= 0 || p.Hq % p.Hkv) return hipErrorInvalidValue;
   if (p.rope_cos == nullptr) {
-    dim3 grid((p.T + 127) / 128, p.Hq, p.B);
-    if (p.D == 128) attn_fwd2_kernel<128><<<grid, NT, 0, st>>>(p);
-    else attn_fwd2_kernel<64><<<grid, NT, 0, st>>>(p);
+    const int qg = attn_fwd_groups(p.D);
+    dim3 grid((p.T + 64 * qg - 1) / (64 * qg), p.Hq, p.B);
+    if (p.D == 128) {
+      if (qg == 1) attn_fwd2_kernel<128, 1><<<grid, NT, 0, st>>>(p);
+      else attn_fwd2_kernel<128, 2><<<grid, NT, 0, st>>>(p);
+    } else {
+      if (qg == 1) attn_fwd2_kernel<64, 1><<<grid, NT, 0, st>>>(p);
+      else attn_fwd2_kernel<64, 2><<<grid, NT, 0, st>>>(p);
+    }
     return hipGetLastError();
   }
   dim3 grid((p.T + BQ - 1) / BQ, p.Hq, p.B);
