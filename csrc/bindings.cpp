@@ -795,7 +795,7 @@ class XgmiComm {
     (void)pda::xgmi_free(flags_);
     (void)pda::xgmi_free(err_);
   }
-  static size_t flag_bytes() { return (size_t)2 * pda::kXgmiMaxBlocks * pda::kXgmiMaxRanks * sizeof(uint32_t); }
+  static size_t flag_bytes() { return (size_t)pda::kXgmiPhases * pda::kXgmiMaxBlocks * pda::kXgmiMaxRanks * sizeof(uint32_t); }
   py::bytes handles() {
     std::string h(2 * HIP_IPC_HANDLE_SIZE, '\0');
     CHECK_HIP_OK(pda::xgmi_get_handle(data_, &h[0]));
@@ -818,8 +818,9 @@ class XgmiComm {
     opened_ = true;
   }
   // in-place all-reduce of a contiguous fp32 / bf16 tensor on this communicator's device
-  void allreduce(Tensor t, bool average) {
+  void allreduce(Tensor t, bool average, int algo) {
     TORCH_CHECK(opened_ || world_ == 1, "xgmi: open() the peer handles first");
+    TORCH_CHECK(algo == 0 || algo == 1, "xgmi: algo 0 (one-shot) or 1 (two-shot)");
     check_gpu(t, "t");
     TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, "xgmi: fp32 / bf16 only");
     const int64_t n = t.numel(), bytes = n * t.element_size();
@@ -840,6 +841,7 @@ class XgmiComm {
     a.epoch = ++epoch_;
     a.timeout_ticks = timeout_ticks_;
     a.err = err_;
+    a.algo = algo;
     CHECK_HIP_OK(pda::xgmi_allreduce(a, t.scalar_type() == at::kBFloat16, st));
   }
   int error() {
@@ -910,7 +912,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("device"), py::arg("timeout") = 10.0)
       .def("handles", &XgmiComm::handles)
       .def("open", &XgmiComm::open)
-      .def("allreduce", &XgmiComm::allreduce, py::arg("t"), py::arg("average") = false)
+      .def("allreduce", &XgmiComm::allreduce, py::arg("t"), py::arg("average") = false, py::arg("algo") = 0)
       .def("error", &XgmiComm::error)
       .def_property_readonly("capacity", &XgmiComm::capacity);
   pda_rt::bind_runtime(m);

@@ -28,12 +28,13 @@ struct AttnParams {
   float* dkv_part;
 };
 
-// ---- xgmi.hip (one-shot all-reduce over IPC-mapped peer buffers)
+// ---- xgmi.hip (one-shot / two-shot all-reduce over IPC-mapped peer buffers)
 constexpr int kXgmiMaxRanks = 8;
 constexpr int kXgmiMaxBlocks = 128;
+constexpr int kXgmiPhases = 3;
 struct XgmiArgs {
   void* data[kXgmiMaxRanks];       // exchange buffer of every rank (own + IPC-mapped peers)
-  uint32_t* flags[kXgmiMaxRanks];  // flag array of every rank: [2 phases][kXgmiMaxBlocks][kXgmiMaxRanks]
+  uint32_t* flags[kXgmiMaxRanks];  // flag array of every rank: [kXgmiPhases][kXgmiMaxBlocks][kXgmiMaxRanks]
   void* out;
   int64_t n;                       // elements, multiple of 8
   int rank, world;
@@ -41,6 +42,7 @@ struct XgmiArgs {
   uint32_t epoch;
   long long timeout_ticks;         // wall_clock64 ticks before a spin gives up
   int* err;
+  int algo;                        // 0 = one-shot, 1 = two-shot (reduce-scatter + all-gather)
 };
 hipError_t xgmi_alloc(void** p, size_t bytes);
 hipError_t xgmi_free(void* p);

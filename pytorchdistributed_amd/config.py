@@ -22,7 +22,7 @@ from dataclasses import dataclass, field, fields
 from typing import Any, Dict, List, Optional, Sequence
 
 _CHOICES = {
-    "allreduce": ("auto", "rccl", "ring", "host", "ipc"),
+    "allreduce": ("auto", "rccl", "ring", "host", "ipc", "oneshot", "twoshot"),
     "precision": ("bf16", "fp32"),
     "schedule": ("gpipe", "1f1b"),
 }
@@ -38,7 +38,7 @@ class Config:
     # --- DDP communication (buckets sized for 7 xGMI links)
     bucket_mb: float = 32.0
     first_bucket_mb: float = 2.0
-    allreduce: str = "auto"          # auto -> RCCL for device tensors, host ring for CPU tensors; ipc -> one-shot xGMI
+    allreduce: str = "auto"          # auto -> RCCL for device tensors, host ring for CPU tensors; oneshot/twoshot -> IPC xGMI kernels, ipc -> size-picked
     comm_priority: bool = True       # high-priority HIP stream for communication
     broadcast_buffers: bool = True
     # --- pipeline / FSDP

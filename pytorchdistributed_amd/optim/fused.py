@@ -92,6 +92,10 @@ class _FusedBase(torch.optim.Optimizer):
             st = self._flat_for(gi, group)
             if st is not None:
                 fg: FlatGroup = st["fg"]
+                if fg.pending_comm:
+                    raise RuntimeError(
+                        f"optimizer step on a flat gradient buffer with {fg.pending_comm} bucket all-reduce(s) "
+                        "the compute stream has not waited on (DDP backward did not finish its final callback)")
                 if any(p.grad is None for p in fg.params):
                     fg.attach_grads()  # grads were set to None without a backward: the flat buffer holds them
                 st["step"] += 1

@@ -117,7 +117,7 @@ class DistributedDataParallel(tnn.Module):
         self._callback_queued = False
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
         self.reducer.prepare()
-        # ---- optional one-shot xGMI all-reduce for buckets (PDA_ALLREDUCE=ipc, single node, RCCL world)
+        # ---- optional IPC all-reduce over xGMI for buckets (PDA_ALLREDUCE=ipc|oneshot|twoshot, single node)
         self.xgmi = None
         if self.world > 1 and self.backend == "nccl" and process_group is None:
             from . import xgmi as _xgmi
@@ -125,6 +125,7 @@ class DistributedDataParallel(tnn.Module):
             if _xgmi.ipc_requested() and _xgmi.single_node():
                 cap = max(b[2] for b in self.bucket_info())
                 self.xgmi = _xgmi.XgmiAllReduce(capacity_mb=cap / 2 ** 20 + 1)
+                self._xgmi_algo = _xgmi.requested_algo()
                 self._ipc_stream = torch.cuda.Stream(self.xgmi.device)
 
     # ------------------------------------------------------------------ communication
@@ -145,6 +146,9 @@ class DistributedDataParallel(tnn.Module):
         t = self._bucket_view(b)
         if self.world == 1:
             return
+        # stream-safety guard: the fused optimizer refuses a flat group whose bucket
+        # collectives the compute stream has not waited on yet (cleared by _finalize)
+        self.groups[self.bucket_slices[b][0]].pending_comm += 1
         nbytes = t.numel() * t.element_size()
         self._stats["comm_bytes"] += nbytes
         self._stats["comm_calls"] += 1
@@ -158,7 +162,7 @@ class DistributedDataParallel(tnn.Module):
             ready.record()
             with torch.cuda.stream(self._ipc_stream), _timing.range(f"ddp.xgmi_all_reduce.b{b}"):
                 self._ipc_stream.wait_event(ready)
-                self.xgmi(t, average=True)
+                self.xgmi(t, average=True, algo=self._xgmi_algo)
                 done = torch.cuda.Event()
                 done.record(self._ipc_stream)
             self._works.append((_EventWork(done), None))
@@ -208,6 +212,8 @@ class DistributedDataParallel(tnn.Module):
             if not self.find_unused_parameters:
                 self.reducer.prepare()
                 self._works.clear()
+                for g in self.groups.values():
+                    g.pending_comm = 0
                 raise RuntimeError(
                     f"DDP: {len(unready)} parameter(s) received no gradient this iteration "
                     f"(e.g. index {unready[:8]}); pass find_unused_parameters=True")
@@ -232,6 +238,7 @@ class DistributedDataParallel(tnn.Module):
         if self.backend != "nccl":
             self._sweep_tickets(force=True)  # gloo waits were blocking: all done
         for g in self.groups.values():
+            g.pending_comm = 0
             g.attach_grads()
         self.reducer.prepare()
 

@@ -27,6 +27,7 @@ class FlatGroup:
         assert len(params) > 0
         self.params: List[torch.nn.Parameter] = list(params)
         self.dtype = params[0].dtype
+        self.pending_comm = 0  # bucket collectives launched but not yet waited on by the compute stream (DDP)
         self.device = params[0].device
         if offsets is None:
             offsets, off = [], 0

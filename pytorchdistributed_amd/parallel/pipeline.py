@@ -23,7 +23,9 @@ averages a stage's gradients over its DP group in flat buckets.
 """
 from __future__ import annotations
 
-from typing import Callable, List, Optional, Sequence, Tuple
+import json
+import os
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -484,6 +486,89 @@ class Pipeline:
         if self.is_last:
             return torch.stack(losses).sum()
         return None
+
+
+# ------------------------------------------------------------------ checkpoints (PP layout)
+def _atomic_save(obj, path: str):
+    tmp = path + ".tmp"
+    torch.save(obj, tmp)
+    os.replace(tmp, path)
+
+
+def save_pipeline_checkpoint(directory: str, pipe: "Pipeline", optimizer=None, step: int = 0,
+                             partition: Optional[List[Tuple[int, int]]] = None, dp_rank: int = 0,
+                             extra: Optional[dict] = None):
+    """Per-stage files + the stage-partition map.
+
+    ``stage_{s:03d}.pt`` = ``{"MODEL_STATE", "OPTIMIZER_STATE", "STEP", "STAGE"}`` of pipeline stage s
+    (written by the stage's DP replica 0 only — replicas are identical after the DP gradient sync);
+    ``pipeline.json`` (stage 0) = stages, schedule, micro-batches, model chunks per rank and the
+    [start, end) layer range of every (virtual) stage, which :func:`consolidate_pipeline` uses to
+    renumber stage-local layers into one full-model state dict.  Collective over nothing: each stage
+    writes its own file; call a barrier afterwards if other ranks read it right away.
+    """
+    if dp_rank != 0:
+        return
+    os.makedirs(directory, exist_ok=True)
+    snap = {"MODEL_STATE": pipe.module.state_dict(), "STEP": int(step), "STAGE": pipe.stage}
+    if optimizer is not None:
+        snap["OPTIMIZER_STATE"] = optimizer.state_dict()
+    if extra:
+        snap.update(extra)
+    _atomic_save(snap, os.path.join(directory, f"stage_{pipe.stage:03d}.pt"))
+    if pipe.stage == 0:
+        meta = {"num_stages": pipe.S, "schedule": pipe.schedule_name, "num_microbatches": pipe.M,
+                "chunks": len(pipe.chunks) if pipe.chunks is not None else 1,
+                "partition": [list(r) for r in partition] if partition is not None else None}
+        tmp = os.path.join(directory, "pipeline.json.tmp")
+        with open(tmp, "w") as f:
+            json.dump(meta, f, indent=1)
+        os.replace(tmp, os.path.join(directory, "pipeline.json"))
+
+
+def load_pipeline_checkpoint(directory: str, pipe: "Pipeline", optimizer=None, map_location="cpu") -> int:
+    """Restore this rank's stage (every DP replica of the stage reads the same file); returns the step."""
+    meta = json.load(open(os.path.join(directory, "pipeline.json")))
+    chunks = len(pipe.chunks) if pipe.chunks is not None else 1
+    if meta["num_stages"] != pipe.S or meta["chunks"] != chunks:
+        raise ValueError(f"checkpoint has {meta['num_stages']} stages x {meta['chunks']} chunks, "
+                         f"pipeline has {pipe.S} x {chunks}")
+    snap = torch.load(os.path.join(directory, f"stage_{pipe.stage:03d}.pt"), map_location=map_location,
+                      weights_only=True)
+    pipe.module.load_state_dict(snap["MODEL_STATE"])
+    if optimizer is not None and "OPTIMIZER_STATE" in snap:
+        optimizer.load_state_dict(snap["OPTIMIZER_STATE"])
+        sync = getattr(optimizer, "sync_from_state", None)
+        if sync is not None:
+            sync()
+    return int(snap.get("STEP", 0))
+
+
+def consolidate_pipeline(directory: str, layer_prefix: str = "h") -> Dict[str, torch.Tensor]:
+    """Offline: merge ``stage_*.pt`` into one full-model state dict.  Keys ``{layer_prefix}.{i}.*`` of
+    (virtual) stage v are renumbered to ``{layer_prefix}.{start_v + i}.*`` using the partition map; for
+    interleaved checkpoints the chunk index prefix (``c.``) selects virtual stage ``c * stages + s``.
+    Other keys (embeddings, final norm, head) pass through unchanged."""
+    meta = json.load(open(os.path.join(directory, "pipeline.json")))
+    S, V, part = meta["num_stages"], meta["chunks"], meta["partition"]
+    out: Dict[str, torch.Tensor] = {}
+    for s in range(S):
+        sd = torch.load(os.path.join(directory, f"stage_{s:03d}.pt"), map_location="cpu",
+                        weights_only=True)["MODEL_STATE"]
+        for k, v in sd.items():
+            c, key = 0, k
+            if V > 1:
+                c_str, key = k.split(".", 1)
+                c = int(c_str)
+            vs = c * S + s
+            head, _, rest = key.partition(".")
+            if part is not None and head == layer_prefix and rest:
+                idx, _, tail = rest.partition(".")
+                key = f"{layer_prefix}.{part[vs][0] + int(idx)}.{tail}" if tail else f"{layer_prefix}.{part[vs][0] + int(idx)}"
+            if key in out:
+                raise ValueError(f"duplicate key {key!r} while consolidating stage {s}")
+            out[key] = v
+    return out
 
 
 def partition_layers(num_layers: int, num_stages: int) -> List[Tuple[int, int]]:

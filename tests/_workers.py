@@ -44,6 +44,8 @@ def ddp_mlp(rank, world, backend, outdir, steps):
         opt.zero_grad()
         loss = F.cross_entropy(ddp(xs), ys)
         loss.backward()
+        # stream-safety guard state: every launched bucket was waited on by the final callback
+        assert all(g.pending_comm == 0 for g in ddp.groups.values())
         opt.step()
     torch.save({k: v.clone() for k, v in model.state_dict().items()}, os.path.join(outdir, f"{rank}.pt"))
     torch.save({"nb": ddp.reducer.num_buckets}, os.path.join(outdir, f"meta{rank}.pt"))
@@ -236,8 +238,9 @@ def debug_checker_worker(rank, world, mode, outdir):
         pd.destroy_process_group()
 
 
-def xgmi_worker(rank, world, outdir):
-    """2 processes on cuda:0; store/gloo only for the handle exchange."""
+def xgmi_worker(rank, world, outdir, algos=("oneshot",)):
+    """`world` processes on cuda:0; store/gloo only for the handle exchange.  Iterations cycle through
+    ``algos`` so consecutive calls switch algorithm (and grid size) on the same exchange buffers."""
     import pytorchdistributed_amd.distributed as pd
     from pytorchdistributed_amd.parallel.xgmi import XgmiAllReduce
 
@@ -245,11 +248,12 @@ def xgmi_worker(rank, world, outdir):
     pd.init_process_group("gloo")
     comm = XgmiAllReduce(capacity_mb=8, device=torch.device("cuda", 0), timeout_s=20.0)
     for it, (n, dt) in enumerate([(8, torch.float32), (1000, torch.float32), (4096 * 129, torch.bfloat16),
-                                  (1 << 20, torch.float32), (8, torch.bfloat16), (3 * (1 << 20), torch.bfloat16)]):
+                                  (1 << 20, torch.float32), (8, torch.bfloat16), (3 * (1 << 20), torch.bfloat16),
+                                  (1000, torch.bfloat16), (1 << 19, torch.float32), (40, torch.float32)]):
         g = torch.Generator().manual_seed(100 + it)
         base = [torch.randn(n, generator=g) for _ in range(world)]
         t = base[rank].to("cuda", dt)
-        comm(t, average=(it % 2 == 1))
+        comm(t, average=(it % 2 == 1), algo=algos[it % len(algos)])
         torch.cuda.synchronize()
         comm.check()
         ref = sum(b.to(dt).float() for b in base)
@@ -347,3 +351,93 @@ def fsdp_llama_gpu_worker(rank, world, outdir):
         f.write(f"ok {worst[0]:.3e}")
     if world > 1:
         pd.destroy_process_group()
+
+
+class _PPFull(torch.nn.Module):
+    """Embedding-like input layer, a `h` stack and a head: the key layout GPT2Stage checkpoints use."""
+
+    def __init__(self, n_layers):
+        super().__init__()
+        torch.manual_seed(7)
+        self.emb = torch.nn.Linear(16, 16)
+        self.h = torch.nn.ModuleList([torch.nn.Linear(16, 16) for _ in range(n_layers)])
+        self.head = torch.nn.Linear(16, 16)
+
+
+class _PPStage(torch.nn.Module):
+    def __init__(self, full, lo, hi, first, last):
+        super().__init__()
+        if first:
+            self.emb = full.emb
+        self.h = torch.nn.ModuleList(full.h[lo:hi])
+        if last:
+            self.head = full.head
+
+    def forward(self, x):
+        if hasattr(self, "emb"):
+            x = self.emb(x)
+        for m in self.h:
+            x = torch.tanh(m(x))
+        if hasattr(self, "head"):
+            x = self.head(x)
+        return x
+
+
+def pipeline_ckpt_worker(rank, world, chunks, outdir):
+    """Train one step, save the PP checkpoint (stage files + partition map), reload into freshly
+    initialised stages and check equality; rank 0 consolidates and compares with the full model."""
+    import torch.distributed as dist
+
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.pipeline import (Pipeline, consolidate_pipeline, load_pipeline_checkpoint,
+                                                          partition_layers, save_pipeline_checkpoint)
+
+    pd.init_process_group("gloo")
+    n_layers = 4 * world * chunks // 2
+    parts = partition_layers(n_layers, world * chunks)
+    full = _PPFull(n_layers)
+
+    def stages(model):
+        mods = [_PPStage(model, *parts[c * world + rank], c * world + rank == 0, c * world + rank == world * chunks - 1)
+                for c in range(chunks)]
+        return mods if chunks > 1 else mods[0]
+
+    mine = stages(full)
+    sched = "interleaved" if chunks > 1 else "1f1b"
+    pipe = Pipeline(mine, list(range(world)), num_microbatches=4, schedule=sched, loss_fn=F.mse_loss,
+                    device=torch.device("cpu"))
+    opt = torch.optim.SGD(pipe.module.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(3)
+    X, Y = torch.randn(8, 16, generator=g), torch.randn(8, 16, generator=g)
+    pipe.step(X, Y)
+    opt.step()
+    ckpt = os.path.join(outdir, "ckpt")
+    save_pipeline_checkpoint(ckpt, pipe, opt, step=5, partition=parts)
+    dist.barrier()
+    fresh_full = _PPFull(n_layers)
+    for p in fresh_full.parameters():
+        torch.nn.init.zeros_(p)
+    mine2 = stages(fresh_full)
+    pipe2 = Pipeline(mine2, list(range(world)), num_microbatches=4, schedule=sched, loss_fn=F.mse_loss,
+                     device=torch.device("cpu"))
+    opt2 = torch.optim.SGD(pipe2.module.parameters(), lr=0.1, momentum=0.9)
+    assert load_pipeline_checkpoint(ckpt, pipe2, opt2) == 5
+    for (n1, a), (n2, b) in zip(pipe.module.state_dict().items(), pipe2.module.state_dict().items()):
+        assert n1 == n2 and torch.equal(a, b), n1
+    assert str(opt.state_dict()["state"]) == str(opt2.state_dict()["state"])
+    # this rank's trained tensors under their full-model names (other ranks' layers are stale here)
+    own = {t.data_ptr() for t in pipe.module.state_dict().values()}
+    torch.save({k: v for k, v in full.state_dict().items() if v.data_ptr() in own},
+               os.path.join(outdir, f"ref{rank}.pt"))
+    dist.barrier()
+    if rank == 0:
+        merged = consolidate_pipeline(ckpt)
+        ref = {}
+        for r in range(world):
+            ref.update(torch.load(os.path.join(outdir, f"ref{r}.pt"), weights_only=True))
+        assert sorted(merged) == sorted(ref), (sorted(merged), sorted(ref))
+        for k in ref:
+            assert torch.equal(merged[k], ref[k]), k
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+        f.write("ok")
+    pd.destroy_process_group()

@@ -116,3 +116,13 @@ def test_interleaved_pipeline_grads_match_single_process(tmp_path, world, chunks
             ref = torch.nn.Sequential(*[m for b in blocks[vs * per:(vs + 1) * per] for m in b])
             for n, p in ref.named_parameters():
                 assert torch.allclose(d["grads"][f"{c}.{n}"], p.grad, atol=1e-5, rtol=1e-4), (r, c, n)
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 1), (2, 2), (4, 1)])
+def test_pipeline_checkpoint_roundtrip_and_consolidate(tmp_path, world, chunks):
+    """PP checkpoint layout: stage files + partition map, reload, consolidation."""
+    spawn(_workers.pipeline_ckpt_worker, args=(world, chunks, str(tmp_path)), nprocs=world, timeout=180)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}").read_text() == "ok"
+    assert sorted(p.name for p in (tmp_path / "ckpt").iterdir()) == \
+        ["pipeline.json"] + [f"stage_{s:03d}.pt" for s in range(world)]

@@ -1,5 +1,5 @@
 """All-reduce bandwidth sweep over bucket sizes: RCCL (torch.distributed
-"nccl") vs the one-shot xGMI IPC kernel, bf16, per size: time, algorithm bandwidth and bus bandwidth
+"nccl") vs the one-shot and two-shot xGMI IPC kernels, bf16, per size: time, algorithm bandwidth and bus bandwidth
 (2(N-1)/N x bytes / time).  Run on one node:
 
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_allreduce.py
@@ -44,7 +44,8 @@ def main():
         n = int(mb * 2 ** 20 / 2) // 8 * 8
         t = torch.randn(n, device="cuda", dtype=torch.bfloat16)
         rec = {"size_mb": mb, "world": world}
-        for name, fn in [("rccl", lambda: dist.all_reduce(t)), ("xgmi_oneshot", lambda: xg(t))]:
+        for name, fn in [("rccl", lambda: dist.all_reduce(t)), ("xgmi_oneshot", lambda: xg(t, algo="oneshot")),
+                         ("xgmi_twoshot", lambda: xg(t, algo="twoshot"))]:
             ms = timeit(fn)
             alg = n * 2 / (ms * 1e-3) / 1e9
             rec[name] = {"ms": round(ms, 4), "alg_GBps": round(alg, 1),
