@@ -715,6 +715,40 @@ void attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, T
   CHECK_HIP_OK(pda::attention_bwd(p, stream_of(q)));
 }
 
+// ------------------------------------------------------------------ decode attention (serving)
+// q [B, 1, Hq, D] (any B/H strides), k/v caches [B, Tmax, Hkv, D] (any strides, contiguous D); attends the
+// first L cache rows; returns o [B, 1, Hq, D]
+Tensor decode_attn(Tensor q, Tensor k, Tensor v, int64_t L, double scale, int64_t splits) {
+  attn_check(q, "q");
+  attn_check(k, "k cache");
+  attn_check(v, "v cache");
+  const int B = q.size(0), Hq = q.size(2), D = q.size(3), Hkv = k.size(2);
+  TORCH_CHECK(q.size(1) == 1, "decode_attn: one query token per sequence");
+  TORCH_CHECK(D == 64 || D == 128, "head dim must be 64 or 128");
+  TORCH_CHECK(k.size(0) == B && k.size(3) == D && v.sizes() == k.sizes(), "decode_attn: cache shape mismatch");
+  TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0 && (Hq / Hkv == 1 || Hq / Hkv == 2 || Hq / Hkv == 4 || Hq / Hkv == 8),
+              "decode_attn: query heads per kv head must be 1, 2, 4 or 8");
+  TORCH_CHECK(L >= 1 && L <= k.size(1), "decode_attn: L must be in [1, cache length]");
+  c10::DeviceGuard g(q.device());
+  Tensor o = at::empty({B, 1, Hq, D}, q.options());
+  pda::DecodeAttnParams p{};
+  p.q = bp(q); p.k = bp(k); p.v = bp(v); p.o = bpm(o);
+  p.q_sb = q.stride(0); p.q_sh = q.stride(2);
+  p.k_sb = k.stride(0); p.k_st = k.stride(1); p.k_sh = k.stride(2);
+  p.v_sb = v.stride(0); p.v_st = v.stride(1); p.v_sh = v.stride(2);
+  p.B = B; p.Hq = Hq; p.Hkv = Hkv; p.D = D; p.L = (int)L;
+  p.splits = splits > 0 ? (int)splits : pda::decode_attn_splits(B, Hkv, (int)L, D);
+  p.scale_log2 = (float)(scale * 1.4426950408889634);
+  Tensor ws;
+  if (p.splits > 1) {
+    ws = at::empty({(int64_t)B * Hq * p.splits * (D + 2)}, q.options().dtype(at::kFloat));
+    p.ws_acc = ws.data_ptr<float>();
+    p.ws_ml = p.ws_acc + (int64_t)B * Hq * p.splits * D;
+  }
+  CHECK_HIP_OK(pda::decode_attention(p, stream_of(q)));
+  return o;
+}
+
 // ------------------------------------------------------------------ embedding / rope
 Tensor embedding_fwd(Tensor idx, Tensor table) {
   check_gpu(idx, "idx");
@@ -903,6 +937,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("rownorm_fwd", &rownorm_fwd);
   m.def("rownorm_bwd", &rownorm_bwd);
   m.def("attn_fwd", &attn_fwd);
+  m.def("decode_attn", &decode_attn, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("L"), py::arg("scale"),
+        py::arg("splits") = 0);
   m.def("attn_bwd", &attn_bwd);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);

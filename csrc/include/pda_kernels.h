@@ -175,6 +175,21 @@ hipError_t attention_fwd(const AttnParams& p, hipStream_t st);
 hipError_t attention_bwd(const AttnParams& p, hipStream_t st);
 int64_t attention_bwd_ws_floats(int B, int T, int Hq, int Hkv, int D, bool rope);
 
+// ---- decode_attn.hip (serving: one query token per sequence vs a bf16 KV cache, split over the sequence)
+struct DecodeAttnParams {
+  const bf16_t* q;  // [B, Hq, D] view (q_sb, q_sh strides), D contiguous
+  const bf16_t* k;  // cache [B, Tmax, Hkv, D] view (k_sb, k_st, k_sh)
+  const bf16_t* v;
+  bf16_t* o;        // [B, Hq, D] contiguous
+  float* ws_acc;    // [B, Hq, splits, D] fp32 (splits > 1)
+  float* ws_ml;     // [B, Hq, splits, 2] fp32 (running max in log2 units, sum)
+  int64_t q_sb, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh;
+  int B, Hq, Hkv, D, L, splits, chunk;
+  float scale_log2;  // softmax scale * log2(e)
+};
+int decode_attn_splits(int B, int Hkv, int L, int D);
+hipError_t decode_attention(DecodeAttnParams p, hipStream_t st);
+
 // ---- embed.hip
 hipError_t embedding_fwd(const int64_t* idx, const bf16_t* table, bf16_t* out, int64_t n, int64_t D, hipStream_t st);
 hipError_t embedding_bwd(const int64_t* idx, const bf16_t* dy, float* acc, int64_t n, int64_t D, hipStream_t st);

@@ -68,6 +68,14 @@ class GPT2Block(tnn.Module):
         h = ops.gelu_tanh(self.c_fc(self.ln_2(x)))
         return x + self.mlp_proj(h)
 
+    @torch.no_grad()
+    def forward_cached(self, x, k_cache, v_cache, pos: int):
+        B, T, d = x.shape
+        qkv = self.c_attn(self.ln_1(x)).view(B, T, 3 * self.n_head, d // self.n_head)
+        a = ops.attention_cached(qkv, self.n_head, self.n_head, k_cache, v_cache, pos)
+        x = x + self.attn_proj(a.reshape(B, T, d))
+        return x + self.mlp_proj(ops.gelu_tanh(self.c_fc(self.ln_2(x))))
+
 
 class GPT2(tnn.Module):
     def __init__(self, cfg: GPT2Config, device=None, dtype=None):
@@ -110,6 +118,30 @@ class GPT2(tnn.Module):
         for blk in self.h:
             x = blk(x)
         return self.head(x, targets)
+
+    # ---------------------------------------------------------------- serving (serving/generate.py)
+    def kv_shape(self):
+        return self.cfg.n_layer, self.cfg.n_head, self.cfg.n_embd // self.cfg.n_head
+
+    @property
+    def layers(self):
+        return self.h
+
+    @torch.no_grad()
+    def forward_cached(self, idx, cache, pos: int, last_only: bool = True):
+        """Logits for tokens ``idx`` [B, T] at positions pos..pos+T-1 over ``cache`` (see Llama)."""
+        dev0 = self.wte.device
+        idx = idx.to(dev0)
+        T = idx.shape[1]
+        positions = torch.arange(pos, pos + T, device=dev0)
+        x = ops.embedding(idx, self.wte) + ops.embedding(positions, self.wpe).unsqueeze(0)
+        for i, blk in enumerate(self.h):
+            x = x.to(blk.c_attn.weight.device, non_blocking=True)
+            x = blk.forward_cached(x, cache.k[i], cache.v[i], pos)
+        if last_only:
+            x = x[:, -1:]
+        x = x.to(dev0, non_blocking=True)  # tied head: LM projection with the embedding table
+        return self.head(x)
 
     def num_params(self, exclude_padding=True) -> int:
         n = sum(p.numel() for p in self.parameters())

@@ -68,6 +68,16 @@ class LlamaBlock(tnn.Module):
         h = x + self.wo(a.reshape(B, T, d))
         return h + self.w2(ops.swiglu(self.w13(self.ffn_norm(h))))
 
+    @torch.no_grad()
+    def forward_cached(self, x, k_cache, v_cache, pos: int, rope):
+        """Inference step over a KV cache (prefill at pos 0 or one decode token); see ops.attention_cached."""
+        B, T, d = x.shape
+        c = self.cfg
+        qkv = self.wqkv(self.attention_norm(x)).view(B, T, c.n_heads + 2 * c.n_kv_heads, c.head_dim)
+        a = ops.attention_cached(qkv, c.n_heads, c.n_kv_heads, k_cache, v_cache, pos, rope)
+        h = x + self.wo(a.reshape(B, T, d))
+        return h + self.w2(ops.swiglu(self.w13(self.ffn_norm(h))))
+
 
 class Llama(tnn.Module):
     def __init__(self, cfg: LlamaConfig, device=None, dtype=None):
@@ -108,6 +118,28 @@ class Llama(tnn.Module):
         if targets is None:
             return logits
         return ops.cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1))
+
+    # ---------------------------------------------------------------- serving (serving/generate.py)
+    def kv_shape(self):
+        """(n_layers, n_kv_heads, head_dim) of the KV cache this model needs."""
+        return self.cfg.n_layers, self.cfg.n_kv_heads, self.cfg.head_dim
+
+    @torch.no_grad()
+    def forward_cached(self, idx, cache, pos: int, last_only: bool = True):
+        """Logits for tokens ``idx`` [B, T] at positions pos..pos+T-1, reading/extending ``cache``
+        (:class:`~pytorchdistributed_amd.serving.KVCache`).  Layers may live on different devices
+        (``serving.place``): the hidden state follows them."""
+        dev0 = self.tok_embeddings.device
+        x = ops.embedding(idx.to(dev0), self.tok_embeddings)
+        for i, blk in enumerate(self.layers):
+            dev = blk.wqkv.weight.device
+            x = x.to(dev, non_blocking=True)
+            rope = self.rope(cache.max_len, dev)
+            x = blk.forward_cached(x, cache.k[i], cache.v[i], pos, rope)
+        if last_only:
+            x = x[:, -1:]
+        x = x.to(self.output.weight.device, non_blocking=True)
+        return self.output(self.norm(x))
 
 
 def llama(name: str = "llama3-8b", device=None, dtype=None, **overrides) -> Llama:

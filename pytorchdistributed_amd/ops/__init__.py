@@ -12,4 +12,5 @@ from .pool import max_pool2d, global_avg_pool2d  # noqa: F401
 from .loss import cross_entropy  # noqa: F401
 from .act import relu, gelu_tanh, swiglu  # noqa: F401
 from .synth import fill_normal_, fill_uniform_, fill_randint_  # noqa: F401
-from .attention import attention_qkv, attention_ref, embedding, rope_tables  # noqa: F401
+from .attention import (attention_cached, attention_qkv, attention_ref, decode_attention, embedding,  # noqa: F401
+                        rope_tables)

@@ -100,6 +100,64 @@ def attention_qkv(qkv: torch.Tensor, n_heads: int, n_kv_heads: Optional[int] = N
     return attention_ref(q, k, v, causal, scale, rope)
 
 
+# ---------------------------------------------------------------- serving (KV cache, no autograd)
+def _rope_at(x, cos, sin, pos):
+    """Reference rotation of x [B, T, H, D] at absolute positions pos..pos+T-1."""
+    return _rope_ref(x, cos[pos: pos + x.shape[1]], sin[pos: pos + x.shape[1]])
+
+
+def decode_attention(q, k_cache, v_cache, L: int, scale: Optional[float] = None, splits: int = 0):
+    """One query token per sequence against the first ``L`` rows of a KV cache.
+
+    q ``[B, 1, Hq, D]``, caches ``[B, Tmax, Hkv, D]`` (GQA: Hq a multiple of Hkv).  GPU bf16: the
+    split-sequence HIP kernel (`csrc/kernels/decode_attn.hip`); otherwise reference math."""
+    D = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if q.is_cuda and q.dtype == torch.bfloat16 and D in (64, 128):
+        return C().decode_attn(q, k_cache, v_cache, L, scale, splits)
+    return attention_ref(q, k_cache[:, :L], v_cache[:, :L], causal=False, scale=scale)
+
+
+@torch.no_grad()
+def attention_cached(qkv: torch.Tensor, n_heads: int, n_kv_heads: int, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                     pos: int, rope: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                     scale: Optional[float] = None) -> torch.Tensor:
+    """Inference attention over a KV cache (SURVEY §2.4 W8 serving path).
+
+    ``qkv`` ``[B, T, Hq + 2*Hkv, D]`` holds the new tokens at positions ``pos .. pos+T-1``; their
+    (rotated) K and V are written into ``k_cache``/``v_cache`` ``[B, Tmax, Hkv, D]`` rows
+    ``pos .. pos+T-1``.  ``T > 1`` is a prefill from position 0 (causal flash attention over the
+    prompt); ``T == 1`` is a decode step (split-sequence decode kernel over ``pos + 1`` rows).
+    ``rope`` = full-length (cos, sin) tables, indexed by absolute position.  Returns ``[B, T, Hq, D]``.
+    """
+    B, T, _, D = qkv.shape
+    hq, hkv = n_heads, n_kv_heads
+    if pos + T > k_cache.shape[1]:
+        raise ValueError(f"KV cache holds {k_cache.shape[1]} positions, step needs {pos + T}")
+    if T > 1 and pos != 0:
+        raise ValueError("multi-token steps are prefills from position 0 (decode one token at a time)")
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    q, k, v = qkv[:, :, :hq], qkv[:, :, hq: hq + hkv], qkv[:, :, hq + hkv:]
+    kc, vc = k_cache[:, pos: pos + T], v_cache[:, pos: pos + T]
+    native = qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128)
+    if rope is not None:
+        cs, sn = rope[0][pos: pos + T], rope[1][pos: pos + T]
+        if native:
+            q = C().rope(q, cs, sn, False, None)
+            C().rope(k, cs, sn, False, kc)  # rotated K straight into the cache rows
+        else:
+            q = _rope_at(q, rope[0], rope[1], pos)
+            kc.copy_(_rope_at(k, rope[0], rope[1], pos))
+    else:
+        kc.copy_(k)
+    vc.copy_(v)
+    if T == 1:
+        return decode_attention(q, k_cache, v_cache, pos + 1, scale)
+    if native:
+        return C().attn_fwd(q, kc, vc, scale, True, None, None)[0]
+    return attention_ref(q, kc, vc, causal=True, scale=scale)
+
+
 class _EmbeddingFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx, table):

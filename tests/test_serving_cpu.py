@@ -1,0 +1,55 @@
+"""Serving path on CPU (reference math): KV-cached generation == uncached full forward, for Llama-3
+(GQA + RoPE) and GPT-2 (learned positions, tied head); placement map; sampling determinism."""
+import pytest
+import torch
+
+from pytorchdistributed_amd.models.gpt2 import gpt2
+from pytorchdistributed_amd.models.llama import llama
+from pytorchdistributed_amd.serving import KVCache, generate, place
+
+
+def _tiny(kind):
+    torch.manual_seed(0)
+    if kind == "llama":
+        return llama("llama3-tiny", dtype=torch.float32).eval()
+    return gpt2("gpt2", n_layer=2, n_embd=128, n_head=2, vocab_size=500, n_positions=128, dtype=torch.float32).eval()
+
+
+@pytest.mark.parametrize("kind", ["llama", "gpt2"])
+def test_cached_generation_matches_full_forward(kind):
+    m = _tiny(kind)
+    g = torch.Generator().manual_seed(1)
+    prompt = torch.randint(0, 500, (2, 7), generator=g)
+    toks, logits = generate(m, prompt, max_new_tokens=6, return_logits=True)
+    assert toks.shape == (2, 13) and torch.equal(toks[:, :7], prompt)
+    with torch.no_grad():
+        for i in range(6):
+            full = m(toks[:, : 7 + i])
+            full = full[..., :logits.shape[-1]]
+            assert torch.allclose(logits[:, i], full[:, -1].float(), atol=1e-4, rtol=1e-4), i
+            # greedy: the emitted token is the argmax of the full-forward logits
+            assert torch.equal(toks[:, 7 + i], full[:, -1].argmax(-1))
+
+
+def test_sampling_is_seeded_and_eos_sticks():
+    m = _tiny("llama")
+    prompt = torch.randint(0, 500, (3, 4), generator=torch.Generator().manual_seed(2))
+    a = generate(m, prompt, 8, temperature=0.8, top_k=20, generator=torch.Generator().manual_seed(5))
+    b = generate(m, prompt, 8, temperature=0.8, top_k=20, generator=torch.Generator().manual_seed(5))
+    assert torch.equal(a, b)
+    first = generate(m, prompt, 1)[:, -1]
+    eos = int(first[0])
+    out = generate(m, prompt, 6, eos_token=eos)
+    assert (out[0, 4:] == eos).all()
+
+
+def test_kv_cache_sizing_and_placement_map():
+    m = _tiny("llama")
+    c = KVCache(m, batch=2, max_len=16)
+    assert c.k[0].shape == (2, 16, 1, 128) and c.nbytes() == 2 * 2 * 2 * 16 * 128 * 4
+    assert KVCache.bytes_per_token(m, torch.bfloat16) == 2 * 2 * 1 * 128 * 2
+    dmap = place(m, devices=["cpu"], max_memory={"cpu": 1 << 40})
+    assert dmap["layers.0"] == torch.device("cpu") and dmap["output"] == torch.device("cpu")
+    # Llama-3-8B: 128 KiB of bf16 KV cache per token (32 layers x 8 KV heads x 128 x 2)
+    big = llama("llama3-8b", device="meta")
+    assert KVCache.bytes_per_token(big) == 131072

@@ -1,0 +1,57 @@
+"""Serving on the MI355X: the split-sequence decode-attention kernel vs fp32 reference math (GQA groups
+1/2/4/8, D 64/128, ragged lengths, forced and automatic splits, NaN-poisoned cache rows beyond L that
+must never be read into the result), and KV-cached bf16 generation vs the uncached forward."""
+import math
+
+import pytest
+import torch
+
+from pytorchdistributed_amd import _native
+from pytorchdistributed_amd.models.gpt2 import gpt2
+from pytorchdistributed_amd.models.llama import llama
+from pytorchdistributed_amd.ops.attention import attention_ref, decode_attention
+from pytorchdistributed_amd.serving import generate
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("B,L,Hq,Hkv,D,splits", [
+    (2, 1, 4, 1, 128, 0), (3, 300, 32, 8, 128, 0), (3, 300, 32, 8, 128, 1), (1, 4097, 16, 16, 64, 0),
+    (4, 1000, 8, 1, 64, 0), (2, 777, 8, 4, 128, 7), (1, 8192, 32, 8, 128, 0), (5, 129, 12, 6, 64, 3)])
+def test_decode_attention_kernel(B, L, Hq, Hkv, D, splits):
+    _native.C()
+    torch.manual_seed(B * 1000 + L)
+    dev = "cuda"
+    Tmax = L + 37
+    k = torch.randn(B, Tmax, Hkv, D, device=dev, dtype=torch.bfloat16)
+    v = torch.randn(B, Tmax, Hkv, D, device=dev, dtype=torch.bfloat16)
+    k[:, L:] = float("nan")
+    v[:, L:] = float("nan")
+    qkv = torch.randn(B, 1, Hq + 2 * Hkv, D, device=dev, dtype=torch.bfloat16)
+    q = qkv[:, :, :Hq]  # strided view, as in the model
+    out = decode_attention(q, k, v, L, splits=splits)
+    ref = attention_ref(q, k[:, :L], v[:, :L], causal=False, scale=1 / math.sqrt(D))
+    assert out.shape == (B, 1, Hq, D)
+    assert torch.isfinite(out.float()).all()
+    err = (out.float() - ref.float()).abs().max().item()
+    assert err < 2e-2, err
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm()).item()
+
+
+@pytest.mark.parametrize("kind", ["llama", "gpt2"])
+def test_cached_generation_bf16_matches_full_forward(kind):
+    torch.manual_seed(0)
+    if kind == "llama":
+        m = llama("llama3-tiny", device="cuda", dtype=torch.bfloat16).eval()
+    else:
+        m = gpt2("gpt2", n_layer=2, n_embd=256, n_head=4, vocab_size=500, n_positions=256, device="cuda",
+                 dtype=torch.bfloat16).eval()
+    prompt = torch.randint(0, 500, (3, 40), device="cuda")
+    toks, logits = generate(m, prompt, max_new_tokens=12, return_logits=True)
+    with torch.no_grad():
+        for i in (0, 5, 11):
+            full = m(toks[:, : 40 + i])[..., : logits.shape[-1]]
+            assert _rel(logits[:, i], full[:, -1]) < 2e-2, i
