@@ -718,7 +718,8 @@ void attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, T
 // ------------------------------------------------------------------ decode attention (serving)
 // q [B, 1, Hq, D] (any B/H strides), k/v caches [B, Tmax, Hkv, D] (any strides, contiguous D); attends the
 // first L cache rows; returns o [B, 1, Hq, D]
-Tensor decode_attn(Tensor q, Tensor k, Tensor v, int64_t L, double scale, int64_t splits) {
+Tensor decode_attn(Tensor q, Tensor k, Tensor v, int64_t L, double scale, int64_t splits,
+                   c10::optional<Tensor> pos_dev) {
   attn_check(q, "q");
   attn_check(k, "k cache");
   attn_check(v, "v cache");
@@ -729,6 +730,10 @@ Tensor decode_attn(Tensor q, Tensor k, Tensor v, int64_t L, double scale, int64_
   TORCH_CHECK(Hkv > 0 && Hq % Hkv == 0 && (Hq / Hkv == 1 || Hq / Hkv == 2 || Hq / Hkv == 4 || Hq / Hkv == 8),
               "decode_attn: query heads per kv head must be 1, 2, 4 or 8");
   TORCH_CHECK(L >= 1 && L <= k.size(1), "decode_attn: L must be in [1, cache length]");
+  if (pos_dev.has_value()) {
+    check_gpu(*pos_dev, "pos");
+    TORCH_CHECK(pos_dev->scalar_type() == at::kInt && pos_dev->numel() == 1, "decode_attn: pos must be one int32");
+  }
   c10::DeviceGuard g(q.device());
   Tensor o = at::empty({B, 1, Hq, D}, q.options());
   pda::DecodeAttnParams p{};
@@ -739,6 +744,8 @@ Tensor decode_attn(Tensor q, Tensor k, Tensor v, int64_t L, double scale, int64_
   p.B = B; p.Hq = Hq; p.Hkv = Hkv; p.D = D; p.L = (int)L;
   p.splits = splits > 0 ? (int)splits : pda::decode_attn_splits(B, Hkv, (int)L, D);
   p.scale_log2 = (float)(scale * 1.4426950408889634);
+  // device position (graph replay): L is the cache capacity here; the kernel reads pos + 1 at run time
+  p.L_dev = pos_dev.has_value() ? pos_dev->data_ptr<int>() : nullptr;
   Tensor ws;
   if (p.splits > 1) {
     ws = at::empty({(int64_t)B * Hq * p.splits * (D + 2)}, q.options().dtype(at::kFloat));
@@ -747,6 +754,41 @@ Tensor decode_attn(Tensor q, Tensor k, Tensor v, int64_t L, double scale, int64_
   }
   CHECK_HIP_OK(pda::decode_attention(p, stream_of(q)));
   return o;
+}
+
+// new decode token: q rotated -> returned [B, 1, Hq, D]; k rotated into k_cache[:, pos]; v into v_cache[:, pos];
+// pos is a device int32 (graph-replayable); rope tables optional (GPT-2 has none)
+Tensor kv_append(Tensor qkv, Tensor k_cache, Tensor v_cache, Tensor pos, int64_t n_heads, int64_t n_kv_heads,
+                 c10::optional<Tensor> cs, c10::optional<Tensor> sn) {
+  attn_check(qkv, "qkv");
+  attn_check(k_cache, "k cache");
+  attn_check(v_cache, "v cache");
+  check_gpu(pos, "pos");
+  TORCH_CHECK(pos.scalar_type() == at::kInt && pos.numel() == 1, "kv_append: pos must be one int32");
+  const int B = qkv.size(0), D = qkv.size(3);
+  TORCH_CHECK(qkv.size(1) == 1 && qkv.size(2) == n_heads + 2 * n_kv_heads, "kv_append: qkv must be [B, 1, Hq+2Hkv, D]");
+  TORCH_CHECK(k_cache.size(0) == B && k_cache.size(2) == n_kv_heads && k_cache.size(3) == D &&
+              v_cache.sizes() == k_cache.sizes(), "kv_append: cache shape mismatch");
+  TORCH_CHECK(D % 2 == 0 && D <= 128, "kv_append: head dim must be even and <= 128");
+  c10::DeviceGuard g(qkv.device());
+  Tensor q = at::empty({B, 1, n_heads, D}, qkv.options());
+  pda::KvAppendParams p{};
+  p.qkv = bp(qkv); p.q_out = bpm(q); p.k_cache = bpm(k_cache); p.v_cache = bpm(v_cache);
+  p.cos = p.sin = nullptr;
+  if (cs.has_value()) {
+    check_f32(*cs, "cos");
+    check_f32(*sn, "sin");
+    TORCH_CHECK(cs->numel() >= k_cache.size(1) * D / 2, "kv_append: rope tables must cover the cache length");
+    p.cos = cs->data_ptr<float>();
+    p.sin = sn->data_ptr<float>();
+  }
+  p.pos = pos.data_ptr<int>();
+  p.x_sb = qkv.stride(0); p.x_sh = qkv.stride(2);
+  p.k_sb = k_cache.stride(0); p.k_st = k_cache.stride(1); p.k_sh = k_cache.stride(2);
+  p.v_sb = v_cache.stride(0); p.v_st = v_cache.stride(1); p.v_sh = v_cache.stride(2);
+  p.B = B; p.Hq = (int)n_heads; p.Hkv = (int)n_kv_heads; p.D = D;
+  CHECK_HIP_OK(pda::kv_append_rope(p, stream_of(qkv)));
+  return q;
 }
 
 // ------------------------------------------------------------------ embedding / rope
@@ -938,7 +980,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("rownorm_bwd", &rownorm_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("decode_attn", &decode_attn, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("L"), py::arg("scale"),
-        py::arg("splits") = 0);
+        py::arg("splits") = 0, py::arg("pos_dev") = py::none());
+  m.def("kv_append", &kv_append);
   m.def("attn_bwd", &attn_bwd);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);

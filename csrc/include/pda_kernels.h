@@ -186,7 +186,19 @@ struct DecodeAttnParams {
   int64_t q_sb, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh;
   int B, Hq, Hkv, D, L, splits, chunk;
   float scale_log2;  // softmax scale * log2(e)
+  const int* L_dev;  // optional: attend *L_dev + 1 rows (graph-replayable decode; overrides L)
 };
+struct KvAppendParams {
+  const bf16_t* qkv;  // new token [B, 1, Hq + 2*Hkv, D] view (x_sb, x_sh), D contiguous
+  bf16_t* q_out;      // [B, Hq, D] contiguous, rotated q
+  bf16_t* k_cache;    // [B, Tmax, Hkv, D] view
+  bf16_t* v_cache;
+  const float *cos, *sin;  // full-length rope tables [Tmax, D/2] or nullptr
+  const int* pos;          // device position of the new token
+  int64_t x_sb, x_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh;
+  int B, Hq, Hkv, D;
+};
+hipError_t kv_append_rope(const KvAppendParams& p, hipStream_t st);
 int decode_attn_splits(int B, int Hkv, int L, int D);
 hipError_t decode_attention(DecodeAttnParams p, hipStream_t st);
 

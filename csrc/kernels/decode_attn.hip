@@ -23,7 +23,7 @@ namespace {
 
 constexpr int kDecThreads = 256;
 constexpr int kDecWaves = kDecThreads / 64;
-constexpr int kSteps = 8;  // row-steps per wave tile (loads in flight per lane)
+constexpr int kMaxSteps = 8;  // row-steps per wave tile (loads in flight per lane)
 
 __device__ __forceinline__ float xor_sum(float v, int lo, int hi) {
   for (int o = lo; o < hi; o <<= 1) v += __shfl_xor(v, o, 64);
@@ -38,12 +38,14 @@ template <int D, int G>
 __global__ void __launch_bounds__(kDecThreads) decode_attn_kernel(DecodeAttnParams p) {
   constexpr int DCH = D / 8;        // 16-B chunks per row
   constexpr int KPI = 64 / DCH;     // rows per wave instruction
+  constexpr int kSteps = G >= 8 ? 4 : kMaxSteps;  // G = 8: fewer rows in flight keeps 1 wave/SIMD spill-free
   constexpr int TILE = KPI * kSteps;  // rows per wave tile
   const int split = blockIdx.x, hkv = blockIdx.y, b = blockIdx.z;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int kk = lane / DCH, c = lane % DCH;
-  const int L = p.L;
-  const int chunk = p.chunk;
+  // graph-replayable decode: the length comes from device memory (pos + 1 of this step)
+  const int L = p.L_dev != nullptr ? *p.L_dev + 1 : p.L;
+  const int chunk = p.L_dev != nullptr ? (L + p.splits - 1) / p.splits : p.chunk;
   const int k0 = split * chunk;
   const int k1 = min(L, k0 + chunk);
 
@@ -194,6 +196,34 @@ __global__ void __launch_bounds__(D) decode_combine_kernel(DecodeAttnParams p) {
   p.o[bh * D + d] = f2bf(ls > 0.f ? o / ls : 0.f);
 }
 
+// New token of a decode step, graph-replayable (position read from device memory): q rotated into
+// q_out, k rotated into k_cache[:, pos], v copied into v_cache[:, pos].  One wave per (batch, head),
+// lane i owns the rotate-half pairs (i, i + D/2) (D = 128: one pair, D = 64: lanes 0..31).
+__global__ void __launch_bounds__(64) kv_append_rope_kernel(KvAppendParams p) {
+  const int b = blockIdx.y, h = blockIdx.x, i = threadIdx.x;
+  const int half = p.D / 2;
+  if (i >= half) return;
+  const int pos = *p.pos;
+  const bf16_t* x = p.qkv + (int64_t)b * p.x_sb + (int64_t)h * p.x_sh;
+  const float x1 = bf2f(x[i]), x2 = bf2f(x[i + half]);
+  if (h >= p.Hq + p.Hkv) {  // V: plain copy
+    bf16_t* dst = p.v_cache + (int64_t)b * p.v_sb + (int64_t)pos * p.v_st + (int64_t)(h - p.Hq - p.Hkv) * p.v_sh;
+    dst[i] = x[i];
+    dst[i + half] = x[i + half];
+    return;
+  }
+  float y1 = x1, y2 = x2;
+  if (p.cos != nullptr) {
+    const float cs = p.cos[(int64_t)pos * half + i], sn = p.sin[(int64_t)pos * half + i];
+    y1 = x1 * cs - x2 * sn;
+    y2 = x2 * cs + x1 * sn;
+  }
+  bf16_t* dst = h < p.Hq ? p.q_out + ((int64_t)b * p.Hq + h) * p.D
+                         : p.k_cache + (int64_t)b * p.k_sb + (int64_t)pos * p.k_st + (int64_t)(h - p.Hq) * p.k_sh;
+  dst[i] = f2bf(y1);
+  dst[i + half] = f2bf(y2);
+}
+
 template <int D, int G>
 hipError_t launch_decode(const DecodeAttnParams& p, hipStream_t st) {
   dim3 grid((unsigned)p.splits, (unsigned)p.Hkv, (unsigned)p.B);
@@ -218,7 +248,7 @@ hipError_t dispatch_g(const DecodeAttnParams& p, hipStream_t st) {
 
 int decode_attn_splits(int B, int Hkv, int L, int D) {
   // enough workgroups to cover the 256 CUs twice, but every split keeps >= one full pass of its 4 waves
-  const int rows_per_pass = kDecWaves * (64 / (D / 8)) * kSteps;
+  const int rows_per_pass = kDecWaves * (64 / (D / 8)) * kMaxSteps;
   const int max_splits = (L + rows_per_pass - 1) / rows_per_pass;
   int s = (512 + B * Hkv - 1) / (B * Hkv);
   if (s > max_splits) s = max_splits;
@@ -226,9 +256,16 @@ int decode_attn_splits(int B, int Hkv, int L, int D) {
   return s < 1 ? 1 : s;
 }
 
+hipError_t kv_append_rope(const KvAppendParams& p, hipStream_t st) {
+  if (p.D % 2 || p.D / 2 > 64) return hipErrorInvalidValue;
+  dim3 grid((unsigned)(p.Hq + 2 * p.Hkv), (unsigned)p.B);
+  kv_append_rope_kernel<<<grid, 64, 0, st>>>(p);
+  return hipGetLastError();
+}
+
 hipError_t decode_attention(DecodeAttnParams p, hipStream_t st) {
-  if (p.L < 1 || p.Hkv < 1 || p.Hq % p.Hkv || p.splits < 1) return hipErrorInvalidValue;
-  p.chunk = (p.L + p.splits - 1) / p.splits;
+  if ((p.L_dev == nullptr && p.L < 1) || p.Hkv < 1 || p.Hq % p.Hkv || p.splits < 1) return hipErrorInvalidValue;
+  p.chunk = p.L_dev != nullptr ? 0 : (p.L + p.splits - 1) / p.splits;
   if (p.D == 64) return dispatch_g<64>(p, st);
   if (p.D == 128) return dispatch_g<128>(p, st);
   return hipErrorInvalidValue;

@@ -133,7 +133,10 @@ class GPT2(tnn.Module):
         dev0 = self.wte.device
         idx = idx.to(dev0)
         T = idx.shape[1]
-        positions = torch.arange(pos, pos + T, device=dev0)
+        if isinstance(pos, torch.Tensor):  # device position (graph-replayed decode step)
+            positions = pos.to(dev0, torch.long).view(1)
+        else:
+            positions = torch.arange(pos, pos + T, device=dev0)
         x = ops.embedding(idx, self.wte) + ops.embedding(positions, self.wpe).unsqueeze(0)
         for i, blk in enumerate(self.h):
             x = x.to(blk.c_attn.weight.device, non_blocking=True)

@@ -120,7 +120,7 @@ def decode_attention(q, k_cache, v_cache, L: int, scale: Optional[float] = None,
 
 @torch.no_grad()
 def attention_cached(qkv: torch.Tensor, n_heads: int, n_kv_heads: int, k_cache: torch.Tensor, v_cache: torch.Tensor,
-                     pos: int, rope: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                     pos, rope: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
                      scale: Optional[float] = None) -> torch.Tensor:
     """Inference attention over a KV cache (SURVEY §2.4 W8 serving path).
 
@@ -129,17 +129,28 @@ def attention_cached(qkv: torch.Tensor, n_heads: int, n_kv_heads: int, k_cache: 
     ``pos .. pos+T-1``.  ``T > 1`` is a prefill from position 0 (causal flash attention over the
     prompt); ``T == 1`` is a decode step (split-sequence decode kernel over ``pos + 1`` rows).
     ``rope`` = full-length (cos, sin) tables, indexed by absolute position.  Returns ``[B, T, Hq, D]``.
+    ``pos`` may be a device int32 tensor (decode only): the position is then read by the kernels at
+    run time, so the whole step can be captured once in a HIP graph and replayed every token.
     """
     B, T, _, D = qkv.shape
     hq, hkv = n_heads, n_kv_heads
+    native = qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if isinstance(pos, torch.Tensor):
+        # device-resident position (HIP-graph replayable decode step): one append + one attention launch
+        if T != 1:
+            raise ValueError("a device position drives single-token decode steps only")
+        if native:
+            cs, sn = rope if rope is not None else (None, None)
+            q = C().kv_append(qkv, k_cache, v_cache, pos, hq, hkv, cs, sn)
+            return C().decode_attn(q, k_cache, v_cache, k_cache.shape[1], scale, 0, pos)
+        pos = int(pos.item())
     if pos + T > k_cache.shape[1]:
         raise ValueError(f"KV cache holds {k_cache.shape[1]} positions, step needs {pos + T}")
     if T > 1 and pos != 0:
         raise ValueError("multi-token steps are prefills from position 0 (decode one token at a time)")
-    scale = scale if scale is not None else 1.0 / math.sqrt(D)
     q, k, v = qkv[:, :, :hq], qkv[:, :, hq: hq + hkv], qkv[:, :, hq + hkv:]
     kc, vc = k_cache[:, pos: pos + T], v_cache[:, pos: pos + T]
-    native = qkv.is_cuda and qkv.dtype == torch.bfloat16 and D in (64, 128)
     if rope is not None:
         cs, sn = rope[0][pos: pos + T], rope[1][pos: pos + T]
         if native:

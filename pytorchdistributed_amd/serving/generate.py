@@ -65,16 +65,47 @@ def _sample(logits: torch.Tensor, temperature: float, top_k: Optional[int], gen:
     return torch.multinomial(probs, 1, generator=gen)
 
 
+class _GraphedDecode:
+    """One decode step (embedding -> all blocks -> head) captured in a HIP graph.  The token and the
+    position live in static device buffers; the append / attention kernels read the position at run
+    time, so replaying the graph after ``tok.copy_(next); pos += 1`` is a real next step."""
+
+    def __init__(self, model, cache: KVCache, pos0: int):
+        dev = next(model.parameters()).device
+        self.tok = torch.zeros(cache.batch, 1, dtype=torch.long, device=dev)
+        self.pos = torch.full((1,), pos0, dtype=torch.int32, device=dev)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # warm-up outside capture (plans, rope tables); row pos0 is rewritten later
+            model.forward_cached(self.tok, cache, self.pos)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.logits = model.forward_cached(self.tok, cache, self.pos)
+
+    def __call__(self, tok):
+        self.tok.copy_(tok)
+        self.graph.replay()
+        self.pos += 1
+        return self.logits
+
+
+def _single_device(model) -> bool:
+    devs = {p.device for p in model.parameters()}
+    return len(devs) == 1 and next(iter(devs)).type == "cuda"
+
+
 @torch.no_grad()
 def generate(model: tnn.Module, prompt: torch.Tensor, max_new_tokens: int, temperature: float = 0.0,
              top_k: Optional[int] = None, eos_token: Optional[int] = None, cache: Optional[KVCache] = None,
-             generator: Optional[torch.Generator] = None, return_logits: bool = False):
+             generator: Optional[torch.Generator] = None, return_logits: bool = False, graph: bool = False):
     """Autoregressive generation: ``prompt`` [B, T0] token ids -> [B, T0 + max_new_tokens].
 
     One prefill over the prompt, then ``max_new_tokens - 1`` single-token decode steps over the KV cache.
     With ``eos_token``, finished sequences keep emitting ``eos_token`` (static batch shape).  With
     ``return_logits`` the per-step last-position logits are returned too (tests compare them with the
-    uncached forward)."""
+    uncached forward).  ``graph=True`` (one-GPU bf16 models) replays every decode step from one HIP
+    graph: no per-kernel launch cost, the step is bound by HBM traffic only."""
     B, T0 = prompt.shape
     if cache is None:
         cache = KVCache(model, B, T0 + max_new_tokens)
@@ -84,6 +115,9 @@ def generate(model: tnn.Module, prompt: torch.Tensor, max_new_tokens: int, tempe
     seq = [prompt]
     all_logits = [logits[:, -1].float().to(out_dev)] if return_logits else None
     done = torch.zeros(B, 1, dtype=torch.bool, device=out_dev)
+    step = None
+    if graph and max_new_tokens > 1 and _single_device(model):
+        step = _GraphedDecode(model, cache, T0)
     for i in range(max_new_tokens):
         nxt = _sample(logits, temperature, top_k, generator).to(out_dev)
         if eos_token is not None:
@@ -92,7 +126,7 @@ def generate(model: tnn.Module, prompt: torch.Tensor, max_new_tokens: int, tempe
         seq.append(nxt)
         if i == max_new_tokens - 1:
             break
-        logits = model.forward_cached(nxt, cache, cache.pos)
+        logits = step(nxt) if step is not None else model.forward_cached(nxt, cache, cache.pos)
         cache.pos += 1
         if return_logits:
             all_logits.append(logits[:, -1].float().to(out_dev))
