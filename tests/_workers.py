@@ -441,3 +441,88 @@ def pipeline_ckpt_worker(rank, world, chunks, outdir):
     with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
         f.write("ok")
     pd.destroy_process_group()
+
+
+def tp_llama_worker(rank, world, sp, outdir):
+    """Tensor-parallel Llama (gloo, CPU fp32): logits, loss and gradients == the full model; with
+    sequence parallelism too; and TP KV-cached generation == full-model generation."""
+    import copy
+
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.models.llama import llama
+    from pytorchdistributed_amd.parallel.tensor_parallel import tensor_parallel_llama, tp_sync_replicated_grads
+    from pytorchdistributed_amd.serving import generate
+
+    pd.init_process_group("gloo")
+    torch.manual_seed(0)
+    full = llama("llama3-tiny", n_heads=4, n_kv_heads=2, dim=256, ffn_dim=512, dtype=torch.float32)
+    tpm = tensor_parallel_llama(copy.deepcopy(full), None, sequence_parallel=sp)
+    g = torch.Generator().manual_seed(1)
+    idx = torch.randint(0, 1024, (2, 16), generator=g)
+    tgt = torch.randint(0, 1024, (2, 16), generator=g)
+    lf = full(idx, tgt)
+    lt = tpm(idx, tgt)
+    assert torch.allclose(lf, lt, atol=1e-5, rtol=1e-5), (lf.item(), lt.item())
+    lf.backward()
+    lt.backward()
+    tp_sync_replicated_grads(tpm)
+    tol = dict(atol=2e-5, rtol=1e-3)
+    assert torch.allclose(full.tok_embeddings.grad, tpm.tok_embeddings.grad, **tol)
+    assert torch.allclose(full.output.weight.grad, tpm.output.weight.grad, **tol)
+    c = full.cfg
+    hd, hq, hkv, f = c.head_dim, c.n_heads // world, c.n_kv_heads // world, c.ffn_dim // world
+    for bf, bt in zip(full.layers, tpm.layers):
+        gw = bf.wqkv.weight.grad
+        q = gw[rank * hq * hd:(rank + 1) * hq * hd]
+        k0 = c.n_heads * hd
+        k = gw[k0 + rank * hkv * hd: k0 + (rank + 1) * hkv * hd]
+        v0 = k0 + c.n_kv_heads * hd
+        v = gw[v0 + rank * hkv * hd: v0 + (rank + 1) * hkv * hd]
+        assert torch.allclose(torch.cat([q, k, v]), bt.wqkv.weight.grad, **tol)
+        assert torch.allclose(bf.wo.weight.grad[:, rank * hq * hd:(rank + 1) * hq * hd], bt.wo.weight.grad, **tol)
+        g13 = bf.w13.weight.grad
+        assert torch.allclose(torch.cat([g13[rank * f:(rank + 1) * f], g13[c.ffn_dim + rank * f: c.ffn_dim + (rank + 1) * f]]),
+                              bt.w13.weight.grad, **tol)
+        assert torch.allclose(bf.w2.weight.grad[:, rank * f:(rank + 1) * f], bt.w2.weight.grad, **tol)
+        assert torch.allclose(bf.attention_norm.weight.grad, bt.attention_norm.weight.grad, **tol)
+        assert torch.allclose(bf.ffn_norm.weight.grad, bt.ffn_norm.weight.grad, **tol)
+    if not sp:
+        prompt = torch.randint(0, 1024, (2, 5), generator=g)
+        t1, l1 = generate(full, prompt, 6, return_logits=True)
+        t2, l2 = generate(tpm, prompt, 6, return_logits=True)
+        assert torch.equal(t1, t2) and torch.allclose(l1, l2, atol=1e-4, rtol=1e-4)
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as fh:
+        fh.write("ok")
+    pd.destroy_process_group()
+
+
+def tp_llama_gpu_worker(rank, world, outdir):
+    """TP=2 Llama on the native bf16 kernels, both ranks sharing cuda:0 over gloo (rehearsal of the
+    RCCL path): loss == full model, TP KV-cached generation logits == full model's."""
+    import copy
+
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.models.llama import llama
+    from pytorchdistributed_amd.parallel.tensor_parallel import tensor_parallel_llama
+    from pytorchdistributed_amd.serving import generate
+
+    torch.cuda.set_device(0)
+    pd.init_process_group("gloo")
+    torch.manual_seed(0)
+    full = llama("llama3-tiny", n_heads=4, n_kv_heads=2, dim=256, ffn_dim=512, device="cuda", dtype=torch.bfloat16)
+    tpm = tensor_parallel_llama(copy.deepcopy(full), None)
+    g = torch.Generator().manual_seed(1)
+    idx = torch.randint(0, 1024, (2, 64), generator=g).cuda()
+    tgt = torch.randint(0, 1024, (2, 64), generator=g).cuda()
+    lf, lt = full(idx, tgt), tpm(idx, tgt)
+    assert abs(lf.item() - lt.item()) < 2e-2 * abs(lf.item()), (lf.item(), lt.item())
+    lt.backward()
+    assert all(torch.isfinite(p.grad.float()).all() for p in tpm.parameters() if p.grad is not None)
+    prompt = idx[:, :16]
+    _, l1 = generate(full.eval(), prompt, 6, return_logits=True)
+    _, l2 = generate(tpm.eval(), prompt, 6, return_logits=True)
+    rel = ((l1 - l2).norm() / l1.norm()).item()
+    assert rel < 3e-2, rel
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as fh:
+        fh.write("ok")
+    pd.destroy_process_group()
