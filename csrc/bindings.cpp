@@ -622,6 +622,25 @@ std::vector<Tensor> rownorm_fwd(Tensor x, Tensor gamma, c10::optional<Tensor> be
   return {y, mean, rstd};
 }
 
+// inference: (h = x + r, norm(h)) in one pass; all bf16, contiguous
+std::vector<Tensor> add_rownorm_fwd(Tensor x, Tensor r, Tensor gamma, c10::optional<Tensor> beta, double eps, bool rms) {
+  check_bf16(x, "x");
+  check_bf16(r, "r");
+  check_bf16(gamma, "gamma");
+  TORCH_CHECK(x.is_contiguous() && r.is_contiguous() && x.sizes() == r.sizes(), "add_rownorm: x, r contiguous, same shape");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && D <= 8192 && gamma.numel() == D, "norm width must be a multiple of 8 and <= 8192");
+  if (!rms) {
+    TORCH_CHECK(beta.has_value() && beta->numel() == D);
+    check_bf16(*beta, "beta");
+  }
+  c10::DeviceGuard g(x.device());
+  Tensor h = at::empty_like(x), y = at::empty_like(x);
+  CHECK_HIP_OK(pda::add_rownorm_fwd(bp(x), bp(r), bp(gamma), rms ? nullptr : bp(*beta), bpm(h), bpm(y), rows, D,
+                                    (float)eps, rms, stream_of(x)));
+  return {h, y};
+}
+
 std::vector<Tensor> rownorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, bool rms) {
   check_f32_or_bf16(dy, "dy");
   check_f32_or_bf16(x, "x");
@@ -977,6 +996,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("colsum", &colsum);
   m.def("simt_gemm", &simt_gemm);
   m.def("rownorm_fwd", &rownorm_fwd);
+  m.def("add_rownorm_fwd", &add_rownorm_fwd);
   m.def("rownorm_bwd", &rownorm_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("decode_attn", &decode_attn, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("L"), py::arg("scale"),

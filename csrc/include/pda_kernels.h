@@ -161,6 +161,8 @@ hipError_t simt_gemm(const void* A, int a_dt, int64_t sam, int64_t sak, const vo
                      const float* bias, bool relu, float beta, hipStream_t st);
 
 // ---- rownorm.hip (LayerNorm / RMSNorm over the last dim, D % 8 == 0, D <= 8192)
+hipError_t add_rownorm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* gamma, const bf16_t* beta, bf16_t* h,
+                           bf16_t* y, int64_t rows, int64_t D, float eps, bool rms, hipStream_t st);
 hipError_t rownorm_fwd(const void* x, bool x_bf16, const void* gamma, const void* beta, bool p_bf16, void* y,
                        float* mean, float* rstd, int64_t rows, int64_t D, float eps, bool rms, hipStream_t st);
 hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* gamma, bool p_bf16, const float* mean,

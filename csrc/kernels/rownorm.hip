@@ -241,6 +241,66 @@ int plan_slabs(int64_t rows, int64_t D) {
   return (int)nslab;
 }
 
+// Serving: residual add fused into the next norm — h = x + r (rounded to bf16, as the unfused add
+// would store it) is written once and normalised from registers (one HBM pass instead of add + norm).
+template <bool RMS, int VPL>
+__global__ void __launch_bounds__(kThreads) add_rownorm_fwd_kernel(const bf16_t* __restrict__ x,
+                                                                   const bf16_t* __restrict__ r,
+                                                                   const bf16_t* __restrict__ gamma,
+                                                                   const bf16_t* __restrict__ beta,
+                                                                   bf16_t* __restrict__ h, bf16_t* __restrict__ y,
+                                                                   int64_t rows, int64_t D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  float v[VPL][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int64_t c = ((int64_t)i * 64 + lane) * 8;
+    if (c < D) {
+      float a[8], b[8];
+      load8(x + row * D + c, a);
+      load8(r + row * D + c, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = bf2f(f2bf(a[j] + b[j]));
+        s += v[i][j];
+      }
+      store8(h + row * D + c, v[i]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  const float mean = RMS ? 0.f : wave_sum(s) / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int64_t c = ((int64_t)i * 64 + lane) * 8;
+    if (c < D) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[i][j] - mean;
+        q += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int64_t c = ((int64_t)i * 64 + lane) * 8;
+    if (c < D) {
+      float g[8], b[8], o[8];
+      load8(gamma + c, g);
+      if (!RMS) load8(beta + c, b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + (RMS ? 0.f : b[j]);
+      store8(y + row * D + c, o);
+    }
+  }
+}
+
 template <typename F>
 void dispatch_vpl(int64_t D, F&& f) {
   const int64_t vpl = (D + 511) / 512;
@@ -252,6 +312,18 @@ void dispatch_vpl(int64_t D, F&& f) {
 }
 
 }  // namespace
+
+hipError_t add_rownorm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* gamma, const bf16_t* beta, bf16_t* h,
+                           bf16_t* y, int64_t rows, int64_t D, float eps, bool rms, hipStream_t st) {
+  if (rows == 0) return hipSuccess;
+  const unsigned grid = (unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock);
+  dispatch_vpl(D, [&](auto vc) {
+    constexpr int V = decltype(vc)::value;
+    if (rms) add_rownorm_fwd_kernel<true, V><<<grid, kThreads, 0, st>>>(x, r, gamma, beta, h, y, rows, D, eps);
+    else add_rownorm_fwd_kernel<false, V><<<grid, kThreads, 0, st>>>(x, r, gamma, beta, h, y, rows, D, eps);
+  });
+  return hipGetLastError();
+}
 
 int64_t colreduce_ws_floats(int64_t rows, int64_t D, int nout) { return (int64_t)nout * plan_slabs(rows, D) * D; }
 

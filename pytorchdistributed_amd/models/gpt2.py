@@ -69,12 +69,19 @@ class GPT2Block(tnn.Module):
         return x + self.mlp_proj(h)
 
     @torch.no_grad()
-    def forward_cached(self, x, k_cache, v_cache, pos: int):
+    def forward_cached(self, x, k_cache, v_cache, pos, res=None):
+        """Serving step; pending-residual convention of LlamaBlock.forward_cached (input x + res,
+        returns (h, y) with output h + y) so each residual add is fused into the next LayerNorm."""
         B, T, d = x.shape
-        qkv = self.c_attn(self.ln_1(x)).view(B, T, 3 * self.n_head, d // self.n_head)
+        ln1, ln2 = self.ln_1, self.ln_2
+        if res is None:
+            h, n = x, ln1(x)
+        else:
+            h, n = ops.add_norm(x, res, ln1.weight, ln1.bias, eps=ln1.eps, rms=False)
+        qkv = self.c_attn(n).view(B, T, 3 * self.n_head, d // self.n_head)
         a = ops.attention_cached(qkv, self.n_head, self.n_head, k_cache, v_cache, pos)
-        x = x + self.attn_proj(a.reshape(B, T, d))
-        return x + self.mlp_proj(ops.gelu_tanh(self.c_fc(self.ln_2(x))))
+        h, n = ops.add_norm(h, self.attn_proj(a.reshape(B, T, d)), ln2.weight, ln2.bias, eps=ln2.eps, rms=False)
+        return h, self.mlp_proj(ops.gelu_tanh(self.c_fc(n)))
 
 
 class GPT2(tnn.Module):
@@ -138,13 +145,18 @@ class GPT2(tnn.Module):
         else:
             positions = torch.arange(pos, pos + T, device=dev0)
         x = ops.embedding(idx, self.wte) + ops.embedding(positions, self.wpe).unsqueeze(0)
+        res = None
         for i, blk in enumerate(self.h):
-            x = x.to(blk.c_attn.weight.device, non_blocking=True)
-            x = blk.forward_cached(x, cache.k[i], cache.v[i], pos)
+            dev = blk.c_attn.weight.device
+            x = x.to(dev, non_blocking=True)
+            res = res.to(dev, non_blocking=True) if res is not None else None
+            x, res = blk.forward_cached(x, cache.k[i], cache.v[i], pos, res)
         if last_only:
-            x = x[:, -1:]
-        x = x.to(dev0, non_blocking=True)  # tied head: LM projection with the embedding table
-        return self.head(x)
+            x, res = x[:, -1:], res[:, -1:]
+        # tied head: LM projection with the embedding table (final LN fused with the last residual add)
+        _, n = ops.add_norm(x.to(dev0, non_blocking=True), res.to(dev0, non_blocking=True), self.ln_f.weight,
+                            self.ln_f.bias, eps=self.ln_f.eps, rms=False)
+        return ops.linear(n, self.wte)[..., : self.cfg.vocab_size]
 
     def num_params(self, exclude_padding=True) -> int:
         n = sum(p.numel() for p in self.parameters())

@@ -69,14 +69,21 @@ class LlamaBlock(tnn.Module):
         return h + self.w2(ops.swiglu(self.w13(self.ffn_norm(h))))
 
     @torch.no_grad()
-    def forward_cached(self, x, k_cache, v_cache, pos: int, rope):
-        """Inference step over a KV cache (prefill at pos 0 or one decode token); see ops.attention_cached."""
+    def forward_cached(self, x, k_cache, v_cache, pos, rope, res=None):
+        """Inference step over a KV cache (prefill at pos 0 or one decode token; see
+        ops.attention_cached).  The residual stream is carried as a pending pair: the block's input
+        is ``x + res`` and it returns ``(h, y)`` whose sum is its output, so every residual add is
+        fused into the following norm (one pass, `add_rownorm_fwd_kernel`)."""
         B, T, d = x.shape
         c = self.cfg
-        qkv = self.wqkv(self.attention_norm(x)).view(B, T, c.n_heads + 2 * c.n_kv_heads, c.head_dim)
+        if res is None:
+            h, n = x, self.attention_norm(x)
+        else:
+            h, n = ops.add_norm(x, res, self.attention_norm.weight, eps=self.attention_norm.eps)
+        qkv = self.wqkv(n).view(B, T, c.n_heads + 2 * c.n_kv_heads, c.head_dim)
         a = ops.attention_cached(qkv, c.n_heads, c.n_kv_heads, k_cache, v_cache, pos, rope)
-        h = x + self.wo(a.reshape(B, T, d))
-        return h + self.w2(ops.swiglu(self.w13(self.ffn_norm(h))))
+        h, n = ops.add_norm(h, self.wo(a.reshape(B, T, d)), self.ffn_norm.weight, eps=self.ffn_norm.eps)
+        return h, self.w2(ops.swiglu(self.w13(n)))
 
 
 class Llama(tnn.Module):
@@ -130,16 +137,19 @@ class Llama(tnn.Module):
         (:class:`~pytorchdistributed_amd.serving.KVCache`).  Layers may live on different devices
         (``serving.place``): the hidden state follows them."""
         dev0 = self.tok_embeddings.device
-        x = ops.embedding(idx.to(dev0), self.tok_embeddings)
+        x, res = ops.embedding(idx.to(dev0), self.tok_embeddings), None
         for i, blk in enumerate(self.layers):
             dev = blk.wqkv.weight.device
             x = x.to(dev, non_blocking=True)
+            res = res.to(dev, non_blocking=True) if res is not None else None
             rope = self.rope(cache.max_len, dev)
-            x = blk.forward_cached(x, cache.k[i], cache.v[i], pos, rope)
+            x, res = blk.forward_cached(x, cache.k[i], cache.v[i], pos, rope, res)
         if last_only:
-            x = x[:, -1:]
-        x = x.to(self.output.weight.device, non_blocking=True)
-        return self.output(self.norm(x))
+            x, res = x[:, -1:], res[:, -1:]
+        dev = self.output.weight.device
+        _, n = ops.add_norm(x.to(dev, non_blocking=True), res.to(dev, non_blocking=True), self.norm.weight,
+                            eps=self.norm.eps)
+        return self.output(n)
 
 
 def llama(name: str = "llama3-8b", device=None, dtype=None, **overrides) -> Llama:

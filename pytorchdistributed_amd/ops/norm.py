@@ -132,3 +132,15 @@ def rms_norm(x, weight, eps=1e-6):
     xf = x.float()
     y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * weight.float()
     return y.to(x.dtype)
+
+
+@torch.no_grad()
+def add_norm(x, r, weight, bias=None, eps=1e-5, rms=True):
+    """Inference: ``h = x + r`` and ``norm(h)`` in one pass (serving path; no autograd).
+    Returns ``(h, normed)``.  GPU bf16: `rownorm.hip:add_rownorm_fwd_kernel`."""
+    if (x.is_cuda and x.dtype == torch.bfloat16 and r.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+            and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192):
+        h, y = C().add_rownorm_fwd(x.contiguous(), r.contiguous(), weight, bias, eps, rms)
+        return h, y
+    h = x + r
+    return h, (rms_norm(h, weight, eps) if rms else layer_norm(h, weight, bias, eps))

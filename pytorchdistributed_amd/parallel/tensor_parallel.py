@@ -199,16 +199,21 @@ class TPLlamaBlock(tnn.Module):
         return h + self.w2(ops.swiglu(self.w13(self.ffn_norm(h))))
 
     @torch.no_grad()
-    def forward_cached(self, x, k_cache, v_cache, pos, rope):
+    def forward_cached(self, x, k_cache, v_cache, pos, rope, res=None):
+        """Serving step (pending-residual convention of LlamaBlock.forward_cached)."""
         B, T, _ = x.shape
-        qkv = ops.linear(self.attention_norm(x), self.wqkv.weight).view(B, T, self.hq + 2 * self.hkv, self.hd)
+        if res is None:
+            h, n = x, self.attention_norm(x)
+        else:
+            h, n = ops.add_norm(x, res, self.attention_norm.weight, eps=self.attention_norm.eps)
+        qkv = ops.linear(n, self.wqkv.weight).view(B, T, self.hq + 2 * self.hkv, self.hd)
         a = ops.attention_cached(qkv, self.hq, self.hkv, k_cache, v_cache, pos, rope)
         o = ops.linear(a.reshape(B, T, self.hq * self.hd), self.wo.weight)
         dist.all_reduce(o, group=self.group)
-        h = x + o
-        y = ops.linear(ops.swiglu(ops.linear(self.ffn_norm(h), self.w13.weight)), self.w2.weight)
+        h, n = ops.add_norm(h, o, self.ffn_norm.weight, eps=self.ffn_norm.eps)
+        y = ops.linear(ops.swiglu(ops.linear(n, self.w13.weight)), self.w2.weight)
         dist.all_reduce(y, group=self.group)
-        return h + y
+        return h, y
 
 
 def tensor_parallel_llama(model, group=None, sequence_parallel: bool = False):

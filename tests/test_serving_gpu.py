@@ -90,3 +90,23 @@ def test_graphed_generation_matches_eager(kind):
     t2, l2 = generate(m, prompt, 10, return_logits=True, graph=True)
     assert _rel(l2, l1) < 1e-2
     assert (t1 == t2).float().mean().item() > 0.9  # bf16 ties may flip a late greedy choice
+
+
+@pytest.mark.parametrize("rows,D,rms", [(32, 4096, True), (7, 1024, False), (130, 1600, False), (1, 8192, True)])
+def test_add_norm_kernel(rows, D, rms):
+    from pytorchdistributed_amd.ops import add_norm
+
+    torch.manual_seed(rows)
+    x = torch.randn(rows, D, device="cuda", dtype=torch.bfloat16)
+    r = torch.randn_like(x)
+    w = torch.randn(D, device="cuda", dtype=torch.bfloat16)
+    b = None if rms else torch.randn(D, device="cuda", dtype=torch.bfloat16)
+    h, y = add_norm(x, r, w, b, eps=1e-5, rms=rms)
+    href = (x + r).float()
+    hb = (x + r).float()
+    if rms:
+        yref = hb * torch.rsqrt(hb.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+    else:
+        yref = torch.nn.functional.layer_norm(hb, (D,), w.float(), b.float(), 1e-5)
+    assert torch.equal(h.float(), href.bfloat16().float())
+    assert (y.float() - yref).abs().max().item() < 5e-2 * max(1.0, yref.abs().max().item() / 8)
