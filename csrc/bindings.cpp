@@ -810,6 +810,43 @@ Tensor kv_append(Tensor qkv, Tensor k_cache, Tensor v_cache, Tensor pos, int64_t
   return q;
 }
 
+// weight-only int8 GEMM (decode): x [M, K] bf16 (M <= 64, rows contiguous), w [N, K] int8, scale [N] fp32;
+// ws [>= 8 * 64 * N] fp32 (partial slabs) and tickets [>= N / 64] int32 (zero-initialised, left zeroed) are
+// caller-owned
+Tensor w8_gemm(Tensor x, Tensor w, Tensor scale, Tensor ws, Tensor tickets, int64_t splits) {
+  check_bf16(x, "x");
+  check_gpu(w, "w");
+  check_f32(scale, "scale");
+  TORCH_CHECK(w.scalar_type() == at::kChar && w.dim() == 2 && w.is_contiguous(), "w8_gemm: w must be int8 [N, K]");
+  const int64_t K = w.size(1), N = w.size(0);
+  TORCH_CHECK(x.size(-1) == K && x.stride(-1) == 1, "w8_gemm: x must be [..., K] with contiguous rows");
+  Tensor x2 = x.reshape({-1, K});
+  const int64_t M = x2.size(0);
+  TORCH_CHECK(M >= 1 && M <= 64, "w8_gemm: at most 64 rows (decode steps)");
+  TORCH_CHECK(N % pda::w8_gemm_rows() == 0 && K % 256 == 0 && scale.numel() == N, "w8_gemm: N % 64 == 0, K % 256 == 0");
+  TORCH_CHECK(x2.stride(0) % 8 == 0, "w8_gemm: x row stride must be a multiple of 8");
+  check_aligned16(x2, "x");
+  const int S = splits > 0 ? (int)splits : pda::w8_gemm_splits((int)N, (int)K);
+  TORCH_CHECK(S <= 8 && K % (256 * S) == 0, "w8_gemm: K must split into 4*S slices of 64 (S <= 8)");
+  if (S > 1) {
+    check_f32(ws, "ws");
+    TORCH_CHECK(ws.numel() >= (int64_t)S * M * N && tickets.scalar_type() == at::kInt &&
+                tickets.numel() >= N / pda::w8_gemm_rows(), "w8_gemm: workspace too small");
+  }
+  c10::DeviceGuard g(x.device());
+  auto sizes = x.sizes().vec();
+  sizes.back() = N;
+  Tensor y = at::empty(sizes, x.options());
+  pda::W8GemmParams p{};
+  p.x = bp(x2); p.w = reinterpret_cast<const int8_t*>(w.data_ptr()); p.scale = scale.data_ptr<float>(); p.y = bpm(y);
+  p.ws = S > 1 ? ws.data_ptr<float>() : nullptr;
+  p.tickets = S > 1 ? tickets.data_ptr<int>() : nullptr;
+  p.ldx = x2.stride(0); p.ldy = N;
+  p.M = (int)M; p.N = (int)N; p.K = (int)K; p.S = S;
+  CHECK_HIP_OK(pda::w8_gemm(p, stream_of(x)));
+  return y;
+}
+
 // ------------------------------------------------------------------ embedding / rope
 Tensor embedding_fwd(Tensor idx, Tensor table) {
   check_gpu(idx, "idx");
@@ -1002,6 +1039,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("decode_attn", &decode_attn, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("L"), py::arg("scale"),
         py::arg("splits") = 0, py::arg("pos_dev") = py::none());
   m.def("kv_append", &kv_append);
+  m.def("w8_gemm", &w8_gemm, py::arg("x"), py::arg("w"), py::arg("scale"), py::arg("ws"), py::arg("tickets"),
+        py::arg("splits") = 0);
   m.def("attn_bwd", &attn_bwd);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);

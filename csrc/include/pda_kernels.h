@@ -201,6 +201,21 @@ struct KvAppendParams {
   int B, Hq, Hkv, D;
 };
 hipError_t kv_append_rope(const KvAppendParams& p, hipStream_t st);
+
+// ---- w8_gemm.hip (serving: weight-only int8 GEMM for decode steps, M <= 64)
+struct W8GemmParams {
+  const bf16_t* x;       // [M, K] rows of stride ldx
+  const int8_t* w;       // [N, K] int8, row-major
+  const float* scale;    // [N] per-row dequantisation scale
+  bf16_t* y;             // [M, N] rows of stride ldy
+  float* ws;             // [S, M, N] fp32 partial slabs (S > 1)
+  int* tickets;          // [N / 64] int32, zero between calls (S > 1; reset by the kernel)
+  int64_t ldx, ldy;
+  int M, N, K, S;
+};
+int w8_gemm_splits(int N, int K);
+int w8_gemm_rows();
+hipError_t w8_gemm(const W8GemmParams& p, hipStream_t st);
 int decode_attn_splits(int B, int Hkv, int L, int D);
 hipError_t decode_attention(DecodeAttnParams p, hipStream_t st);
 

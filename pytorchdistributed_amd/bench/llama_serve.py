@@ -26,6 +26,9 @@ def main(argv=None):
     ap.add_argument("--repeat", type=int, default=2)
     ap.add_argument("--layers", type=int, default=None, help="override depth (smoke runs only)")
     ap.add_argument("--graph", action="store_true", help="replay each decode step from one HIP graph")
+    ap.add_argument("--int8", action="store_true", help="weight-only int8 block projections (w8_gemm kernel)")
+    ap.add_argument("--int8-head", action="store_true", help="also quantise the LM head")
+    ap.add_argument("--int8-names", default="w13", help="block projections to quantise with --int8 (w13: the measured win; the split-K shapes wqkv/wo/w2 run slower in int8 today)")
     a = ap.parse_args(argv)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -33,6 +36,11 @@ def main(argv=None):
     over = {} if a.layers is None else {"n_layers": a.layers}
     torch.manual_seed(0)
     model = Llama(config(a.model, **over), device=dev, dtype=torch.bfloat16).eval()
+    if a.int8 or a.int8_head:
+        from ..ops import quantize_linears
+
+        quantize_linears(model, names=a.int8_names.split(",") if a.int8 else (), head=a.int8_head)
+        torch.cuda.empty_cache()
     prompt = torch.randint(0, model.cfg.vocab_size, (a.batch, a.prompt), device=dev)
     cache = KVCache(model, a.batch, a.prompt + a.new)
 
@@ -58,7 +66,8 @@ def main(argv=None):
     steps = a.new - 1
     print(json.dumps({
         "metric": "Llama-3 KV-cached generation (1 GPU)", "model": a.model + ("" if a.layers is None else f"-{a.layers}L"),
-        "batch": a.batch, "decode_graph": a.graph, "prompt": a.prompt, "new_tokens": a.new, "dtype": "bf16",
+        "batch": a.batch, "decode_graph": a.graph, "weights": f"int8 (per-row scale): {a.int8_names}" if a.int8 else "bf16",
+        "int8_head": a.int8_head, "prompt": a.prompt, "new_tokens": a.new, "dtype": "bf16",
         "data": "synthetic prompts, random-init weights", "gemm_table": table,
         "prefill_ms": round(t_pre * 1e3, 2), "prefill_tokens_per_s": round(a.batch * a.prompt / t_pre, 1),
         "decode_ms_per_step": round(t_dec / steps * 1e3, 3),

@@ -53,3 +53,18 @@ def test_kv_cache_sizing_and_placement_map():
     # Llama-3-8B: 128 KiB of bf16 KV cache per token (32 layers x 8 KV heads x 128 x 2)
     big = llama("llama3-8b", device="meta")
     assert KVCache.bytes_per_token(big) == 131072
+
+
+def test_int8_weight_only_quantization_cpu():
+    from pytorchdistributed_amd.ops import quantize_int8, quantize_linears
+
+    w = torch.randn(64, 256)
+    q, s = quantize_int8(w)
+    assert q.dtype == torch.int8 and (q.abs() <= 127).all()
+    assert ((q.float() * s[:, None] - w).abs() <= s[:, None] / 2 + 1e-6).all()
+    m = _tiny("llama")
+    prompt = torch.randint(0, 500, (2, 6), generator=torch.Generator().manual_seed(4))
+    _, ref = generate(m, prompt, 4, return_logits=True)
+    assert quantize_linears(m, head=True) == 2 * 4 + 1
+    _, got = generate(m, prompt, 4, return_logits=True)
+    assert ((got - ref).norm() / ref.norm()).item() < 0.05
