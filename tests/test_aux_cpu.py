@@ -107,3 +107,26 @@ def test_examples_run_on_cpu(tmp_path):
     assert out.returncode == 0
     rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["n_ranks"] == 2 and rec["value"] > 0
+
+
+def test_merge_rank_traces_and_overlap(tmp_path):
+    """tools/merge_traces.py: per-rank rocprofv3 kernel traces -> one Perfetto trace + exposed RCCL time."""
+    import importlib.util
+    import json as _json
+
+    hdr = "Kind,Queue_Id,Kernel_Name,Start_Timestamp,End_Timestamp\n"
+    rows = {0: [("gemm", 0, 100), ("ncclDevKernel_AllReduce", 50, 150), ("bn", 100, 120)],
+            1: [("gemm", 10, 110), ("ncclDevKernel_AllReduce", 200, 260)]}
+    for r, ks in rows.items():
+        d = tmp_path / "prof" / f"rank{r}" / "host"
+        d.mkdir(parents=True)
+        (d / "trace_kernel_trace.csv").write_text(hdr + "".join(f"KERNEL_DISPATCH,1,{n},{s * 10**6},{e * 10**6}\n" for n, s, e in ks))
+    spec = importlib.util.spec_from_file_location("merge_traces", os.path.join(ROOT, "tools", "merge_traces.py"))
+    mt = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mt)
+    out = tmp_path / "merged.json"
+    rep = mt.merge(str(tmp_path / "prof"), str(out))
+    assert rep[0]["comm_exposed_ms"] == 30 and rep[0]["overlap_ratio"] == 0.7
+    assert rep[1]["overlap_ratio"] == 0.0
+    ev = _json.loads(out.read_text())["traceEvents"]
+    assert {e["pid"] for e in ev} == {0, 1} and min(e["ts"] for e in ev if e["ph"] == "X") == 0
