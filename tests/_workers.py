@@ -526,3 +526,37 @@ def tp_llama_gpu_worker(rank, world, outdir):
     with open(os.path.join(outdir, f"ok{rank}"), "w") as fh:
         fh.write("ok")
     pd.destroy_process_group()
+
+
+def ulysses_worker(rank, world, device, outdir):
+    """Ulysses SP attention == full attention on the gathered sequence; gradients of the local shards ==
+    the matching slices of the full-attention gradients (GQA heads, causal)."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.ops.attention import attention_ref
+    from pytorchdistributed_amd.parallel.ulysses import ulysses_attention
+
+    if device == "cuda":
+        torch.cuda.set_device(0)
+    pd.init_process_group("gloo")
+    dt = torch.bfloat16 if device == "cuda" else torch.float32
+    g = torch.Generator().manual_seed(0)
+    B, T, Hq, Hkv, D = 2, 64 * world, 4 * world // 2 * 2, 2 * world // 2 * 2, 64
+    q = torch.randn(B, T, Hq, D, generator=g).to(device, dt)
+    k = torch.randn(B, T, Hkv, D, generator=g).to(device, dt)
+    v = torch.randn(B, T, Hkv, D, generator=g).to(device, dt)
+    go = torch.randn(B, T, Hq, D, generator=g).to(device, dt)
+    full = [t.clone().requires_grad_() for t in (q, k, v)]
+    ref = attention_ref(*full, causal=True)
+    ref.float().mul(go.float()).sum().backward()
+    sl = slice(rank * (T // world), (rank + 1) * (T // world))
+    loc = [t[:, sl].clone().requires_grad_() for t in (q, k, v)]
+    out = ulysses_attention(*loc, causal=True)
+    out.float().mul(go[:, sl].float()).sum().backward()
+    tol = 3e-2 if device == "cuda" else 1e-4
+    assert (out.float() - ref[:, sl].float()).abs().max().item() < tol * 4
+    for a, b in zip(loc, full):
+        err = (a.grad.float() - b.grad[:, sl].float()).abs().max().item()
+        assert err < tol * 8, err
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as fh:
+        fh.write("ok")
+    pd.destroy_process_group()
