@@ -823,7 +823,7 @@ Tensor w8_gemm(Tensor x, Tensor w, Tensor scale, Tensor ws, Tensor tickets, int6
   Tensor x2 = x.reshape({-1, K});
   const int64_t M = x2.size(0);
   TORCH_CHECK(M >= 1 && M <= 64, "w8_gemm: at most 64 rows (decode steps)");
-  TORCH_CHECK(N % pda::w8_gemm_rows() == 0 && K % 256 == 0 && scale.numel() == N, "w8_gemm: N % 64 == 0, K % 256 == 0");
+  TORCH_CHECK(N % pda::w8_gemm_rows() == 0 && K % 256 == 0 && scale.numel() == N, "w8_gemm: N % 16 == 0, K % 256 == 0");
   TORCH_CHECK(x2.stride(0) % 8 == 0, "w8_gemm: x row stride must be a multiple of 8");
   check_aligned16(x2, "x");
   const int S = splits > 0 ? (int)splits : pda::w8_gemm_splits((int)N, (int)K);

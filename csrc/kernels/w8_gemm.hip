@@ -11,12 +11,13 @@
 //  * each lane streams 16 contiguous int8 (one 16-B load) per n-block per 64-k step and uses them for
 //    two MFMAs (k sub-steps 0-7 / 8-15 of its 16-element group; the activation fragment uses the same
 //    permutation, so the dot products are unchanged);
-//  * a wave owns 64 output rows (4 n-blocks), so each activation fragment feeds 8 MFMAs (activation
-//    bytes per weight byte = M/32, read from L2); a workgroup's 4 waves split K and reduce through LDS;
-//  * small-N projections are additionally split over S workgroups (>= one per CU): each writes its
-//    fp32 partial tile to its own slab with plain stores, takes an atomic ticket, and the last one of
-//    the tile sums the S slabs and writes bf16 (tickets reset by it) — ONE launch, graph-capturable.
-//    (v1 used fp32 atomic adds into one buffer: measured 3-10x slower on the wo / w2 shapes.)
+//  * large N: a wave owns 64 output rows (4 n-blocks), so each activation fragment feeds 8 MFMAs
+//    (activation bytes per weight byte = M/32, read from L2); small N (< 256 such tiles): 16-row tiles,
+//    4x the workgroups; in both the workgroup's 4 waves split K and reduce through LDS;
+//  * optional inter-workgroup split-K (S > 1): fp32 partial slabs + an atomic ticket, the last
+//    workgroup of a tile sums them — one launch, graph-capturable, but measured slower than S = 1 on
+//    every Llama shape (publishing a slab across XCDs costs an L2 write-back), so S = 1 by default.
+//    (v1 used fp32 atomic adds into one buffer: 3-10x slower still.)
 #include "pda_common.h"
 #include "pda_kernels.h"
 
@@ -27,8 +28,6 @@ typedef __bf16 mbf16x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kW8Threads = 256;
-constexpr int kNB = 4;                // n-blocks of 16 rows per wave
-constexpr int kW8Rows = 16 * kNB;     // output rows (N) per workgroup
 
 __device__ __forceinline__ mbf16x8 i8_to_bf16x8(uint32_t lo, uint32_t hi) {
   mbf16x8 r;
@@ -40,8 +39,10 @@ __device__ __forceinline__ mbf16x8 i8_to_bf16x8(uint32_t lo, uint32_t hi) {
   return r;
 }
 
-template <int MB>
+// NB = n-blocks of 16 output rows per workgroup (every wave covers the same rows, the 4 waves split K)
+template <int MB, int kNB>
 __global__ void __launch_bounds__(kW8Threads) w8_gemm_kernel(W8GemmParams p) {
+  constexpr int kW8Rows = 16 * kNB;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r16 = lane & 15, kg = lane >> 4;
   const int ntile = blockIdx.x, split = blockIdx.y;
@@ -138,23 +139,32 @@ __global__ void __launch_bounds__(kW8Threads) w8_gemm_kernel(W8GemmParams p) {
 
 }  // namespace
 
-int w8_gemm_rows() { return kW8Rows; }
+int w8_gemm_rows() { return 16; }
 
 int w8_gemm_splits(int N, int K) {
-  // >= one workgroup per CU; the fp32 slabs cost 8·M·S/K of the int8 weight bytes, so stop there
-  const int tiles = N / kW8Rows;
-  int s = 1;
-  while (tiles * s < 256 && s < 8 && K % (64 * 4 * (s * 2)) == 0) s *= 2;
-  return s;
+  // Measured (profiles/r1_w8_gemm_splits.jsonl, M = 32): inter-workgroup split-K loses on every Llama
+  // shape — the agent-scope release that publishes a slab to another XCD writes back L2 — so the
+  // parallelism comes from narrower row tiles (NB = 1 -> N/16 workgroups) instead.
+  (void)N;
+  (void)K;
+  return 1;
+}
+
+template <int NB>
+static hipError_t launch_w8(const W8GemmParams& p, hipStream_t st) {
+  dim3 grid((unsigned)(p.N / (16 * NB)), (unsigned)p.S);
+  if (p.M <= 16) w8_gemm_kernel<1, NB><<<grid, kW8Threads, 0, st>>>(p);
+  else if (p.M <= 32) w8_gemm_kernel<2, NB><<<grid, kW8Threads, 0, st>>>(p);
+  else w8_gemm_kernel<4, NB><<<grid, kW8Threads, 0, st>>>(p);
+  return hipGetLastError();
 }
 
 hipError_t w8_gemm(const W8GemmParams& p, hipStream_t st) {
-  if (p.M < 1 || p.M > 64 || p.N % kW8Rows || p.S < 1 || p.S > 8 || p.K % (64 * 4 * p.S)) return hipErrorInvalidValue;
-  dim3 grid((unsigned)(p.N / kW8Rows), (unsigned)p.S);
-  if (p.M <= 16) w8_gemm_kernel<1><<<grid, kW8Threads, 0, st>>>(p);
-  else if (p.M <= 32) w8_gemm_kernel<2><<<grid, kW8Threads, 0, st>>>(p);
-  else w8_gemm_kernel<4><<<grid, kW8Threads, 0, st>>>(p);
-  return hipGetLastError();
+  if (p.M < 1 || p.M > 64 || p.N % 16 || p.S < 1 || p.S > 8 || p.K % (64 * 4 * p.S)) return hipErrorInvalidValue;
+  // 64-row tiles (activation fragment reused by 8 MFMAs) while they still give >= 256 workgroups;
+  // 16-row tiles otherwise (4x the workgroups; activations re-read from L2 instead)
+  if (p.N % 64 == 0 && (p.N / 64) * p.S >= 256) return launch_w8<4>(p, st);
+  return launch_w8<1>(p, st);
 }
 
 }  // namespace pda

@@ -1,12 +1,11 @@
 """Weight-only int8 for serving (the reference's ``load_in_8bit=True``
 Llama, `03 模型并行/03_model_parallel.ipynb` raw line 86).
 
-Measured on MI355X (`profiles/r1_w8_gemm_microbench_v2.jsonl`, `r1_llama3_8b_serve_int8_v2.jsonl`): the
-kernel streams int8 at 4.2-4.9 TB/s on the large-N shapes (Llama-3-8B w13, LM head: 1.3-1.7x the bf16
-GEMM at M <= 16), but the small-N projections that need inter-workgroup split-K (wqkv, wo, w2) are
-still latency-bound (~25-35 us); quantising w13 + head gives Llama-3-8B decode +10 % (bs 32) / +24 %
-(bs 8) over bf16, quantising everything is slower.  Halving the resident weight bytes also lets
-2x larger models (or KV caches) fit per GPU.
+Measured on MI355X (`profiles/r1_w8_gemm_microbench_v3.jsonl`, `r1_llama3_8b_serve_int8_v2.jsonl`): the
+kernel streams int8 at 3-4.9 TB/s at M <= 16 (1.3-3.7x the bf16 GEMM on wqkv / wo / w13 / LM head;
+w2 at 2.2-2.6 TB/s), falling off at M >= 32 where the activation re-reads from L2 grow.  Llama-3-8B
+decode: bs 8 all-int8 4.29 ms/step vs 5.38 bf16 (+25 %); bs 32 w13 + head int8 5.34 vs 5.89 (+10 %),
+all-int8 5.74.  Halving the resident weight bytes also lets 2x larger models (or KV caches) fit.
 
 Per-output-row symmetric quantisation (``scale = absmax / 127``).  Decode steps (<= 64 token rows) run
 the int8-streaming MFMA kernel `csrc/kernels/w8_gemm.hip` (half the weight bytes of bf16 — the decode
@@ -27,13 +26,14 @@ _WS: Dict[torch.device, list] = {}  # device -> [fp32 split-K slabs, int32 ticke
 
 
 def _workspace(device: torch.device, N: int):
-    """Per-device scratch for w8_gemm: 8 x 64 x N fp32 partial slabs and N/64 tickets.  Grown (never
+    """Per-device scratch for w8_gemm (only used with explicit split-K): 8 x 64 x N fp32 partial slabs
+    and N/16 tickets.  Grown (never
     during HIP-graph capture: the warm-up step allocates it) and shared by every call on the device —
     calls are stream-ordered and each leaves the tickets zeroed."""
     ent = _WS.get(device)
     if ent is None or ent[0].numel() < 8 * 64 * N:
         ent = _WS[device] = [torch.empty(8 * 64 * N, dtype=torch.float32, device=device),
-                             torch.zeros((N + 63) // 64, dtype=torch.int32, device=device)]
+                             torch.zeros((N + 15) // 16, dtype=torch.int32, device=device)]
     return ent
 
 
@@ -49,7 +49,7 @@ def quantize_int8(w: torch.Tensor):
 def w8_linear(x: torch.Tensor, q: torch.Tensor, scale: torch.Tensor, bias: Optional[torch.Tensor] = None):
     N, K = q.shape
     rows = x.numel() // K
-    if (x.is_cuda and x.dtype == torch.bfloat16 and rows <= 64 and N % 64 == 0 and K % 256 == 0
+    if (x.is_cuda and x.dtype == torch.bfloat16 and rows <= 64 and N % 16 == 0 and K % 256 == 0
             and x.stride(-1) == 1):
         ws, tk = _workspace(x.device, N)
         y = C().w8_gemm(x.contiguous(), q, scale, ws, tk)
