@@ -155,6 +155,14 @@ class RowParallelLinear(tnn.Module):
         return y + self.bias if self.bias is not None else y
 
 
+def _local(mod, x):
+    """This rank's part of a TP projection without its collective (serving); int8-quantised projections
+    (``ops.quantize_linears`` replaces the TP layers by ``Int8Linear``) run their own kernel."""
+    if isinstance(mod, (ColumnParallelLinear, RowParallelLinear)):
+        return ops.linear(x, mod.weight, mod.bias if isinstance(mod, ColumnParallelLinear) else None)
+    return mod(x)
+
+
 def _rows(w: torch.Tensor, lo: int, hi: int) -> torch.Tensor:
     return w[lo:hi]
 
@@ -206,12 +214,12 @@ class TPLlamaBlock(tnn.Module):
             h, n = x, self.attention_norm(x)
         else:
             h, n = ops.add_norm(x, res, self.attention_norm.weight, eps=self.attention_norm.eps)
-        qkv = ops.linear(n, self.wqkv.weight).view(B, T, self.hq + 2 * self.hkv, self.hd)
+        qkv = _local(self.wqkv, n).view(B, T, self.hq + 2 * self.hkv, self.hd)
         a = ops.attention_cached(qkv, self.hq, self.hkv, k_cache, v_cache, pos, rope)
-        o = ops.linear(a.reshape(B, T, self.hq * self.hd), self.wo.weight)
+        o = _local(self.wo, a.reshape(B, T, self.hq * self.hd))
         dist.all_reduce(o, group=self.group)
         h, n = ops.add_norm(h, o, self.ffn_norm.weight, eps=self.ffn_norm.eps)
-        y = ops.linear(ops.swiglu(ops.linear(n, self.w13.weight)), self.w2.weight)
+        y = _local(self.w2, ops.swiglu(_local(self.w13, n)))
         dist.all_reduce(y, group=self.group)
         return h, y
 

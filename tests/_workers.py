@@ -491,6 +491,12 @@ def tp_llama_worker(rank, world, sp, outdir):
         t1, l1 = generate(full, prompt, 6, return_logits=True)
         t2, l2 = generate(tpm, prompt, 6, return_logits=True)
         assert torch.equal(t1, t2) and torch.allclose(l1, l2, atol=1e-4, rtol=1e-4)
+        # int8 serving on the TP shards (each rank quantises its own rows): close to the bf16 TP model
+        from pytorchdistributed_amd.ops import quantize_linears
+
+        quantize_linears(tpm)
+        _, l3 = generate(tpm, prompt, 1, return_logits=True)
+        assert ((l3[:, 0] - l2[:, 0]).norm() / l2[:, 0].norm()).item() < 0.05
     with open(os.path.join(outdir, f"ok{rank}"), "w") as fh:
         fh.write("ok")
     pd.destroy_process_group()
