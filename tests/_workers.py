@@ -566,3 +566,70 @@ def ulysses_worker(rank, world, device, outdir):
     with open(os.path.join(outdir, f"ok{rank}"), "w") as fh:
         fh.write("ok")
     pd.destroy_process_group()
+
+
+def moe_ep_worker(rank, world, outdir):
+    """Expert-parallel MoE (gloo, CPU fp32): every rank's outputs == the dense all-experts oracle on its
+    tokens; local expert grads == the full-batch oracle's grads of those experts; summed router grads
+    == the oracle's router grad."""
+    import torch.distributed as dist
+
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.expert_parallel import ExpertParallelMoE, dense_moe_reference
+
+    pd.init_process_group("gloo")
+    E, d, F_, k, N = 8, 32, 48, 2, 24
+    moe = ExpertParallelMoE(d, F_, E, k, dtype=torch.float32, seed=3)
+    g = torch.Generator().manual_seed(3)  # oracle weights: the same unsharded init as the module
+    std = 1.0 / (d ** 0.5)
+    router = (torch.randn(E, d, generator=g) * std).requires_grad_()
+    w13 = (torch.randn(E, 2 * F_, d, generator=g) * std).requires_grad_()
+    w2 = (torch.randn(E, d, F_, generator=g) / (F_ ** 0.5)).requires_grad_()
+    gx = torch.Generator().manual_seed(11)
+    X = torch.randn(world * N, d, generator=gx)
+    G = torch.randn(world * N, d, generator=gx)
+    ref = dense_moe_reference(X, router, w13, w2, k)
+    (ref * G).sum().backward()
+    sl = slice(rank * N, (rank + 1) * N)
+    out = moe(X[sl])
+    assert torch.allclose(out, ref[sl].detach(), atol=1e-5, rtol=1e-4)
+    (out * G[sl]).sum().backward()
+    moe.sync_router_grads()
+    El = E // world
+    assert torch.allclose(moe.w13.grad, w13.grad[rank * El:(rank + 1) * El], atol=1e-5, rtol=1e-4)
+    assert torch.allclose(moe.w2.grad, w2.grad[rank * El:(rank + 1) * El], atol=1e-5, rtol=1e-4)
+    assert torch.allclose(moe.router.grad, router.grad, atol=1e-5, rtol=1e-4)
+    dist.barrier()
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as fh:
+        fh.write("ok")
+    pd.destroy_process_group()
+
+
+def moe_ep_gpu_worker(rank, world, outdir):
+    """EP MoE on the native bf16 kernels, ranks sharing cuda:0 over gloo: outputs close to the oracle."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.expert_parallel import ExpertParallelMoE, dense_moe_reference
+
+    torch.cuda.set_device(0)
+    pd.init_process_group("gloo")
+    E, d, F_, k, N = 8, 256, 512, 2, 64
+    moe = ExpertParallelMoE(d, F_, E, k, device="cuda", dtype=torch.bfloat16, seed=5)
+    g = torch.Generator().manual_seed(5)
+    std = 1.0 / (d ** 0.5)
+    router = torch.randn(E, d, generator=g) * std
+    w13 = torch.randn(E, 2 * F_, d, generator=g) * std
+    w2 = torch.randn(E, d, F_, generator=g) / (F_ ** 0.5)
+    x = torch.randn(N, d, generator=torch.Generator().manual_seed(20 + rank)).cuda().bfloat16()
+    out = moe(x)
+    from pytorchdistributed_amd import ops
+
+    top = torch.topk(ops.linear(x, moe.router).float(), k, dim=-1)  # the module's own (bf16) routing
+    ref = dense_moe_reference(x.cpu().float(), router.bfloat16().float(), w13.bfloat16().float(),
+                              w2.bfloat16().float(), k, top=(top[0].cpu(), top[1].cpu()))
+    rel = ((out.float().cpu() - ref).norm() / ref.norm()).item()
+    assert rel < 3e-2, rel
+    out.float().sum().backward()
+    assert torch.isfinite(moe.w13.grad.float()).all()
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as fh:
+        fh.write("ok")
+    pd.destroy_process_group()
