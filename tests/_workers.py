@@ -534,11 +534,12 @@ def tp_llama_gpu_worker(rank, world, outdir):
     pd.destroy_process_group()
 
 
-def ulysses_worker(rank, world, device, outdir):
-    """Ulysses SP attention == full attention on the gathered sequence; gradients of the local shards ==
-    the matching slices of the full-attention gradients (GQA heads, causal)."""
+def ulysses_worker(rank, world, device, outdir, impl="ulysses"):
+    """Ulysses SP / ring (context-parallel) attention == full attention on the gathered sequence;
+    gradients of the local shards == the matching slices of the full-attention gradients (GQA, causal)."""
     import pytorchdistributed_amd.distributed as pd
     from pytorchdistributed_amd.ops.attention import attention_ref
+    from pytorchdistributed_amd.parallel.ring_attention import ring_attention
     from pytorchdistributed_amd.parallel.ulysses import ulysses_attention
 
     if device == "cuda":
@@ -556,7 +557,7 @@ def ulysses_worker(rank, world, device, outdir):
     ref.float().mul(go.float()).sum().backward()
     sl = slice(rank * (T // world), (rank + 1) * (T // world))
     loc = [t[:, sl].clone().requires_grad_() for t in (q, k, v)]
-    out = ulysses_attention(*loc, causal=True)
+    out = (ulysses_attention if impl == "ulysses" else ring_attention)(*loc, causal=True)
     out.float().mul(go[:, sl].float()).sum().backward()
     tol = 3e-2 if device == "cuda" else 1e-4
     assert (out.float() - ref[:, sl].float()).abs().max().item() < tol * 4
