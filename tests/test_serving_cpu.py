@@ -68,3 +68,38 @@ def test_int8_weight_only_quantization_cpu():
     assert quantize_linears(m, head=True) == 2 * 4 + 1
     _, got = generate(m, prompt, 4, return_logits=True)
     assert ((got - ref).norm() / ref.norm()).item() < 0.05
+
+
+def test_batching_engine_and_http_front_end():
+    import threading
+
+    from fastapi.testclient import TestClient
+
+    from pytorchdistributed_amd.serving import BatchingEngine, create_app
+
+    m = _tiny("llama")
+    eng = BatchingEngine(m, max_batch=8, window_ms=50)
+    try:
+        g = torch.Generator().manual_seed(9)
+        prompts = [torch.randint(0, 500, (6,), generator=g).tolist() for _ in range(5)]
+        futs = [eng.submit(p, 4) for p in prompts]
+        res = [f.result(timeout=60) for f in futs]
+        ref = generate(m, torch.tensor(prompts), 4)[:, 6:].tolist()
+        assert [r["tokens"] for r in res] == ref
+        assert max(r["batch"] for r in res) > 1  # requests were batched together
+        client = TestClient(create_app(eng))
+        out = {}
+
+        def call(i):
+            out[i] = client.post("/generate", json={"prompt": prompts[i], "max_new_tokens": 4}).json()
+
+        ts = [threading.Thread(target=call, args=(i,)) for i in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert [out[i]["tokens"] for i in range(3)] == ref[:3]
+        assert client.get("/health").json()["status"] == "ok"
+        assert client.post("/generate", json={"prompt": []}).status_code == 400
+    finally:
+        eng.close()

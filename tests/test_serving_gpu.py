@@ -152,3 +152,21 @@ def test_int8_llama_generation_close_to_bf16():
     t_e = generate(m, prompt, 8)
     t_g = generate(m, prompt, 8, graph=True)
     assert torch.equal(t_e, t_g)
+
+
+def test_batching_engine_gpu_graph():
+    from pytorchdistributed_amd.serving import BatchingEngine
+
+    torch.manual_seed(0)
+    m = llama("llama3-tiny", device="cuda", dtype=torch.bfloat16).eval()
+    eng = BatchingEngine(m, max_batch=4, window_ms=50)
+    try:
+        prompts = [torch.randint(0, 1000, (12,)).tolist() for _ in range(6)]
+        res = [f.result(timeout=120) for f in [eng.submit(p, 5) for p in prompts]]
+        for i in range(0, 6, 4):  # the engine runs at most 4 per batch: compare against the same batches
+            chunk = prompts[i: i + 4]
+            ref = generate(m, torch.tensor(chunk, device="cuda"), 5)[:, 12:].tolist()
+            assert [r["tokens"] for r in res[i: i + 4]] == ref
+        assert eng.batches_run >= 2
+    finally:
+        eng.close()
