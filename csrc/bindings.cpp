@@ -905,7 +905,7 @@ class XgmiComm {
     c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, device));
     CHECK_HIP_OK(pda::xgmi_alloc(&data_, (size_t)cap_));
     CHECK_HIP_OK(pda::xgmi_alloc(&flags_, flag_bytes()));
-    CHECK_HIP_OK(pda::xgmi_alloc(reinterpret_cast<void**>(&err_), 64));
+    CHECK_HIP_OK(pda::xgmi_alloc_error_word(&err_host_, &err_));
     int rate_khz = 0;
     CHECK_HIP_OK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, device));
     timeout_ticks_ = (long long)(timeout_s * (double)rate_khz * 1000.0);
@@ -925,7 +925,7 @@ class XgmiComm {
       }
     (void)pda::xgmi_free(data_);
     (void)pda::xgmi_free(flags_);
-    (void)pda::xgmi_free(err_);
+    (void)pda::xgmi_free_error_word(err_host_);
   }
   static size_t flag_bytes() { return (size_t)pda::kXgmiPhases * pda::kXgmiMaxBlocks * pda::kXgmiMaxRanks * sizeof(uint32_t); }
   py::bytes handles() {
@@ -976,11 +976,9 @@ class XgmiComm {
     a.algo = algo;
     CHECK_HIP_OK(pda::xgmi_allreduce(a, t.scalar_type() == at::kBFloat16, st));
   }
-  int error() {
-    int e = 0;
-    CHECK_HIP_OK(hipMemcpy(&e, err_, sizeof(int), hipMemcpyDeviceToHost));
-    return e;
-  }
+  // non-blocking: the kernels store the error word into pinned host memory; 0 = no timeout so far
+  int error() const { return __atomic_load_n(err_host_, __ATOMIC_ACQUIRE); }
+  void reset_error() { __atomic_store_n(err_host_, 0, __ATOMIC_RELEASE); }
   int64_t capacity() const { return cap_; }
 
  private:
@@ -989,7 +987,8 @@ class XgmiComm {
   int dev_;
   void* data_ = nullptr;
   void* flags_ = nullptr;
-  int* err_ = nullptr;
+  int* err_ = nullptr;       // device alias of err_host_
+  int* err_host_ = nullptr;  // pinned host-coherent error word
   void* peer_data_[pda::kXgmiMaxRanks];
   uint32_t* peer_flags_[pda::kXgmiMaxRanks];
   uint32_t epoch_ = 0;
@@ -1052,6 +1051,7 @@ PYBIND11_MODULE(_C, m) {
       .def("open", &XgmiComm::open)
       .def("allreduce", &XgmiComm::allreduce, py::arg("t"), py::arg("average") = false, py::arg("algo") = 0)
       .def("error", &XgmiComm::error)
+      .def("reset_error", &XgmiComm::reset_error)
       .def_property_readonly("capacity", &XgmiComm::capacity);
   pda_rt::bind_runtime(m);
 }

@@ -46,6 +46,8 @@ struct XgmiArgs {
 };
 hipError_t xgmi_alloc(void** p, size_t bytes);
 hipError_t xgmi_free(void* p);
+hipError_t xgmi_alloc_error_word(int** host, int** dev);  // pinned, host-coherent, zeroed
+hipError_t xgmi_free_error_word(int* host);
 hipError_t xgmi_get_handle(void* p, char* out64);
 hipError_t xgmi_open_handle(const char* in64, void** p);
 hipError_t xgmi_close_handle(void* p);

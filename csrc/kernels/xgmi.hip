@@ -15,7 +15,9 @@
 // reads it).  Flags and exchange buffers are uncached device memory (hipDeviceMallocUncached), so
 // stores are visible to peers on other GPUs / other XCDs without relying on L2 write-back; the flag
 // stores are release / the spin loads acquire at system scope.  Every spin is bounded by a
-// wall-clock deadline: on timeout the kernel records an error and exits instead of hanging.
+// wall-clock deadline: on timeout the kernel records an error and exits instead of hanging.  The error
+// word is pinned host memory, so callers (DDP) poll it every step without synchronising the device;
+// a communicator that reported a timeout is poisoned (its peers' epochs no longer line up).
 #include "pda_common.h"
 #include "pda_kernels.h"
 
@@ -37,7 +39,10 @@ __device__ __forceinline__ void flag_barrier(const XgmiArgs& a, int phase) {
     const long long t0 = wall_clock64();
     while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
       if (wall_clock64() - t0 > a.timeout_ticks) {
-        atomicExch(a.err, 1 + phase);
+        // err lives in host-coherent pinned memory: the host polls it without a device sync.  Keep
+        // the FIRST phase that timed out (later barriers of the same call time out as a consequence).
+        if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0)
+          __hip_atomic_store(a.err, 1 + phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -113,6 +118,14 @@ hipError_t xgmi_alloc(void** p, size_t bytes) {
 }
 
 hipError_t xgmi_free(void* p) { return hipFree(p); }
+
+hipError_t xgmi_alloc_error_word(int** host, int** dev) {
+  PDA_CHECK_HIP(hipHostMalloc(reinterpret_cast<void**>(host), 64, hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(*host, 0, 64);
+  return hipHostGetDevicePointer(reinterpret_cast<void**>(dev), *host, 0);
+}
+
+hipError_t xgmi_free_error_word(int* host) { return hipHostFree(host); }
 
 hipError_t xgmi_get_handle(void* p, char* out64) {
   hipIpcMemHandle_t h;

@@ -147,7 +147,7 @@ class GPT2(tnn.Module):
         x = ops.embedding(idx, self.wte) + ops.embedding(positions, self.wpe).unsqueeze(0)
         res = None
         for i, blk in enumerate(self.h):
-            dev = blk.c_attn.weight.device
+            dev = blk.ln_1.weight.device  # (c_attn may be an Int8Linear)
             x = x.to(dev, non_blocking=True)
             res = res.to(dev, non_blocking=True) if res is not None else None
             x, res = blk.forward_cached(x, cache.k[i], cache.v[i], pos, res)

@@ -139,14 +139,14 @@ class Llama(tnn.Module):
         dev0 = self.tok_embeddings.device
         x, res = ops.embedding(idx.to(dev0), self.tok_embeddings), None
         for i, blk in enumerate(self.layers):
-            dev = blk.wqkv.weight.device
+            dev = blk.attention_norm.weight.device  # (wqkv may be an Int8Linear)
             x = x.to(dev, non_blocking=True)
             res = res.to(dev, non_blocking=True) if res is not None else None
             rope = self.rope(cache.max_len, dev)
             x, res = blk.forward_cached(x, cache.k[i], cache.v[i], pos, rope, res)
         if last_only:
             x, res = x[:, -1:], res[:, -1:]
-        dev = self.output.weight.device
+        dev = self.norm.weight.device
         _, n = ops.add_norm(x.to(dev, non_blocking=True), res.to(dev, non_blocking=True), self.norm.weight,
                             eps=self.norm.eps)
         return self.output(n)

@@ -79,8 +79,16 @@ class Int8Linear(tnn.Module):
         return cls(q, s, getattr(lin, "bias", None))
 
     @property
-    def weight(self):  # dequantised view for code that reads .weight (device placement, shapes)
-        return self.q
+    def device(self) -> torch.device:
+        return self.q.device
+
+    @property
+    def weight(self) -> torch.Tensor:
+        """The DEQUANTISED weight (``q * scale``, bf16 on a GPU / fp32 on the CPU), computed on every
+        access — for code that genuinely needs the float weight.  Hot paths use ``forward`` or
+        ``q``/``scale``; placement code uses :attr:`device`."""
+        dt = torch.bfloat16 if self.q.is_cuda else torch.float32
+        return self.q.to(dt) * self.scale[:, None].to(dt)
 
     def forward(self, x):
         return w8_linear(x, self.q, self.scale, self.bias)

@@ -119,9 +119,11 @@ class DistributedDataParallel(tnn.Module):
         self.reducer.prepare()
         # ---- optional IPC all-reduce over xGMI for buckets (PDA_ALLREDUCE=ipc|oneshot|twoshot, single node)
         self.xgmi = None
-        if self.world > 1 and self.backend == "nccl" and process_group is None:
+        on_gpu = bool(params) and all(p.is_cuda for p in params)
+        if self.world > 1 and on_gpu and self.backend in ("nccl", "gloo") and process_group is None:
             from . import xgmi as _xgmi
 
+            # gloo only carries the IPC-handle exchange here (multi-rank rehearsal on one GPU)
             if _xgmi.ipc_requested() and _xgmi.single_node():
                 cap = max(b[2] for b in self.bucket_info())
                 self.xgmi = _xgmi.XgmiAllReduce(capacity_mb=cap / 2 ** 20 + 1)
@@ -160,12 +162,15 @@ class DistributedDataParallel(tnn.Module):
             # one-shot IPC all-reduce on a side stream, ordered after the kernels that produced the bucket
             ready = torch.cuda.Event()
             ready.record()
+            ticket = _watchdog.arm(f"ddp xgmi all_reduce bucket {b} ({nbytes / 2**20:.1f} MB, {t.dtype})")
             with torch.cuda.stream(self._ipc_stream), _timing.range(f"ddp.xgmi_all_reduce.b{b}"):
                 self._ipc_stream.wait_event(ready)
                 self.xgmi(t, average=True, algo=self._xgmi_algo)
                 done = torch.cuda.Event()
                 done.record(self._ipc_stream)
-            self._works.append((_EventWork(done), None))
+            work = _EventWork(done)
+            self._works.append((work, None))
+            self._tickets.append((ticket, work))
             return
         ticket = _watchdog.arm(f"ddp all_reduce bucket {b} ({nbytes / 2**20:.1f} MB, {t.dtype})")
         with _timing.range(f"ddp.all_reduce.b{b}"):
@@ -235,8 +240,9 @@ class DistributedDataParallel(tnn.Module):
             ev[1].record()
             self._exposed_events.append(ev)
         self._works.clear()
-        if self.backend != "nccl":
+        if self.backend != "nccl" and self.xgmi is None:
             self._sweep_tickets(force=True)  # gloo waits were blocking: all done
+        self._check_xgmi()
         for g in self.groups.values():
             g.pending_comm = 0
             g.attach_grads()
@@ -255,7 +261,15 @@ class DistributedDataParallel(tnn.Module):
             self._exposed_events = []
         return out
 
+    def _check_xgmi(self):
+        """Fail loudly if an IPC bucket all-reduce of an earlier step hit a peer-barrier timeout (its
+        output is stale); a non-blocking poll of the pinned error word, once per backward and forward."""
+        if self.xgmi is not None and self.xgmi.poll():
+            self._sweep_tickets(force=True)
+            self.xgmi.check(sync=False)
+
     def forward(self, *args, **kwargs):
+        self._check_xgmi()
         if self._tickets:
             self._sweep_tickets()
         if self.broadcast_buffers and self.world > 1 and self.module.training and self._buffer_flats:

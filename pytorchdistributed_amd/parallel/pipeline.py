@@ -231,7 +231,7 @@ class Pipeline:
         self.loss_fn = loss_fn
         self.recompute = recompute
         self.group = group
-        self.device = device or next(stage_module.parameters()).device
+        self.device = device or next(self.module.parameters()).device
         self.prev = self.ranks[self.stage - 1] if self.stage > 0 else None
         self.next = self.ranks[self.stage + 1] if self.stage < self.S - 1 else None
         self._fwd_meta = None  # (shape, dtype) received from prev

@@ -69,11 +69,24 @@ class XgmiAllReduce:
         self.comm.allreduce(t, average, self.pick(t.numel() * t.element_size(), algo))
         return t
 
-    def check(self):
-        """Raise if a barrier of any previous call timed out (synchronises the device)."""
+    def poll(self) -> int:
+        """Non-blocking: 0, or 1 + the phase of a peer barrier that timed out in a call that already
+        ran.  The kernels write the error word into pinned host memory, so no device sync is needed;
+        calls still in flight are covered by a later poll."""
+        return self.comm.error()
+
+    def check(self, sync: bool = True):
+        """Raise if a peer barrier of any previous call timed out.  ``sync=True`` first waits for the
+        device so every issued call is covered; ``sync=False`` is the cheap per-step poll.  The error is
+        reset once reported; the communicator is poisoned after a timeout (peer epochs no longer line
+        up), so callers should fail the step rather than retry."""
+        if sync:
+            torch.cuda.synchronize(self.device)
         e = self.comm.error()
         if e:
-            raise RuntimeError(f"xgmi all-reduce: peer barrier timed out (phase {e - 1}) on rank {self.rank}")
+            self.comm.reset_error()
+            raise RuntimeError(f"xgmi all-reduce: peer barrier timed out (phase {e - 1}) on rank {self.rank}; "
+                               f"results of that call are invalid")
 
 
 def ipc_requested() -> bool:

@@ -38,6 +38,7 @@ class BatchingEngine:
         self.q: "queue.Queue[Tuple[tuple, List[int], Future]]" = queue.Queue()
         self.batches_run = 0
         self._stop = threading.Event()
+        self._lock = threading.Lock()  # submit's closed-check + enqueue vs close()
         self._thread = threading.Thread(target=self._loop, name="pda-serving", daemon=True)
         self._thread.start()
 
@@ -46,15 +47,45 @@ class BatchingEngine:
         if not prompt:
             raise ValueError("empty prompt")
         fut: Future = Future()
-        self.q.put(((len(prompt), int(max_new_tokens), float(temperature), top_k), list(prompt), fut))
+        with self._lock:
+            if self._stop.is_set():
+                raise RuntimeError("engine closed")
+            self.q.put(((len(prompt), int(max_new_tokens), float(temperature), top_k), list(prompt), fut))
         return fut
 
     def close(self):
-        self._stop.set()
+        """Stop the worker; every request not yet served fails with ``RuntimeError('engine closed')``
+        instead of leaving its caller blocked."""
+        with self._lock:
+            self._stop.set()
         self._thread.join(timeout=10)
+        self._fail_queued()
+
+    def _fail_queued(self, pending=()):
+        err = RuntimeError("engine closed")
+        for _, _, fut in pending:
+            if not fut.done():
+                fut.set_exception(err)
+        while True:
+            try:
+                _, _, fut = self.q.get_nowait()
+            except queue.Empty:
+                break
+            if not fut.done():
+                fut.set_exception(err)
 
     def _loop(self):
+        # the current HIP device is per thread: make this worker's match the engine's device, or a
+        # graph captured here would record on device 0's stream while the kernels run on cuda:N
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
         pending: List[Tuple[tuple, List[int], Future]] = []
+        try:
+            self._serve(pending)
+        finally:
+            self._fail_queued(pending)
+
+    def _serve(self, pending):
         while not self._stop.is_set():
             try:
                 pending.append(self.q.get(timeout=0.05))
@@ -70,7 +101,7 @@ class BatchingEngine:
             groups: Dict[tuple, List[Tuple[List[int], Future]]] = {}
             for key, prompt, fut in pending:
                 groups.setdefault(key, []).append((prompt, fut))
-            pending = []
+            pending.clear()
             for (T, new, temp, top_k), reqs in groups.items():
                 for i in range(0, len(reqs), self.max_batch):
                     self._run(reqs[i: i + self.max_batch], new, temp, top_k)
@@ -108,7 +139,12 @@ def create_app(engine: BatchingEngine):
             fut = engine.submit(req.prompt, req.max_new_tokens, req.temperature, req.top_k)
         except ValueError as e:
             raise HTTPException(status_code=400, detail=str(e))
-        return fut.result(timeout=600)
+        except RuntimeError as e:  # engine closed
+            raise HTTPException(status_code=503, detail=str(e))
+        try:
+            return fut.result(timeout=600)
+        except RuntimeError as e:
+            raise HTTPException(status_code=503, detail=str(e))
 
     gen.__annotations__ = {"req": GenerateRequest}
     app.get("/health")(health)

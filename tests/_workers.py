@@ -266,6 +266,75 @@ def xgmi_worker(rank, world, outdir, algos=("oneshot",)):
     pd.destroy_process_group()
 
 
+def xgmi_timeout_worker(rank, world, outdir):
+    """Only rank 0 issues an all-reduce: its peer barrier must time out, the error word must become
+    visible to a non-blocking poll, check() must raise once and then report clean."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.xgmi import XgmiAllReduce
+
+    torch.cuda.set_device(0)
+    pd.init_process_group("gloo")
+    comm = XgmiAllReduce(capacity_mb=1, device=torch.device("cuda", 0), timeout_s=0.5)
+    msg = "no-call"
+    if rank == 0:
+        t = torch.ones(64, device="cuda")
+        comm(t, algo="oneshot")
+        torch.cuda.synchronize()  # the kernel gave up after ~0.5 s instead of hanging
+        assert comm.poll() == 1, comm.poll()  # phase-0 barrier, seen without a device sync
+        try:
+            comm.check(sync=False)
+            msg = "no-raise"
+        except RuntimeError as e:
+            msg = "raised" if "timed out" in str(e) else f"wrong error: {e}"
+        assert comm.poll() == 0  # reported once
+    pd.barrier()
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+        f.write(msg)
+    pd.destroy_process_group()
+
+
+def ddp_xgmi_gpu_worker(rank, world, outdir):
+    """DDP with PDA_ALLREDUCE=ipc (bucket all-reduces on the xGMI IPC kernels), `world` ranks sharing
+    cuda:0 (gloo only exchanges the IPC handles): bucket gradients == mean of the per-rank gradients,
+    over several steps with the per-step error poll and watchdog tickets active."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.models.mlp import MnistMLP
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+    import torch.distributed as dist
+
+    os.environ["PDA_ALLREDUCE"] = "ipc"
+    torch.cuda.set_device(0)
+    pd.init_process_group("gloo")
+    torch.manual_seed(0)
+    base = MnistMLP().to("cuda")
+    model = DistributedDataParallel(base, device_ids=[0], bucket_cap_mb=0.25, first_bucket_mb=0.05)
+    assert model.xgmi is not None, "IPC path not selected"
+    local = MnistMLP().to("cuda")
+    local.load_state_dict(base.state_dict())
+    worst = 0.0
+    for step in range(3):
+        g = torch.Generator().manual_seed(1000 * step + rank)
+        x = torch.randn(16, 784, generator=g).cuda()
+        y = torch.randint(0, 10, (16,), generator=g).cuda()
+        for m in (model, local):
+            for p in m.parameters():
+                p.grad = None
+        F.cross_entropy(model(x), y).backward()
+        F.cross_entropy(local(x), y).backward()
+        for p, q in zip(base.parameters(), local.parameters()):
+            mine = q.grad.float().clone()
+            allg = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(allg, mine)
+            ref = torch.stack(allg).mean(0)
+            worst = max(worst, ((p.grad.float() - ref).norm() / ref.norm().clamp_min(1e-12)).item())
+    model.xgmi.check(sync=True)
+    assert model.reducer.num_buckets > 1
+    assert worst < 1e-5, worst
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+        f.write("ok")
+    pd.destroy_process_group()
+
+
 def ddp_resnet_gpu_worker(rank, world, outdir):
     """DDP ResNet-50 on the native kernels, `world` ranks sharing cuda:0 over gloo (RCCL refuses two
     ranks per GPU): the all-reduced bucket gradients must equal the mean of every rank's local

@@ -68,6 +68,9 @@ def test_int8_weight_only_quantization_cpu():
     assert quantize_linears(m, head=True) == 2 * 4 + 1
     _, got = generate(m, prompt, 4, return_logits=True)
     assert ((got - ref).norm() / ref.norm()).item() < 0.05
+    lin = m.layers[0].wqkv  # .weight is the dequantised float weight, never the raw int8 codes
+    assert lin.weight.dtype == torch.float32 and lin.device == lin.q.device
+    assert torch.equal(lin.weight, lin.q.float() * lin.scale[:, None])
 
 
 def test_batching_engine_and_http_front_end():
@@ -103,3 +106,34 @@ def test_batching_engine_and_http_front_end():
         assert client.post("/generate", json={"prompt": []}).status_code == 400
     finally:
         eng.close()
+
+
+def test_batching_engine_close_fails_pending_and_rejects_new():
+    from concurrent.futures import Future
+
+    from pytorchdistributed_amd.serving import BatchingEngine
+
+    m = _tiny("llama")
+    eng = BatchingEngine(m, max_batch=8, window_ms=5)
+    eng._stop.set()  # worker exits without serving: whatever is queued must fail, not hang
+    eng._thread.join(timeout=10)
+    fut = Future()
+    eng.q.put(((3, 2, 0.0, None), [1, 2, 3], fut))
+    eng.close()
+    with pytest.raises(RuntimeError, match="engine closed"):
+        fut.result(timeout=5)
+    with pytest.raises(RuntimeError, match="engine closed"):
+        eng.submit([1, 2, 3], 2)
+
+
+def test_batching_engine_worker_sets_its_device(monkeypatch):
+    """The current HIP device is per thread: the worker must select the engine's device (cuda:N,
+    N != 0) before it captures decode graphs there."""
+    from pytorchdistributed_amd.serving import BatchingEngine
+
+    seen = []
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: seen.append(torch.device(d)))
+    m = _tiny("llama")
+    eng = BatchingEngine(m, graph=False, device=torch.device("cuda", 3))
+    eng.close()
+    assert seen == [torch.device("cuda", 3)]

@@ -25,3 +25,15 @@ def test_xgmi_twoshot_processes_one_gpu(tmp_path, world):
           nprocs=world, timeout=300)
     for r in range(world):
         assert (tmp_path / f"ok{r}").read_text() == "ok"
+
+
+def test_xgmi_barrier_timeout_is_reported(tmp_path):
+    spawn(_workers.xgmi_timeout_worker, args=(2, str(tmp_path)), nprocs=2, timeout=300)
+    assert (tmp_path / "ok0").read_text() == "raised"
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ddp_buckets_over_xgmi_ipc(tmp_path, world):
+    spawn(_workers.ddp_xgmi_gpu_worker, args=(world, str(tmp_path)), nprocs=world, timeout=300)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}").read_text() == "ok"
