@@ -18,6 +18,8 @@
 #include "pda_common.h"
 #include "pda_kernels.h"
 
+#include <cstdlib>
+
 namespace pda {
 namespace {
 
@@ -290,6 +292,65 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16_t* __rest
   }
 }
 
+// Register-table variant, used when the grid stride is a multiple of C/8 (every ResNet shape: C is a
+// power of two <= 2048 and the stride a multiple of 256 vectors): a lane's 8-channel group never
+// changes, so its scale/shift live in registers — no LDS table, no per-vector 64-bit modulo, no LDS
+// bank conflicts (the LDS variant's lanes read coefficients 32 B apart: 8-way conflicts) — and four
+// vectors (4-8 loads) are kept in flight per lane.
+template <bool RES, bool RELU>
+__device__ __forceinline__ void bn_apply_reg(const float (&xv)[8], const float (&rv)[8], const float (&sc)[8],
+                                             const float (&sh)[8], bf16_t* __restrict__ y,
+                                             uint8_t* __restrict__ bits, int64_t v) {
+  float a[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = fmaf(xv[j], sc[j], sh[j]) + (RES ? rv[j] : 0.f);
+  if (RELU) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      m |= (a[j] > 0.f ? 1u : 0u) << j;
+      a[j] = fmaxf(a[j], 0.f);
+    }
+    if (bits) bits[v] = (uint8_t)m;
+  }
+  store8(y + v * 8, a);
+}
+
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(kThreads) bn_apply_reg_kernel(const bf16_t* __restrict__ x,
+                                                                const bf16_t* __restrict__ res,
+                                                                bf16_t* __restrict__ y, int64_t M, int C,
+                                                                const float* __restrict__ scale,
+                                                                const float* __restrict__ shift,
+                                                                uint8_t* __restrict__ bits) {
+  const int cv = C / 8;
+  const int64_t nvec = M * cv;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(v % cv) * 8;  // fixed for this lane (stride % cv == 0)
+  float sc[8], sh[8];
+  load8(scale + c0, sc);
+  load8(shift + c0, sh);
+  constexpr int U = 4;
+  for (; v + (U - 1) * stride < nvec; v += U * stride) {
+    float a[U][8], r[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load8(x + (v + u * stride) * 8, a[u]);
+    if (RES) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) load8(res + (v + u * stride) * 8, r[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) bn_apply_reg<RES, RELU>(a[u], r[u], sc, sh, y, bits, v + u * stride);
+  }
+  for (; v < nvec; v += stride) {
+    float a0[8], r0[8];
+    load8(x + v * 8, a0);
+    if (RES) load8(res + v * 8, r0);
+    bn_apply_reg<RES, RELU>(a0, r0, sc, sh, y, bits, v);
+  }
+}
+
 // ---------------------------------------------------------------- backward reduction
 // MASK: 0 no ReLU; 1 ReLU mask from the saved output y; 2 ReLU mask recomputed from x and the
 // forward's per-channel scale/shift (BN+ReLU without residual: y is never saved or re-read);
@@ -455,9 +516,88 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16_t* __
   }
 }
 
+// Register-coefficient variant of the backward apply (same condition as bn_apply_reg_kernel): the
+// lane's A, B, Cc (and MASK-2 scale/shift) for its fixed 8 channels are loaded once into registers.
+template <int MASK, bool DRES>
+__global__ void __launch_bounds__(kThreads) bn_bwd_apply_reg_kernel(const bf16_t* __restrict__ dy,
+                                                                    const bf16_t* __restrict__ x,
+                                                                    const bf16_t* __restrict__ y,
+                                                                    const float* __restrict__ ss, int64_t M, int C,
+                                                                    const float* __restrict__ coef,
+                                                                    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres) {
+  const int cv = C / 8;
+  const int64_t nvec = M * cv;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c0 = (int)(v % cv) * 8;
+  float cA[8], cB[8], cC[8], sc[8], sh[8];
+  load8(coef + c0, cA);
+  load8(coef + C + c0, cB);
+  load8(coef + 2 * C + c0, cC);
+  if constexpr (MASK == 2) {
+    load8(ss + c0, sc);
+    load8(ss + C + c0, sh);
+  }
+  auto one = [&](float (&g)[8], float (&xv)[8], uint32_t mb, int64_t vv) {
+    if constexpr (MASK == 3) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
+    } else if constexpr (MASK == 2) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
+    } else if constexpr (MASK == 1) {
+      const u16x8 yr = *reinterpret_cast<const u16x8*>(y + vv * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = bf2f(yr[j]) > 0.f ? g[j] : 0.f;
+    }
+    if (DRES) store8(dres + vv * 8, g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = fmaf(cA[j], g[j], fmaf(cB[j], xv[j], cC[j]));
+    store8(dx + vv * 8, xv);
+  };
+  constexpr int U = 3;
+  for (; v + (U - 1) * stride < nvec; v += U * stride) {  // 3 vectors x (dy, x, mask) in flight per lane
+    float g[U][8], xv[U][8];
+    uint32_t mb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      load8(dy + (v + u * stride) * 8, g[u]);
+      load8(x + (v + u * stride) * 8, xv[u]);
+      mb[u] = MASK == 3 ? reinterpret_cast<const uint8_t*>(y)[v + u * stride] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(g[u], xv[u], mb[u], v + u * stride);
+  }
+  for (; v < nvec; v += stride) {
+    float g[8], xv[8];
+    load8(dy + v * 8, g);
+    load8(x + v * 8, xv);
+    one(g, xv, MASK == 3 ? reinterpret_cast<const uint8_t*>(y)[v] : 0u, v);
+  }
+}
+
+// A/B switch read once per process (PDA_BN_LDS_TABLES=1 forces the LDS-table kernels)
+inline bool lds_tables_forced() {
+  static const bool v = [] {
+    const char* e = getenv("PDA_BN_LDS_TABLES");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+// the grid-stride loop keeps each lane on one channel group when the stride is a multiple of C/8
+inline bool reg_tables(int grid, int C) { return ((int64_t)grid * kThreads) % (C / 8) == 0; }
+
 hipError_t launch_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int C, const float* scale,
                         const float* shift, bool relu, uint8_t* bits, hipStream_t st) {
   const int grid = ew_grid(M * C / 8);
+  if (reg_tables(grid, C) && !lds_tables_forced()) {
+    if (res && relu) bn_apply_reg_kernel<true, true><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits);
+    else if (res) bn_apply_reg_kernel<true, false><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr);
+    else if (relu) bn_apply_reg_kernel<false, true><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits);
+    else bn_apply_reg_kernel<false, false><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr);
+    return hipGetLastError();
+  }
   const size_t lds = 2 * (size_t)C * sizeof(float);
   if (res && relu) bn_apply_kernel<true, true><<<grid, kThreads, lds, st>>>(x, res, y, M, C, scale, shift, bits);
   else if (res) bn_apply_kernel<true, false><<<grid, kThreads, lds, st>>>(x, res, y, M, C, scale, shift, nullptr);
@@ -546,9 +686,13 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint
                                                                          dgamma_b, dbeta_f, dbeta_b, coef);
   PDA_CHECK_HIP(hipGetLastError());
   const int grid = ew_grid(M * C / 8);
-  const size_t lds = 5 * (size_t)C * sizeof(float);
-#define BWD_APPLY(MK, DR) \
-  bn_bwd_apply_kernel<MK, DR><<<grid, kThreads, lds, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres)
+  const bool reg = reg_tables(grid, (int)C) && !lds_tables_forced();
+  const size_t lds = reg ? 0 : 5 * (size_t)C * sizeof(float);
+#define BWD_APPLY(MK, DR)                                                                             \
+  do {                                                                                                \
+    if (reg) bn_bwd_apply_reg_kernel<MK, DR><<<grid, kThreads, 0, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres); \
+    else bn_bwd_apply_kernel<MK, DR><<<grid, kThreads, lds, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres); \
+  } while (0)
   if (mask == 0) { if (dres) BWD_APPLY(0, true); else BWD_APPLY(0, false); }
   else if (mask == 1) { if (dres) BWD_APPLY(1, true); else BWD_APPLY(1, false); }
   else if (mask == 2) { if (dres) BWD_APPLY(2, true); else BWD_APPLY(2, false); }
