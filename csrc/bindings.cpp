@@ -474,8 +474,11 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   const int R = w.size(1), S = w.size(2), C = w.size(3);
   TORCH_CHECK(w.size(0) == Cout && C % 8 == 0 && Cout % 8 == 0);
   c10::DeviceGuard g(dy.device());
-  Tensor wt = at::empty({C, R, S, Cout}, w.options());
-  CHECK_HIP_OK(pda::conv_weight_transpose(bp(w), bpm(wt), Cout, R, S, C, stride, pad, dil, stream_of(dy)));
+  Tensor wt;
+  if (pda::conv_dgrad_needs_wt(R, S, (int)stride, (int)pad)) {
+    wt = at::empty({C, R, S, Cout}, w.options());
+    CHECK_HIP_OK(pda::conv_weight_transpose(bp(w), bpm(wt), Cout, R, S, C, stride, pad, dil, stream_of(dy)));
+  }
   Tensor dx = at::empty({N, H, W, C}, dy.options());
   if (addend.has_value()) {
     check_bf16(*addend, "addend");
@@ -488,7 +491,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
                     addend_bits->numel() * 8 == dx.numel(),
                 "addend_bits must be numel/8 contiguous bytes");
   }
-  CHECK_HIP_OK(pda::conv2d_dgrad(bp(dy), bp(wt), bpm(dx), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
+  CHECK_HIP_OK(pda::conv2d_dgrad(bp(dy), bp(w), wt.defined() ? bp(wt) : nullptr, bpm(dx), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
                                  addend.has_value() ? bp(*addend) : nullptr,
                                  addend_bits.has_value() ? addend_bits->data_ptr<uint8_t>() : nullptr, stream_of(dy)));
   return dx;

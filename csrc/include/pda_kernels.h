@@ -139,8 +139,11 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H,
                       float* stats, const float* stats_shift, int stats_rows, hipStream_t st);
 // addend (optional, bf16, dx's layout): dx = dgrad + addend, fused into the store; addend_bits (optional,
 // [numel/8] bytes, bit j of byte v for element 8v + j): only the addend elements whose bit is set
-hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* wt, bf16_t* dx, int N, int H, int W, int C, int Cout, int R,
-                        int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,
+// wt: the weight transposed by conv_weight_transpose — except for a 1x1 stride-1 unpadded conv
+// (conv_dgrad_needs_wt() false), whose dgrad is a plain GEMM that reads w [Cout][C] MN-major in place.
+bool conv_dgrad_needs_wt(int R, int S, int stride, int pad);
+hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf16_t* dx, int N, int H, int W, int C,
+                        int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,
                         const uint8_t* addend_bits, hipStream_t st);
 hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32, int N, int H, int W, int C,
                         int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, float* slab,

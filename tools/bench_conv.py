@@ -14,7 +14,8 @@ import sys
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# PDA_AB_ROOT: import another build of the package (tools/ab_build.sh) for an A/B on the same box
+sys.path.insert(0, os.environ.get("PDA_AB_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pytorchdistributed_amd._native import C  # noqa: E402
 
 # (H, Cin, Cout, R, stride) for every distinct ResNet-50 conv (input spatial size H)
