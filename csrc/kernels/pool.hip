@@ -102,6 +102,65 @@ __global__ void __launch_bounds__(kThreads) maxpool_bwd_kernel(const bf16_t* __r
   }
 }
 
+// 3x3 / stride 2 / pad 1 (the ResNet stem pool): one thread per 2x2 input block (2p..2p+1, 2q..2q+1)
+// and 8 channels.  Exactly the outputs (p..p+1, q..q+1) cover the block, so each dy / argmax vector
+// is read once per block instead of once per covering input pixel (4x fewer L2 reads than the
+// generic gather above), and all index math is 32-bit (no 64-bit div/mod per vector).
+//   dx(2p,   2q)   = [i(p,q)=4] g(p,q)
+//   dx(2p,   2q+1) = [i(p,q)=5] g(p,q)   + [i(p,q+1)=3] g(p,q+1)
+//   dx(2p+1, 2q)   = [i(p,q)=7] g(p,q)   + [i(p+1,q)=1] g(p+1,q)
+//   dx(2p+1, 2q+1) = [i(p,q)=8] g(p,q) + [i(p,q+1)=6] g(p,q+1) + [i(p+1,q)=2] g(p+1,q) + [i(p+1,q+1)=0] g(p+1,q+1)
+__global__ void __launch_bounds__(kThreads) maxpool3s2_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                                  const uint8_t* __restrict__ idx,
+                                                                  bf16_t* __restrict__ dx, int N, int H, int W, int C,
+                                                                  int P, int Q) {
+  const int cv = C >> 3;
+  const int Hb = (H + 1) >> 1, Wb = (W + 1) >> 1;
+  const int total = N * Hb * Wb * cv;
+  const int stride = gridDim.x * blockDim.x;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int c8 = t % cv;
+    int pix = t / cv;
+    const int q = pix % Wb;
+    pix /= Wb;
+    const int p = pix % Hb;
+    const int n = pix / Hb;
+    float g[4][8];
+    uint64_t id[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int pp = p + (o >> 1), qq = q + (o & 1);
+      if (pp < P && qq < Q) {
+        const int64_t off = (((int64_t)n * P + pp) * Q + qq) * C + c8 * 8;
+        id[o] = *reinterpret_cast<const uint64_t*>(idx + off);
+        load8(dy + off, g[o]);
+      } else {
+        id[o] = ~0ull;  // no tap matches 0xFF
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[o][j] = 0.f;
+      }
+    }
+    float d00[8], d01[8], d10[8], d11[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i0 = (uint32_t)(id[0] >> (8 * j)) & 0xFF, i1 = (uint32_t)(id[1] >> (8 * j)) & 0xFF;
+      const uint32_t i2 = (uint32_t)(id[2] >> (8 * j)) & 0xFF, i3 = (uint32_t)(id[3] >> (8 * j)) & 0xFF;
+      d00[j] = i0 == 4 ? g[0][j] : 0.f;
+      d01[j] = (i0 == 5 ? g[0][j] : 0.f) + (i1 == 3 ? g[1][j] : 0.f);
+      d10[j] = (i0 == 7 ? g[0][j] : 0.f) + (i2 == 1 ? g[2][j] : 0.f);
+      d11[j] = ((i0 == 8 ? g[0][j] : 0.f) + (i1 == 6 ? g[1][j] : 0.f)) + ((i2 == 2 ? g[2][j] : 0.f) + (i3 == 0 ? g[3][j] : 0.f));
+    }
+    const int h = 2 * p, w = 2 * q;
+    bf16_t* base = dx + (((int64_t)n * H + h) * W + w) * C + c8 * 8;
+    store8(base, d00);
+    if (w + 1 < W) store8(base + C, d01);
+    if (h + 1 < H) {
+      store8(base + (int64_t)W * C, d10);
+      if (w + 1 < W) store8(base + (int64_t)W * C + C, d11);
+    }
+  }
+}
+
 // Global average pool: x [N, HW, C] -> y [N, C]
 template <typename O>
 __global__ void __launch_bounds__(kThreads) avgpool_fwd_kernel(const bf16_t* __restrict__ x, O* __restrict__ y, int N,
@@ -155,6 +214,11 @@ hipError_t maxpool2d_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H,
 
 hipError_t maxpool2d_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C, int P, int Q,
                          int k, int s, int pad, hipStream_t st) {
+  const int64_t blocks = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+  if (k == 3 && s == 2 && pad == 1 && P == (H - 1) / 2 + 1 && Q == (W - 1) / 2 + 1 && blocks < (1ll << 31) - 2048 * 256) {
+    maxpool3s2_bwd_kernel<<<ew_grid(blocks), kThreads, 0, st>>>(dy, idx, dx, N, H, W, C, P, Q);
+    return hipGetLastError();
+  }
   const int64_t total = (int64_t)N * H * W * (C / 8);
   maxpool_bwd_kernel<<<ew_grid(total), kThreads, 0, st>>>(dy, idx, dx, N, H, W, C, P, Q, k, s, pad);
   return hipGetLastError();

@@ -12,6 +12,7 @@ import torch.nn.functional as F
 
 from .._native import C
 from ..parallel.flat import grad_target
+from . import streams as _streams
 from .grad_join import MaskedGrad
 
 
@@ -55,8 +56,17 @@ class _Conv2dFn(torch.autograd.Function):
                     addend, bits = addend.grad, addend.bits
                 dx = C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation, addend, bits)
         if ctx.needs_input_grad[1]:
-            dw = C().conv_wgrad(dy, x, w.shape[1], w.shape[2], stride, padding, dilation, w.dtype == torch.float32,
-                                grad_target(ctx.wparam))
+            target = grad_target(ctx.wparam)
+            args = (dy, x, w.shape[1], w.shape[2], stride, padding, dilation, w.dtype == torch.float32, target)
+            # Off the critical path: the wgrad overlaps the BN backward / dgrad of the layers below it.
+            # Only when the kernel writes the parameter's final gradient storage (a flat-buffer slot that
+            # AccumulateGrad adopts without a kernel); a freshly allocated dw would be read on the main
+            # stream by AccumulateGrad's accumulate / clone, which knows nothing of the side stream.
+            if target is not None and _streams.enabled():
+                with _streams.wgrad_stream(dy.device, dy, x):
+                    dw = C().conv_wgrad(*args)
+            else:
+                dw = C().conv_wgrad(*args)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.reshape(-1, dy.shape[-1]).sum(0, dtype=torch.float32).to(dy.dtype)
         return dx, dw, db, None, None, None, None, None

@@ -1,0 +1,95 @@
+"""Side-stream weight gradients (MI355X: overlap compute-bound wgrad GEMMs with the memory-bound
+BatchNorm backward and the next layer's data gradient).
+
+In a conv/linear backward the data gradient (dx) is on the critical path — the next layer's
+backward needs it — while the weight gradient (dw) only feeds the gradient all-reduce and the
+optimizer.  With ``PDA_WGRAD_STREAM=1`` (default on a GPU) the dw GEMM of each layer is launched on
+a per-device side stream, ordered after the producing kernels by an event, so it runs concurrently
+with the main stream's dgrad, BatchNorm backward reductions and applies of the layers below it:
+the BN kernels stream HBM at 4-5 TB/s with the MFMA pipes idle, the wide wgrad tiles are MFMA-bound,
+and the GPU's dispatcher fills CUs from both queues (also the CUs a wgrad launch's last, partial
+round of tiles leaves idle: ResNet-50's M = 256*49*k rows quantise to 0.77 of 256 CUs).
+
+Stream safety:
+* every tensor read on the side stream is ``record_stream``-ed, so the caching allocator does not
+  hand its memory to a main-stream allocation while the side kernel still reads it;
+* the first side launch of a backward pass queues an autograd final callback that makes the main
+  stream wait for the side stream, so anything after ``backward()`` (optimizer, grad clipping,
+  checkpointing, HIP-graph capture end) sees finished gradients;
+* :func:`producer_streams` lets a gradient all-reduce (DDP buckets) wait for the side stream as
+  well as the main stream before it reads a bucket.
+"""
+from __future__ import annotations
+
+import contextlib
+import os
+from typing import Dict, List
+
+import torch
+
+_streams: Dict[int, torch.cuda.Stream] = {}
+_join_pending: Dict[int, bool] = {}
+_enabled_override = None
+
+
+def enabled() -> bool:
+    if _enabled_override is not None:
+        return _enabled_override
+    return os.environ.get("PDA_WGRAD_STREAM", "1") == "1"
+
+
+def set_enabled(flag) -> None:
+    """Force side-stream weight gradients on/off (None: back to ``PDA_WGRAD_STREAM``)."""
+    global _enabled_override
+    _enabled_override = flag
+
+
+def side_stream(device: torch.device) -> torch.cuda.Stream:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _streams.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _streams[idx] = s
+    return s
+
+
+def _join(idx: int) -> None:
+    _join_pending[idx] = False
+    s = _streams.get(idx)
+    if s is not None:
+        torch.cuda.current_stream(idx).wait_stream(s)
+
+
+def active(device: torch.device) -> bool:
+    """True while a backward pass has side-stream work on ``device`` not yet joined."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return _join_pending.get(idx, False)
+
+
+@contextlib.contextmanager
+def wgrad_stream(device: torch.device, *tensors: torch.Tensor):
+    """Run the body on the device's side stream, after everything queued so far on the current
+    stream; ``tensors`` (inputs the body reads) are protected from reuse until the side stream is
+    done with them.  Must be entered inside an autograd backward pass (it queues the join)."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    main = torch.cuda.current_stream(idx)
+    s = side_stream(device)
+    s.wait_stream(main)
+    for t in tensors:
+        if t is not None:
+            t.record_stream(s)
+    if not _join_pending.get(idx, False):
+        _join_pending[idx] = True
+        torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(idx))
+    with torch.cuda.stream(s):
+        yield s
+
+
+def producer_streams(device: torch.device) -> List[torch.cuda.Stream]:
+    """Streams whose queued work may still be writing gradients on ``device``: the current stream
+    and, during a backward pass with side-stream weight gradients, the side stream."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    out = [torch.cuda.current_stream(idx)]
+    if _join_pending.get(idx, False) and idx in _streams:
+        out.append(_streams[idx])
+    return out

@@ -32,6 +32,7 @@ import torch.nn as tnn
 
 from .. import _native
 from .. import distributed as pdist
+from ..ops import streams as _streams
 from ..utils import timing as _timing
 from ..utils import watchdog as _watchdog
 from .flat import FlatGroup, flatten_buffers
@@ -158,13 +159,15 @@ class DistributedDataParallel(tnn.Module):
             with _watchdog.watch(f"ddp host-ring all_reduce bucket {b} ({nbytes / 2**20:.1f} MB)"):
                 pdist.ring_all_reduce(t, average=True)
             return
+        # the bucket's gradients may still be in flight on the side (weight-gradient) stream as well as
+        # on the current stream (ops/streams.py): the collective is ordered after both
+        producers = _streams.producer_streams(t.device) if t.is_cuda else []
         if self.xgmi is not None and self.xgmi.fits(t):
             # one-shot IPC all-reduce on a side stream, ordered after the kernels that produced the bucket
-            ready = torch.cuda.Event()
-            ready.record()
             ticket = _watchdog.arm(f"ddp xgmi all_reduce bucket {b} ({nbytes / 2**20:.1f} MB, {t.dtype})")
             with torch.cuda.stream(self._ipc_stream), _timing.range(f"ddp.xgmi_all_reduce.b{b}"):
-                self._ipc_stream.wait_event(ready)
+                for s in producers:
+                    self._ipc_stream.wait_stream(s)
                 self.xgmi(t, average=True, algo=self._xgmi_algo)
                 done = torch.cuda.Event()
                 done.record(self._ipc_stream)
@@ -175,9 +178,19 @@ class DistributedDataParallel(tnn.Module):
         ticket = _watchdog.arm(f"ddp all_reduce bucket {b} ({nbytes / 2**20:.1f} MB, {t.dtype})")
         with _timing.range(f"ddp.all_reduce.b{b}"):
             if self.backend == "nccl":
-                work = dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
+                # RCCL orders its stream after the CURRENT stream: make that the side stream, itself
+                # ordered after the main stream, when weight gradients are still being produced there
+                side = producers[1] if len(producers) > 1 else None
+                ctx = contextlib.nullcontext()
+                if side is not None:
+                    side.wait_stream(producers[0])
+                    ctx = torch.cuda.stream(side)
+                with ctx:
+                    work = dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.process_group, async_op=True)
                 self._works.append((work, None))
             else:
+                if len(producers) > 1:  # gloo reads the tensor after the current stream only
+                    producers[0].wait_stream(producers[1])
                 work = dist.all_reduce(t, group=self.process_group, async_op=True)
                 self._works.append((work, t))
         self._tickets.append((ticket, work))

@@ -282,15 +282,18 @@ def test_batchnorm_eval():
 
 
 # ----------------------------------------------------------------------------- pooling
-def test_maxpool_fwd_bwd():
+@pytest.mark.parametrize("H,W,k,s,p", [(17, 16, 3, 2, 1), (16, 17, 3, 2, 1), (56, 56, 3, 2, 1), (7, 7, 3, 2, 1),
+                                      (1, 2, 3, 2, 1), (12, 13, 2, 2, 0), (9, 9, 3, 1, 1)])
+def test_maxpool_fwd_bwd(H, W, k, s, p):
+    """3x3/2/1 backward runs the 2x2-block gather kernel, the others the generic gather."""
     torch.manual_seed(3)
-    x = torch.randn(2, 17, 16, 64).to(torch.bfloat16).float().requires_grad_()
-    y = F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    x = torch.randn(2, H, W, 64).to(torch.bfloat16).float().requires_grad_()
+    y = F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1)
     dy = torch.randn_like(y).to(torch.bfloat16).float()
     y.backward(dy)
-    yg, idx = C().maxpool_fwd(bf(x.detach()), 3, 2, 1)
+    yg, idx = C().maxpool_fwd(bf(x.detach()), k, s, p)
     assert torch.equal(yg.cpu().float(), y.detach())
-    dx = C().maxpool_bwd(bf(dy), idx, 17, 16, 3, 2, 1)
+    dx = C().maxpool_bwd(bf(dy), idx, H, W, k, s, p)
     assert rel_err(dx.cpu(), x.grad) < 1e-2
 
 

@@ -154,3 +154,41 @@ def test_fsdp_llama_tiny_matches_unsharded(tmp_path, world):
     spawn(_workers.fsdp_llama_gpu_worker, args=(world, str(tmp_path)), nprocs=world, timeout=300)
     for r in range(world):
         assert (tmp_path / f"ok{r}").read_text().startswith("ok")
+
+
+def test_side_stream_wgrad_matches_single_stream():
+    """Weight gradients on the side stream (ops/streams.py) must match the single-stream path: two
+    DDP(world 1) + fused-SGD steps of ResNet-50 from the same init, grads written straight into the
+    flat bucket buffer by wgrad kernels running concurrently with the BN backward; every parameter's
+    step-2 gradient is compared (a missed dependency shows as an O(1) error on some layer; BN batch
+    statistics are summed with float atomics, so the two runs agree to rounding, not bitwise)."""
+    from pytorchdistributed_amd.data.device import DeviceSyntheticImages
+    from pytorchdistributed_amd.models.resnet import resnet50
+    from pytorchdistributed_amd.ops import cross_entropy, streams
+    from pytorchdistributed_amd.optim import SGD
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+
+    def run(side):
+        streams.set_enabled(side)
+        try:
+            torch.manual_seed(0)
+            model = DistributedDataParallel(resnet50(device="cuda", dtype=torch.bfloat16), device_ids=[0])
+            opt = SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-5)
+            data = DeviceSyntheticImages(16, 96, 1000, device=torch.device("cuda", 0), dtype=torch.bfloat16, seed=3)
+            for _ in range(2):
+                x, y = data.next()
+                opt.zero_grad(set_to_none=True)
+                loss = cross_entropy(model(x), y)
+                loss.backward()
+                grads = {n: p.grad.detach().float().clone() for n, p in model.module.named_parameters()}
+                opt.step()
+            torch.cuda.synchronize()
+            return loss.item(), grads
+        finally:
+            streams.set_enabled(None)
+
+    l0, g0 = run(False)
+    l1, g1 = run(True)
+    assert abs(l0 - l1) <= 1e-2 * abs(l0), (l0, l1)
+    worst = max((rel_err(g1[n], g0[n]), n) for n in g0)
+    assert worst[0] < 3e-2, worst
