@@ -20,12 +20,14 @@ import torch.nn.functional as F
 
 from .._native import C
 from ..parallel.flat import grad_target
+from . import streams as _streams
 
 
 def _mfma_ok(x2, w):
     return (x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0)
 
 
+_SIDE_MAX_NUMEL = 256 * 256 * 256  # 256 CUs x one 256x256 tile
 _BLAS_MIN_WORK = 1 << 27  # M*N*K below this: launch-latency bound, the native kernel is as good
 
 
@@ -112,7 +114,17 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _gemm_dgrad(dy2, w).reshape(ctx.shape)
         if ctx.needs_input_grad[1]:
-            dw = _gemm_wgrad(dy2, x2, w.dtype, grad_target(ctx.wparam))
+            target = grad_target(ctx.wparam)
+            if target is not None and _streams.enabled() and target.numel() < _SIDE_MAX_NUMEL:
+                # written straight into the flat gradient slot: run it beside the critical path
+                # (ops/streams.py; same contract as the conv weight gradient).  A dW with a full wave
+                # of 256x256 output tiles per CU fills the chip by itself; beside other work it only
+                # adds interference (Llama-3-8B FSDP: -2.4 %; GPT-2-medium DDP, 1-16 tiles + split-K:
+                # +9.9 %, profiles/r2_wgrad_stream_transformers.jsonl)
+                with _streams.wgrad_stream(dy2.device, dy2, x2):
+                    dw = _gemm_wgrad(dy2, x2, w.dtype, target)
+            else:
+                dw = _gemm_wgrad(dy2, x2, w.dtype, target)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             tb = grad_target(ctx.bparam)
             db = C().colsum(dy2)

@@ -30,6 +30,7 @@ Checkpoints: :meth:`full_state_dict` (rank-0 consolidated, original names) and
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -39,6 +40,7 @@ import torch.distributed as dist
 import torch.nn as tnn
 
 from .. import distributed as pdist
+from ..ops import streams as _streams
 
 ALIGN = 8
 
@@ -281,11 +283,23 @@ class FullyShardedDataParallel(tnn.Module):
             out, work = grad_full, None
         else:
             out = torch.empty(u.shard_numel, dtype=grad_full.dtype, device=grad_full.device)
-            if self.nccl:
-                work = dist.reduce_scatter_tensor(out, grad_full, op=dist.ReduceOp.AVG, group=self.group,
-                                                  async_op=True)
-            else:
-                work = dist.reduce_scatter_tensor(out, grad_full, group=self.group, async_op=True)
+            # weight gradients of this unit may still be running on the side stream (ops/streams.py):
+            # order the collective after both streams (RCCL waits on the current stream)
+            producers = _streams.producer_streams(grad_full.device) if grad_full.is_cuda else []
+            ctx = contextlib.nullcontext()
+            if len(producers) > 1:
+                if self.nccl:
+                    producers[1].wait_stream(producers[0])
+                    ctx = torch.cuda.stream(producers[1])
+                    out.record_stream(producers[1])
+                else:
+                    producers[0].wait_stream(producers[1])
+            with ctx:
+                if self.nccl:
+                    work = dist.reduce_scatter_tensor(out, grad_full, op=dist.ReduceOp.AVG, group=self.group,
+                                                      async_op=True)
+                else:
+                    work = dist.reduce_scatter_tensor(out, grad_full, group=self.group, async_op=True)
         self._pending_rs = (u, work, out)
         if u is not self.root_unit:
             u.reshard()
