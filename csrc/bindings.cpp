@@ -955,7 +955,8 @@ class XgmiComm {
   // in-place all-reduce of a contiguous fp32 / bf16 tensor on this communicator's device
   void allreduce(Tensor t, bool average, int algo) {
     TORCH_CHECK(opened_ || world_ == 1, "xgmi: open() the peer handles first");
-    TORCH_CHECK(algo == 0 || algo == 1, "xgmi: algo 0 (one-shot) or 1 (two-shot)");
+    TORCH_CHECK(algo == pda::kXgmiOneShot || algo == pda::kXgmiTwoShot || algo == pda::kXgmiRing,
+                "xgmi: algo 0 (one-shot), 1 (two-shot) or 2 (ring)");
     check_gpu(t, "t");
     TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, "xgmi: fp32 / bf16 only");
     const int64_t n = t.numel(), bytes = n * t.element_size();
@@ -963,21 +964,59 @@ class XgmiComm {
     c10::DeviceGuard g(t.device());
     auto st = stream_of(t);
     CHECK_HIP_OK(hipMemcpyAsync(data_, t.data_ptr(), (size_t)bytes, hipMemcpyDeviceToDevice, st));
+    launch(t.data_ptr(), n, average ? 1.f / (float)world_ : 1.f, algo, t.scalar_type() == at::kBFloat16, st);
+  }
+  void launch(void* out, int64_t n, float scale, int algo, bool bf16, hipStream_t st) {
     pda::XgmiArgs a{};
     for (int r = 0; r < pda::kXgmiMaxRanks; ++r) {
       a.data[r] = peer_data_[r];
       a.flags[r] = peer_flags_[r];
     }
-    a.out = t.data_ptr();
+    a.out = out;
     a.n = n;
     a.rank = rank_;
     a.world = world_;
-    a.scale = average ? 1.f / (float)world_ : 1.f;
+    a.scale = scale;
     a.epoch = ++epoch_;
     a.timeout_ticks = timeout_ticks_;
     a.err = err_;
     a.algo = algo;
-    CHECK_HIP_OK(pda::xgmi_allreduce(a, t.scalar_type() == at::kBFloat16, st));
+    CHECK_HIP_OK(pda::xgmi_allreduce(a, bf16, st));
+  }
+  // out[world * n] = every rank's `in` [n] in rank order (all-gather over the IPC mesh)
+  void allgather(Tensor in, Tensor out) {
+    TORCH_CHECK(opened_ || world_ == 1, "xgmi: open() the peer handles first");
+    check_gpu(in, "in");
+    check_gpu(out, "out");
+    TORCH_CHECK(in.scalar_type() == out.scalar_type() &&
+                    (in.scalar_type() == at::kFloat || in.scalar_type() == at::kBFloat16),
+                "xgmi: fp32 / bf16, same dtype");
+    TORCH_CHECK(in.is_contiguous() && out.is_contiguous(), "xgmi: contiguous tensors");
+    const int64_t n = in.numel(), bytes = n * in.element_size();
+    TORCH_CHECK(n % 8 == 0 && bytes <= cap_ && out.numel() == n * world_,
+                "xgmi all-gather: shard numel % 8 == 0, shard fits the exchange buffer, out = world x shard");
+    c10::DeviceGuard g(in.device());
+    auto st = stream_of(in);
+    CHECK_HIP_OK(hipMemcpyAsync(data_, in.data_ptr(), (size_t)bytes, hipMemcpyDeviceToDevice, st));
+    launch(out.data_ptr(), n, 1.f, pda::kXgmiAllGather, in.scalar_type() == at::kBFloat16, st);
+  }
+  // out[n / world] = scale * sum over ranks of chunk `rank` of `in` [n]
+  void reduce_scatter(Tensor in, Tensor out, bool average) {
+    TORCH_CHECK(opened_ || world_ == 1, "xgmi: open() the peer handles first");
+    check_gpu(in, "in");
+    check_gpu(out, "out");
+    TORCH_CHECK(in.scalar_type() == out.scalar_type() &&
+                    (in.scalar_type() == at::kFloat || in.scalar_type() == at::kBFloat16),
+                "xgmi: fp32 / bf16, same dtype");
+    TORCH_CHECK(in.is_contiguous() && out.is_contiguous(), "xgmi: contiguous tensors");
+    const int64_t n = in.numel(), bytes = n * in.element_size();
+    TORCH_CHECK(n % (8 * world_) == 0 && bytes <= cap_ && out.numel() * world_ == n,
+                "xgmi reduce-scatter: numel % (8 world) == 0, input fits the exchange buffer, out = shard");
+    c10::DeviceGuard g(in.device());
+    auto st = stream_of(in);
+    CHECK_HIP_OK(hipMemcpyAsync(data_, in.data_ptr(), (size_t)bytes, hipMemcpyDeviceToDevice, st));
+    launch(out.data_ptr(), n, average ? 1.f / (float)world_ : 1.f, pda::kXgmiReduceScatter,
+           in.scalar_type() == at::kBFloat16, st);
   }
   // non-blocking: the kernels store the error word into pinned host memory; 0 = no timeout so far
   int error() const { return __atomic_load_n(err_host_, __ATOMIC_ACQUIRE); }
@@ -1053,6 +1092,8 @@ PYBIND11_MODULE(_C, m) {
       .def("handles", &XgmiComm::handles)
       .def("open", &XgmiComm::open)
       .def("allreduce", &XgmiComm::allreduce, py::arg("t"), py::arg("average") = false, py::arg("algo") = 0)
+      .def("allgather", &XgmiComm::allgather, py::arg("inp"), py::arg("out"))
+      .def("reduce_scatter", &XgmiComm::reduce_scatter, py::arg("inp"), py::arg("out"), py::arg("average") = false)
       .def("error", &XgmiComm::error)
       .def("reset_error", &XgmiComm::reset_error)
       .def_property_readonly("capacity", &XgmiComm::capacity);

@@ -32,6 +32,8 @@ struct AttnParams {
 constexpr int kXgmiMaxRanks = 8;
 constexpr int kXgmiMaxBlocks = 128;
 constexpr int kXgmiPhases = 3;
+// XgmiArgs::algo: all-reduce one-shot / two-shot / ring, all-gather, reduce-scatter
+constexpr int kXgmiOneShot = 0, kXgmiTwoShot = 1, kXgmiRing = 2, kXgmiAllGather = 3, kXgmiReduceScatter = 4;
 struct XgmiArgs {
   void* data[kXgmiMaxRanks];       // exchange buffer of every rank (own + IPC-mapped peers)
   uint32_t* flags[kXgmiMaxRanks];  // flag array of every rank: [kXgmiPhases][kXgmiMaxBlocks][kXgmiMaxRanks]
@@ -42,7 +44,7 @@ struct XgmiArgs {
   uint32_t epoch;
   long long timeout_ticks;         // wall_clock64 ticks before a spin gives up
   int* err;
-  int algo;                        // 0 = one-shot, 1 = two-shot (reduce-scatter + all-gather)
+  int algo;                        // kXgmi* below
 };
 hipError_t xgmi_alloc(void** p, size_t bytes);
 hipError_t xgmi_free(void* p);

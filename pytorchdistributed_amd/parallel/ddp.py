@@ -162,7 +162,7 @@ class DistributedDataParallel(tnn.Module):
         # the bucket's gradients may still be in flight on the side (weight-gradient) stream as well as
         # on the current stream (ops/streams.py): the collective is ordered after both
         producers = _streams.producer_streams(t.device) if t.is_cuda else []
-        if self.xgmi is not None and self.xgmi.fits(t):
+        if self.xgmi is not None and self.xgmi.fits(t, self._xgmi_algo):
             # one-shot IPC all-reduce on a side stream, ordered after the kernels that produced the bucket
             ticket = _watchdog.arm(f"ddp xgmi all_reduce bucket {b} ({nbytes / 2**20:.1f} MB, {t.dtype})")
             with torch.cuda.stream(self._ipc_stream), _timing.range(f"ddp.xgmi_all_reduce.b{b}"):

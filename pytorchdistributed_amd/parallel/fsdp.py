@@ -49,6 +49,19 @@ def _round(n, a):
     return (n + a - 1) // a * a
 
 
+class _StreamWork:
+    """Work handle of a side-stream collective: wait() orders the current stream after it."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+
+    def is_completed(self):
+        return self.event.query()
+
+
 class _Unit:
     def __init__(self, fsdp: "FullyShardedDataParallel", module: tnn.Module, params: List[Tuple[tnn.Module, str]],
                  index: int):
@@ -148,6 +161,10 @@ class _Unit:
             if self.fsdp.world == 1:
                 self.flat.copy_(send)
                 self.gathered = True
+            elif self.fsdp.xgmi is not None:
+                flat = self.flat
+                self.pending_ag = self.fsdp._ipc(lambda: self.fsdp.xgmi.all_gather_into_tensor(flat, send),
+                                                 [torch.cuda.current_stream(self.device)], [send])
             else:
                 self.pending_ag = dist.all_gather_into_tensor(self.flat, send, group=self.fsdp.group,
                                                               async_op=True)
@@ -221,6 +238,31 @@ class FullyShardedDataParallel(tnn.Module):
                 u.module.register_forward_hook(self._make_post_fwd(u))
         self._pending_rs = None
         self._callback_queued = False
+        # ---- optional direct xGMI collectives (PDA_FSDP_COMM=ipc, one node): the unit all-gathers pull
+        # every peer's shard over its own link and the gradient reduce-scatters reduce chunk `rank` of
+        # every peer's buffer (csrc/kernels/xgmi.hip), on one ordered side stream; RCCL by default
+        self.xgmi = None
+        if os.environ.get("PDA_FSDP_COMM", "rccl").lower() in ("ipc", "xgmi") and self.world > 1 and \
+                process_group is None and all(u.device.type == "cuda" for u in self.units):
+            from . import xgmi as _xgmi
+
+            if _xgmi.single_node():
+                cap = max(u.numel for u in self.units) * torch.tensor([], dtype=self.param_dtype).element_size()
+                self.xgmi = _xgmi.XgmiAllReduce(capacity_mb=cap / 2 ** 20 + 1, device=self.units[0].device)
+                self._ipc_stream = torch.cuda.Stream(self.units[0].device)
+
+    def _ipc(self, fn, producers, tensors):
+        """Run ``fn`` on the IPC stream after ``producers``; returns a work handle (wait = stream wait)."""
+        s = self._ipc_stream
+        for p in producers:
+            s.wait_stream(p)
+        for t in tensors:
+            t.record_stream(s)
+        with torch.cuda.stream(s):
+            fn()
+            done = torch.cuda.Event()
+            done.record(s)
+        return _StreamWork(done)
 
     # ------------------------------------------------------------ forward hooks
     def _next_in_order(self, u: _Unit, backward: bool) -> Optional[_Unit]:
@@ -287,6 +329,15 @@ class FullyShardedDataParallel(tnn.Module):
             # order the collective after both streams (RCCL waits on the current stream)
             producers = _streams.producer_streams(grad_full.device) if grad_full.is_cuda else []
             ctx = contextlib.nullcontext()
+            if self.xgmi is not None:
+                self._pending_rs = (u, self._ipc(lambda: self.xgmi.reduce_scatter_tensor(out, grad_full, average=True),
+                                                 producers, [out]), out)
+                if u is not self.root_unit:
+                    u.reshard()
+                if not self._callback_queued:
+                    self._callback_queued = True
+                    torch.autograd.Variable._execution_engine.queue_callback(self._post_backward_final)
+                return
             if len(producers) > 1:
                 if self.nccl:
                     producers[1].wait_stream(producers[0])
@@ -314,7 +365,7 @@ class FullyShardedDataParallel(tnn.Module):
         self._pending_rs = None
         if work is not None:
             work.wait()
-        if not self.nccl and self.world > 1:
+        if not self.nccl and self.xgmi is None and self.world > 1:
             out.div_(self.world)
         g = out if out.dtype == u.shard.dtype else out.to(u.shard.dtype)
         if u.shard.grad is None:

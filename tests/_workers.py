@@ -380,7 +380,42 @@ def ddp_resnet_gpu_worker(rank, world, outdir):
     pd.destroy_process_group()
 
 
-def fsdp_llama_gpu_worker(rank, world, outdir):
+def xgmi_collectives_worker(rank, world, outdir):
+    """All-gather and reduce-scatter over the IPC mesh (FSDP's collectives), interleaved with ring
+    all-reduces on the same exchange buffers: results vs the concatenation / chunk sums, fp32 and bf16."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.xgmi import XgmiAllReduce
+
+    torch.cuda.set_device(0)
+    pd.init_process_group("gloo")
+    comm = XgmiAllReduce(capacity_mb=8, device=torch.device("cuda", 0), timeout_s=20.0)
+    for it, (shard, dt) in enumerate([(8, torch.float32), (1024, torch.bfloat16), (8 * 1001, torch.float32),
+                                      (1 << 18, torch.bfloat16), (40, torch.bfloat16)]):
+        g = torch.Generator().manual_seed(7 + it)
+        shards = [torch.randn(shard, generator=g).to(dt) for _ in range(world)]
+        out = torch.empty(world * shard, device="cuda", dtype=dt)
+        comm.all_gather_into_tensor(out, shards[rank].cuda())
+        torch.cuda.synchronize()
+        comm.check()
+        assert torch.equal(out.cpu(), torch.cat(shards)), ("allgather", it)
+        fulls = [torch.randn(world * shard, generator=g).to(dt) for _ in range(world)]
+        rs = torch.empty(shard, device="cuda", dtype=dt)
+        comm.reduce_scatter_tensor(rs, fulls[rank].cuda(), average=(it % 2 == 0))
+        ar = fulls[rank].cuda().clone()
+        comm(ar, average=False, algo="ring")
+        torch.cuda.synchronize()
+        comm.check()
+        tot = sum(f.float() for f in fulls)
+        ref = tot[rank * shard:(rank + 1) * shard] / (world if it % 2 == 0 else 1)
+        tol = 1e-6 if dt == torch.float32 else 1e-2
+        assert ((rs.float().cpu() - ref).norm() / ref.norm()).item() < tol, ("reduce_scatter", it)
+        assert ((ar.float().cpu() - tot).norm() / tot.norm()).item() < tol, ("ring", it)
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+        f.write("ok")
+    pd.destroy_process_group()
+
+
+def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl"):
     """FSDP (bf16 shards, fused AdamW with fp32 masters, gradients written into the units' flat buffers)
     on a tiny Llama, `world` ranks sharing cuda:0 (gloo when world > 1): after 2 steps the consolidated
     parameters match an unsharded replica trained on the concatenated batch."""
@@ -389,6 +424,7 @@ def fsdp_llama_gpu_worker(rank, world, outdir):
     from pytorchdistributed_amd.optim import AdamW
     from pytorchdistributed_amd.parallel.fsdp import FullyShardedDataParallel
 
+    os.environ["PDA_FSDP_COMM"] = comm  # "ipc": unit gathers / gradient reduce-scatters over the IPC mesh
     torch.cuda.set_device(0)
     if world > 1:
         pd.init_process_group("gloo")
@@ -398,6 +434,7 @@ def fsdp_llama_gpu_worker(rank, world, outdir):
     model = Llama(cfg, device="cuda", dtype=torch.bfloat16)
     model.load_state_dict(ref.state_dict())
     fsdp = FullyShardedDataParallel(model, unit_types=(LlamaBlock,))
+    assert (fsdp.xgmi is not None) == (comm == "ipc" and world > 1)
     opt = AdamW(fsdp.parameters(), lr=1e-3, weight_decay=0.1)
     ropt = AdamW(ref.parameters(), lr=1e-3, weight_decay=0.1)
     g = torch.Generator().manual_seed(5)

@@ -286,3 +286,27 @@ def test_grad_join_masked_grad():
     j3.stash(mg)
     j3.stash(other)
     assert torch.allclose(j3.take(), other + dz * mask)
+
+
+def test_xgmi_tuning_table_from_sweep(tmp_path, monkeypatch):
+    """tools/bench_allreduce.py --write-table: per size the fastest transport, equal neighbours merged,
+    last range open-ended; load_table checks the world size and the algorithm names."""
+    import json
+
+    from pytorchdistributed_amd.parallel import xgmi
+
+    def rec(mb, r, o, t):
+        return {"size_mb": mb, "rccl": {"ms": r}, "xgmi_oneshot": {"ms": o}, "xgmi_twoshot": {"ms": t}}
+
+    recs = [rec(0.25, 0.05, 0.01, 0.02), rec(1, 0.06, 0.02, 0.03), rec(4, 0.10, 0.09, 0.05), rec(64, 0.5, 2.0, 0.6)]
+    tab = xgmi.table_from_sweep(recs, 8)
+    assert tab["world"] == 8
+    assert [e["algo"] for e in tab["entries"]] == ["oneshot", "twoshot", "rccl"]
+    assert tab["entries"][0]["max_bytes"] == 2 ** 20 and tab["entries"][1]["max_bytes"] == 4 * 2 ** 20
+    assert tab["entries"][-1]["max_bytes"] >= 1 << 60
+    p = tmp_path / "t.json"
+    p.write_text(json.dumps(tab))
+    assert xgmi.load_table(8, str(p)) == tab["entries"]
+    assert xgmi.load_table(4, str(p)) is None  # table of another world size
+    monkeypatch.setenv("PDA_XGMI_TUNING", str(p))
+    assert xgmi.load_table(8) == tab["entries"]

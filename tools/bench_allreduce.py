@@ -1,9 +1,12 @@
 """All-reduce bandwidth sweep over bucket sizes: RCCL (torch.distributed
-"nccl") vs the one-shot and two-shot xGMI IPC kernels, bf16, per size: time, algorithm bandwidth and bus bandwidth
-(2(N-1)/N x bytes / time).  Run on one node:
+"nccl") vs the one-shot, two-shot and ring xGMI IPC kernels, bf16, per size: time, algorithm bandwidth
+and bus bandwidth (2(N-1)/N x bytes / time).  ``--write-table PATH`` (default: the per-node location
+``parallel.xgmi.default_table_path``) stores the per-size winner of RCCL / one-shot / two-shot as the
+crossover table that ``PDA_ALLREDUCE=ipc`` (DDP buckets) then follows.  Run on one node:
 
-    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_allreduce.py
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/bench_allreduce.py --write-table
 """
+import argparse
 import json
 import os
 import sys
@@ -13,7 +16,7 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import pytorchdistributed_amd.distributed as pd  # noqa: E402
-from pytorchdistributed_amd.parallel.xgmi import XgmiAllReduce  # noqa: E402
+from pytorchdistributed_amd.parallel.xgmi import XgmiAllReduce, default_table_path, table_from_sweep  # noqa: E402
 
 SIZES_MB = [0.25, 1, 2, 4, 8, 16, 32, 64, 128]
 
@@ -35,24 +38,36 @@ def timeit(fn, iters=20):
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--write-table", nargs="?", const="", default=None,
+                    help="write the RCCL / one-shot / two-shot crossover table (optional path)")
+    args = ap.parse_args()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     pd.init_process_group("nccl", device_id=local)
     world, rank = dist.get_world_size(), dist.get_rank()
     xg = XgmiAllReduce(capacity_mb=max(SIZES_MB) + 1)
+    records = []
     for mb in SIZES_MB:
         n = int(mb * 2 ** 20 / 2) // 8 * 8
         t = torch.randn(n, device="cuda", dtype=torch.bfloat16)
         rec = {"size_mb": mb, "world": world}
         for name, fn in [("rccl", lambda: dist.all_reduce(t)), ("xgmi_oneshot", lambda: xg(t, algo="oneshot")),
-                         ("xgmi_twoshot", lambda: xg(t, algo="twoshot"))]:
+                         ("xgmi_twoshot", lambda: xg(t, algo="twoshot")), ("xgmi_ring", lambda: xg(t, algo="ring"))]:
             ms = timeit(fn)
             alg = n * 2 / (ms * 1e-3) / 1e9
             rec[name] = {"ms": round(ms, 4), "alg_GBps": round(alg, 1),
                          "bus_GBps": round(alg * 2 * (world - 1) / world, 1)}
+        records.append(rec)
         if rank == 0:
             print(json.dumps(rec), flush=True)
     xg.check()
+    if args.write_table is not None and rank == 0:
+        path = args.write_table or default_table_path(world)
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(table_from_sweep(records, world), f, indent=1)
+        print(f"crossover table -> {path}", flush=True)
     pd.destroy_process_group()
 
 
