@@ -9,6 +9,9 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
+# (importing the package first raises GPU_MAX_HW_QUEUES before HIP initialises: see
+# pytorchdistributed_amd/__init__.py:_ensure_hw_queues)
+import pytorchdistributed_amd  # noqa: E402,F401
 from pytorchdistributed_amd.bench.resnet_ddp import main  # noqa: E402
 
 if __name__ == "__main__":

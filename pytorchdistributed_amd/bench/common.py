@@ -36,7 +36,10 @@ def setup(n_gpus: int):
                                  f"rank; PDA_DIST_BACKEND=gloo rehearses with shared GPUs)")
             gpu = local % count
         torch.cuda.set_device(gpu)
-    if world > 1 and not dist.is_initialized():
+    # PDA_DDP_FORCE_COMM=1 at N=1: a one-rank RCCL group, so the bucket all-reduces of the multi-GPU
+    # path run (and are timed) on a single GPU
+    force = os.environ.get("PDA_DDP_FORCE_COMM") == "1" and use_gpu and backend == "nccl"
+    if (world > 1 or force) and not dist.is_initialized():
         pdist.init_process_group(backend, rank=rank, world_size=world,
                                  device_id=gpu if use_gpu and backend == "nccl" else None)
     device = torch.device("cuda", gpu) if use_gpu else torch.device("cpu")

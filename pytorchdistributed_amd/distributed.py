@@ -155,6 +155,13 @@ def init_process_group(
         kwargs["init_method"] = init_method
     if device_id is not None and backend == "nccl":
         kwargs["device_id"] = torch.device("cuda", device_id)
+    if backend == "nccl" and os.environ.get("PDA_COMM_PRIORITY", "1") != "0":
+        # RCCL's internal streams at high priority (SURVEY §2.3 N01, config.comm_priority): a bucket
+        # all-reduce's kernels are dispatched ahead of queued backward kernels, so communication
+        # starts as soon as its bucket is ready instead of behind the compute stream's backlog
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        kwargs["pg_options"] = opts
     dist.init_process_group(**kwargs)
     _STATE["backend"] = "ring" if want_ring else backend
     if want_ring:

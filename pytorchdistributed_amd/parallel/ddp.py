@@ -78,6 +78,10 @@ class DistributedDataParallel(tnn.Module):
         self._stats = {"comm_bytes": 0, "comm_calls": 0}
         self._exposed_events: List = []
         self._tickets: List = []
+        # PDA_DDP_FORCE_COMM=1: issue the bucket collectives even at world size 1 (a one-rank RCCL group
+        # on a one-GPU box runs every RCCL call, stream wait and watchdog ticket of the multi-GPU path)
+        self._force_comm = os.environ.get("PDA_DDP_FORCE_COMM") == "1"
+        self._comm = self.world > 1 or (self._force_comm and dist.is_initialized())
 
         params = [p for p in module.parameters() if p.requires_grad]
         self._params = params
@@ -105,7 +109,7 @@ class DistributedDataParallel(tnn.Module):
         self._param_index = {id(p): i for i, p in enumerate(params)}
         # ---- rank-0 state broadcast (X04) as one collective per flat buffer
         self._buffer_flats = flatten_buffers(module)
-        if self.world > 1:
+        if self._comm:
             with torch.no_grad():
                 for g in self.groups.values():
                     self._bcast(g.param_buffer)
@@ -147,7 +151,7 @@ class DistributedDataParallel(tnn.Module):
 
     def _launch(self, b: int):
         t = self._bucket_view(b)
-        if self.world == 1:
+        if not self._comm:
             return
         # stream-safety guard: the fused optimizer refuses a flat group whose bucket
         # collectives the compute stream has not waited on yet (cleared by _finalize)
@@ -285,7 +289,7 @@ class DistributedDataParallel(tnn.Module):
         self._check_xgmi()
         if self._tickets:
             self._sweep_tickets()
-        if self.broadcast_buffers and self.world > 1 and self.module.training and self._buffer_flats:
+        if self.broadcast_buffers and self._comm and self.module.training and self._buffer_flats:
             with torch.no_grad():
                 for flat in self._buffer_flats.values():
                     self._bcast(flat)

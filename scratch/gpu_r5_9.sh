@@ -1,0 +1,14 @@
+#!/bin/bash
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > gpurun_out/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -2 gpurun_out/$name.log | cut -c1-250
+  if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
+}
+step pytest_rccl1 300 python -u -m pytest tests/test_models_gpu.py -k rccl -q -x -p no:cacheprovider --timeout 200 --timeout-method thread
+step bench_plain 300 python bench.py --steps 30 --warmup 5
+PDA_DDP_FORCE_COMM=1 step bench_rccl1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 1 --steps 30 --warmup 5

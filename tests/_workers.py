@@ -415,6 +415,51 @@ def xgmi_collectives_worker(rank, world, outdir):
     pd.destroy_process_group()
 
 
+def ddp_rccl_world1_worker(rank, world, outdir):
+    """A ONE-rank RCCL group (the only RCCL group a one-GPU box can form) with PDA_DDP_FORCE_COMM=1:
+    every bucket goes through the nccl branch of DDP — high-priority RCCL streams, AVG all-reduces
+    ordered after the main AND the weight-gradient side stream, watchdog tickets, buffer broadcasts —
+    and the gradients must equal a plain replica's; three steps of ResNet-50 (bf16, fused SGD)."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.models.resnet import resnet50
+    from pytorchdistributed_amd.ops import cross_entropy
+    from pytorchdistributed_amd.optim import SGD
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+
+    os.environ["PDA_DDP_FORCE_COMM"] = "1"
+    os.environ["PDA_TRACK_COMM"] = "1"
+    torch.cuda.set_device(0)
+    pd.init_process_group("nccl", device_id=0)
+    torch.manual_seed(3)
+    base = resnet50(device="cuda", dtype=torch.bfloat16)
+    model = DistributedDataParallel(base, device_ids=[0], bucket_cap_mb=8, first_bucket_mb=1)
+    local = resnet50(device="cuda", dtype=torch.bfloat16)
+    local.load_state_dict(base.state_dict())
+    opt = SGD(model.parameters(), lr=0.05, momentum=0.9)
+    lopt = SGD(local.parameters(), lr=0.05, momentum=0.9)
+    g = torch.Generator().manual_seed(11)
+    worst = (0.0, "")
+    for _ in range(3):
+        x = torch.randn(8, 64, 64, 3, generator=g).to("cuda", torch.bfloat16)
+        y = torch.randint(0, 1000, (8,), generator=g).to("cuda")
+        opt.zero_grad(set_to_none=True)
+        cross_entropy(model(x), y).backward()
+        lopt.zero_grad(set_to_none=True)
+        cross_entropy(local(x), y).backward()
+        for (n, p), (_, q) in zip(base.named_parameters(), local.named_parameters()):
+            a, b = p.grad.float(), q.grad.float()
+            worst = max(worst, (((a - b).norm() / b.norm().clamp_min(1e-12)).item(), n))
+        opt.step()
+        lopt.step()
+    stats = model.comm_stats()
+    assert stats["comm_calls"] == 3 * model.reducer.num_buckets and model.reducer.num_buckets > 3, stats
+    assert "exposed_comm_ms" in stats, stats
+    assert worst[0] < 3e-2, worst
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+        f.write(f"ok {worst[0]:.3e} buckets={model.reducer.num_buckets} exposed_ms={stats['exposed_comm_ms']:.3f}")
+    pd.destroy_process_group()
+
+
 def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl"):
     """FSDP (bf16 shards, fused AdamW with fp32 masters, gradients written into the units' flat buffers)
     on a tiny Llama, `world` ranks sharing cuda:0 (gloo when world > 1): after 2 steps the consolidated

@@ -144,6 +144,15 @@ def test_ddp_resnet50_two_ranks_share_gpu(tmp_path):
         assert (tmp_path / f"ok{r}").read_text().startswith("ok")
 
 
+def test_ddp_rccl_one_rank_group_matches_local(tmp_path):
+    """The RCCL branch of DDP (what the driver's 2/4/8-GPU runs execute) on a one-rank RCCL group."""
+    import _workers
+    from pytorchdistributed_amd.launch import spawn
+
+    spawn(_workers.ddp_rccl_world1_worker, args=(1, str(tmp_path)), nprocs=1, timeout=300)
+    assert (tmp_path / "ok0").read_text().startswith("ok")
+
+
 @pytest.mark.parametrize("world", [1, 2])
 def test_fsdp_llama_tiny_matches_unsharded(tmp_path, world):
     """FSDP on the native transformer path: world 1 (the shard aliases the gathered buffer) and world 2
