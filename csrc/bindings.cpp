@@ -644,10 +644,38 @@ std::vector<Tensor> add_rownorm_fwd(Tensor x, Tensor r, Tensor gamma, c10::optio
   return {h, y};
 }
 
-std::vector<Tensor> rownorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, bool rms) {
+// training: (h = x + r, norm(h), mean(h), rstd(h)); all bf16, contiguous
+std::vector<Tensor> add_rownorm_fwd_train(Tensor x, Tensor r, Tensor gamma, c10::optional<Tensor> beta, double eps,
+                                          bool rms) {
+  check_bf16(x, "x");
+  check_bf16(r, "r");
+  check_bf16(gamma, "gamma");
+  TORCH_CHECK(x.is_contiguous() && r.is_contiguous() && x.sizes() == r.sizes(), "add_rownorm: x, r contiguous, same shape");
+  const int64_t D = x.size(-1), rows = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && D <= 8192 && gamma.numel() == D, "norm width must be a multiple of 8 and <= 8192");
+  if (!rms) {
+    TORCH_CHECK(beta.has_value() && beta->numel() == D);
+    check_bf16(*beta, "beta");
+  }
+  c10::DeviceGuard g(x.device());
+  Tensor h = at::empty_like(x), y = at::empty_like(x);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({rms ? 1 : rows}, fo), rstd = at::empty({rows}, fo);
+  CHECK_HIP_OK(pda::add_rownorm_fwd(bp(x), bp(r), bp(gamma), rms ? nullptr : bp(*beta), bpm(h), bpm(y), rows, D,
+                                    (float)eps, rms, stream_of(x), mean.data_ptr<float>(), rstd.data_ptr<float>()));
+  return {h, y, mean, rstd};
+}
+
+std::vector<Tensor> rownorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, bool rms,
+                                c10::optional<Tensor> addend) {
   check_f32_or_bf16(dy, "dy");
   check_f32_or_bf16(x, "x");
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type());
+  if (addend.has_value()) {
+    TORCH_CHECK(addend->sizes() == x.sizes() && addend->scalar_type() == x.scalar_type() && addend->is_contiguous(),
+                "rownorm_bwd: addend must match x");
+    check_gpu(*addend, "addend");
+  }
   const int64_t D = x.size(-1), rows = x.numel() / D;
   c10::DeviceGuard g(x.device());
   Tensor dx = at::empty_like(x);
@@ -657,7 +685,7 @@ std::vector<Tensor> rownorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, 
   CHECK_HIP_OK(pda::rownorm_bwd(dy.data_ptr(), x.data_ptr(), is_bf16(x), gamma.data_ptr(), is_bf16(gamma),
                                 rms ? nullptr : mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(),
                                 dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), rows, D, rms, ws.data_ptr<float>(),
-                                stream_of(x)));
+                                stream_of(x), addend.has_value() ? addend->data_ptr() : nullptr));
   return {dx, dgamma, dbeta};
 }
 
@@ -1075,7 +1103,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("simt_gemm", &simt_gemm);
   m.def("rownorm_fwd", &rownorm_fwd);
   m.def("add_rownorm_fwd", &add_rownorm_fwd);
-  m.def("rownorm_bwd", &rownorm_bwd);
+  m.def("rownorm_bwd", &rownorm_bwd, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
+        py::arg("rms"), py::arg("addend") = py::none());
+  m.def("add_rownorm_fwd_train", &add_rownorm_fwd_train);
   m.def("attn_fwd", &attn_fwd);
   m.def("decode_attn", &decode_attn, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("L"), py::arg("scale"),
         py::arg("splits") = 0, py::arg("pos_dev") = py::none());

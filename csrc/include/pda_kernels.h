@@ -169,12 +169,13 @@ hipError_t simt_gemm(const void* A, int a_dt, int64_t sam, int64_t sak, const vo
 
 // ---- rownorm.hip (LayerNorm / RMSNorm over the last dim, D % 8 == 0, D <= 8192)
 hipError_t add_rownorm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* gamma, const bf16_t* beta, bf16_t* h,
-                           bf16_t* y, int64_t rows, int64_t D, float eps, bool rms, hipStream_t st);
+                           bf16_t* y, int64_t rows, int64_t D, float eps, bool rms, hipStream_t st,
+                           float* mean = nullptr, float* rstd = nullptr);  // stats of h: training
 hipError_t rownorm_fwd(const void* x, bool x_bf16, const void* gamma, const void* beta, bool p_bf16, void* y,
                        float* mean, float* rstd, int64_t rows, int64_t D, float eps, bool rms, hipStream_t st);
 hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* gamma, bool p_bf16, const float* mean,
                        const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, bool rms,
-                       float* ws, hipStream_t st);
+                       float* ws, hipStream_t st, const void* addend = nullptr);  // dx += addend (same layout)
 // column sums via slab partials (cols % 8 == 0); ws holds colreduce_ws_floats(rows, cols, 1) floats
 hipError_t colsum(const void* x, bool bf16, float* out, int64_t rows, int64_t cols, float* ws, hipStream_t st);
 int64_t colreduce_ws_floats(int64_t rows, int64_t D, int nout);

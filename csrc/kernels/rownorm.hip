@@ -85,7 +85,8 @@ __global__ void __launch_bounds__(kThreads) rownorm_bwd_dx_kernel(const T* __res
                                                                   const P* __restrict__ gamma,
                                                                   const float* __restrict__ mean_in,
                                                                   const float* __restrict__ rstd_in,
-                                                                  T* __restrict__ dx, int64_t rows, int64_t D) {
+                                                                  T* __restrict__ dx, int64_t rows, int64_t D,
+                                                                  const T* __restrict__ addend) {
   constexpr bool kKeep = VPL <= 4;
   constexpr int KV = kKeep ? VPL : 1;
   const int lane = threadIdx.x & 63;
@@ -133,6 +134,12 @@ __global__ void __launch_bounds__(kThreads) rownorm_bwd_dx_kernel(const T* __res
         load8(gamma + c, g);
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rstd * (g[j] * d[j] - m1 - (xv[j] - mean) * rstd * m2);
+      }
+      if (addend) {  // the residual stream's own gradient (fused add + norm): dx = norm_bwd(dy) + dh
+        float a[8];
+        load8(addend + row * D + c, a);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += a[j];
       }
       store8(dx + row * D + c, o);
     }
@@ -241,15 +248,18 @@ int plan_slabs(int64_t rows, int64_t D) {
   return (int)nslab;
 }
 
-// Serving: residual add fused into the next norm — h = x + r (rounded to bf16, as the unfused add
-// would store it) is written once and normalised from registers (one HBM pass instead of add + norm).
+// Residual add fused into the next norm — h = x + r (rounded to bf16, as the unfused add would store
+// it) is written once and normalised from registers (one HBM pass instead of add + norm).  Serving
+// passes no statistics buffers; training stores mean / rstd of h for the backward.
 template <bool RMS, int VPL>
 __global__ void __launch_bounds__(kThreads) add_rownorm_fwd_kernel(const bf16_t* __restrict__ x,
                                                                    const bf16_t* __restrict__ r,
                                                                    const bf16_t* __restrict__ gamma,
                                                                    const bf16_t* __restrict__ beta,
                                                                    bf16_t* __restrict__ h, bf16_t* __restrict__ y,
-                                                                   int64_t rows, int64_t D, float eps) {
+                                                                   int64_t rows, int64_t D, float eps,
+                                                                   float* __restrict__ mean_out,
+                                                                   float* __restrict__ rstd_out) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -299,6 +309,10 @@ __global__ void __launch_bounds__(kThreads) add_rownorm_fwd_kernel(const bf16_t*
       store8(y + row * D + c, o);
     }
   }
+  if (rstd_out && lane == 0) {  // training: the backward's statistics of h
+    if (!RMS) mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
 }
 
 template <typename F>
@@ -314,13 +328,14 @@ void dispatch_vpl(int64_t D, F&& f) {
 }  // namespace
 
 hipError_t add_rownorm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* gamma, const bf16_t* beta, bf16_t* h,
-                           bf16_t* y, int64_t rows, int64_t D, float eps, bool rms, hipStream_t st) {
+                           bf16_t* y, int64_t rows, int64_t D, float eps, bool rms, hipStream_t st, float* mean,
+                           float* rstd) {
   if (rows == 0) return hipSuccess;
   const unsigned grid = (unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock);
   dispatch_vpl(D, [&](auto vc) {
     constexpr int V = decltype(vc)::value;
-    if (rms) add_rownorm_fwd_kernel<true, V><<<grid, kThreads, 0, st>>>(x, r, gamma, beta, h, y, rows, D, eps);
-    else add_rownorm_fwd_kernel<false, V><<<grid, kThreads, 0, st>>>(x, r, gamma, beta, h, y, rows, D, eps);
+    if (rms) add_rownorm_fwd_kernel<true, V><<<grid, kThreads, 0, st>>>(x, r, gamma, beta, h, y, rows, D, eps, mean, rstd);
+    else add_rownorm_fwd_kernel<false, V><<<grid, kThreads, 0, st>>>(x, r, gamma, beta, h, y, rows, D, eps, mean, rstd);
   });
   return hipGetLastError();
 }
@@ -353,7 +368,7 @@ hipError_t rownorm_fwd(const void* x, bool x_bf16, const void* gamma, const void
 
 hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* gamma, bool p_bf16, const float* mean,
                        const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, bool rms,
-                       float* ws, hipStream_t st) {
+                       float* ws, hipStream_t st, const void* addend) {
   if (rows == 0) {
     PDA_CHECK_HIP(hipMemsetAsync(dgamma, 0, D * sizeof(float), st));
     if (!rms) PDA_CHECK_HIP(hipMemsetAsync(dbeta, 0, D * sizeof(float), st));
@@ -363,7 +378,7 @@ hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* g
   dispatch_vpl(D, [&](auto vc) {
     constexpr int V = decltype(vc)::value;
 #define L(T, P, R) \
-  rownorm_bwd_dx_kernel<T, P, R, V><<<grid, kThreads, 0, st>>>((const T*)dy, (const T*)x, (const P*)gamma, mean, rstd, (T*)dx, rows, D)
+  rownorm_bwd_dx_kernel<T, P, R, V><<<grid, kThreads, 0, st>>>((const T*)dy, (const T*)x, (const P*)gamma, mean, rstd, (T*)dx, rows, D, (const T*)addend)
     if (rms) {
       if (x_bf16 && p_bf16) L(bf16_t, bf16_t, true);
       else if (x_bf16) L(bf16_t, float, true);

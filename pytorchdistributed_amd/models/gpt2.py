@@ -60,13 +60,19 @@ class GPT2Block(tnn.Module):
         self.c_fc = pnn.Linear(d, 4 * d, **kw)
         self.mlp_proj = pnn.Linear(4 * d, d, **kw)
 
-    def forward(self, x):
+    def forward(self, x, res=None, pending: bool = False):
+        """``pending=False``: the block output.  ``pending=True``: the residual stream is carried as a
+        pair — the input is ``x + res`` (``res=None``: just ``x``) and the block returns ``(h, y)`` whose
+        sum is its output, so each residual add runs inside the next LayerNorm, forward and backward
+        (:func:`ops.add_norm_train`)."""
         B, T, d = x.shape
-        qkv = self.c_attn(self.ln_1(x)).view(B, T, 3 * self.n_head, d // self.n_head)
+        h, n = ops.add_norm_train(x, res, self.ln_1.weight, self.ln_1.bias, self.ln_1.eps, rms=False)
+        qkv = self.c_attn(n).view(B, T, 3 * self.n_head, d // self.n_head)
         a = ops.attention_qkv(qkv, self.n_head, self.n_head, causal=True)
-        x = x + self.attn_proj(a.reshape(B, T, d))
-        h = ops.gelu_tanh(self.c_fc(self.ln_2(x)))
-        return x + self.mlp_proj(h)
+        h, n = ops.add_norm_train(h, self.attn_proj(a.reshape(B, T, d)), self.ln_2.weight, self.ln_2.bias,
+                                  self.ln_2.eps, rms=False)
+        y = self.mlp_proj(ops.gelu_tanh(self.c_fc(n)))
+        return (h, y) if pending else h + y
 
     @torch.no_grad()
     def forward_cached(self, x, k_cache, v_cache, pos, res=None):
@@ -113,18 +119,20 @@ class GPT2(tnn.Module):
         pos = torch.arange(T, device=idx.device)
         return ops.embedding(idx, self.wte) + ops.embedding(pos, self.wpe).unsqueeze(0)
 
-    def head(self, x, targets=None):
-        logits = ops.linear(self.ln_f(x), self.wte)
+    def head(self, x, targets=None, res=None):
+        """LN_f (fused with a pending residual ``res``) + tied LM head (+ loss)."""
+        _, n = ops.add_norm_train(x, res, self.ln_f.weight, self.ln_f.bias, self.ln_f.eps, rms=False)
+        logits = ops.linear(n, self.wte)
         if targets is None:
             return logits[..., : self.cfg.vocab_size]
         return ops.cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1),
                                  num_valid_classes=self.cfg.vocab_size)
 
     def forward(self, idx, targets=None):
-        x = self.embed(idx)
+        x, res = self.embed(idx), None
         for blk in self.h:
-            x = blk(x)
-        return self.head(x, targets)
+            x, res = blk(x, res, pending=True)
+        return self.head(x, targets, res)
 
     # ---------------------------------------------------------------- serving (serving/generate.py)
     def kv_shape(self):
@@ -186,11 +194,13 @@ class GPT2Stage(tnn.Module):
         if self.first:
             T = x.shape[1]
             x = ops.embedding(x, self.wte) + ops.embedding(torch.arange(T, device=x.device), self.wpe).unsqueeze(0)
+        res = None
         for blk in self.h:
-            x = blk(x)
+            x, res = blk(x, res, pending=True)
         if self.last:
-            x = ops.linear(self.ln_f(x), self.lm_head)
-        return x
+            _, n = ops.add_norm_train(x, res, self.ln_f.weight, self.ln_f.bias, self.ln_f.eps, rms=False)
+            return ops.linear(n, self.lm_head)
+        return x + res if res is not None else x
 
     def loss(self, logits, targets):
         return ops.cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1),

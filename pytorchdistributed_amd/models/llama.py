@@ -60,13 +60,18 @@ class LlamaBlock(tnn.Module):
         self.w13 = pnn.Linear(cfg.dim, 2 * cfg.ffn_dim, bias=False, **kw)  # gate | up
         self.w2 = pnn.Linear(cfg.ffn_dim, cfg.dim, bias=False, **kw)
 
-    def forward(self, x, rope):
+    def forward(self, x, rope, res=None, pending: bool = False):
+        """``pending=True``: input ``x + res``, output the pair ``(h, y)`` (see GPT2Block.forward) — the
+        residual adds run inside the RMSNorms (:func:`ops.add_norm_train`)."""
         B, T, d = x.shape
         c = self.cfg
-        qkv = self.wqkv(self.attention_norm(x)).view(B, T, c.n_heads + 2 * c.n_kv_heads, c.head_dim)
+        an, fn = self.attention_norm, self.ffn_norm
+        h, n = ops.add_norm_train(x, res, an.weight, eps=an.eps)
+        qkv = self.wqkv(n).view(B, T, c.n_heads + 2 * c.n_kv_heads, c.head_dim)
         a = ops.attention_qkv(qkv, c.n_heads, c.n_kv_heads, causal=True, rope=rope)
-        h = x + self.wo(a.reshape(B, T, d))
-        return h + self.w2(ops.swiglu(self.w13(self.ffn_norm(h))))
+        h, n = ops.add_norm_train(h, self.wo(a.reshape(B, T, d)), fn.weight, eps=fn.eps)
+        y = self.w2(ops.swiglu(self.w13(n)))
+        return (h, y) if pending else h + y
 
     @torch.no_grad()
     def forward_cached(self, x, k_cache, v_cache, pos, rope, res=None):
@@ -118,10 +123,11 @@ class Llama(tnn.Module):
     def forward(self, idx, targets=None):
         T = idx.shape[1]
         rope = self.rope(T, idx.device)
-        x = ops.embedding(idx, self.tok_embeddings)
+        x, res = ops.embedding(idx, self.tok_embeddings), None
         for blk in self.layers:
-            x = blk(x, rope)
-        logits = self.output(self.norm(x))
+            x, res = blk(x, rope, res, pending=True)
+        _, n = ops.add_norm_train(x, res, self.norm.weight, eps=self.norm.eps)
+        logits = self.output(n)
         if targets is None:
             return logits
         return ops.cross_entropy(logits.reshape(-1, logits.shape[-1]), targets.reshape(-1))

@@ -3,6 +3,10 @@
 * :func:`batch_norm` — training/eval BatchNorm over channels-last activations with fused residual add
   and ReLU (reference ResNet-50 BN ×53, `03_model_parallel.ipynb` raw line 314).
 * :func:`layer_norm`, :func:`rms_norm` — row norms for GPT-2 / Llama-3 (K19, K20).
+* :func:`add_norm_train` — the residual add fused into the following norm, with autograd (training
+  counterpart of the serving :func:`add_norm`): one forward pass writes ``h = x + r`` and ``norm(h)``,
+  and the backward writes ``dh_total = norm_bwd(dn) + dh`` once (no separate add kernels in either
+  direction for the residual stream).
 """
 from __future__ import annotations
 
@@ -132,6 +136,39 @@ def rms_norm(x, weight, eps=1e-6):
     xf = x.float()
     y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * weight.float()
     return y.to(x.dtype)
+
+
+class _AddRowNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r, gamma, beta, eps, rms):
+        h, y, mean, rstd = C().add_rownorm_fwd_train(x.contiguous(), r.contiguous(), gamma, beta, eps, rms)
+        ctx.save_for_backward(h, gamma, mean, rstd)
+        ctx.rms = rms
+        ctx.has_beta = beta is not None
+        return h, y
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        h, gamma, mean, rstd = ctx.saved_tensors
+        if dy is None:  # the normed output is unused: the residual gradient passes straight through
+            return dh, dh, None, None, None, None
+        addend = dh.contiguous() if dh is not None else None
+        dx, dg, db = C().rownorm_bwd(dy.contiguous(), h, gamma, mean, rstd, ctx.rms, addend)
+        return dx, dx, dg.to(gamma.dtype), (db.to(gamma.dtype) if ctx.has_beta else None), None, None
+
+
+def add_norm_train(x, r, weight, bias=None, eps=1e-5, rms=True):
+    """``h = x + r`` and ``norm(h)`` with autograd; ``r=None`` is the plain norm (h = x).  Returns
+    ``(h, normed)``.  GPU bf16: `rownorm.hip:add_rownorm_fwd_kernel` forward, `rownorm_bwd_dx_kernel`
+    with the residual gradient as addend backward."""
+    if r is None:
+        return x, (rms_norm(x, weight, eps) if rms else layer_norm(x, weight, bias, eps))
+    if (x.is_cuda and x.dtype == torch.bfloat16 and r.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16
+            and (bias is None or bias.dtype == torch.bfloat16) and x.shape[-1] % 8 == 0 and x.shape[-1] <= 8192
+            and x.shape == r.shape):
+        return _AddRowNormFn.apply(x, r, weight, None if rms else bias, eps, rms)
+    h = x + r
+    return h, (rms_norm(h, weight, eps) if rms else layer_norm(h, weight, bias, eps))
 
 
 @torch.no_grad()

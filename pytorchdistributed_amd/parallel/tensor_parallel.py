@@ -197,14 +197,18 @@ class TPLlamaBlock(tnn.Module):
         self.w13 = ColumnParallelLinear(torch.cat([gate, up], 0), None, group, sequence_parallel)
         self.w2 = RowParallelLinear(blk.w2.weight[:, rank * f:(rank + 1) * f], None, group, sequence_parallel)
 
-    def forward(self, x, rope):
-        # x: [B, T, d] replicated (or [B, T/tp, d] with sequence parallelism)
-        a_in = self.wqkv(self.attention_norm(x))
+    def forward(self, x, rope, res=None, pending: bool = False):
+        # x: [B, T, d] replicated (or [B, T/tp, d] with sequence parallelism); pending-residual
+        # convention of LlamaBlock.forward (residual adds fused into the RMSNorms)
+        an, fn = self.attention_norm, self.ffn_norm
+        h, n = ops.add_norm_train(x, res, an.weight, eps=an.eps)
+        a_in = self.wqkv(n)
         B, T = a_in.shape[:2]
         qkv = a_in.view(B, T, self.hq + 2 * self.hkv, self.hd)
         a = ops.attention_qkv(qkv, self.hq, self.hkv, causal=True, rope=rope)
-        h = x + self.wo(a.reshape(B, T, self.hq * self.hd))
-        return h + self.w2(ops.swiglu(self.w13(self.ffn_norm(h))))
+        h, n = ops.add_norm_train(h, self.wo(a.reshape(B, T, self.hq * self.hd)), fn.weight, eps=fn.eps)
+        y = self.w2(ops.swiglu(self.w13(n)))
+        return (h, y) if pending else h + y
 
     @torch.no_grad()
     def forward_cached(self, x, k_cache, v_cache, pos, rope, res=None):

@@ -407,6 +407,38 @@ def test_rownorm(rms, D, rows):
         assert rel_err(bg.grad.cpu(), br.grad) < 2e-2
 
 
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("D,rows", [(64, 37), (1024, 2500), (1600, 37), (4096, 300)])
+def test_add_norm_train(rms, D, rows):
+    """Residual add fused into the norm, with autograd: h = x + r and norm(h) forward; backward
+    dx = dr = norm_bwd(dn) + dh (the residual stream's own gradient added in the dx kernel)."""
+    from pytorchdistributed_amd.ops import add_norm_train
+
+    torch.manual_seed(8)
+    x = (torch.randn(rows, D) * 2 + 0.3).to(torch.bfloat16).float()
+    r = torch.randn(rows, D).to(torch.bfloat16).float()
+    g = (torch.rand(D) + 0.5).to(torch.bfloat16).float()
+    b = torch.randn(D).to(torch.bfloat16).float()
+    xr, rr = x.clone().requires_grad_(), r.clone().requires_grad_()
+    gr, br = g.clone().requires_grad_(), b.clone().requires_grad_()
+    h = (xr + rr).to(torch.bfloat16).float()  # the fused kernel rounds h to bf16 like a separate add
+    n = h * torch.rsqrt(h.pow(2).mean(-1, keepdim=True) + 1e-6) * gr if rms else F.layer_norm(h, (D,), gr, br, 1e-5)
+    dh, dn = torch.randn_like(h), torch.randn_like(n)
+    torch.autograd.backward([h, n], [dh, dn])
+    xg, rg = x.to(DEV, torch.bfloat16).requires_grad_(), r.to(DEV, torch.bfloat16).requires_grad_()
+    gg = g.to(DEV, torch.bfloat16).requires_grad_()
+    bg = b.to(DEV, torch.bfloat16).requires_grad_()
+    hg, ng = add_norm_train(xg, rg, gg, None if rms else bg, 1e-6 if rms else 1e-5, rms=rms)
+    torch.autograd.backward([hg, ng], [dh.to(DEV, torch.bfloat16), dn.to(DEV, torch.bfloat16)])
+    assert rel_err(hg.cpu(), h.detach()) < 1e-2
+    assert rel_err(ng.cpu(), n.detach()) < 1e-2
+    assert rel_err(xg.grad.cpu(), xr.grad) < 2e-2
+    assert rel_err(rg.grad.cpu(), rr.grad) < 2e-2
+    assert rel_err(gg.grad.cpu(), gr.grad) < 2e-2
+    if not rms:
+        assert rel_err(bg.grad.cpu(), br.grad) < 2e-2
+
+
 @pytest.mark.parametrize("rows,cols", [(1, 8), (37, 64), (5000, 1024), (300, 1600), (64, 50304), (33, 5)])
 def test_colsum(rows, cols):
     x = torch.randn(rows, cols)
