@@ -113,7 +113,6 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = _gemm_dgrad(dy2, w).reshape(ctx.shape)
-        db_done = False
         if ctx.needs_input_grad[1]:
             target = grad_target(ctx.wparam)
             if target is not None and _streams.enabled() and target.numel() < _SIDE_MAX_NUMEL:
@@ -122,15 +121,14 @@ class _LinearFn(torch.autograd.Function):
                 # of 256x256 output tiles per CU fills the chip by itself; beside other work it only
                 # adds interference (Llama-3-8B FSDP: -2.4 %; GPT-2-medium DDP, 1-16 tiles + split-K:
                 # +9.9 %, profiles/r2_wgrad_stream_transformers.jsonl)
-                tb = grad_target(ctx.bparam) if ctx.has_bias and ctx.needs_input_grad[2] else None
+                # (the bias gradient stays on the compute stream: as a side-stream column sum its
+                # hundreds of memory-bound workgroups delayed the critical-path dgrad GEMMs — GPT-2-medium
+                # 55.7 -> 57.0 ms/step, profiles/r2_gpt2_addnorm_ab.md)
                 with _streams.wgrad_stream(dy2.device, dy2, x2):
                     dw = _gemm_wgrad(dy2, x2, w.dtype, target)
-                    if tb is not None:  # the bias gradient (a column sum of dy) rides along
-                        db = tb.copy_(C().colsum(dy2))
-                        db_done = True
             else:
                 dw = _gemm_wgrad(dy2, x2, w.dtype, target)
-        if ctx.has_bias and ctx.needs_input_grad[2] and not db_done:
+        if ctx.has_bias and ctx.needs_input_grad[2]:
             tb = grad_target(ctx.bparam)
             db = C().colsum(dy2)
             db = tb.copy_(db) if tb is not None else db.to(ctx.bparam.dtype)
