@@ -658,6 +658,135 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd2_kernel(AttnParams p) {
   }
 }
 
+// v3 forward: the K/V LDS images are double-buffered, so one barrier per key tile (v2: two — one
+// before overwriting the single stage, one before reading it).  Iteration j multiplies tile j from
+// stage j&1 while tile j+1 (prefetched into VGPRs during iteration j-1) is written into the other
+// stage and tile j+2 is fetched; the only wait on global memory is for loads issued one whole
+// iteration earlier.  Waves whose queries all precede a tile skip its math but not its barrier.
+template <int D, int QG>
+__global__ void __launch_bounds__(NT, 2) attn_fwd3_kernel(AttnParams p) {
+  constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2, BQW = 64 * QG;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];  // [stage][K row image | V tr image]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int qt = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z;  // heavy causal tiles first
+  const int hk = h / (p.Hq / p.Hkv);
+  const int T = p.T;
+  const int qbase = qt * BQW + w * 16 * QG;
+  const bf16_t* qb = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* vb = p.v + b * p.v_sb + hk * p.v_sh;
+  const int kv_end = p.causal ? min(T, (qt + 1) * BQW) : T;
+  const int ntiles = (kv_end + BKV - 1) / BKV;
+  TileRegs<D> tr;
+  fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, 0, T);
+  mbf16x8 qf[QG][KS];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[qg][ks] = load_frag_global(qb, p.q_st, qbase + 16 * qg + (lane & 15), T, ks, lane);
+  store_tile<D>(tr, smem, nullptr, nullptr, smem + IMG);
+  if (ntiles > 1) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, BKV, T);
+  __syncthreads();
+  const float c = p.scale * LOG2E;
+  float m[QG], l[QG];
+  f32x4 o[QG][DT];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    m[qg] = NEG_BIG;
+    l[qg] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[qg][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int j = 0; j < ntiles; ++j) {
+    const int kv0 = j * BKV;
+    const char* Ks = smem + (j & 1) * 2 * IMG;
+    const char* Vs = Ks + IMG;
+    if (j + 1 < ntiles) {  // stage (j+1)&1 was last read in iteration j-1, before its barrier
+      char* nk = smem + ((j + 1) & 1) * 2 * IMG;
+      store_tile<D>(tr, nk, nullptr, nullptr, nk + IMG);
+      if (j + 2 < ntiles) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, kv0 + 2 * BKV, T);
+    }
+    if (!(p.causal && kv0 > qbase + 16 * QG - 1)) {
+      f32x4 s[QG][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) s[qg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const mbf16x8 kf = frag_row<D>(Ks, 16 * t, ks, lane);
+#pragma unroll
+          for (int qg = 0; qg < QG; ++qg) s[qg][t] = mfma(kf, qf[qg][ks], s[qg][t]);
+        }
+      }
+      const bool need_mask = kv0 + BKV > T || (p.causal && kv0 + BKV - 1 > qbase);
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) {
+        const int qrow = qbase + 16 * qg + (lane & 15);
+        float mx = NEG_BIG;
+        if (need_mask) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int kv = kv0 + 16 * t + 4 * g + r;
+              if (kv >= T || (p.causal && kv > qrow)) s[qg][t][r] = -INFINITY;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[qg][t][r]);
+        const float m_new = fmaxf(m[qg], max_x16_x32(mx));
+        const float alpha = fast_exp2((m[qg] - m_new) * c);
+        const float mc = m_new * c;
+        float rs = 0.f;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float e = fast_exp2(fmaf(s[qg][t][r], c, -mc));
+            s[qg][t][r] = e;
+            rs += e;
+          }
+        l[qg] = fmaf(l[qg], alpha, rs);
+        m[qg] = m_new;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[qg][dt] *= alpha;
+      }
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        mbf16x8 pf[QG];
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) pf[qg] = pack_p(s[qg][2 * cc], s[qg][2 * cc + 1]);
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const mbf16x8 vf = frag_tr<D>(Vs, 32 * cc, 16 * dt, lane);
+#pragma unroll
+          for (int qg = 0; qg < QG; ++qg) o[qg][dt] = mfma(vf, pf[qg], o[qg][dt]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    const int qrow = qbase + 16 * qg + (lane & 15);
+    const float lsum = sum_x16_x32(l[qg]);
+    if (qrow >= T) continue;
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16_t* ob = p.o + b * p.o_sb + (int64_t)qrow * p.o_st + h * p.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      u16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[qg][dt][r] * inv);
+      *reinterpret_cast<u16x4*>(ob + 16 * dt + 4 * g) = v;
+    }
+    if (g == 0) p.lse[((int64_t)b * p.Hq + h) * T + qrow] = (m[qg] * c + log2f(lsum)) / LOG2E;
+  }
+}
+
 // dQ, query-stationary, prefetched K/V tiles; QG query groups of 16 rows per wave (query tile =
 // 64 * QG): every K / V fragment read from LDS feeds QG MFMAs.
 template <int D, int QG>
@@ -953,15 +1082,25 @@ __global__ void __launch_bounds__(NT) attn_dkv_reduce_kernel(AttnParams p) {
 }
 
 // query groups per wave of the forward kernel (PDA_ATTN_FWD_QG=1|2 overrides).  Measured
-// (profiles/r1_attn_microbench_v3.jsonl): D = 64 293 vs 273 TFLOP/s with 2 groups; D = 128 ties
-// (357 / 360), and 1 group keeps the D = 128 kernel free of spills.
+// (profiles/r1_attn_microbench_v3.jsonl, profiles/r2_attn_fwd3.jsonl): 2 groups for both head dims —
+// D = 64 287 vs 259 TFLOP/s; D = 128 with the double-buffered v3 kernel 406 vs 383 (v2: a tie).
 int attn_fwd_groups(int D) {
   static const int env = [] {
     const char* e = getenv("PDA_ATTN_FWD_QG");
     return e ? atoi(e) : 0;
   }();
   if (env == 1 || env == 2) return env;
-  return D == 128 ? 1 : 2;
+  (void)D;
+  return 2;
+}
+
+// forward kernel generation: 3 (default) double-buffered K/V, one barrier per tile; 2 single stage
+int attn_fwd_version() {
+  static const int v = [] {
+    const char* e = getenv("PDA_ATTN_FWD");
+    return e ? atoi(e) : 3;
+  }();
+  return v;
 }
 
 }  // namespace
@@ -972,12 +1111,22 @@ hipError_t attention_fwd(const AttnParams& p, hipStream_t st) {
   if (p.rope_cos == nullptr) {
     const int qg = attn_fwd_groups(p.D);
     dim3 grid((p.T + 64 * qg - 1) / (64 * qg), p.Hq, p.B);
+    if (attn_fwd_version() == 2) {
+      if (p.D == 128) {
+        if (qg == 1) attn_fwd2_kernel<128, 1><<<grid, NT, 0, st>>>(p);
+        else attn_fwd2_kernel<128, 2><<<grid, NT, 0, st>>>(p);
+      } else {
+        if (qg == 1) attn_fwd2_kernel<64, 1><<<grid, NT, 0, st>>>(p);
+        else attn_fwd2_kernel<64, 2><<<grid, NT, 0, st>>>(p);
+      }
+      return hipGetLastError();
+    }
     if (p.D == 128) {
-      if (qg == 1) attn_fwd2_kernel<128, 1><<<grid, NT, 0, st>>>(p);
-      else attn_fwd2_kernel<128, 2><<<grid, NT, 0, st>>>(p);
+      if (qg == 1) attn_fwd3_kernel<128, 1><<<grid, NT, 0, st>>>(p);
+      else attn_fwd3_kernel<128, 2><<<grid, NT, 0, st>>>(p);
     } else {
-      if (qg == 1) attn_fwd2_kernel<64, 1><<<grid, NT, 0, st>>>(p);
-      else attn_fwd2_kernel<64, 2><<<grid, NT, 0, st>>>(p);
+      if (qg == 1) attn_fwd3_kernel<64, 1><<<grid, NT, 0, st>>>(p);
+      else attn_fwd3_kernel<64, 2><<<grid, NT, 0, st>>>(p);
     }
     return hipGetLastError();
   }
