@@ -789,13 +789,12 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd3_kernel(AttnParams p) {
 
 // dQ, query-stationary, prefetched K/V tiles; QG query groups of 16 rows per wave (query tile =
 // 64 * QG): every K / V fragment read from LDS feeds QG MFMAs.
-template <int D, int QG>
+// DB: K/V images double-buffered (one barrier per key tile, as attn_fwd3_kernel) at twice the LDS.
+template <int D, int QG, bool DB = false>
 __global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
   constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2, BQW = BQ * QG;
-  __shared__ __attribute__((aligned(16))) char smem[3 * IMG];
-  char* Kr = smem;
-  char* Kt = smem + IMG;
-  char* Vr = smem + 2 * IMG;
+  constexpr int STAGE = 3 * IMG;
+  __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * STAGE];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int qt = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int hk = h / (p.Hq / p.Hkv);
@@ -829,13 +828,33 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
   const int ntiles = (kv_end + BKV - 1) / BKV;
   TileRegs<D> tr;
   fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, 0, T);
+  if constexpr (DB) {
+    store_tile<D>(tr, smem, smem + IMG, smem + 2 * IMG, nullptr);
+    if (ntiles > 1) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, BKV, T);
+    __syncthreads();
+  }
   for (int j = 0; j < ntiles; ++j) {
     const int kv0 = j * BKV;
-    __syncthreads();
-    store_tile<D>(tr, Kr, Kt, Vr, nullptr);
-    __syncthreads();
-    if (j + 1 < ntiles) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, kv0 + BKV, T);
-    if (p.causal && kv0 > qbase + 16 * QG - 1) continue;  // every key of this tile is in this wave's future
+    char* Kr = smem + (DB ? (j & 1) * STAGE : 0);
+    char* Kt = Kr + IMG;
+    char* Vr = Kr + 2 * IMG;
+    if constexpr (DB) {
+      if (j + 1 < ntiles) {  // the other stage was last read before the previous barrier
+        char* nx = smem + ((j + 1) & 1) * STAGE;
+        store_tile<D>(tr, nx, nx + IMG, nx + 2 * IMG, nullptr);
+        if (j + 2 < ntiles) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, kv0 + 2 * BKV, T);
+      }
+    } else {
+      __syncthreads();
+      store_tile<D>(tr, Kr, Kt, Vr, nullptr);
+      __syncthreads();
+      if (j + 1 < ntiles) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, kv0 + BKV, T);
+    }
+    // every key of this tile is in this wave's future (DB: skip the math, not the barrier)
+    if (p.causal && kv0 > qbase + 16 * QG - 1) {
+      if constexpr (DB) __syncthreads();
+      continue;
+    }
     f32x4 s[QG][4], dp[QG][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -881,6 +900,7 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
 #pragma unroll
         for (int qg = 0; qg < QG; ++qg) dq[qg][dt] = mfma(ktf, sf[cc][qg], dq[qg][dt]);
       }
+    if constexpr (DB) __syncthreads();
   }
 #pragma unroll
   for (int qg = 0; qg < QG; ++qg) {
@@ -901,16 +921,11 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
 // fp32 partials [2][B][Hq][T][D] summed over the group by attn_dkv_reduce_kernel.
 // KG key groups of 16 per wave (key tile = 64 * KG): every Q / dO fragment read from LDS and every
 // transposed Q / dO fragment feeds KG MFMAs, and each staged Q / dO tile serves 64 * KG keys.
-template <int D, int KG>
+template <int D, int KG, bool DB = false>
 __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
   constexpr int KS = D / 32, DT = D / 16, IMG = BQ * D * 2, BK = BKV * KG;
-  __shared__ __attribute__((aligned(16))) char smem[4 * IMG + 2 * BQ * 4];
-  char* Qr = smem;
-  char* Qt = smem + IMG;
-  char* Dr = smem + 2 * IMG;
-  char* Dt = smem + 3 * IMG;
-  float* s_lse = reinterpret_cast<float*>(smem + 4 * IMG);
-  float* s_dl = s_lse + BQ;
+  constexpr int STAGE = 4 * IMG + 2 * BQ * 4;  // Q row / Q tr / dO row / dO tr images + lse / delta
+  __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * STAGE];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int kt = blockIdx.x, hq = blockIdx.y, b = blockIdx.z;
   const int T = p.T, G = p.Hq / p.Hkv, hk = hq / G;
@@ -945,24 +960,58 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
       nd = q < T ? dlt[q] : 0.f;
     }
   };
+  auto put = [&](char* st) {  // staged registers -> one stage's images and stats
+    store_tile<D>(tr, st, st + IMG, st + 2 * IMG, st + 3 * IMG);
+    if (threadIdx.x < BQ) {
+      float* sl = reinterpret_cast<float*>(st + 4 * IMG);
+      sl[threadIdx.x] = nl;
+      sl[BQ + threadIdx.x] = nd;
+    }
+  };
   if (q_begin < T) {
     fetch_tile<D>(tr, qb, p.q_st, dob, p.do_st, q_begin, T);
     fetch_stats(q_begin);
   }
-  for (int q0 = q_begin; q0 < T; q0 += BQ) {
-    __syncthreads();
-    store_tile<D>(tr, Qr, Qt, Dr, Dt);
-    if (threadIdx.x < BQ) {
-      s_lse[threadIdx.x] = nl;
-      s_dl[threadIdx.x] = nd;
+  if constexpr (DB) {
+    if (q_begin < T) {
+      put(smem);
+      if (q_begin + BQ < T) {
+        fetch_tile<D>(tr, qb, p.q_st, dob, p.do_st, q_begin + BQ, T);
+        fetch_stats(q_begin + BQ);
+      }
     }
     __syncthreads();
-    if (q0 + BQ < T) {
-      fetch_tile<D>(tr, qb, p.q_st, dob, p.do_st, q0 + BQ, T);
-      fetch_stats(q0 + BQ);
+  }
+  for (int q0 = q_begin, j = 0; q0 < T; q0 += BQ, ++j) {
+    char* st = smem + (DB ? (j & 1) * STAGE : 0);
+    const char* Qr = st;
+    const char* Qt = st + IMG;
+    const char* Dr = st + 2 * IMG;
+    const char* Dt = st + 3 * IMG;
+    const float* s_lse = reinterpret_cast<const float*>(st + 4 * IMG);
+    const float* s_dl = s_lse + BQ;
+    if constexpr (DB) {
+      if (q0 + BQ < T) {  // the other stage was last read before the previous barrier
+        put(smem + ((j + 1) & 1) * STAGE);
+        if (q0 + 2 * BQ < T) {
+          fetch_tile<D>(tr, qb, p.q_st, dob, p.do_st, q0 + 2 * BQ, T);
+          fetch_stats(q0 + 2 * BQ);
+        }
+      }
+    } else {
+      __syncthreads();
+      put(st);
+      __syncthreads();
+      if (q0 + BQ < T) {
+        fetch_tile<D>(tr, qb, p.q_st, dob, p.do_st, q0 + BQ, T);
+        fetch_stats(q0 + BQ);
+      }
     }
     // every query of this tile is before all of this wave's keys: nothing to add (wave-uniform)
-    if (p.causal && q0 + BQ - 1 < kvbase) continue;
+    if (p.causal && q0 + BQ - 1 < kvbase) {
+      if constexpr (DB) __syncthreads();
+      continue;
+    }
     f32x4 s[KG][4], dp[KG][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -1019,6 +1068,7 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
         }
       }
     }
+    if constexpr (DB) __syncthreads();
   }
 #pragma unroll
   for (int kg = 0; kg < KG; ++kg) {
@@ -1153,12 +1203,22 @@ hipError_t attention_bwd(const AttnParams& p, hipStream_t st) {
   if (p.rope_cos == nullptr) {
     dim3 gq2((p.T + 2 * BQ - 1) / (2 * BQ), p.Hq, p.B);
     if (p.Hq > p.Hkv && p.dkv_part == nullptr) return hipErrorInvalidValue;
+    static const int db = [] {  // bit 0: dQ kernel double-buffered, bit 1: dK/dV kernel
+      const char* e = getenv("PDA_ATTN_BWD_DB");
+      return e ? atoi(e) : 0;
+    }();
     if (p.D == 128) {  // (two key groups per wave would exceed the 256-VGPR budget at D = 128)
-      attn_bwd_dq2_kernel<128, 1><<<gq, NT, 0, st>>>(p);
-      attn_bwd_dkdv2_kernel<128, 1><<<dim3((p.T + BKV - 1) / BKV, p.Hq, p.B), NT, 0, st>>>(p);
+      if (db & 1) attn_bwd_dq2_kernel<128, 1, true><<<gq, NT, 0, st>>>(p);
+      else attn_bwd_dq2_kernel<128, 1><<<gq, NT, 0, st>>>(p);
+      const dim3 gk((p.T + BKV - 1) / BKV, p.Hq, p.B);
+      if (db & 2) attn_bwd_dkdv2_kernel<128, 1, true><<<gk, NT, 0, st>>>(p);
+      else attn_bwd_dkdv2_kernel<128, 1><<<gk, NT, 0, st>>>(p);
     } else {
-      attn_bwd_dq2_kernel<64, 2><<<gq2, NT, 0, st>>>(p);
-      attn_bwd_dkdv2_kernel<64, 2><<<dim3((p.T + 2 * BKV - 1) / (2 * BKV), p.Hq, p.B), NT, 0, st>>>(p);
+      if (db & 1) attn_bwd_dq2_kernel<64, 2, true><<<gq2, NT, 0, st>>>(p);
+      else attn_bwd_dq2_kernel<64, 2><<<gq2, NT, 0, st>>>(p);
+      const dim3 gk((p.T + 2 * BKV - 1) / (2 * BKV), p.Hq, p.B);
+      if (db & 2) attn_bwd_dkdv2_kernel<64, 2, true><<<gk, NT, 0, st>>>(p);
+      else attn_bwd_dkdv2_kernel<64, 2><<<gk, NT, 0, st>>>(p);
     }
     PDA_CHECK_HIP(hipGetLastError());
     if (p.Hq > p.Hkv) {
