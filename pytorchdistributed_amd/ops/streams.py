@@ -29,6 +29,7 @@ import torch
 
 _streams: Dict[int, torch.cuda.Stream] = {}
 _join_pending: Dict[int, bool] = {}
+_join_task: Dict[int, int] = {}  # autograd graph task whose final callback joins the device's side stream
 _enabled_override = None
 
 
@@ -55,9 +56,17 @@ def side_stream(device: torch.device) -> torch.cuda.Stream:
 
 def _join(idx: int) -> None:
     _join_pending[idx] = False
+    _join_task.pop(idx, None)
     s = _streams.get(idx)
     if s is not None:
         torch.cuda.current_stream(idx).wait_stream(s)
+
+
+def join(device: torch.device) -> None:
+    """Make the current stream wait for the device's side stream now (also what the autograd final
+    callback does).  Needed only after a backward that raised: its queued callbacks never ran."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    _join(idx)
 
 
 def active(device: torch.device) -> bool:
@@ -78,8 +87,12 @@ def wgrad_stream(device: torch.device, *tensors: torch.Tensor):
     for t in tensors:
         if t is not None:
             t.record_stream(s)
-    if not _join_pending.get(idx, False):
+    # one join per backward pass: keyed on the autograd graph task, so a backward that raised (its
+    # callbacks never run) cannot leave a stale "join pending" that stops the next pass from queueing
+    task = torch._C._current_graph_task_id()
+    if not _join_pending.get(idx, False) or _join_task.get(idx) != task:
         _join_pending[idx] = True
+        _join_task[idx] = task
         torch.autograd.Variable._execution_engine.queue_callback(lambda: _join(idx))
     with torch.cuda.stream(s):
         yield s

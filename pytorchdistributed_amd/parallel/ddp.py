@@ -120,6 +120,7 @@ class DistributedDataParallel(tnn.Module):
         # ---- autograd hooks
         self._works: List = []
         self._callback_queued = False
+        self._callback_task = -1
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
         self.reducer.prepare()
         # ---- optional IPC all-reduce over xGMI for buckets (PDA_ALLREDUCE=ipc|oneshot|twoshot, single node)
@@ -220,8 +221,17 @@ class DistributedDataParallel(tnn.Module):
             if p.grad is not None and p.grad.data_ptr() != view.data_ptr():
                 view.copy_(p.grad)
                 p.grad = view
-            if not self._callback_queued:
+            task = torch._C._current_graph_task_id()
+            if not self._callback_queued or self._callback_task != task:
+                if self._callback_queued:
+                    # the previous backward raised before its final callback ran: start this pass clean
+                    self._works.clear()
+                    self._sweep_tickets(force=True)
+                    for grp in self.groups.values():
+                        grp.pending_comm = 0
+                    self.reducer.prepare()
                 self._callback_queued = True
+                self._callback_task = task
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
             for b in self.reducer.mark_ready(i):
                 self._launch(b)

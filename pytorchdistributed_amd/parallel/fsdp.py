@@ -238,6 +238,7 @@ class FullyShardedDataParallel(tnn.Module):
                 u.module.register_forward_hook(self._make_post_fwd(u))
         self._pending_rs = None
         self._callback_queued = False
+        self._callback_task = -1
         # ---- optional direct xGMI collectives (PDA_FSDP_COMM=ipc, one node): the unit all-gathers pull
         # every peer's shard over its own link and the gradient reduce-scatters reduce chunk `rank` of
         # every peer's buffer (csrc/kernels/xgmi.hip), on one ordered side stream; RCCL by default
@@ -299,6 +300,22 @@ class FullyShardedDataParallel(tnn.Module):
             return out
         return hook
 
+    def _queue_final(self):
+        """One final callback per backward pass, keyed on the autograd graph task (a backward that
+        raised never ran its callback: the next pass must queue its own and start clean)."""
+        task = torch._C._current_graph_task_id()
+        if self._callback_queued and self._callback_task == task:
+            return
+        if self._callback_queued:  # aborted pass: drop its partial arrivals / pending reduce-scatter
+            self._pending_rs = None
+            for u in self.units:
+                u.arrived = 0
+                for leaf in u.leaves:
+                    leaf._pda_seen = False
+        self._callback_queued = True
+        self._callback_task = task
+        torch.autograd.Variable._execution_engine.queue_callback(self._post_backward_final)
+
     def _pre_backward(self, u: _Unit, g):
         if not u.gathered:
             u.start_gather()
@@ -307,9 +324,7 @@ class FullyShardedDataParallel(tnn.Module):
             nxt = self._next_in_order(u, backward=True)
             if nxt is not None and nxt is not self.root_unit:
                 nxt.start_gather()
-        if not self._callback_queued:
-            self._callback_queued = True
-            torch.autograd.Variable._execution_engine.queue_callback(self._post_backward_final)
+        self._queue_final()
         return g
 
     # ------------------------------------------------------------ gradient reduce-scatter
@@ -334,9 +349,7 @@ class FullyShardedDataParallel(tnn.Module):
                                                  producers, [out]), out)
                 if u is not self.root_unit:
                     u.reshard()
-                if not self._callback_queued:
-                    self._callback_queued = True
-                    torch.autograd.Variable._execution_engine.queue_callback(self._post_backward_final)
+                self._queue_final()
                 return
             if len(producers) > 1:
                 if self.nccl:
@@ -354,9 +367,7 @@ class FullyShardedDataParallel(tnn.Module):
         self._pending_rs = (u, work, out)
         if u is not self.root_unit:
             u.reshard()
-        if not self._callback_queued:
-            self._callback_queued = True
-            torch.autograd.Variable._execution_engine.queue_callback(self._post_backward_final)
+        self._queue_final()
 
     def _finish_rs(self):
         if self._pending_rs is None:

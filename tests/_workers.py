@@ -23,8 +23,20 @@ def collectives(rank, world, outdir):
     pd.destroy_process_group()
 
 
-def ddp_mlp(rank, world, backend, outdir, steps):
-    """DDP on an MLP: after `steps` SGD steps the params must equal single-process full-batch training."""
+class _RaiseInBackward(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        raise RuntimeError("injected backward failure")
+
+
+def ddp_mlp(rank, world, backend, outdir, steps, abort_first=False):
+    """DDP on an MLP: after `steps` SGD steps the params must equal single-process full-batch training.
+    ``abort_first``: before the first real step, a backward raises halfway (after the later layers'
+    gradient hooks already launched their buckets); DDP must start the next pass clean."""
     import pytorchdistributed_amd.distributed as pd
     from pytorchdistributed_amd.models.mlp import MnistMLP
     from pytorchdistributed_amd.optim import SGD
@@ -38,6 +50,16 @@ def ddp_mlp(rank, world, backend, outdir, steps):
     g = torch.Generator().manual_seed(7)
     X = torch.randn(steps, world * 4, 16, generator=g)
     Y = torch.randint(0, 10, (steps, world * 4), generator=g)
+    if abort_first:
+        layer = [m for m in model.modules() if isinstance(m, torch.nn.Module) and list(m.parameters(recurse=False))][1]
+        h = layer.register_forward_hook(lambda m, i, o: _RaiseInBackward.apply(o))
+        opt.zero_grad()
+        try:
+            F.cross_entropy(ddp(X[0, rank * 4:(rank + 1) * 4]), Y[0, rank * 4:(rank + 1) * 4]).backward()
+            raise AssertionError("the injected failure did not raise")
+        except RuntimeError as e:
+            assert "injected backward failure" in str(e)
+        h.remove()
     for s in range(steps):
         xs = X[s, rank * 4:(rank + 1) * 4]
         ys = Y[s, rank * 4:(rank + 1) * 4]

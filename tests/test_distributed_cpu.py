@@ -24,10 +24,11 @@ def test_collectives_ring_and_gloo(tmp_path, world):
         assert torch.allclose(d["g"], torch.tensor([[q, q * 10.0] for q in range(world)]).flatten())
 
 
-@pytest.mark.parametrize("backend", ["gloo", "ring"])
-def test_ddp_matches_single_process(tmp_path, backend):
+@pytest.mark.parametrize("backend,abort_first", [("gloo", False), ("ring", False), ("gloo", True)])
+def test_ddp_matches_single_process(tmp_path, backend, abort_first):
+    """abort_first: a backward that raised halfway (buckets already launched) precedes training."""
     world, steps = 2, 3
-    spawn(_workers.ddp_mlp, args=(world, backend, str(tmp_path), steps), nprocs=world, timeout=120)
+    spawn(_workers.ddp_mlp, args=(world, backend, str(tmp_path), steps, abort_first), nprocs=world, timeout=120)
     s0 = torch.load(tmp_path / "0.pt", weights_only=True)
     s1 = torch.load(tmp_path / "1.pt", weights_only=True)
     meta = torch.load(tmp_path / "meta0.pt", weights_only=True)

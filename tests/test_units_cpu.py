@@ -310,3 +310,41 @@ def test_xgmi_tuning_table_from_sweep(tmp_path, monkeypatch):
     assert xgmi.load_table(4, str(p)) is None  # table of another world size
     monkeypatch.setenv("PDA_XGMI_TUNING", str(p))
     assert xgmi.load_table(8) == tab["entries"]
+
+
+def test_side_stream_join_is_per_backward_pass(monkeypatch):
+    """ops/streams.py queues one join callback per autograd graph task: a backward that raised (its
+    final callbacks never run) must not stop the next backward from queueing its own join."""
+    import torch
+
+    from pytorchdistributed_amd.ops import streams
+
+    queued = []
+    monkeypatch.setattr(streams, "side_stream", lambda device: None)
+
+    class _Eng:
+        @staticmethod
+        def queue_callback(cb):
+            queued.append(cb)
+
+    monkeypatch.setattr(torch.autograd.Variable, "_execution_engine", _Eng)
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda idx=None: None)
+    monkeypatch.setattr(torch.cuda, "stream", lambda s: __import__("contextlib").nullcontext())
+
+    class _S:
+        def wait_stream(self, other):
+            pass
+
+    monkeypatch.setattr(streams, "side_stream", lambda device: _S())
+    dev = torch.device("cuda", 0)
+    ids = iter([5, 5, 6])
+    monkeypatch.setattr(torch._C, "_current_graph_task_id", lambda: next(ids))
+    for _ in range(2):  # same graph task: one callback
+        with streams.wgrad_stream(dev):
+            pass
+    assert len(queued) == 1
+    with streams.wgrad_stream(dev):  # a new task although the first never joined
+        pass
+    assert len(queued) == 2
+    streams._join_pending.clear()
+    streams._join_task.clear()
