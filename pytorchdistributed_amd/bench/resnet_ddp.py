@@ -47,7 +47,11 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("PDA_BENCH_BATCH", "256")),
+    # per-GPU batch: 512 uses the 288 GB of an MI355X for throughput (bigger GEMM grids — the 14^2 / 7^2
+    # convs' tile rounds quantise better — and half the per-image launch / epilogue overhead); measured
+    # on one MI355X (profiles/r2_resnet50_batch_sweep.jsonl): 256 -> 9.94k, 384 -> 10.25k,
+    # 512 -> 10.68k, 640 -> 11.06k, 768 -> 10.88k img/s.  --batch 256 reproduces the round-1 setting.
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("PDA_BENCH_BATCH", "512")),
                     help="per-GPU batch")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=None)
@@ -56,7 +60,12 @@ def main(argv=None):
     if device.type == "cpu":  # plumbing-only run on a machine without a GPU
         a.batch, a.image = min(a.batch, 2), min(a.image, 64)
     _, _, step = build(a.batch, a.image, device, rank, bucket_mb=a.bucket_mb)
-    secs = timed(step, a.steps, a.warmup)
+    losses = []
+    secs = timed(lambda: losses.append(step()), a.steps, a.warmup)
+    # (after the timed window) a benchmark that diverged would be measuring garbage
+    last = float(losses[-1].item())
+    if last != last or abs(last) == float("inf"):
+        raise SystemExit(f"non-finite training loss {last} in the benchmark run")
     ms = secs / a.steps * 1e3
     imgs = a.batch * world * a.steps / secs
     emit({
@@ -67,8 +76,10 @@ def main(argv=None):
         "config": {"model": "resnet50", "global_batch": a.batch * world, "per_gpu_batch": a.batch,
                    "image_size": a.image, "seq_len": None, "parallelism": f"dp{world}",
                    "optimizer": "SGD(momentum=0.9, wd=5e-5), fp32 master weights"},
-        "notes": "reference publishes no number for this metric (BASELINE.json published={}); NB03 parity "
-                 "numbers are produced by pytorchdistributed_amd.bench.nb03",
+        "final_loss": round(last, 4),
+        "notes": "reference publishes no number for this metric (BASELINE.json published={}); per-GPU batch "
+                 "512 (throughput-optimal power of two on 288 GB HBM; --batch 256 gives the round-1 "
+                 "setting); NB03 parity numbers are produced by pytorchdistributed_amd.bench.nb03",
     }, rank)
     teardown()
 
