@@ -292,62 +292,124 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16_t* __rest
   }
 }
 
-// Register-table variant, used when the grid stride is a multiple of C/8 (every ResNet shape: C is a
-// power of two <= 2048 and the stride a multiple of 256 vectors): a lane's 8-channel group never
-// changes, so its scale/shift live in registers — no LDS table, no per-vector 64-bit modulo, no LDS
-// bank conflicts (the LDS variant's lanes read coefficients 32 B apart: 8-way conflicts) — and four
-// vectors (4-8 loads) are kept in flight per lane.
-template <bool RES, bool RELU>
-__device__ __forceinline__ void bn_apply_reg(const float (&xv)[8], const float (&rv)[8], const float (&sc)[8],
-                                             const float (&sh)[8], bf16_t* __restrict__ y,
-                                             uint8_t* __restrict__ bits, int64_t v) {
-  float a[8];
+// Wave-contiguous register-coefficient variant (every ResNet shape).  One wave iteration covers 256
+// consecutive 8-channel vectors: four coalesced 1-KB instructions per tensor, and the 256 ReLU-mask
+// bytes of the iteration leave as ONE 4-byte store per lane (regrouped with four shuffles) instead of
+// 256 one-byte stores — the byte stores cost the BN+residual+ReLU apply 15-20 % of its time on the
+// ResNet-50 bs512 shapes (4.3-4.7 -> 5.3-5.6 TB/s, tools/bnlab/apply_lab.hip).  Outputs are written
+// with nontemporal stores (they are next read by another kernel, not this one: +2-3 %).  A lane's
+// coefficients live in registers: its channel group is fixed when 64 % cv == 0 and cycles through
+// NS = cv / 64 groups when cv is a multiple of 64 (up to 4: C = 2048).
+constexpr int kWaveVec = 256;  // vectors per wave iteration
+
+inline int wave_sets(int cv) {
+  if (cv <= 64) return 64 % cv == 0 ? 1 : 0;
+  return (cv % 64 == 0 && cv / 64 <= 4) ? cv / 64 : 0;
+}
+inline int wave_grid(int64_t nvec) {
+  int64_t g = (nvec + kWaveVec * (kThreads / 64) - 1) / (kWaveVec * (kThreads / 64));
+  if (g > 2048) g = 2048;
+  return g < 1 ? 1 : (int)g;
+}
+
+__device__ __forceinline__ void store8_nt(bf16_t* p, const float (&v)[8]) {
+  u16x8 r;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) a[j] = fmaf(xv[j], sc[j], sh[j]) + (RES ? rv[j] : 0.f);
-  if (RELU) {
-    uint32_t m = 0;
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(v[j]);
+  __builtin_nontemporal_store(r, reinterpret_cast<u16x8*>(p));
+}
+
+// mask bytes m_u of vectors base + 64u + lane (u < 4, packed w = m_0 | m_1 << 8 | ...) -> the 4-byte
+// word of vectors base + 4 lane .. 4 lane + 3 (lane l reads byte l >> 4 of lanes 4l .. 4l + 3 mod 64)
+__device__ __forceinline__ uint32_t mask_words_out(uint32_t w, int lane) {
+  uint32_t out = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      m |= (a[j] > 0.f ? 1u : 0u) << j;
-      a[j] = fmaxf(a[j], 0.f);
-    }
-    if (bits) bits[v] = (uint8_t)m;
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t t = (uint32_t)__shfl((int)w, (4 * lane + k) & 63, 64);
+    out |= ((t >> (8 * (lane >> 4))) & 0xFFu) << (8 * k);
   }
-  store8(y + v * 8, a);
+  return out;
+}
+// inverse: lane l holds the word of vectors base + 4l .. 4l + 3; returns byte u of vector 64u + lane
+__device__ __forceinline__ uint32_t mask_words_in(uint32_t word, int lane) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const uint32_t t = (uint32_t)__shfl((int)word, 16 * u + (lane >> 2), 64);
+    w |= ((t >> (8 * (lane & 3))) & 0xFFu) << (8 * u);
+  }
+  return w;
 }
 
 template <bool RES, bool RELU>
-__global__ void __launch_bounds__(kThreads) bn_apply_reg_kernel(const bf16_t* __restrict__ x,
-                                                                const bf16_t* __restrict__ res,
-                                                                bf16_t* __restrict__ y, int64_t M, int C,
-                                                                const float* __restrict__ scale,
-                                                                const float* __restrict__ shift,
-                                                                uint8_t* __restrict__ bits) {
-  const int cv = C / 8;
-  const int64_t nvec = M * cv;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int c0 = (int)(v % cv) * 8;  // fixed for this lane (stride % cv == 0)
-  float sc[8], sh[8];
-  load8(scale + c0, sc);
-  load8(shift + c0, sh);
-  constexpr int U = 4;
-  for (; v + (U - 1) * stride < nvec; v += U * stride) {
-    float a[U][8], r[U][8];
+__device__ __forceinline__ uint32_t bn_apply8(float (&a)[8], const float (&xv)[8], const float (&rv)[8],
+                                              const float (&sc)[8], const float (&sh)[8]) {
+  uint32_t m = 0;
 #pragma unroll
-    for (int u = 0; u < U; ++u) load8(x + (v + u * stride) * 8, a[u]);
+  for (int j = 0; j < 8; ++j) {
+    a[j] = fmaf(xv[j], sc[j], sh[j]) + (RES ? rv[j] : 0.f);
+    if (RELU) {
+      m |= (a[j] > 0.f ? 1u : 0u) << j;
+      a[j] = fmaxf(a[j], 0.f);
+    }
+  }
+  return m;
+}
+
+template <bool RES, bool RELU, int NS>
+__global__ void __launch_bounds__(kThreads) bn_apply_wave_kernel(const bf16_t* __restrict__ x,
+                                                                 const bf16_t* __restrict__ res,
+                                                                 bf16_t* __restrict__ y, int64_t M, int C,
+                                                                 const float* __restrict__ scale,
+                                                                 const float* __restrict__ shift,
+                                                                 uint8_t* __restrict__ bits) {
+  const int cv = C / 8, lane = threadIdx.x & 63;
+  const int64_t nvec = M * cv;
+  const int64_t tw = (int64_t)gridDim.x * (kThreads / 64);
+  float sc[NS][8], sh[NS][8];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int c0 = ((64 * s + lane) % cv) * 8;
+    load8(scale + c0, sc[s]);
+    load8(shift + c0, sh[s]);
+  }
+  int64_t base = ((int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * kWaveVec;
+  for (; base + kWaveVec <= nvec; base += tw * kWaveVec) {
+    u16x8 xa[4], ra[4];  // loads kept packed until used (register budget: 4 vectors x 2 tensors in flight)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) xa[u] = *reinterpret_cast<const u16x8*>(x + (base + 64 * u + lane) * 8);
     if (RES) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) load8(res + (v + u * stride) * 8, r[u]);
+      for (int u = 0; u < 4; ++u) ra[u] = *reinterpret_cast<const u16x8*>(res + (base + 64 * u + lane) * 8);
     }
+    uint32_t w = 0;
 #pragma unroll
-    for (int u = 0; u < U; ++u) bn_apply_reg<RES, RELU>(a[u], r[u], sc, sh, y, bits, v + u * stride);
+    for (int u = 0; u < 4; ++u) {
+      float o[8], a[8], r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a[j] = bf2f(xa[u][j]);
+        r[j] = RES ? bf2f(ra[u][j]) : 0.f;
+      }
+      w |= bn_apply8<RES, RELU>(o, a, r, sc[u % NS], sh[u % NS]) << (8 * u);
+      store8_nt(y + (base + 64 * u + lane) * 8, o);
+    }
+    if (RELU && bits) {
+      const uint32_t out = mask_words_out(w, lane);
+      __builtin_nontemporal_store(out, reinterpret_cast<uint32_t*>(bits + base) + lane);
+    }
   }
-  for (; v < nvec; v += stride) {
-    float a0[8], r0[8];
-    load8(x + v * 8, a0);
-    if (RES) load8(res + v * 8, r0);
-    bn_apply_reg<RES, RELU>(a0, r0, sc, sh, y, bits, v);
+  // the last partial iteration (nvec % 256 vectors, one wave): a byte per vector
+  for (int64_t v = base + lane; base < nvec && v < nvec; v += 64) {
+    const int c0 = (int)(v % cv) * 8;
+    float s1[8], h1[8], a[8], r[8], o[8];
+    load8(scale + c0, s1);
+    load8(shift + c0, h1);
+    load8(x + v * 8, a);
+    if (RES) load8(res + v * 8, r);
+    const uint32_t m = bn_apply8<RES, RELU>(o, a, r, s1, h1);
+    if (RELU && bits) bits[v] = (uint8_t)m;
+    store8(y + v * 8, o);
   }
 }
 
@@ -516,63 +578,94 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const bf16_t* __
   }
 }
 
-// Register-coefficient variant of the backward apply (same condition as bn_apply_reg_kernel): the
-// lane's A, B, Cc (and MASK-2 scale/shift) for its fixed 8 channels are loaded once into registers.
-template <int MASK, bool DRES>
-__global__ void __launch_bounds__(kThreads) bn_bwd_apply_reg_kernel(const bf16_t* __restrict__ dy,
-                                                                    const bf16_t* __restrict__ x,
-                                                                    const bf16_t* __restrict__ y,
-                                                                    const float* __restrict__ ss, int64_t M, int C,
-                                                                    const float* __restrict__ coef,
-                                                                    bf16_t* __restrict__ dx, bf16_t* __restrict__ dres) {
-  const int cv = C / 8;
+// Wave-contiguous register-coefficient backward apply (layout and mask words as bn_apply_wave_kernel:
+// the 256 mask bytes of an iteration arrive as one 4-byte load per lane; dx / dres are written with
+// nontemporal stores).
+template <int MASK, bool DRES, int NS>
+__global__ void __launch_bounds__(kThreads) bn_bwd_apply_wave_kernel(const bf16_t* __restrict__ dy,
+                                                                     const bf16_t* __restrict__ x,
+                                                                     const bf16_t* __restrict__ y,
+                                                                     const float* __restrict__ ss, int64_t M, int C,
+                                                                     const float* __restrict__ coef,
+                                                                     bf16_t* __restrict__ dx,
+                                                                     bf16_t* __restrict__ dres) {
+  const int cv = C / 8, lane = threadIdx.x & 63;
   const int64_t nvec = M * cv;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int c0 = (int)(v % cv) * 8;
-  float cA[8], cB[8], cC[8], sc[8], sh[8];
-  load8(coef + c0, cA);
-  load8(coef + C + c0, cB);
-  load8(coef + 2 * C + c0, cC);
-  if constexpr (MASK == 2) {
-    load8(ss + c0, sc);
-    load8(ss + C + c0, sh);
+  const int64_t tw = (int64_t)gridDim.x * (kThreads / 64);
+  const uint8_t* mbytes = reinterpret_cast<const uint8_t*>(y);  // MASK 3: the bit mask
+  float cA[NS][8], cB[NS][8], cC[NS][8], sc[NS][8], sh[NS][8];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int c0 = ((64 * s + lane) % cv) * 8;
+    load8(coef + c0, cA[s]);
+    load8(coef + C + c0, cB[s]);
+    load8(coef + 2 * C + c0, cC[s]);
+    if constexpr (MASK == 2) {
+      load8(ss + c0, sc[s]);
+      load8(ss + C + c0, sh[s]);
+    }
   }
-  auto one = [&](float (&g)[8], float (&xv)[8], uint32_t mb, int64_t vv) {
+  auto one = [&](float (&g)[8], float (&xv)[8], uint32_t mb, const bf16_t* yv, int s, bf16_t* dxp, bf16_t* drp,
+                 bool nt) {
     if constexpr (MASK == 3) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = (mb >> j) & 1u ? g[j] : 0.f;
     } else if constexpr (MASK == 2) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = fmaf(xv[j], sc[j], sh[j]) > 0.f ? g[j] : 0.f;
+      for (int j = 0; j < 8; ++j) g[j] = fmaf(xv[j], sc[s][j], sh[s][j]) > 0.f ? g[j] : 0.f;
     } else if constexpr (MASK == 1) {
-      const u16x8 yr = *reinterpret_cast<const u16x8*>(y + vv * 8);
+      const u16x8 yr = *reinterpret_cast<const u16x8*>(yv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = bf2f(yr[j]) > 0.f ? g[j] : 0.f;
     }
-    if (DRES) store8(dres + vv * 8, g);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) xv[j] = fmaf(cA[j], g[j], fmaf(cB[j], xv[j], cC[j]));
-    store8(dx + vv * 8, xv);
-  };
-  constexpr int U = 3;
-  for (; v + (U - 1) * stride < nvec; v += U * stride) {  // 3 vectors x (dy, x, mask) in flight per lane
-    float g[U][8], xv[U][8];
-    uint32_t mb[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      load8(dy + (v + u * stride) * 8, g[u]);
-      load8(x + (v + u * stride) * 8, xv[u]);
-      mb[u] = MASK == 3 ? reinterpret_cast<const uint8_t*>(y)[v + u * stride] : 0u;
+    if (DRES) {
+      if (nt) store8_nt(drp, g);
+      else store8(drp, g);
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) one(g[u], xv[u], mb[u], v + u * stride);
+    for (int j = 0; j < 8; ++j) xv[j] = fmaf(cA[s][j], g[j], fmaf(cB[s][j], xv[j], cC[s][j]));
+    if (nt) store8_nt(dxp, xv);
+    else store8(dxp, xv);
+  };
+  int64_t base = ((int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * kWaveVec;
+  for (; base + kWaveVec <= nvec; base += tw * kWaveVec) {
+    u16x8 ga[4], xa[4];  // packed until used
+    uint32_t word = 0;
+    if constexpr (MASK == 3) word = reinterpret_cast<const uint32_t*>(mbytes + base)[lane];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t v = base + 64 * u + lane;
+      ga[u] = *reinterpret_cast<const u16x8*>(dy + v * 8);
+      xa[u] = *reinterpret_cast<const u16x8*>(x + v * 8);
+    }
+    const uint32_t w = MASK == 3 ? mask_words_in(word, lane) : 0u;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t v = base + 64 * u + lane;
+      float g[8], xv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        g[j] = bf2f(ga[u][j]);
+        xv[j] = bf2f(xa[u][j]);
+      }
+      one(g, xv, w >> (8 * u), y + v * 8, u % NS, dx + v * 8, DRES ? dres + v * 8 : nullptr, true);
+    }
   }
-  for (; v < nvec; v += stride) {
+  for (int64_t v = base + lane; base < nvec && v < nvec; v += 64) {  // last partial iteration
+    // (the channel group of a tail vector is its own: (v % cv) — reload that group's coefficients)
+    const int c0 = (int)(v % cv) * 8;
+    load8(coef + c0, cA[0]);
+    load8(coef + C + c0, cB[0]);
+    load8(coef + 2 * C + c0, cC[0]);
+    if constexpr (MASK == 2) {
+      load8(ss + c0, sc[0]);
+      load8(ss + C + c0, sh[0]);
+    }
     float g[8], xv[8];
     load8(dy + v * 8, g);
     load8(x + v * 8, xv);
-    one(g, xv, MASK == 3 ? reinterpret_cast<const uint8_t*>(y)[v] : 0u, v);
+    one(g, xv, MASK == 3 ? (uint32_t)mbytes[v] : 0u, y + v * 8, 0, dx + v * 8, DRES ? dres + v * 8 : nullptr,
+        false);
   }
 }
 
@@ -585,19 +678,24 @@ inline bool lds_tables_forced() {
   return v;
 }
 
-// the grid-stride loop keeps each lane on one channel group when the stride is a multiple of C/8
-inline bool reg_tables(int grid, int C) { return ((int64_t)grid * kThreads) % (C / 8) == 0; }
+template <int NS>
+void launch_apply_wave(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int C, const float* scale,
+                       const float* shift, bool relu, uint8_t* bits, hipStream_t st) {
+  const int grid = wave_grid(M * C / 8);
+  if (res && relu) bn_apply_wave_kernel<true, true, NS><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits);
+  else if (res) bn_apply_wave_kernel<true, false, NS><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr);
+  else if (relu) bn_apply_wave_kernel<false, true, NS><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits);
+  else bn_apply_wave_kernel<false, false, NS><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr);
+}
 
 hipError_t launch_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int C, const float* scale,
                         const float* shift, bool relu, uint8_t* bits, hipStream_t st) {
+  const int ns = lds_tables_forced() ? 0 : wave_sets(C / 8);
+  if (ns == 1) launch_apply_wave<1>(x, res, y, M, C, scale, shift, relu, bits, st);
+  else if (ns == 2) launch_apply_wave<2>(x, res, y, M, C, scale, shift, relu, bits, st);
+  else if (ns == 4) launch_apply_wave<4>(x, res, y, M, C, scale, shift, relu, bits, st);
+  if (ns == 1 || ns == 2 || ns == 4) return hipGetLastError();
   const int grid = ew_grid(M * C / 8);
-  if (reg_tables(grid, C) && !lds_tables_forced()) {
-    if (res && relu) bn_apply_reg_kernel<true, true><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits);
-    else if (res) bn_apply_reg_kernel<true, false><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr);
-    else if (relu) bn_apply_reg_kernel<false, true><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits);
-    else bn_apply_reg_kernel<false, false><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr);
-    return hipGetLastError();
-  }
   const size_t lds = 2 * (size_t)C * sizeof(float);
   if (res && relu) bn_apply_kernel<true, true><<<grid, kThreads, lds, st>>>(x, res, y, M, C, scale, shift, bits);
   else if (res) bn_apply_kernel<true, false><<<grid, kThreads, lds, st>>>(x, res, y, M, C, scale, shift, nullptr);
@@ -685,13 +783,16 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint
                                                                          save_invstd, gamma_f, gamma_b, dgamma_f,
                                                                          dgamma_b, dbeta_f, dbeta_b, coef);
   PDA_CHECK_HIP(hipGetLastError());
-  const int grid = ew_grid(M * C / 8);
-  const bool reg = reg_tables(grid, (int)C) && !lds_tables_forced();
-  const size_t lds = reg ? 0 : 5 * (size_t)C * sizeof(float);
-#define BWD_APPLY(MK, DR)                                                                             \
-  do {                                                                                                \
-    if (reg) bn_bwd_apply_reg_kernel<MK, DR><<<grid, kThreads, 0, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres); \
-    else bn_bwd_apply_kernel<MK, DR><<<grid, kThreads, lds, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres); \
+  int ns = lds_tables_forced() ? 0 : wave_sets((int)(C / 8));
+  if (ns == 3 || ns > 4) ns = 0;
+  const int grid = ns ? wave_grid(M * C / 8) : ew_grid(M * C / 8);
+  const size_t lds = 5 * (size_t)C * sizeof(float);
+#define BWD_APPLY(MK, DR)                                                                                        \
+  do {                                                                                                           \
+    if (ns == 1) bn_bwd_apply_wave_kernel<MK, DR, 1><<<grid, kThreads, 0, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres); \
+    else if (ns == 2) bn_bwd_apply_wave_kernel<MK, DR, 2><<<grid, kThreads, 0, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres); \
+    else if (ns == 4) bn_bwd_apply_wave_kernel<MK, DR, 4><<<grid, kThreads, 0, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres); \
+    else bn_bwd_apply_kernel<MK, DR><<<grid, kThreads, lds, st>>>(dy, x, y, ss, M, (int)C, coef, dx, dres);     \
   } while (0)
   if (mask == 0) { if (dres) BWD_APPLY(0, true); else BWD_APPLY(0, false); }
   else if (mask == 1) { if (dres) BWD_APPLY(1, true); else BWD_APPLY(1, false); }

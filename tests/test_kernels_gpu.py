@@ -228,7 +228,10 @@ def test_conv_fwd_epilogue_bn_sums(case, wide):
 
 # ----------------------------------------------------------------------------- batch norm
 @pytest.mark.parametrize("shape", [(4, 8, 8, 64), (2, 7, 7, 2048), (3, 5, 5, 200), (2, 56, 56, 256),
-                                   (64, 28, 28, 64)])
+                                   (64, 28, 28, 64),
+                                   # partial last wave iteration (vectors % 256 != 0) with 1 and 2
+                                   # coefficient sets per lane
+                                   (3, 7, 7, 64), (1, 3, 7, 128), (1, 3, 5, 1024)])
 @pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
 def test_batchnorm_train(shape, relu, res):
     torch.manual_seed(2)
