@@ -20,7 +20,7 @@ from pytorchdistributed_amd._native import C  # noqa: E402
 
 # (H, Cin, Cout, R, stride) for every distinct ResNet-50 conv (input spatial size H)
 RESNET_CONVS = [
-    (224, 8, 64, 7, 2),
+    (115, 16, 64, 4, 1),  # the 7x7/2 stem as run: 4x4/1 valid conv over the 2x2 space-to-depth image
     (56, 64, 64, 1, 1), (56, 64, 64, 3, 1), (56, 64, 256, 1, 1), (56, 256, 64, 1, 1),
     (56, 256, 128, 1, 1), (56, 128, 128, 3, 2), (28, 128, 512, 1, 1), (56, 256, 512, 1, 2),
     (28, 512, 128, 1, 1), (28, 128, 128, 3, 1),
@@ -52,6 +52,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--torch", action="store_true", help="also time MIOpen / hipBLASLt")
     ap.add_argument("--wide", type=int, default=-1, help="wide-tile GEMM path: -1 env, 0 off, 1 auto, 2 force")
+    ap.add_argument("--compare", action="store_true",
+                    help="per shape and op, time the auto / 128-tile / wide-tile paths interleaved (min of 3)")
     a = ap.parse_args()
     c = C()
     c.set_gemm_paths(a.wide)
@@ -70,7 +72,7 @@ def main():
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     tot_t = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     for (H, Ci, Co, R, st), cnt in zip(RESNET_CONVS, COUNT):
-        pad = R // 2
+        pad = 0 if R == 4 else R // 2
         P = (H + 2 * pad - R) // st + 1
         x = torch.randn(a.batch, H, H, Ci, device=dev, dtype=torch.bfloat16)
         w = torch.randn(Co, R, R, Ci, device=dev, dtype=torch.bfloat16) * 0.05
@@ -80,7 +82,22 @@ def main():
         fns = {"fwd": lambda: c.conv_fwd(x, w, st, pad, 1, None, False),
                "dgrad": lambda: c.conv_dgrad(dy, w, H, H, st, pad, 1, None),
                "wgrad": lambda: c.conv_wgrad(dy, x, R, R, st, pad, 1, True, dwo)}
+        if R == 4:
+            del fns["dgrad"]  # the stem's input needs no gradient
         rec = {"op": "conv", "H": H, "Cin": Ci, "Cout": Co, "R": R, "stride": st, "count": cnt}
+        if a.compare:
+            for k, fn in fns.items():
+                best = {}
+                for _ in range(3):
+                    for mode, name in ((-1, "auto"), (0, "narrow"), (2, "wide")):
+                        c.set_gemm_paths(mode)
+                        ms = time_fn(fn, a.iters)
+                        best[name] = min(best.get(name, 1e9), ms)
+                c.set_gemm_paths(a.wide)
+                for name, ms in best.items():
+                    rec[f"{k}_{name}_ms"] = round(ms, 4)
+            print(json.dumps(rec), flush=True)
+            continue
         for k, fn in fns.items():
             ms = time_fn(fn, a.iters)
             tot[k] += ms * cnt
