@@ -506,6 +506,88 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// bf16 epilogue of a 4-wave (2x2) BM x BN tile whose accumulators are acc[i][j][r] =
+// C[m0 + wm*WM + 16 i + (lane & 15)][n0 + wn*WN + 16 j + 4 (lane >> 4) + r]; `smem` is the operand LDS
+// (>= BM * (BN + 8) * 2 bytes + the statistics scratch), free once every wave has left the K loop.
+template <int BM, int BN>
+__device__ __forceinline__ void tile_epilogue_bf16(const f32x4 (&acc)[BM / 32][BN / 32], char* smem, const Epi& epi,
+                                                   int64_t m0, int64_t n0, int64_t M, int64_t N, int tm) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  // bf16 output: stage the tile through LDS (row stride BN + 8 elements keeps both the 8-B fragment
+  // writes and the 16-B row reads bank-conflict free), then write whole 16-B chunks of rows —
+  // coalesced stores (and addend loads) instead of 16 rows x 32 B per wave instruction.  The K loop
+  // ended with a barrier, so every wave is done reading the operand tiles.
+  constexpr int SROW = BN + 8;
+  bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * WM + 16 * i + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cc = wn * WN + 16 * j + 4 * (lane >> 4);
+      f32x4 v = acc[i][j];
+      if (epi.bias) {
+        const int64_t n = n0 + cc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (n + q < N)
+            v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
+      }
+      if (epi.relu) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+      }
+      u16x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
+      *reinterpret_cast<u16x4*>(stg + r * SROW + cc) = o;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  static_assert(NT % CPR == 0, "a thread keeps one column chunk");
+  // column chunk of this thread is fixed (NT % CPR == 0): BN statistics accumulate in registers
+  float st1[8], st2[8], kshift[8];
+  const bool want_stats = epi.stats != nullptr;
+  {
+    const int64_t n = n0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      st1[q] = st2[q] = 0.f;
+      kshift[q] = (want_stats && n + q < N) ? epi.stats_shift[n + q] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int c = tid; c < BM * CPR; c += NT) {
+    const int r = c / CPR, ch = c % CPR;
+    const int64_t m = m0 + r, n = n0 + ch * 8;
+    if (m >= M || n >= N) continue;
+    const int64_t crow = epi_row(epi, m);
+    u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * SROW + ch * 8);
+    if (epi.addend) {
+      float a[8];
+      epi_addend8(epi, crow, n, a);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
+    }
+    if (want_stats) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float d = bf2f(v[q]) - kshift[q];
+        st1[q] += d;
+        st2[q] += d * d;
+      }
+    }
+    *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
+  }
+  if (want_stats) {
+    epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + BM * SROW * 2), CPR, NT, tm, n0, N);
+  }
+}
+
 // ------------------------------------------------------------------ the kernel
 template <int BM, int BN, class LA, class LB>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K, int tiles_n,
@@ -578,78 +660,9 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
 
   // epilogue: acc[i][j][r] = C[m0 + wm*WM + 16 i + (lane & 15)][n0 + wn*WN + 16 j + 4 (lane >> 4) + r]
   if (!epi.slab && !epi.c_f32) {
-    // bf16 output: stage the tile through LDS (row stride BN + 8 elements keeps both the 8-B fragment
-    // writes and the 16-B row reads bank-conflict free), then write whole 16-B chunks of rows —
-    // coalesced stores (and addend loads) instead of 16 rows x 32 B per wave instruction.  The K loop
-    // ended with a barrier, so every wave is done reading the operand tiles.
-    constexpr int SROW = BN + 8;
-    static_assert(BM * SROW * 2 <= 2 * (A_BYTES + B_BYTES), "staging tile must fit the operand LDS");
-    bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int r = wm * WM + 16 * i + (lane & 15);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int cc = wn * WN + 16 * j + 4 * (lane >> 4);
-        f32x4 v = acc[i][j];
-        if (epi.bias) {
-          const int64_t n = n0 + cc;
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (n + q < N)
-              v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
-        }
-        if (epi.relu) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-        }
-        u16x4 o;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
-        *reinterpret_cast<u16x4*>(stg + r * SROW + cc) = o;
-      }
-    }
-    __syncthreads();
-    constexpr int CPR = BN / 8;
-    static_assert(NT % CPR == 0, "a thread keeps one column chunk");
-    // column chunk of this thread is fixed (NT % CPR == 0): BN statistics accumulate in registers
-    float st1[8], st2[8], kshift[8];
-    const bool want_stats = epi.stats != nullptr;
-    {
-      const int64_t n = n0 + (tid % CPR) * 8;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        st1[q] = st2[q] = 0.f;
-        kshift[q] = (want_stats && n + q < N) ? epi.stats_shift[n + q] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int c = tid; c < BM * CPR; c += NT) {
-      const int r = c / CPR, ch = c % CPR;
-      const int64_t m = m0 + r, n = n0 + ch * 8;
-      if (m >= M || n >= N) continue;
-      const int64_t crow = epi_row(epi, m);
-      u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * SROW + ch * 8);
-      if (epi.addend) {
-        float a[8];
-        epi_addend8(epi, crow, n, a);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
-      }
-      if (want_stats) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float d = bf2f(v[q]) - kshift[q];
-          st1[q] += d;
-          st2[q] += d * d;
-        }
-      }
-      *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
-    }
-    if (want_stats) {
-      static_assert(BM * SROW * 2 + (NT / 64) * BN * 2 * 4 <= 2 * (A_BYTES + B_BYTES), "stats scratch must fit");
-      epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + BM * SROW * 2), CPR, NT, tm, n0, N);
-    }
+    static_assert(BM * (BN + 8) * 2 + (NT / 64) * BN * 2 * 4 <= 2 * (A_BYTES + B_BYTES),
+                  "staging tile + stats scratch must fit the operand LDS");
+    tile_epilogue_bf16<BM, BN>(acc, smem, epi, m0, n0, M, N, tm);
     return;
   }
 #pragma unroll
@@ -685,6 +698,163 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
       *reinterpret_cast<f32x4*>((float*)epi.C + crow * epi.ldc + n) = v;
     }
   }
+}
+
+// ------------------------------------------------------------------ 3x3 / stride-1 halo kernel
+// Conv fwd (and stride-1 dgrad, which is the same conv over dy with the 180-degree-rotated transposed
+// weights) of a 3x3 / pad-1 / stride-1 conv without the implicit-GEMM im2col gather.  The gather
+// fetches every input pixel 9 times through L2 (once per tap); with the 256x256 and 128-row tiles
+// already at the L2's per-CU share of bandwidth, that traffic, not the MFMAs, bounds the 3x3 convs
+// (~0.5-0.6 PF/s).  Here a workgroup owns 128 consecutive output pixels (flattened n,p,q) x BN
+// output channels; per 64-channel chunk of the source it DMAs the BAND of source rows those pixels
+// touch — their rows plus one halo row each side, full width, once — into LDS, then runs the 9 taps
+// as 9 K-steps whose A fragments are read from the band at the tap's pixel offset (zero outside the
+// image), while only the weight tiles stream (double-buffered) per tap.  L2 operand traffic per
+// K-step drops from (128 + BN) rows to ~BN rows + band/9.
+//   band: source rows v0 .. v1 (flattened n*H + h) of W pixels x 64 channels, 128-B rows, chunk XOR
+//   swizzle as kmaj_off (pixel = (v - v0) * W + w); sized by the host: band_px >= rows * W.
+// B operand: K-major weights, row = output channel, k = tap * Cg + channel (OHWI for fwd; for dgrad
+// the plain transposed wt[ci][r][s][co], read at tap 8 - t: `flip`).
+// weight-stage ring depth: 4 x 8 KB for 64-channel tiles, 3 x 16 KB for 128
+constexpr __host__ __device__ int halo_stages(int bn) { return bn == 64 ? 4 : 3; }
+
+struct HaloGeom {
+  int H, W, Cg;      // source spatial dims (= output dims) and channels
+  FastDiv fW, fH;
+  int band_px;       // LDS band capacity in pixels (host bound)
+  int flip;
+};
+
+template <int BN>
+__global__ void __launch_bounds__(NT, 2) conv3x3_halo_kernel(const bf16_t* __restrict__ src, HaloGeom hg,
+                                                            PlainK<BN> lb, int64_t M, int64_t N, int tiles_n,
+                                                            Epi epi) {
+  constexpr int BM = 128, WM = 64, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int B_BYTES = BN * BK * 2;
+  constexpr int D = halo_stages(BN);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* band = smem;
+  char* bst = smem + hg.band_px * 128;  // D weight stages
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntiles = gridDim.x;
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  int tm, tn;
+  grouped_tile(tile, ntiles / tiles_n, tiles_n, 8, tm, tn);
+  const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+  const int H = hg.H, W = hg.W, Cg = hg.Cg;
+
+  // band rows: from the first pixel's row - 1 to the last pixel's row + 1, clipped to their images
+  int v0, v1;
+  {
+    const uint32_t t0 = fdiv((uint32_t)m0, hg.fW);  // n*H + p of the first pixel
+    const uint32_t n0i = fdiv(t0, hg.fH);
+    const int p0 = (int)(t0 - n0i * H);
+    v0 = (int)t0 - (p0 > 0 ? 1 : 0);
+    const int64_t ml = (m0 + BM - 1 < M ? m0 + BM - 1 : M - 1);
+    const uint32_t t1 = fdiv((uint32_t)ml, hg.fW);
+    const uint32_t n1i = fdiv(t1, hg.fH);
+    const int p1 = (int)(t1 - n1i * H);
+    v1 = (int)t1 + (p1 < H - 1 ? 1 : 0);
+  }
+  const int band_n = (v1 - v0 + 1) * W;  // < hg.band_px (host bound): pixel band_px - 1 stays zero
+  const int zpx = hg.band_px - 1;
+
+  // per-lane output pixels of the TM fragment rows: band pixel of the centre tap, p, q
+  int cpix[TM], pp[TM], qq[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int64_t m = m0 + wm * WM + 16 * i + (lane & 15);
+    const bool ok = m < M;
+    const uint32_t mm = ok ? (uint32_t)m : 0u;
+    const uint32_t t = fdiv(mm, hg.fW);
+    qq[i] = (int)(mm - t * W);
+    const uint32_t n = fdiv(t, hg.fH);
+    pp[i] = ok ? (int)(t - n * H) : -4;  // -4: every tap invalid
+    cpix[i] = ((int)t - v0) * W + qq[i];
+  }
+
+  typename PlainK<BN>::State sb;
+  lb.init(sb, n0, tid);
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nchunks = Cg / 64;
+  const int64_t src_px0 = (int64_t)v0 * W;
+  auto load_band = [&](int c) {
+    // thread t fills pixel (t >> 3) + 32 k, LDS slot t & 7 with logical chunk slot ^ swizzle(pixel)
+    const int slot = tid & 7;
+    for (int k = 0; k * 32 < hg.band_px; ++k) {
+      const int px = k * 32 + (tid >> 3);
+      const int lc = slot ^ ((px >> 1) & 7);
+      const bf16_t* q = px < band_n ? src + (src_px0 + px) * Cg + c * 64 + lc * 8 : g_zero_page;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)q,
+                                       (void __attribute__((address_space(3)))*)(band + k * 4096 + wid * 1024), 16,
+                                       0, 0);
+    }
+  };
+  auto load_b = [&](int c, int t, int stage) {
+    const int tb = hg.flip ? 8 - t : t;
+    glds_tile(lb, sb, (int64_t)tb * Cg + c * 64, bst + stage * B_BYTES, wid);
+  };
+
+  // weights stream through a ring of D stages, D - 1 K-steps ahead (a K-step is short — 128 x BN x 64
+  // — so one step of prefetch cannot cover the L2 latency); at the top of step s the loads of steps
+  // s .. s + D - 2 are in flight, vmcnt counts them in issue order
+  const int S = 9 * nchunks;
+  load_band(0);
+#pragma unroll
+  for (int d = 0; d < D - 1; ++d)
+    if (d < S) load_b(d / 9, d % 9, d);
+#pragma unroll 1
+  for (int st = 0; st < S; ++st) {
+    const int c = st / 9, t = st - 9 * c;
+    if (t == 0 && c > 0) {
+      raw_barrier();  // every wave is done with the previous chunk's band
+      load_band(c);
+      wait_vm<0>();
+    } else if (st + D - 2 < S) {
+      wait_vm<(D - 2) * PlainK<BN>::NCH>();
+    } else {
+      wait_vm<0>();
+    }
+    raw_barrier();  // everyone's loads for step st landed; everyone is done with step st - 1's stage
+    if (st + D - 1 < S) load_b((st + D - 1) / 9, (st + D - 1) % 9, (st + D - 1) % D);
+    const int dr = t / 3 - 1, ds = t % 3 - 1;
+    const int off = dr * W + ds;
+    const char* Bs = bst + (st % D) * B_BYTES;
+    // every fragment of the step is read up front (unconditional reads: a tap outside the image reads
+    // the band's zero pixel), then the 2 x TM x TN MFMAs
+    mfma_bf16x8 af[2][TM], bfr[2][TN];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int chunk = 4 * h + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const bool ok = (unsigned)(pp[i] + dr) < (unsigned)H && (unsigned)(qq[i] + ds) < (unsigned)W;
+        const int px = ok ? cpix[i] + off : zpx;
+        af[h][i] = *reinterpret_cast<const mfma_bf16x8*>(band + kmaj_off(px, chunk));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[h][j] = read_frag<true, BN>(Bs, wn * WN + 16 * j, 32 * h, lane);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[h][j], af[h][i], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();
+  // (every wave has left the K loop: the band and weight stages are free for the staging tile)
+  tile_epilogue_bf16<BM, BN>(acc, smem, epi, m0, n0, M, N, tm);
 }
 
 // ------------------------------------------------------------------ big-tile kernel (K-major x K-major)
@@ -1435,6 +1605,73 @@ int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, 
   return split_slab_floats(M, Nn, K, plan_wgrad(M, Nn, K, true));
 }
 
+// 3x3 halo path (conv3x3_halo_kernel): a 3x3 / pad-1 / stride-1 / dil-1 conv whose source has
+// channels % 64 == 0 and whose band (rows spanned by 128 consecutive output pixels + 2 halo rows, full
+// width) fits in LDS beside the two weight stages at two workgroups per CU.  PDA_CONV_HALO=0 disables it.
+constexpr int kHaloLdsCap = 80 * 1024;
+
+int halo_band_px(int H, int W) {
+  // 128 consecutive pixels span at most ceil(127 / W) + 1 rows; + 1 halo row each side; + 1 zero pixel
+  // (the target of taps outside the image); rounded up to the 32 pixels of one loader round
+  const int rows = (127 + W - 1) / W + 1 + 2;
+  return (rows * W + 1 + 31) / 32 * 32;
+}
+
+bool halo_mode_on() {
+  static const bool on = [] {
+    const char* e = getenv("PDA_CONV_HALO");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int halo_lds_bytes(int H, int W, int BN) {
+  int b = halo_band_px(H, W) * 128 + halo_stages(BN) * BN * BK * 2;
+  const int epi_b = 128 * (BN + 8) * 2 + (NT / 64) * BN * 2 * 4;
+  return b > epi_b ? b : epi_b;
+}
+
+bool use_halo(int H, int W, int Cg, int Nout, int R, int S, int stride, int pad, int dil, const Epi& epi) {
+  if (!halo_mode_on() || R != 3 || S != 3 || stride != 1 || pad != 1 || dil != 1) return false;
+  // 128-channel outputs only (measured, bench_conv bs 512, same box): 28^2 128->128 fwd 158 -> 144 us,
+  // dgrad 162 -> 147 us.  At Nout >= 256 the 256x256 implicit-GEMM tile streams as many weight bytes
+  // per FLOP as a 128-channel halo tile and ties it (14^2 256, 7^2 512: +-2 %); at Nout = 64 (56^2
+  // 64->64) the 77-KB band + 4-stage workgroup fits 2 per CU against the 128x64 implicit-GEMM tile's
+  // 3, and the layer is latency- rather than L2-bound there: +6 %.
+  if (Cg % 64 || Nout != 128 || epi.c_f32 || epi.slab || epi.rm_on) return false;
+  return halo_lds_bytes(H, W, 128) <= kHaloLdsCap;
+}
+
+template <int BN>
+hipError_t launch_halo_bn(const bf16_t* src, const bf16_t* B, int Nimg, int H, int W, int Cg, int Nout, bool flip,
+                          const Epi& epi, hipStream_t st) {
+  const int lds = halo_lds_bytes(H, W, BN);
+  static bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_halo_kernel<BN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kHaloLdsCap);
+    return true;
+  }();
+  (void)attr;
+  HaloGeom hg;
+  hg.H = H; hg.W = W; hg.Cg = Cg;
+  hg.fW = make_fastdiv((uint32_t)W);
+  hg.fH = make_fastdiv((uint32_t)H);
+  hg.band_px = halo_band_px(H, W);
+  hg.flip = flip ? 1 : 0;
+  const int64_t M = (int64_t)Nimg * H * W, K = 9LL * Cg;
+  PlainK<BN> lb;
+  lb.p = B; lb.rows = Nout; lb.K = K; lb.ld = K;
+  const int tiles_n = (Nout + BN - 1) / BN;
+  const int tiles = (int)((M + 127) / 128) * tiles_n;
+  conv3x3_halo_kernel<BN><<<tiles, NT, lds, st>>>(src, hg, lb, M, Nout, tiles_n, epi);
+  return hipGetLastError();
+}
+
+hipError_t launch_halo(const bf16_t* src, const bf16_t* B, int Nimg, int H, int W, int Cg, int Nout, bool flip,
+                       const Epi& epi, hipStream_t st) {
+  return launch_halo_bn<128>(src, B, Nimg, H, W, Cg, Nout, flip, epi, st);
+}
+
 // y[N,P,Q,Cout] = conv(x[N,H,W,C], w[Cout,R,S,C]) (+bias, relu)
 hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int Cout, int R, int S,
                       int P, int Q, int stride, int pad, int dil, const void* bias, bool bias_f32, bool relu,
@@ -1446,6 +1683,7 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H,
   epi.stats_shift = stats_shift;
   epi.stats_rows = stats_rows > 0 ? stats_rows : 1;
 
+  if (use_halo(H, W, C, Cout, R, S, stride, pad, dil, epi)) return launch_halo(x, w, N, H, W, C, Cout, false, epi, st);
   ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
   auto mk_a = [&](auto t) { t.x = x; t.g = g; t.M = M; t.K = K; return t; };
   auto mk_b = [&](auto t) { t.p = w; t.rows = Nn; t.K = K; t.ld = K; return t; };
@@ -1482,6 +1720,13 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf1
     auto mk_a = [&](auto t) { t.dy = dy; t.g = g; t.M = M; t.K = K; return t; };
     auto mk_b = [&](auto t) { t.p = wt; t.rows = Nn; t.K = K; t.ld = K; return t; };
     return dispatch_bn<ConvDgradK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
+  }
+  if (stride == 1) {
+    // stride-1 dgrad = the 3x3 conv of dy with the rotated transposed weights (halo path)
+    Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
+    epi.addend = addend;
+    epi.addend_bits = addend_bits;
+    if (use_halo(H, W, Cout, C, R, S, stride, pad, dil, epi)) return launch_halo(dy, wt, N, H, W, Cout, C, true, epi, st);
   }
   const int nph = stride;  // phases per dim (1 for stride 1)
   for (int ph = 0; ph < nph; ++ph) {

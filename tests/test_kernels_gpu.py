@@ -153,6 +153,9 @@ CONV_CASES = [
     (16, 56, 56, 64, 256, 1, 1, 0),     # >= 256 tiles: 256x128 three-stage kernel (fwd)
     (16, 56, 56, 256, 64, 1, 1, 0),     # ... and for the dgrad (with and without the fused addend)
     (8, 57, 57, 128, 128, 3, 1, 1),     # big tiles with ragged M and 3x3 gathers
+    (6, 7, 7, 128, 128, 3, 1, 1),       # 3x3 halo path: 128-pixel tiles spanning 3 images
+    (2, 28, 28, 128, 128, 3, 1, 1),     # 3x3 halo path (layer2 shape), 2 source-channel chunks
+    (3, 9, 13, 64, 128, 3, 1, 1),       # halo fwd (its dgrad, 64 out channels, stays implicit GEMM)
 ]
 
 
