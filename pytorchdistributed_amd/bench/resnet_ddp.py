@@ -47,11 +47,12 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    # per-GPU batch: 512 uses the 288 GB of an MI355X for throughput (bigger GEMM grids — the 14^2 / 7^2
-    # convs' tile rounds quantise better — and half the per-image launch / epilogue overhead); measured
-    # on one MI355X (profiles/r2_resnet50_batch_sweep.jsonl): 256 -> 9.94k, 384 -> 10.25k,
-    # 512 -> 10.68k, 640 -> 11.06k, 768 -> 10.88k img/s.  --batch 256 reproduces the round-1 setting.
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("PDA_BENCH_BATCH", "512")),
+    # per-GPU batch: 640 uses the 288 GB of an MI355X for throughput (bigger GEMM grids — the 14^2 / 7^2
+    # convs' tile rounds quantise better: 640 * 196 / 256 = 490 tiles = 1.91 rounds of 256 CUs against
+    # 1.53 at 512 — and less per-image launch / epilogue overhead); measured on one MI355X with the
+    # current kernels (profiles/r2_resnet50_batch_sweep_v23.jsonl): 512 -> 10.94k, 576 -> 11.27k,
+    # 640 -> 11.31k, 704 -> 11.07k, 768 -> 11.13k img/s (round-1 setting: --batch 256).
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("PDA_BENCH_BATCH", "640")),
                     help="per-GPU batch")
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=None)
@@ -78,8 +79,8 @@ def main(argv=None):
                    "optimizer": "SGD(momentum=0.9, wd=5e-5), fp32 master weights"},
         "final_loss": round(last, 4),
         "notes": "reference publishes no number for this metric (BASELINE.json published={}); per-GPU batch "
-                 "512 (throughput-optimal power of two on 288 GB HBM; --batch 256 gives the round-1 "
-                 "setting); NB03 parity numbers are produced by pytorchdistributed_amd.bench.nb03",
+                 f"{a.batch} (640 = throughput-optimal on 288 GB HBM by a 512-768 sweep; --batch 256 gives "
+                 "the round-1 setting); NB03 parity numbers are produced by pytorchdistributed_amd.bench.nb03",
     }, rank)
     teardown()
 
