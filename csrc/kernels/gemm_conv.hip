@@ -857,6 +857,143 @@ __global__ void __launch_bounds__(NT, 2) conv3x3_halo_kernel(const bf16_t* __res
   tile_epilogue_bf16<BM, BN>(acc, smem, epi, m0, n0, M, N, tm);
 }
 
+// ------------------------------------------------------------------ 3x3 / stride-1 weight gradient, all taps
+// dw[co][r][s][ci] = sum over output pixels of dy[px][co] * x[px + (r-1, s-1)][ci].  The implicit GEMM
+// (M = Cout, N = 9 C, K = pixels) gathers im2col(x) per N tile: every x pixel is fetched from L2 once
+// per tap and per 128-column tile (~43 FLOP per L2 byte at 64 output channels: L2-bound, 0.3 PF/s
+// on the 56^2 layer).  Here one workgroup owns a 64 x 576 output block — 64 output channels x all
+// 9 taps of 64 input channels — and walks K in row groups: R_k whole output rows of one image
+// (R_k * W <= 64 pixels) per K-step.  Per step it DMAs the dy rows (an MN-major [64 px][64 co] tile)
+// and the x BAND they touch (R_k + 2 rows of W + 2 pixels, zero-padded at the image border) into LDS
+// once, and the 9 taps are 9 shifted views of the band (~150 FLOP per L2 byte).  Wave w owns input
+// channels 16w .. 16w+15 of every tap: acc[co block][tap] (36 tiles).  Split-K over row groups writes
+// fp32 slabs that splitk_reduce_kernel sums into dw.
+//   band pixel b = row_slot * (W + 2) + col + 1 (row_slot 0 = image row p0 - 1); [b][64 ci] MN-major
+//   image with the 32-B slot XOR swizzle of mn_off<64> keyed by b.
+struct Wg3Geom {
+  int N, H, W, C, Cout;
+  int rk;         // output rows per K-step (rk * W <= 64)
+  int gpi;        // row groups per image = ceil(H / rk)
+  int groups;     // N * gpi
+  int gps;        // row groups per split
+  int band_px;    // band pixels (multiple of 32) >= (rk + 2) * (W + 2)
+  int tiles_ci;   // C / 64
+};
+
+__device__ __forceinline__ int band_mn_off(int b, int m) {
+  const int h = ((b >> 1) & 1) | (((b >> 3) & 1) << 1);
+  return b * 128 + ((((m >> 4) ^ h) & 3) << 5) + ((m & 15) << 1);
+}
+
+__global__ void __launch_bounds__(NT, 2) conv3x3_wgrad_kernel(const bf16_t* __restrict__ dy,
+                                                              const bf16_t* __restrict__ x, Wg3Geom g,
+                                                              float* __restrict__ slab) {
+  constexpr int A_BYTES = 64 * BK * 2;  // [64 px][64 co]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int stage_bytes = A_BYTES + g.band_px * 128;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tco = blockIdx.x / g.tiles_ci, tci = blockIdx.x - tco * g.tiles_ci;
+  const int co0 = tco * 64, ci0 = tci * 64;
+  const int W = g.W, H = g.H, W2 = W + 2;
+  const int gb = blockIdx.y * g.gps;
+  const int ge = min(g.groups, gb + g.gps);
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane band pixels of the k-rows this lane addresses in the transposed B reads:
+  // j = kk + 8 (lane >> 4) + ((lane & 15) >> 2) (+ 4), kk in {0, 32}
+  int pixj[2][2];
+#pragma unroll
+  for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+    for (int lh = 0; lh < 2; ++lh) {
+      const int j = 32 * h2 + 8 * (lane >> 4) + ((lane & 15) >> 2) + 4 * lh;
+      const int rj = j / W, cj = j - rj * W;
+      pixj[h2][lh] = j < g.rk * W ? rj * W2 + cj : 0;  // past the group: any finite band pixel (dy = 0)
+    }
+
+  auto issue = [&](int grp, int stg) {
+    char* base = smem + stg * stage_bytes;
+    const int n = grp / g.gpi, p0 = (grp - n * g.gpi) * g.rk;
+    const int rows = min(g.rk, H - p0);
+    // dy rows p0 .. p0 + rows - 1: rows * W consecutive pixels, an MN-major [k = px][m = co] tile
+    PlainMN<64> la;
+    la.p = dy + ((int64_t)n * H + p0) * W * g.Cout + co0;
+    la.K = rows * W;
+    la.cols = 64;
+    la.ld = g.Cout;
+    typename PlainMN<64>::State sa;
+    la.init(sa, 0, tid);
+    glds_tile(la, sa, 0, base, w);
+    // x band: image rows p0 - 1 .. p0 + rk, cols -1 .. W (zero outside the image)
+    char* band = base + A_BYTES;
+    const int s16 = tid & 7;
+    for (int k = 0; k * 32 < g.band_px; ++k) {
+      const int b = k * 32 + (tid >> 3);
+      const int rs = b / W2, cs = b - rs * W2;
+      const int ih = p0 - 1 + rs, iw = cs - 1;
+      const int hb = ((b >> 1) & 1) | (((b >> 3) & 1) << 1);
+      const int ci = ci0 + 16 * ((s16 >> 1) ^ hb) + 8 * (s16 & 1);
+      const bool ok = rs < g.rk + 2 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      const bf16_t* q = ok ? x + (((int64_t)n * H + ih) * W + iw) * g.C + ci : g_zero_page;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)q,
+                                       (void __attribute__((address_space(3)))*)(band + k * 4096 + w * 1024), 16,
+                                       0, 0);
+    }
+  };
+
+  if (gb < ge) issue(gb, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const int mcol = 16 * w + 4 * ((lane & 15) & 3);
+  for (int grp = gb; grp < ge; ++grp) {
+    const int stg = (grp - gb) & 1;
+    if (grp + 1 < ge) issue(grp + 1, stg ^ 1);
+    const char* As = smem + stg * stage_bytes;
+    const char* band = As + A_BYTES;
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      mfma_bf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<false, 64>(As, 16 * i, 32 * h2, lane);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int toff = (t / 3) * W2 + (t % 3);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)(band + band_mn_off(pixj[h2][0] + toff, mcol)));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)(band + band_mn_off(pixj[h2][1] + toff, mcol)));
+        s16x8 f;
+        f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+        f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+        const mfma_bf16x8 bf = __builtin_bit_cast(mfma_bf16x8, f);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf, af[i], acc[i][t], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // fp32 partials: acc[i][t][q] = dw[co0 + 16 i + (lane & 15)][t][ci0 + 16 w + 4 (lane >> 4) + q]
+  const int64_t Nn = 9LL * g.C;
+  float* out = slab + (int64_t)blockIdx.y * g.Cout * Nn;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = co0 + 16 * i + (lane & 15);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      *reinterpret_cast<f32x4*>(out + (int64_t)co * Nn + (int64_t)t * g.C + ci0 + 16 * w + 4 * (lane >> 4)) =
+          acc[i][t];
+  }
+}
+
 // ------------------------------------------------------------------ big-tile kernel (K-major x K-major)
 // 256 x 128 output tile, 8 waves (4 along M x 2 along N, 64 x 64 each — the same per-wave work as the
 // 128-tile kernel), THREE LDS stages of 48 KB (144 KB of the CU's 160 KB): the DMA of tile t+2 is in
@@ -1599,11 +1736,7 @@ hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* 
   return dispatch_bn<PlainMN, PlainMN>(M, N, K, p, epi, slab, st, mk_amn, mk_bmn);
 }
 
-int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, int S, int P, int Q) {
-  if (mode != 2) return 0;  // only wgrad splits K
-  const int64_t M = Cout, Nn = (int64_t)R * S * C, K = (int64_t)N * P * Q;
-  return split_slab_floats(M, Nn, K, plan_wgrad(M, Nn, K, true));
-}
+
 
 // 3x3 halo path (conv3x3_halo_kernel): a 3x3 / pad-1 / stride-1 / dil-1 conv whose source has
 // channels % 64 == 0 and whose band (rows spanned by 128 consecutive output pixels + 2 halo rows, full
@@ -1671,6 +1804,43 @@ hipError_t launch_halo(const bf16_t* src, const bf16_t* B, int Nimg, int H, int 
                        const Epi& epi, hipStream_t st) {
   return launch_halo_bn<128>(src, B, Nimg, H, W, Cg, Nout, flip, epi, st);
 }
+
+// 3x3 all-taps weight gradient (conv3x3_wgrad_kernel): stride 1, pad 1, dil 1, C and Cout multiples of
+// 64, W <= 64.  PDA_CONV_WG3=0 disables it.
+bool wg3_mode_on() {
+  static const bool on = [] {
+    const char* e = getenv("PDA_CONV_WG3");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+bool wg3_geom(int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad, int dil, Wg3Geom& g) {
+  if (!wg3_mode_on() || R != 3 || S != 3 || stride != 1 || pad != 1 || dil != 1) return false;
+  // W >= 28 (the 56^2 and 28^2 layers: wgrad 367 -> 209 us and 233 -> 188 us at bs 512, bench_conv);
+  // at 14^2 / 7^2 (4-7 rows per K-step, 16-64 output blocks re-reading each band) the implicit GEMM's
+  // 256x256 split-K tile measured 7 % faster
+  if (C % 64 || Cout % 64 || W > 64 || W < 28 || H < 1) return false;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.Cout = Cout;
+  g.rk = 64 / W;
+  if (g.rk > H) g.rk = H;
+  g.gpi = (H + g.rk - 1) / g.rk;
+  g.groups = N * g.gpi;
+  g.band_px = ((g.rk + 2) * (W + 2) + 31) / 32 * 32;
+  g.tiles_ci = C / 64;
+  const int tiles = (Cout / 64) * g.tiles_ci;
+  // ~512 workgroups (2 per CU), >= 4 row groups each, fp32 partial slabs capped at 96 MB
+  int splits = 512 / tiles;
+  if (splits < 1) splits = 1;
+  if (splits > g.groups / 4) splits = g.groups / 4 > 1 ? g.groups / 4 : 1;
+  const int64_t per = (int64_t)Cout * 9 * C;
+  const int64_t cap = ((int64_t)96 << 20) / (per * 4);
+  if (splits > cap) splits = cap > 1 ? (int)cap : 1;
+  g.gps = (g.groups + splits - 1) / splits;
+  return 2 * (64 * BK * 2 + g.band_px * 128) <= 80 * 1024;
+}
+
+int wg3_splits(const Wg3Geom& g) { return (g.groups + g.gps - 1) / g.gps; }
 
 // y[N,P,Q,Cout] = conv(x[N,H,W,C], w[Cout,R,S,C]) (+bias, relu)
 hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int Cout, int R, int S,
@@ -1762,13 +1932,44 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf1
   return hipSuccess;
 }
 
+int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, int S, int P, int Q) {
+  if (mode != 2) return 0;  // only wgrad splits K
+  const int64_t M = Cout, Nn = (int64_t)R * S * C, K = (int64_t)N * P * Q;
+  int64_t n = split_slab_floats(M, Nn, K, plan_wgrad(M, Nn, K, true));
+  Wg3Geom g;
+  if (P == H && Q == W && wg3_geom(N, H, W, C, Cout, R, S, 1, 1, 1, g)) {
+    const int64_t w3 = (int64_t)wg3_splits(g) * M * Nn;
+    if (w3 > n) n = w3;
+  }
+  return n;
+}
+
 // dw[Cout, R*S*C] = dy[NPQ, Cout]^T * im2col(x)[NPQ, R*S*C]   (fp32 or bf16 output)
 hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32, int N, int H, int W, int C,
                         int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, float* slab,
                         hipStream_t st) {
   const int64_t M = Cout, Nn = (int64_t)R * S * C, K = (int64_t)N * P * Q;
-  Plan p = plan_wgrad(M, Nn, K, slab != nullptr);
   Epi epi{dw, Nn, dw_f32 ? 1 : 0, nullptr, 0, 0, nullptr};
+  Wg3Geom g3;
+  if (slab && P == H && Q == W && wg3_geom(N, H, W, C, Cout, R, S, stride, pad, dil, g3)) {
+    static bool attr = [] {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wgrad_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+      return true;
+    }();
+    (void)attr;
+    const int splits = wg3_splits(g3);
+    const int lds = 2 * (64 * BK * 2 + g3.band_px * 128);
+    conv3x3_wgrad_kernel<<<dim3((Cout / 64) * g3.tiles_ci, splits), NT, lds, st>>>(dy, x, g3, slab);
+    PDA_CHECK_HIP(hipGetLastError());
+    int ll = 0;
+    while (ll < 4 && (splits >> ll) > 16) ++ll;
+    const int64_t per_block = 256 >> ll;
+    const int64_t gr = (M * Nn / 4 + per_block - 1) / per_block;
+    splitk_reduce_kernel<<<(unsigned)gr, 256, 0, st>>>(slab, splits, M, Nn, ll, epi);
+    return hipGetLastError();
+  }
+  Plan p = plan_wgrad(M, Nn, K, slab != nullptr);
   ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
   auto mk_a = [&](auto t) { t.p = dy; t.K = K; t.cols = M; t.ld = Cout; return t; };
   auto mk_b = [&](auto t) { t.x = x; t.g = g; t.K = K; t.cols = Nn; return t; };

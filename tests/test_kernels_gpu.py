@@ -156,6 +156,8 @@ CONV_CASES = [
     (6, 7, 7, 128, 128, 3, 1, 1),       # 3x3 halo path: 128-pixel tiles spanning 3 images
     (2, 28, 28, 128, 128, 3, 1, 1),     # 3x3 halo path (layer2 shape), 2 source-channel chunks
     (3, 9, 13, 64, 128, 3, 1, 1),       # halo fwd (its dgrad, 64 out channels, stays implicit GEMM)
+    (2, 5, 30, 64, 64, 3, 1, 1),        # all-taps 3x3 wgrad: 2 rows per K-step, a 1-row last group
+    (3, 4, 56, 128, 64, 3, 1, 1),       # all-taps 3x3 wgrad: 1 row per K-step, 2 input-channel blocks
 ]
 
 
