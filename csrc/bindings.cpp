@@ -5,6 +5,9 @@
 // and raise on any HIP error.  Runtime bindings (TCP store, bucket reducer, host ring) are CPU-only.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
+
+#include <map>
+#include <mutex>
 #include <c10/core/DeviceGuard.h>
 
 #include "pda_kernels.h"
@@ -269,6 +272,20 @@ Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> ga
   return y;
 }
 
+// In-launch BN-backward finalize (batchnorm.hip:bwd_fused_finish) for C <= this threshold.  Default 0
+// (off): measured on ResNet-50 bs 640 (profiles/r2_bn_bwd_fused_finalize_DROPPED.jsonl) it is neutral
+// for C <= 256 and -1.2 % at 2048 (the atomic adds of ~1024 blocks into a few table rows contend at the
+// memory side); the separate finalize launch's long dispatch waits beside the side-stream wgrads are
+// time the GPU spends on those wgrads anyway.  PDA_BN_BWD_FUSED_MAXC or set_bn_bwd_fused_max_c().
+int64_t& bn_bwd_fused_max_c() {
+  static int64_t v = [] {
+    const char* e = getenv("PDA_BN_BWD_FUSED_MAXC");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  return v;
+}
+void set_bn_bwd_fused_max_c(int64_t c) { bn_bwd_fused_max_c() = c; }
+
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::optional<Tensor> ss, Tensor mean,
                            Tensor invstd, c10::optional<Tensor> gamma, bool relu, bool want_dres,
                            c10::optional<Tensor> dgamma_out, c10::optional<Tensor> dbeta_out) {
@@ -305,14 +322,36 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::op
   check_gpu(dgamma, "dgamma");
   check_gpu(dbeta, "dbeta");
   const bool pb = pdt == at::kBFloat16;
-  Tensor ws = at::empty({pda::bn_workspace_floats(M, C)}, x.options().dtype(at::kFloat));
+  // fused finalize for C <= PDA_BN_BWD_FUSED_MAXC (0 -> always the separate finalize launch): a persistent zeroed
+  // table + ticket per (device, stream) — BN backwards on one stream are serialised, and every call
+  // leaves both zero again
+  const bool fused = C <= bn_bwd_fused_max_c();
+  float* fin_table = nullptr;
+  unsigned* fin_ticket = nullptr;
+  const int fin_rows = pda::bn_bwd_table_rows(C);
+  hipStream_t st = stream_of(x);
+  if (fused) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, Tensor> tables;
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_pair((int)x.device().index(), st);
+    auto it = tables.find(key);
+    if (it == tables.end()) {
+      // [128 rows x 2 x 2048] floats covers every (rows, C) pair; + 16 floats for the ticket
+      it = tables.emplace(key, at::zeros({128 * 2 * 2048 + 16}, x.options().dtype(at::kFloat))).first;
+    }
+    fin_table = it->second.data_ptr<float>();
+    fin_ticket = reinterpret_cast<unsigned*>(fin_table + 128 * 2 * 2048);
+    TORCH_CHECK((int64_t)fin_rows * 2 * C <= 128 * 2 * 2048);
+  }
+  Tensor ws = at::empty({fused ? 3 * C : pda::bn_workspace_floats(M, C)}, x.options().dtype(at::kFloat));
   const float* ssp = (relu && !y.has_value()) ? ss->data_ptr<float>() : nullptr;
   CHECK_HIP_OK(pda::bn_bwd(bp(dy), bp(x), (relu && y.has_value() && !bits) ? bp(*y) : nullptr,
                            bits ? y->data_ptr<uint8_t>() : nullptr, ssp, M, C, mean.data_ptr<float>(),
                            invstd.data_ptr<float>(), gf, gb, relu, bpm(dx), want_dres ? bpm(dres) : nullptr,
                            pb ? nullptr : dgamma.data_ptr<float>(), pb ? bpm(dgamma) : nullptr,
                            pb ? nullptr : dbeta.data_ptr<float>(), pb ? bpm(dbeta) : nullptr, ws.data_ptr<float>(),
-                           stream_of(x)));
+                           fin_table, fin_ticket, fin_rows, st));
   return {dx, dres, dgamma, dbeta};
 }
 
@@ -1065,9 +1104,33 @@ class XgmiComm {
   long long timeout_ticks_ = 0;
   bool opened_ = false;
 };
+// HIP stream at an explicit queue priority (PyTorch's stream pools only reach normal and high; the
+// weight-gradient side stream wants LOW, so the dispatcher hands a freed CU to the critical-path
+// queue first).  Returns the raw handle for torch.cuda.ExternalStream; lives for the process.
+int64_t stream_create(int64_t device, int64_t priority) {
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  int least = 0, greatest = 0;
+  CHECK_HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  int p = (int)priority;
+  // HIP: numerically lower = higher priority; clamp into [greatest, least]
+  if (p > least) p = least;
+  if (p < greatest) p = greatest;
+  hipStream_t s = nullptr;
+  CHECK_HIP_OK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, p));
+  return reinterpret_cast<int64_t>(s);
+}
+
+std::vector<int64_t> stream_priority_range(int64_t device) {
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  int least = 0, greatest = 0;
+  CHECK_HIP_OK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  return {least, greatest};
+}
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
+  m.def("stream_create", &stream_create, py::arg("device"), py::arg("priority"));
+  m.def("stream_priority_range", &stream_priority_range, py::arg("device"));
   m.doc() = "pytorchdistributed_amd native layer: CDNA4 HIP kernels + C++ runtime";
   m.def("sgd_step", &sgd_step);
   m.def("adam_step", &adam_step);
@@ -1078,6 +1141,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_bwd", &bn_bwd);
+  m.def("set_bn_bwd_fused_max_c", &set_bn_bwd_fused_max_c);
+  m.def("bn_bwd_fused_max_c", []() { return bn_bwd_fused_max_c(); });
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("stem_s2d", &stem_s2d);
   m.def("maxpool_bwd", &maxpool_bwd);

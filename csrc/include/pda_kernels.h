@@ -105,7 +105,11 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint
                   int64_t M, int64_t C,
                   const float* save_mean, const float* save_invstd, const float* gamma_f, const bf16_t* gamma_b,
                   bool relu, bf16_t* dx, bf16_t* dres, float* dgamma_f, bf16_t* dgamma_b, float* dbeta_f,
-                  bf16_t* dbeta_b, float* ws, hipStream_t st);
+                  bf16_t* dbeta_b, float* ws, float* fin_table, unsigned* fin_ticket, int fin_rows,
+                  hipStream_t st);
+// fused finalize (fin_table != nullptr): the reduce kernel's last block finalizes in-launch from a
+// persistent zeroed [fin_rows][2][C] table + ticket (left zero); rows for C channels:
+int bn_bwd_table_rows(int64_t C);
 
 // ---- pool.hip (NHWC, C % 8 == 0)
 hipError_t maxpool2d_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int k,

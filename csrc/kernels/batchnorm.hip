@@ -436,14 +436,126 @@ __device__ __forceinline__ void relu_mask(float (&g)[8], const bf16_t* __restric
   }
 }
 
-template <int MASK>
+// In-launch finalize of the backward reduce (replaces bn_bwd_finalize_kernel's separate launch).
+//
+// Why: a wide wgrad GEMM workgroup on the side stream holds 144 KB of LDS and ~470 of a SIMD's 512
+// VGPRs, so a critical-path kernel launched beside it waits for a whole CU to drain; the finalize's
+// 1024-thread workgroups waited longest (9 us alone, ~145 us per call beside the wgrads at bs 640).
+// How: every reduce block adds its per-channel partials into a small persistent table [R][2][C] with
+// no-return float atomics (executed at the memory side, so coherent across the 8 XCDs without
+// fences), drains them (vmcnt(0)) and draws a ticket; the block that draws the last ticket reads AND
+// re-zeroes the table with atomic exchanges (also memory-side: no stale L2 copy can be read), sums
+// the R rows, writes dgamma / dbeta / the apply coefficients and resets the ticket.  The table and
+// ticket are zero on entry (allocated zeroed; every call leaves them zero).
+struct BwdFin {
+  float* table;   // [R][2][C] fp32, zero on entry and exit
+  unsigned* ticket;
+  int R;
+  const float* invstd;
+  const float* gamma_f;
+  const bf16_t* gamma_b;
+  float* dgamma_f;
+  bf16_t* dgamma_b;
+  float* dbeta_f;
+  bf16_t* dbeta_b;
+  float* coef;
+};
+
+__device__ __forceinline__ void bwd_fused_finish(float (&a)[8], float (&b)[8], int tx, int ty, int cols, int rpi,
+                                                 int vcol, int C, int64_t M, const float* __restrict__ mean,
+                                                 const BwdFin& f) {
+  __shared__ float s_a[kThreads * 8];
+  __shared__ float s_b[kThreads * 8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s_a[threadIdx.x * 8 + j] = a[j];
+    s_b[threadIdx.x * 8 + j] = b[j];
+  }
+  __syncthreads();
+  if (ty == 0 && vcol * 8 < C) {
+    for (int k = 1; k < rpi; ++k) {
+      const int t = k * cols + tx;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        a[j] += s_a[t * 8 + j];
+        b[j] += s_b[t * 8 + j];
+      }
+    }
+    float* ra = f.table + (int64_t)(blockIdx.x % f.R) * 2 * C + vcol * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      __hip_atomic_fetch_add(ra + j, a[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(ra + C + j, b[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every adding wave: its adds are performed
+  __syncthreads();
+  unsigned* s_flag = reinterpret_cast<unsigned*>(s_a);
+  if (threadIdx.x == 0)
+    s_flag[0] = __hip_atomic_fetch_add(f.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                gridDim.x * gridDim.y - 1;
+  __syncthreads();
+  if (!s_flag[0]) return;
+  __syncthreads();  // everyone has read the flag before s_a is reused below
+  // last block: thread t sums channel vector (t % cv) over table rows t / cv, t / cv + rpt, ...
+  const int cv = C / 8;
+  const int rpt = kThreads / cv;  // >= 1 (C <= 2048)
+  const int v = threadIdx.x % cv, r0 = threadIdx.x / cv;
+  float sa[8], sb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.f;
+  if (r0 < rpt) {
+    for (int r = r0; r < f.R; r += rpt) {
+      float* ra = f.table + (int64_t)r * 2 * C + v * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sa[j] += __hip_atomic_exchange(ra + j, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sb[j] += __hip_atomic_exchange(ra + C + j, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s_a[threadIdx.x * 8 + j] = sa[j];
+    s_b[threadIdx.x * 8 + j] = sb[j];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(f.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x >= cv) return;
+  for (int k = 1; k < rpt; ++k) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sa[j] += s_a[(k * cv + v) * 8 + j];
+      sb[j] += s_b[(k * cv + v) * 8 + j];
+    }
+  }
+  const float invM = 1.f / (float)M;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = v * 8 + j;
+    const float is = f.invstd[c], mu = mean[c];
+    const float g = param_at(f.gamma_f, f.gamma_b, c, 1.f);
+    const float sdz = sa[j], dg = sb[j] * is;
+    if (f.dgamma_f) f.dgamma_f[c] = dg;
+    if (f.dgamma_b) f.dgamma_b[c] = f2bf(dg);
+    if (f.dbeta_f) f.dbeta_f[c] = sdz;
+    if (f.dbeta_b) f.dbeta_b[c] = f2bf(sdz);
+    const float A = g * is;
+    const float B = -A * is * dg * invM;
+    f.coef[c] = A;
+    f.coef[C + c] = B;
+    f.coef[2 * C + c] = -A * sdz * invM - B * mu;
+  }
+}
+
+template <int MASK, bool FUSED>
 __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy,
                                                                  const bf16_t* __restrict__ x,
                                                                  const bf16_t* __restrict__ y,
                                                                  const float* __restrict__ ss,
                                                                  const float* __restrict__ mean, int64_t M, int C,
                                                                  int cols, int rpi, int64_t rpb,
-                                                                 float* __restrict__ slab) {
+                                                                 float* __restrict__ slab, BwdFin fin) {
   const int tx = threadIdx.x % cols, ty = threadIdx.x / cols;
   const int vcol = blockIdx.y * cols + tx;
   const bool active = ty < rpi && vcol * 8 < C;
@@ -503,7 +615,8 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* _
       }
     }
   }
-  block_col_reduce_store(sa, sb, tx, ty, cols, rpi, vcol, C, slab, slab + (int64_t)gridDim.x * C);
+  if constexpr (FUSED) bwd_fused_finish(sa, sb, tx, ty, cols, rpi, vcol, C, M, mean, fin);
+  else block_col_reduce_store(sa, sb, tx, ty, cols, rpi, vcol, C, slab, slab + (int64_t)gridDim.x * C);
 }
 
 // dgamma = invstd * sum(dz (x-mean)), dbeta = sum(dz);  coefficients for dx = A*dz + B*x + Cc
@@ -706,6 +819,14 @@ hipError_t launch_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M
 
 }  // namespace
 
+// rows of the fused-finalize table for C channels: enough rows that the ~1024 reduce blocks' atomic
+// adds do not pile onto a few hundred bytes (8 K floats per slab), few enough that the last block's
+// exchange sweep stays short
+int bn_bwd_table_rows(int64_t C) {
+  int r = (int)(8192 / (C > 0 ? C : 1));
+  return r < 8 ? 8 : (r > 128 ? 128 : r);
+}
+
 // workspace: 2 partial slabs [nrb][C] + 3 per-channel tables [C]
 int64_t bn_workspace_floats(int64_t M, int64_t C) {
   BnGeom g = bn_geom(M, C);
@@ -762,27 +883,40 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint
                   int64_t M, int64_t C,
                   const float* save_mean, const float* save_invstd, const float* gamma_f, const bf16_t* gamma_b,
                   bool relu, bf16_t* dx, bf16_t* dres, float* dgamma_f, bf16_t* dgamma_b, float* dbeta_f,
-                  bf16_t* dbeta_b, float* ws, hipStream_t st) {
+                  bf16_t* dbeta_b, float* ws, float* fin_table, unsigned* fin_ticket, int fin_rows, hipStream_t st) {
   if (C > kMaxC || C % 8) return hipErrorInvalidValue;
   if (relu && !y && !ss && !relu_bits) return hipErrorInvalidValue;
+  if (fin_table && (fin_rows < 1 || !fin_ticket)) return hipErrorInvalidValue;
   BnGeom g = bn_geom(M, C);
-  float* coef = ws + 2 * (int64_t)g.nrb * C;
+  // fused finalize: ws holds only the 3 coefficient tables (no slabs)
+  float* coef = fin_table ? ws : ws + 2 * (int64_t)g.nrb * C;
+  if (fin_table && g.gy != 1) return hipErrorInvalidValue;
   const int mask = !relu ? 0 : (relu_bits ? 3 : (y ? 1 : 2));
   if (mask == 3) y = reinterpret_cast<const bf16_t*>(relu_bits);  // the mask kernels index it as bytes
   const dim3 rg(g.nrb, g.gy);
-  if (mask == 0)
-    bn_bwd_reduce_kernel<0><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
-  else if (mask == 1)
-    bn_bwd_reduce_kernel<1><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
-  else if (mask == 2)
-    bn_bwd_reduce_kernel<2><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
-  else
-    bn_bwd_reduce_kernel<3><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, g.rpb, ws);
+  BwdFin fin{fin_table, fin_ticket, fin_rows, save_invstd, gamma_f, gamma_b, dgamma_f, dgamma_b, dbeta_f, dbeta_b, coef};
+  const bool fused = fin_table != nullptr;
+#define BWD_REDUCE(MK)                                                                                       \
+  do {                                                                                                       \
+    if (fused)                                                                                               \
+      bn_bwd_reduce_kernel<MK, true><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols, g.rpi, \
+                                                             g.rpb, ws, fin);                                \
+    else                                                                                                     \
+      bn_bwd_reduce_kernel<MK, false><<<rg, kThreads, 0, st>>>(dy, x, y, ss, save_mean, M, (int)C, g.cols,     \
+                                                              g.rpi, g.rpb, ws, fin);                        \
+  } while (0)
+  if (mask == 0) BWD_REDUCE(0);
+  else if (mask == 1) BWD_REDUCE(1);
+  else if (mask == 2) BWD_REDUCE(2);
+  else BWD_REDUCE(3);
+#undef BWD_REDUCE
   PDA_CHECK_HIP(hipGetLastError());
-  bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(ws, g.nrb, M, (int)C, save_mean,
-                                                                         save_invstd, gamma_f, gamma_b, dgamma_f,
-                                                                         dgamma_b, dbeta_f, dbeta_b, coef);
-  PDA_CHECK_HIP(hipGetLastError());
+  if (!fused) {
+    bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(ws, g.nrb, M, (int)C, save_mean,
+                                                                           save_invstd, gamma_f, gamma_b, dgamma_f,
+                                                                           dgamma_b, dbeta_f, dbeta_b, coef);
+    PDA_CHECK_HIP(hipGetLastError());
+  }
   int ns = lds_tables_forced() ? 0 : wave_sets((int)(C / 8));
   if (ns == 3 || ns > 4) ns = 0;
   const int grid = ns ? wave_grid(M * C / 8) : ew_grid(M * C / 8);

@@ -8,6 +8,7 @@ backward.  Weak scaling: the per-GPU batch is fixed.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import os
 
 import torch
@@ -60,9 +61,15 @@ def main(argv=None):
     rank, world, local, device = setup(a.gpus)
     if device.type == "cpu":  # plumbing-only run on a machine without a GPU
         a.batch, a.image = min(a.batch, 2), min(a.image, 64)
-    _, _, step = build(a.batch, a.image, device, rank, bucket_mb=a.bucket_mb)
-    losses = []
-    secs = timed(lambda: losses.append(step()), a.steps, a.warmup)
+    # PDA_MAIN_PRIO=high: the whole step on a high-priority HIP stream (A/B knob for queue arbitration
+    # against the low-priority weight-gradient side stream, ops/streams.py)
+    ctx = contextlib.nullcontext()
+    if device.type == "cuda" and os.environ.get("PDA_MAIN_PRIO") == "high":
+        ctx = torch.cuda.stream(torch.cuda.Stream(device=device, priority=-1))
+    with ctx:
+        _, _, step = build(a.batch, a.image, device, rank, bucket_mb=a.bucket_mb)
+        losses = []
+        secs = timed(lambda: losses.append(step()), a.steps, a.warmup)
     # (after the timed window) a benchmark that diverged would be measuring garbage
     last = float(losses[-1].item())
     if last != last or abs(last) == float("inf"):

@@ -45,11 +45,29 @@ def set_enabled(flag) -> None:
     _enabled_override = flag
 
 
+def side_priority() -> str:
+    """Queue priority of the side stream: ``normal`` (default) or ``low`` (``PDA_WGRAD_PRIO``).
+
+    A wgrad GEMM wave holds a whole SIMD's register file, so a critical-path kernel launched while
+    wgrad tiles are resident waits for a CU to drain; at equal priority the dispatcher often refills
+    that CU from the side queue first (BN-backward finalize: 9 us alone, ~105 us beside the wgrads).
+    Measured on ResNet-50 bs 640 (profiles/r2_stream_priority_ab.jsonl): low / normal side queue x
+    high / normal main stream all within 0.5 % — HIP queue priority does not reorder CU dispatch
+    here, so the default stays the plain pool stream."""
+    return os.environ.get("PDA_WGRAD_PRIO", "normal")
+
+
 def side_stream(device: torch.device) -> torch.cuda.Stream:
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _streams.get(idx)
     if s is None:
-        s = torch.cuda.Stream(device=idx)
+        if side_priority() == "low":
+            from .._native import C
+
+            lo, _hi = C().stream_priority_range(idx)
+            s = torch.cuda.ExternalStream(C().stream_create(idx, lo), device=torch.device("cuda", idx))
+        else:
+            s = torch.cuda.Stream(device=idx)
         _streams[idx] = s
     return s
 

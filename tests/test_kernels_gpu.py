@@ -280,6 +280,47 @@ def test_batchnorm_train(shape, relu, res):
             assert rel_err(dres.cpu(), rr.grad) < 1e-2
 
 
+def test_batchnorm_bwd_fused_finalize_reuse():
+    """The in-launch finalize's persistent [R][2][C] table and ticket must be left zero by every call:
+    back-to-back backwards of different widths (table rows R = 8192 / C, clamped to 8..128) on the
+    default stream and on a second stream (its own table) all match the fp32 reference."""
+    torch.manual_seed(5)
+    cases = []
+    for shape in [(4, 6, 6, 64), (2, 7, 7, 2048), (3, 5, 5, 200), (4, 6, 6, 64), (1, 9, 9, 1024)]:
+        Cc = shape[-1]
+        x = (torch.randn(shape) * 2 + 0.5).to(torch.bfloat16).float()
+        g = torch.rand(Cc) + 0.5
+        dy = torch.randn(shape).to(torch.bfloat16).float()
+        xr, gr, br = x.clone().requires_grad_(), g.clone().requires_grad_(), torch.zeros(Cc, requires_grad=True)
+        y = F.batch_norm(xr.reshape(-1, Cc), None, None, gr, br, True, 0.1, 1e-5).reshape(shape)
+        y.backward(dy)
+        cases.append((x, g, dy, xr.grad, gr.grad, br.grad))
+    side = torch.cuda.Stream()
+    prev = C().bn_bwd_fused_max_c()
+    C().set_bn_bwd_fused_max_c(2048)
+    try:
+        _fused_finalize_cases(cases, side)
+    finally:
+        C().set_bn_bwd_fused_max_c(prev)
+
+
+def _fused_finalize_cases(cases, side):
+    for rep in range(3):
+        for i, (x, g, dy, dx_ref, dg_ref, db_ref) in enumerate(cases):
+            Cc = x.shape[-1]
+            stream = side if (rep + i) % 2 else torch.cuda.current_stream()
+            with torch.cuda.stream(stream):
+                _, mean, invstd, _, _ = C().bn_fwd_train(bf(x), None, g.to(DEV), torch.zeros(Cc, device=DEV),
+                                                         torch.zeros(Cc, device=DEV), torch.ones(Cc, device=DEV),
+                                                         0.1, 1e-5, False, False, None)
+                dx, _, dgamma, dbeta = C().bn_bwd(bf(dy), bf(x), None, None, mean, invstd, g.to(DEV), False, False,
+                                                  None, None)
+            torch.cuda.synchronize()
+            assert rel_err(dx.cpu(), dx_ref) < 2e-2, (rep, i)
+            assert rel_err(dgamma.cpu(), dg_ref) < 1e-2, (rep, i)
+            assert rel_err(dbeta.cpu(), db_ref) < 1e-2, (rep, i)
+
+
 def test_batchnorm_eval():
     x = torch.randn(2, 4, 4, 64)
     g, b = torch.rand(64) + 0.5, torch.randn(64)
