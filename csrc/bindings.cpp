@@ -456,6 +456,34 @@ void gemm(Tensor A, bool a_kmajor, int64_t lda, Tensor B, bool b_kmajor, int64_t
                               slab_n > 0 ? slab.data_ptr<float>() : nullptr, slab_n > 0, stream_of(A)));
 }
 
+// GEMM with a fused GELU-tanh epilogue (bf16 C [M, ldc]):
+//   act 1 (forward):  C = gelu(A B + bias) and aux = A B + bias (the pre-activation the backward needs)
+//   act 2 (backward): C = (A B) * gelu'(aux), aux = that pre-activation
+void gemm_act(Tensor A, bool a_kmajor, int64_t lda, Tensor B, bool b_kmajor, int64_t ldb, Tensor C, int64_t ldc,
+              int64_t M, int64_t N, int64_t K, c10::optional<Tensor> bias, int64_t act, Tensor aux) {
+  check_bf16(A, "A");
+  check_bf16(B, "B");
+  check_bf16(C, "C");
+  check_bf16(aux, "aux");
+  TORCH_CHECK(act == 1 || act == 2, "act must be 1 (gelu fwd) or 2 (gelu bwd)");
+  TORCH_CHECK(N % 8 == 0 && ldc % 8 == 0, "gemm_act needs N and ldc multiples of 8");
+  TORCH_CHECK((!a_kmajor && !b_kmajor) || K % 8 == 0, "gemm with a K-major operand needs K % 8 == 0");
+  TORCH_CHECK(a_kmajor || M % 8 == 0, "M-major A needs M % 8 == 0");
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0, "leading dims must be 16-byte multiples");
+  TORCH_CHECK((a_kmajor ? (M - 1) * lda + K : (K - 1) * lda + M) <= A.numel(), "A too small");
+  TORCH_CHECK((b_kmajor ? (N - 1) * ldb + K : (K - 1) * ldb + N) <= B.numel(), "B too small");
+  TORCH_CHECK((M - 1) * ldc + N <= C.numel() && (M - 1) * ldc + N <= aux.numel(), "C / aux too small");
+  for (auto* t : {&A, &B, &C, &aux}) check_aligned16(*t, "gemm_act operand");
+  if (bias) {
+    check_f32_or_bf16(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N && act == 1, "bias only with the forward activation");
+  }
+  c10::DeviceGuard g(A.device());
+  CHECK_HIP_OK(pda::gemm_bf16_act(bp(A), a_kmajor, lda, bp(B), b_kmajor, ldb, bpm(C), ldc, M, N, K,
+                                  bias ? bias->data_ptr() : nullptr, bias ? !is_bf16(*bias) : false, (int)act,
+                                  bpm(aux), stream_of(A)));
+}
+
 void conv_check(const Tensor& x, const Tensor& w) {
   check_bf16(x, "x");
   check_bf16(w, "w");
@@ -1151,6 +1179,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("fill_random", &fill_random);
   m.def("fill_randint", &fill_randint);
   m.def("gemm", &gemm);
+  m.def("gemm_act", &gemm_act);
   m.def("set_gemm_paths", &pda::set_gemm_paths, "force a GEMM kernel path: wide=-1 env default, 0 off, 1 auto, 2 force",
         pybind11::arg("wide"), pybind11::arg("variant") = -1);
   m.def("conv_fwd", &conv_fwd);

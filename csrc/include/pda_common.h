@@ -122,4 +122,27 @@ __device__ __forceinline__ void grouped_tile(int tile, int tiles_m, int tiles_n,
   tn = r / rows;
 }
 
+// GELU (tanh approximation, GPT-2's gelu_new) and its derivative: shared by the elementwise kernels
+// (act.hip) and the GEMM epilogues that fuse them (gemm_conv.hip, act = 1 / 2).  Written with the
+// identity 0.5 (1 + tanh(u)) = sigmoid(2u) on the bare v_exp_f32 + v_rcp_f32: a few VALU ops per
+// element instead of tanhf's libcall, which a GEMM epilogue (one 512-thread workgroup per CU, 128
+// elements per lane) cannot hide.
+__device__ __forceinline__ float gelu_sig2u(float x, float& du) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float x2 = x * x;
+  const float u2 = 2.f * k0 * fmaf(k1 * x2, x, x);                 // 2u
+  const float s = __frcp_rn(1.f + __builtin_amdgcn_exp2f(-u2 * 1.4426950408889634f));  // sigmoid(2u)
+  du = 2.f * k0 * fmaf(3.f * k1, x2, 1.f);                         // d(2u)/dx
+  return s;
+}
+__device__ __forceinline__ float gelu_tanh(float x) {
+  float du;
+  return x * gelu_sig2u(x, du);
+}
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  float du;
+  const float s = gelu_sig2u(x, du);
+  return fmaf(x * s * (1.f - s), du, s);
+}
+
 }  // namespace pda

@@ -136,6 +136,10 @@ int64_t gemm_slab_floats(int64_t M, int64_t N, int64_t K, bool allow_split);
 hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
                      void* C, bool c_f32, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
                      bool bias_f32, bool relu, float* slab, bool allow_split, hipStream_t st);
+// act 1: C = gelu_tanh(A B + bias), act_aux = A B + bias (pre-activation); act 2: C = (A B) * gelu_tanh'(act_aux)
+hipError_t gemm_bf16_act(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
+                         bf16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias, bool bias_f32,
+                         int act, bf16_t* act_aux, hipStream_t st);
 int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, int S, int P, int Q);
 // stats (optional): BatchNorm sums of the output accumulated (atomically; must start zeroed) into a
 // [stats_rows][2][Cout] fp32 table: sum(y - K) and sum((y - K)^2) with K = stats_shift (e.g. the running

@@ -14,17 +14,6 @@ inline int grid_for(int64_t n8) {
   return g < 1 ? 1 : (int)g;
 }
 
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
-}
-__device__ __forceinline__ float gelu_tanh_grad(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  const float t = tanhf(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
-}
 __device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
 
 // op: 0 relu, 1 gelu_tanh

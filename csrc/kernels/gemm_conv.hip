@@ -423,7 +423,25 @@ struct Epi {
   float* stats;
   const float* stats_shift;
   int stats_rows;
+  // optional fused activation of a bf16 output (staged epilogues; no split-K): 1 = GELU-tanh forward,
+  // the pre-activation written to act_aux (C's layout) for the backward; 2 = GELU-tanh backward,
+  // C = (A B) * gelu'(act_aux) with act_aux the forward's pre-activation (the MLP's fc2 dgrad fused
+  // with the activation backward: no separate elementwise pass over two [tokens, 4d] tensors)
+  int act;
+  bf16_t* act_aux;
 };
+
+__device__ __forceinline__ void epi_act8(const Epi& e, int64_t crow, int64_t n, u16x8& v) {
+  if (e.act == 1) {
+    *reinterpret_cast<u16x8*>(e.act_aux + crow * e.ldc + n) = v;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = f2bf(gelu_tanh(bf2f(v[q])));
+  } else if (e.act == 2) {
+    const u16x8 h = *reinterpret_cast<const u16x8*>(e.act_aux + crow * e.ldc + n);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) * gelu_tanh_grad(bf2f(h[q])));
+  }
+}
 
 // One workgroup's column partials (8 consecutive columns per thread, `cpr` column chunks per row,
 // `nt` threads): fold the lanes of a wave that share a chunk, then the waves through `red` (nt/64 x
@@ -573,6 +591,7 @@ __device__ __forceinline__ void tile_epilogue_bf16(const f32x4 (&acc)[BM / 32][B
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
     }
+    if (epi.act) epi_act8(epi, crow, n, v);
     if (want_stats) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -1114,6 +1133,7 @@ __global__ void __launch_bounds__(BIG_NT, 1) gemm_big_kernel(LA la, LB lb, int64
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
     }
+    if (epi.act) epi_act8(epi, crow, n, v);
     *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
   }
 }
@@ -1347,6 +1367,7 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
     }
+    if (epi.act) epi_act8(epi, crow, n, v);
     if (want_stats) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -1734,6 +1755,26 @@ hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* 
   if (a_kmajor) return dispatch_bn<PlainK, PlainMN>(M, N, K, p, epi, slab, st, mk_ak, mk_bmn);
   if (b_kmajor) return dispatch_bn<PlainMN, PlainK>(M, N, K, p, epi, slab, st, mk_amn, mk_bk);
   return dispatch_bn<PlainMN, PlainMN>(M, N, K, p, epi, slab, st, mk_amn, mk_bmn);
+}
+
+// gemm_bf16 with a fused GELU epilogue (Epi::act): bf16 C, no split-K (the activation lives in the
+// staged epilogues of the 128 / 256x128 / 256x256 tiles, not in splitk_reduce_kernel).
+hipError_t gemm_bf16_act(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
+                         bf16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias, bool bias_f32,
+                         int act, bf16_t* act_aux, hipStream_t st) {
+  if ((act != 1 && act != 2) || !act_aux || N % 8 || ldc % 8) return hipErrorInvalidValue;
+  Plan p = plan_gemm(M, N, K, false, 512);
+  Epi epi{C, ldc, 0, bias, bias_f32 ? 1 : 0, 0, nullptr};
+  epi.act = act;
+  epi.act_aux = act_aux;
+  auto mk_ak = [&](auto t) { t.p = A; t.rows = M; t.K = K; t.ld = lda; return t; };
+  auto mk_amn = [&](auto t) { t.p = A; t.K = K; t.cols = M; t.ld = lda; return t; };
+  auto mk_bk = [&](auto t) { t.p = B; t.rows = N; t.K = K; t.ld = ldb; return t; };
+  auto mk_bmn = [&](auto t) { t.p = B; t.K = K; t.cols = N; t.ld = ldb; return t; };
+  if (a_kmajor && b_kmajor) return dispatch_bn<PlainK, PlainK>(M, N, K, p, epi, nullptr, st, mk_ak, mk_bk);
+  if (a_kmajor) return dispatch_bn<PlainK, PlainMN>(M, N, K, p, epi, nullptr, st, mk_ak, mk_bmn);
+  if (b_kmajor) return dispatch_bn<PlainMN, PlainK>(M, N, K, p, epi, nullptr, st, mk_amn, mk_bk);
+  return dispatch_bn<PlainMN, PlainMN>(M, N, K, p, epi, nullptr, st, mk_amn, mk_bmn);
 }
 
 

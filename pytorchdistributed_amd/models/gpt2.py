@@ -71,7 +71,7 @@ class GPT2Block(tnn.Module):
         a = ops.attention_qkv(qkv, self.n_head, self.n_head, causal=True)
         h, n = ops.add_norm_train(h, self.attn_proj(a.reshape(B, T, d)), self.ln_2.weight, self.ln_2.bias,
                                   self.ln_2.eps, rms=False)
-        y = self.mlp_proj(ops.gelu_tanh(self.c_fc(n)))
+        y = ops.mlp_gelu(n, self.c_fc.weight, self.c_fc.bias, self.mlp_proj.weight, self.mlp_proj.bias)
         return (h, y) if pending else h + y
 
     @torch.no_grad()

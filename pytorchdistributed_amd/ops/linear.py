@@ -29,6 +29,7 @@ def _mfma_ok(x2, w):
 
 _SIDE_MAX_NUMEL = 256 * 256 * 256  # 256 CUs x one 256x256 tile
 _BLAS_MIN_WORK = 1 << 27  # M*N*K below this: launch-latency bound, the native kernel is as good
+_WGRAD_BLAS_MIN_OUT = int(os.environ.get("PDA_WGRAD_BLAS_MIN_OUT", "0"))
 
 
 def _use_blas(a, b, M, N, K) -> bool:
@@ -80,7 +81,12 @@ def _gemm_wgrad(dy, x2, out_dtype, target=None):
     dw = target if target is not None else torch.empty(N, K, device=dy.device, dtype=out_dtype)
     if M == 0:
         return dw.zero_()
-    if dw.dtype == dy.dtype and _use_blas(dy, x2, M, N, K):
+    # PDA_WGRAD_BLAS_MIN_OUT > 0: hipBLASLt only for weight gradients with at least that many outputs.
+    # In isolation the native tile wins below 4M outputs (GPT-2-medium proj / qkv at 32K tokens: 660 /
+    # 694 vs 350 / 584 TFLOP/s, profiles/r2_gpt2_gemm_shapes.jsonl), but inside the step, beside the
+    # critical-path kernels on the side stream, it cost 1 % (profiles/r2_gpt2_mlp_fused_ab.jsonl):
+    # default 0 = the library for every large plain GEMM
+    if dw.dtype == dy.dtype and N * K >= _WGRAD_BLAS_MIN_OUT and _use_blas(dy, x2, M, N, K):
         return torch.mm(dy.t(), x2, out=dw)
     if dy.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and N % 8 == 0 and K % 8 == 0:
         # dw[N,K] = dy^T x: A(m=n, k=r) = dy[r*N + n] (MN-major), B(k=r, col) = x[r*K + col] (MN-major)
@@ -88,6 +94,32 @@ def _gemm_wgrad(dy, x2, out_dtype, target=None):
     else:
         C().simt_gemm(dy, 1, N, x2, K, 1, dw, K, 1, N, K, M, None, False, 0.0)
     return dw
+
+
+def _param_grads(dy2, x2, wparam, bparam, need_w, need_b):
+    """Weight and bias gradients of ``y = x W^T + b`` (dy2 [M, N], x2 [M, K]), written into the flat
+    gradient buffers when the parameters have them."""
+    dw = db = None
+    if need_w:
+        target = grad_target(wparam)
+        if target is not None and _streams.enabled() and target.numel() < _SIDE_MAX_NUMEL:
+            # written straight into the flat gradient slot: run it beside the critical path
+            # (ops/streams.py; same contract as the conv weight gradient).  A dW with a full wave
+            # of 256x256 output tiles per CU fills the chip by itself; beside other work it only
+            # adds interference (Llama-3-8B FSDP: -2.4 %; GPT-2-medium DDP, 1-16 tiles + split-K:
+            # +9.9 %, profiles/r2_wgrad_stream_transformers.jsonl)
+            # (the bias gradient stays on the compute stream: as a side-stream column sum its
+            # hundreds of memory-bound workgroups delayed the critical-path dgrad GEMMs — GPT-2-medium
+            # 55.7 -> 57.0 ms/step, profiles/r2_gpt2_addnorm_ab.md)
+            with _streams.wgrad_stream(dy2.device, dy2, x2):
+                dw = _gemm_wgrad(dy2, x2, wparam.dtype, target)
+        else:
+            dw = _gemm_wgrad(dy2, x2, wparam.dtype, target)
+    if need_b:
+        tb = grad_target(bparam)
+        db = C().colsum(dy2)
+        db = tb.copy_(db) if tb is not None else db.to(bparam.dtype)
+    return dw, db
 
 
 class _LinearFn(torch.autograd.Function):
@@ -113,26 +145,69 @@ class _LinearFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = _gemm_dgrad(dy2, w).reshape(ctx.shape)
-        if ctx.needs_input_grad[1]:
-            target = grad_target(ctx.wparam)
-            if target is not None and _streams.enabled() and target.numel() < _SIDE_MAX_NUMEL:
-                # written straight into the flat gradient slot: run it beside the critical path
-                # (ops/streams.py; same contract as the conv weight gradient).  A dW with a full wave
-                # of 256x256 output tiles per CU fills the chip by itself; beside other work it only
-                # adds interference (Llama-3-8B FSDP: -2.4 %; GPT-2-medium DDP, 1-16 tiles + split-K:
-                # +9.9 %, profiles/r2_wgrad_stream_transformers.jsonl)
-                # (the bias gradient stays on the compute stream: as a side-stream column sum its
-                # hundreds of memory-bound workgroups delayed the critical-path dgrad GEMMs — GPT-2-medium
-                # 55.7 -> 57.0 ms/step, profiles/r2_gpt2_addnorm_ab.md)
-                with _streams.wgrad_stream(dy2.device, dy2, x2):
-                    dw = _gemm_wgrad(dy2, x2, w.dtype, target)
-            else:
-                dw = _gemm_wgrad(dy2, x2, w.dtype, target)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            tb = grad_target(ctx.bparam)
-            db = C().colsum(dy2)
-            db = tb.copy_(db) if tb is not None else db.to(ctx.bparam.dtype)
+        dw, db = _param_grads(dy2, x2, ctx.wparam, ctx.bparam if ctx.has_bias else None,
+                              ctx.needs_input_grad[1], ctx.has_bias and ctx.needs_input_grad[2])
         return dx, dw, db, None
+
+
+class _MlpGeluFn(torch.autograd.Function):
+    """``fc2(gelu_tanh(fc1(x)))`` with the activation inside the GEMM epilogues: the fc1 forward writes
+    the pre-activation h and g = gelu(h) in one pass, and the fc2 data gradient is produced as
+    ``(dy W2) * gelu'(h)`` (gemm_conv.hip Epi::act) — no elementwise pass over the two [tokens, 4d]
+    tensors in either direction."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        ctx.params = (w1, b1, w2, b2)  # the parameters themselves: grad_target finds their flat slots
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        w1, w2 = w1.contiguous(), w2.contiguous()
+        M, K = x2.shape
+        F_ = w1.shape[0]
+        h = torch.empty(M, F_, device=x.device, dtype=x.dtype)
+        g = torch.empty_like(h)
+        if M > 0:
+            C().gemm_act(x2, True, K, w1, True, K, g, F_, M, F_, K, b1, 1, h)
+        y = _gemm_fwd(g, w2, b2, False)
+        ctx.save_for_backward(x2, w1, h, g, w2)
+        ctx.shape = shape
+        return y.reshape(*shape[:-1], w2.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w1, h, g, w2 = ctx.saved_tensors
+        pw1, pb1, pw2, pb2 = ctx.params
+        N = w2.shape[0]
+        dy2 = dy.reshape(-1, N).contiguous()
+        M, F_ = h.shape
+        # fc2 data gradient fused with the GELU backward: dh = (dy W2) * gelu'(h)
+        dh = torch.empty_like(h)
+        if M > 0:
+            C().gemm_act(dy2, True, N, w2, False, F_, dh, F_, M, F_, N, None, 2, h)
+        dw2, db2 = _param_grads(dy2, g, pw2, pb2, ctx.needs_input_grad[3], pb2 is not None and ctx.needs_input_grad[4])
+        dx = _gemm_dgrad(dh, w1).reshape(ctx.shape) if ctx.needs_input_grad[0] else None
+        dw1, db1 = _param_grads(dh, x2, pw1, pb1, ctx.needs_input_grad[1], pb1 is not None and ctx.needs_input_grad[2])
+        return dx, dw1, db1, dw2, db2
+
+
+def mlp_fused_ok(x, w1, w2) -> bool:
+    """The fused GELU MLP applies: GPU bf16, widths multiples of 8, ``PDA_MLP_FUSED=1``.  Off by default:
+    on GPT-2-medium (32 x 1024 tokens) the native tile's fc1 forward / fc2 dgrad run at ~85 % of
+    hipBLASLt's rate and the 256x256 tile's epilogue (one workgroup per CU, a second [tokens, 4d]
+    stream in it) is exposed, which outweighs the two elementwise passes it removes: 303-305k vs
+    311-312k tokens/s same box (profiles/r2_gpt2_mlp_fused_ab.jsonl)."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and _mfma_ok(x, w1) and _mfma_ok(x, w2)
+            and os.environ.get("PDA_MLP_FUSED", "0") == "1")
+
+
+def mlp_gelu(x, w1, b1, w2, b2):
+    """``linear(gelu_tanh(linear(x, w1, b1)), w2, b2)`` — GPT-2's MLP.  GPU bf16: :class:`_MlpGeluFn`
+    (activation fused into the GEMM epilogues); otherwise the unfused composition."""
+    if mlp_fused_ok(x, w1, w2):
+        return _MlpGeluFn.apply(x, w1, b1, w2, b2)
+    from .act import gelu_tanh
+
+    return linear(gelu_tanh(linear(x, w1, b1)), w2, b2)
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias=None, relu: bool = False) -> torch.Tensor:

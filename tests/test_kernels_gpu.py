@@ -126,6 +126,68 @@ def test_gemm_wide_layouts(M, N, K, split, ak, bk, force_wide):
     assert rel_err(out.cpu(), ref) < 1e-5
 
 
+def _gelu_grad_ref(h):
+    k0, k1 = 0.7978845608028654, 0.044715
+    t = torch.tanh(k0 * (h + k1 * h ** 3))
+    return 0.5 * (1 + t) + 0.5 * h * (1 - t * t) * k0 * (1 + 3 * k1 * h * h)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 520, 136), (4096, 1024, 512), (1000, 4096, 256)])
+@pytest.mark.parametrize("wide", [-1, 0, 2])
+def test_gemm_gelu_epilogues(M, N, K, wide):
+    """GEMM with the fused GELU epilogues (128 / 256x128 / 256x256 tiles): act 1 writes
+    gelu(A B + bias) and the pre-activation, act 2 multiplies A B by gelu'(aux)."""
+    torch.manual_seed(11)
+    A, W, b = torch.randn(M, K), torch.randn(N, K) * 0.05, torch.randn(N)
+    C().set_gemm_paths(wide)
+    try:
+        g = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        h = torch.empty_like(g)
+        C().gemm_act(bf(A), True, K, bf(W), True, K, g, N, M, N, K, b.to(DEV), 1, h)
+        pre = A.to(torch.bfloat16).float() @ W.to(torch.bfloat16).float().t() + b
+        assert rel_err(h.cpu(), pre) < 1e-2
+        assert rel_err(g.cpu(), F.gelu(pre, approximate="tanh")) < 1e-2
+        # backward form: dH = (dY W) * gelu'(h), dY [M, K'] K-major, W [K', N] read MN-major
+        Kp = 128
+        dY, W2 = torch.randn(M, Kp), torch.randn(Kp, N) * 0.05
+        dh = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        C().gemm_act(bf(dY), True, Kp, bf(W2), False, N, dh, N, M, N, Kp, None, 2, h)
+        ref = (dY.to(torch.bfloat16).float() @ W2.to(torch.bfloat16).float()) * _gelu_grad_ref(h.cpu().float())
+        assert rel_err(dh.cpu(), ref) < 1e-2
+    finally:
+        C().set_gemm_paths(-1)
+
+
+def test_mlp_gelu_fused_matches_unfused():
+    """ops.mlp_gelu (GELU inside the GEMM epilogues) == linear -> gelu_tanh -> linear, values and all
+    five gradients."""
+    from pytorchdistributed_amd import ops
+    from pytorchdistributed_amd.ops.act import gelu_tanh
+
+    torch.manual_seed(12)
+    d, f, T = 256, 1024, 2 * 384
+    x0 = torch.randn(T, d, device=DEV).to(torch.bfloat16)
+    p0 = [torch.randn(f, d, device=DEV) * 0.05, torch.randn(f, device=DEV) * 0.1,
+          torch.randn(d, f, device=DEV) * 0.03, torch.randn(d, device=DEV) * 0.1]
+    p0 = [t.to(torch.bfloat16) for t in p0]
+    dy = torch.randn(T, d, device=DEV).to(torch.bfloat16)
+    outs, grads = [], []
+    for fused in (True, False):
+        x = x0.clone().requires_grad_()
+        ps = [t.clone().requires_grad_() for t in p0]
+        if fused:
+            y = ops.mlp_gelu(x.view(2, T // 2, d), *ps)
+        else:
+            y = ops.linear(gelu_tanh(ops.linear(x.view(2, T // 2, d), ps[0], ps[1])), ps[2], ps[3])
+        y.backward(dy.view(2, T // 2, d))
+        torch.cuda.synchronize()
+        outs.append(y.detach().float().reshape(T, d))
+        grads.append([x.grad.float()] + [p.grad.float() for p in ps])
+    assert rel_err(outs[0], outs[1]) < 1e-2
+    for a, b in zip(grads[0], grads[1]):
+        assert rel_err(a, b) < 2e-2
+
+
 def test_gemm_bias_relu_bf16_out():
     M, N, K = 257, 136, 96
     A, W, b = torch.randn(M, K), torch.randn(N, K), torch.randn(N)
