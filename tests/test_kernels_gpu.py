@@ -158,11 +158,14 @@ def test_gemm_gelu_epilogues(M, N, K, wide):
         C().set_gemm_paths(-1)
 
 
-def test_mlp_gelu_fused_matches_unfused():
-    """ops.mlp_gelu (GELU inside the GEMM epilogues) == linear -> gelu_tanh -> linear, values and all
-    five gradients."""
+def test_mlp_gelu_fused_matches_unfused(monkeypatch):
+    """ops.mlp_gelu (GELU inside the GEMM epilogues, PDA_MLP_FUSED=1) == linear -> gelu_tanh -> linear,
+    values and all five gradients."""
     from pytorchdistributed_amd import ops
     from pytorchdistributed_amd.ops.act import gelu_tanh
+    from pytorchdistributed_amd.ops.linear import mlp_fused_ok
+
+    monkeypatch.setenv("PDA_MLP_FUSED", "1")
 
     torch.manual_seed(12)
     d, f, T = 256, 1024, 2 * 384
@@ -171,6 +174,7 @@ def test_mlp_gelu_fused_matches_unfused():
           torch.randn(d, f, device=DEV) * 0.03, torch.randn(d, device=DEV) * 0.1]
     p0 = [t.to(torch.bfloat16) for t in p0]
     dy = torch.randn(T, d, device=DEV).to(torch.bfloat16)
+    assert mlp_fused_ok(x0, p0[0], p0[2])
     outs, grads = [], []
     for fused in (True, False):
         x = x0.clone().requires_grad_()
