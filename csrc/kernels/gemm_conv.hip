@@ -1522,11 +1522,27 @@ Plan plan_gemm(int64_t M, int64_t N, int64_t K, bool allow_split, int target_blo
 // per CU (one workgroup per CU leaves every SIMD with a single wave: SQ_WAIT_ANY doubled on the
 // 14x14 3x3 256 layer at 252 workgroups), with the fp32 partial slabs (written + re-read once)
 // capped at 48 MB but always allowing 4 splits.
+// PDA_WGRAD_CUS=n sizes every split-K (weight-gradient) grid for n CUs instead of all 256: the
+// wgrad kernels hold a whole CU per workgroup pair (230-256 VGPRs x 2 waves per SIMD) for their
+// entire one-round lifetime, so a side-stream wgrad sized for the chip locks the main stream's
+// BN / dgrad kernels out of every CU until it drains; fewer, longer-lived split-K workgroups leave
+// 256 - n CUs to the critical path.  ResNet-50 bs 640 (profiles/r2_wgrad_cus_sweep_v26.jsonl, two
+// interleaved passes): 256 -> 11.34k img/s, 128 -> 11.29k, 160 -> 11.43k, 176 -> 11.45k, 184-224 ->
+// 11.47-11.56k (plateau); default 192.
+int wgrad_cus() {
+  static const int n = [] {
+    const char* e = getenv("PDA_WGRAD_CUS");
+    int v = e ? atoi(e) : 192;
+    return v < 16 ? 16 : (v > 256 ? 256 : v);
+  }();
+  return n;
+}
+
 Plan plan_wgrad(int64_t M, int64_t N, int64_t K, bool allow_split) {
   int64_t cap = ((int64_t)48 << 20) / (M * N * 4);
   if (cap > 1024) cap = 1024;
   if (cap < 4) cap = 4;
-  return plan_gemm(M, N, K, allow_split, 512, (int)cap);
+  return plan_gemm(M, N, K, allow_split, 2 * wgrad_cus(), (int)cap);
 }
 
 template <int BM, int BN, class LA, class LB>
@@ -1617,7 +1633,7 @@ bool use_wide(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) {
 int wide_split_count(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   const int ktiles = (int)((K + BK - 1) / BK);
-  int s = (int)(256 / tiles);  // floor: a 257th workgroup would start a second round on one CU
+  int s = (int)(wgrad_cus() / tiles);  // floor: a 257th workgroup would start a second round on one CU
   const int max_s = ktiles / 4 > 1 ? ktiles / 4 : 1;
   int64_t cap = ((int64_t)96 << 20) / (M * N * 4);
   if (cap < 4) cap = 4;
@@ -1871,7 +1887,7 @@ bool wg3_geom(int N, int H, int W, int C, int Cout, int R, int S, int stride, in
   g.tiles_ci = C / 64;
   const int tiles = (Cout / 64) * g.tiles_ci;
   // ~512 workgroups (2 per CU), >= 4 row groups each, fp32 partial slabs capped at 96 MB
-  int splits = 512 / tiles;
+  int splits = 2 * wgrad_cus() / tiles;
   if (splits < 1) splits = 1;
   if (splits > g.groups / 4) splits = g.groups / 4 > 1 ? g.groups / 4 : 1;
   const int64_t per = (int64_t)Cout * 9 * C;
