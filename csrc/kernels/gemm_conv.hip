@@ -1643,9 +1643,17 @@ int wide_split_count(int64_t M, int64_t N, int64_t K) {
 }
 
 // Returns the wide split count (0: keep the 128-tile plan).
+int wgrad_wide_mode() {  // PDA_WGRAD_WIDE=0: split-K GEMMs stay on the 128-tile kernel (A/B knob)
+  static const int m = [] {
+    const char* e = getenv("PDA_WGRAD_WIDE");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return m;
+}
+
 int wide_splits(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) {
   const int mode = wide_mode();
-  if (mode == 0 || p.splits <= 1 || epi.stats || K < 64) return 0;
+  if (mode == 0 || !wgrad_wide_mode() || p.splits <= 1 || epi.stats || K < 64) return 0;
   if (mode == 1) {
     if (M < 256 || N < 256) return 0;
     const double useful = (double)M * N;
