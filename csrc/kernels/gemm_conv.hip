@@ -1538,6 +1538,21 @@ int wgrad_cus() {
   return n;
 }
 
+int env_cus(const char* name) {  // per-kernel-family override of wgrad_cus() (A/B knobs)
+  const char* e = getenv(name);
+  if (!e) return wgrad_cus();
+  int v = atoi(e);
+  return v < 16 ? 16 : (v > 256 ? 256 : v);
+}
+int wide_wgrad_cus() {
+  static const int n = env_cus("PDA_WGRAD_CUS_WIDE");
+  return n;
+}
+int wg3_wgrad_cus() {
+  static const int n = env_cus("PDA_WGRAD_CUS_WG3");
+  return n;
+}
+
 Plan plan_wgrad(int64_t M, int64_t N, int64_t K, bool allow_split) {
   int64_t cap = ((int64_t)48 << 20) / (M * N * 4);
   if (cap > 1024) cap = 1024;
@@ -1633,7 +1648,7 @@ bool use_wide(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) {
 int wide_split_count(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ((M + 255) / 256) * ((N + 255) / 256);
   const int ktiles = (int)((K + BK - 1) / BK);
-  int s = (int)(wgrad_cus() / tiles);  // floor: a 257th workgroup would start a second round on one CU
+  int s = (int)(wide_wgrad_cus() / tiles);  // floor: a 257th workgroup would start a second round on one CU
   const int max_s = ktiles / 4 > 1 ? ktiles / 4 : 1;
   int64_t cap = ((int64_t)96 << 20) / (M * N * 4);
   if (cap < 4) cap = 4;
@@ -1895,7 +1910,7 @@ bool wg3_geom(int N, int H, int W, int C, int Cout, int R, int S, int stride, in
   g.tiles_ci = C / 64;
   const int tiles = (Cout / 64) * g.tiles_ci;
   // ~512 workgroups (2 per CU), >= 4 row groups each, fp32 partial slabs capped at 96 MB
-  int splits = 2 * wgrad_cus() / tiles;
+  int splits = 2 * wg3_wgrad_cus() / tiles;
   if (splits < 1) splits = 1;
   if (splits > g.groups / 4) splits = g.groups / 4 > 1 ? g.groups / 4 : 1;
   const int64_t per = (int64_t)Cout * 9 * C;

@@ -668,3 +668,36 @@ def test_conv_dgrad_masked_addend_paths(case, wide):
         C().set_gemm_paths(-1)
     ref = dx0.float().cpu() + add.float() * mask
     assert rel_err(dx.cpu(), ref) < 1e-2
+
+
+_WGRAD_BUDGET_SCRIPT = r"""
+import math, torch, torch.nn.functional as F
+from pytorchdistributed_amd._native import C
+for N, H, W, Cin, Cout, k, s, p in [(8, 28, 28, 64, 64, 1, 1, 0), (2, 28, 28, 128, 128, 3, 1, 1),
+                                    (4, 14, 14, 256, 512, 3, 1, 1), (3, 7, 7, 512, 2048, 1, 1, 0)]:
+    torch.manual_seed(3)
+    x = torch.randn(N, H, W, Cin).to(torch.bfloat16).float()
+    w = (torch.randn(Cout, k, k, Cin) / math.sqrt(Cin * k * k)).to(torch.bfloat16).float().requires_grad_()
+    y = F.conv2d(x.permute(0, 3, 1, 2), w.permute(0, 3, 1, 2), None, s, p).permute(0, 2, 3, 1)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    bf = lambda t: t.to("cuda", torch.bfloat16).contiguous()
+    dw = C().conv_wgrad(bf(dy), bf(x), k, k, s, p, 1, True, None).cpu()
+    err = ((dw - w.grad).norm() / w.grad.norm()).item()
+    assert err < 1e-3, (N, H, W, Cin, Cout, k, err)
+print("budget ok")
+"""
+
+
+@pytest.mark.parametrize("env", [{"PDA_WGRAD_CUS": "48"}, {"PDA_WGRAD_CUS": "256", "PDA_WGRAD_CUS_WG3": "32"}])
+def test_conv_wgrad_cu_budgets(env):
+    """Split-K weight gradients planned for other CU budgets (PDA_WGRAD_CUS*, read once per process:
+    run in a child) — the split counts and the slab sizing must agree at every budget."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _WGRAD_BUDGET_SCRIPT], cwd=root, env={**os.environ, **env},
+                       capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "budget ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
