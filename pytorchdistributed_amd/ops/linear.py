@@ -84,8 +84,9 @@ def _gemm_wgrad(dy, x2, out_dtype, target=None):
     # PDA_WGRAD_BLAS_MIN_OUT > 0: hipBLASLt only for weight gradients with at least that many outputs.
     # In isolation the native tile wins below 4M outputs (GPT-2-medium proj / qkv at 32K tokens: 660 /
     # 694 vs 350 / 584 TFLOP/s, profiles/r2_gpt2_gemm_shapes.jsonl), but inside the step, beside the
-    # critical-path kernels on the side stream, it cost 1 % (profiles/r2_gpt2_mlp_fused_ab.jsonl):
-    # default 0 = the library for every large plain GEMM
+    # critical-path kernels on the side stream, it cost 1 % (profiles/r2_gpt2_mlp_fused_ab.jsonl); with
+    # the native split-K grids sized for 192 CUs: 4M -> +0.15 % (noise), every wgrad native -> -4.9 %
+    # (profiles/r2_gpt2_wgrad_native_vs_blas_v27.jsonl): default 0 = the library for every large plain GEMM
     if dw.dtype == dy.dtype and N * K >= _WGRAD_BLAS_MIN_OUT and _use_blas(dy, x2, M, N, K):
         return torch.mm(dy.t(), x2, out=dw)
     if dy.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and N % 8 == 0 and K % 8 == 0:

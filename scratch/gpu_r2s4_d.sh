@@ -10,7 +10,7 @@ for rep in 1 2; do
   IFS=";" read -ra CL <<< "${CFGS:-X=1}"
   for cfg in "${CL[@]}"; do
     i=$((i+1))
-    env $cfg timeout -k 10 150 python bench.py --steps 20 --warmup 5 > gpurun_out/ab_$i.log 2>&1
+    env $cfg timeout -k 10 150 ${BENCH:-python bench.py --steps 20 --warmup 5} > gpurun_out/ab_$i.log 2>&1
     rc=$?
     if [ $rc -ne 0 ]; then echo "rc=$rc at $cfg"; tail -5 gpurun_out/ab_$i.log; exit $rc; fi
     echo "{\"env\": \"$cfg\", \"rep\": $rep, \"bench\": $(grep '^{' gpurun_out/ab_$i.log)}" >> $out
