@@ -251,6 +251,59 @@ std::vector<Tensor> bn_fwd_train_sums(Tensor x, Tensor table, Tensor shift, c10:
   return {y, mean, invstd, ss, bits};
 }
 
+bool bn_dual_ok(int64_t C) { return pda::bn_dual_ok(C); }
+
+// y = relu(bn(x) + bn2(x2)) (bottleneck output with a downsample shortcut), both BNs from their conv
+// epilogues' statistics tables; returns {y, relu bits, mean, invstd, mean2, invstd2}
+std::vector<Tensor> bn_fwd_train_sums_dual(Tensor x, Tensor table, Tensor shift, c10::optional<Tensor> gamma,
+                                           c10::optional<Tensor> beta, Tensor running_mean, Tensor running_var,
+                                           c10::optional<Tensor> num_batches, Tensor x2, Tensor table2,
+                                           Tensor shift2, c10::optional<Tensor> gamma2, c10::optional<Tensor> beta2,
+                                           Tensor running_mean2, Tensor running_var2,
+                                           c10::optional<Tensor> num_batches2, double momentum, double eps) {
+  check_bf16(x, "x");
+  check_bf16(x2, "x2");
+  TORCH_CHECK(x2.sizes() == x.sizes(), "dual BN: both inputs must have one shape");
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(pda::bn_dual_ok(C), "dual BN apply needs the register-table path (C = 8..2048 dividing 512 or 512k)");
+  Tensor tabs[2] = {table, table2}, shifts[2] = {shift, shift2};
+  for (int i = 0; i < 2; ++i) {
+    check_f32(tabs[i], "table");
+    check_f32(shifts[i], "shift");
+    TORCH_CHECK(shifts[i].numel() == C && tabs[i].numel() % (2 * C) == 0 && tabs[i].numel() > 0 &&
+                tabs[i].is_contiguous(), "table must be [R, 2, C]");
+  }
+  check_f32(running_mean, "running_mean");
+  check_f32(running_var, "running_var");
+  check_f32(running_mean2, "running_mean2");
+  check_f32(running_var2, "running_var2");
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty_like(x);
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor stats = at::empty({2, 4, C}, fo);  // per BN: mean, invstd, scale, shift
+  Tensor bits = at::empty({M * C / 8}, x.options().dtype(at::kByte));
+  pda::BnSumsArgs a[2];
+  c10::optional<Tensor> gam[2] = {gamma, gamma2}, bet[2] = {beta, beta2}, nb[2] = {num_batches, num_batches2};
+  Tensor rm[2] = {running_mean, running_mean2}, rv[2] = {running_var, running_var2};
+  for (int i = 0; i < 2; ++i) {
+    bn_param_ptrs(gam[i], &a[i].gamma_f, &a[i].gamma_b, C);
+    bn_param_ptrs(bet[i], &a[i].beta_f, &a[i].beta_b, C);
+    a[i].table = tabs[i].data_ptr<float>();
+    a[i].table_rows = (int)(tabs[i].numel() / (2 * C));
+    a[i].shift = shifts[i].data_ptr<float>();
+    a[i].running_mean = rm[i].data_ptr<float>();
+    a[i].running_var = rv[i].data_ptr<float>();
+    float* st = stats.data_ptr<float>() + (int64_t)i * 4 * C;
+    a[i].save_mean = st;
+    a[i].save_invstd = st + C;
+    a[i].save_ss = st + 2 * C;
+    a[i].num_batches = nbt_ptr(nb[i], x);
+  }
+  CHECK_HIP_OK(pda::bn_fwd_train_sums_dual(bp(x), bp(x2), bpm(y), M, C, a[0], a[1], (float)momentum, (float)eps,
+                                           bits.data_ptr<uint8_t>(), stream_of(x)));
+  return {y, bits, stats[0][0], stats[0][1], stats[1][0], stats[1][1]};
+}
+
 Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
                    Tensor running_mean, Tensor running_var, double eps, bool relu) {
   check_bf16(x, "x");
@@ -1185,6 +1238,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("conv_fwd_stats", &conv_fwd_stats);
   m.def("bn_fwd_train_sums", &bn_fwd_train_sums);
+  m.def("bn_fwd_train_sums_dual", &bn_fwd_train_sums_dual);
+  m.def("bn_dual_ok", &bn_dual_ok);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"),
         py::arg("pad"), py::arg("dil"), py::arg("addend") = py::none(), py::arg("addend_bits") = py::none());
   m.def("conv_wgrad", &conv_wgrad);

@@ -96,6 +96,28 @@ hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int6
                              const float* beta_f, const bf16_t* beta_b, float* running_mean, float* running_var,
                              float momentum, float eps, bool relu, float* save_mean, float* save_invstd,
                              float* save_ss, uint8_t* relu_bits, int64_t* num_batches, hipStream_t st);
+// one BN of bn_fwd_train_sums_dual: its statistics table / shift, affine params, running stats and
+// outputs (save_ss: [2, C] scale then shift)
+struct BnSumsArgs {
+  float* table;
+  int table_rows;
+  const float* shift;
+  const float* gamma_f;
+  const bf16_t* gamma_b;
+  const float* beta_f;
+  const bf16_t* beta_b;
+  float* running_mean;
+  float* running_var;
+  float* save_mean;
+  float* save_invstd;
+  float* save_ss;
+  int64_t* num_batches;
+};
+bool bn_dual_ok(int64_t C);
+// y = relu(bn_a(x) + bn_b(x2)) from two conv-epilogue statistics tables; writes the 1-bit ReLU mask
+hipError_t bn_fwd_train_sums_dual(const bf16_t* x, const bf16_t* x2, bf16_t* y, int64_t M, int64_t C,
+                                  const BnSumsArgs& a, const BnSumsArgs& b, float momentum, float eps,
+                                  uint8_t* relu_bits, hipStream_t st);
 hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,
                        const bf16_t* gamma_b, const float* beta_f, const bf16_t* beta_b, const float* running_mean,
                        const float* running_var, float eps, bool relu, float* ws, hipStream_t st);

@@ -356,22 +356,31 @@ __device__ __forceinline__ uint32_t bn_apply8(float (&a)[8], const float (&xv)[8
   return m;
 }
 
-template <bool RES, bool RELU, int NS>
+// RBN: the residual is itself a batch-normalised tensor, res * scale2 + shift2 (a bottleneck's
+// downsample branch applied inside the block's output kernel: its BN output is never stored).
+template <bool RES, bool RELU, int NS, bool RBN = false>
 __global__ void __launch_bounds__(kThreads) bn_apply_wave_kernel(const bf16_t* __restrict__ x,
                                                                  const bf16_t* __restrict__ res,
                                                                  bf16_t* __restrict__ y, int64_t M, int C,
                                                                  const float* __restrict__ scale,
                                                                  const float* __restrict__ shift,
-                                                                 uint8_t* __restrict__ bits) {
+                                                                 uint8_t* __restrict__ bits,
+                                                                 const float* __restrict__ scale2,
+                                                                 const float* __restrict__ shift2) {
   const int cv = C / 8, lane = threadIdx.x & 63;
   const int64_t nvec = M * cv;
   const int64_t tw = (int64_t)gridDim.x * (kThreads / 64);
-  float sc[NS][8], sh[NS][8];
+  constexpr int NS2 = RBN ? NS : 1;
+  float sc[NS][8], sh[NS][8], sc2[NS2][8], sh2[NS2][8];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     const int c0 = ((64 * s + lane) % cv) * 8;
     load8(scale + c0, sc[s]);
     load8(shift + c0, sh[s]);
+    if constexpr (RBN) {
+      load8(scale2 + c0, sc2[s]);
+      load8(shift2 + c0, sh2[s]);
+    }
   }
   int64_t base = ((int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * kWaveVec;
   for (; base + kWaveVec <= nvec; base += tw * kWaveVec) {
@@ -389,7 +398,8 @@ __global__ void __launch_bounds__(kThreads) bn_apply_wave_kernel(const bf16_t* _
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         a[j] = bf2f(xa[u][j]);
-        r[j] = RES ? bf2f(ra[u][j]) : 0.f;
+        if constexpr (RBN) r[j] = fmaf(bf2f(ra[u][j]), sc2[u % NS][j], sh2[u % NS][j]);
+        else r[j] = RES ? bf2f(ra[u][j]) : 0.f;
       }
       w |= bn_apply8<RES, RELU>(o, a, r, sc[u % NS], sh[u % NS]) << (8 * u);
       store8_nt(y + (base + 64 * u + lane) * 8, o);
@@ -407,6 +417,13 @@ __global__ void __launch_bounds__(kThreads) bn_apply_wave_kernel(const bf16_t* _
     load8(shift + c0, h1);
     load8(x + v * 8, a);
     if (RES) load8(res + v * 8, r);
+    if constexpr (RBN) {
+      float s2[8], h2[8];
+      load8(scale2 + c0, s2);
+      load8(shift2 + c0, h2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = fmaf(r[j], s2[j], h2[j]);
+    }
     const uint32_t m = bn_apply8<RES, RELU>(o, a, r, s1, h1);
     if (RELU && bits) bits[v] = (uint8_t)m;
     store8(y + v * 8, o);
@@ -795,10 +812,19 @@ template <int NS>
 void launch_apply_wave(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int C, const float* scale,
                        const float* shift, bool relu, uint8_t* bits, hipStream_t st) {
   const int grid = wave_grid(M * C / 8);
-  if (res && relu) bn_apply_wave_kernel<true, true, NS><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits);
-  else if (res) bn_apply_wave_kernel<true, false, NS><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr);
-  else if (relu) bn_apply_wave_kernel<false, true, NS><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits);
-  else bn_apply_wave_kernel<false, false, NS><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr);
+  const float* n = nullptr;
+  if (res && relu) bn_apply_wave_kernel<true, true, NS><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits, n, n);
+  else if (res) bn_apply_wave_kernel<true, false, NS><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr, n, n);
+  else if (relu) bn_apply_wave_kernel<false, true, NS><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, bits, n, n);
+  else bn_apply_wave_kernel<false, false, NS><<<grid, kThreads, 0, st>>>(x, res, y, M, C, scale, shift, nullptr, n, n);
+}
+
+template <int NS>
+void launch_apply_dual_wave(const bf16_t* x, const bf16_t* x2, bf16_t* y, int64_t M, int C, const float* ss,
+                            const float* ss2, uint8_t* bits, hipStream_t st) {
+  const int grid = wave_grid(M * C / 8);
+  bn_apply_wave_kernel<true, true, NS, true><<<grid, kThreads, 0, st>>>(x, x2, y, M, C, ss, ss + C, bits, ss2,
+                                                                        ss2 + C);
 }
 
 hipError_t launch_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int C, const float* scale,
@@ -864,6 +890,32 @@ hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int6
       eps, save_mean, save_invstd, scale, shift_out, num_batches);
   PDA_CHECK_HIP(hipGetLastError());
   return launch_apply(x, res, y, M, (int)C, scale, shift_out, relu, relu_bits, st);
+}
+
+// Bottleneck output with a downsample shortcut: y = relu(bn(x) + bn2(x2)), both BNs finalized from
+// their conv-epilogue statistics tables; one pass reads x and x2 and writes y + the 1-bit ReLU mask
+// (the shortcut's normalised tensor is never stored, nor its gradient in the backward: both BN
+// backwards read dy and the mask).  C must take the register-table path (bn_dual_ok).
+bool bn_dual_ok(int64_t C) { return C % 8 == 0 && C <= kMaxC && !lds_tables_forced() && wave_sets((int)(C / 8)) > 0; }
+
+hipError_t bn_fwd_train_sums_dual(const bf16_t* x, const bf16_t* x2, bf16_t* y, int64_t M, int64_t C,
+                                  const BnSumsArgs& a, const BnSumsArgs& b, float momentum, float eps,
+                                  uint8_t* relu_bits, hipStream_t st) {
+  if (!bn_dual_ok(C) || a.table_rows < 1 || b.table_rows < 1) return hipErrorInvalidValue;
+  const BnSumsArgs* ab[2] = {&a, &b};
+  const bf16_t* xs[2] = {x, x2};
+  for (int i = 0; i < 2; ++i) {
+    const BnSumsArgs& p = *ab[i];
+    bn_finalize_kernel<true, true><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
+        xs[i], p.shift, p.table, p.table_rows, M, (int)C, p.gamma_f, p.gamma_b, p.beta_f, p.beta_b, p.running_mean,
+        p.running_var, momentum, eps, p.save_mean, p.save_invstd, p.save_ss, p.save_ss + C, p.num_batches);
+    PDA_CHECK_HIP(hipGetLastError());
+  }
+  const int ns = wave_sets((int)(C / 8));
+  if (ns == 1) launch_apply_dual_wave<1>(x, x2, y, M, (int)C, a.save_ss, b.save_ss, relu_bits, st);
+  else if (ns == 2) launch_apply_dual_wave<2>(x, x2, y, M, (int)C, a.save_ss, b.save_ss, relu_bits, st);
+  else launch_apply_dual_wave<4>(x, x2, y, M, (int)C, a.save_ss, b.save_ss, relu_bits, st);
+  return hipGetLastError();
 }
 
 hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M, int64_t C, const float* gamma_f,

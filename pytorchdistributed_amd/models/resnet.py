@@ -53,12 +53,20 @@ class Bottleneck(tnn.Module):
         out = self.bn1(self.conv1(x, grad_join=join, bn=self.bn1), relu=True)
         out = self.bn2(self.conv2(out, bn=self.bn2), relu=True)
         if self.downsample is not None:
-            idn = self.downsample[1](self.downsample[0](x, grad_join=join, bn=self.downsample[1]))
-            return self.bn3(self.conv3(out, bn=self.bn3), residual=idn, relu=True)
+            conv_ds, bn_ds = self.downsample
+            zd = conv_ds(x, grad_join=join, bn=bn_ds)
+            z3 = self.conv3(out, bn=self.bn3)
+            if (_DUAL_BN and zd[1] is not None and z3[1] is not None and ops.dual_bn_ok(z3[0], self.bn3.training)
+                    and (bn_ds.eps, bn_ds.momentum) == (self.bn3.eps, self.bn3.momentum)):
+                # relu(bn3(z3) + bn_ds(zd)) in one kernel: the shortcut's BN output and its gradient
+                # are never stored (PDA_DUAL_BN=0: the separate shortcut BN apply)
+                return ops.batch_norm_dual(z3[0], self.bn3, zd[0], bn_ds, z3[1], zd[1])
+            return self.bn3(z3, residual=bn_ds(zd), relu=True)
         return self.bn3(self.conv3(out, bn=self.bn3), residual=x, relu=True, residual_join=join)
 
 
 _STEM_S2D = os.environ.get("PDA_STEM_S2D", "1") == "1"
+_DUAL_BN = os.environ.get("PDA_DUAL_BN", "1") == "1"
 
 
 def space_to_depth_stem(x: torch.Tensor, w: torch.Tensor):

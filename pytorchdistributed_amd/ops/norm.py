@@ -75,6 +75,58 @@ class _BatchNormFn(torch.autograd.Function):
         return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None, None, None, None, None
 
 
+def _param_targets(ctx, gamma, beta, ig, ib):
+    tg = grad_target(gamma) if gamma is not None and ctx.needs_input_grad[ig] else None
+    tb = grad_target(beta) if beta is not None and ctx.needs_input_grad[ib] else None
+    return (None, None) if (tg is None) != (tb is None) else (tg, tb)
+
+
+class _DualBatchNormFn(torch.autograd.Function):
+    """``y = relu(bn(x) + bn2(x2))`` — a bottleneck's output with its downsample shortcut, both BNs
+    finalized from their producing convs' statistics tables.  The forward writes y and the 1-bit ReLU
+    mask in one pass (the shortcut's normalised tensor is never stored); the backward runs the two BN
+    backwards on (dy, mask) directly, so the shortcut's gradient dy * mask is never stored either."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, x2, gamma2, beta2, rm, rv, rm2, rv2, table, shift, table2, shift2, nbt, nbt2,
+                momentum, eps):
+        x, x2 = x.contiguous(), x2.contiguous()
+        y, bits, mean, invstd, mean2, invstd2 = C().bn_fwd_train_sums_dual(
+            x, table, shift, gamma, beta, rm, rv, nbt, x2, table2, shift2, gamma2, beta2, rm2, rv2, nbt2, momentum,
+            eps)
+        ctx.save_for_backward(x, x2, bits, mean, invstd, mean2, invstd2, gamma, gamma2)
+        ctx.betas = (beta, beta2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, x2, bits, mean, invstd, mean2, invstd2, gamma, gamma2 = ctx.saved_tensors
+        beta, beta2 = ctx.betas
+        dy = dy.contiguous()
+        outs = []
+        for xi, mi, si, gi, bi, ig, ib in ((x, mean, invstd, gamma, beta, 1, 2), (x2, mean2, invstd2, gamma2, beta2, 4, 5)):
+            tg, tb = _param_targets(ctx, gi, bi, ig, ib)
+            dxi, _, dg, db = C().bn_bwd(dy, xi, bits, None, mi, si, gi, True, False, tg, tb)
+            outs.append((dxi, dg if gi is not None and ctx.needs_input_grad[ig] else None,
+                         db if bi is not None and ctx.needs_input_grad[ib] else None))
+        (dx, dg, db), (dx2, dg2, db2) = outs
+        return (dx, dg, db, dx2, dg2, db2) + (None,) * 12
+
+
+def dual_bn_ok(x: torch.Tensor, training: bool) -> bool:
+    """True when :func:`batch_norm_dual` runs as one native kernel for ``x``."""
+    return training and x.is_cuda and x.dtype == torch.bfloat16 and C().bn_dual_ok(x.shape[-1])
+
+
+def batch_norm_dual(x, bn, x2, bn2, stats, stats2):
+    """``relu(bn(x) + bn2(x2))`` for two training-mode ``BatchNorm2d`` modules whose batch statistics
+    were accumulated by the producing convs (``stats = (table, shift)`` from ``Conv2d(..., bn=...)``)."""
+    (t1, s1), (t2, s2) = stats, stats2
+    return _DualBatchNormFn.apply(x, bn.weight, bn.bias, x2, bn2.weight, bn2.bias, bn.running_mean, bn.running_var,
+                                  bn2.running_mean, bn2.running_var, t1, s1, t2, s2, bn.num_batches_tracked,
+                                  bn2.num_batches_tracked, bn.momentum, bn.eps)
+
+
 def _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu):
     C_ = x.shape[-1]
     xf = x.reshape(-1, C_)
