@@ -304,6 +304,57 @@ std::vector<Tensor> bn_fwd_train_sums_dual(Tensor x, Tensor table, Tensor shift,
   return {y, bits, stats[0][0], stats[0][1], stats[1][0], stats[1][1]};
 }
 
+bool bn_bwd_dual_ok(int64_t C) { return pda::bn_bwd_dual_ok(C); }
+
+// backward of bn_fwd_train_sums_dual: {dx, dx2, dgamma, dbeta, dgamma2, dbeta2}; the parameter gradients
+// go to the given outputs (flat-buffer slots) when passed, else are allocated in the parameter dtype
+std::vector<Tensor> bn_bwd_dual(Tensor dy, Tensor bits, Tensor x, Tensor mean, Tensor invstd,
+                                c10::optional<Tensor> gamma, Tensor x2, Tensor mean2, Tensor invstd2,
+                                c10::optional<Tensor> gamma2, c10::optional<Tensor> dgamma_out,
+                                c10::optional<Tensor> dbeta_out, c10::optional<Tensor> dgamma2_out,
+                                c10::optional<Tensor> dbeta2_out) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  check_bf16(x2, "x2");
+  TORCH_CHECK(dy.sizes() == x.sizes() && x2.sizes() == x.sizes(), "dual BN backward: one shape for dy, x, x2");
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(pda::bn_bwd_dual_ok(C), "dual BN backward needs C with 1 or 2 register coefficient sets");
+  check_gpu(bits, "relu_bits");
+  TORCH_CHECK(bits.scalar_type() == at::kByte && bits.is_contiguous() && bits.numel() * 8 == x.numel(),
+              "relu bit mask must hold numel/8 bytes");
+  c10::DeviceGuard g(x.device());
+  Tensor xs[2] = {x, x2}, means[2] = {mean, mean2}, invs[2] = {invstd, invstd2};
+  c10::optional<Tensor> gam[2] = {gamma, gamma2}, dgo[2] = {dgamma_out, dgamma2_out}, dbo[2] = {dbeta_out, dbeta2_out};
+  Tensor dxs[2], dgs[2], dbs[2], wss[2];
+  pda::BnBwdSide side[2];
+  for (int i = 0; i < 2; ++i) {
+    check_f32(means[i], "mean");
+    check_f32(invs[i], "invstd");
+    bn_param_ptrs(gam[i], &side[i].gamma_f, &side[i].gamma_b, C);
+    const auto pdt = gam[i].has_value() ? gam[i]->scalar_type() : at::kFloat;
+    dxs[i] = at::empty_like(x);
+    dgs[i] = dgo[i].has_value() ? *dgo[i] : at::empty({C}, x.options().dtype(pdt));
+    dbs[i] = dbo[i].has_value() ? *dbo[i] : at::empty({C}, x.options().dtype(pdt));
+    TORCH_CHECK(dgs[i].numel() == C && dbs[i].numel() == C && dgs[i].scalar_type() == pdt &&
+                dbs[i].scalar_type() == pdt);
+    check_gpu(dgs[i], "dgamma");
+    check_gpu(dbs[i], "dbeta");
+    wss[i] = at::empty({pda::bn_workspace_floats(M, C)}, x.options().dtype(at::kFloat));
+    const bool pb = pdt == at::kBFloat16;
+    side[i].x = bp(xs[i]);
+    side[i].mean = means[i].data_ptr<float>();
+    side[i].invstd = invs[i].data_ptr<float>();
+    side[i].dx = bpm(dxs[i]);
+    side[i].dgamma_f = pb ? nullptr : dgs[i].data_ptr<float>();
+    side[i].dgamma_b = pb ? bpm(dgs[i]) : nullptr;
+    side[i].dbeta_f = pb ? nullptr : dbs[i].data_ptr<float>();
+    side[i].dbeta_b = pb ? bpm(dbs[i]) : nullptr;
+    side[i].ws = wss[i].data_ptr<float>();
+  }
+  CHECK_HIP_OK(pda::bn_bwd_dual(bp(dy), bits.data_ptr<uint8_t>(), M, C, side[0], side[1], stream_of(x)));
+  return {dxs[0], dxs[1], dgs[0], dbs[0], dgs[1], dbs[1]};
+}
+
 Tensor bn_fwd_eval(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma, c10::optional<Tensor> beta,
                    Tensor running_mean, Tensor running_var, double eps, bool relu) {
   check_bf16(x, "x");
@@ -1240,6 +1291,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd_train_sums", &bn_fwd_train_sums);
   m.def("bn_fwd_train_sums_dual", &bn_fwd_train_sums_dual);
   m.def("bn_dual_ok", &bn_dual_ok);
+  m.def("bn_bwd_dual", &bn_bwd_dual);
+  m.def("bn_bwd_dual_ok", &bn_bwd_dual_ok);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"),
         py::arg("pad"), py::arg("dil"), py::arg("addend") = py::none(), py::arg("addend_bits") = py::none());
   m.def("conv_wgrad", &conv_wgrad);

@@ -114,6 +114,25 @@ struct BnSumsArgs {
   int64_t* num_batches;
 };
 bool bn_dual_ok(int64_t C);
+// one BN of bn_bwd_dual: input, saved statistics, affine weight, outputs, workspace (bn_workspace_floats)
+struct BnBwdSide {
+  const bf16_t* x;
+  const float* mean;
+  const float* invstd;
+  const float* gamma_f;
+  const bf16_t* gamma_b;
+  bf16_t* dx;
+  float* dgamma_f;
+  bf16_t* dgamma_b;
+  float* dbeta_f;
+  bf16_t* dbeta_b;
+  float* ws;
+};
+bool bn_bwd_dual_ok(int64_t C);
+// backward of y = relu(bn_a(x_a) + bn_b(x_b)) from dy and the forward's ReLU bits: one reduce pass over
+// (dy, bits, x_a, x_b), two finalizes, one apply pass writing dx_a and dx_b
+hipError_t bn_bwd_dual(const bf16_t* dy, const uint8_t* relu_bits, int64_t M, int64_t C, const BnBwdSide& a,
+                       const BnBwdSide& b, hipStream_t st);
 // y = relu(bn_a(x) + bn_b(x2)) from two conv-epilogue statistics tables; writes the 1-bit ReLU mask
 hipError_t bn_fwd_train_sums_dual(const bf16_t* x, const bf16_t* x2, bf16_t* y, int64_t M, int64_t C,
                                   const BnSumsArgs& a, const BnSumsArgs& b, float momentum, float eps,

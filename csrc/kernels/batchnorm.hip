@@ -636,6 +636,71 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_kernel(const bf16_t* _
   else block_col_reduce_store(sa, sb, tx, ty, cols, rpi, vcol, C, slab, slab + (int64_t)gridDim.x * C);
 }
 
+// Two BNs fed by one masked gradient (a downsample bottleneck's relu(bn(x) + bn2(x2)), MASK 3): one
+// pass over dy, the bit mask, x and x2.  sum(dz) is shared; sum(dz (x - mean)) per input.
+__global__ void __launch_bounds__(kThreads) bn_bwd_reduce_dual_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ x2,
+    const uint8_t* __restrict__ bits, const float* __restrict__ mean, const float* __restrict__ mean2, int64_t M,
+    int C, int cols, int rpi, int64_t rpb, float* __restrict__ slab, float* __restrict__ slab2) {
+  const int tx = threadIdx.x % cols, ty = threadIdx.x / cols;
+  const int vcol = blockIdx.y * cols + tx;
+  const bool active = ty < rpi && vcol * 8 < C;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = min(r0 + rpb, M);
+  const int c0 = vcol * 8;
+  float sa[8], sb[8], sb2[8], mu[8], mu2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sa[j] = sb[j] = sb2[j] = 0.f;
+  if (active) {
+    load8(mean + c0, mu);
+    load8(mean2 + c0, mu2);
+    int64_t r = r0 + ty;
+    for (; r + 3 * rpi < r1; r += 4 * rpi) {  // 4 rows x 3 tensors in flight per lane
+      u16x8 ga[4], xa[4], x2a[4];
+      uint32_t mb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t off = (r + u * rpi) * C + c0;
+        ga[u] = *reinterpret_cast<const u16x8*>(dy + off);
+        xa[u] = *reinterpret_cast<const u16x8*>(x + off);
+        x2a[u] = *reinterpret_cast<const u16x8*>(x2 + off);
+        mb[u] = bits[off >> 3];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float g = (mb[u] >> j) & 1u ? bf2f(ga[u][j]) : 0.f;
+          sa[j] += g;
+          sb[j] += g * (bf2f(xa[u][j]) - mu[j]);
+          sb2[j] += g * (bf2f(x2a[u][j]) - mu2[j]);
+        }
+      }
+    }
+    for (; r < r1; r += rpi) {
+      const int64_t off = r * C + c0;
+      float g[8], xv[8], x2v[8];
+      load8(dy + off, g);
+      load8(x + off, xv);
+      load8(x2 + off, x2v);
+      const uint32_t m = bits[off >> 3];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gm = (m >> j) & 1u ? g[j] : 0.f;
+        sa[j] += gm;
+        sb[j] += gm * (xv[j] - mu[j]);
+        sb2[j] += gm * (x2v[j] - mu2[j]);
+      }
+    }
+  }
+  float sa2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sa2[j] = sa[j];  // (the store reduces its arguments in place)
+  block_col_reduce_store(sa, sb, tx, ty, cols, rpi, vcol, C, slab, slab + (int64_t)gridDim.x * C);
+  __syncthreads();
+  block_col_reduce_store(sa2, sb2, tx, ty, cols, rpi, vcol, C, slab2, slab2 + (int64_t)gridDim.x * C);
+}
+
 // dgamma = invstd * sum(dz (x-mean)), dbeta = sum(dz);  coefficients for dx = A*dz + B*x + Cc
 __global__ void __launch_bounds__(kFinThreads) bn_bwd_finalize_kernel(
     float* __restrict__ slab, int nrb, int64_t M, int C, const float* __restrict__ mean,
@@ -843,6 +908,79 @@ hipError_t launch_apply(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M
   return hipGetLastError();
 }
 
+// Dual backward apply (MASK 3): dx = A g + B x + Cc and dx2 = A2 g + B2 x2 + C2 from one read of dy
+// and the mask; register coefficient tables for both BNs (NS <= 2).
+template <int NS>
+__global__ void __launch_bounds__(kThreads) bn_bwd_apply_dual_wave_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x, const bf16_t* __restrict__ x2,
+    const uint8_t* __restrict__ bits, int64_t M, int C, const float* __restrict__ coef,
+    const float* __restrict__ coef2, bf16_t* __restrict__ dx, bf16_t* __restrict__ dx2) {
+  const int cv = C / 8, lane = threadIdx.x & 63;
+  const int64_t nvec = M * cv;
+  const int64_t tw = (int64_t)gridDim.x * (kThreads / 64);
+  float cA[NS][8], cB[NS][8], cC[NS][8], dA[NS][8], dB[NS][8], dC[NS][8];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int c0 = ((64 * s + lane) % cv) * 8;
+    load8(coef + c0, cA[s]);
+    load8(coef + C + c0, cB[s]);
+    load8(coef + 2 * C + c0, cC[s]);
+    load8(coef2 + c0, dA[s]);
+    load8(coef2 + C + c0, dB[s]);
+    load8(coef2 + 2 * C + c0, dC[s]);
+  }
+  int64_t base = ((int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * kWaveVec;
+  for (; base + kWaveVec <= nvec; base += tw * kWaveVec) {
+    u16x8 ga[4], xa[4], x2a[4];
+    const uint32_t word = reinterpret_cast<const uint32_t*>(bits + base)[lane];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t v = base + 64 * u + lane;
+      ga[u] = *reinterpret_cast<const u16x8*>(dy + v * 8);
+      xa[u] = *reinterpret_cast<const u16x8*>(x + v * 8);
+      x2a[u] = *reinterpret_cast<const u16x8*>(x2 + v * 8);
+    }
+    const uint32_t w = mask_words_in(word, lane);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t v = base + 64 * u + lane;
+      const int s = u % NS;
+      const uint32_t mb = w >> (8 * u);
+      float o[8], o2[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float g = (mb >> j) & 1u ? bf2f(ga[u][j]) : 0.f;
+        o[j] = fmaf(cA[s][j], g, fmaf(cB[s][j], bf2f(xa[u][j]), cC[s][j]));
+        o2[j] = fmaf(dA[s][j], g, fmaf(dB[s][j], bf2f(x2a[u][j]), dC[s][j]));
+      }
+      store8_nt(dx + v * 8, o);
+      store8_nt(dx2 + v * 8, o2);
+    }
+  }
+  for (int64_t v = base + lane; base < nvec && v < nvec; v += 64) {  // last partial iteration
+    const int c0 = (int)(v % cv) * 8;
+    float a[8], b[8], c[8], a2[8], b2[8], c2[8], g[8], xv[8], x2v[8], o[8], o2[8];
+    load8(coef + c0, a);
+    load8(coef + C + c0, b);
+    load8(coef + 2 * C + c0, c);
+    load8(coef2 + c0, a2);
+    load8(coef2 + C + c0, b2);
+    load8(coef2 + 2 * C + c0, c2);
+    load8(dy + v * 8, g);
+    load8(x + v * 8, xv);
+    load8(x2 + v * 8, x2v);
+    const uint32_t mb = bits[v];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gm = (mb >> j) & 1u ? g[j] : 0.f;
+      o[j] = fmaf(a[j], gm, fmaf(b[j], xv[j], c[j]));
+      o2[j] = fmaf(a2[j], gm, fmaf(b2[j], x2v[j], c2[j]));
+    }
+    store8(dx + v * 8, o);
+    store8(dx2 + v * 8, o2);
+  }
+}
+
 }  // namespace
 
 // rows of the fused-finalize table for C channels: enough rows that the ~1024 reduce blocks' atomic
@@ -985,6 +1123,40 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint
   else if (mask == 2) { if (dres) BWD_APPLY(2, true); else BWD_APPLY(2, false); }
   else { if (dres) BWD_APPLY(3, true); else BWD_APPLY(3, false); }
 #undef BWD_APPLY
+  return hipGetLastError();
+}
+
+bool bn_bwd_dual_ok(int64_t C) {
+  if (C % 8 || C > kMaxC || lds_tables_forced()) return false;
+  const int ns = wave_sets((int)(C / 8));
+  return ns == 1 || ns == 2;
+}
+
+hipError_t bn_bwd_dual(const bf16_t* dy, const uint8_t* relu_bits, int64_t M, int64_t C, const BnBwdSide& a,
+                       const BnBwdSide& b, hipStream_t st) {
+  if (!bn_bwd_dual_ok(C) || !relu_bits) return hipErrorInvalidValue;
+  BnGeom g = bn_geom(M, C);
+  float* coef = a.ws + 2 * (int64_t)g.nrb * C;
+  float* coef2 = b.ws + 2 * (int64_t)g.nrb * C;
+  bn_bwd_reduce_dual_kernel<<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(dy, a.x, b.x, relu_bits, a.mean, b.mean, M, (int)C,
+                                                                   g.cols, g.rpi, g.rpb, a.ws, b.ws);
+  PDA_CHECK_HIP(hipGetLastError());
+  const BnBwdSide* sides[2] = {&a, &b};
+  float* coefs[2] = {coef, coef2};
+  for (int i = 0; i < 2; ++i) {
+    const BnBwdSide& p = *sides[i];
+    bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
+        p.ws, g.nrb, M, (int)C, p.mean, p.invstd, p.gamma_f, p.gamma_b, p.dgamma_f, p.dgamma_b, p.dbeta_f, p.dbeta_b,
+        coefs[i]);
+    PDA_CHECK_HIP(hipGetLastError());
+  }
+  const int grid = wave_grid(M * C / 8);
+  if (wave_sets((int)(C / 8)) == 1)
+    bn_bwd_apply_dual_wave_kernel<1><<<grid, kThreads, 0, st>>>(dy, a.x, b.x, relu_bits, M, (int)C, coef, coef2, a.dx,
+                                                                 b.dx);
+  else
+    bn_bwd_apply_dual_wave_kernel<2><<<grid, kThreads, 0, st>>>(dy, a.x, b.x, relu_bits, M, (int)C, coef, coef2, a.dx,
+                                                                 b.dx);
   return hipGetLastError();
 }
 

@@ -10,6 +10,8 @@
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -81,6 +83,9 @@ def _param_targets(ctx, gamma, beta, ig, ib):
     return (None, None) if (tg is None) != (tb is None) else (tg, tb)
 
 
+_DUAL_BWD = os.environ.get("PDA_DUAL_BN_BWD", "1") == "1"
+
+
 class _DualBatchNormFn(torch.autograd.Function):
     """``y = relu(bn(x) + bn2(x2))`` — a bottleneck's output with its downsample shortcut, both BNs
     finalized from their producing convs' statistics tables.  The forward writes y and the 1-bit ReLU
@@ -103,14 +108,19 @@ class _DualBatchNormFn(torch.autograd.Function):
         x, x2, bits, mean, invstd, mean2, invstd2, gamma, gamma2 = ctx.saved_tensors
         beta, beta2 = ctx.betas
         dy = dy.contiguous()
-        outs = []
-        for xi, mi, si, gi, bi, ig, ib in ((x, mean, invstd, gamma, beta, 1, 2), (x2, mean2, invstd2, gamma2, beta2, 4, 5)):
-            tg, tb = _param_targets(ctx, gi, bi, ig, ib)
-            dxi, _, dg, db = C().bn_bwd(dy, xi, bits, None, mi, si, gi, True, False, tg, tb)
-            outs.append((dxi, dg if gi is not None and ctx.needs_input_grad[ig] else None,
-                         db if bi is not None and ctx.needs_input_grad[ib] else None))
-        (dx, dg, db), (dx2, dg2, db2) = outs
-        return (dx, dg, db, dx2, dg2, db2) + (None,) * 12
+        tg, tb = _param_targets(ctx, gamma, beta, 1, 2)
+        tg2, tb2 = _param_targets(ctx, gamma2, beta2, 4, 5)
+        if _DUAL_BWD and C().bn_bwd_dual_ok(x.shape[-1]):
+            # one reduce pass over (dy, bits, x, x2) and one apply pass writing dx and dx2
+            dx, dx2, dg, db, dg2, db2 = C().bn_bwd_dual(dy, bits, x, mean, invstd, gamma, x2, mean2, invstd2, gamma2,
+                                                        tg, tb, tg2, tb2)
+        else:
+            dx, _, dg, db = C().bn_bwd(dy, x, bits, None, mean, invstd, gamma, True, False, tg, tb)
+            dx2, _, dg2, db2 = C().bn_bwd(dy, x2, bits, None, mean2, invstd2, gamma2, True, False, tg2, tb2)
+        ng = ctx.needs_input_grad
+        return (dx, dg if gamma is not None and ng[1] else None, db if beta is not None and ng[2] else None,
+                dx2, dg2 if gamma2 is not None and ng[4] else None, db2 if beta2 is not None and ng[5] else None) \
+            + (None,) * 12
 
 
 def dual_bn_ok(x: torch.Tensor, training: bool) -> bool:

@@ -11,4 +11,4 @@ step() {
 }
 step dualtest 200 python -u -m pytest tests/test_kernels_gpu.py -k "dual_bn" -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 step models 400 python -u -m pytest tests/test_models_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
-CFGS="X=1;PDA_DUAL_BN=0" bash scratch/gpu_r2s4_d.sh
+CFGS="${CFGS:-X=1;PDA_DUAL_BN=0}" bash scratch/gpu_r2s4_d.sh

@@ -703,8 +703,9 @@ def test_conv_wgrad_cu_budgets(env):
     assert r.returncode == 0 and "budget ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
+@pytest.mark.parametrize("dual_bwd", [True, False])
 @pytest.mark.parametrize("inplanes,planes,stride", [(64, 64, 1), (256, 128, 2), (512, 256, 2), (1024, 512, 2)])
-def test_dual_bn_bottleneck_matches_unfused(inplanes, planes, stride, monkeypatch):
+def test_dual_bn_bottleneck_matches_unfused(inplanes, planes, stride, dual_bwd, monkeypatch):
     """Downsample bottleneck: relu(bn3(z3) + bn_ds(z_ds)) in one kernel (PDA_DUAL_BN) vs the separate
     shortcut BN apply + residual BN, both against the fp32 block on the CPU: output, input / parameter
     gradients and running statistics (bf16 gradients of both paths sit ~6 % from fp32 at 588 rows per
@@ -713,7 +714,9 @@ def test_dual_bn_bottleneck_matches_unfused(inplanes, planes, stride, monkeypatc
     import copy
 
     from pytorchdistributed_amd.models import resnet as R
+    from pytorchdistributed_amd.ops import norm as Nm
 
+    monkeypatch.setattr(Nm, "_DUAL_BWD", dual_bwd)  # one-pass dual backward (C <= 1024) or two BN backwards
     torch.manual_seed(21)
     blk = R.Bottleneck(inplanes, planes, stride=stride, downsample=True, device=DEV, dtype=torch.bfloat16)
     with torch.no_grad():  # non-trivial affine parameters so both BNs' gamma / beta matter

@@ -170,7 +170,10 @@ def test_side_stream_wgrad_matches_single_stream():
     DDP(world 1) + fused-SGD steps of ResNet-50 from the same init, grads written straight into the
     flat bucket buffer by wgrad kernels running concurrently with the BN backward; every parameter's
     step-2 gradient is compared (a missed dependency shows as an O(1) error on some layer; BN batch
-    statistics are summed with float atomics, so the two runs agree to rounding, not bitwise)."""
+    statistics are summed with float atomics, so the two runs agree to rounding, not bitwise).  The
+    learning rate keeps step 2 well conditioned: at lr 0.05 the random-init net diverges in step 1
+    (loss ~14) and a last-bit difference of one atomic sum moved step-2 BN gradients by O(1) even
+    between two runs of one configuration (tools/debug_dualbwd.py)."""
     from pytorchdistributed_amd.data.device import DeviceSyntheticImages
     from pytorchdistributed_amd.models.resnet import resnet50
     from pytorchdistributed_amd.ops import cross_entropy, streams
@@ -182,7 +185,7 @@ def test_side_stream_wgrad_matches_single_stream():
         try:
             torch.manual_seed(0)
             model = DistributedDataParallel(resnet50(device="cuda", dtype=torch.bfloat16), device_ids=[0])
-            opt = SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-5)
+            opt = SGD(model.parameters(), lr=1e-3, momentum=0.9, weight_decay=5e-5)
             data = DeviceSyntheticImages(16, 96, 1000, device=torch.device("cuda", 0), dtype=torch.bfloat16, seed=3)
             for _ in range(2):
                 x, y = data.next()
