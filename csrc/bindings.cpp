@@ -473,6 +473,47 @@ std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
   return {y, idx};
 }
 
+// stem: BN finalize from the conv epilogue's table, then maxpool of relu(bn(x)) without storing the BN
+// output; returns {y, idx, mean, invstd, ss}
+std::vector<Tensor> bn_relu_maxpool_fwd(Tensor x, Tensor table, Tensor shift, c10::optional<Tensor> gamma,
+                                        c10::optional<Tensor> beta, Tensor running_mean, Tensor running_var,
+                                        c10::optional<Tensor> num_batches, double momentum, double eps, int64_t k,
+                                        int64_t s, int64_t pad) {
+  check_bf16(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "x must be a contiguous [N,H,W,C] tensor");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 8 == 0 && C <= 2048 && k * k <= 255);
+  check_f32(table, "table");
+  check_f32(shift, "shift");
+  check_f32(running_mean, "running_mean");
+  check_f32(running_var, "running_var");
+  TORCH_CHECK(shift.numel() == C && table.numel() % (2 * C) == 0 && table.numel() > 0 && table.is_contiguous(),
+              "table must be [R, 2, C]");
+  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  c10::DeviceGuard g(x.device());
+  auto fo = x.options().dtype(at::kFloat);
+  Tensor stats = at::empty({4, C}, fo);  // mean, invstd, scale, shift
+  pda::BnSumsArgs a;
+  bn_param_ptrs(gamma, &a.gamma_f, &a.gamma_b, C);
+  bn_param_ptrs(beta, &a.beta_f, &a.beta_b, C);
+  a.table = table.data_ptr<float>();
+  a.table_rows = (int)(table.numel() / (2 * C));
+  a.shift = shift.data_ptr<float>();
+  a.running_mean = running_mean.data_ptr<float>();
+  a.running_var = running_var.data_ptr<float>();
+  a.save_mean = stats.data_ptr<float>();
+  a.save_invstd = a.save_mean + C;
+  a.save_ss = a.save_mean + 2 * C;
+  a.num_batches = nbt_ptr(num_batches, x);
+  hipStream_t st = stream_of(x);
+  CHECK_HIP_OK(pda::bn_finalize_sums(bp(x), (int64_t)N * H * W, C, a, (float)momentum, (float)eps, st));
+  Tensor y = at::empty({N, P, Q, C}, x.options());
+  Tensor idx = at::empty({N, P, Q, C}, x.options().dtype(at::kByte));
+  CHECK_HIP_OK(pda::maxpool2d_bn_fwd(bp(x), a.save_ss, bpm(y), idx.data_ptr<uint8_t>(), N, H, W, C, P, Q, k, s, pad,
+                                     st));
+  return {y, idx, stats[0], stats[1], stats.narrow(0, 2, 2)};
+}
+
 // x [N,H,W,Cx] bf16 (first c channels used) -> [N, ceil((H+2pad)/2), ceil((W+2pad)/2), 16]
 Tensor stem_s2d(Tensor x, int64_t c, int64_t pad) {
   check_bf16(x, "x");
@@ -1276,6 +1317,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_bn_bwd_fused_max_c", &set_bn_bwd_fused_max_c);
   m.def("bn_bwd_fused_max_c", []() { return bn_bwd_fused_max_c(); });
   m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);
   m.def("stem_s2d", &stem_s2d);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

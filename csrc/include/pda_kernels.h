@@ -113,6 +113,10 @@ struct BnSumsArgs {
   float* save_ss;
   int64_t* num_batches;
 };
+// finalize only (no apply): mean, invstd, scale / shift (save_ss [2, C]) and the running statistics from a
+// conv epilogue's statistics table, which it re-zeroes
+hipError_t bn_finalize_sums(const bf16_t* x, int64_t M, int64_t C, const BnSumsArgs& a, float momentum, float eps,
+                            hipStream_t st);
 bool bn_dual_ok(int64_t C);
 // one BN of bn_bwd_dual: input, saved statistics, affine weight, outputs, workspace (bn_workspace_floats)
 struct BnBwdSide {
@@ -155,6 +159,9 @@ int bn_bwd_table_rows(int64_t C);
 // ---- pool.hip (NHWC, C % 8 == 0)
 hipError_t maxpool2d_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int k,
                          int s, int pad, hipStream_t st);
+// maxpool of relu(x * ss[0:C] + ss[C:2C]) (BatchNorm + ReLU applied on the fly), same outputs as maxpool2d_fwd
+hipError_t maxpool2d_bn_fwd(const bf16_t* x, const float* ss, bf16_t* y, uint8_t* idx, int N, int H, int W, int C,
+                            int P, int Q, int k, int s, int pad, hipStream_t st);
 hipError_t maxpool2d_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C, int P, int Q,
                          int k, int s, int pad, hipStream_t st);
 // stem space-to-depth: y[N, U, V, 16] from x[N, H, W, Cx] (first C <= 4 channels), 2x2 blocks, pad

@@ -1034,6 +1034,15 @@ hipError_t bn_fwd_train_sums(const bf16_t* x, const bf16_t* res, bf16_t* y, int6
 // their conv-epilogue statistics tables; one pass reads x and x2 and writes y + the 1-bit ReLU mask
 // (the shortcut's normalised tensor is never stored, nor its gradient in the backward: both BN
 // backwards read dy and the mask).  C must take the register-table path (bn_dual_ok).
+hipError_t bn_finalize_sums(const bf16_t* x, int64_t M, int64_t C, const BnSumsArgs& p, float momentum, float eps,
+                            hipStream_t st) {
+  if (C > kMaxC || C % 8 || p.table_rows < 1) return hipErrorInvalidValue;
+  bn_finalize_kernel<true, true><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
+      x, p.shift, p.table, p.table_rows, M, (int)C, p.gamma_f, p.gamma_b, p.beta_f, p.beta_b, p.running_mean,
+      p.running_var, momentum, eps, p.save_mean, p.save_invstd, p.save_ss, p.save_ss + C, p.num_batches);
+  return hipGetLastError();
+}
+
 bool bn_dual_ok(int64_t C) { return C % 8 == 0 && C <= kMaxC && !lds_tables_forced() && wave_sets((int)(C / 8)) > 0; }
 
 hipError_t bn_fwd_train_sums_dual(const bf16_t* x, const bf16_t* x2, bf16_t* y, int64_t M, int64_t C,

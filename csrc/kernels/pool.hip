@@ -18,9 +18,13 @@ inline int ew_grid(int64_t n) {
   return g < 1 ? 1 : (int)g;
 }
 
+// BN: the pooled tensor is relu(x * ss[c] + ss[C + c]) computed on the fly from the BatchNorm input
+// (stem conv -> BN -> ReLU -> maxpool: the BN+ReLU output is never stored)
+template <bool BN>
 __global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                                uint8_t* __restrict__ idx, int N, int H, int W, int C,
-                                                               int P, int Q, int k, int s, int pad) {
+                                                               int P, int Q, int k, int s, int pad,
+                                                               const float* __restrict__ ss) {
   const int cv = C / 8;
   const int64_t total = (int64_t)N * P * Q * cv;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -31,12 +35,16 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(const bf16_t* __r
     pix /= Q;
     const int p = (int)(pix % P);
     const int n = (int)(pix / P);
-    float best[8];
+    float best[8], sc[8], sh[8];
     uint8_t bi[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       best[j] = -INFINITY;
       bi[j] = 0;
+    }
+    if constexpr (BN) {
+      load8(ss + c8 * 8, sc);
+      load8(ss + C + c8 * 8, sh);
     }
     for (int kh = 0; kh < k; ++kh) {
       const int h = p * s - pad + kh;
@@ -46,6 +54,10 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(const bf16_t* __r
         if (w < 0 || w >= W) continue;
         float v[8];
         load8(x + (((int64_t)n * H + h) * W + w) * C + c8 * 8, v);
+        if constexpr (BN) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = bf2f(f2bf(fmaxf(fmaf(v[j], sc[j], sh[j]), 0.f)));  // as stored
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           if (v[j] > best[j] || (v[j] != v[j])) {  // NaN propagates like torch
@@ -208,7 +220,14 @@ __global__ void __launch_bounds__(kThreads) avgpool_bwd_kernel(const G* __restri
 hipError_t maxpool2d_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int k,
                          int s, int pad, hipStream_t st) {
   const int64_t total = (int64_t)N * P * Q * (C / 8);
-  maxpool_fwd_kernel<<<ew_grid(total), kThreads, 0, st>>>(x, y, idx, N, H, W, C, P, Q, k, s, pad);
+  maxpool_fwd_kernel<false><<<ew_grid(total), kThreads, 0, st>>>(x, y, idx, N, H, W, C, P, Q, k, s, pad, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t maxpool2d_bn_fwd(const bf16_t* x, const float* ss, bf16_t* y, uint8_t* idx, int N, int H, int W, int C,
+                            int P, int Q, int k, int s, int pad, hipStream_t st) {
+  const int64_t total = (int64_t)N * P * Q * (C / 8);
+  maxpool_fwd_kernel<true><<<ew_grid(total), kThreads, 0, st>>>(x, y, idx, N, H, W, C, P, Q, k, s, pad, ss);
   return hipGetLastError();
 }
 

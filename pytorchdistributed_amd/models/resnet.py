@@ -67,6 +67,7 @@ class Bottleneck(tnn.Module):
 
 _STEM_S2D = os.environ.get("PDA_STEM_S2D", "1") == "1"
 _DUAL_BN = os.environ.get("PDA_DUAL_BN", "1") == "1"
+_STEM_BN_POOL = os.environ.get("PDA_STEM_BN_POOL", "1") == "1"
 
 
 def space_to_depth_stem(x: torch.Tensor, w: torch.Tensor):
@@ -121,7 +122,10 @@ class Stem(tnn.Module):
             if pnn._EPILOGUE_STATS and bn.training and x2.dtype == torch.bfloat16:
                 table = bn.stat_table(x2.device)
                 y = ops.conv2d_bn_stats(x2, w2, 1, 0, 1, bn.running_mean, table)
-                return self.maxpool(bn((y, (table, bn.running_mean)), relu=True))
+                mp = self.maxpool
+                if _STEM_BN_POOL:  # BN + ReLU applied inside the pool's loads: the BN output is never stored
+                    return ops.bn_relu_max_pool2d(y, bn, (table, bn.running_mean), mp.k, mp.s, mp.p)
+                return mp(bn((y, (table, bn.running_mean)), relu=True))
             return self.maxpool(bn(ops.conv2d(x2, w2, None, 1, 0), relu=True))
         if x.is_cuda and x.shape[-1] % 8 != 0:
             x = F.pad(x, (0, 8 - x.shape[-1] % 8))

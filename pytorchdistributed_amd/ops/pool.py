@@ -23,6 +23,48 @@ class _MaxPoolFn(torch.autograd.Function):
         return C().maxpool_bwd(dy.contiguous(), idx, H, W, k, s, p), None, None, None
 
 
+class _BnReluMaxPoolFn(torch.autograd.Function):
+    """``max_pool2d(relu(batch_norm(z)))`` for the ResNet stem, the BN finalized from the stem conv's
+    epilogue statistics table: the pool applies BN + ReLU to each window element as it loads it, so the
+    BN output (the largest activation of the network) is never stored.  Backward: the pool's gather
+    backward, then the BN+ReLU backward with the mask recomputed from z and the saved scale / shift."""
+
+    @staticmethod
+    def forward(ctx, z, gamma, beta, running_mean, running_var, table, shift, nbt, momentum, eps, k, s, p):
+        z = z.contiguous()
+        y, idx, mean, invstd, ss = C().bn_relu_maxpool_fwd(z, table, shift, gamma, beta, running_mean, running_var,
+                                                             nbt, momentum, eps, k, s, p)
+        ctx.save_for_backward(z, idx, mean, invstd, ss, gamma)
+        ctx.beta = beta
+        ctx.cfg = (z.shape[1], z.shape[2], k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..parallel.flat import grad_target
+
+        z, idx, mean, invstd, ss, gamma = ctx.saved_tensors
+        H, W, k, s, p = ctx.cfg
+        beta = ctx.beta
+        ng = ctx.needs_input_grad
+        tg = grad_target(gamma) if gamma is not None and ng[1] else None
+        tb = grad_target(beta) if beta is not None and ng[2] else None
+        if (tg is None) != (tb is None):
+            tg = tb = None
+        da = C().maxpool_bwd(dy.contiguous(), idx, H, W, k, s, p)
+        dz, _, dg, db = C().bn_bwd(da, z, None, ss, mean, invstd, gamma, True, False, tg, tb)
+        return (dz, dg if gamma is not None and ng[1] else None, db if beta is not None and ng[2] else None) \
+            + (None,) * 10
+
+
+def bn_relu_max_pool2d(z, bn, stats, kernel_size=3, stride=2, padding=1):
+    """GPU training path of ``max_pool2d(relu(bn(z)))``; ``stats = (table, shift)`` from
+    ``Conv2d(..., bn=bn)``."""
+    table, shift = stats
+    return _BnReluMaxPoolFn.apply(z, bn.weight, bn.bias, bn.running_mean, bn.running_var, table, shift,
+                                  bn.num_batches_tracked, bn.momentum, bn.eps, kernel_size, stride, padding)
+
+
 class _AvgPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, out_fp32):

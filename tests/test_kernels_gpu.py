@@ -748,3 +748,37 @@ def test_dual_bn_bottleneck_matches_unfused(inplanes, planes, stride, dual_bwd, 
             assert rel_err(a, b) < 1e-2
     for e_dual, e_sep in zip(errs[True], errs[False]):
         assert e_dual < 0.15 and e_dual <= 1.25 * e_sep + 2e-3, (errs[True], errs[False])
+
+
+def test_stem_bn_relu_maxpool_matches_unfused(monkeypatch):
+    """ResNet stem with BN + ReLU applied inside the maxpool's loads (PDA_STEM_BN_POOL) == conv -> BN+ReLU
+    apply -> maxpool: same rounding of the pooled values, so output, parameter gradients and running
+    statistics agree to the float-atomic summation order of the conv-epilogue statistics."""
+    import copy
+
+    from pytorchdistributed_amd.models import resnet as R
+
+    torch.manual_seed(22)
+    stem = R.Stem(device=DEV, dtype=torch.bfloat16)
+    with torch.no_grad():
+        stem.bn1.weight.uniform_(0.5, 1.5)
+        stem.bn1.bias.uniform_(-0.3, 0.3)
+    x = torch.randn(4, 3, 58, 62, device=DEV).to(torch.bfloat16)  # odd pooled sizes, NCHW input
+    runs = []
+    for fused in (True, False):
+        monkeypatch.setattr(R, "_STEM_BN_POOL", fused)
+        s = copy.deepcopy(stem)
+        y = s(x)
+        if not runs:
+            dy = torch.randn_like(y)
+        y.backward(dy)
+        torch.cuda.synchronize()
+        runs.append((y.float(), [p.grad.float() for p in s.parameters()],
+                     [t.float() for n, t in s.named_buffers() if "running" in n]))
+    (y1, g1, r1), (y2, g2, r2) = runs
+    assert y1.shape == y2.shape == (4, 15, 16, 64)
+    assert rel_err(y1, y2) < 1e-2
+    for a, b in zip(g1, g2):
+        assert rel_err(a, b) < 1e-2
+    for a, b in zip(r1, r2):
+        assert rel_err(a, b) < 1e-4
