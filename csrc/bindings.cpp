@@ -514,6 +514,44 @@ std::vector<Tensor> bn_relu_maxpool_fwd(Tensor x, Tensor table, Tensor shift, c1
   return {y, idx, stats[0], stats[1], stats.narrow(0, 2, 2)};
 }
 
+bool stem_pool_bn_bwd_ok(int64_t H, int64_t W, int64_t C, int64_t k, int64_t s, int64_t pad) {
+  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  return pda::stem_pool_bn_bwd_ok((int)H, (int)W, (int)C, P, Q, (int)k, (int)s, (int)pad);
+}
+
+// backward of bn_relu_maxpool_fwd (3x3 / 2 / pad 1): {dz, dgamma, dbeta}
+std::vector<Tensor> stem_pool_bn_bwd(Tensor dp, Tensor idx, Tensor z, Tensor ss, Tensor mean, Tensor invstd,
+                                     c10::optional<Tensor> gamma, c10::optional<Tensor> dgamma_out,
+                                     c10::optional<Tensor> dbeta_out) {
+  check_bf16(dp, "dp");
+  check_bf16(z, "z");
+  TORCH_CHECK(z.dim() == 4 && dp.dim() == 4 && z.is_contiguous() && dp.is_contiguous());
+  const int N = z.size(0), H = z.size(1), W = z.size(2), C = z.size(3), P = dp.size(1), Q = dp.size(2);
+  TORCH_CHECK(dp.size(0) == N && dp.size(3) == C && idx.numel() == dp.numel() && idx.scalar_type() == at::kByte);
+  TORCH_CHECK(pda::stem_pool_bn_bwd_ok(H, W, C, P, Q, 3, 2, 1), "stem pool+BN backward: 3x3/2/1 pool only");
+  check_f32(ss, "ss");
+  check_f32(mean, "mean");
+  check_f32(invstd, "invstd");
+  TORCH_CHECK(ss.numel() == 2 * C && ss.is_contiguous());
+  const float* gf;
+  const pda::bf16_t* gb;
+  bn_param_ptrs(gamma, &gf, &gb, C);
+  c10::DeviceGuard g(z.device());
+  const auto pdt = gamma.has_value() ? gamma->scalar_type() : at::kFloat;
+  Tensor dz = at::empty_like(z);
+  Tensor dgamma = dgamma_out.has_value() ? *dgamma_out : at::empty({C}, z.options().dtype(pdt));
+  Tensor dbeta = dbeta_out.has_value() ? *dbeta_out : at::empty({C}, z.options().dtype(pdt));
+  TORCH_CHECK(dgamma.numel() == C && dbeta.numel() == C && dgamma.scalar_type() == pdt && dbeta.scalar_type() == pdt);
+  const bool pb = pdt == at::kBFloat16;
+  Tensor ws = at::empty({pda::stem_pool_bn_bwd_ws_floats(C)}, z.options().dtype(at::kFloat));
+  CHECK_HIP_OK(pda::stem_pool_bn_bwd(bp(dp), idx.data_ptr<uint8_t>(), bp(z), ss.data_ptr<float>(),
+                                     mean.data_ptr<float>(), invstd.data_ptr<float>(), gf, gb, N, H, W, C, P, Q,
+                                     bpm(dz), pb ? nullptr : dgamma.data_ptr<float>(), pb ? bpm(dgamma) : nullptr,
+                                     pb ? nullptr : dbeta.data_ptr<float>(), pb ? bpm(dbeta) : nullptr,
+                                     ws.data_ptr<float>(), stream_of(z)));
+  return {dz, dgamma, dbeta};
+}
+
 // x [N,H,W,Cx] bf16 (first c channels used) -> [N, ceil((H+2pad)/2), ceil((W+2pad)/2), 16]
 Tensor stem_s2d(Tensor x, int64_t c, int64_t pad) {
   check_bf16(x, "x");
@@ -1318,6 +1356,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_fused_max_c", []() { return bn_bwd_fused_max_c(); });
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);
+  m.def("stem_pool_bn_bwd", &stem_pool_bn_bwd);
+  m.def("stem_pool_bn_bwd_ok", &stem_pool_bn_bwd_ok);
   m.def("stem_s2d", &stem_s2d);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

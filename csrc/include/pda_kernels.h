@@ -117,6 +117,14 @@ struct BnSumsArgs {
 // conv epilogue's statistics table, which it re-zeroes
 hipError_t bn_finalize_sums(const bf16_t* x, int64_t M, int64_t C, const BnSumsArgs& a, float momentum, float eps,
                             hipStream_t st);
+// ResNet stem backward of maxpool(3, 2, 1) over relu(bn(z)): dp [N,P,Q,C] + argmax bytes -> dz [N,H,W,C],
+// dgamma / dbeta; the pooled-input gradient is gathered in registers (never stored)
+bool stem_pool_bn_bwd_ok(int H, int W, int C, int P, int Q, int k, int s, int pad);
+int64_t stem_pool_bn_bwd_ws_floats(int64_t C);
+hipError_t stem_pool_bn_bwd(const bf16_t* dp, const uint8_t* idx, const bf16_t* z, const float* ss,
+                            const float* mean, const float* invstd, const float* gamma_f, const bf16_t* gamma_b,
+                            int N, int H, int W, int C, int P, int Q, bf16_t* dz, float* dgamma_f, bf16_t* dgamma_b,
+                            float* dbeta_f, bf16_t* dbeta_b, float* ws, hipStream_t st);
 bool bn_dual_ok(int64_t C);
 // one BN of bn_bwd_dual: input, saved statistics, affine weight, outputs, workspace (bn_workspace_floats)
 struct BnBwdSide {

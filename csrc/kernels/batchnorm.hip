@@ -94,6 +94,7 @@ __device__ __forceinline__ void block_col_reduce_store(float (&a)[8], float (&b)
 }
 
 // Sum the [nrb][C] slabs for 64 channels per workgroup: kFinThreads = 64 channels x 16 row-lanes.
+constexpr int kStemBlocks = 2048;  // stem pool+BN backward grid (slab rows of its reduce phase)
 constexpr int kFinThreads = 1024;
 // Rows are `ld` floats apart (C for the [nrb][C] slabs, 2C for a conv epilogue's [R][2][C] table).
 // CLEAR: zero every entry after reading it (the epilogue table must be zero for its next conv).
@@ -981,6 +982,109 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_dual_wave_kernel(
   }
 }
 
+// ---------------------------------------------------------------- stem: maxpool(3, 2, 1) + BN + ReLU backward
+// The pooled input gradient da of an input pixel is gathered from the (up to 4) windows whose argmax
+// byte picked it (as maxpool3s2_bwd_kernel: one thread = a 2x2 input block x 8 channels) and used in
+// registers: PHASE 0 reduces sum(g), sum(g (z - mean)) with g = da * relu_mask(z * sc + sh) into
+// per-block slabs; PHASE 1 writes dz = A g + B z + Cc.  da is never stored.
+template <int PHASE>
+__global__ void __launch_bounds__(kThreads) stem_pool_bn_bwd_kernel(
+    const bf16_t* __restrict__ dp, const uint8_t* __restrict__ idx, const bf16_t* __restrict__ z,
+    const float* __restrict__ ss, const float* __restrict__ mean, const float* __restrict__ coef, int N, int H, int W,
+    int C, int P, int Q, float* __restrict__ slab, bf16_t* __restrict__ dz) {
+  const int cv = C >> 3;
+  const int Hb = (H + 1) >> 1, Wb = (W + 1) >> 1;
+  const int total = N * Hb * Wb * cv;
+  const int stride = gridDim.x * blockDim.x;  // a multiple of cv (host-checked): c8 is fixed per thread
+  const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c8 = t0 % cv;
+  float sc[8], sh[8], mu[8], cA[8], cB[8], cC[8], sa[8], sb[8];
+  load8(ss + c8 * 8, sc);
+  load8(ss + C + c8 * 8, sh);
+  if (PHASE == 0) {
+    load8(mean + c8 * 8, mu);
+  } else {
+    load8(coef + c8 * 8, cA);
+    load8(coef + C + c8 * 8, cB);
+    load8(coef + 2 * C + c8 * 8, cC);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sa[j] = sb[j] = 0.f;
+  for (int t = t0; t < total; t += stride) {
+    int pix = t / cv;
+    const int q = pix % Wb;
+    pix /= Wb;
+    const int p = pix % Hb;
+    const int n = pix / Hb;
+    float g[4][8];
+    uint64_t id[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int pp = p + (o >> 1), qq = q + (o & 1);
+      if (pp < P && qq < Q) {
+        const int64_t off = (((int64_t)n * P + pp) * Q + qq) * C + c8 * 8;
+        id[o] = *reinterpret_cast<const uint64_t*>(idx + off);
+        load8(dp + off, g[o]);
+      } else {
+        id[o] = ~0ull;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[o][j] = 0.f;
+      }
+    }
+    float d[4][8];  // 2x2 block: (0,0) (0,1) (1,0) (1,1)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t i0 = (uint32_t)(id[0] >> (8 * j)) & 0xFF, i1 = (uint32_t)(id[1] >> (8 * j)) & 0xFF;
+      const uint32_t i2 = (uint32_t)(id[2] >> (8 * j)) & 0xFF, i3 = (uint32_t)(id[3] >> (8 * j)) & 0xFF;
+      d[0][j] = i0 == 4 ? g[0][j] : 0.f;
+      d[1][j] = (i0 == 5 ? g[0][j] : 0.f) + (i1 == 3 ? g[1][j] : 0.f);
+      d[2][j] = (i0 == 7 ? g[0][j] : 0.f) + (i2 == 1 ? g[2][j] : 0.f);
+      d[3][j] = ((i0 == 8 ? g[0][j] : 0.f) + (i1 == 6 ? g[1][j] : 0.f)) + ((i2 == 2 ? g[2][j] : 0.f) + (i3 == 0 ? g[3][j] : 0.f));
+    }
+    const int h = 2 * p, w = 2 * q;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int hh = h + (e >> 1), ww = w + (e & 1);
+      if (hh >= H || ww >= W) continue;
+      const int64_t off = (((int64_t)n * H + hh) * W + ww) * C + c8 * 8;
+      float zv[8];
+      load8(z + off, zv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float gm = fmaf(zv[j], sc[j], sh[j]) > 0.f ? d[e][j] : 0.f;
+        if (PHASE == 0) {
+          sa[j] += gm;
+          sb[j] += gm * (zv[j] - mu[j]);
+        } else {
+          zv[j] = fmaf(cA[j], gm, fmaf(cB[j], zv[j], cC[j]));
+        }
+      }
+      if (PHASE == 1) store8(dz + off, zv);
+    }
+  }
+  if (PHASE == 0) {
+    __shared__ float s_a[kThreads * 8];
+    __shared__ float s_b[kThreads * 8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s_a[threadIdx.x * 8 + j] = sa[j];
+      s_b[threadIdx.x * 8 + j] = sb[j];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < cv) {  // thread c sums the threads c, c + cv, ... (same channel group)
+      for (int k = threadIdx.x + cv; k < kThreads; k += cv) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sa[j] += s_a[k * 8 + j];
+          sb[j] += s_b[k * 8 + j];
+        }
+      }
+      store8(slab + (int64_t)blockIdx.x * C + c8 * 8, sa);
+      store8(slab + (int64_t)gridDim.x * C + (int64_t)blockIdx.x * C + c8 * 8, sb);
+    }
+  }
+}
+
 }  // namespace
 
 // rows of the fused-finalize table for C channels: enough rows that the ~1024 reduce blocks' atomic
@@ -1166,6 +1270,32 @@ hipError_t bn_bwd_dual(const bf16_t* dy, const uint8_t* relu_bits, int64_t M, in
   else
     bn_bwd_apply_dual_wave_kernel<2><<<grid, kThreads, 0, st>>>(dy, a.x, b.x, relu_bits, M, (int)C, coef, coef2, a.dx,
                                                                  b.dx);
+  return hipGetLastError();
+}
+
+bool stem_pool_bn_bwd_ok(int H, int W, int C, int P, int Q, int k, int s, int pad) {
+  return k == 3 && s == 2 && pad == 1 && P == (H - 1) / 2 + 1 && Q == (W - 1) / 2 + 1 && C % 8 == 0 && C <= kMaxC &&
+         kThreads % (C / 8) == 0;
+}
+
+int64_t stem_pool_bn_bwd_ws_floats(int64_t C) { return 2 * (int64_t)kStemBlocks * C + 3 * C; }
+
+hipError_t stem_pool_bn_bwd(const bf16_t* dp, const uint8_t* idx, const bf16_t* z, const float* ss,
+                            const float* mean, const float* invstd, const float* gamma_f, const bf16_t* gamma_b,
+                            int N, int H, int W, int C, int P, int Q, bf16_t* dz, float* dgamma_f, bf16_t* dgamma_b,
+                            float* dbeta_f, bf16_t* dbeta_b, float* ws, hipStream_t st) {
+  if (!stem_pool_bn_bwd_ok(H, W, C, P, Q, 3, 2, 1)) return hipErrorInvalidValue;
+  float* coef = ws + 2 * (int64_t)kStemBlocks * C;
+  const int64_t M = (int64_t)N * H * W;
+  stem_pool_bn_bwd_kernel<0><<<kStemBlocks, kThreads, 0, st>>>(dp, idx, z, ss, mean, nullptr, N, H, W, C, P, Q, ws,
+                                                              nullptr);
+  PDA_CHECK_HIP(hipGetLastError());
+  bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(ws, kStemBlocks, M, C, mean, invstd,
+                                                                           gamma_f, gamma_b, dgamma_f, dgamma_b,
+                                                                           dbeta_f, dbeta_b, coef);
+  PDA_CHECK_HIP(hipGetLastError());
+  stem_pool_bn_bwd_kernel<1><<<kStemBlocks, kThreads, 0, st>>>(dp, idx, z, ss, mean, coef, N, H, W, C, P, Q, nullptr,
+                                                              dz);
   return hipGetLastError();
 }
 

@@ -2,6 +2,8 @@
 reference `03_model_parallel.ipynb` raw lines 333 and 341)."""
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -21,6 +23,9 @@ class _MaxPoolFn(torch.autograd.Function):
         (idx,) = ctx.saved_tensors
         H, W, k, s, p = ctx.cfg
         return C().maxpool_bwd(dy.contiguous(), idx, H, W, k, s, p), None, None, None
+
+
+_FUSED_BWD = os.environ.get("PDA_STEM_POOL_BN_BWD", "1") == "1"
 
 
 class _BnReluMaxPoolFn(torch.autograd.Function):
@@ -51,8 +56,12 @@ class _BnReluMaxPoolFn(torch.autograd.Function):
         tb = grad_target(beta) if beta is not None and ng[2] else None
         if (tg is None) != (tb is None):
             tg = tb = None
-        da = C().maxpool_bwd(dy.contiguous(), idx, H, W, k, s, p)
-        dz, _, dg, db = C().bn_bwd(da, z, None, ss, mean, invstd, gamma, True, False, tg, tb)
+        if _FUSED_BWD and C().stem_pool_bn_bwd_ok(H, W, z.shape[-1], k, s, p):
+            # pool gradient gathered in registers by both BN-backward passes (never stored)
+            dz, dg, db = C().stem_pool_bn_bwd(dy.contiguous(), idx, z, ss, mean, invstd, gamma, tg, tb)
+        else:
+            da = C().maxpool_bwd(dy.contiguous(), idx, H, W, k, s, p)
+            dz, _, dg, db = C().bn_bwd(da, z, None, ss, mean, invstd, gamma, True, False, tg, tb)
         return (dz, dg if gamma is not None and ng[1] else None, db if beta is not None and ng[2] else None) \
             + (None,) * 10
 

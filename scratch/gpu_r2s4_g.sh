@@ -9,6 +9,6 @@ step() {
   echo "== $name rc=$rc"; tail -3 gpurun_out/$name.log | cut -c1-600
   if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
 }
-step dualtest 200 python -u -m pytest tests/test_kernels_gpu.py -k "dual_bn" -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
+step dualtest 200 python -u -m pytest tests/test_kernels_gpu.py -k "dual_bn or stem_bn" -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 step models 400 python -u -m pytest tests/test_models_gpu.py -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
 CFGS="${CFGS:-X=1;PDA_DUAL_BN=0}" bash scratch/gpu_r2s4_d.sh

@@ -750,14 +750,17 @@ def test_dual_bn_bottleneck_matches_unfused(inplanes, planes, stride, dual_bwd, 
         assert e_dual < 0.15 and e_dual <= 1.25 * e_sep + 2e-3, (errs[True], errs[False])
 
 
-def test_stem_bn_relu_maxpool_matches_unfused(monkeypatch):
+@pytest.mark.parametrize("fused_bwd", [True, False])
+def test_stem_bn_relu_maxpool_matches_unfused(fused_bwd, monkeypatch):
     """ResNet stem with BN + ReLU applied inside the maxpool's loads (PDA_STEM_BN_POOL) == conv -> BN+ReLU
     apply -> maxpool: same rounding of the pooled values, so output, parameter gradients and running
     statistics agree to the float-atomic summation order of the conv-epilogue statistics."""
     import copy
 
     from pytorchdistributed_amd.models import resnet as R
+    from pytorchdistributed_amd.ops import pool as Pl
 
+    monkeypatch.setattr(Pl, "_FUSED_BWD", fused_bwd)  # pool gradient gathered inside the BN backward or stored
     torch.manual_seed(22)
     stem = R.Stem(device=DEV, dtype=torch.bfloat16)
     with torch.no_grad():
