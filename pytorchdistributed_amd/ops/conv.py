@@ -7,6 +7,8 @@ weight-gradient (split-K over N*P*Q with a deterministic slab reduction).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -14,6 +16,11 @@ from .._native import C
 from ..parallel.flat import grad_target
 from . import streams as _streams
 from .grad_join import MaskedGrad
+
+
+# PDA_WGRAD_SIDE_1X1=0: 1x1 weight gradients (HBM-bound like the BN kernels they would overlap) stay on
+# the compute stream; only the MFMA-bound 3x3 / 7x7 ones go to the side stream (A/B knob)
+_SIDE_1X1 = os.environ.get("PDA_WGRAD_SIDE_1X1", "1") == "1"
 
 
 def _ref_conv(x, w, stride, padding, dilation, bias=None):
@@ -62,7 +69,7 @@ class _Conv2dFn(torch.autograd.Function):
             # Only when the kernel writes the parameter's final gradient storage (a flat-buffer slot that
             # AccumulateGrad adopts without a kernel); a freshly allocated dw would be read on the main
             # stream by AccumulateGrad's accumulate / clone, which knows nothing of the side stream.
-            if target is not None and _streams.enabled():
+            if target is not None and _streams.enabled() and (_SIDE_1X1 or w.shape[1] * w.shape[2] > 1):
                 with _streams.wgrad_stream(dy.device, dy, x):
                     dw = C().conv_wgrad(*args)
             else:
