@@ -1632,9 +1632,20 @@ bool wide_pays(int64_t M, int64_t N) {
   return w_time < n_time;
 }
 
+// PDA_WIDE_MIN_K: shortest reduction that takes the (one workgroup per CU) wide tile; below it the
+// 128-tile kernel's two workgroups per CU overlap one tile's epilogue stores with the other's loads
+int wide_min_k() {
+  static const int k = [] {
+    const char* e = getenv("PDA_WIDE_MIN_K");
+    return e ? atoi(e) : 64;
+  }();
+  return k;
+}
+
 bool use_wide(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) {
   const int mode = wide_mode();
   if (mode == 0 || p.splits > 1 || epi.c_f32 || epi.slab || N < 256 || K < 64) return false;
+  if (mode == 1 && K < wide_min_k()) return false;
   if (mode == 2) return true;
   return wide_pays(M, N);
 }
