@@ -1,3 +1,13 @@
+"""Step-1 / step-2 gradient agreement of ResNet-50 under DDP(world 1) across execution variants.
+
+    python tools/debug_dualbwd.py            # lr 0.05 (the old side-stream test's setting)
+    LR=0.001 python tools/debug_dualbwd.py
+
+Compares single- vs side-stream weight gradients and the one-pass dual BN backward vs two BN backwards
+(ops/norm.py:_DUAL_BWD).  Used to show that at lr 0.05 step 2 is chaotic — a last-bit difference of
+one float-atomic BN sum moves step-2 BN gradients by O(1) even between two runs of one configuration —
+while step-1 gradients agree to 1e-4 and at lr 1e-3 every variant agrees bitwise.
+"""
 import os, sys, torch
 sys.path.insert(0, os.getcwd())
 from pytorchdistributed_amd.data.device import DeviceSyntheticImages
