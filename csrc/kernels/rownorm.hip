@@ -146,6 +146,122 @@ __global__ void __launch_bounds__(kThreads) rownorm_bwd_dx_kernel(const T* __res
   }
 }
 
+// Fused backward (rows stay in registers, D <= 2048): workgroup = one row slab of ws_rows rows, each
+// wave walks every 4th row of it writing dx, and the lanes keep the parameter-gradient partials of
+// their own columns (sum dy * xhat, sum dy) across the slab — the column sums need no second pass over
+// dy and x (colstrip_partial_kernel).  The 4 waves meet in LDS and write one slab partial per column.
+template <typename T, typename P, bool RMS, int VPL>
+__global__ void __launch_bounds__(kThreads) rownorm_bwd_fused_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                                     const P* __restrict__ gamma,
+                                                                     const float* __restrict__ mean_in,
+                                                                     const float* __restrict__ rstd_in,
+                                                                     T* __restrict__ dx, int64_t rows, int64_t D,
+                                                                     const T* __restrict__ addend, float* __restrict__ ws,
+                                                                     int64_t rows_per_slab, int nslab) {
+  static_assert(VPL <= 4, "rows kept in registers");
+  __shared__ float red[kRowsPerBlock - 1][2][2048];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_slab;
+  const int64_t r1 = min(rows, r0 + rows_per_slab);
+  float g[VPL][8], pg[VPL][8], pb[VPL][8];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int64_t c = ((int64_t)i * 64 + lane) * 8;
+    if (c < D) load8(gamma + c, g[i]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pg[i][j] = pb[i][j] = 0.f;
+  }
+  for (int64_t row = r0 + w; row < r1; row += kRowsPerBlock) {
+    const float mean = RMS ? 0.f : mean_in[row], rstd = rstd_in[row];
+    const T* xr = x + row * D;
+    const T* dyr = dy + row * D;
+    float xh[VPL][8], gd[VPL][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int64_t c = ((int64_t)i * 64 + lane) * 8;
+      if (c < D) {
+        float xv[8], d[8];
+        load8(xr + c, xv);
+        load8(dyr + c, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float h = (xv[j] - mean) * rstd, q = g[i][j] * d[j];
+          s1 += q;
+          s2 += q * h;
+          xh[i][j] = h;
+          gd[i][j] = q;
+          pg[i][j] = fmaf(d[j], h, pg[i][j]);
+          pb[i][j] += d[j];
+        }
+      }
+    }
+    const float m1 = RMS ? 0.f : wave_sum(s1) / (float)D;
+    const float m2 = wave_sum(s2) / (float)D;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int64_t c = ((int64_t)i * 64 + lane) * 8;
+      if (c < D) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (gd[i][j] - m1 - xh[i][j] * m2);
+        if (addend) {
+          float a[8];
+          load8(addend + row * D + c, a);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += a[j];
+        }
+        store8(dx + row * D + c, o);
+      }
+    }
+  }
+  // waves 1..3 hand their partials to wave 0 through LDS; wave 0 writes the slab row
+  if (w > 0) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (c < D) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          red[w - 1][0][c + j] = pg[i][j];
+          red[w - 1][1][c + j] = pb[i][j];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = (i * 64 + lane) * 8;
+      if (c < D) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+#pragma unroll
+          for (int k = 0; k < kRowsPerBlock - 1; ++k) {
+            pg[i][j] += red[k][0][c + j];
+            pb[i][j] += red[k][1][c + j];
+          }
+        }
+        store8(ws + (int64_t)blockIdx.x * D + c, pg[i]);
+        if (!RMS) store8(ws + ((int64_t)nslab + blockIdx.x) * D + c, pb[i]);
+      }
+    }
+  }
+}
+
+// PDA_ROWNORM_FUSED_BWD=1 selects it.  Measured neutral on GPT-2-medium (311.3k vs 311.2k tok/s,
+// profiles/r2_rownorm_fused_bwd_ab_v32.jsonl): the saved pass over dy and x is paid back by the fewer
+// rows in flight per wave (512 slab workgroups instead of one workgroup per 4 rows), so the default
+// stays the row kernel + column-strip pass.
+bool rownorm_fused_bwd_on() {
+  static const bool on = [] {
+    const char* e = getenv("PDA_ROWNORM_FUSED_BWD");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // ------------------------------------------------------------------ column-strip reductions
 // Block = 64 column vectors (512 columns) x 4 row lanes; blockIdx.y = row slab.  Each block writes
 // its slab partial(s) to ws[k][slab][col]; colreduce_finalize sums the slabs.
@@ -374,6 +490,34 @@ hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* g
     if (!rms) PDA_CHECK_HIP(hipMemsetAsync(dbeta, 0, D * sizeof(float), st));
     return hipSuccess;
   }
+  const int nslab = plan_slabs(rows, D);
+  const int64_t rps = (rows + nslab - 1) / nslab;
+  if (rownorm_fused_bwd_on() && D <= 2048) {
+    // one pass: dx plus the slab partials of dgamma / dbeta (ws sized by colreduce_ws_floats)
+    dispatch_vpl(D, [&](auto vc) {
+      constexpr int V = decltype(vc)::value;
+      if constexpr (V <= 4) {
+#define L(T, P, R) \
+  rownorm_bwd_fused_kernel<T, P, R, V><<<(unsigned)nslab, kThreads, 0, st>>>((const T*)dy, (const T*)x, (const P*)gamma, mean, rstd, (T*)dx, rows, D, (const T*)addend, ws, rps, nslab)
+        if (rms) {
+          if (x_bf16 && p_bf16) L(bf16_t, bf16_t, true);
+          else if (x_bf16) L(bf16_t, float, true);
+          else if (p_bf16) L(float, bf16_t, true);
+          else L(float, float, true);
+        } else {
+          if (x_bf16 && p_bf16) L(bf16_t, bf16_t, false);
+          else if (x_bf16) L(bf16_t, float, false);
+          else if (p_bf16) L(float, bf16_t, false);
+          else L(float, float, false);
+        }
+#undef L
+      }
+    });
+    PDA_CHECK_HIP(hipGetLastError());
+    const int nout = rms ? 1 : 2;
+    colreduce_finalize_kernel<<<fin_grid(D * nout), kFinCols * kFinLanes, 0, st>>>(ws, nslab, D, nout, dgamma, dbeta);
+    return hipGetLastError();
+  }
   const unsigned grid = (unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock);
   dispatch_vpl(D, [&](auto vc) {
     constexpr int V = decltype(vc)::value;
@@ -393,8 +537,6 @@ hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* g
 #undef L
   });
   PDA_CHECK_HIP(hipGetLastError());
-  const int nslab = plan_slabs(rows, D);
-  const int64_t rps = (rows + nslab - 1) / nslab;
   dim3 pg((unsigned)((D + kStripCols - 1) / kStripCols), (unsigned)nslab);
 #define P(T, R) \
   colstrip_partial_kernel<T, true, R><<<pg, kThreads, 0, st>>>((const T*)dy, (const T*)x, mean, rstd, ws, rows, D, rps, nslab)

@@ -785,3 +785,40 @@ def test_stem_bn_relu_maxpool_matches_unfused(fused_bwd, monkeypatch):
         assert rel_err(a, b) < 1e-2
     for a, b in zip(r1, r2):
         assert rel_err(a, b) < 1e-4
+
+
+_ROWNORM_FUSED_SCRIPT = r"""
+import torch, torch.nn.functional as F
+from pytorchdistributed_amd.ops import layer_norm, rms_norm
+def rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+for rms in (False, True):
+    for D, rows in [(64, 37), (1024, 2500), (1600, 37), (2048, 300)]:
+        torch.manual_seed(7)
+        x = (torch.randn(rows, D) * 2 + 0.3).to(torch.bfloat16).float()
+        g, b = torch.rand(D) + 0.5, torch.randn(D)
+        xr, gr, br = x.clone().requires_grad_(), g.clone().requires_grad_(), b.clone().requires_grad_()
+        y = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * gr if rms else F.layer_norm(xr, (D,), gr, br, 1e-5)
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        xg = x.to("cuda", torch.bfloat16).requires_grad_()
+        gg, bg = g.cuda().requires_grad_(), b.cuda().requires_grad_()
+        yg = rms_norm(xg, gg, 1e-6) if rms else layer_norm(xg, gg, bg, 1e-5)
+        yg.backward(dy.to("cuda", torch.bfloat16))
+        errs = [rel(xg.grad.cpu(), xr.grad), rel(gg.grad.cpu(), gr.grad)] + ([] if rms else [rel(bg.grad.cpu(), br.grad)])
+        assert max(errs) < 2e-2, (rms, D, rows, errs)
+print("fused ok")
+"""
+
+
+def test_rownorm_fused_bwd_path():
+    """LayerNorm / RMSNorm backward with the parameter-gradient partials accumulated by the dx kernel
+    (PDA_ROWNORM_FUSED_BWD=1, read once per process: run in a child) against the fp32 reference."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _ROWNORM_FUSED_SCRIPT], cwd=root,
+                       env={**os.environ, "PDA_ROWNORM_FUSED_BWD": "1"}, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "fused ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
