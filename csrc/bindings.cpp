@@ -265,7 +265,7 @@ std::vector<Tensor> bn_fwd_train_sums_dual(Tensor x, Tensor table, Tensor shift,
   check_bf16(x2, "x2");
   TORCH_CHECK(x2.sizes() == x.sizes(), "dual BN: both inputs must have one shape");
   const int64_t C = x.size(-1), M = x.numel() / C;
-  TORCH_CHECK(pda::bn_dual_ok(C), "dual BN apply needs the register-table path (C = 8..2048 dividing 512 or 512k)");
+  TORCH_CHECK(pda::bn_dual_ok(C), "dual BN apply needs the register-table path: C/8 dividing 64, or 64, 128 or 256 * 8");
   Tensor tabs[2] = {table, table2}, shifts[2] = {shift, shift2};
   for (int i = 0; i < 2; ++i) {
     check_f32(tabs[i], "table");

@@ -1147,7 +1147,11 @@ hipError_t bn_finalize_sums(const bf16_t* x, int64_t M, int64_t C, const BnSumsA
   return hipGetLastError();
 }
 
-bool bn_dual_ok(int64_t C) { return C % 8 == 0 && C <= kMaxC && !lds_tables_forced() && wave_sets((int)(C / 8)) > 0; }
+bool bn_dual_ok(int64_t C) {
+  if (C % 8 || C > kMaxC || lds_tables_forced()) return false;
+  const int ns = wave_sets((int)(C / 8));  // register tables with 1, 2 or 4 sets per lane (not 3: C = 1536)
+  return ns == 1 || ns == 2 || ns == 4;
+}
 
 hipError_t bn_fwd_train_sums_dual(const bf16_t* x, const bf16_t* x2, bf16_t* y, int64_t M, int64_t C,
                                   const BnSumsArgs& a, const BnSumsArgs& b, float momentum, float eps,
