@@ -304,6 +304,7 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const bf16_t* __rest
 constexpr int kWaveVec = 256;  // vectors per wave iteration
 
 inline int wave_sets(int cv) {
+  if (cv <= 0) return 0;  // C < 8: no register-table path (and no division by zero)
   if (cv <= 64) return 64 % cv == 0 ? 1 : 0;
   return (cv % 64 == 0 && cv / 64 <= 4) ? cv / 64 : 0;
 }

@@ -16,8 +16,14 @@ def _ensure_hw_queues():
     RCCL's streams and the IPC collective stream; with 4 queues two of them land on one queue, and a
     stream-wait packet at the head of a shared queue stalls the other stream's kernels behind it.
     Measured: ResNet-50 DDP over a one-rank RCCL group 9.30k img/s at 4 queues, 9.82k at 8 (= 16;
-    profiles/r2_hw_queues.jsonl).  Only effective before the process's first HIP call."""
-    want = min(int(_os.environ.get("PDA_HW_QUEUES", "8")), 32)
+    profiles/r2_hw_queues.jsonl).  Only effective before the process's first HIP call.
+
+    An exported ``GPU_MAX_HW_QUEUES`` is respected unless ``PDA_HW_QUEUES`` is also set (bench.py sets
+    ``PDA_HW_QUEUES=8`` by default: its one-rank RCCL group lost 5 % at 4 queues)."""
+    explicit = _os.environ.get("PDA_HW_QUEUES")
+    if "GPU_MAX_HW_QUEUES" in _os.environ and not explicit:
+        return  # the user chose HIP's queue count: leave it (PDA_HW_QUEUES overrides it explicitly)
+    want = min(int(explicit or "8"), 32)
     have = int(_os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
     if want > have:
         _os.environ["GPU_MAX_HW_QUEUES"] = str(want)

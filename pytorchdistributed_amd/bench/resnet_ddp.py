@@ -18,7 +18,7 @@ from ..models.resnet import resnet50
 from ..ops import cross_entropy
 from ..optim import SGD
 from ..parallel.ddp import DistributedDataParallel
-from .common import emit, setup, teardown, timed
+from .common import emit, group_info, setup, teardown, timed
 
 METRIC = "images/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X; scaling efficiency"
 
@@ -58,7 +58,8 @@ def main(argv=None):
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=None)
     a = ap.parse_args(argv)
-    rank, world, local, device = setup(a.gpus)
+    # N=1 runs the DDP bucket all-reduces over a one-rank RCCL group (PDA_DDP_FORCE_COMM=0 turns it off)
+    rank, world, local, device = setup(a.gpus, one_rank_group=True)
     if device.type == "cpu":  # plumbing-only run on a machine without a GPU
         a.batch, a.image = min(a.batch, 2), min(a.image, 64)
     # PDA_MAIN_PRIO=high: the whole step on a high-priority HIP stream (A/B knob for queue arbitration
@@ -75,11 +76,13 @@ def main(argv=None):
     if last != last or abs(last) == float("inf"):
         raise SystemExit(f"non-finite training loss {last} in the benchmark run")
     ms = secs / a.steps * 1e3
+    grp = group_info(device)
+    world = grp["world"]
     imgs = a.batch * world * a.steps / secs
     emit({
         "metric": METRIC, "value": round(imgs, 2), "unit": "images/sec", "n_gpus": world, "steps": a.steps,
         "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "bf16" if device.type == "cuda" else "bf16-cpu-plumbing",
+        "vs_baseline": None, "rccl_world": grp["rccl_world"], "backend": grp["backend"], "dtype": "bf16" if device.type == "cuda" else "bf16-cpu-plumbing",
         "data": "synthetic (on-device Philox, ImageNet shape 224x224x3, 1000 classes), random-init weights",
         "config": {"model": "resnet50", "global_batch": a.batch * world, "per_gpu_batch": a.batch,
                    "image_size": a.image, "seq_len": None, "parallelism": f"dp{world}",

@@ -123,6 +123,7 @@ def run_workers(cmd: List[str], nproc_per_node: int, nnodes: int = 1, node_rank:
     server = None
     if node_rank == 0:
         server = pdist.start_store_server("0.0.0.0", master_port)
+        master_port = server.port  # master_port=0: the store picked a free port
     world = nproc_per_node * nnodes
     if "OMP_NUM_THREADS" not in os.environ and nproc_per_node > 1:
         sys.stderr.write(

@@ -69,7 +69,7 @@ class _Conv2dFn(torch.autograd.Function):
             # Only when the kernel writes the parameter's final gradient storage (a flat-buffer slot that
             # AccumulateGrad adopts without a kernel); a freshly allocated dw would be read on the main
             # stream by AccumulateGrad's accumulate / clone, which knows nothing of the side stream.
-            if target is not None and _streams.enabled() and (_SIDE_1X1 or w.shape[1] * w.shape[2] > 1):
+            if target is not None and _streams.side_ok(ctx.wparam) and (_SIDE_1X1 or w.shape[1] * w.shape[2] > 1):
                 with _streams.wgrad_stream(dy.device, dy, x):
                     dw = C().conv_wgrad(*args)
             else:

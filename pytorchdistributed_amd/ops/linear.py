@@ -103,7 +103,7 @@ def _param_grads(dy2, x2, wparam, bparam, need_w, need_b):
     dw = db = None
     if need_w:
         target = grad_target(wparam)
-        if target is not None and _streams.enabled() and target.numel() < _SIDE_MAX_NUMEL:
+        if target is not None and _streams.side_ok(wparam) and target.numel() < _SIDE_MAX_NUMEL:
             # written straight into the flat gradient slot: run it beside the critical path
             # (ops/streams.py; same contract as the conv weight gradient).  A dW with a full wave
             # of 256x256 output tiles per CU fills the chip by itself; beside other work it only

@@ -87,6 +87,25 @@ def join(device: torch.device) -> None:
     _join(idx)
 
 
+def wait_side(device: torch.device) -> None:
+    """Order the current stream after the side stream's queued work (without ending the pass's
+    side-stream use): a gradient the current stream is about to combine with a side-stream output."""
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _streams.get(idx)
+    if s is not None and _join_pending.get(idx, False):
+        torch.cuda.current_stream(idx).wait_stream(s)
+
+
+def side_ok(param: torch.Tensor) -> bool:
+    """May ``param``'s weight gradient be written on the side stream?
+
+    Not for a parameter used more than once in a graph (tied weights, marked by
+    :func:`..parallel.flat.grad_target`): autograd sums its gradients on the compute stream.  Not
+    under ``create_graph=True`` (grad mode on inside backward): AccumulateGrad then clones the
+    gradient on the compute stream instead of adopting the flat-buffer slot."""
+    return enabled() and not getattr(param, "_pda_shared", False) and not torch.is_grad_enabled()
+
+
 def active(device: torch.device) -> bool:
     """True while a backward pass has side-stream work on ``device`` not yet joined."""
     idx = device.index if device.index is not None else torch.cuda.current_device()

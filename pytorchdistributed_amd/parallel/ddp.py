@@ -225,6 +225,9 @@ class DistributedDataParallel(tnn.Module):
             if not self._callback_queued or self._callback_task != task:
                 if self._callback_queued:
                     # the previous backward raised before its final callback ran: start this pass clean
+                    # (its side-stream weight gradients were never joined either)
+                    if p.is_cuda:
+                        _streams.join(p.device)
                     self._works.clear()
                     self._sweep_tickets(force=True)
                     for grp in self.groups.values():

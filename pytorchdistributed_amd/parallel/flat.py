@@ -78,7 +78,15 @@ def grad_target(param: torch.Tensor) -> Optional[torch.Tensor]:
         return None
     if getattr(param, "_pda_claimed", False):
         # used more than once in this graph (tied weights): only the first backward writes in place,
-        # the others allocate; autograd sums them before AccumulateGrad (DDP's hook clears the claim)
+        # the others allocate; autograd sums them on the compute stream before AccumulateGrad (DDP's
+        # hook clears the claim).  The first use may still be writing the slot on the side stream:
+        # the compute stream waits for it here, and the parameter is marked shared so later passes
+        # keep all of its gradients on the compute stream (ops/streams.py:side_ok).
+        param._pda_shared = True
+        if param.is_cuda:
+            from ..ops import streams as _streams
+
+            _streams.wait_side(param.device)
         return None
     param._pda_claimed = True
     fg, off = info

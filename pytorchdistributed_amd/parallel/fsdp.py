@@ -62,6 +62,14 @@ class _StreamWork:
         return self.event.query()
 
 
+def _join_side_streams(units) -> None:
+    """A backward that raised never ran its final callback, so its side-stream weight gradients were
+    never joined: order the compute stream after them before anything reuses the buffers."""
+    devs = {leaf.device for u in units for leaf in u.leaves if leaf.is_cuda}
+    for d in devs:
+        _streams.join(d)
+
+
 class _Unit:
     def __init__(self, fsdp: "FullyShardedDataParallel", module: tnn.Module, params: List[Tuple[tnn.Module, str]],
                  index: int):
@@ -308,6 +316,7 @@ class FullyShardedDataParallel(tnn.Module):
             return
         if self._callback_queued:  # aborted pass: drop its partial arrivals / pending reduce-scatter
             self._pending_rs = None
+            _join_side_streams(self.units)
             for u in self.units:
                 u.arrived = 0
                 for leaf in u.leaves:

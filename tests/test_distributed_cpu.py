@@ -191,3 +191,42 @@ def test_watchdog_report_mode():
     assert wd.expired() == ["bucket 0"] and len(wd.pending()) == 1
     assert wd.disarm(t) and wd.pending() == []
     wd.stop()
+
+
+def _bench(args, env=None, timeout=240):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "MASTER_ADDR"):
+        e.pop(k, None)
+    e["PDA_DIST_BACKEND"] = "gloo"
+    if env:
+        e.update(env)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=e,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_launches_its_own_ranks():
+    """`bench.py --gpus 2` without a launcher starts 2 ranks itself (reference `ddp_gpus.py:94-98`
+    mp.spawn) and reports the live group's size."""
+    import json
+
+    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["backend"] == "gloo" and rec["config"]["global_batch"] == 2 * rec["config"]["per_gpu_batch"]
+
+
+def test_bench_refuses_mismatched_world():
+    """Under a launcher whose WORLD_SIZE disagrees with --gpus the bench refuses (never downgrades)."""
+    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0"], env={"WORLD_SIZE": "1", "RANK": "0",
+                                                                        "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "refusing" in r.stderr
+
+
+def test_bench_rank_failure_fails_the_launch():
+    """One rank failing makes the self-launched run exit non-zero (the group is torn down)."""
+    r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--image", "-3"], timeout=120)
+    assert r.returncode != 0

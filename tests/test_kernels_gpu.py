@@ -704,7 +704,9 @@ def test_conv_wgrad_cu_budgets(env):
 
 
 @pytest.mark.parametrize("dual_bwd", [True, False])
-@pytest.mark.parametrize("inplanes,planes,stride", [(64, 64, 1), (256, 128, 2), (512, 256, 2), (1024, 512, 2)])
+# (768, 384): C = 1536 has no register-table layout -> the guard (bn_dual_ok) takes the separate-BN path
+@pytest.mark.parametrize("inplanes,planes,stride", [(64, 64, 1), (256, 128, 2), (512, 256, 2), (1024, 512, 2),
+                                                    (768, 384, 2)])
 def test_dual_bn_bottleneck_matches_unfused(inplanes, planes, stride, dual_bwd, monkeypatch):
     """Downsample bottleneck: relu(bn3(z3) + bn_ds(z_ds)) in one kernel (PDA_DUAL_BN) vs the separate
     shortcut BN apply + residual BN, both against the fp32 block on the CPU: output, input / parameter

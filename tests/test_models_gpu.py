@@ -204,3 +204,41 @@ def test_side_stream_wgrad_matches_single_stream():
     assert abs(l0 - l1) <= 1e-2 * abs(l0), (l0, l1)
     worst = max((rel_err(g1[n], g0[n]), n) for n in g0)
     assert worst[0] < 3e-2, worst
+
+
+def test_tied_embedding_side_stream_matches_single_stream():
+    """A small-vocab GPT-2 (tied wte under 256^3 elements, so the head's weight gradient is eligible
+    for the side stream) under DDP: the tied parameter's gradient — the LM head's dW plus the
+    embedding's scatter-add, summed by autograd — must match the single-stream run (the
+    second use used to be summed on the compute stream while the first was still being written on
+    the side stream)."""
+    from pytorchdistributed_amd.models.gpt2 import GPT2, GPT2Config
+    from pytorchdistributed_amd.ops import streams
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+
+    cfg = GPT2Config(vocab_size=512, n_positions=64, n_embd=128, n_layer=2, n_head=4)
+
+    def run(side):
+        streams.set_enabled(side)
+        try:
+            torch.manual_seed(0)
+            model = DistributedDataParallel(GPT2(cfg, device="cuda", dtype=torch.bfloat16), device_ids=[0])
+            g = torch.Generator(device="cuda").manual_seed(5)
+            idx = torch.randint(0, cfg.vocab_size, (4, 64), device="cuda", generator=g)
+            out = []
+            for _ in range(2):
+                for p in model.parameters():
+                    p.grad = None
+                loss = model(idx, targets=idx)
+                loss.backward()
+                out.append(model.module.wte.grad.detach().float().clone())
+            torch.cuda.synchronize()
+            return out
+        finally:
+            streams.set_enabled(None)
+
+    ref = run(False)
+    got = run(True)
+    for a, b in zip(got, ref):
+        assert rel_err(a, b) < 1e-2, rel_err(a, b)
+

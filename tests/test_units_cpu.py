@@ -348,3 +348,13 @@ def test_side_stream_join_is_per_backward_pass(monkeypatch):
     assert len(queued) == 2
     streams._join_pending.clear()
     streams._join_task.clear()
+
+
+def test_bn_dual_guard_channel_counts():
+    """bn_dual_ok: register-table channel counts only (C = 1536 needs 3 sets per lane -> separate BN),
+    and a C < 8 query returns false instead of dividing by zero on the host."""
+    C = _native.C
+
+    assert C().bn_dual_ok(2048) and C().bn_dual_ok(256)
+    assert not C().bn_dual_ok(1536)
+    assert not C().bn_dual_ok(0) and not C().bn_dual_ok(4)
