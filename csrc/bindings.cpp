@@ -16,6 +16,9 @@
 namespace pda_rt {
 void bind_runtime(pybind11::module& m);
 }
+namespace pda_comm {
+void bind_comm(pybind11::module& m);
+}
 
 namespace py = pybind11;
 using at::Tensor;
@@ -677,7 +680,8 @@ void conv_check(const Tensor& x, const Tensor& w) {
   TORCH_CHECK(x.numel() < (1LL << 31), "activation too large for 32-bit index math");
 }
 
-Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, c10::optional<Tensor> bias, bool relu) {
+Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, c10::optional<Tensor> bias, bool relu,
+                bool out_f32) {
   conv_check(x, w);
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int Cout = w.size(0), R = w.size(1), S = w.size(2);
@@ -685,8 +689,8 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t dil, c1
   TORCH_CHECK(P > 0 && Q > 0);
   if (bias) TORCH_CHECK(bias->numel() == Cout);
   c10::DeviceGuard g(x.device());
-  Tensor y = at::empty({N, P, Q, Cout}, x.options());
-  CHECK_HIP_OK(pda::conv2d_fwd(bp(x), bp(w), bpm(y), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
+  Tensor y = at::empty({N, P, Q, Cout}, x.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  CHECK_HIP_OK(pda::conv2d_fwd(bp(x), bp(w), y.data_ptr(), out_f32, N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
                                bias ? bias->data_ptr() : nullptr, bias ? !is_bf16(*bias) : false, relu, nullptr,
                                nullptr, 0, stream_of(x)));
   return y;
@@ -710,14 +714,14 @@ Tensor conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t d
   c10::DeviceGuard g(x.device());
   Tensor y = at::empty({N, P, Q, Cout}, x.options());
   const int rows = (int)(table.numel() / (2 * (int64_t)Cout));
-  CHECK_HIP_OK(pda::conv2d_fwd(bp(x), bp(w), bpm(y), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil, nullptr, false,
+  CHECK_HIP_OK(pda::conv2d_fwd(bp(x), bp(w), bpm(y), false, N, H, W, C, Cout, R, S, P, Q, stride, pad, dil, nullptr, false,
                                false, table.data_ptr<float>(), shift.data_ptr<float>(), rows, stream_of(x)));
   return y;
 }
 
 // addend_bits: optional ReLU bit mask of the addend (numel/8 bytes): dx = dgrad + addend * mask
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad, int64_t dil,
-                  c10::optional<Tensor> addend, c10::optional<Tensor> addend_bits) {
+                  c10::optional<Tensor> addend, c10::optional<Tensor> addend_bits, bool out_f32) {
   check_bf16(dy, "dy");
   check_bf16(w, "w");
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), Cout = dy.size(3);
@@ -729,7 +733,8 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
     wt = at::empty({C, R, S, Cout}, w.options());
     CHECK_HIP_OK(pda::conv_weight_transpose(bp(w), bpm(wt), Cout, R, S, C, stride, pad, dil, stream_of(dy)));
   }
-  Tensor dx = at::empty({N, H, W, C}, dy.options());
+  Tensor dx = at::empty({N, H, W, C}, dy.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  TORCH_CHECK(!(out_f32 && addend.has_value()), "conv_dgrad: an addend needs the bf16 output");
   if (addend.has_value()) {
     check_bf16(*addend, "addend");
     TORCH_CHECK(addend->sizes() == dx.sizes() && addend->is_contiguous(), "addend must have dx's shape");
@@ -741,7 +746,7 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
                     addend_bits->numel() * 8 == dx.numel(),
                 "addend_bits must be numel/8 contiguous bytes");
   }
-  CHECK_HIP_OK(pda::conv2d_dgrad(bp(dy), bp(w), wt.defined() ? bp(wt) : nullptr, bpm(dx), N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
+  CHECK_HIP_OK(pda::conv2d_dgrad(bp(dy), bp(w), wt.defined() ? bp(wt) : nullptr, dx.data_ptr(), out_f32, N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
                                  addend.has_value() ? bp(*addend) : nullptr,
                                  addend_bits.has_value() ? addend_bits->data_ptr<uint8_t>() : nullptr, stream_of(dy)));
   return dx;
@@ -1339,6 +1344,167 @@ std::vector<int64_t> stream_priority_range(int64_t device) {
 }
 }  // namespace
 
+// ------------------------------------------------------------------ fp32 path (fp32x3.hip)
+// hi / lo bf16 split of an fp32 tensor, laid out along a GEMM's K:
+//   stack=false: [rows, C] -> [rows, nseg * C] (segments side by side in each row; rows = numel / C_last)
+//   stack=true:  [d0, ...] -> [nseg * d0, ...] (segments stacked along the leading dim)
+// bit s of lo_mask selects the lo part for segment s
+Tensor split_bf16(Tensor x, int64_t nseg, int64_t lo_mask, bool stack) {
+  check_f32(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.dim() >= 1, "split_bf16: contiguous input");
+  TORCH_CHECK(nseg >= 1 && nseg <= 4, "split_bf16: 1..4 segments");
+  c10::DeviceGuard g(x.device());
+  auto sizes = x.sizes().vec();
+  Tensor out;
+  if (stack) {
+    sizes[0] *= nseg;
+    out = at::empty(sizes, x.options().dtype(at::kBFloat16));
+    TORCH_CHECK(x.numel() % 4 == 0, "split_bf16: numel % 4");
+    CHECK_HIP_OK(pda::split_bf16(x.data_ptr<float>(), bpm(out), 1, x.numel(), (int)nseg, (int)lo_mask, x.numel(),
+                                 x.numel() * nseg, stream_of(x)));
+  } else {
+    const int64_t C = sizes.back();
+    TORCH_CHECK(C % 4 == 0, "split_bf16: last dim % 4");
+    sizes.back() = C * nseg;
+    out = at::empty(sizes, x.options().dtype(at::kBFloat16));
+    CHECK_HIP_OK(pda::split_bf16(x.data_ptr<float>(), bpm(out), x.numel() / C, C, (int)nseg, (int)lo_mask, C,
+                                 C * nseg, stream_of(x)));
+  }
+  return out;
+}
+
+const float* fptr(const c10::optional<Tensor>& t, int64_t n, const char* name) {
+  if (!t.has_value()) return nullptr;
+  check_f32(*t, name);
+  TORCH_CHECK(t->numel() == n && t->is_contiguous(), name, ": wrong size");
+  return t->data_ptr<float>();
+}
+
+// BatchNorm training forward over the last dim of fp32 x: returns {y, save_mean, save_invstd}
+std::vector<Tensor> bn_f32_fwd_train(Tensor x, c10::optional<Tensor> res, c10::optional<Tensor> gamma,
+                                     c10::optional<Tensor> beta, c10::optional<Tensor> running_mean,
+                                     c10::optional<Tensor> running_var, double momentum, double eps, bool relu,
+                                     c10::optional<Tensor> num_batches) {
+  check_f32(x, "x");
+  TORCH_CHECK(x.is_contiguous());
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(C % 4 == 0, "bn fp32: C % 4");
+  if (res) {
+    check_f32(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous());
+  }
+  c10::DeviceGuard g(x.device());
+  auto fo = x.options();
+  Tensor y = at::empty_like(x), mean = at::empty({C}, fo), invstd = at::empty({C}, fo), ss = at::empty({2 * C}, fo);
+  Tensor part = at::empty({(int64_t)pda::bn_f32_partials(M, (int)C) * 2 * C}, fo);
+  // shift = running mean (a close guess of the batch mean: shifted sums keep the variance accurate)
+  const float* rm = fptr(running_mean, C, "running_mean");
+  Tensor shift = rm ? running_mean->clone() : at::zeros({C}, fo);
+  int64_t* nb = nullptr;
+  if (num_batches) {
+    check_gpu(*num_batches, "num_batches");
+    TORCH_CHECK(num_batches->scalar_type() == at::kLong && num_batches->numel() == 1);
+    nb = num_batches->data_ptr<int64_t>();
+  }
+  CHECK_HIP_OK(pda::bn_f32_fwd_train(x.data_ptr<float>(), res ? res->data_ptr<float>() : nullptr,
+                                     fptr(gamma, C, "gamma"), fptr(beta, C, "beta"), (float*)rm,
+                                     (float*)fptr(running_var, C, "running_var"), shift.data_ptr<float>(),
+                                     (float)momentum, (float)eps, relu ? 1 : 0, y.data_ptr<float>(),
+                                     mean.data_ptr<float>(), invstd.data_ptr<float>(), ss.data_ptr<float>(),
+                                     part.data_ptr<float>(), nb, M, (int)C, stream_of(x)));
+  return {y, mean, invstd};
+}
+
+// y = x * ss[:C] + ss[C:] (+ res) (relu)  (eval-mode BN with host-folded coefficients)
+Tensor bn_f32_apply(Tensor x, c10::optional<Tensor> res, Tensor ss, bool relu) {
+  check_f32(x, "x");
+  TORCH_CHECK(x.is_contiguous());
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  check_f32(ss, "ss");
+  TORCH_CHECK(ss.numel() == 2 * C && C % 4 == 0);
+  if (res) {
+    check_f32(*res, "res");
+    TORCH_CHECK(res->sizes() == x.sizes() && res->is_contiguous());
+  }
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty_like(x);
+  CHECK_HIP_OK(pda::bn_f32_apply(x.data_ptr<float>(), res ? res->data_ptr<float>() : nullptr, ss.data_ptr<float>(),
+                                 y.data_ptr<float>(), M, (int)C, relu ? 1 : 0, stream_of(x)));
+  return y;
+}
+
+// BN backward: y (optional) = the forward output for the ReLU mask; returns {dx, g (masked dy, or
+// undefined), dgamma, dbeta}
+std::vector<Tensor> bn_f32_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, Tensor mean, Tensor invstd,
+                               c10::optional<Tensor> gamma, bool want_g) {
+  check_f32(dy, "dy");
+  check_f32(x, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.is_contiguous() && x.is_contiguous());
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(C % 4 == 0);
+  if (y) {
+    check_f32(*y, "y");
+    TORCH_CHECK(y->sizes() == x.sizes() && y->is_contiguous());
+  }
+  c10::DeviceGuard g(x.device());
+  auto fo = x.options();
+  Tensor dx = at::empty_like(x), gout = want_g ? at::empty_like(x) : Tensor();
+  Tensor dgamma = at::empty({C}, fo), dbeta = at::empty({C}, fo), co = at::empty({3 * C}, fo);
+  Tensor part = at::empty({(int64_t)pda::bn_f32_partials(M, (int)C) * 2 * C}, fo);
+  CHECK_HIP_OK(pda::bn_f32_bwd(dy.data_ptr<float>(), x.data_ptr<float>(), y ? y->data_ptr<float>() : nullptr,
+                               fptr(mean, C, "mean"), fptr(invstd, C, "invstd"), fptr(gamma, C, "gamma"),
+                               dx.data_ptr<float>(), want_g ? gout.data_ptr<float>() : nullptr,
+                               dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), part.data_ptr<float>(),
+                               co.data_ptr<float>(), M, (int)C, stream_of(x)));
+  return {dx, gout, dgamma, dbeta};
+}
+
+std::vector<Tensor> maxpool_f32_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
+  check_f32(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "x must be [N,H,W,C]");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(C % 4 == 0 && k * k <= 255);
+  const int P = (H + 2 * pad - k) / s + 1, Q = (W + 2 * pad - k) / s + 1;
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty({N, P, Q, C}, x.options());
+  Tensor idx = at::empty({N, P, Q, C}, x.options().dtype(at::kByte));
+  CHECK_HIP_OK(pda::maxpool2d_f32_fwd(x.data_ptr<float>(), y.data_ptr<float>(), idx.data_ptr<uint8_t>(), N, H, W, C, P,
+                                      Q, k, s, pad, stream_of(x)));
+  return {y, idx};
+}
+
+Tensor maxpool_f32_bwd(Tensor dy, Tensor idx, int64_t H, int64_t W, int64_t k, int64_t s, int64_t pad) {
+  check_f32(dy, "dy");
+  check_gpu(idx, "idx");
+  TORCH_CHECK(idx.sizes() == dy.sizes() && dy.is_contiguous() && idx.scalar_type() == at::kByte);
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  c10::DeviceGuard g(dy.device());
+  Tensor dx = at::empty({N, H, W, C}, dy.options());
+  CHECK_HIP_OK(pda::maxpool2d_f32_bwd(dy.data_ptr<float>(), idx.data_ptr<uint8_t>(), dx.data_ptr<float>(), N, H, W, C,
+                                      P, Q, k, s, pad, stream_of(dy)));
+  return dx;
+}
+
+Tensor avgpool_f32_fwd(Tensor x) {
+  check_f32(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous());
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  c10::DeviceGuard g(x.device());
+  Tensor y = at::empty({N, C}, x.options());
+  CHECK_HIP_OK(pda::avgpool_f32_fwd(x.data_ptr<float>(), y.data_ptr<float>(), N, HW, C, stream_of(x)));
+  return y;
+}
+
+Tensor avgpool_f32_bwd(Tensor dy, int64_t H, int64_t W) {
+  check_f32(dy, "dy");
+  TORCH_CHECK(dy.dim() == 2 && dy.is_contiguous());
+  const int N = dy.size(0), C = dy.size(1);
+  c10::DeviceGuard g(dy.device());
+  Tensor dx = at::empty({N, H, W, C}, dy.options());
+  CHECK_HIP_OK(pda::avgpool_f32_bwd(dy.data_ptr<float>(), dx.data_ptr<float>(), N, H * W, C, stream_of(dy)));
+  return dx;
+}
+
 PYBIND11_MODULE(_C, m) {
   m.def("stream_create", &stream_create, py::arg("device"), py::arg("priority"));
   m.def("stream_priority_range", &stream_priority_range, py::arg("device"));
@@ -1368,7 +1534,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_act", &gemm_act);
   m.def("set_gemm_paths", &pda::set_gemm_paths, "force a GEMM kernel path: wide=-1 env default, 0 off, 1 auto, 2 force",
         pybind11::arg("wide"), pybind11::arg("variant") = -1);
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
+        py::arg("bias") = py::none(), py::arg("relu") = false, py::arg("out_f32") = false);
+  m.def("split_bf16", &split_bf16, py::arg("x"), py::arg("nseg"), py::arg("lo_mask"), py::arg("stack"));
+  m.def("bn_f32_fwd_train", &bn_f32_fwd_train);
+  m.def("bn_f32_apply", &bn_f32_apply);
+  m.def("bn_f32_bwd", &bn_f32_bwd);
+  m.def("maxpool_f32_fwd", &maxpool_f32_fwd);
+  m.def("maxpool_f32_bwd", &maxpool_f32_bwd);
+  m.def("avgpool_f32_fwd", &avgpool_f32_fwd);
+  m.def("avgpool_f32_bwd", &avgpool_f32_bwd);
   m.def("conv_fwd_stats", &conv_fwd_stats);
   m.def("bn_fwd_train_sums", &bn_fwd_train_sums);
   m.def("bn_fwd_train_sums_dual", &bn_fwd_train_sums_dual);
@@ -1376,7 +1551,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_dual", &bn_bwd_dual);
   m.def("bn_bwd_dual_ok", &bn_bwd_dual_ok);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"),
-        py::arg("pad"), py::arg("dil"), py::arg("addend") = py::none(), py::arg("addend_bits") = py::none());
+        py::arg("pad"), py::arg("dil"), py::arg("addend") = py::none(), py::arg("addend_bits") = py::none(),
+        py::arg("out_f32") = false);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);
@@ -1412,4 +1588,5 @@ PYBIND11_MODULE(_C, m) {
       .def("reset_error", &XgmiComm::reset_error)
       .def_property_readonly("capacity", &XgmiComm::capacity);
   pda_rt::bind_runtime(m);
+  pda_comm::bind_comm(m);
 }

@@ -1,0 +1,328 @@
+// Native RCCL communicator (the reference reaches NCCL through
+// `init_process_group(backend="nccl")`, `02 DDP基本概念/ddp_gpus.py:20-22`, and torch's ProcessGroupNCCL).
+//
+// One communicator = one ncclComm_t over a group of ranks (one process per GPU) + one HIGH-priority
+// HIP stream of its own.  Every collective is enqueued on that stream after an event-wait on the
+// streams that produced its input, and returns a Work handle: an event recorded behind the collective,
+// which a consumer stream waits on (hipStreamWaitEvent, no host blocking) or the host polls.  So
+// gradient buckets are reduced on the comm stream while backward kernels keep running on the compute
+// and weight-gradient streams, and the compute stream only waits where it consumes the result.
+//
+// Bootstrap: rank 0 of the group creates the ncclUniqueId, the ranks exchange it through the
+// framework's key-value store (Python side, pytorchdistributed_amd/comm.py), then ncclCommInitRank.
+// Failure handling: every live communicator is registered with the process-wide abort hook that the
+// native collective watchdog (csrc/runtime/watchdog.cpp) runs on a timeout, so a hung collective is
+// ncclCommAbort-ed (its kernels exit, the waiting streams are released) before the watchdog acts.
+//
+// librccl is torch's own copy (linked from torch/lib, so this and ProcessGroupNCCL share one RCCL).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <stdexcept>
+#include <string>
+
+#include "runtime.h"
+
+namespace pda_comm {
+
+namespace {
+
+void check_nccl(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess && r != ncclInProgress)
+    throw std::runtime_error(std::string("RCCL ") + what + " failed: " + ncclGetErrorString(r));
+}
+
+void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP ") + what + " failed: " + hipGetErrorString(e));
+}
+
+// framework dtype ids (pytorchdistributed_amd/comm.py:_DTYPE)
+ncclDataType_t to_nccl_dtype(int d) {
+  switch (d) {
+    case 0: return ncclFloat32;
+    case 1: return ncclBfloat16;
+    case 2: return ncclFloat16;
+    case 3: return ncclFloat64;
+    case 4: return ncclInt64;
+    case 5: return ncclInt32;
+    case 6: return ncclUint8;
+    case 7: return ncclInt8;
+    default: throw std::invalid_argument("communicator: unsupported dtype id " + std::to_string(d));
+  }
+}
+
+ncclRedOp_t to_nccl_op(int op) {
+  switch (op) {
+    case 0: return ncclSum;
+    case 1: return ncclAvg;
+    case 2: return ncclMax;
+    case 3: return ncclMin;
+    case 4: return ncclProd;
+    default: throw std::invalid_argument("communicator: unsupported reduce op " + std::to_string(op));
+  }
+}
+
+// current-device guard
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    check_hip(hipGetDevice(&prev), "hipGetDevice");
+    if (prev != dev) check_hip(hipSetDevice(dev), "hipSetDevice");
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+}  // namespace
+
+// Completion handle of one enqueued collective (or of a group of point-to-point ops).
+class Work {
+ public:
+  Work(int device, hipStream_t s) : device_(device) {
+    DeviceGuard g(device_);
+    check_hip(hipEventCreateWithFlags(&ev_, hipEventDisableTiming), "hipEventCreate");
+    check_hip(hipEventRecord(ev_, s), "hipEventRecord");
+  }
+  ~Work() {
+    if (ev_) (void)hipEventDestroy(ev_);
+  }
+  Work(const Work&) = delete;
+  Work& operator=(const Work&) = delete;
+  // order `stream` after the collective (no host wait)
+  void wait(uintptr_t stream) {
+    DeviceGuard g(device_);
+    check_hip(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ev_, 0), "hipStreamWaitEvent");
+  }
+  bool is_completed() {
+    const hipError_t e = hipEventQuery(ev_);
+    if (e == hipSuccess) return true;
+    if (e == hipErrorNotReady) return false;
+    check_hip(e, "hipEventQuery");
+    return false;
+  }
+  void synchronize() { check_hip(hipEventSynchronize(ev_), "hipEventSynchronize"); }
+
+ private:
+  int device_;
+  hipEvent_t ev_ = nullptr;
+};
+
+class Communicator;
+
+namespace {
+std::mutex g_live_mu;
+std::set<Communicator*> g_live;
+}  // namespace
+
+class Communicator {
+ public:
+  Communicator(const std::string& uid, int nranks, int rank, int device, bool high_priority)
+      : nranks_(nranks), rank_(rank), device_(device) {
+    if (uid.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("communicator: bad unique id size");
+    if (nranks < 1 || rank < 0 || rank >= nranks) throw std::invalid_argument("communicator: bad rank / size");
+    ncclUniqueId id;
+    std::memcpy(&id, uid.data(), sizeof(id));
+    DeviceGuard g(device_);
+    int lo = 0, hi = 0;
+    check_hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+    check_hip(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, high_priority ? hi : lo),
+              "hipStreamCreateWithPriority");
+    check_hip(hipEventCreateWithFlags(&dep_, hipEventDisableTiming), "hipEventCreate");
+    check_nccl(ncclCommInitRank(&comm_, nranks, id, rank), "ncclCommInitRank");
+    std::lock_guard<std::mutex> l(g_live_mu);
+    g_live.insert(this);
+  }
+
+  ~Communicator() {
+    {
+      std::lock_guard<std::mutex> l(g_live_mu);
+      g_live.erase(this);
+    }
+    DeviceGuard g(device_);
+    if (comm_) {
+      if (aborted_) {
+        (void)ncclCommDestroy(comm_);
+      } else {
+        (void)hipStreamSynchronize(stream_);
+        (void)ncclCommDestroy(comm_);
+      }
+    }
+    if (dep_) (void)hipEventDestroy(dep_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+  }
+
+  int rank() const { return rank_; }
+  int size() const { return nranks_; }
+  int device() const { return device_; }
+  uintptr_t stream() const { return reinterpret_cast<uintptr_t>(stream_); }
+  bool aborted() const { return aborted_; }
+
+  // the comm stream waits for everything queued so far on `s` (the producers of the next input)
+  void wait_stream(uintptr_t s) {
+    DeviceGuard g(device_);
+    check_hip(hipEventRecord(dep_, reinterpret_cast<hipStream_t>(s)), "hipEventRecord");
+    check_hip(hipStreamWaitEvent(stream_, dep_, 0), "hipStreamWaitEvent");
+  }
+
+  std::shared_ptr<Work> all_reduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op) {
+    live();
+    DeviceGuard g(device_);
+    check_nccl(ncclAllReduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), (size_t)count,
+                             to_nccl_dtype(dtype), to_nccl_op(op), comm_, stream_),
+               "ncclAllReduce");
+    return done();
+  }
+
+  // recv[recvcount] = op over ranks of send[rank * recvcount : (rank + 1) * recvcount]
+  std::shared_ptr<Work> reduce_scatter(uintptr_t send, uintptr_t recv, int64_t recvcount, int dtype, int op) {
+    live();
+    DeviceGuard g(device_);
+    check_nccl(ncclReduceScatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv),
+                                 (size_t)recvcount, to_nccl_dtype(dtype), to_nccl_op(op), comm_, stream_),
+               "ncclReduceScatter");
+    return done();
+  }
+
+  // recv[r * sendcount : (r + 1) * sendcount] = send of rank r
+  std::shared_ptr<Work> all_gather(uintptr_t send, uintptr_t recv, int64_t sendcount, int dtype) {
+    live();
+    DeviceGuard g(device_);
+    check_nccl(ncclAllGather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), (size_t)sendcount,
+                             to_nccl_dtype(dtype), comm_, stream_),
+               "ncclAllGather");
+    return done();
+  }
+
+  std::shared_ptr<Work> broadcast(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int root) {
+    live();
+    DeviceGuard g(device_);
+    check_nccl(ncclBroadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), (size_t)count,
+                             to_nccl_dtype(dtype), root, comm_, stream_),
+               "ncclBroadcast");
+    return done();
+  }
+
+  // point-to-point: inside group_start / group_end they are fused into one launch (returns None then)
+  std::shared_ptr<Work> send(uintptr_t buf, int64_t count, int dtype, int peer) {
+    live();
+    DeviceGuard g(device_);
+    check_nccl(ncclSend(reinterpret_cast<const void*>(buf), (size_t)count, to_nccl_dtype(dtype), peer, comm_, stream_),
+               "ncclSend");
+    return group_depth_ ? nullptr : done();
+  }
+
+  std::shared_ptr<Work> recv(uintptr_t buf, int64_t count, int dtype, int peer) {
+    live();
+    DeviceGuard g(device_);
+    check_nccl(ncclRecv(reinterpret_cast<void*>(buf), (size_t)count, to_nccl_dtype(dtype), peer, comm_, stream_),
+               "ncclRecv");
+    return group_depth_ ? nullptr : done();
+  }
+
+  void group_start() {
+    check_nccl(ncclGroupStart(), "ncclGroupStart");
+    ++group_depth_;
+  }
+
+  std::shared_ptr<Work> group_end() {
+    if (group_depth_ == 0) throw std::runtime_error("communicator: group_end without group_start");
+    DeviceGuard g(device_);
+    check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+    --group_depth_;
+    return group_depth_ ? nullptr : done();
+  }
+
+  // abort: in-flight collectives exit, further calls raise (used by the watchdog hook)
+  void abort() {
+    if (aborted_ || !comm_) return;
+    aborted_ = true;
+    (void)ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
+
+  std::string async_error() {
+    if (!comm_) return aborted_ ? "aborted" : "";
+    ncclResult_t r = ncclSuccess;
+    if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
+    return r == ncclSuccess || r == ncclInProgress ? "" : ncclGetErrorString(r);
+  }
+
+  static int abort_all() {
+    std::lock_guard<std::mutex> l(g_live_mu);
+    int n = 0;
+    for (Communicator* c : g_live) {
+      if (!c->aborted_) {
+        c->abort();
+        ++n;
+      }
+    }
+    return n;
+  }
+
+ private:
+  void live() const {
+    if (aborted_) throw std::runtime_error("communicator was aborted (collective timeout / abort())");
+  }
+  std::shared_ptr<Work> done() { return std::make_shared<Work>(device_, stream_); }
+
+  int nranks_, rank_, device_;
+  ncclComm_t comm_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  hipEvent_t dep_ = nullptr;
+  int group_depth_ = 0;
+  bool aborted_ = false;
+};
+
+void bind_comm(pybind11::module& m) {
+  namespace py = pybind11;
+  m.def("rccl_unique_id", [] {
+    ncclUniqueId id;
+    check_nccl(ncclGetUniqueId(&id), "ncclGetUniqueId");
+    return py::bytes(reinterpret_cast<const char*>(&id), sizeof(id));
+  });
+  m.def("rccl_version", [] {
+    int v = 0;
+    check_nccl(ncclGetVersion(&v), "ncclGetVersion");
+    return v;
+  });
+  m.def("rccl_abort_all", &Communicator::abort_all, "ncclCommAbort every live communicator of this process");
+  py::class_<Work, std::shared_ptr<Work>>(m, "RcclWork")
+      .def("wait", &Work::wait, py::arg("stream"))
+      .def("is_completed", &Work::is_completed)
+      .def("synchronize", &Work::synchronize, py::call_guard<py::gil_scoped_release>());
+  py::class_<Communicator>(m, "RcclComm")
+      .def(py::init([](py::bytes uid, int nranks, int rank, int device, bool high_priority) {
+             std::string u = uid;
+             py::gil_scoped_release nogil;  // ncclCommInitRank blocks until every rank joined
+             return new Communicator(u, nranks, rank, device, high_priority);
+           }),
+           py::arg("uid"), py::arg("nranks"), py::arg("rank"), py::arg("device"), py::arg("high_priority") = true)
+      .def_property_readonly("rank", &Communicator::rank)
+      .def_property_readonly("size", &Communicator::size)
+      .def_property_readonly("device", &Communicator::device)
+      .def_property_readonly("stream", &Communicator::stream)
+      .def_property_readonly("aborted", &Communicator::aborted)
+      .def("wait_stream", &Communicator::wait_stream)
+      .def("all_reduce", &Communicator::all_reduce)
+      .def("reduce_scatter", &Communicator::reduce_scatter)
+      .def("all_gather", &Communicator::all_gather)
+      .def("broadcast", &Communicator::broadcast)
+      .def("send", &Communicator::send)
+      .def("recv", &Communicator::recv)
+      .def("group_start", &Communicator::group_start)
+      .def("group_end", &Communicator::group_end)
+      .def("abort", &Communicator::abort)
+      .def("async_error", &Communicator::async_error);
+  // the watchdog aborts every communicator before it acts on a timed-out collective
+  pda_rt::set_abort_hook([] { Communicator::abort_all(); });
+}
+
+}  // namespace pda_comm

@@ -200,16 +200,17 @@ int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, 
 // stats (optional): BatchNorm sums of the output accumulated (atomically; must start zeroed) into a
 // [stats_rows][2][Cout] fp32 table: sum(y - K) and sum((y - K)^2) with K = stats_shift (e.g. the running
 // mean), each output tile adding into row (tile_m % stats_rows)
-hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int Cout, int R, int S,
-                      int P, int Q, int stride, int pad, int dil, const void* bias, bool bias_f32, bool relu,
-                      float* stats, const float* stats_shift, int stats_rows, hipStream_t st);
+// y / dx: bf16, or fp32 with y_f32 / dx_f32 (the split-bf16 fp32 path, fp32x3.hip)
+hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int Cout,
+                      int R, int S, int P, int Q, int stride, int pad, int dil, const void* bias, bool bias_f32,
+                      bool relu, float* stats, const float* stats_shift, int stats_rows, hipStream_t st);
 // addend (optional, bf16, dx's layout): dx = dgrad + addend, fused into the store; addend_bits (optional,
 // [numel/8] bytes, bit j of byte v for element 8v + j): only the addend elements whose bit is set
 // wt: the weight transposed by conv_weight_transpose — except for a 1x1 stride-1 unpadded conv
 // (conv_dgrad_needs_wt() false), whose dgrad is a plain GEMM that reads w [Cout][C] MN-major in place.
 bool conv_dgrad_needs_wt(int R, int S, int stride, int pad);
-hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf16_t* dx, int N, int H, int W, int C,
-                        int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,
+hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, void* dx, bool dx_f32, int N, int H, int W,
+                        int C, int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,
                         const uint8_t* addend_bits, hipStream_t st);
 hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32, int N, int H, int W, int C,
                         int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, float* slab,
@@ -297,5 +298,25 @@ hipError_t embedding_bwd(const int64_t* idx, const bf16_t* dy, float* acc, int64
 hipError_t rope_apply(const bf16_t* x, bf16_t* y, const float* cos, const float* sin, int B, int T, int H, int D,
                       int64_t sb, int64_t st_, int64_t sh, int64_t yb, int64_t yt, int64_t yh, bool inverse,
                       hipStream_t st);
+
+// ---- fp32x3.hip (fp32 training path: split-bf16 GEMM operands + fp32 BN / pooling)
+hipError_t split_bf16(const float* x, bf16_t* out, int64_t rows, int64_t C, int nseg, int lo_mask, int64_t seg_stride,
+                      int64_t row_stride, hipStream_t st);
+int bn_f32_partials(int64_t M, int C);
+hipError_t bn_f32_fwd_train(const float* x, const float* res, const float* gamma, const float* beta,
+                            float* running_mean, float* running_var, const float* shift, float momentum, float eps,
+                            int relu, float* y, float* save_mean, float* save_invstd, float* ss, float* part,
+                            int64_t* num_batches, int64_t M, int C, hipStream_t st);
+hipError_t bn_f32_apply(const float* x, const float* res, const float* ss, float* y, int64_t M, int C, int relu,
+                        hipStream_t st);
+hipError_t bn_f32_bwd(const float* dy, const float* x, const float* y, const float* mean, const float* invstd,
+                      const float* gamma, float* dx, float* gout, float* dgamma, float* dbeta, float* part, float* co,
+                      int64_t M, int C, hipStream_t st);
+hipError_t maxpool2d_f32_fwd(const float* x, float* y, uint8_t* idx, int N, int H, int W, int C, int P, int Q, int k,
+                             int s, int pad, hipStream_t st);
+hipError_t maxpool2d_f32_bwd(const float* dy, const uint8_t* idx, float* dx, int N, int H, int W, int C, int P, int Q,
+                             int k, int s, int pad, hipStream_t st);
+hipError_t avgpool_f32_fwd(const float* x, float* y, int N, int HW, int C, hipStream_t st);
+hipError_t avgpool_f32_bwd(const float* dy, float* dx, int N, int HW, int C, hipStream_t st);
 
 }  // namespace pda

@@ -1934,12 +1934,13 @@ bool wg3_geom(int N, int H, int W, int C, int Cout, int R, int S, int stride, in
 int wg3_splits(const Wg3Geom& g) { return (g.groups + g.gps - 1) / g.gps; }
 
 // y[N,P,Q,Cout] = conv(x[N,H,W,C], w[Cout,R,S,C]) (+bias, relu)
-hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H, int W, int C, int Cout, int R, int S,
-                      int P, int Q, int stride, int pad, int dil, const void* bias, bool bias_f32, bool relu,
-                      float* stats, const float* stats_shift, int stats_rows, hipStream_t st) {
+hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int Cout,
+                      int R, int S, int P, int Q, int stride, int pad, int dil, const void* bias, bool bias_f32,
+                      bool relu, float* stats, const float* stats_shift, int stats_rows, hipStream_t st) {
   const int64_t M = (int64_t)N * P * Q, Nn = Cout, K = (int64_t)R * S * C;
+  if (y_f32 && stats) return hipErrorInvalidValue;  // epilogue statistics are a bf16-output feature
   Plan p = plan_gemm(M, Nn, K, false, 512);
-  Epi epi{y, Cout, 0, bias, bias_f32 ? 1 : 0, relu ? 1 : 0, nullptr};
+  Epi epi{y, Cout, y_f32 ? 1 : 0, bias, bias_f32 ? 1 : 0, relu ? 1 : 0, nullptr};
   epi.stats = stats;
   epi.stats_shift = stats_shift;
   epi.stats_rows = stats_rows > 0 ? stats_rows : 1;
@@ -1955,16 +1956,17 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, bf16_t* y, int N, int H,
 // it (wt phase-packed by conv_weight_transpose); folded single launch when stride > 1 and dil > 1.
 bool conv_dgrad_needs_wt(int R, int S, int stride, int pad) { return !(R == 1 && S == 1 && stride == 1 && pad == 0); }
 
-hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf16_t* dx, int N, int H, int W, int C,
-                        int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,
+hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, void* dx, bool dx_f32, int N, int H, int W,
+                        int C, int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,
                         const uint8_t* addend_bits, hipStream_t st) {
+  const int cf = dx_f32 ? 1 : 0;
   if (!conv_dgrad_needs_wt(R, S, stride, pad)) {
     // 1x1 stride 1: dx[NHW, C] = dy[NHW, Cout] * w[Cout, C] — dy rows are the K-major A operand and the
     // OHWI weight is already the MN-major B operand (k = co rows of C contiguous channels): no weight
     // transpose launch (36 of ResNet-50's 53 convs are 1x1, 32 of them stride 1)
     const int64_t M = (int64_t)N * H * W, Nn = C, K = Cout;
     Plan p = plan_gemm(M, Nn, K, false, 512);
-    Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
+    Epi epi{dx, C, cf, nullptr, 0, 0, nullptr};
     epi.addend = addend;
     epi.addend_bits = addend_bits;
     auto mk_a = [&](auto t) { t.p = dy; t.rows = M; t.K = K; t.ld = Cout; return t; };
@@ -1975,7 +1977,7 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf1
   if (!dgrad_phased(stride, dil)) {
     const int64_t M = (int64_t)N * H * W, Nn = C, K = (int64_t)R * S * Cout;
     Plan p = plan_gemm(M, Nn, K, false, 512);
-    Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
+    Epi epi{dx, C, cf, nullptr, 0, 0, nullptr};
     epi.addend = addend;
     epi.addend_bits = addend_bits;
     auto mk_a = [&](auto t) { t.dy = dy; t.g = g; t.M = M; t.K = K; return t; };
@@ -1984,7 +1986,7 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf1
   }
   if (stride == 1) {
     // stride-1 dgrad = the 3x3 conv of dy with the rotated transposed weights (halo path)
-    Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
+    Epi epi{dx, C, cf, nullptr, 0, 0, nullptr};
     epi.addend = addend;
     epi.addend_bits = addend_bits;
     if (use_halo(H, W, Cout, C, R, S, stride, pad, dil, epi)) return launch_halo(dy, wt, N, H, W, Cout, C, true, epi, st);
@@ -2007,7 +2009,7 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, bf1
       const int64_t M = (int64_t)N * Hh * Wh, Nn = C, K = (int64_t)a.n * b.n * Cout;
       const bf16_t* wph = wt + ((int64_t)a.cum * S + (int64_t)a.n * b.cum) * C * Cout;
       Plan p = plan_gemm(M, Nn, K, false, 512);
-      Epi epi{dx, C, 0, nullptr, 0, 0, nullptr};
+      Epi epi{dx, C, cf, nullptr, 0, 0, nullptr};
       epi.addend = addend;
       epi.addend_bits = addend_bits;
       if (stride > 1) {

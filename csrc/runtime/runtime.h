@@ -123,6 +123,11 @@ class HostRing {
 // ------------------------------------------------------------------ collective watchdog
 // Per-process native thread (no GIL) that enforces a deadline on every armed collective; on expiry it
 // reports all pending operations and aborts / exits the rank (see watchdog.cpp).
+// Process-wide hook run by the watchdog before it acts on a timed-out collective (the RCCL communicators
+// register ncclCommAbort of every live communicator here: csrc/comm/communicator.cpp).
+void set_abort_hook(void (*hook)());
+void run_abort_hook();
+
 class Watchdog {
  public:
   Watchdog(double timeout_s, int rank, const std::string& action, int exit_code, double poll_s);

@@ -10,6 +10,7 @@
 //     stack, the launcher sees the abnormal exit and tears the job down), or
 //   * _exit(code), or
 //   * only records the expiry (report mode, used by tests and by callers that poll `expired()`).
+#include <atomic>
 #include <chrono>
 #include <csignal>
 #include <cstdio>
@@ -19,6 +20,16 @@
 #include "runtime.h"
 
 namespace pda_rt {
+
+namespace {
+std::atomic<void (*)()> g_abort_hook{nullptr};
+}  // namespace
+
+void set_abort_hook(void (*hook)()) { g_abort_hook.store(hook); }
+
+void run_abort_hook() {
+  if (auto h = g_abort_hook.load()) h();
+}
 
 namespace {
 double now_s() {
@@ -108,6 +119,11 @@ void Watchdog::loop() {
               (long long)kv.first, kv.second.desc.c_str(), t - kv.second.start, kv.second.deadline - kv.second.start);
     fflush(stderr);
     if (action_ == "report") continue;
+    // release every RCCL communicator first: their in-flight kernels exit and the streams waiting on
+    // them drain, so the abort / exit below does not leave the GPU with a stuck collective
+    lk.unlock();
+    run_abort_hook();
+    lk.lock();
     if (action_ == "exit") {
       fprintf(stderr, "[pda watchdog] rank %d: exiting with code %d\n", rank_, exit_code_);
       fflush(stderr);

@@ -6,6 +6,7 @@ to the MI355X box already carries the compiled extension.
 
 * ``csrc/kernels/*.hip``  -> ``hipcc --offload-arch=gfx950`` (pure HIP, no torch headers: fast)
 * ``csrc/runtime/*.cpp``  -> host C++ (pybind11 only)
+* ``csrc/comm/*.cpp``     -> host C++ against HIP + RCCL (torch's bundled librccl, one RCCL per process)
 * ``csrc/bindings.cpp``   -> host C++ against the torch headers
 """
 from __future__ import annotations
@@ -47,7 +48,8 @@ def _torch_paths():
 def _sources():
     hip = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     rt = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
-    return hip, rt, [os.path.join(CSRC, "bindings.cpp")]
+    comm = sorted(glob.glob(os.path.join(CSRC, "comm", "*.cpp")))
+    return hip, rt, comm, [os.path.join(CSRC, "bindings.cpp")]
 
 
 def write_ninja(debug: bool = False) -> str:
@@ -56,7 +58,7 @@ def write_ninja(debug: bool = False) -> str:
     tinc, tlib, abi = _torch_paths()
     pyinc = sysconfig.get_paths()["include"]
     os.makedirs(BUILD, exist_ok=True)
-    hip, rt, bind = _sources()
+    hip, rt, comm, bind = _sources()
     opt = "-O0 -g" if debug else "-O3"
     common_inc = f"-I{CSRC}/include -I{CSRC}/runtime"
     hipcc = os.path.join(ROCM, "bin", "hipcc")
@@ -68,12 +70,14 @@ def write_ninja(debug: bool = False) -> str:
         f"hipflags = --offload-arch={ARCH} {opt} -std=c++17 -fPIC -Wall -Wno-unused-function {common_inc}",
         f"rtflags = {opt} -std=c++17 -fPIC -Wall {common_inc} -I{pybind11.get_include()} -I{pyinc}"
         f" -D_GLIBCXX_USE_CXX11_ABI={abi}",
+        f"commflags = {opt} -std=c++17 -fPIC -Wall {common_inc} -I{pybind11.get_include()} -I{pyinc}"
+        f" -isystem {ROCM}/include -D__HIP_PLATFORM_AMD__=1 -D_GLIBCXX_USE_CXX11_ABI={abi}",
         f"bindflags = -O2 -std=c++17 -fPIC {common_inc} -I{pybind11.get_include()} -I{pyinc} "
         + " ".join(f"-isystem {p}" for p in tinc)
         + f" -isystem {ROCM}/include -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -DTORCH_EXTENSION_NAME={EXT_NAME}"
         f" -DTORCH_API_INCLUDE_EXTENSION_H -D_GLIBCXX_USE_CXX11_ABI={abi}",
         f"ldflags = -shared -fPIC --offload-arch={ARCH} -L{tlib} -Wl,-rpath,{tlib} -lc10 -lc10_hip -ltorch -ltorch_cpu"
-        f" -ltorch_hip -ltorch_python -L{ROCM}/lib -lamdhip64",
+        f" -ltorch_hip -ltorch_python -lrccl -L{ROCM}/lib -lamdhip64",
         "rule hip",
         "  command = $hipcc $hipflags -MD -MF $out.d -c $in -o $out",
         "  depfile = $out.d",
@@ -84,6 +88,11 @@ def write_ninja(debug: bool = False) -> str:
         "  depfile = $out.d",
         "  deps = gcc",
         "  description = CXX $in",
+        "rule comm",
+        "  command = $cxx $commflags -MD -MF $out.d -c $in -o $out",
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = CXX(rccl) $in",
         "rule bind",
         "  command = $cxx $bindflags -MD -MF $out.d -c $in -o $out",
         "  depfile = $out.d",
@@ -94,7 +103,8 @@ def write_ninja(debug: bool = False) -> str:
         "  description = LINK $out",
     ]
     objs = []
-    for src, rule in [(s, "hip") for s in hip] + [(s, "rt") for s in rt] + [(s, "bind") for s in bind]:
+    for src, rule in ([(s, "hip") for s in hip] + [(s, "rt") for s in rt] + [(s, "comm") for s in comm]
+                      + [(s, "bind") for s in bind]):
         rel = os.path.relpath(src, CSRC).replace(os.sep, "_")
         obj = os.path.join(BUILD, rel + ".o")
         objs.append(obj)

@@ -11,7 +11,11 @@ Modes:
   (`utils/graphs.py`); every replay is a full optimizer step on a fresh device batch.
 Variants: ``single`` (1 device), ``mp`` (layer split, stem..layer2 on dev0, rest on dev1), ``pp``
 (micro-batch pipeline, ``--split-size``), ``sweep`` (pp over the reference's split sizes).
-Precision: bf16 compute with fp32 master weights (the reference ran fp32/TF32 on A100).
+Precision (``--dtype``): ``fp32`` (default, the reference's precision: fp32 activations / weights /
+Adam; convs on split-bf16 MFMA operands, ~1e-5 relative — the reference's A100 ran its convs in TF32,
+~1e-3) or ``bf16`` (bf16 compute, fp32 master weights).
+Device layout: with one visible GPU the two "devices" of mp / pp are the same GPU (``devices`` in the
+output says so); the reference used two A100s.
 """
 from __future__ import annotations
 
@@ -35,19 +39,20 @@ REFERENCE_S = {"single": 0.248, "mp": 0.272, "pp20": 0.454,
 SPLITS = [1, 3, 5, 8, 10, 12, 20, 40, 60]
 
 
-def make_model(kind, devs, split=20):
+def make_model(kind, devs, split=20, dtype=torch.float32):
     if kind == "single":
-        return resnet50(device=devs[0], dtype=torch.bfloat16), devs[0]
-    base = resnet50(dtype=torch.bfloat16)
+        return resnet50(device=devs[0], dtype=dtype), devs[0]
+    base = resnet50(dtype=dtype)
     if kind == "mp":
         return ModelParallelResNet50(base, devices=devs), devs[1]
     return PipelineParallelResNet50(base, devices=devs, split_size=split), devs[1]
 
 
-def run(kind, devs, mode, split=20, repeat=10, batch=120, size=128, graph=False):
-    model, out_dev = make_model(kind, devs, split)
+def run(kind, devs, mode, split=20, repeat=10, batch=120, size=128, graph=False, dtype=torch.float32):
+    model, out_dev = make_model(kind, devs, split, dtype)
     in_dev = devs[0]
-    dev_data = DeviceSyntheticImages(batch, size, 1000, device=in_dev, seed=0) if mode == "clean" else None
+    dev_data = (DeviceSyntheticImages(batch, size, 1000, device=in_dev, seed=0, dtype=dtype) if mode == "clean"
+                else None)
     opt_holder = {}
     if graph:
         if mode != "clean":
@@ -84,7 +89,7 @@ def run(kind, devs, mode, split=20, repeat=10, batch=120, size=128, graph=False)
         for _ in range(3):
             if mode == "parity":
                 inputs, labels = random_image_batch(batch, (size, size), 1000)
-                x = inputs.to(in_dev).permute(0, 2, 3, 1).to(torch.bfloat16)
+                x = inputs.to(in_dev).permute(0, 2, 3, 1).to(dtype)
                 y = labels.to(out_dev)
             else:
                 x, yi = dev_data.next()
@@ -110,13 +115,15 @@ def main(argv=None):
     ap.add_argument("--repeat", type=int, default=10)
     ap.add_argument("--sweep", action="store_true")
     ap.add_argument("--graph", action="store_true", help="capture each step into a HIP graph (clean mode)")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     a = ap.parse_args(argv)
     n = torch.cuda.device_count()
     devs = [int(d) for d in a.devices.split(",")] if a.devices else ([0, 1] if n >= 2 else [0, 0])
     devs = [torch.device("cuda", d) for d in devs]
+    dtype = torch.float32 if a.dtype == "fp32" else torch.bfloat16
     results = {}
     for v in a.variants.split(","):
-        m, s = run(v, devs, a.mode, a.split_size, a.repeat, graph=a.graph)
+        m, s = run(v, devs, a.mode, a.split_size, a.repeat, graph=a.graph, dtype=dtype)
         key = "pp20" if v == "pp" and a.split_size == 20 else v
         ref = REFERENCE_S.get(key)
         results[v] = {"mean_s": round(m, 4), "std_s": round(s, 4), "img_per_s": round(360 / m, 1),
@@ -124,13 +131,16 @@ def main(argv=None):
     if a.sweep:
         sw = {}
         for sp in SPLITS:
-            m, s = run("pp", devs, a.mode, sp, a.repeat, graph=a.graph)
+            m, s = run("pp", devs, a.mode, sp, a.repeat, graph=a.graph, dtype=dtype)
             ref = REFERENCE_S["sweep"][sp]
             sw[sp] = {"mean_s": round(m, 4), "std_s": round(s, 4), "reference_s_A100": ref,
                       "speedup_vs_reference": round(ref / m, 2)}
         results["sweep"] = sw
     print(json.dumps({"benchmark": "NB03 ResNet-50 train() (3 Adam steps x 120 imgs @128px)", "mode": a.mode, "graph": a.graph,
-                      "devices": [str(d) for d in devs], "dtype": "bf16 (fp32 masters)", "results": results}))
+                      "devices": [str(d) for d in devs],
+                      "dtype": ("fp32 (convs: split-bf16 x3 MFMA, fp32 accumulate)" if a.dtype == "fp32"
+                                else "bf16 (fp32 masters)"),
+                      "results": results}))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,183 @@
+"""Native RCCL communicator (reference `init_process_group(backend="nccl")` at
+`02 DDP基本概念/ddp_gpus.py:20-22`, which torch serves with ProcessGroupNCCL).
+
+:class:`Communicator` owns an ``ncclComm_t`` over a process group and a high-priority HIP stream of
+its own (`csrc/comm/communicator.cpp`).  A collective is enqueued on that stream after an event-wait
+on the streams that produce its input and returns a :class:`Work`: ``wait()`` orders the current
+stream after the collective without blocking the host, ``is_completed()`` polls.  The bootstrap is
+the framework's own: group rank 0 calls ``ncclGetUniqueId`` and publishes the id in the rendezvous
+store (the native C++ store when the framework launched the job, the launcher's otherwise), every
+rank reads it and joins with ``ncclCommInitRank``.  Every communicator is registered with the native
+collective watchdog's abort hook: a collective that outlives its deadline is ``ncclCommAbort``-ed.
+
+torch.distributed (c10d) remains the control plane — rendezvous, barriers, object collectives; the
+gradient / parameter traffic of DDP, FSDP and the pipeline's DP group runs here (``PDA_COMM=c10d``
+switches it back to ProcessGroupNCCL).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Iterable, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import _native
+
+_DTYPE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3, torch.int64: 4, torch.int32: 5,
+          torch.uint8: 6, torch.int8: 7}
+_OPS = {"sum": 0, "avg": 1, "max": 2, "min": 3, "prod": 4}
+_created: Dict[Tuple[int, ...], int] = {}
+_cache: Dict[Tuple[Tuple[int, ...], int], "Communicator"] = {}
+
+
+def enabled() -> bool:
+    """Gradient collectives on the native communicator (default) or on c10d (``PDA_COMM=c10d``)."""
+    return os.environ.get("PDA_COMM", "native") == "native"
+
+
+def _store():
+    from . import distributed as pdist
+
+    st = pdist._STATE.get("store")
+    if st is None:
+        st = dist.distributed_c10d._get_default_store()
+    return st
+
+
+class Work:
+    """Completion handle of one enqueued collective; keeps its tensors alive until completion."""
+
+    def __init__(self, w, keep: tuple = ()):
+        self._w = w
+        self._keep = keep
+
+    def wait(self, stream: Optional[torch.cuda.Stream] = None):
+        s = stream if stream is not None else torch.cuda.current_stream()
+        self._w.wait(s.cuda_stream)
+        return True
+
+    def is_completed(self) -> bool:
+        done = self._w.is_completed()
+        if done:
+            self._keep = ()
+        return done
+
+    def synchronize(self):
+        self._w.synchronize()
+        self._keep = ()
+
+
+class Communicator:
+    """RCCL communicator over ``group`` (default: the world) on this rank's GPU."""
+
+    def __init__(self, group=None, device: Optional[torch.device] = None, high_priority: bool = True):
+        if not dist.is_initialized():
+            raise RuntimeError("Communicator needs an initialised default process group (rendezvous / store)")
+        self.group = group
+        self.ranks: List[int] = (dist.get_process_group_ranks(group) if group is not None
+                                 else list(range(dist.get_world_size())))
+        self.rank = dist.get_rank(group)
+        self.size = len(self.ranks)
+        self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        key_ranks = tuple(self.ranks)
+        seq = _created.get(key_ranks, 0)
+        _created[key_ranks] = seq + 1
+        key = f"pda/rccl/{'-'.join(map(str, key_ranks))}/{seq}"
+        store = _store()
+        C = _native.C()
+        if self.rank == 0:
+            uid = C.rccl_unique_id()
+            store.set(key, uid)
+        else:
+            uid = store.get(key)
+        self._c = C.RcclComm(bytes(uid), self.size, self.rank, self.device.index, high_priority)
+        self.stream = torch.cuda.ExternalStream(self._c.stream, device=self.device)
+
+    # ---------------------------------------------------------------- ordering
+    def _after(self, streams: Optional[Iterable[torch.cuda.Stream]]):
+        for s in (streams if streams is not None else [torch.cuda.current_stream(self.device)]):
+            self._c.wait_stream(s.cuda_stream)
+
+    def _hold(self, *ts: torch.Tensor):
+        for t in ts:
+            t.record_stream(self.stream)  # the caching allocator must not recycle it under the collective
+
+    # ---------------------------------------------------------------- collectives
+    def all_reduce(self, t: torch.Tensor, op: str = "sum", streams=None) -> Work:
+        """In place; ``op`` in sum / avg / max / min / prod.  ``streams``: producers of ``t`` (default:
+        the current stream)."""
+        assert t.is_contiguous() and t.device == self.device
+        self._after(streams)
+        self._hold(t)
+        return Work(self._c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPE[t.dtype], _OPS[op]), (t,))
+
+    def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum", streams=None) -> Work:
+        """``out`` = op over ranks of this rank's ``out.numel()`` chunk of ``inp``."""
+        assert inp.numel() == out.numel() * self.size and inp.dtype == out.dtype
+        assert inp.is_contiguous() and out.is_contiguous()
+        self._after(streams)
+        self._hold(out, inp)
+        return Work(self._c.reduce_scatter(inp.data_ptr(), out.data_ptr(), out.numel(), _DTYPE[out.dtype], _OPS[op]),
+                    (out, inp))
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor, streams=None) -> Work:
+        """``out`` = concatenation over ranks of ``inp``."""
+        assert out.numel() == inp.numel() * self.size and inp.dtype == out.dtype
+        assert inp.is_contiguous() and out.is_contiguous()
+        self._after(streams)
+        self._hold(out, inp)
+        return Work(self._c.all_gather(inp.data_ptr(), out.data_ptr(), inp.numel(), _DTYPE[inp.dtype]), (out, inp))
+
+    def broadcast(self, t: torch.Tensor, root: int = 0, streams=None) -> Work:
+        """In place from group rank ``root``."""
+        assert t.is_contiguous()
+        self._after(streams)
+        self._hold(t)
+        return Work(self._c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPE[t.dtype], root), (t,))
+
+    def send_recv(self, sends: List[Tuple[torch.Tensor, int]], recvs: List[Tuple[torch.Tensor, int]],
+                  streams=None) -> Work:
+        """One fused group of point-to-point transfers (group ranks as peers)."""
+        self._after(streams)
+        self._c.group_start()
+        try:
+            for t, peer in sends:
+                assert t.is_contiguous()
+                self._hold(t)
+                self._c.send(t.data_ptr(), t.numel(), _DTYPE[t.dtype], peer)
+            for t, peer in recvs:
+                assert t.is_contiguous()
+                self._hold(t)
+                self._c.recv(t.data_ptr(), t.numel(), _DTYPE[t.dtype], peer)
+        finally:
+            w = self._c.group_end()
+        return Work(w, tuple(t for t, _ in sends) + tuple(t for t, _ in recvs))
+
+    # ---------------------------------------------------------------- failure handling
+    def abort(self):
+        self._c.abort()
+
+    @property
+    def aborted(self) -> bool:
+        return self._c.aborted
+
+    def async_error(self) -> str:
+        return self._c.async_error()
+
+
+def for_group(group=None, device: Optional[torch.device] = None) -> Communicator:
+    """The process's communicator for ``group`` on ``device`` (created once; all ranks of the group
+    must ask for it in the same order, like any collective)."""
+    ranks = tuple(dist.get_process_group_ranks(group)) if group is not None else tuple(range(dist.get_world_size()))
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    key = (ranks, dev.index)
+    c = _cache.get(key)
+    if c is None or c.aborted:
+        c = _cache[key] = Communicator(group, dev)
+    return c
+
+
+def reset():
+    """Drop cached communicators (destroy_process_group)."""
+    _cache.clear()

@@ -242,6 +242,9 @@ def set_device(local_rank: int):
 
 
 def destroy_process_group():
+    from . import comm as _comm
+
+    _comm.reset()  # native RCCL communicators first (ncclCommDestroy), then c10d's
     if dist.is_initialized():
         dist.destroy_process_group()
     _STATE["ring"] = None

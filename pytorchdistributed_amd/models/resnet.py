@@ -49,7 +49,8 @@ class Bottleneck(tnn.Module):
         # x feeds conv1 and the shortcut: its two gradients are summed inside conv1's (or the
         # downsample conv's) dgrad store instead of by a separate autograd add (ops/grad_join.py)
         # Every conv also reduces the batch statistics of the BN it feeds in its epilogue (bn=...).
-        join = GradJoin(2) if (x.is_cuda and x.requires_grad and torch.is_grad_enabled()) else None
+        join = (GradJoin(2) if (x.is_cuda and x.dtype == torch.bfloat16 and x.requires_grad and torch.is_grad_enabled())
+                else None)
         out = self.bn1(self.conv1(x, grad_join=join, bn=self.bn1), relu=True)
         out = self.bn2(self.conv2(out, bn=self.bn2), relu=True)
         if self.downsample is not None:

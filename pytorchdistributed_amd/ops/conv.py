@@ -119,6 +119,10 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias=None, stride: int = 1, pa
     if x.is_cuda:
         if weight.shape[-1] != x.shape[-1]:  # stem: input channels padded to a multiple of 8
             weight = F.pad(weight, (0, x.shape[-1] - weight.shape[-1]))
+        if x.dtype == torch.float32:  # split-bf16 operands on the same MFMA kernels (ops/fp32.py)
+            from . import fp32
+
+            return fp32.conv2d(x, weight, bias, stride, padding, dilation, relu)
         return _Conv2dFn.apply(x, weight, bias, stride, padding, dilation, relu, grad_join)
     if weight.shape[-1] != x.shape[-1]:
         x = x[..., : weight.shape[-1]]

@@ -163,6 +163,11 @@ def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=Tru
         table, shift = stats if stats is not None else (None, None)
         return _BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
                                   relu, residual_join, table, shift, num_batches_tracked if training else None)
+    if x.is_cuda and x.dtype == torch.float32 and x.shape[-1] % 4 == 0 and residual_join is None:
+        from . import fp32
+
+        return fp32.batch_norm(x, gamma, beta, running_mean, running_var, training, momentum, eps, residual, relu,
+                               num_batches_tracked)
     if training and num_batches_tracked is not None:
         num_batches_tracked.add_(1)
     return _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu)

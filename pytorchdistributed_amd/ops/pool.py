@@ -88,6 +88,10 @@ class _AvgPoolFn(torch.autograd.Function):
 def max_pool2d(x, kernel_size=3, stride=2, padding=1):
     if x.is_cuda and x.dtype == torch.bfloat16:
         return _MaxPoolFn.apply(x, kernel_size, stride, padding)
+    if x.is_cuda and x.dtype == torch.float32 and x.shape[-1] % 4 == 0:
+        from .fp32 import MaxPoolF32Fn
+
+        return MaxPoolF32Fn.apply(x, kernel_size, stride, padding)
     y = F.max_pool2d(x.permute(0, 3, 1, 2), kernel_size, stride, padding)
     return y.permute(0, 2, 3, 1).contiguous()
 
@@ -96,5 +100,9 @@ def global_avg_pool2d(x, out_fp32=False):
     """``[N,H,W,C] -> [N,C]`` spatial mean."""
     if x.is_cuda and x.dtype == torch.bfloat16:
         return _AvgPoolFn.apply(x, out_fp32)
+    if x.is_cuda and x.dtype == torch.float32:
+        from .fp32 import AvgPoolF32Fn
+
+        return AvgPoolF32Fn.apply(x)
     y = x.float().mean(dim=(1, 2))
     return y if out_fp32 else y.to(x.dtype)

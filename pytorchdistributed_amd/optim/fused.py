@@ -50,8 +50,49 @@ class _FusedBase(torch.optim.Optimizer):
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         self._dstep.clear()
+        # loaded per-parameter tensors replace the flat-buffer views in self.state: copy them back into
+        # the flat buffers the update kernels read (and re-bind the views)
+        for st in self._flat.values():
+            self._link(st, load=True)
+
+    def state_dict(self):
+        # the flat path keeps the step count per group: mirror it into every parameter's state (torch's
+        # layout: state[p]["step"]) so a resumed Adam continues its bias correction
+        for st in self._flat.values():
+            for p in st["fg"].params:
+                self.state[p]["step"] = torch.tensor(float(st["step"]))
+        return super().state_dict()
 
     # --------------------------------------------------------------- flat path
+    def _link(self, st: dict, load: bool = False, old: Optional[dict] = None):
+        """Expose per-parameter views of the flat state as regular optimizer state (checkpoint layout =
+        torch's).  ``load``: tensors already in ``self.state`` (a loaded checkpoint) are copied into the
+        flat buffers first.  ``old``: the state of the FlatGroup this one replaced (DDP re-bucketing):
+        every parameter's slice is carried over to its new offset."""
+        fg = st["fg"]
+        names = list(self._state_names) + (["master_param"] if st["master"] is not fg.param_buffer else [])
+        bufs = {n: st[n] for n in self._state_names}
+        bufs["master_param"] = st["master"]
+        ofg = old["fg"] if old is not None else None
+        for p, off in zip(fg.params, fg.offsets):
+            s = self.state[p]
+            n = p.numel()
+            for name in names:
+                view = bufs[name][off: off + n].view_as(p)
+                if old is not None and name in old and name != "master_param":
+                    o = ofg.offsets[ofg.index[id(p)]]
+                    view.copy_(old[name][o: o + n].view_as(p))
+                elif old is not None and name == "master_param" and old["master"] is not ofg.param_buffer:
+                    o = ofg.offsets[ofg.index[id(p)]]
+                    view.copy_(old["master"][o: o + n].view_as(p))
+                elif load and name in s and s[name].data_ptr() != view.data_ptr():
+                    view.copy_(s[name].reshape(p.shape).to(view.dtype))
+                s[name] = view
+            if load and "step" in s:
+                st["step"] = int(float(s["step"]))
+        if old is not None:
+            st["step"] = old["step"]
+
     def _flat_for(self, gi: int, group) -> Optional[dict]:
         params = [p for p in group["params"]]
         if not params or not params[0].is_cuda:
@@ -61,6 +102,7 @@ class _FusedBase(torch.optim.Optimizer):
             return None
         st = self._flat.get(gi)
         if st is None or st["fg"] is not fg:
+            old = st if st is not None and getattr(st["fg"], "_pda_replaced_by", None) is fg else None
             # low-precision parameters always get an fp32 master; fp32 ones only on request
             need_master = fg.dtype != torch.float32 or bool(self.master_weights)
             master = fg.param_buffer.float().clone() if need_master else fg.param_buffer
@@ -69,13 +111,10 @@ class _FusedBase(torch.optim.Optimizer):
             for name in self._state_names:
                 st[name] = torch.zeros(fg.numel, dtype=torch.float32, device=fg.device)
             self._flat[gi] = st
-            # expose per-parameter views as regular optimizer state (checkpoint layout = torch's)
-            for p, off in zip(fg.params, fg.offsets):
-                s = self.state[p]
-                for name in self._state_names:
-                    s[name] = st[name][off: off + p.numel()].view_as(p)
-                if need_master:
-                    s["master_param"] = master[off: off + p.numel()].view_as(p)
+            # a checkpoint loaded before the first step left per-parameter tensors in self.state
+            loaded = old is None and any(name in self.state.get(p, {}) for p in fg.params
+                                         for name in self._state_names)
+            self._link(st, load=loaded, old=old)
         return st
 
     def zero_grad(self, set_to_none: bool = True):

@@ -72,6 +72,7 @@ class DistributedDataParallel(tnn.Module):
         self.rank = pdist.get_rank(process_group)
         self.backend = pdist.backend() if dist.is_initialized() else None
         self.require_backward_grad_sync = True
+        self.rebuilt = False
         bucket_cap_mb = bucket_cap_mb if bucket_cap_mb is not None else _mb("PDA_BUCKET_MB", 32)
         first_bucket_mb = first_bucket_mb if first_bucket_mb is not None else _mb("PDA_FIRST_BUCKET_MB", 2)
         self.track_comm = bool(os.environ.get("PDA_METRICS_DIR")) or os.environ.get("PDA_TRACK_COMM") == "1"
@@ -85,28 +86,19 @@ class DistributedDataParallel(tnn.Module):
 
         params = [p for p in module.parameters() if p.requires_grad]
         self._params = params
-        # ---- native bucket assignment
-        C = _native.C()
-        self.reducer = C.BucketReducer([p.numel() for p in params], [p.element_size() for p in params],
-                                       [_DTYPE_IDS.get(p.dtype, 9) for p in params], int(bucket_cap_mb * 2 ** 20),
-                                       int(first_bucket_mb * 2 ** 20), 8, [])
-        nb = self.reducer.num_buckets
-        # ---- flat storage in bucket order, one group per dtype
-        by_dtype: Dict[int, list] = {}
-        for b in range(nb):
-            by_dtype.setdefault(self.reducer.bucket_dtype(b), []).append(b)
+        self._bucket_caps = (int(bucket_cap_mb * 2 ** 20), int(first_bucket_mb * 2 ** 20))
+        # bucket order: reverse registration until the first backward has shown the real gradient order,
+        # then (PDA_DDP_REBUILD=1, default) the buckets are rebuilt once in that order (torch's Reducer
+        # semantics behind `ddp_gpus.py:35`), so no bucket waits on a late gradient of an earlier layer
+        self._rebuild_pending = os.environ.get("PDA_DDP_REBUILD", "1") == "1" and not static_graph
+        # ---- native bucket assignment + flat storage in bucket order, one group per dtype
         self.groups: Dict[int, FlatGroup] = {}
-        self.bucket_slices: List[tuple] = [None] * nb  # (group, start, numel)
-        for dt, blist in by_dtype.items():
-            gparams, goffs, start = [], [], 0
-            for b in blist:
-                for pi, off in zip(self.reducer.bucket_params(b), self.reducer.bucket_offsets(b)):
-                    gparams.append(params[pi])
-                    goffs.append(start + off)
-                self.bucket_slices[b] = (dt, start, self.reducer.bucket_numel(b))
-                start += self.reducer.bucket_numel(b)
-            self.groups[dt] = FlatGroup(gparams, goffs, start)
+        self._layout([])
         self._param_index = {id(p): i for i, p in enumerate(params)}
+        # PDA_GRAD_REDUCE_DTYPE=fp32: low-precision buckets are summed in fp32 (upcast on the comm stream,
+        # fp32 ring, one rounding back) instead of accumulating bf16 partial sums over N ranks
+        self.reduce_fp32 = os.environ.get("PDA_GRAD_REDUCE_DTYPE", "") in ("fp32", "float32")
+        self._f32: Dict[int, torch.Tensor] = {}
         # ---- rank-0 state broadcast (X04) as one collective per flat buffer
         self._buffer_flats = flatten_buffers(module)
         if self._comm:
@@ -123,6 +115,14 @@ class DistributedDataParallel(tnn.Module):
         self._callback_task = -1
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
         self.reducer.prepare()
+        # ---- native RCCL communicator for the bucket all-reduces (comm.py; PDA_COMM=c10d: ProcessGroupNCCL)
+        self._ncomm = None
+        on_gpu0 = bool(params) and all(p.is_cuda for p in params)
+        if self._comm and self.backend == "nccl" and on_gpu0:
+            from .. import comm as _comm
+
+            if _comm.enabled():
+                self._ncomm = _comm.for_group(process_group, params[0].device)
         # ---- optional IPC all-reduce over xGMI for buckets (PDA_ALLREDUCE=ipc|oneshot|twoshot, single node)
         self.xgmi = None
         on_gpu = bool(params) and all(p.is_cuda for p in params)
@@ -135,6 +135,88 @@ class DistributedDataParallel(tnn.Module):
                 self.xgmi = _xgmi.XgmiAllReduce(capacity_mb=cap / 2 ** 20 + 1)
                 self._xgmi_algo = _xgmi.requested_algo()
                 self._ipc_stream = torch.cuda.Stream(self.xgmi.device)
+
+    # ------------------------------------------------------------------ bucket layout
+    def _layout(self, order: List[int]):
+        """(Re)assign buckets in ``order`` (param indices in gradient-arrival order; [] = reverse
+        registration) and lay the flat parameter / gradient buffers out in bucket order.  A re-layout
+        moves parameter data and current gradients to the new buffers; the old groups point at their
+        replacements (the fused optimizer carries its state over, optim/fused.py:_link)."""
+        params = self._params
+        C = _native.C()
+        reducer = C.BucketReducer([p.numel() for p in params], [p.element_size() for p in params],
+                                  [_DTYPE_IDS.get(p.dtype, 9) for p in params], self._bucket_caps[0],
+                                  self._bucket_caps[1], 8, list(order))
+        nb = reducer.num_buckets
+        by_dtype: Dict[int, list] = {}
+        for b in range(nb):
+            by_dtype.setdefault(reducer.bucket_dtype(b), []).append(b)
+        old_groups = self.groups
+        old_grads = {}
+        for g in old_groups.values():
+            for i, p in enumerate(g.params):
+                old_grads[id(p)] = g.grad_view(i)
+        groups: Dict[int, FlatGroup] = {}
+        slices: List[tuple] = [None] * nb  # (group, start, numel)
+        for dt, blist in by_dtype.items():
+            gparams, goffs, start = [], [], 0
+            for b in blist:
+                for pi, off in zip(reducer.bucket_params(b), reducer.bucket_offsets(b)):
+                    gparams.append(params[pi])
+                    goffs.append(start + off)
+                slices[b] = (dt, start, reducer.bucket_numel(b))
+                start += reducer.bucket_numel(b)
+            groups[dt] = FlatGroup(gparams, goffs, start)
+            if old_groups:
+                for j, p in enumerate(gparams):
+                    groups[dt].grad_view(j).copy_(old_grads[id(p)])
+        for dt, g in old_groups.items():
+            g._pda_replaced_by = groups.get(dt)
+        self.reducer, self.groups, self.bucket_slices = reducer, groups, slices
+        self._f32 = {}
+
+    def _maybe_rebuild(self):
+        """After the first complete backward: rebuild the buckets in the observed gradient order (rank
+        0's order, so every rank issues the same collectives)."""
+        self._rebuild_pending = False
+        order = list(self.reducer.ready_order())
+        if len(order) != len(self._params):
+            return
+        if self.world > 1 and dist.is_initialized():
+            dev = self._params[0].device if self.backend == "nccl" else torch.device("cpu")
+            t = torch.tensor(order, dtype=torch.int64, device=dev)
+            dist.broadcast(t, 0, group=self.process_group)
+            order = t.tolist()
+        current = [pi for b in range(self.reducer.num_buckets) for pi in self.reducer.bucket_params(b)]
+        if order == current:
+            return
+        # same buckets (as parameter sets, in the same launch order) -> nothing to gain
+        probe = _native.C().BucketReducer([p.numel() for p in self._params], [p.element_size() for p in self._params],
+                                          [_DTYPE_IDS.get(p.dtype, 9) for p in self._params], self._bucket_caps[0],
+                                          self._bucket_caps[1], 8, order)
+        same = probe.num_buckets == self.reducer.num_buckets and all(
+            sorted(probe.bucket_params(b)) == sorted(self.reducer.bucket_params(b)) for b in range(probe.num_buckets))
+        if same:
+            return
+        if self._params[0].is_cuda:
+            _streams.join(self._params[0].device)
+        with torch.no_grad():
+            self._layout(order)
+        self.rebuilt = True
+        if self.xgmi is not None:
+            from . import xgmi as _xgmi
+
+            cap = max(b[2] for b in self.bucket_info())
+            if cap > self.xgmi.capacity:
+                self.xgmi = _xgmi.XgmiAllReduce(capacity_mb=cap / 2 ** 20 + 1)
+
+    def _f32_view(self, b: int) -> torch.Tensor:
+        dt, start, n = self.bucket_slices[b]
+        buf = self._f32.get(dt)
+        if buf is None:
+            buf = self._f32[dt] = torch.empty(self.groups[dt].numel, dtype=torch.float32,
+                                              device=self.groups[dt].device)
+        return buf[start: start + n]
 
     # ------------------------------------------------------------------ communication
     def _use_ring(self):
@@ -181,8 +263,25 @@ class DistributedDataParallel(tnn.Module):
             self._tickets.append((ticket, work))
             return
         ticket = _watchdog.arm(f"ddp all_reduce bucket {b} ({nbytes / 2**20:.1f} MB, {t.dtype})")
+        up = self.reduce_fp32 and t.dtype != torch.float32
         with _timing.range(f"ddp.all_reduce.b{b}"):
-            if self.backend == "nccl":
+            if self._ncomm is not None:
+                c = self._ncomm
+                if up:
+                    # upcast, fp32 all-reduce and the rounding back, all on the comm stream
+                    red = self._f32_view(b)
+                    c._after(producers)
+                    with torch.cuda.stream(c.stream):
+                        red.copy_(t)
+                        c.all_reduce(red, "avg", streams=[])
+                        t.copy_(red)
+                        done = torch.cuda.Event()
+                        done.record(c.stream)
+                    work = _EventWork(done)
+                else:
+                    work = c.all_reduce(t, "avg", streams=producers)
+                self._works.append((work, None))
+            elif self.backend == "nccl":
                 # RCCL orders its stream after the CURRENT stream: make that the side stream, itself
                 # ordered after the main stream, when weight gradients are still being produced there
                 side = producers[1] if len(producers) > 1 else None
@@ -196,8 +295,14 @@ class DistributedDataParallel(tnn.Module):
             else:
                 if len(producers) > 1:  # gloo reads the tensor after the current stream only
                     producers[0].wait_stream(producers[1])
-                work = dist.all_reduce(t, group=self.process_group, async_op=True)
-                self._works.append((work, t))
+                if up:
+                    red = self._f32_view(b)
+                    red.copy_(t)
+                    work = dist.all_reduce(red, group=self.process_group, async_op=True)
+                    self._works.append((work, (t, red)))
+                else:
+                    work = dist.all_reduce(t, group=self.process_group, async_op=True)
+                    self._works.append((work, t))
         self._tickets.append((ticket, work))
 
     def _sweep_tickets(self, force: bool = False):
@@ -264,7 +369,10 @@ class DistributedDataParallel(tnn.Module):
             ev[0].record()
         for work, t in self._works:
             work.wait()
-            if t is not None:
+            if isinstance(t, tuple):  # fp32 reduction of a low-precision bucket (gloo)
+                t[1].div_(self.world)
+                t[0].copy_(t[1])
+            elif t is not None:
                 t.div_(self.world)
         if ev is not None:
             ev[1].record()
@@ -275,6 +383,9 @@ class DistributedDataParallel(tnn.Module):
         self._check_xgmi()
         for g in self.groups.values():
             g.pending_comm = 0
+        if self._rebuild_pending and self.require_backward_grad_sync and self.reducer.all_launched():
+            self._maybe_rebuild()
+        for g in self.groups.values():
             g.attach_grads()
         self.reducer.prepare()
 

@@ -7,8 +7,9 @@ raw lines 325-349, ``PipelineParallelResNet50`` raw lines 538-561, ``device_map=
   layer3+layer4+avgpool+fc on device 1.
 * :class:`PipelineParallelResNet50` — the reference's ``split_size`` micro-batch pipeline, but with
   explicit concurrency instead of "the CPU happens to run ahead": every stage runs on its own device
-  stream, each boundary copy is ordered by events, and the outputs land in preallocated slices of one
-  output tensor (no ``torch.cat``).
+  stream, each boundary copy is ordered by events, and each micro-batch's logits are written into its
+  slice of one preallocated output tensor as soon as that micro-batch finishes (an autograd-recorded
+  slice write on the stage's stream; no ``torch.cat`` of the outputs at the end).
 * :func:`auto_place` — budget-driven placement of a sequential model's children across devices
   (GPU > CPU), the analogue of HF ``device_map="auto"``.
 """
@@ -97,8 +98,14 @@ class PipelineParallelResNet50(ModelParallelResNet50):
             # issued on the capturing stream only: backward through side-stream forwards breaks
             # hipStreamEndCapture on this ROCm stack (tools/graph_stream_repro.py, mode C), and the
             # replayed graph has no launch gaps to hide anyway.
-            outs = [self.head(self.seq2(self.seq1(s.to(self.dev0)).to(self.dev1))) for s in splits]
-            return torch.cat(outs)
+            out = None
+            lo = 0
+            for s in splits:
+                o = self.head(self.seq2(self.seq1(s.to(self.dev0)).to(self.dev1)))
+                out = self._out(out, x.shape[0], o)
+                out[lo: lo + o.shape[0]] = o
+                lo += o.shape[0]
+            return out
         # stage-0 work of micro-batch i overlaps stage-1 work of micro-batch i-1: the two devices
         # run independent streams, joined only by the activation hand-off event of each split.
         cur0, cur1 = torch.cuda.current_stream(self.dev0), torch.cuda.current_stream(self.dev1)
@@ -111,18 +118,32 @@ class PipelineParallelResNet50(ModelParallelResNet50):
                 ev = torch.cuda.Event()
                 ev.record(s0)
                 handoff.append((a, ev))
-        outs = []
+        out = None
+        lo = 0
         with torch.cuda.stream(s1):
             for a, ev in handoff:
                 s1.wait_event(ev)
                 a.record_stream(s1)  # produced on s0, read on s1: keep the allocator from recycling it early
                 a1 = a.to(self.dev1, non_blocking=True)
                 o = self.head(self.seq2(a1))
-                o.record_stream(cur1)
-                outs.append(o)
+                if out is None:  # allocated on the stream that consumes it after the join below
+                    with torch.cuda.stream(cur1):
+                        out = self._out(None, x.shape[0], o)
+                    out.record_stream(s1)
+                # this micro-batch's logits go straight into their slice of the output (autograd records
+                # the slice write; its backward hands each micro-batch a view of its gradient rows)
+                out[lo: lo + o.shape[0]] = o
+                lo += o.shape[0]
         cur0.wait_stream(s0)
         cur1.wait_stream(s1)
-        return torch.cat(outs)
+        return out
+
+    @staticmethod
+    def _out(out, rows, o):
+        """The preallocated [rows, classes] output (no ``torch.cat`` of micro-batch outputs)."""
+        if out is None:
+            out = torch.empty((rows,) + tuple(o.shape[1:]), device=o.device, dtype=o.dtype)
+        return out
 
 
 def auto_place(model: tnn.Module, max_memory: Optional[Dict] = None, devices: Optional[Sequence] = None,

@@ -1,0 +1,15 @@
+#!/bin/bash
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {
+  local name=$1 t=$2; shift 2
+  timeout -k 10 "$t" "$@" > gpurun_out/$name.log 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; grep -v amdgpu gpurun_out/$name.log | tail -3 | cut -c1-600
+  if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
+}
+step tests 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_models_gpu.py -k "tied or side_stream or rccl" 
+step bench1 200 python bench.py --steps 20 --warmup 5
+step bench1_nocomm 200 env PDA_DDP_FORCE_COMM=0 python bench.py --steps 20 --warmup 5
+step bench2_gloo 300 env PDA_DIST_BACKEND=gloo python bench.py --gpus 2 --steps 5 --warmup 2 --batch 128

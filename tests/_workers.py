@@ -437,7 +437,7 @@ def xgmi_collectives_worker(rank, world, outdir):
     pd.destroy_process_group()
 
 
-def ddp_rccl_world1_worker(rank, world, outdir):
+def ddp_rccl_world1_worker(rank, world, outdir, mode="native"):
     """A ONE-rank RCCL group (the only RCCL group a one-GPU box can form) with PDA_DDP_FORCE_COMM=1:
     every bucket goes through the nccl branch of DDP — high-priority RCCL streams, AVG all-reduces
     ordered after the main AND the weight-gradient side stream, watchdog tickets, buffer broadcasts —
@@ -450,6 +450,9 @@ def ddp_rccl_world1_worker(rank, world, outdir):
 
     os.environ["PDA_DDP_FORCE_COMM"] = "1"
     os.environ["PDA_TRACK_COMM"] = "1"
+    os.environ["PDA_COMM"] = "c10d" if mode == "c10d" else "native"
+    if mode == "native_fp32":
+        os.environ["PDA_GRAD_REDUCE_DTYPE"] = "fp32"
     torch.cuda.set_device(0)
     pd.init_process_group("nccl", device_id=0)
     torch.manual_seed(3)
@@ -459,9 +462,12 @@ def ddp_rccl_world1_worker(rank, world, outdir):
     local.load_state_dict(base.state_dict())
     opt = SGD(model.parameters(), lr=0.05, momentum=0.9)
     lopt = SGD(local.parameters(), lr=0.05, momentum=0.9)
+    assert (model._ncomm is not None) == (mode != "c10d"), mode
     g = torch.Generator().manual_seed(11)
     worst = (0.0, "")
+    nbs = []
     for _ in range(3):
+        nbs.append(model.reducer.num_buckets)
         x = torch.randn(8, 64, 64, 3, generator=g).to("cuda", torch.bfloat16)
         y = torch.randint(0, 1000, (8,), generator=g).to("cuda")
         opt.zero_grad(set_to_none=True)
@@ -474,11 +480,11 @@ def ddp_rccl_world1_worker(rank, world, outdir):
         opt.step()
         lopt.step()
     stats = model.comm_stats()
-    assert stats["comm_calls"] == 3 * model.reducer.num_buckets and model.reducer.num_buckets > 3, stats
+    assert stats["comm_calls"] == sum(nbs) and model.reducer.num_buckets > 3, (stats, nbs)
     assert "exposed_comm_ms" in stats, stats
     assert worst[0] < 3e-2, worst
     with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
-        f.write(f"ok {worst[0]:.3e} buckets={model.reducer.num_buckets} exposed_ms={stats['exposed_comm_ms']:.3f}")
+        f.write(f"ok {worst[0]:.3e} buckets={nbs} rebuilt={model.rebuilt} exposed_ms={stats['exposed_comm_ms']:.3f}")
     pd.destroy_process_group()
 
 
@@ -806,4 +812,115 @@ def moe_ep_gpu_worker(rank, world, outdir):
     assert torch.isfinite(moe.w13.grad.float()).all()
     with open(os.path.join(outdir, f"ok{rank}"), "w") as fh:
         fh.write("ok")
+    pd.destroy_process_group()
+
+
+class _Swapped(torch.nn.Module):
+    """Registers `a` before `b` but runs b -> a, so the gradient order (a first) differs from reverse
+    registration (b first): DDP must rebuild its buckets after the first backward."""
+
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(32, 10)
+        self.b = torch.nn.Linear(16, 32)
+        self.c = torch.nn.Linear(16, 16)
+
+    def forward(self, x):
+        return self.a(torch.relu(self.b(torch.relu(self.c(x)))))
+
+
+def ddp_rebuild_worker(rank, world, outdir, steps=3):
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+
+    pd.init_process_group("gloo")
+    torch.manual_seed(5)
+    model = _Swapped()
+    ddp = DistributedDataParallel(model, bucket_cap_mb=0.0015, first_bucket_mb=0.0005)
+    before = [list(ddp.reducer.bucket_params(b)) for b in range(ddp.reducer.num_buckets)]
+    opt = torch.optim.SGD(ddp.parameters(), lr=0.1)
+    g = torch.Generator().manual_seed(9)
+    X = torch.randn(steps, world * 4, 16, generator=g)
+    Y = torch.randint(0, 10, (steps, world * 4), generator=g)
+    grads = []
+    for s in range(steps):
+        opt.zero_grad()
+        F.cross_entropy(ddp(X[s, rank * 4:(rank + 1) * 4]), Y[s, rank * 4:(rank + 1) * 4]).backward()
+        grads.append({n: p.grad.clone() for n, p in model.named_parameters()})
+        opt.step()
+    after = [list(ddp.reducer.bucket_params(b)) for b in range(ddp.reducer.num_buckets)]
+    torch.save({"before": before, "after": after, "rebuilt": ddp.rebuilt, "grads": grads,
+                "state": {k: v.clone() for k, v in model.state_dict().items()}},
+               os.path.join(outdir, f"{rank}.pt"))
+    pd.destroy_process_group()
+
+
+def ddp_fp32_reduce_worker(rank, world, outdir):
+    """bf16 parameters with PDA_GRAD_REDUCE_DTYPE=fp32: the bucket is summed in fp32 and rounded once."""
+    os.environ["PDA_GRAD_REDUCE_DTYPE"] = "fp32"
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+
+    pd.init_process_group("gloo")
+    torch.manual_seed(5)
+    model = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 10)).to(torch.bfloat16)
+    ref = copy_module(model)
+    ddp = DistributedDataParallel(model, bucket_cap_mb=0.001, first_bucket_mb=0.0005)
+    assert ddp.reduce_fp32
+    g = torch.Generator().manual_seed(11)
+    X = torch.randn(world * 4, 16, generator=g).to(torch.bfloat16)
+    Y = torch.randint(0, 10, (world * 4,), generator=g)
+    F.cross_entropy(ddp(X[rank * 4:(rank + 1) * 4]).float(), Y[rank * 4:(rank + 1) * 4]).backward()
+    # every rank's local bf16 gradients, from the same weights (no DDP)
+    local = []
+    for r in range(world):
+        m = copy_module(ref)
+        F.cross_entropy(m(X[r * 4:(r + 1) * 4]).float(), Y[r * 4:(r + 1) * 4]).backward()
+        local.append({n: p.grad.clone() for n, p in m.named_parameters()})
+    out = {n: p.grad.clone() for n, p in model.named_parameters()}
+    torch.save({"ddp": out, "local": local}, os.path.join(outdir, f"{rank}.pt"))
+    pd.destroy_process_group()
+
+
+def copy_module(m):
+    import copy
+
+    return copy.deepcopy(m)
+
+
+def rccl_comm_world1_worker(rank, world, outdir):
+    """The native communicator (comm.py) on a one-rank RCCL group: every collective's result and its
+    ordering after the producing stream (a kernel still running when the collective is enqueued)."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd import comm
+
+    torch.cuda.set_device(0)
+    pd.init_process_group("nccl", device_id=0)
+    c = comm.for_group(None, torch.device("cuda", 0))
+    assert comm.for_group(None, torch.device("cuda", 0)) is c and c.size == 1 and c.rank == 0
+    a = torch.randn(1 << 22, device="cuda")
+    t = a * 3.0  # produced on the current stream, consumed on the comm stream
+    w = c.all_reduce(t, "sum")
+    w.wait()
+    assert torch.equal(t, a * 3.0)
+    tb = (a * 2).to(torch.bfloat16)
+    c.all_reduce(tb, "avg").wait()
+    assert torch.equal(tb, (a * 2).to(torch.bfloat16))
+    out = torch.empty(1000, device="cuda")
+    c.all_gather(out, a[:1000]).wait()
+    assert torch.equal(out, a[:1000])
+    rs = torch.empty(1000, device="cuda")
+    c.reduce_scatter(rs, a[:1000] * 2, "max").wait()
+    assert torch.equal(rs, a[:1000] * 2)
+    b = torch.arange(16, device="cuda", dtype=torch.int64)
+    c.broadcast(b, 0).wait()
+    assert torch.equal(b, torch.arange(16, device="cuda"))
+    s_, r_ = torch.randn(4096, device="cuda"), torch.empty(4096, device="cuda")
+    c.send_recv([(s_, 0)], [(r_, 0)]).wait()
+    assert torch.equal(s_, r_)
+    w = c.all_reduce(t, "sum")
+    w.synchronize()
+    assert w.is_completed() and c.async_error() == ""
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+        f.write("ok")
     pd.destroy_process_group()

@@ -230,3 +230,43 @@ def test_bench_rank_failure_fails_the_launch():
     """One rank failing makes the self-launched run exit non-zero (the group is torn down)."""
     r = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--image", "-3"], timeout=120)
     assert r.returncode != 0
+
+
+def test_ddp_rebuilds_buckets_in_gradient_order(tmp_path):
+    """A model whose gradients arrive in a different order than reverse registration: after the first
+    backward DDP rebuilds its buckets in the observed order (torch Reducer semantics behind
+    `ddp_gpus.py:35`), and training still matches single-process full-batch SGD."""
+    world, steps = 2, 3
+    spawn(_workers.ddp_rebuild_worker, args=(world, str(tmp_path), steps), nprocs=world, timeout=120)
+    d0 = torch.load(tmp_path / "0.pt", weights_only=True)
+    d1 = torch.load(tmp_path / "1.pt", weights_only=True)
+    assert d0["rebuilt"] and d1["rebuilt"]
+    assert d0["after"] == d1["after"] and d0["before"] != d0["after"]
+    import torch.nn.functional as F
+
+    torch.manual_seed(5)
+    ref = _workers._Swapped()
+    opt = torch.optim.SGD(ref.parameters(), lr=0.1)
+    g = torch.Generator().manual_seed(9)
+    X = torch.randn(steps, world * 4, 16, generator=g)
+    Y = torch.randint(0, 10, (steps, world * 4), generator=g)
+    for s in range(steps):
+        opt.zero_grad()
+        F.cross_entropy(ref(X[s]), Y[s]).backward()
+        for n, p in ref.named_parameters():  # every step's averaged gradient, before and after the rebuild
+            assert torch.allclose(d0["grads"][s][n], p.grad, atol=1e-6), (s, n)
+        opt.step()
+    for k, v in ref.state_dict().items():
+        assert torch.allclose(d0["state"][k], v, atol=1e-5), k
+        assert torch.equal(d0["state"][k], d1["state"][k]), k
+
+
+def test_ddp_fp32_gradient_reduction(tmp_path):
+    """PDA_GRAD_REDUCE_DTYPE=fp32 on bf16 parameters: the averaged gradient is the fp32 mean of the
+    ranks' bf16 gradients rounded once (no bf16 partial sums)."""
+    world = 2
+    spawn(_workers.ddp_fp32_reduce_worker, args=(world, str(tmp_path)), nprocs=world, timeout=120)
+    d = torch.load(tmp_path / "0.pt", weights_only=True)
+    for n, g in d["ddp"].items():
+        want = (sum(loc[n].float() for loc in d["local"]) / world).to(torch.bfloat16)
+        assert torch.equal(g, want), n

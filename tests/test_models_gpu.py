@@ -144,12 +144,25 @@ def test_ddp_resnet50_two_ranks_share_gpu(tmp_path):
         assert (tmp_path / f"ok{r}").read_text().startswith("ok")
 
 
-def test_ddp_rccl_one_rank_group_matches_local(tmp_path):
-    """The RCCL branch of DDP (what the driver's 2/4/8-GPU runs execute) on a one-rank RCCL group."""
+@pytest.mark.parametrize("mode", ["native", "c10d", "native_fp32"])
+def test_ddp_rccl_one_rank_group_matches_local(tmp_path, mode):
+    """The RCCL branch of DDP (what the driver's 2/4/8-GPU runs execute) on a one-rank RCCL group:
+    the native communicator (default), torch's ProcessGroupNCCL (PDA_COMM=c10d), and fp32 reduction of
+    the bf16 buckets (PDA_GRAD_REDUCE_DTYPE=fp32), each matching a plain replica's gradients."""
     import _workers
     from pytorchdistributed_amd.launch import spawn
 
-    spawn(_workers.ddp_rccl_world1_worker, args=(1, str(tmp_path)), nprocs=1, timeout=300)
+    spawn(_workers.ddp_rccl_world1_worker, args=(1, str(tmp_path), mode), nprocs=1, timeout=300)
+    assert (tmp_path / "ok0").read_text().startswith("ok")
+
+
+def test_native_rccl_communicator_one_rank(tmp_path):
+    """csrc/comm/communicator.cpp through comm.py: all-reduce (sum / avg, fp32 / bf16), all-gather,
+    reduce-scatter, broadcast, fused send/recv, work handles, stream ordering."""
+    import _workers
+    from pytorchdistributed_amd.launch import spawn
+
+    spawn(_workers.rccl_comm_world1_worker, args=(1, str(tmp_path)), nprocs=1, timeout=200)
     assert (tmp_path / "ok0").read_text().startswith("ok")
 
 
