@@ -18,12 +18,22 @@ import torch
 from .._native import C
 from ..parallel.flat import grad_target
 
-NSEG = int(os.environ.get("PDA_FP32_SPLIT", "3"))
-if NSEG not in (3, 4):
-    raise ValueError("PDA_FP32_SPLIT must be 3 or 4")
 # segment s of an operand is its lo part when bit s is set: A = (hi, hi, lo[, lo]), B = (hi, lo, hi[, lo])
-MASK_A = {3: 0b100, 4: 0b1100}[NSEG]
-MASK_B = {3: 0b010, 4: 0b1010}[NSEG]
+_MASKS = {3: (0b100, 0b010), 4: (0b1100, 0b1010)}
+NSEG = 3
+MASK_A, MASK_B = _MASKS[3]
+
+
+def set_split(n: int) -> None:
+    """Number of split products per fp32 GEMM: 3 (hi.hi + hi.lo + lo.hi, ~1e-5) or 4 (+ lo.lo, ~1e-7)."""
+    global NSEG, MASK_A, MASK_B
+    if n not in _MASKS:
+        raise ValueError("the fp32 split must be 3 or 4")
+    NSEG = n
+    MASK_A, MASK_B = _MASKS[n]
+
+
+set_split(int(os.environ.get("PDA_FP32_SPLIT", "3")))
 
 
 def _split(t: torch.Tensor, mask: int, stack: bool) -> torch.Tensor:

@@ -21,12 +21,18 @@ root unit holding the remaining parameters):
   into the shard's grad; the next unit's all-gather is prefetched while the current unit computes
   (forward order recorded on the first iteration, reversed for backward).
 
+Collectives run on the native RCCL communicator's stream (comm.py): the all-gathers (prefetch
+included) and the reduce-scatters queue there in issue order; a unit's reduce-scatter never makes the
+compute stream wait — the shard gradients are collected once, in the final backward callback.
+
 Memory per rank for Llama-3 8B: 8.03e9 x (2 B shard + 4 B master + 8 B Adam) / 8 ~= 14 GB, plus the
-persistent full-size gradient buffers (16 GB bf16) and the gathered units in flight: a small fraction
-of the 288 GB HBM, so neither prefetch depth nor ``reshard_after_forward=False`` (no backward
-re-gather) is memory-limited.
-Checkpoints: :meth:`full_state_dict` (rank-0 consolidated, original names) and
-:meth:`sharded_state_dict` / :meth:`load_sharded_state_dict` (``shard_{rank:05d}.pt`` + ``meta.json``).
+gradient buffers of the units whose backward / reduce-scatter is in flight (allocated at the unit's
+backward, released once its reduce-scatter is queued) and the gathered units in flight: a small
+fraction of the 288 GB HBM.
+Checkpoints: :meth:`full_state_dict` (consolidated, original names), :meth:`save_sharded` /
+:meth:`load_sharded` (``shard_{rank:05d}.pt`` with the rank's optimizer state — fp32 master, Adam
+moments, step — + ``meta.json``: an exact resume), :func:`consolidate` (model only) and
+:func:`consolidate_snapshot` (the stock ``{"MODEL_STATE", "OPTIMIZER_STATE"}`` file).
 """
 from __future__ import annotations
 
@@ -98,8 +104,18 @@ class _Unit:
         self.alias = W == 1 and fsdp.shard_dtype == fsdp.param_dtype
         self.flat = self.shard.detach() if self.alias else torch.empty(self.numel, dtype=fsdp.param_dtype,
                                                                        device=self.device)
-        # flat gradient buffer (padding stays zero; every slot is fully rewritten each backward)
+        # flat gradient buffer (every slot is fully rewritten each backward; the alignment padding is
+        # zeroed whenever the storage is (re)allocated).  Transient above world 1: allocated when the
+        # unit's backward starts, released as soon as its reduce-scatter is queued (the comm stream
+        # keeps it alive until the collective has read it), so a rank holds the gradient of the units
+        # in flight, not of the whole model (the root unit's, whose leaves get gradients at both ends
+        # of backward, stays resident)
         self.grad_buffer = torch.zeros(self.numel, dtype=fsdp.param_dtype, device=self.device)
+        covered = torch.zeros(self.numel, dtype=torch.bool)
+        for (_owner, _name, _shape, o, n) in self.entries:
+            covered[o: o + n] = True
+        self.pad_index = (~covered).nonzero().flatten().to(self.device)
+        self.transient_grad = False  # set by the FSDP wrapper for non-root units at world > 1
         self.arrived = 0
         # persistent leaf tensors (plain tensors, not registered Parameters: the optimizer sees only the
         # shard) viewing the gathered buffer; `_pda_flat` routes native backward kernels to the grad slot
@@ -151,6 +167,18 @@ class _Unit:
             self.arrived = len(self.leaves)
             self.fsdp._grad_ready(self)
 
+    def alloc_grad(self):
+        """(Re)allocate a released gradient buffer (zero padding) before the unit's backward writes it."""
+        st = self.grad_buffer.untyped_storage()
+        if st.size() == 0:
+            st.resize_(self.numel * self.grad_buffer.element_size())
+            if self.pad_index.numel():
+                self.grad_buffer.index_fill_(0, self.pad_index, 0)
+
+    def release_grad(self):
+        if self.transient_grad:
+            self.grad_buffer.untyped_storage().resize_(0)
+
     def _send_buffer(self) -> torch.Tensor:
         if self.shard.dtype == self.fsdp.param_dtype:
             return self.shard.detach()
@@ -172,7 +200,9 @@ class _Unit:
             elif self.fsdp.xgmi is not None:
                 flat = self.flat
                 self.pending_ag = self.fsdp._ipc(lambda: self.fsdp.xgmi.all_gather_into_tensor(flat, send),
-                                                 [torch.cuda.current_stream(self.device)], [send])
+                                                 [torch.cuda.current_stream(self.device)], [send, flat])
+            elif self.fsdp.ncomm is not None:
+                self.pending_ag = self.fsdp.ncomm.all_gather(self.flat, send)
             else:
                 self.pending_ag = dist.all_gather_into_tensor(self.flat, send, group=self.fsdp.group,
                                                               async_op=True)
@@ -244,9 +274,21 @@ class FullyShardedDataParallel(tnn.Module):
             if u is not self.root_unit:
                 u.module.register_forward_pre_hook(self._make_pre_fwd(u))
                 u.module.register_forward_hook(self._make_post_fwd(u))
-        self._pending_rs = None
+        self._pending_rs: List[tuple] = []  # (unit, work, out) reduce-scatters queued this backward
         self._callback_queued = False
         self._callback_task = -1
+        # ---- native RCCL communicator for the unit all-gathers / reduce-scatters (comm.py; ordered on
+        # one high-priority comm stream, so a unit's reduce-scatter never makes the compute stream wait:
+        # the shard gradients are collected in the final callback).  PDA_COMM=c10d: ProcessGroupNCCL.
+        self.ncomm = None
+        if self.nccl and all(u.device.type == "cuda" for u in self.units) and self.world > 1:
+            from .. import comm as _comm
+
+            if _comm.enabled():
+                self.ncomm = _comm.for_group(process_group, self.units[0].device)
+        for u in self.units:
+            u.transient_grad = self.world > 1 and u is not self.root_unit
+            u.release_grad()
         # ---- optional direct xGMI collectives (PDA_FSDP_COMM=ipc, one node): the unit all-gathers pull
         # every peer's shard over its own link and the gradient reduce-scatters reduce chunk `rank` of
         # every peer's buffer (csrc/kernels/xgmi.hip), on one ordered side stream; RCCL by default
@@ -314,8 +356,8 @@ class FullyShardedDataParallel(tnn.Module):
         task = torch._C._current_graph_task_id()
         if self._callback_queued and self._callback_task == task:
             return
-        if self._callback_queued:  # aborted pass: drop its partial arrivals / pending reduce-scatter
-            self._pending_rs = None
+        if self._callback_queued:  # aborted pass: drop its partial arrivals / pending reduce-scatters
+            self._pending_rs = []
             _join_side_streams(self.units)
             for u in self.units:
                 u.arrived = 0
@@ -326,6 +368,7 @@ class FullyShardedDataParallel(tnn.Module):
         torch.autograd.Variable._execution_engine.queue_callback(self._post_backward_final)
 
     def _pre_backward(self, u: _Unit, g):
+        u.alloc_grad()
         if not u.gathered:
             u.start_gather()
             u.finish_gather()
@@ -338,7 +381,6 @@ class FullyShardedDataParallel(tnn.Module):
 
     # ------------------------------------------------------------ gradient reduce-scatter
     def _grad_ready(self, u: _Unit):
-        self._finish_rs()
         grad_full = u.grad_buffer
         if self.world == 1:
             # the shard's gradient IS the flat gradient buffer (no copy); the slots were just rewritten,
@@ -346,25 +388,26 @@ class FullyShardedDataParallel(tnn.Module):
             if u.shard.grad is not None and u.shard.grad.data_ptr() == grad_full.data_ptr():
                 raise RuntimeError("FSDP at world size 1 does not accumulate gradients across backward "
                                    "passes: call zero_grad(set_to_none=True) between steps")
-            out, work = grad_full, None
+            self._pending_rs.append((u, None, grad_full))
+            self._queue_final()
+            return
+        out = torch.empty(u.shard_numel, dtype=grad_full.dtype, device=grad_full.device)
+        # weight gradients of this unit may still be running on the side stream (ops/streams.py): the
+        # collective is ordered after both streams
+        producers = _streams.producer_streams(grad_full.device) if grad_full.is_cuda else []
+        if self.xgmi is not None:
+            work = self._ipc(lambda: self.xgmi.reduce_scatter_tensor(out, grad_full, average=True), producers,
+                             [out, grad_full])
+        elif self.ncomm is not None:
+            work = self.ncomm.reduce_scatter(out, grad_full, "avg", streams=producers)
         else:
-            out = torch.empty(u.shard_numel, dtype=grad_full.dtype, device=grad_full.device)
-            # weight gradients of this unit may still be running on the side stream (ops/streams.py):
-            # order the collective after both streams (RCCL waits on the current stream)
-            producers = _streams.producer_streams(grad_full.device) if grad_full.is_cuda else []
             ctx = contextlib.nullcontext()
-            if self.xgmi is not None:
-                self._pending_rs = (u, self._ipc(lambda: self.xgmi.reduce_scatter_tensor(out, grad_full, average=True),
-                                                 producers, [out]), out)
-                if u is not self.root_unit:
-                    u.reshard()
-                self._queue_final()
-                return
             if len(producers) > 1:
-                if self.nccl:
+                if self.nccl:  # RCCL waits on the current stream: make it the side stream, after main
                     producers[1].wait_stream(producers[0])
                     ctx = torch.cuda.stream(producers[1])
                     out.record_stream(producers[1])
+                    grad_full.record_stream(producers[1])
                 else:
                     producers[0].wait_stream(producers[1])
             with ctx:
@@ -373,25 +416,26 @@ class FullyShardedDataParallel(tnn.Module):
                                                       async_op=True)
                 else:
                     work = dist.reduce_scatter_tensor(out, grad_full, group=self.group, async_op=True)
-        self._pending_rs = (u, work, out)
+        self._pending_rs.append((u, work, out))
+        u.release_grad()  # the collective's stream holds the storage until it has read it
         if u is not self.root_unit:
             u.reshard()
         self._queue_final()
 
     def _finish_rs(self):
-        if self._pending_rs is None:
-            return
-        u, work, out = self._pending_rs
-        self._pending_rs = None
-        if work is not None:
-            work.wait()
-        if not self.nccl and self.xgmi is None and self.world > 1:
-            out.div_(self.world)
-        g = out if out.dtype == u.shard.dtype else out.to(u.shard.dtype)
-        if u.shard.grad is None:
-            u.shard.grad = g
-        else:
-            u.shard.grad.add_(g)
+        """Collect every queued reduce-scatter into its shard's gradient (the compute stream waits on
+        the collectives here, once, at the end of backward)."""
+        pending, self._pending_rs = self._pending_rs, []
+        for u, work, out in pending:
+            if work is not None:
+                work.wait()
+            if not self.nccl and self.xgmi is None and self.world > 1:
+                out.div_(self.world)
+            g = out if out.dtype == u.shard.dtype else out.to(u.shard.dtype)
+            if u.shard.grad is None:
+                u.shard.grad = g
+            else:
+                u.shard.grad.add_(g)
 
     def _post_backward_final(self):
         self._callback_queued = False
@@ -434,25 +478,60 @@ class FullyShardedDataParallel(tnn.Module):
                 out[full_name] = full[o: o + n].view(shape).clone().cpu()
         return out
 
-    def sharded_state_dict(self) -> Dict[str, torch.Tensor]:
-        return {f"unit{u.index}": u.shard.detach().cpu() for u in self.units}
+    def sharded_state_dict(self, optimizer=None) -> Dict[str, object]:
+        """This rank's shards and, with ``optimizer``, its state for them (fp32 master, Adam moments,
+        step) and the param-group hyperparameters: everything a bit-exact resume needs."""
+        sd: Dict[str, object] = {f"unit{u.index}": u.shard.detach().cpu() for u in self.units}
+        if optimizer is not None:
+            ost = {}
+            for u in self.units:
+                st = optimizer.state.get(u.shard, {})
+                ost[f"unit{u.index}"] = {k: (v.detach().cpu().clone() if torch.is_tensor(v) else torch.tensor(v))
+                                         for k, v in st.items()}
+            sd["optim"] = ost
+            sd["param_groups"] = [{k: v for k, v in g.items() if k != "params"} for g in optimizer.param_groups]
+        return sd
 
-    def save_sharded(self, directory: str):
+    def save_sharded(self, directory: str, optimizer=None):
+        """``shard_{rank:05d}.pt`` per rank (+ optimizer state) and ``meta.json`` (layout of units and of
+        the optimizer state) from rank 0."""
         os.makedirs(directory, exist_ok=True)
-        torch.save(self.sharded_state_dict(), os.path.join(directory, f"shard_{self.rank:05d}.pt"))
+        sd = self.sharded_state_dict(optimizer)
+        tmp = os.path.join(directory, f"shard_{self.rank:05d}.pt.tmp")
+        torch.save(sd, tmp)
+        os.replace(tmp, os.path.join(directory, f"shard_{self.rank:05d}.pt"))
         if self.rank == 0:
             meta = {"world_size": self.world, "units": [
                 {"numel": u.numel, "shard_numel": u.shard_numel,
                  "params": [{"name": nm, "shape": list(e[2]), "offset": e[3], "numel": e[4]}
                             for e, nm in zip(u.entries, names)]} for u, names in zip(self.units, self.names)]}
+            if optimizer is not None:
+                st0 = sd["optim"]["unit0"]
+                meta["optimizer"] = {
+                    "type": type(optimizer).__name__,
+                    "state": {k: {"dtype": str(v.dtype).replace("torch.", ""), "per_element": v.dim() > 0}
+                              for k, v in st0.items()},
+                    "param_groups": [{k: v for k, v in g.items() if isinstance(v, (int, float, bool, str, list, tuple))}
+                                     for g in sd["param_groups"]]}
             with open(os.path.join(directory, "meta.json"), "w") as f:
                 json.dump(meta, f, indent=1)
 
     @torch.no_grad()
-    def load_sharded(self, directory: str):
+    def load_sharded(self, directory: str, optimizer=None):
         sd = torch.load(os.path.join(directory, f"shard_{self.rank:05d}.pt"), map_location="cpu", weights_only=True)
         for u in self.units:
             u.shard.copy_(sd[f"unit{u.index}"])
+            u._cast = None
+        if optimizer is not None and "optim" in sd:
+            for u in self.units:
+                st = optimizer.state[u.shard]
+                for k, v in sd["optim"][f"unit{u.index}"].items():
+                    if k == "step" and v.dim() == 0:
+                        st[k] = int(v.item()) if v.dtype in (torch.int64, torch.int32) else float(v.item())
+                    else:
+                        st[k] = v.to(u.shard.device)
+            for g, saved in zip(optimizer.param_groups, sd.get("param_groups", [])):
+                g.update(saved)
 
 
 def consolidate(directory: str) -> Dict[str, torch.Tensor]:
@@ -467,6 +546,40 @@ def consolidate(directory: str) -> Dict[str, torch.Tensor]:
         for p in u["params"]:
             out[p["name"]] = full[p["offset"]: p["offset"] + p["numel"]].view(p["shape"]).clone()
     return out
+
+
+def consolidate_snapshot(directory: str, path: Optional[str] = None) -> Dict[str, object]:
+    """Offline: merge a sharded checkpoint saved WITH its optimizer into the framework's single-file
+    snapshot layout ``{"MODEL_STATE", "OPTIMIZER_STATE", "EPOCHS_RUN"}`` (utils/checkpoint.py), the
+    optimizer state in torch's format (parameter index = order of ``MODEL_STATE``; per-element state
+    such as ``exp_avg`` / ``master_param`` un-sharded to each parameter's shape).  Written to ``path``
+    when given."""
+    meta = json.load(open(os.path.join(directory, "meta.json")))
+    W = meta["world_size"]
+    shards = [torch.load(os.path.join(directory, f"shard_{r:05d}.pt"), map_location="cpu", weights_only=True)
+              for r in range(W)]
+    model, ostate, pi = {}, {}, 0
+    for i, u in enumerate(meta["units"]):
+        full = torch.cat([s_[f"unit{i}"] for s_ in shards])
+        opt_full = {}
+        if "optim" in shards[0]:
+            for k, v in shards[0]["optim"][f"unit{i}"].items():
+                opt_full[k] = torch.cat([s_["optim"][f"unit{i}"][k] for s_ in shards]) if v.dim() > 0 else v
+        for p in u["params"]:
+            sl = slice(p["offset"], p["offset"] + p["numel"])
+            model[p["name"]] = full[sl].view(p["shape"]).clone()
+            if opt_full:
+                ostate[pi] = {k: (v[sl].view(p["shape"]).clone() if v.dim() > 0 else v) for k, v in opt_full.items()}
+            pi += 1
+    snap: Dict[str, object] = {"MODEL_STATE": model, "EPOCHS_RUN": 0}
+    if ostate:
+        groups = [dict(g) for g in shards[0].get("param_groups", [{}])]
+        for g in groups:
+            g["params"] = list(range(pi))
+        snap["OPTIMIZER_STATE"] = {"state": ostate, "param_groups": groups[:1]}
+    if path is not None:
+        torch.save(snap, path)
+    return snap
 
 
 def _is_child(parent: tnn.Module, m: tnn.Module) -> bool:

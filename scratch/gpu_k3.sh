@@ -9,7 +9,7 @@ step() {
   echo "== $name rc=$rc"; grep -v amdgpu gpurun_out/$name.log | tail -4 | cut -c1-900
   if [ $rc -ne 0 ]; then echo "stopping after $name"; exit $rc; fi
 }
-step tests 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_fp32_gpu.py tests/test_models_gpu.py -k "fp32 or split or batchnorm or pools or tied or side_stream or rccl"
+step tests 700 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_fp32_gpu.py tests/test_models_gpu.py -k "fp32 or split or batchnorm or pools or tied or side_stream or rccl or fsdp"
 step tests_dual 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "dual_bn"
 step bench1 200 python bench.py --steps 20 --warmup 5
 step bench1_c10d 200 env PDA_COMM=c10d python bench.py --steps 20 --warmup 5

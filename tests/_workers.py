@@ -924,3 +924,39 @@ def rccl_comm_world1_worker(rank, world, outdir):
     with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
         f.write("ok")
     pd.destroy_process_group()
+
+
+def fsdp_resume_worker(rank, world, outdir, phase):
+    """phase "full": 6 AdamW steps, losses saved; "first": 3 steps then a sharded checkpoint WITH the
+    optimizer state; "resume": fresh model + optimizer, load the checkpoint, steps 4-6."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.optim import AdamW
+    from pytorchdistributed_amd.parallel.fsdp import FullyShardedDataParallel
+
+    pd.init_process_group("gloo")
+    torch.manual_seed(0)
+    net = _Net()
+    model = FullyShardedDataParallel(net, unit_types=(_Block,))
+    opt = AdamW(model.parameters(), lr=1e-2, weight_decay=0.1)
+    g = torch.Generator().manual_seed(3)
+    batches = []
+    for step in range(6):
+        X = torch.randn(world * 4, 8, generator=g)
+        Y = torch.randint(0, 4, (world * 4,), generator=g)
+        batches.append((X[rank * 4:(rank + 1) * 4], Y[rank * 4:(rank + 1) * 4]))
+    ckpt = os.path.join(outdir, "ckpt")
+    steps = range(6) if phase == "full" else (range(3) if phase == "first" else range(3, 6))
+    if phase == "resume":
+        model.load_sharded(ckpt, opt)
+    losses = []
+    for step in steps:
+        xs, ys = batches[step]
+        opt.zero_grad()
+        loss = F.cross_entropy(model(xs), ys)
+        loss.backward()
+        opt.step()
+        losses.append(loss.detach().clone())
+    if phase == "first":
+        model.save_sharded(ckpt, opt)
+    torch.save({"losses": losses, "state": model.full_state_dict()}, os.path.join(outdir, f"{phase}{rank}.pt"))
+    pd.destroy_process_group()
