@@ -822,20 +822,31 @@ Tensor swiglu_bwd(Tensor dy, Tensor gu) {
   return dgu;
 }
 
-Tensor colsum(Tensor x) {
+// column sums (bias gradients); ``out``: write straight into that tensor (e.g. a bf16 gradient slot),
+// otherwise a new tensor of dtype ``out_bf16 ? bf16 : fp32``
+Tensor colsum(Tensor x, c10::optional<Tensor> out, bool out_bf16) {
   check_f32_or_bf16(x, "x");
   const int64_t cols = x.size(-1), rows = x.numel() / cols;
   c10::DeviceGuard g(x.device());
-  Tensor out = at::empty({cols}, x.options().dtype(at::kFloat));
+  Tensor o;
+  if (out.has_value()) {
+    o = *out;
+    check_f32_or_bf16(o, "out");
+    TORCH_CHECK(o.numel() == cols && o.is_contiguous(), "colsum: out must be [cols] contiguous");
+  } else {
+    o = at::empty({cols}, x.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  }
   if (cols % 8 != 0 || !x.is_contiguous()) {
     Tensor xc = x.contiguous();
-    CHECK_HIP_OK(pda::colsum_unaligned(xc.data_ptr(), is_bf16(x), out.data_ptr<float>(), rows, cols, stream_of(x)));
-    return out;
+    Tensor f = o.scalar_type() == at::kFloat ? o : at::empty({cols}, x.options().dtype(at::kFloat));
+    CHECK_HIP_OK(pda::colsum_unaligned(xc.data_ptr(), is_bf16(x), f.data_ptr<float>(), rows, cols, stream_of(x)));
+    if (!f.is_same(o)) o.copy_(f);
+    return o;
   }
   Tensor ws = at::empty({pda::colreduce_ws_floats(rows, cols, 1)}, x.options().dtype(at::kFloat));
-  CHECK_HIP_OK(pda::colsum(x.data_ptr(), is_bf16(x), out.data_ptr<float>(), rows, cols, ws.data_ptr<float>(),
+  CHECK_HIP_OK(pda::colsum(x.data_ptr(), is_bf16(x), o.data_ptr(), is_bf16(o), rows, cols, ws.data_ptr<float>(),
                            stream_of(x)));
-  return out;
+  return o;
 }
 
 // C[M,N] (+)= A[M,K] B[K,N] with explicit element strides (any alignment / dtype fp32|bf16)
@@ -921,8 +932,11 @@ std::vector<Tensor> add_rownorm_fwd_train(Tensor x, Tensor r, Tensor gamma, c10:
   return {h, y, mean, rstd};
 }
 
+// dgamma / dbeta in the parameter dtype, written into ``dgamma_out`` / ``dbeta_out`` when given (the
+// parameters' gradient slots: no cast kernel, no copy)
 std::vector<Tensor> rownorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, Tensor rstd, bool rms,
-                                c10::optional<Tensor> addend) {
+                                c10::optional<Tensor> addend, c10::optional<Tensor> dgamma_out,
+                                c10::optional<Tensor> dbeta_out) {
   check_f32_or_bf16(dy, "dy");
   check_f32_or_bf16(x, "x");
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type());
@@ -934,13 +948,20 @@ std::vector<Tensor> rownorm_bwd(Tensor dy, Tensor x, Tensor gamma, Tensor mean, 
   const int64_t D = x.size(-1), rows = x.numel() / D;
   c10::DeviceGuard g(x.device());
   Tensor dx = at::empty_like(x);
-  auto fo = x.options().dtype(at::kFloat);
-  Tensor dgamma = at::empty({D}, fo), dbeta = at::empty({D}, fo);
-  Tensor ws = at::empty({pda::colreduce_ws_floats(rows, D, rms ? 1 : 2)}, fo);
+  auto po = x.options().dtype(gamma.scalar_type());
+  auto take = [&](const c10::optional<Tensor>& t, const char* name) {
+    if (!t.has_value()) return at::empty({D}, po);
+    TORCH_CHECK(t->scalar_type() == gamma.scalar_type() && t->numel() == D && t->is_contiguous(), name,
+                ": must be a contiguous [D] tensor of the parameter dtype");
+    return *t;
+  };
+  Tensor dgamma = take(dgamma_out, "dgamma_out");
+  Tensor dbeta = rms ? at::empty({0}, po) : take(dbeta_out, "dbeta_out");
+  Tensor ws = at::empty({pda::colreduce_ws_floats(rows, D, rms ? 1 : 2)}, x.options().dtype(at::kFloat));
   CHECK_HIP_OK(pda::rownorm_bwd(dy.data_ptr(), x.data_ptr(), is_bf16(x), gamma.data_ptr(), is_bf16(gamma),
                                 rms ? nullptr : mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(),
-                                dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), rows, D, rms, ws.data_ptr<float>(),
-                                stream_of(x), addend.has_value() ? addend->data_ptr() : nullptr));
+                                dgamma.data_ptr(), rms ? nullptr : dbeta.data_ptr(), is_bf16(gamma), rows, D, rms,
+                                ws.data_ptr<float>(), stream_of(x), addend.has_value() ? addend->data_ptr() : nullptr));
   return {dx, dgamma, dbeta};
 }
 
@@ -1559,12 +1580,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("relu_bwd", &relu_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);
   m.def("swiglu_bwd", &swiglu_bwd);
-  m.def("colsum", &colsum);
+  m.def("colsum", &colsum, py::arg("x"), py::arg("out") = py::none(), py::arg("out_bf16") = false);
   m.def("simt_gemm", &simt_gemm);
   m.def("rownorm_fwd", &rownorm_fwd);
   m.def("add_rownorm_fwd", &add_rownorm_fwd);
   m.def("rownorm_bwd", &rownorm_bwd, py::arg("dy"), py::arg("x"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
-        py::arg("rms"), py::arg("addend") = py::none());
+        py::arg("rms"), py::arg("addend") = py::none(), py::arg("dgamma_out") = py::none(),
+        py::arg("dbeta_out") = py::none());
   m.def("add_rownorm_fwd_train", &add_rownorm_fwd_train);
   m.def("attn_fwd", &attn_fwd);
   m.def("decode_attn", &decode_attn, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("L"), py::arg("scale"),

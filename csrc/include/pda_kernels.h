@@ -239,10 +239,11 @@ hipError_t add_rownorm_fwd(const bf16_t* x, const bf16_t* r, const bf16_t* gamma
 hipError_t rownorm_fwd(const void* x, bool x_bf16, const void* gamma, const void* beta, bool p_bf16, void* y,
                        float* mean, float* rstd, int64_t rows, int64_t D, float eps, bool rms, hipStream_t st);
 hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* gamma, bool p_bf16, const float* mean,
-                       const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, bool rms,
-                       float* ws, hipStream_t st, const void* addend = nullptr);  // dx += addend (same layout)
+                       const float* rstd, void* dx, void* dgamma, void* dbeta, bool dparam_bf16, int64_t rows,
+                       int64_t D, bool rms, float* ws, hipStream_t st, const void* addend = nullptr);  // dx += addend (same layout)
 // column sums via slab partials (cols % 8 == 0); ws holds colreduce_ws_floats(rows, cols, 1) floats
-hipError_t colsum(const void* x, bool bf16, float* out, int64_t rows, int64_t cols, float* ws, hipStream_t st);
+hipError_t colsum(const void* x, bool bf16, void* out, bool out_bf16, int64_t rows, int64_t cols, float* ws,
+                  hipStream_t st);
 int64_t colreduce_ws_floats(int64_t rows, int64_t D, int nout);
 
 // ---- attention.hip (flash attention fwd / bwd, D in {64, 128}, GQA, causal or not)

@@ -322,10 +322,12 @@ __global__ void __launch_bounds__(kThreads) colstrip_partial_kernel(const T* __r
 // sets the time.  (One thread per column walking ~512 slabs 4 loads deep took ~30 us per call on the
 // GPT-2 bias / LayerNorm gradients.)
 constexpr int kFinCols = 64, kFinLanes = 16;
+// (out_bf16: the outputs are written as bf16 — straight into a bf16 parameter's gradient slot)
 __global__ void __launch_bounds__(kFinCols * kFinLanes) colreduce_finalize_kernel(const float* __restrict__ ws,
                                                                                   int nslab, int64_t D, int nout,
-                                                                                  float* __restrict__ out0,
-                                                                                  float* __restrict__ out1) {
+                                                                                  void* __restrict__ out0,
+                                                                                  void* __restrict__ out1,
+                                                                                  int out_bf16) {
   __shared__ float red[kFinLanes][kFinCols];
   const int cl = threadIdx.x % kFinCols, lane = threadIdx.x / kFinCols;
   const int64_t t = (int64_t)blockIdx.x * kFinCols + cl;  // output index over nout x D
@@ -350,7 +352,9 @@ __global__ void __launch_bounds__(kFinCols * kFinLanes) colreduce_finalize_kerne
   float r = 0.f;
 #pragma unroll
   for (int l = 0; l < kFinLanes; ++l) r += red[l][cl];
-  (k == 0 ? out0 : out1)[col] = r;
+  void* o = k == 0 ? out0 : out1;
+  if (out_bf16) static_cast<bf16_t*>(o)[col] = f2bf(r);
+  else static_cast<float*>(o)[col] = r;
 }
 
 inline unsigned fin_grid(int64_t n) { return (unsigned)((n + kFinCols - 1) / kFinCols); }
@@ -483,11 +487,13 @@ hipError_t rownorm_fwd(const void* x, bool x_bf16, const void* gamma, const void
 }
 
 hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* gamma, bool p_bf16, const float* mean,
-                       const float* rstd, void* dx, float* dgamma, float* dbeta, int64_t rows, int64_t D, bool rms,
-                       float* ws, hipStream_t st, const void* addend) {
+                       const float* rstd, void* dx, void* dgamma, void* dbeta, bool dparam_bf16, int64_t rows,
+                       int64_t D, bool rms, float* ws, hipStream_t st, const void* addend) {
+  const int ob = dparam_bf16 ? 1 : 0;
+  const size_t osz = dparam_bf16 ? 2 : 4;
   if (rows == 0) {
-    PDA_CHECK_HIP(hipMemsetAsync(dgamma, 0, D * sizeof(float), st));
-    if (!rms) PDA_CHECK_HIP(hipMemsetAsync(dbeta, 0, D * sizeof(float), st));
+    PDA_CHECK_HIP(hipMemsetAsync(dgamma, 0, D * osz, st));
+    if (!rms) PDA_CHECK_HIP(hipMemsetAsync(dbeta, 0, D * osz, st));
     return hipSuccess;
   }
   const int nslab = plan_slabs(rows, D);
@@ -515,7 +521,7 @@ hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* g
     });
     PDA_CHECK_HIP(hipGetLastError());
     const int nout = rms ? 1 : 2;
-    colreduce_finalize_kernel<<<fin_grid(D * nout), kFinCols * kFinLanes, 0, st>>>(ws, nslab, D, nout, dgamma, dbeta);
+    colreduce_finalize_kernel<<<fin_grid(D * nout), kFinCols * kFinLanes, 0, st>>>(ws, nslab, D, nout, dgamma, dbeta, ob);
     return hipGetLastError();
   }
   const unsigned grid = (unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock);
@@ -548,13 +554,14 @@ hipError_t rownorm_bwd(const void* dy, const void* x, bool x_bf16, const void* g
 #undef P
   PDA_CHECK_HIP(hipGetLastError());
   const int nout = rms ? 1 : 2;
-  colreduce_finalize_kernel<<<fin_grid(D * nout), kFinCols * kFinLanes, 0, st>>>(ws, nslab, D, nout, dgamma, dbeta);
+  colreduce_finalize_kernel<<<fin_grid(D * nout), kFinCols * kFinLanes, 0, st>>>(ws, nslab, D, nout, dgamma, dbeta, ob);
   return hipGetLastError();
 }
 
-// Column sums of a [rows, cols] matrix (bias gradients): out[c] = sum_r x[r, c] (fp32 out), cols % 8 == 0.
-hipError_t colsum(const void* x, bool bf16, float* out, int64_t rows, int64_t cols, float* ws, hipStream_t st) {
-  if (rows == 0) return hipMemsetAsync(out, 0, cols * sizeof(float), st);
+// Column sums of a [rows, cols] matrix (bias gradients): out[c] = sum_r x[r, c] (fp32 or bf16 out), cols % 8 == 0.
+hipError_t colsum(const void* x, bool bf16, void* out, bool out_bf16, int64_t rows, int64_t cols, float* ws,
+                  hipStream_t st) {
+  if (rows == 0) return hipMemsetAsync(out, 0, cols * (out_bf16 ? 2 : 4), st);
   const int nslab = plan_slabs(rows, cols);
   const int64_t rps = (rows + nslab - 1) / nslab;
   dim3 pg((unsigned)((cols + kStripCols - 1) / kStripCols), (unsigned)nslab);
@@ -565,7 +572,7 @@ hipError_t colsum(const void* x, bool bf16, float* out, int64_t rows, int64_t co
     colstrip_partial_kernel<float, false, false><<<pg, kThreads, 0, st>>>((const float*)x, nullptr, nullptr, nullptr,
                                                                           ws, rows, cols, rps, nslab);
   PDA_CHECK_HIP(hipGetLastError());
-  colreduce_finalize_kernel<<<fin_grid(cols), kFinCols * kFinLanes, 0, st>>>(ws, nslab, cols, 1, out, nullptr);
+  colreduce_finalize_kernel<<<fin_grid(cols), kFinCols * kFinLanes, 0, st>>>(ws, nslab, cols, 1, out, nullptr, out_bf16 ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -2,8 +2,9 @@
 
     python -m torch.distributed.run --nproc-per-node 8 -m pytorchdistributed_amd.bench.gpt2xl_pp --gpus 8
 World = pp x dp (default pp = min(4, world)); 1F1B schedule (``--schedule interleaved --chunks v``: v
-model chunks per rank, virtual stage c*pp + stage); per-stage gradient averaging over the DP group after
-the pipeline flush; fused AdamW per stage.
+model chunks per rank, virtual stage c*pp + stage); the stage's gradient average over its DP group runs
+through DDP (buckets launched during the last micro-batch's backward; after the flush for interleaved);
+fused AdamW per stage.
 """
 from __future__ import annotations
 
@@ -14,6 +15,7 @@ import torch
 from ..data.device import DeviceSyntheticTokens
 from ..models.gpt2 import GPT2Stage, config
 from ..optim import AdamW
+from ..parallel.ddp import DistributedDataParallel
 from ..parallel.pipeline import Pipeline, dp_sync_grads, partition_layers, pp_dp_groups
 from ..utils.tunable import use_tuned_gemms
 from .common import emit, setup, teardown, timed
@@ -53,11 +55,16 @@ def main(argv=None):
         mod = torch.nn.ModuleList(chunks)
         pipe = Pipeline(chunks, ranks, a.micro, schedule="interleaved",
                         loss_fn=chunks[-1].loss if stage == pp - 1 else None, group=pp_group, device=device)
+        ddp = None
     else:
         lo, hi = partition_layers(cfg.n_layer, pp)[stage]
         mod = GPT2Stage(cfg, lo, hi, stage == 0, stage == pp - 1, device=device, dtype=torch.bfloat16)
+        # the stage's DP gradient average: DDP over the DP group, buckets launched during the last
+        # micro-batch's backward (overlapped with it and the drain); flat buffers -> one AdamW launch
+        ddp = DistributedDataParallel(mod, device_ids=[device.index] if device.type == "cuda" else None,
+                                      process_group=dp_group)
         pipe = Pipeline(mod, ranks, a.micro, schedule=a.schedule, loss_fn=mod.loss if stage == pp - 1 else None,
-                        group=pp_group, device=device)
+                        group=pp_group, device=device, dp_module=ddp)
     opt = AdamW(mod.parameters(), lr=1e-4, weight_decay=0.1)
     data = DeviceSyntheticTokens(a.micro * a.micro_batch, a.seq, cfg.vocab_size, device=device, rank=dp_rank)
 
@@ -65,15 +72,17 @@ def main(argv=None):
         x, y = data.next()
         opt.zero_grad(set_to_none=True)
         pipe.step(x, y)
-        dp_sync_grads(mod, dp_group)
+        if ddp is None:
+            dp_sync_grads(mod, dp_group)
         opt.step()
 
     secs = timed(step, a.steps, a.warmup)
+    comm = ddp.comm_stats() if ddp is not None else {}
     toks = a.micro * a.micro_batch * a.seq * dp * a.steps / secs
     emit({"metric": "tokens/sec (whole job) GPT-2-XL pipeline x DDP", "value": round(toks, 1),
           "unit": "tokens/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
           "ms_per_step": round(secs / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-          "vs_baseline": None, "dtype": "bf16", "data": "synthetic tokens (on-device), random-init weights", "gemm_table": gemm_table,
+          "vs_baseline": None, "dtype": "bf16", "dp_comm": comm, "data": "synthetic tokens (on-device), random-init weights", "gemm_table": gemm_table,
           "config": {"model": a.model, "global_batch": a.micro * a.micro_batch * dp, "seq_len": a.seq,
                      "parallelism": f"pp{pp}xdp{dp}", "schedule": a.schedule, "microbatches": a.micro,
                      **({"chunks": a.chunks} if a.schedule == "interleaved" else {})}}, rank)

@@ -172,6 +172,14 @@ class ResNet(tnn.Module):
         x = ops.global_avg_pool2d(x)
         return self.fc(x)
 
+    # checkpoint layout of the reference (torchvision ResNet: `conv1`/`bn1` at top level, OIHW conv
+    # weights) — utils/checkpoint.py saves MODEL_STATE in it, so a stock torchvision ResNet-50 loads it
+    def reference_state_dict(self) -> dict:
+        return to_torchvision_state_dict(self)
+
+    def load_reference_state_dict(self, sd: dict):
+        return from_torchvision_state_dict(self, sd)
+
     def stage_modules(self) -> List[tnn.Module]:
         """Ordered top-level stages (used by model/pipeline parallel splits, `NB03:325-349`)."""
         return [self.stem, self.layer1, self.layer2, self.layer3, self.layer4, _Head(self.fc)]

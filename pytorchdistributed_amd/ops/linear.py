@@ -117,9 +117,11 @@ def _param_grads(dy2, x2, wparam, bparam, need_w, need_b):
         else:
             dw = _gemm_wgrad(dy2, x2, wparam.dtype, target)
     if need_b:
+        # written in the parameter dtype, straight into its flat-buffer slot when it has one
         tb = grad_target(bparam)
-        db = C().colsum(dy2)
-        db = tb.copy_(db) if tb is not None else db.to(bparam.dtype)
+        db = C().colsum(dy2, out=tb, out_bf16=bparam.dtype == torch.bfloat16)
+        if db.dtype != bparam.dtype:
+            db = db.to(bparam.dtype)
     return dw, db
 
 

@@ -173,6 +173,21 @@ def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=Tru
     return _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu)
 
 
+def _param_grad_slots(ctx, gi: int):
+    """Flat-buffer gradient slots of (gamma, beta) when both have one (the norm backward's finalize
+    writes dgamma / dbeta there in the parameter dtype: no cast kernel, no copy into the DDP bucket)."""
+    gamma, beta = ctx.params
+    ng = ctx.needs_input_grad
+    tg = grad_target(gamma) if ng[gi] else None
+    tb = grad_target(beta) if (beta is not None and ng[gi + 1]) else None
+    if beta is not None and (tg is None) != (tb is None):  # one slot only: let both allocate
+        for p, t in ((gamma, tg), (beta, tb)):
+            if t is not None:
+                p._pda_claimed = False
+        tg = tb = None
+    return tg, tb
+
+
 class _RowNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, eps, rms):
@@ -181,13 +196,15 @@ class _RowNormFn(torch.autograd.Function):
         ctx.save_for_backward(x, gamma, mean, rstd)
         ctx.rms = rms
         ctx.has_beta = beta is not None
+        ctx.params = (gamma, beta)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, gamma, mean, rstd = ctx.saved_tensors
-        dx, dg, db = C().rownorm_bwd(dy.contiguous(), x, gamma, mean, rstd, ctx.rms)
-        return dx, dg.to(gamma.dtype), (db.to(gamma.dtype) if ctx.has_beta else None), None, None
+        tg, tb = _param_grad_slots(ctx, 1)
+        dx, dg, db = C().rownorm_bwd(dy.contiguous(), x, gamma, mean, rstd, ctx.rms, None, tg, tb)
+        return dx, dg, (db if ctx.has_beta else None), None, None
 
 
 def layer_norm(x, weight, bias, eps=1e-5):
@@ -212,6 +229,7 @@ class _AddRowNormFn(torch.autograd.Function):
         ctx.save_for_backward(h, gamma, mean, rstd)
         ctx.rms = rms
         ctx.has_beta = beta is not None
+        ctx.params = (gamma, beta)
         return h, y
 
     @staticmethod
@@ -220,8 +238,9 @@ class _AddRowNormFn(torch.autograd.Function):
         if dy is None:  # the normed output is unused: the residual gradient passes straight through
             return dh, dh, None, None, None, None
         addend = dh.contiguous() if dh is not None else None
-        dx, dg, db = C().rownorm_bwd(dy.contiguous(), h, gamma, mean, rstd, ctx.rms, addend)
-        return dx, dx, dg.to(gamma.dtype), (db.to(gamma.dtype) if ctx.has_beta else None), None, None
+        tg, tb = _param_grad_slots(ctx, 2)
+        dx, dg, db = C().rownorm_bwd(dy.contiguous(), h, gamma, mean, rstd, ctx.rms, addend, tg, tb)
+        return dx, dx, dg, (db if ctx.has_beta else None), None, None
 
 
 def add_norm_train(x, r, weight, bias=None, eps=1e-5, rms=True):

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import time
 from typing import Dict, List, Optional
 
 import torch
@@ -185,7 +186,7 @@ class DistributedDataParallel(tnn.Module):
         if self.world > 1 and dist.is_initialized():
             dev = self._params[0].device if self.backend == "nccl" else torch.device("cpu")
             t = torch.tensor(order, dtype=torch.int64, device=dev)
-            dist.broadcast(t, 0, group=self.process_group)
+            dist.broadcast(t, self._src0(), group=self.process_group)
             order = t.tolist()
         current = [pi for b in range(self.reducer.num_buckets) for pi in self.reducer.bucket_params(b)]
         if order == current:
@@ -222,11 +223,15 @@ class DistributedDataParallel(tnn.Module):
     def _use_ring(self):
         return self.backend == "ring"
 
+    def _src0(self) -> int:
+        """Global rank of the group's rank 0 (torch's broadcast takes a global source rank)."""
+        return dist.get_global_rank(self.process_group, 0) if self.process_group is not None else 0
+
     def _bcast(self, t: torch.Tensor):
         if self._use_ring() and t.device.type == "cpu":
             pdist.host_ring().broadcast(t.data_ptr(), t.numel() * t.element_size(), 0)
         else:
-            dist.broadcast(t, 0, group=self.process_group)
+            dist.broadcast(t, self._src0(), group=self.process_group)
 
     def _bucket_view(self, b: int) -> torch.Tensor:
         dt, start, n = self.bucket_slices[b]
@@ -364,9 +369,12 @@ class DistributedDataParallel(tnn.Module):
             for b in self.reducer.flush_unready():
                 self._launch(b)
         ev = None
+        host_t0 = None
         if self.track_comm and self._works and torch.cuda.is_available() and self.backend == "nccl":
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
+        elif self.track_comm and self._works:
+            host_t0 = time.perf_counter()  # gloo / host ring: the waits block the host
         for work, t in self._works:
             work.wait()
             if isinstance(t, tuple):  # fp32 reduction of a low-precision bucket (gloo)
@@ -377,6 +385,8 @@ class DistributedDataParallel(tnn.Module):
         if ev is not None:
             ev[1].record()
             self._exposed_events.append(ev)
+        if host_t0 is not None:
+            self._stats["exposed_host_ms"] = self._stats.get("exposed_host_ms", 0.0) + (time.perf_counter() - host_t0) * 1e3
         self._works.clear()
         if self.backend != "nccl" and self.xgmi is None:
             self._sweep_tickets(force=True)  # gloo waits were blocking: all done
@@ -397,6 +407,8 @@ class DistributedDataParallel(tnn.Module):
         if self._exposed_events:
             self._exposed_events[-1][1].synchronize()
             out["exposed_comm_ms"] = sum(a.elapsed_time(b) for a, b in self._exposed_events)
+        elif "exposed_host_ms" in out:
+            out["exposed_comm_ms"] = out.pop("exposed_host_ms")
         if reset:
             self._stats = {"comm_bytes": 0, "comm_calls": 0}
             self._exposed_events = []

@@ -18,11 +18,14 @@ as ONE batched P2P group (likewise "send gradient to s-1" + "receive next activa
 neighbours never wait on each other's opposite-direction transfer (the classic blocking-P2P deadlock).
 ``recompute=True`` keeps only each micro-batch's stage input and re-runs the stage forward in backward
 (GPipe re-materialisation, raw lines 637-643).  :func:`pp_dp_groups` builds the PP x DP process groups
-(e.g. 4 stages x 2 replicas: PP {0-3},{4-7}; DP {0,4},{1,5},{2,6},{3,7}) and :func:`dp_sync_grads`
-averages a stage's gradients over its DP group in flat buckets.
+(e.g. 4 stages x 2 replicas: PP {0-3},{4-7}; DP {0,4},{1,5},{2,6},{3,7}).  The DP gradient average
+runs through the stage's :class:`~.ddp.DistributedDataParallel` over the DP group (``dp_module``):
+bucketed, launched during the last micro-batch's backward, overlapped with it and with the drain;
+:func:`dp_sync_grads` (after the flush, blocking) remains for the interleaved schedule.
 """
 from __future__ import annotations
 
+import contextlib
 import json
 import os
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -33,6 +36,8 @@ import torch.nn as tnn
 from torch.utils.checkpoint import checkpoint
 
 from .. import distributed as pdist
+
+_nullctx = contextlib.nullcontext
 
 
 # ------------------------------------------------------------------ schedules (pure functions)
@@ -215,7 +220,11 @@ class Pipeline:
 
     def __init__(self, stage_module, ranks: Sequence[int], num_microbatches: int,
                  schedule: str = "1f1b", loss_fn: Optional[Callable] = None, recompute: bool = False,
-                 group=None, device=None):
+                 group=None, device=None, dp_module=None):
+        """``dp_module``: the stage wrapped in :class:`~.ddp.DistributedDataParallel` over its DP group
+        (PP x DP).  Micro-batches 0..M-2 run backward under ``no_sync`` (local accumulation); the last
+        micro-batch's backward launches the gradient buckets as they become ready, so the DP all-reduce
+        overlaps that backward and the pipeline drain (reference DDP semantics, `ddp_gpus.py:35,41`)."""
         # schedule="interleaved": ``stage_module`` is the list of this rank's model chunks (chunk c =
         # virtual stage c * len(ranks) + stage)
         self.chunks = list(stage_module) if isinstance(stage_module, (list, tuple, tnn.ModuleList)) else None
@@ -236,6 +245,9 @@ class Pipeline:
         self.next = self.ranks[self.stage + 1] if self.stage < self.S - 1 else None
         self._fwd_meta = None  # (shape, dtype) received from prev
         self._bwd_meta = None  # (shape, dtype) of our output (grad received from next)
+        self.dp_module = dp_module
+        if dp_module is not None and schedule == "interleaved":
+            raise ValueError("dp_module with the interleaved schedule: sync the chunks with dp_sync_grads")
 
     @property
     def is_first(self):
@@ -425,10 +437,13 @@ class Pipeline:
 
         def run_backward(i, dy):
             out = acts_out[i]
-            if self.is_last:
-                out.backward()
-            else:
-                torch.autograd.backward(out, dy)
+            # DP gradient sync only in the last micro-batch's backward (both schedules run it last)
+            ctx = self.dp_module.no_sync() if (self.dp_module is not None and i != M - 1) else _nullctx()
+            with ctx:
+                if self.is_last:
+                    out.backward()
+                else:
+                    torch.autograd.backward(out, dy)
             dx = acts_in[i].grad if not self.is_first else None
             acts_in[i] = acts_out[i] = None
             return dx

@@ -36,7 +36,13 @@ def set_rng_state(st):
 
 
 def save_snapshot(path: str, model, optimizer=None, epochs_run: int = 0, extra: dict | None = None):
-    snap = {"MODEL_STATE": unwrap(model).state_dict(), "EPOCHS_RUN": epochs_run}
+    """Models with a reference layout (``reference_state_dict()``, e.g. the channels-last ResNet-50 ->
+    torchvision's OIHW / top-level ``conv1``) are saved in it, tagged ``"LAYOUT": "reference"``."""
+    m = unwrap(model)
+    if hasattr(m, "reference_state_dict"):
+        snap = {"MODEL_STATE": m.reference_state_dict(), "LAYOUT": "reference", "EPOCHS_RUN": epochs_run}
+    else:
+        snap = {"MODEL_STATE": m.state_dict(), "EPOCHS_RUN": epochs_run}
     if optimizer is not None:
         snap["OPTIMIZER_STATE"] = optimizer.state_dict()
     snap["RNG"] = rng_state()
@@ -50,7 +56,11 @@ def save_snapshot(path: str, model, optimizer=None, epochs_run: int = 0, extra: 
 
 def load_snapshot(path: str, model, optimizer=None, map_location="cpu") -> int:
     snap = torch.load(path, map_location=map_location, weights_only=True)
-    unwrap(model).load_state_dict(snap["MODEL_STATE"])
+    m = unwrap(model)
+    if snap.get("LAYOUT") == "reference" and hasattr(m, "load_reference_state_dict"):
+        m.load_reference_state_dict(snap["MODEL_STATE"])
+    else:
+        m.load_state_dict(snap["MODEL_STATE"])
     if optimizer is not None and "OPTIMIZER_STATE" in snap:
         optimizer.load_state_dict(snap["OPTIMIZER_STATE"])
         sync = getattr(optimizer, "sync_from_state", None)

@@ -121,9 +121,12 @@ def _tiny_stack(n_layers=4, d=16, seed=0):
     return nn.Sequential(*layers)
 
 
-def pipeline_worker(rank, world, pp, dp, schedule, recompute, outdir):
-    """PP x DP on gloo: stage grads after one pipeline step must equal the single-process grads."""
+def pipeline_worker(rank, world, pp, dp, schedule, recompute, outdir, dp_mode="sync"):
+    """PP x DP on gloo: stage grads after one pipeline step must equal the single-process grads.
+    ``dp_mode``: "sync" = dp_sync_grads after the flush; "ddp" = the stage wrapped in DDP over its DP group
+    (buckets launched during the last micro-batch's backward)."""
     import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
     from pytorchdistributed_amd.parallel.pipeline import Pipeline, dp_sync_grads, partition_layers, pp_dp_groups
 
     pd.init_process_group("gloo")
@@ -136,12 +139,21 @@ def pipeline_worker(rank, world, pp, dp, schedule, recompute, outdir):
     X = torch.randn(dp * 8, 16, generator=g)
     Y = torch.randn(dp * 8, 16, generator=g)
     xs, ys = X[dp_rank * 8:(dp_rank + 1) * 8], Y[dp_rank * 8:(dp_rank + 1) * 8]
-    pipe = Pipeline(stage_mod, ranks, num_microbatches=4, schedule=schedule, loss_fn=F.mse_loss,
-                    recompute=recompute, device=torch.device("cpu"))
+    ddp = None
+    if dp_mode == "ddp":
+        os.environ["PDA_TRACK_COMM"] = "1"
+        ddp = DistributedDataParallel(stage_mod, process_group=dp_group, bucket_cap_mb=0.002, first_bucket_mb=0.001)
+    pipe = Pipeline(ddp.module if ddp is not None else stage_mod, ranks, num_microbatches=4, schedule=schedule,
+                    loss_fn=F.mse_loss, recompute=recompute, device=torch.device("cpu"), dp_module=ddp)
     loss = pipe.step(xs, ys)
-    dp_sync_grads(stage_mod, dp_group)
+    stats = None
+    if ddp is None:
+        dp_sync_grads(stage_mod, dp_group)
+    else:
+        stats = ddp.comm_stats()
+        assert stats["comm_calls"] == ddp.reducer.num_buckets or stats["comm_calls"] > 0, stats
     torch.save({"grads": {n: p.grad.clone() for n, p in stage_mod.named_parameters()}, "lo": lo,
-                "loss": loss}, os.path.join(outdir, f"{rank}.pt"))
+                "loss": loss, "stats": stats}, os.path.join(outdir, f"{rank}.pt"))
     pd.destroy_process_group()
 
 

@@ -157,19 +157,29 @@ def test_resnet50_fp32_matches_cpu_fp32():
             assert rel_err(pg.grad.cpu(), pr.grad) < 1e-3, n
 
 
-def test_resnet50_fp32_whole_model_gradients():
-    """Whole-model train-mode gradients of the fp32 ResNet-50 against an fp64 CPU oracle.  A random-init
-    ResNet-50 on 4 images is ill-conditioned (batch statistics over 16 values in layer4): CPU fp32
-    itself sits up to ~2 % from fp64 on some BN parameters.  So: the loss at equal weights to 1e-4; the
-    whole gradient vector norm-wise; per parameter, the 4-product split (fp32-grade products) within a
-    small factor of CPU fp32's own error, the default 3-product split within a larger one."""
+def _round_tf32(t):
+    """fp32 -> TF32 (10-bit mantissa, round to nearest) as cuDNN feeds A100 tensor cores; the rounding
+    is applied to the values only (straight-through for autograd, whose conv backward sees the rounded
+    operands as well)."""
+    d = t.detach().contiguous()
+    r = ((d.view(torch.int32) + 0x1000) & ~0x1FFF).view(torch.float32)
+    return t + (r - d)
+
+
+def test_resnet50_fp32_whole_model_gradients(monkeypatch):
+    """Whole-model train-mode gradients of the fp32 ResNet-50 against an fp64 CPU oracle, compared with
+    what the reference's own precision gets: its A100 ran the convs in TF32 (emulated here on the CPU by
+    rounding every conv operand to TF32).  A random-init ResNet-50 is ill-conditioned (batch-statistics
+    BN backward), so errors are judged against those two yardsticks, not absolute: the default 3-product
+    split must beat TF32 whole-vector and per parameter; the 4-product split must be fp32-grade."""
     from pytorchdistributed_amd.data.datasets import random_image_batch
     from pytorchdistributed_amd.models.resnet import resnet50
+    from pytorchdistributed_amd.ops import conv as conv_mod
     from pytorchdistributed_amd.ops import cross_entropy, fp32
 
     torch.manual_seed(0)
     cpu = resnet50()
-    x, y = random_image_batch(4, (64, 64), 1000)
+    x, y = random_image_batch(6, (96, 96), 1000)
 
     def grads(m, dev, dt):
         m.zero_grad()
@@ -179,6 +189,10 @@ def test_resnet50_fp32_whole_model_gradients():
 
     l64, g64 = grads(copy.deepcopy(cpu).double(), "cpu", torch.float64)
     l32, g32 = grads(copy.deepcopy(cpu), "cpu", torch.float32)
+    ref_conv = conv_mod._ref_conv
+    with monkeypatch.context() as mp:
+        mp.setattr(conv_mod, "_ref_conv", lambda x_, w_, *a, **k: ref_conv(_round_tf32(x_), _round_tf32(w_), *a, **k))
+        ltf, gtf = grads(copy.deepcopy(cpu), "cpu", torch.float32)
     res = {}
     for nseg in (3, 4):
         fp32.set_split(nseg)
@@ -187,24 +201,22 @@ def test_resnet50_fp32_whole_model_gradients():
         finally:
             fp32.set_split(3)
 
-    def per_param(g):
-        return {n: rel_err(g[n], g64[n]) for n in g64}
+    def worst(g):
+        return max(rel_err(g[n], g64[n]) for n in g64)
 
     def whole(g):
-        a = torch.cat([g[n].flatten() for n in g64])
-        b = torch.cat([g64[n].flatten() for n in g64])
-        return rel_err(a, b)
+        return rel_err(torch.cat([g[n].flatten() for n in g64]), torch.cat([g64[n].flatten() for n in g64]))
 
-    e32 = per_param(g32)
-    worst32 = max(e32.values())
+    print(f"cpu fp32: whole {whole(g32):.2e} worst {worst(g32):.2e}; tf32 convs: whole {whole(gtf):.2e} "
+          f"worst {worst(gtf):.2e}")
+    for nseg, (loss, g) in res.items():
+        print(f"split {nseg}: loss {abs(loss - l64) / abs(l64):.2e} whole {whole(g):.2e} worst {worst(g):.2e}")
     for nseg, (loss, g) in res.items():
         assert abs(loss - l64) < 1e-4 * abs(l64), (nseg, loss, l64)
-        e = per_param(g)
-        worst = max(e.values())
-        print(f"split {nseg}: whole {whole(g):.2e} worst {worst:.2e} (cpu fp32: whole {whole(g32):.2e} worst "
-              f"{worst32:.2e})")
-        assert whole(g) < 1e-3, (nseg, whole(g))
-        assert worst < (3 * worst32 + 1e-3 if nseg == 4 else 15 * worst32 + 1e-3), (nseg, worst, worst32)
+    _, g3 = res[3]
+    _, g4 = res[4]
+    assert whole(g3) < whole(gtf) and worst(g3) < worst(gtf), (whole(g3), whole(gtf), worst(g3), worst(gtf))
+    assert whole(g4) < 3 * whole(g32) + 1e-4 and worst(g4) < 3 * worst(g32) + 1e-3, (whole(g4), whole(g32))
 
 
 def test_resnet50_fp32_adam_step():

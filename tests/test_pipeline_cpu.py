@@ -48,12 +48,19 @@ def _reference_grads(dp):
     return full
 
 
-@pytest.mark.parametrize("pp,dp,schedule,recompute", [(2, 1, "gpipe", False), (2, 1, "1f1b", False),
-                                                      (4, 1, "1f1b", True), (2, 2, "1f1b", False)])
-def test_pipeline_grads_match_single_process(tmp_path, pp, dp, schedule, recompute):
+@pytest.mark.parametrize("pp,dp,schedule,recompute,dp_mode", [
+    (2, 1, "gpipe", False, "sync"), (2, 1, "1f1b", False, "sync"), (4, 1, "1f1b", True, "sync"),
+    (2, 2, "1f1b", False, "sync"), (2, 2, "1f1b", False, "ddp"), (2, 2, "gpipe", True, "ddp")])
+def test_pipeline_grads_match_single_process(tmp_path, pp, dp, schedule, recompute, dp_mode):
+    """``dp_mode="ddp"``: the DP average runs through the stage's DDP over its DP group, launched during
+    the last micro-batch's backward (no_sync before), reporting the exposed communication time."""
     world = pp * dp
-    spawn(_workers.pipeline_worker, args=(world, pp, dp, schedule, recompute, str(tmp_path)), nprocs=world,
-          timeout=180)
+    spawn(_workers.pipeline_worker, args=(world, pp, dp, schedule, recompute, str(tmp_path), dp_mode),
+          nprocs=world, timeout=180)
+    if dp_mode == "ddp":
+        for r in range(world):
+            st = torch.load(tmp_path / f"{r}.pt", weights_only=True)["stats"]
+            assert st["comm_calls"] > 0 and "exposed_comm_ms" in st, st
     ref = _reference_grads(dp)
     ref_blocks = [ref[3 * i: 3 * i + 3] for i in range(4)]
     for r in range(world):

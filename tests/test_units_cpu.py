@@ -358,3 +358,31 @@ def test_bn_dual_guard_channel_counts():
     assert C().bn_dual_ok(2048) and C().bn_dual_ok(256)
     assert not C().bn_dual_ok(1536)
     assert not C().bn_dual_ok(0) and not C().bn_dual_ok(4)
+
+
+def test_resnet_snapshot_in_torchvision_layout(tmp_path):
+    """ResNet-50 snapshots carry MODEL_STATE in the reference's torchvision layout (top-level conv1 / bn1,
+    OIHW conv weights; `03_model_parallel.ipynb` raw lines 107-110, 314), so a stock torchvision
+    ResNet-50 could load them; load_snapshot converts back to the channels-last model exactly."""
+    from pytorchdistributed_amd.models.resnet import resnet50
+    from pytorchdistributed_amd.utils.checkpoint import load_snapshot, save_snapshot
+
+    torch.manual_seed(0)
+    m = resnet50()
+    path = str(tmp_path / "snap.pt")
+    save_snapshot(path, m, None, epochs_run=1)
+    snap = torch.load(path, weights_only=True)
+    sd = snap["MODEL_STATE"]
+    assert snap["LAYOUT"] == "reference"
+    assert tuple(sd["conv1.weight"].shape) == (64, 3, 7, 7)  # torchvision shapes / names
+    assert tuple(sd["layer1.0.conv2.weight"].shape) == (64, 64, 3, 3)
+    assert tuple(sd["layer4.2.conv3.weight"].shape) == (2048, 512, 1, 1)
+    assert tuple(sd["fc.weight"].shape) == (1000, 2048) and "bn1.running_var" in sd
+    assert "layer1.0.downsample.0.weight" in sd and "layer1.0.downsample.1.num_batches_tracked" in sd
+    assert not any(k.startswith("stem.") for k in sd) and sum(v.numel() for k, v in sd.items()
+                                                             if not k.endswith(("running_mean", "running_var",
+                                                                                "num_batches_tracked"))) == 25557032
+    m2 = resnet50()
+    assert load_snapshot(path, m2) == 1
+    for (k, a), (_, b) in zip(m.state_dict().items(), m2.state_dict().items()):
+        assert torch.equal(a, b), k
