@@ -10,7 +10,8 @@
 //   conv fwd:    x -> [.., 3C] (hi, hi, lo) channels,    w -> [Co, R, S, 3C] (hi, lo, hi)
 //   conv dgrad:  dy -> [.., 3Co] (hi, hi, lo) channels,  w -> [3Co, R, S, C] stacked (hi, lo, hi)
 //   conv wgrad:  dy -> [3N, ..] stacked (hi, lo, hi),    x -> [3N, ..] stacked (hi, hi, lo)
-// Relative error ~1e-5 of the fp32 result (TF32 keeps 11 bits: ~1e-3); 4 segments ~1e-7.
+// hi + lo carries 16 significant bits: ~1e-5 relative per GEMM (TF32 keeps 11 bits: ~5e-4); a 4th
+// product (lo.lo) does not lower that representation floor.
 //
 // Plus the fp32 elementwise / reduction kernels the fp32 ResNet needs: BatchNorm2d (training batch
 // statistics in two passes with shifted sums and a double-precision finalize, fused residual add +

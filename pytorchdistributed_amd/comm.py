@@ -99,6 +99,14 @@ class Communicator:
         for s in (streams if streams is not None else [torch.cuda.current_stream(self.device)]):
             self._c.wait_stream(s.cuda_stream)
 
+    def _check(self, op: str, *ts, **kw):
+        """``PDA_DEBUG=collectives``: the cross-rank fingerprint check (parallel/debug.py) covers the
+        native collectives too (op, dtype, shape, reduce op / root)."""
+        from .parallel import debug as _debug
+
+        if _debug._CHECKER is not None:
+            _debug._CHECKER.check("rccl." + op, ts, dict(kw, group=self.group))
+
     def _hold(self, *ts: torch.Tensor):
         for t in ts:
             t.record_stream(self.stream)  # the caching allocator must not recycle it under the collective
@@ -108,6 +116,7 @@ class Communicator:
         """In place; ``op`` in sum / avg / max / min / prod.  ``streams``: producers of ``t`` (default:
         the current stream)."""
         assert t.is_contiguous() and t.device == self.device
+        self._check("all_reduce", t, op=op)
         self._after(streams)
         self._hold(t)
         return Work(self._c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPE[t.dtype], _OPS[op]), (t,))
@@ -116,6 +125,7 @@ class Communicator:
         """``out`` = op over ranks of this rank's ``out.numel()`` chunk of ``inp``."""
         assert inp.numel() == out.numel() * self.size and inp.dtype == out.dtype
         assert inp.is_contiguous() and out.is_contiguous()
+        self._check("reduce_scatter", out, inp, op=op)
         self._after(streams)
         self._hold(out, inp)
         return Work(self._c.reduce_scatter(inp.data_ptr(), out.data_ptr(), out.numel(), _DTYPE[out.dtype], _OPS[op]),
@@ -125,6 +135,7 @@ class Communicator:
         """``out`` = concatenation over ranks of ``inp``."""
         assert out.numel() == inp.numel() * self.size and inp.dtype == out.dtype
         assert inp.is_contiguous() and out.is_contiguous()
+        self._check("all_gather", out, inp)
         self._after(streams)
         self._hold(out, inp)
         return Work(self._c.all_gather(inp.data_ptr(), out.data_ptr(), inp.numel(), _DTYPE[inp.dtype]), (out, inp))
@@ -132,6 +143,7 @@ class Communicator:
     def broadcast(self, t: torch.Tensor, root: int = 0, streams=None) -> Work:
         """In place from group rank ``root``."""
         assert t.is_contiguous()
+        self._check("broadcast", t, src=root)
         self._after(streams)
         self._hold(t)
         return Work(self._c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPE[t.dtype], root), (t,))

@@ -5,7 +5,10 @@ The reference trains in fp32 (`03 模型并行/03_model_parallel.ipynb` raw line
 bf16 rate, so conv GEMMs here run on the bf16 MFMA kernels with split operands (`csrc/kernels/fp32x3.hip`):
 ``x = hi + lo`` (two bf16), ``x.w ~ hi.hi + hi.lo + lo.hi`` accumulated in fp32 — the three products
 laid side by side along the GEMM's K, so one launch of the ordinary conv kernel computes them
-(``PDA_FP32_SPLIT=4`` adds ``lo.lo``).  Relative error ~1e-5 (TF32 ~1e-3).  BatchNorm, pooling and
+(``PDA_FP32_SPLIT=4`` adds ``lo.lo``).  ``hi + lo`` carries 16 significant bits of x, so every
+product is good to ~2^-17 relative (~1e-5 per GEMM; TF32, the reference's A100 conv precision, keeps
+11 bits: ~5e-4) — whole-model gradients land >5x closer to an fp64 oracle than TF32 convs
+(tests/test_fp32_gpu.py).  BatchNorm, pooling and
 the ReLU / residual epilogues are native fp32 kernels; the Linear layer keeps the exact fp32 SIMT
 GEMM (`ops/linear.py`) and cross-entropy reads fp32 logits natively.
 """
@@ -25,7 +28,8 @@ MASK_A, MASK_B = _MASKS[3]
 
 
 def set_split(n: int) -> None:
-    """Number of split products per fp32 GEMM: 3 (hi.hi + hi.lo + lo.hi, ~1e-5) or 4 (+ lo.lo, ~1e-7)."""
+    """Number of split products per fp32 GEMM: 3 (hi.hi + hi.lo + lo.hi) or 4 (+ lo.lo); both are bound
+    by the 16-bit hi + lo representation of the operands (~1e-5 relative)."""
     global NSEG, MASK_A, MASK_B
     if n not in _MASKS:
         raise ValueError("the fp32 split must be 3 or 4")

@@ -248,6 +248,16 @@ class Pipeline:
         self.dp_module = dp_module
         if dp_module is not None and schedule == "interleaved":
             raise ValueError("dp_module with the interleaved schedule: sync the chunks with dp_sync_grads")
+        # activations / gradients between stages on the native RCCL communicator of the PP group
+        # (comm.py: one fused send/recv group per transfer pair, ordered on its own stream; the consumer
+        # stream waits on an event, no host blocking); c10d batch_isend_irecv on gloo / PDA_COMM=c10d
+        self._ncomm = None
+        if (self.device.type == "cuda" and dist.is_initialized() and dist.get_backend(group) == "nccl"
+                and self.S > 1):
+            from .. import comm as _comm
+
+            if _comm.enabled():
+                self._ncomm = _comm.for_group(group, self.device)
 
     @property
     def is_first(self):
@@ -273,6 +283,15 @@ class Pipeline:
         return tuple(int(v) for v in meta[2: 2 + nd]), dtype
 
     def _p2p(self, send: Optional[Tuple[torch.Tensor, int]] = None, recv: Optional[Tuple[torch.Tensor, int]] = None):
+        if self._ncomm is not None and (send is not None or recv is not None):
+            g = self.group
+
+            def peer(r):
+                return dist.get_group_rank(g, r) if g is not None else r
+            sends = [(send[0].contiguous(), peer(send[1]))] if send is not None else []
+            recvs = [(recv[0], peer(recv[1]))] if recv is not None else []
+            self._ncomm.send_recv(sends, recvs).wait()
+            return
         ops = []
         if send is not None:
             ops.append(dist.P2POp(dist.isend, send[0].contiguous(), send[1], group=self.group))
