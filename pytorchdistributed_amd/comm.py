@@ -99,13 +99,13 @@ class Communicator:
         for s in (streams if streams is not None else [torch.cuda.current_stream(self.device)]):
             self._c.wait_stream(s.cuda_stream)
 
-    def _check(self, op: str, *ts, **kw):
+    def _check(self, name: str, *ts, **kw):
         """``PDA_DEBUG=collectives``: the cross-rank fingerprint check (parallel/debug.py) covers the
         native collectives too (op, dtype, shape, reduce op / root)."""
         from .parallel import debug as _debug
 
         if _debug._CHECKER is not None:
-            _debug._CHECKER.check("rccl." + op, ts, dict(kw, group=self.group))
+            _debug._CHECKER.check("rccl." + name, ts, dict(kw, group=self.group))
 
     def _hold(self, *ts: torch.Tensor):
         for t in ts:
@@ -188,6 +188,26 @@ def for_group(group=None, device: Optional[torch.device] = None) -> Communicator
     if c is None or c.aborted:
         c = _cache[key] = Communicator(group, dev)
     return c
+
+
+def try_for_group(group=None, device: Optional[torch.device] = None) -> Optional[Communicator]:
+    """:func:`for_group`, or None on every rank when it failed on any rank (the ranks agree through one
+    c10d all-reduce of a success flag, so no rank drives the native path while another uses c10d)."""
+    import warnings
+
+    comm, err = None, None
+    try:
+        comm = for_group(group, device)
+    except Exception as e:  # noqa: BLE001 - reported below, the caller falls back to c10d
+        err = e
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    ok = torch.tensor([0 if err is None else 1], dtype=torch.int32, device=dev)
+    dist.all_reduce(ok, group=group)
+    if int(ok.item()) == 0:
+        return comm
+    warnings.warn(f"native RCCL communicator unavailable ({err or 'failed on another rank'}); "
+                  "gradient collectives fall back to torch.distributed")
+    return None
 
 
 def reset():

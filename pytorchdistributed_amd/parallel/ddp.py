@@ -123,7 +123,7 @@ class DistributedDataParallel(tnn.Module):
             from .. import comm as _comm
 
             if _comm.enabled():
-                self._ncomm = _comm.for_group(process_group, params[0].device)
+                self._ncomm = _comm.try_for_group(process_group, params[0].device)
         # ---- optional IPC all-reduce over xGMI for buckets (PDA_ALLREDUCE=ipc|oneshot|twoshot, single node)
         self.xgmi = None
         on_gpu = bool(params) and all(p.is_cuda for p in params)

@@ -285,7 +285,7 @@ class FullyShardedDataParallel(tnn.Module):
             from .. import comm as _comm
 
             if _comm.enabled():
-                self.ncomm = _comm.for_group(process_group, self.units[0].device)
+                self.ncomm = _comm.try_for_group(process_group, self.units[0].device)
         for u in self.units:
             u.transient_grad = self.world > 1 and u is not self.root_unit
             u.release_grad()

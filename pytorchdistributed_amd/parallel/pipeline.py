@@ -257,7 +257,7 @@ class Pipeline:
             from .. import comm as _comm
 
             if _comm.enabled():
-                self._ncomm = _comm.for_group(group, self.device)
+                self._ncomm = _comm.try_for_group(group, self.device)
 
     @property
     def is_first(self):
