@@ -156,7 +156,11 @@ class Communicator {
       }
     }
     if (dep_) (void)hipEventDestroy(dep_);
-    if (stream_) (void)hipStreamDestroy(stream_);
+    // stream_ is deliberately NOT destroyed: tensors the collectives used were record_stream()-ed on it
+    // (comm.py _hold), and the caching allocator records an event on that stream when such a tensor
+    // is freed — possibly after the communicator is gone (destroy_process_group, then the tensors go
+    // out of scope).  An event record on a destroyed stream is a use-after-free; one idle stream per
+    // communicator ever created is the price.
   }
 
   int rank() const { return rank_; }

@@ -1186,6 +1186,94 @@ __device__ __forceinline__ mfma_bf16x8 wide_frag(const char* half, int row, int 
   else return read_frag<false, 64>(half + (row >> 6) * (W_HALF / 2), row & 63, kk, lane);
 }
 
+// Ping-pong main loop (VAR 4).  The two 4-wave halves of the workgroup (wr = 0 / 1; waves w and w + 4
+// share a SIMD) run half a phase apart: group 1 takes one extra barrier up front, so every barrier
+// pairs one group's "operands ready, start multiplying" with the other's "done multiplying", and on
+// each SIMD one wave issues its 16 MFMAs while the other reads the next phase's fragments and issues
+// DMA.  The MFMA pipe never waits for a wave's own fragment reads, which is what bounded the
+// one-barrier-per-K-step schedule (every wave reading, then every wave multiplying).
+// A K step is 4 phases of 16 MFMAs, phase p = (k half p >> 1) x (64-row quarter qa = p & 1) of the
+// wave's 128 x 64 tile; fragments: A 4 (one quarter, one k half), B 4 (all 64 columns, one k half) —
+// 32 VGPRs, read just in time (8 / 4 / 8 / 4 ds_reads).  LDS is the same two 64 KB stages, refilled
+// a slot at a time as soon as its last reader is done: B slots of stage t & 1 are last read in phase
+// 2 of K step t, so K step t + 2's B is DMA'd in phase 3; A slots are last read in phase 3, so K step
+// t + 1's A is DMA'd in phase 0 of step t (after step t - 1's last read).  Every DMA is retired by the
+// vmcnt(0) in phase 3 of the step before its readers' step (phase 3 then holds no DMA of its own yet:
+// it waits, then issues), and read one phase after that wait — the wait precedes the phase's first
+// barrier and each group's next read follows one barrier later.  Reads retire (lgkmcnt(0)) before the
+// barrier that ends their load section, so a slot DMA'd one phase after its last read is never
+// overwritten under a reader.  sched_barrier(0) pins the MFMAs between their two barriers.
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int QA>
+__device__ __forceinline__ void pp_mma(f32x4 (&acc)[8][4], const mfma_bf16x8 (&fa)[4], const mfma_bf16x8 (&fb)[4]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      acc[4 * QA + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[4 * QA + i][j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <class IA, class IB, class RA, class RB>
+__device__ __forceinline__ void wide_pp_loop(f32x4 (&acc)[8][4], char* smem, int kt0, int nk, int wr, int lane,
+                                             IA issue_a, IB issue_b, RA rd_a, RB rd_b4) {
+  auto stage = [&](int t) { return t & 1; };
+  if (kt0 < nk) {
+    issue_a(kt0);
+    issue_b(kt0);
+    if (kt0 + 1 < nk) {
+      issue_a(kt0 + 1);
+      issue_b(kt0 + 1);
+      wait_vm<8>();  // K step kt0 landed (per thread: 4 half tiles x 2 DMAs of step kt0 + 1 in flight)
+    } else {
+      wait_vm<0>();
+    }
+  }
+  raw_barrier();
+  if (wr == 1) pp_barrier();  // the stagger
+  mfma_bf16x8 fa[4], fb[4];
+  for (int t = kt0; t < nk; ++t) {
+    const char* cs = smem + stage(t) * W_STAGE;
+    // phase 0: k 0..31, rows 0..63 of the wave tile; DMA step t + 1's A (its slots' last reader was
+    // phase 3 of step t - 1; step kt0 + 1 came with the prologue)
+    rd_b4(cs, 0, fb);
+    rd_a(cs, 0, 0, fa);
+    if (t > kt0 && t + 1 < nk) issue_a(t + 1);
+    pp_barrier();
+    pp_mma<0>(acc, fa, fb);
+    pp_barrier();
+    // phase 1: k 0..31, rows 64..127
+    rd_a(cs, 1, 0, fa);
+    pp_barrier();
+    pp_mma<1>(acc, fa, fb);
+    pp_barrier();
+    // phase 2: k 32..63, rows 0..63 (the last reads of this stage's B slots)
+    rd_b4(cs, 32, fb);
+    rd_a(cs, 0, 32, fa);
+    pp_barrier();
+    pp_mma<0>(acc, fa, fb);
+    pp_barrier();
+    // phase 3: k 32..63, rows 64..127; step t + 1 must have landed (read from the next phase on),
+    // then step t + 2's B goes into this stage's B slots
+    rd_a(cs, 1, 32, fa);
+    wait_vm<0>();
+    if (t + 2 < nk) issue_b(t + 2);
+    pp_barrier();
+    pp_mma<1>(acc, fa, fb);
+    pp_barrier();
+  }
+  if (wr == 0) pp_barrier();  // group 0 matches group 1's extra barrier
+  (void)lane;
+}
+
 // blockIdx.y = K split (ktiles_per_split K tiles each); split launches write fp32 slabs.
 template <class LA, class LB, int VAR>
 __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K,
@@ -1238,6 +1326,13 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
     for (int j = 0; j < 2; ++j) f[j] = wide_frag<LB>(st + b_off, b_row + 32 * qb + 16 * j, kk, lane);
   };
 
+  if constexpr (VAR == 4) {
+    wide_pp_loop(acc, smem, kt0, nk, wr, lane, issue_a, issue_b, rd_a,
+                 [&](const char* st, int kk, mfma_bf16x8 (&f)[4]) {
+#pragma unroll
+                   for (int j = 0; j < 4; ++j) f[j] = wide_frag<LB>(st + b_off, b_row + 16 * j, kk, lane);
+                 });
+  } else {
   mfma_bf16x8 fa0[4], fa1[4], fb0[2], fb1[2];
   if (kt0 < nk) {
     issue_a(kt0);
@@ -1276,6 +1371,7 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
       rd_b(ns, 0, 0, fb0);
     }
     wide_mma<0, 1, VAR>(acc, fa1, fb1);
+  }
   }
   __syncthreads();  // every wave is done with the operand stages before they become the staging tile
 
@@ -1921,7 +2017,12 @@ int wide_splits(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) 
   return wide_split_count(M, N, K);
 }
 
-int g_wide_variant = 3;  // setprio + MFMA/ds_read interleave: best or tied on every measured shape
+// main-loop schedule of the wide kernel: 3 = one barrier per K step, setprio + MFMA/ds_read
+// interleave; 4 = ping-pong wave groups (wide_pp_loop).  PDA_WIDE_VARIANT overrides.
+int g_wide_variant = [] {
+  const char* e = getenv("PDA_WIDE_VARIANT");
+  return e && e[0] >= '0' && e[0] <= '4' ? e[0] - '0' : 3;
+}();
 
 template <class LA, class LB, int VAR>
 hipError_t launch_wide_v(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, int splits,
@@ -1995,6 +2096,7 @@ hipError_t launch_wide(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t
     case 1: r = launch_wide_v<LA, LB, 1>(la, lb, M, N, K, e, splits, st); break;
     case 2: r = launch_wide_v<LA, LB, 2>(la, lb, M, N, K, e, splits, st); break;
     case 3: r = launch_wide_v<LA, LB, 3>(la, lb, M, N, K, e, splits, st); break;
+    case 4: r = launch_wide_v<LA, LB, 4>(la, lb, M, N, K, e, splits, st); break;
     default: r = launch_wide_v<LA, LB, 0>(la, lb, M, N, K, e, splits, st); break;
   }
   if (r != hipSuccess || splits <= 1) return r;

@@ -31,6 +31,9 @@ class ProcessRaisedException(RuntimeError):
 
 def _child(fn, rank: int, args: tuple, env: Dict[str, str], errq):
     os.environ.update(env)
+    import faulthandler
+
+    faulthandler.enable()  # a worker that dies on a signal leaves its Python stack on stderr
     try:
         fn(rank, *args)
     except KeyboardInterrupt:
