@@ -512,10 +512,11 @@ __device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else static_assert(N == 0 || N == 4 || N == 6 || N == 8, "add the literal");
+  else static_assert(N == 0 || N == 2 || N == 4 || N == 6 || N == 8, "add the literal");
 }
 
 __device__ __forceinline__ void raw_barrier() {
@@ -1274,6 +1275,86 @@ __device__ __forceinline__ void wide_pp_loop(f32x4 (&acc)[8][4], char* smem, int
   (void)lane;
 }
 
+// Ping-pong, quadrant order (VAR 5): phase p multiplies one 64 x 32 quadrant of the wave tile over
+// the whole 64-deep K step — (qa, qb) = (0,0) (0,1) (1,1) (1,0) — so A fragments are read twice per
+// step (8 each) and B twice (4 each; the (.,0) B fragments stay in registers for phase 3): 12 / 4 / 8 /
+// 0 ds_reads per phase and 64 fragment VGPRs.  B slots are last read in phase 1 and A slots in phase 2,
+// which spreads the DMA evenly — one half tile (2 DMAs per thread) per phase: phase 0 / 1 stage step
+// t + 1's A halves (into the other stage, free since phase 3 of step t - 1), phase 2 / 3 step t + 2's
+// B halves (into this stage).  Phase 3 waits (vmcnt(2): the B half issued in phase 2 may stay in flight)
+// for everything step t + 1 reads from its phase 0 on.
+template <int QA, int QB>
+__device__ __forceinline__ void pp_mma_q(f32x4 (&acc)[8][4], const mfma_bf16x8 (&fa)[8], const mfma_bf16x8 (&fb)[4]) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[4 * QA + i][2 * QB + j] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[2 * kk + j], fa[4 * kk + i], acc[4 * QA + i][2 * QB + j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+}
+
+template <bool DMA_FIRST, class IA0, class IA1, class IB0, class IB1, class RA, class RB>
+__device__ __forceinline__ void wide_pp_quad_loop(f32x4 (&acc)[8][4], char* smem, int kt0, int nk, int wr,
+                                                  IA0 issue_a0, IA1 issue_a1, IB0 issue_b0, IB1 issue_b1, RA rd_a8,
+                                                  RB rd_b4) {
+  if (kt0 < nk) {
+    issue_a0(kt0);
+    issue_a1(kt0);
+    issue_b0(kt0);
+    issue_b1(kt0);
+    if (kt0 + 1 < nk) {
+      issue_b0(kt0 + 1);
+      issue_b1(kt0 + 1);
+      wait_vm<4>();  // step kt0 landed; step kt0 + 1's B in flight (its A follows in phases 0 / 1)
+    } else {
+      wait_vm<0>();
+    }
+  }
+  raw_barrier();
+  if (wr == 1) pp_barrier();  // the stagger
+  mfma_bf16x8 fa[8], fb0[4], fb1[4];
+  for (int t = kt0; t < nk; ++t) {
+    const char* cs = smem + (t & 1) * W_STAGE;
+    const bool next = t + 1 < nk, next2 = t + 2 < nk;
+    // phase 0: quadrant (0, 0); step t + 1's A0 half
+    // (DMA_FIRST: each phase's DMA is issued before its fragment reads — no lgkmcnt wait ahead of the
+    // DMA, at the price of whatever wait the compiler puts before the reads)
+    if (DMA_FIRST && next) issue_a0(t + 1);
+    rd_b4(cs, 0, fb0);
+    rd_a8(cs, 0, fa);
+    if (!DMA_FIRST && next) issue_a0(t + 1);
+    pp_barrier();
+    pp_mma_q<0, 0>(acc, fa, fb0);
+    pp_barrier();
+    // phase 1: quadrant (0, 1) — the last B reads of this stage; step t + 1's A1 half
+    if (DMA_FIRST && next) issue_a1(t + 1);
+    rd_b4(cs, 1, fb1);
+    if (!DMA_FIRST && next) issue_a1(t + 1);
+    pp_barrier();
+    pp_mma_q<0, 1>(acc, fa, fb1);
+    pp_barrier();
+    // phase 2: quadrant (1, 1) — the last A reads; step t + 2's B0 half into this stage's B slots
+    if (DMA_FIRST && next2) issue_b0(t + 2);
+    rd_a8(cs, 1, fa);
+    if (!DMA_FIRST && next2) issue_b0(t + 2);
+    pp_barrier();
+    pp_mma_q<1, 1>(acc, fa, fb1);
+    pp_barrier();
+    // phase 3: quadrant (1, 0), no reads; step t + 1 complete (read from the next phase on), then B1
+    if (next2) wait_vm<2>();
+    else wait_vm<0>();
+    if (next2) issue_b1(t + 2);
+    pp_barrier();
+    pp_mma_q<1, 0>(acc, fa, fb0);
+    pp_barrier();
+  }
+  if (wr == 0) pp_barrier();
+}
+
 // blockIdx.y = K split (ktiles_per_split K tiles each); split launches write fp32 slabs.
 template <class LA, class LB, int VAR>
 __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K,
@@ -1326,7 +1407,26 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
     for (int j = 0; j < 2; ++j) f[j] = wide_frag<LB>(st + b_off, b_row + 32 * qb + 16 * j, kk, lane);
   };
 
-  if constexpr (VAR == 4) {
+  if constexpr (VAR == 5 || VAR == 6) {
+    auto half_issue = [&](const auto& ld, const auto& st, int t, int off) {
+      glds_tile(ld, st, (int64_t)t * BK, smem + (t & 1) * W_STAGE + off + grp * (W_HALF / 2), gwid);
+    };
+    wide_pp_quad_loop<VAR == 6>(
+        acc, smem, kt0, nk, wr, [&](int t) { half_issue(la, sa0, t, 0); }, [&](int t) { half_issue(la, sa1, t, W_HALF); },
+        [&](int t) { half_issue(lb, sb0, t, 2 * W_HALF); }, [&](int t) { half_issue(lb, sb1, t, 3 * W_HALF); },
+        [&](const char* st, int qa, mfma_bf16x8 (&f)[8]) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) f[4 * kk + i] = wide_frag<LA>(st + a_off, 64 * qa + 16 * i, 32 * kk, lane);
+        },
+        [&](const char* st, int qb, mfma_bf16x8 (&f)[4]) {
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) f[2 * kk + j] = wide_frag<LB>(st + b_off, b_row + 32 * qb + 16 * j, 32 * kk, lane);
+        });
+  } else if constexpr (VAR == 4) {
     wide_pp_loop(acc, smem, kt0, nk, wr, lane, issue_a, issue_b, rd_a,
                  [&](const char* st, int kk, mfma_bf16x8 (&f)[4]) {
 #pragma unroll
@@ -2021,7 +2121,7 @@ int wide_splits(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) 
 // interleave; 4 = ping-pong wave groups (wide_pp_loop).  PDA_WIDE_VARIANT overrides.
 int g_wide_variant = [] {
   const char* e = getenv("PDA_WIDE_VARIANT");
-  return e && e[0] >= '0' && e[0] <= '4' ? e[0] - '0' : 3;
+  return e && e[0] >= '0' && e[0] <= '6' ? e[0] - '0' : 3;
 }();
 
 template <class LA, class LB, int VAR>
@@ -2097,6 +2197,8 @@ hipError_t launch_wide(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t
     case 2: r = launch_wide_v<LA, LB, 2>(la, lb, M, N, K, e, splits, st); break;
     case 3: r = launch_wide_v<LA, LB, 3>(la, lb, M, N, K, e, splits, st); break;
     case 4: r = launch_wide_v<LA, LB, 4>(la, lb, M, N, K, e, splits, st); break;
+    case 5: r = launch_wide_v<LA, LB, 5>(la, lb, M, N, K, e, splits, st); break;
+    case 6: r = launch_wide_v<LA, LB, 6>(la, lb, M, N, K, e, splits, st); break;
     default: r = launch_wide_v<LA, LB, 0>(la, lb, M, N, K, e, splits, st); break;
   }
   if (r != hipSuccess || splits <= 1) return r;

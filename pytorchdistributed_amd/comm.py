@@ -71,7 +71,7 @@ class Work:
 class Communicator:
     """RCCL communicator over ``group`` (default: the world) on this rank's GPU."""
 
-    def __init__(self, group=None, device: Optional[torch.device] = None, high_priority: bool = True):
+    def __init__(self, group=None, device: Optional[torch.device] = None, high_priority: Optional[bool] = None):
         if not dist.is_initialized():
             raise RuntimeError("Communicator needs an initialised default process group (rendezvous / store)")
         self.group = group
@@ -80,6 +80,8 @@ class Communicator:
         self.rank = dist.get_rank(group)
         self.size = len(self.ranks)
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if high_priority is None:  # PDA_COMM_PRIORITY=normal: the comm stream at the default priority
+            high_priority = os.environ.get("PDA_COMM_PRIORITY", "high") != "normal"
         key_ranks = tuple(self.ranks)
         seq = _created.get(key_ranks, 0)
         _created[key_ranks] = seq + 1

@@ -708,8 +708,8 @@ def test_wide_persistent_matches_wide(case):
                                   (8, 57, 57, 128, 128, 3, 1, 1), (4, 14, 14, 256, 512, 3, 1, 1),
                                   (2, 7, 7, 512, 2048, 1, 1, 0), (3, 9, 13, 64, 256, 3, 2, 1)])
 def test_wide_pingpong_matches_wide(case):
-    """Ping-pong wide schedule (variant 4: the two wave groups alternate MFMA and load sections, slots
-    refilled as soon as their last reader is done) == the one-barrier-per-K-step schedule (variant 3),
+    """Ping-pong wide schedules (variants 4-6: the two wave groups alternate MFMA and load sections,
+    slots refilled as soon as their last reader is done) == the one-barrier-per-K-step schedule (3),
     bit for bit (same per-accumulator k order): conv fwd (+bias/relu, +BN sums), dgrad with the masked
     addend, wgrad through the split-K slabs (K ranges of 1..n K steps per split), and plain GEMMs whose
     K step count is 1, 2, 3 and odd."""
@@ -726,7 +726,7 @@ def test_wide_pingpong_matches_wide(case):
     gemms = [(torch.randn(M_, K_, device=DEV).to(torch.bfloat16), torch.randn(N_, K_, device=DEV).to(torch.bfloat16))
              for M_, N_, K_ in [(512, 256, 64), (300, 520, 128), (1000, 768, 192), (256, 512, 1000)]]
     res = []
-    for var in (3, 4):
+    for var in (3, 4, 5, 6):
         C().set_gemm_paths(2, var)
         try:
             table = torch.zeros(3, 2, Cout, device=DEV)
@@ -742,9 +742,10 @@ def test_wide_pingpong_matches_wide(case):
         finally:
             C().set_gemm_paths(-1, 3)
         res.append((outs, table.sum(0)))
-    for a, c in zip(res[0][0], res[1][0]):
-        assert torch.equal(a, c)
-    assert rel_err(res[1][1].cpu(), res[0][1].cpu()) < 1e-5
+    for r in res[1:]:
+        for a, c in zip(res[0][0], r[0]):
+            assert torch.equal(a, c)
+        assert rel_err(r[1].cpu(), res[0][1].cpu()) < 1e-5
 
 
 _WGRAD_BUDGET_SCRIPT = r"""

@@ -36,7 +36,7 @@ def t(fn, it=10):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="3,4")
+    ap.add_argument("--variants", default="3,4,5,6")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--convs", action="store_true")
     ap.add_argument("--no-gemm", action="store_true")
