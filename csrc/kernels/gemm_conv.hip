@@ -1160,7 +1160,8 @@ constexpr int W_SROW = 256 + 8;       // epilogue staging row (bf16 elements)
 constexpr int W_STATS_OFF = 2 * W_STAGE > 256 * W_SROW * 2 ? 2 * W_STAGE : 256 * W_SROW * 2;
 constexpr int W_LDS = W_STATS_OFF + (W_NT / 64) * 256 * 2 * 4;  // + epilogue BN-statistics scratch (16 KB)
 
-// VAR (schedule experiments, selected at run time): bit 0 = s_setprio(1) around each MFMA cluster,
+// VAR 3 (the one-barrier-per-K-step schedule; 4-6 are the ping-pong loops below): bit 0 = s_setprio(1)
+// around each MFMA cluster,
 // bit 1 = interleave each MFMA with one of the next phase's ds_reads (sched_group_barrier).
 template <int QA, int QB, int VAR>
 __device__ __forceinline__ void wide_mma(f32x4 (&acc)[8][4], const mfma_bf16x8 (&fa)[4], const mfma_bf16x8 (&fb)[2]) {
@@ -1577,237 +1578,6 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
   if (want_stats) epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + W_STATS_OFF), CPR, W_NT, tm, n0, N);
 }
 
-// ------------------------------------------------------------------ persistent wide-tile kernel
-// The wide kernel's schedule, but one workgroup per CU walks a strided list of 256 x 256 tiles and the
-// first K step of its NEXT tile is DMA'd into the free operand stage while the current tile's
-// epilogue runs.  Why: with one 512-thread workgroup per CU every CU is in the same phase — all main
-// loops, then all epilogues (profiles/r2_wide_epilogue_cost.md: on the output-heavy 1x1 convs the
-// epilogue costs as much as the main loop, 56^2 64->256 fwd 128 us vs 49 us without it), so the next
-// tile's load latency is paid in full after every epilogue.  Here it is hidden behind the epilogue's
-// LDS staging, statistics and stores.  The epilogue stages the tile in four 64-row slices (32 rows of
-// each wave row) through the operand stage the finished tile no longer reads (34 KB of its 64 KB), so
-// the stage being filled for the next tile is never touched; every barrier inside the epilogue is LDS-only (lgkmcnt + s_barrier:
-// a __syncthreads() would drain the in-flight DMA with vmcnt(0)).  Same loaders, LDS images and
-// fragment order as gemm_wide_kernel; bf16 output, no split-K (the launch gates).
-constexpr int P_SROWS = 64;  // staged rows per epilogue quarter
-constexpr int P_LDS = 2 * W_STAGE + (W_NT / 64) * 256 * 2 * 4;
-static_assert(P_SROWS * W_SROW * 2 <= W_STAGE, "an epilogue quarter fits one operand stage");
-
-template <class LA, class LB>
-__global__ void __launch_bounds__(W_NT, 1) gemm_wide_persist_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K,
-                                                                   int tiles_n, int ntiles, Epi epi) {
-  static_assert(LA::NCH == 2 && LB::NCH == 2, "64-row / 64-column loaders");
-  constexpr int VAR = 3;  // the wide kernel's production schedule (setprio + MFMA / ds_read interleave)
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int grp = tid >> 8, gtid = tid & 255, gwid = wid & 3;
-  const int wr = wid >> 2, wc = wid & 3;
-  const int ktiles = (int)((K + BK - 1) / BK);
-  const int tiles_m = ntiles / tiles_n;
-
-  int it = blockIdx.x;
-  if (it >= ntiles) return;
-  auto coords = [&](int idx, int& tm, int& tn) {
-    grouped_tile(xcd_remap(idx, ntiles), tiles_m, tiles_n, 8, tm, tn);
-  };
-  int tm, tn;
-  coords(it, tm, tn);
-
-  typename LA::State sa0, sa1;
-  typename LB::State sb0, sb1;
-  auto init_states = [&](int tm_, int tn_) {
-    const int64_t m0 = (int64_t)tm_ * 256, n0 = (int64_t)tn_ * 256;
-    la.init(sa0, m0 + 64 * grp, gtid);
-    la.init(sa1, m0 + 128 + 64 * grp, gtid);
-    lb.init(sb0, n0 + 64 * grp, gtid);
-    lb.init(sb1, n0 + 128 + 64 * grp, gtid);
-  };
-  auto issue_a = [&](int t, int stage) {
-    char* b = smem + stage * W_STAGE + grp * (W_HALF / 2);
-    glds_tile(la, sa0, (int64_t)t * BK, b, gwid);
-    glds_tile(la, sa1, (int64_t)t * BK, b + W_HALF, gwid);
-  };
-  auto issue_b = [&](int t, int stage) {
-    char* b = smem + stage * W_STAGE + 2 * W_HALF + grp * (W_HALF / 2);
-    glds_tile(lb, sb0, (int64_t)t * BK, b, gwid);
-    glds_tile(lb, sb1, (int64_t)t * BK, b + W_HALF, gwid);
-  };
-  const int a_off = wr * W_HALF, b_off = 2 * W_HALF + (wc >> 1) * W_HALF, b_row = (wc & 1) * 64;
-  auto rd_a = [&](const char* st, int qa, int kk, mfma_bf16x8 (&f)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) f[i] = wide_frag<LA>(st + a_off, 64 * qa + 16 * i, kk, lane);
-  };
-  auto rd_b = [&](const char* st, int qb, int kk, mfma_bf16x8 (&f)[2]) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) f[j] = wide_frag<LB>(st + b_off, b_row + 32 * qb + 16 * j, kk, lane);
-  };
-
-  init_states(tm, tn);
-  int cur = 0;  // operand stage of the K step about to run
-  if (ktiles > 0) {
-    issue_a(0, cur);
-    issue_b(0, cur);
-  }
-  f32x4 acc[8][4];
-  mfma_bf16x8 fa0[4], fa1[4], fb0[2], fb1[2];
-  for (;;) {
-    const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
-    const int next_it = it + gridDim.x;
-    const bool has_next = next_it < ntiles;
-    int ntm = 0, ntn = 0;
-    if (has_next) coords(next_it, ntm, ntn);
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // this tile's first stage (DMA'd during the previous tile's epilogue, or just above) has landed;
-    // the previous epilogue's stores drain here too (they are younger than the DMA in vmcnt order)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (ktiles > 0) {
-      rd_a(smem + cur * W_STAGE, 0, 0, fa0);
-      rd_b(smem + cur * W_STAGE, 0, 0, fb0);
-    }
-    for (int t = 0; t < ktiles; ++t) {
-      const char* cs = smem + cur * W_STAGE;
-      const bool more = t + 1 < ktiles;
-      const int nst = cur ^ 1;
-      if (!more && has_next) init_states(ntm, ntn);  // this tile issued its last loads one step ago
-      // k 0..31  (the next step's operands — this tile's, or the next tile's first — go to stage nst)
-      if (more) issue_a(t + 1, nst);
-      else if (has_next) issue_a(0, nst);
-      rd_b(cs, 1, 0, fb1);
-      wide_mma<0, 0, VAR>(acc, fa0, fb0);
-      if (more) issue_b(t + 1, nst);
-      else if (has_next) issue_b(0, nst);
-      rd_a(cs, 1, 0, fa1);
-      wide_mma<0, 1, VAR>(acc, fa0, fb1);
-      wide_mma<1, 1, VAR>(acc, fa1, fb1);
-      rd_a(cs, 1, 32, fa0);
-      rd_b(cs, 1, 32, fb1);
-      wide_mma<1, 0, VAR>(acc, fa1, fb0);
-      // k 32..63
-      rd_b(cs, 0, 32, fb0);
-      wide_mma<1, 1, VAR>(acc, fa0, fb1);
-      rd_a(cs, 0, 32, fa1);
-      wide_mma<1, 0, VAR>(acc, fa0, fb0);
-      wide_mma<0, 0, VAR>(acc, fa1, fb0);
-      if (more) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        rd_a(smem + nst * W_STAGE, 0, 0, fa0);
-        rd_b(smem + nst * W_STAGE, 0, 0, fb0);
-      }
-      wide_mma<0, 1, VAR>(acc, fa1, fb1);
-      cur = nst;
-    }
-    // every wave is done reading the last operand stage (cur ^ 1), which becomes the staging area;
-    // stage `cur` is being filled with the next tile's first K step — neither waited on here
-    raw_barrier();
-    bf16_t* stg = reinterpret_cast<bf16_t*>(smem + (cur ^ 1) * W_STAGE);
-    constexpr int CPR = 256 / 8;
-    const bool want_stats = epi.stats != nullptr;
-    // BN statistics: per quarter, each thread's column-chunk sums are folded over the wave's two row
-    // halves (lanes l, l + 32 share a chunk) and added into this wave's slot of `red` (one owner lane
-    // per slot, no atomics); after the last quarter the waves' slots are summed and flushed.  Keeping
-    // the running sums in LDS instead of registers leaves the accumulators room (no spills).
-    float* red = reinterpret_cast<float*>(smem + 2 * W_STAGE);
-#pragma unroll
-    for (int quarter = 0; quarter < 4; ++quarter) {
-      // accumulator blocks i in {2 quarter, 2 quarter + 1} of every wave: tile rows
-      // [wr 128 + 32 quarter, +32) land in staging rows [32 wr, +32).  Every wave retires a quarter of
-      // its accumulators per quarter, so the live set shrinks as the epilogue proceeds.
-      {
-#pragma unroll
-        for (int ii = 0; ii < 2; ++ii) {
-          const int i = 2 * quarter + ii;
-          const int r = 32 * wr + 16 * ii + (lane & 15);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int cc = wc * 64 + 16 * j + 4 * (lane >> 4);
-            f32x4 v = acc[i][j];
-            if (epi.bias) {
-              const int64_t n = n0 + cc;
-#pragma unroll
-              for (int q = 0; q < 4; ++q)
-                if (n + q < N)
-                  v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
-            }
-            if (epi.relu) {
-#pragma unroll
-              for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-            }
-            u16x4 o;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
-            *reinterpret_cast<u16x4*>(stg + r * W_SROW + cc) = o;
-          }
-        }
-      }
-      raw_barrier();
-      float st1[8], st2[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) st1[q] = st2[q] = 0.f;
-      // (not unrolled: the accumulators of later quarters are still live here — unrolling the four row
-      // chunks overlapped their loads and pushed the kernel past 256 VGPRs into scratch)
-#pragma unroll 1
-      for (int c = tid; c < P_SROWS * CPR; c += W_NT) {
-        const int r = c / CPR, ch = c % CPR;
-        const int64_t m = m0 + 128 * (r >> 5) + 32 * quarter + (r & 31), n = n0 + ch * 8;
-        if (m >= M || n >= N) continue;
-        const int64_t crow = epi_row(epi, m);
-        u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * W_SROW + ch * 8);
-        if (epi.addend) {
-          float a[8];
-          epi_addend8(epi, crow, n, a);
-#pragma unroll
-          for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
-        }
-        if (epi.act) epi_act8(epi, crow, n, v);
-        if (want_stats) {
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const float d = bf2f(v[q]) - epi.stats_shift[n + q];
-            st1[q] += d;
-            st2[q] = fmaf(d, d, st2[q]);
-          }
-        }
-        *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
-      }
-      if (want_stats) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          st1[q] += __shfl_xor(st1[q], 32, 64);
-          st2[q] += __shfl_xor(st2[q], 32, 64);
-        }
-        if (lane < CPR) {
-          float* slot = red + (wid * 256 + lane * 8) * 2;
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            slot[2 * q] = (quarter ? slot[2 * q] : 0.f) + st1[q];
-            slot[2 * q + 1] = (quarter ? slot[2 * q + 1] : 0.f) + st2[q];
-          }
-        }
-      }
-      raw_barrier();  // the staging rows are rewritten by the next quarter; `red` complete after the last
-    }
-    if (want_stats && tid < 256 && n0 + tid < N) {
-      float a = 0.f, b = 0.f;
-      for (int w = 0; w < W_NT / 64; ++w) {
-        a += red[(w * 256 + tid) * 2];
-        b += red[(w * 256 + tid) * 2 + 1];
-      }
-      float* row = epi.stats + (int64_t)(tm % epi.stats_rows) * 2 * N;
-      unsafeAtomicAdd(row + n0 + tid, a);
-      unsafeAtomicAdd(row + N + n0 + tid, b);
-    }
-    if (!has_next) break;
-    it = next_it;
-    tm = ntm;
-    tn = ntn;
-  }
-}
-
 // Split-K reduction: out[m, n] = act(sum_s slab[s, m, n] + bias[n]).  A workgroup is (256 / L) output
 // float4s x L split lanes; each lane keeps 8 slab loads in flight and the L partials meet in LDS, so
 // a small output with a deep split (conv wgrad of 64 x 64 with ~1000 slabs) still spreads over
@@ -2121,7 +1891,7 @@ int wide_splits(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) 
 // interleave; 4 = ping-pong wave groups (wide_pp_loop).  PDA_WIDE_VARIANT overrides.
 int g_wide_variant = [] {
   const char* e = getenv("PDA_WIDE_VARIANT");
-  return e && e[0] >= '0' && e[0] <= '6' ? e[0] - '0' : 3;
+  return e && e[0] >= '3' && e[0] <= '6' ? e[0] - '0' : 3;
 }();
 
 template <class LA, class LB, int VAR>
@@ -2141,49 +1911,11 @@ hipError_t launch_wide_v(const LA& la, const LB& lb, int64_t M, int64_t N, int64
   return hipGetLastError();
 }
 
-int g_wide_persist = -1;  // set_gemm_paths(): -1 = PDA_WIDE_PERSIST (default off), 0 off, 1 on
-
-bool wide_persist_on() {
-  static const int env = [] {
-    const char* e = getenv("PDA_WIDE_PERSIST");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return (g_wide_persist >= 0 ? g_wide_persist : env) == 1;
-}
-
-int cu_count() {
-  static const int n = [] {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-    return cus;
-  }();
-  return n;
-}
-
-template <class LA, class LB>
-hipError_t launch_wide_persist(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st) {
-  static bool attr = [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_wide_persist_kernel<LA, LB>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, P_LDS);
-    return true;
-  }();
-  (void)attr;
-  const int tiles_n = (int)((N + 255) / 256);
-  const int ntiles = (int)((M + 255) / 256) * tiles_n;
-  // one workgroup per CU; fewer tiles than CUs: one tile each (the plain wide kernel's grid)
-  const int grid = ntiles < cu_count() ? ntiles : cu_count();
-  gemm_wide_persist_kernel<LA, LB><<<grid, W_NT, P_LDS, st>>>(la, lb, M, N, K, tiles_n, ntiles, epi);
-  return hipGetLastError();
-}
-
 // splits > 1: epi.slab receives [splits][M][N] fp32 partials, reduced (with the caller's epilogue)
 // by splitk_reduce_kernel; the effective split count is recomputed from the per-split K tiles.
 template <class LA, class LB>
 hipError_t launch_wide(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st,
                        int splits = 1, float* slab = nullptr) {
-  if (splits <= 1 && !epi.c_f32 && !epi.slab && wide_persist_on()) return launch_wide_persist(la, lb, M, N, K, epi, st);
   Epi e = epi;
   if (splits > 1) {
     const int ktiles = (int)((K + BK - 1) / BK);
@@ -2193,13 +1925,10 @@ hipError_t launch_wide(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t
   if (splits > 1) e.slab = slab;
   hipError_t r;
   switch (g_wide_variant) {
-    case 1: r = launch_wide_v<LA, LB, 1>(la, lb, M, N, K, e, splits, st); break;
-    case 2: r = launch_wide_v<LA, LB, 2>(la, lb, M, N, K, e, splits, st); break;
-    case 3: r = launch_wide_v<LA, LB, 3>(la, lb, M, N, K, e, splits, st); break;
     case 4: r = launch_wide_v<LA, LB, 4>(la, lb, M, N, K, e, splits, st); break;
     case 5: r = launch_wide_v<LA, LB, 5>(la, lb, M, N, K, e, splits, st); break;
     case 6: r = launch_wide_v<LA, LB, 6>(la, lb, M, N, K, e, splits, st); break;
-    default: r = launch_wide_v<LA, LB, 0>(la, lb, M, N, K, e, splits, st); break;
+    default: r = launch_wide_v<LA, LB, 3>(la, lb, M, N, K, e, splits, st); break;
   }
   if (r != hipSuccess || splits <= 1) return r;
   int ll = 0;
@@ -2245,10 +1974,9 @@ bool dgrad_phased(int stride, int dil) { return stride == 1 || dil == 1; }
 
 }  // namespace
 
-void set_gemm_paths(int wide, int variant, int persist) {
+void set_gemm_paths(int wide, int variant) {
   g_wide_override = wide;
   if (variant >= 0) g_wide_variant = variant;
-  if (persist >= -1) g_wide_persist = persist;
 }
 
 // slab sizing covers both the 128-tile plan and the wide tile's (possibly deeper) split
