@@ -1,7 +1,7 @@
 // Native RCCL communicator (the reference reaches NCCL through
 // `init_process_group(backend="nccl")`, `02 DDP基本概念/ddp_gpus.py:20-22`, and torch's ProcessGroupNCCL).
 //
-// One communicator = one ncclComm_t over a group of ranks (one process per GPU) + one HIGH-priority
+// One communicator = one ncclComm_t over a group of ranks (one process per GPU) + one
 // HIP stream of its own.  Every collective is enqueued on that stream after an event-wait on the
 // streams that produced its input, and returns a Work handle: an event recorded behind the collective,
 // which a consumer stream waits on (hipStreamWaitEvent, no host blocking) or the host polls.  So
@@ -26,6 +26,8 @@
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "runtime.h"
 
@@ -83,16 +85,51 @@ struct DeviceGuard {
 
 }  // namespace
 
+// Recycled completion events (one hipEventCreate per collective showed up as host time on the
+// launch path); shared by a communicator and its outstanding Work handles.
+class EventPool {
+ public:
+  explicit EventPool(int device) : device_(device) {}
+  ~EventPool() {
+    for (hipEvent_t e : free_) (void)hipEventDestroy(e);
+  }
+  hipEvent_t get() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      if (!free_.empty()) {
+        hipEvent_t e = free_.back();
+        free_.pop_back();
+        return e;
+      }
+    }
+    DeviceGuard g(device_);
+    hipEvent_t e = nullptr;
+    check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    return e;
+  }
+  void put(hipEvent_t e) {
+    std::lock_guard<std::mutex> l(mu_);
+    free_.push_back(e);
+  }
+
+ private:
+  int device_;
+  std::mutex mu_;
+  std::vector<hipEvent_t> free_;
+};
+
 // Completion handle of one enqueued collective (or of a group of point-to-point ops).
 class Work {
  public:
-  Work(int device, hipStream_t s) : device_(device) {
+  Work(int device, hipStream_t s, std::shared_ptr<EventPool> pool) : device_(device), pool_(std::move(pool)) {
     DeviceGuard g(device_);
-    check_hip(hipEventCreateWithFlags(&ev_, hipEventDisableTiming), "hipEventCreate");
+    ev_ = pool_->get();
     check_hip(hipEventRecord(ev_, s), "hipEventRecord");
   }
   ~Work() {
-    if (ev_) (void)hipEventDestroy(ev_);
+    // a re-record of a recycled event only moves its completion point forward, so handing it out
+    // while the GPU has not reached it yet is harmless: nothing waits on this handle any more
+    if (ev_) pool_->put(ev_);
   }
   Work(const Work&) = delete;
   Work& operator=(const Work&) = delete;
@@ -112,6 +149,7 @@ class Work {
 
  private:
   int device_;
+  std::shared_ptr<EventPool> pool_;
   hipEvent_t ev_ = nullptr;
 };
 
@@ -125,7 +163,7 @@ std::set<Communicator*> g_live;
 class Communicator {
  public:
   Communicator(const std::string& uid, int nranks, int rank, int device, bool high_priority)
-      : nranks_(nranks), rank_(rank), device_(device) {
+      : nranks_(nranks), rank_(rank), device_(device), pool_(std::make_shared<EventPool>(device)) {
     if (uid.size() != sizeof(ncclUniqueId)) throw std::invalid_argument("communicator: bad unique id size");
     if (nranks < 1 || rank < 0 || rank >= nranks) throw std::invalid_argument("communicator: bad rank / size");
     ncclUniqueId id;
@@ -275,9 +313,10 @@ class Communicator {
   void live() const {
     if (aborted_) throw std::runtime_error("communicator was aborted (collective timeout / abort())");
   }
-  std::shared_ptr<Work> done() { return std::make_shared<Work>(device_, stream_); }
+  std::shared_ptr<Work> done() { return std::make_shared<Work>(device_, stream_, pool_); }
 
   int nranks_, rank_, device_;
+  std::shared_ptr<EventPool> pool_;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
   hipEvent_t dep_ = nullptr;

@@ -1160,8 +1160,7 @@ constexpr int W_SROW = 256 + 8;       // epilogue staging row (bf16 elements)
 constexpr int W_STATS_OFF = 2 * W_STAGE > 256 * W_SROW * 2 ? 2 * W_STAGE : 256 * W_SROW * 2;
 constexpr int W_LDS = W_STATS_OFF + (W_NT / 64) * 256 * 2 * 4;  // + epilogue BN-statistics scratch (16 KB)
 
-// VAR 3 (the one-barrier-per-K-step schedule; 4-6 are the ping-pong loops below): bit 0 = s_setprio(1)
-// around each MFMA cluster,
+// VAR (schedule bits; production = 3): bit 0 = s_setprio(1) around each MFMA cluster,
 // bit 1 = interleave each MFMA with one of the next phase's ds_reads (sched_group_barrier).
 template <int QA, int QB, int VAR>
 __device__ __forceinline__ void wide_mma(f32x4 (&acc)[8][4], const mfma_bf16x8 (&fa)[4], const mfma_bf16x8 (&fb)[2]) {
@@ -1186,174 +1185,6 @@ template <class L>
 __device__ __forceinline__ mfma_bf16x8 wide_frag(const char* half, int row, int kk, int lane) {
   if constexpr (L::kMajor) return read_frag<true, 128>(half, row, kk, lane);
   else return read_frag<false, 64>(half + (row >> 6) * (W_HALF / 2), row & 63, kk, lane);
-}
-
-// Ping-pong main loop (VAR 4).  The two 4-wave halves of the workgroup (wr = 0 / 1; waves w and w + 4
-// share a SIMD) run half a phase apart: group 1 takes one extra barrier up front, so every barrier
-// pairs one group's "operands ready, start multiplying" with the other's "done multiplying", and on
-// each SIMD one wave issues its 16 MFMAs while the other reads the next phase's fragments and issues
-// DMA.  The MFMA pipe never waits for a wave's own fragment reads, which is what bounded the
-// one-barrier-per-K-step schedule (every wave reading, then every wave multiplying).
-// A K step is 4 phases of 16 MFMAs, phase p = (k half p >> 1) x (64-row quarter qa = p & 1) of the
-// wave's 128 x 64 tile; fragments: A 4 (one quarter, one k half), B 4 (all 64 columns, one k half) —
-// 32 VGPRs, read just in time (8 / 4 / 8 / 4 ds_reads).  LDS is the same two 64 KB stages, refilled
-// a slot at a time as soon as its last reader is done: B slots of stage t & 1 are last read in phase
-// 2 of K step t, so K step t + 2's B is DMA'd in phase 3; A slots are last read in phase 3, so K step
-// t + 1's A is DMA'd in phase 0 of step t (after step t - 1's last read).  Every DMA is retired by the
-// vmcnt(0) in phase 3 of the step before its readers' step (phase 3 then holds no DMA of its own yet:
-// it waits, then issues), and read one phase after that wait — the wait precedes the phase's first
-// barrier and each group's next read follows one barrier later.  Reads retire (lgkmcnt(0)) before the
-// barrier that ends their load section, so a slot DMA'd one phase after its last read is never
-// overwritten under a reader.  sched_barrier(0) pins the MFMAs between their two barriers.
-__device__ __forceinline__ void pp_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int QA>
-__device__ __forceinline__ void pp_mma(f32x4 (&acc)[8][4], const mfma_bf16x8 (&fa)[4], const mfma_bf16x8 (&fb)[4]) {
-  __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      acc[4 * QA + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[4 * QA + i][j], 0, 0, 0);
-  __builtin_amdgcn_s_setprio(0);
-}
-
-template <class IA, class IB, class RA, class RB>
-__device__ __forceinline__ void wide_pp_loop(f32x4 (&acc)[8][4], char* smem, int kt0, int nk, int wr, int lane,
-                                             IA issue_a, IB issue_b, RA rd_a, RB rd_b4) {
-  auto stage = [&](int t) { return t & 1; };
-  if (kt0 < nk) {
-    issue_a(kt0);
-    issue_b(kt0);
-    if (kt0 + 1 < nk) {
-      issue_a(kt0 + 1);
-      issue_b(kt0 + 1);
-      wait_vm<8>();  // K step kt0 landed (per thread: 4 half tiles x 2 DMAs of step kt0 + 1 in flight)
-    } else {
-      wait_vm<0>();
-    }
-  }
-  raw_barrier();
-  if (wr == 1) pp_barrier();  // the stagger
-  mfma_bf16x8 fa[4], fb[4];
-  for (int t = kt0; t < nk; ++t) {
-    const char* cs = smem + stage(t) * W_STAGE;
-    // phase 0: k 0..31, rows 0..63 of the wave tile; DMA step t + 1's A (its slots' last reader was
-    // phase 3 of step t - 1; step kt0 + 1 came with the prologue)
-    rd_b4(cs, 0, fb);
-    rd_a(cs, 0, 0, fa);
-    if (t > kt0 && t + 1 < nk) issue_a(t + 1);
-    pp_barrier();
-    pp_mma<0>(acc, fa, fb);
-    pp_barrier();
-    // phase 1: k 0..31, rows 64..127
-    rd_a(cs, 1, 0, fa);
-    pp_barrier();
-    pp_mma<1>(acc, fa, fb);
-    pp_barrier();
-    // phase 2: k 32..63, rows 0..63 (the last reads of this stage's B slots)
-    rd_b4(cs, 32, fb);
-    rd_a(cs, 0, 32, fa);
-    pp_barrier();
-    pp_mma<0>(acc, fa, fb);
-    pp_barrier();
-    // phase 3: k 32..63, rows 64..127; step t + 1 must have landed (read from the next phase on),
-    // then step t + 2's B goes into this stage's B slots
-    rd_a(cs, 1, 32, fa);
-    wait_vm<0>();
-    if (t + 2 < nk) issue_b(t + 2);
-    pp_barrier();
-    pp_mma<1>(acc, fa, fb);
-    pp_barrier();
-  }
-  if (wr == 0) pp_barrier();  // group 0 matches group 1's extra barrier
-  (void)lane;
-}
-
-// Ping-pong, quadrant order (VAR 5): phase p multiplies one 64 x 32 quadrant of the wave tile over
-// the whole 64-deep K step — (qa, qb) = (0,0) (0,1) (1,1) (1,0) — so A fragments are read twice per
-// step (8 each) and B twice (4 each; the (.,0) B fragments stay in registers for phase 3): 12 / 4 / 8 /
-// 0 ds_reads per phase and 64 fragment VGPRs.  B slots are last read in phase 1 and A slots in phase 2,
-// which spreads the DMA evenly — one half tile (2 DMAs per thread) per phase: phase 0 / 1 stage step
-// t + 1's A halves (into the other stage, free since phase 3 of step t - 1), phase 2 / 3 step t + 2's
-// B halves (into this stage).  Phase 3 waits (vmcnt(2): the B half issued in phase 2 may stay in flight)
-// for everything step t + 1 reads from its phase 0 on.
-template <int QA, int QB>
-__device__ __forceinline__ void pp_mma_q(f32x4 (&acc)[8][4], const mfma_bf16x8 (&fa)[8], const mfma_bf16x8 (&fb)[4]) {
-  __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[4 * QA + i][2 * QB + j] =
-            __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[2 * kk + j], fa[4 * kk + i], acc[4 * QA + i][2 * QB + j], 0, 0, 0);
-  __builtin_amdgcn_s_setprio(0);
-}
-
-template <bool DMA_FIRST, class IA0, class IA1, class IB0, class IB1, class RA, class RB>
-__device__ __forceinline__ void wide_pp_quad_loop(f32x4 (&acc)[8][4], char* smem, int kt0, int nk, int wr,
-                                                  IA0 issue_a0, IA1 issue_a1, IB0 issue_b0, IB1 issue_b1, RA rd_a8,
-                                                  RB rd_b4) {
-  if (kt0 < nk) {
-    issue_a0(kt0);
-    issue_a1(kt0);
-    issue_b0(kt0);
-    issue_b1(kt0);
-    if (kt0 + 1 < nk) {
-      issue_b0(kt0 + 1);
-      issue_b1(kt0 + 1);
-      wait_vm<4>();  // step kt0 landed; step kt0 + 1's B in flight (its A follows in phases 0 / 1)
-    } else {
-      wait_vm<0>();
-    }
-  }
-  raw_barrier();
-  if (wr == 1) pp_barrier();  // the stagger
-  mfma_bf16x8 fa[8], fb0[4], fb1[4];
-  for (int t = kt0; t < nk; ++t) {
-    const char* cs = smem + (t & 1) * W_STAGE;
-    const bool next = t + 1 < nk, next2 = t + 2 < nk;
-    // phase 0: quadrant (0, 0); step t + 1's A0 half
-    // (DMA_FIRST: each phase's DMA is issued before its fragment reads — no lgkmcnt wait ahead of the
-    // DMA, at the price of whatever wait the compiler puts before the reads)
-    if (DMA_FIRST && next) issue_a0(t + 1);
-    rd_b4(cs, 0, fb0);
-    rd_a8(cs, 0, fa);
-    if (!DMA_FIRST && next) issue_a0(t + 1);
-    pp_barrier();
-    pp_mma_q<0, 0>(acc, fa, fb0);
-    pp_barrier();
-    // phase 1: quadrant (0, 1) — the last B reads of this stage; step t + 1's A1 half
-    if (DMA_FIRST && next) issue_a1(t + 1);
-    rd_b4(cs, 1, fb1);
-    if (!DMA_FIRST && next) issue_a1(t + 1);
-    pp_barrier();
-    pp_mma_q<0, 1>(acc, fa, fb1);
-    pp_barrier();
-    // phase 2: quadrant (1, 1) — the last A reads; step t + 2's B0 half into this stage's B slots
-    if (DMA_FIRST && next2) issue_b0(t + 2);
-    rd_a8(cs, 1, fa);
-    if (!DMA_FIRST && next2) issue_b0(t + 2);
-    pp_barrier();
-    pp_mma_q<1, 1>(acc, fa, fb1);
-    pp_barrier();
-    // phase 3: quadrant (1, 0), no reads; step t + 1 complete (read from the next phase on), then B1
-    if (next2) wait_vm<2>();
-    else wait_vm<0>();
-    if (next2) issue_b1(t + 2);
-    pp_barrier();
-    pp_mma_q<1, 0>(acc, fa, fb0);
-    pp_barrier();
-  }
-  if (wr == 0) pp_barrier();
 }
 
 // blockIdx.y = K split (ktiles_per_split K tiles each); split launches write fp32 slabs.
@@ -1408,32 +1239,7 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
     for (int j = 0; j < 2; ++j) f[j] = wide_frag<LB>(st + b_off, b_row + 32 * qb + 16 * j, kk, lane);
   };
 
-  if constexpr (VAR == 5 || VAR == 6) {
-    auto half_issue = [&](const auto& ld, const auto& st, int t, int off) {
-      glds_tile(ld, st, (int64_t)t * BK, smem + (t & 1) * W_STAGE + off + grp * (W_HALF / 2), gwid);
-    };
-    wide_pp_quad_loop<VAR == 6>(
-        acc, smem, kt0, nk, wr, [&](int t) { half_issue(la, sa0, t, 0); }, [&](int t) { half_issue(la, sa1, t, W_HALF); },
-        [&](int t) { half_issue(lb, sb0, t, 2 * W_HALF); }, [&](int t) { half_issue(lb, sb1, t, 3 * W_HALF); },
-        [&](const char* st, int qa, mfma_bf16x8 (&f)[8]) {
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) f[4 * kk + i] = wide_frag<LA>(st + a_off, 64 * qa + 16 * i, 32 * kk, lane);
-        },
-        [&](const char* st, int qb, mfma_bf16x8 (&f)[4]) {
-#pragma unroll
-          for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) f[2 * kk + j] = wide_frag<LB>(st + b_off, b_row + 32 * qb + 16 * j, 32 * kk, lane);
-        });
-  } else if constexpr (VAR == 4) {
-    wide_pp_loop(acc, smem, kt0, nk, wr, lane, issue_a, issue_b, rd_a,
-                 [&](const char* st, int kk, mfma_bf16x8 (&f)[4]) {
-#pragma unroll
-                   for (int j = 0; j < 4; ++j) f[j] = wide_frag<LB>(st + b_off, b_row + 16 * j, kk, lane);
-                 });
-  } else {
+  {
   mfma_bf16x8 fa0[4], fa1[4], fb0[2], fb1[2];
   if (kt0 < nk) {
     issue_a(kt0);
@@ -1887,12 +1693,7 @@ int wide_splits(int64_t M, int64_t N, int64_t K, const Plan& p, const Epi& epi) 
   return wide_split_count(M, N, K);
 }
 
-// main-loop schedule of the wide kernel: 3 = one barrier per K step, setprio + MFMA/ds_read
-// interleave; 4 = ping-pong wave groups (wide_pp_loop).  PDA_WIDE_VARIANT overrides.
-int g_wide_variant = [] {
-  const char* e = getenv("PDA_WIDE_VARIANT");
-  return e && e[0] >= '3' && e[0] <= '6' ? e[0] - '0' : 3;
-}();
+
 
 template <class LA, class LB, int VAR>
 hipError_t launch_wide_v(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, int splits,
@@ -1923,13 +1724,7 @@ hipError_t launch_wide(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t
     splits = (ktiles + kps - 1) / kps;
   }
   if (splits > 1) e.slab = slab;
-  hipError_t r;
-  switch (g_wide_variant) {
-    case 4: r = launch_wide_v<LA, LB, 4>(la, lb, M, N, K, e, splits, st); break;
-    case 5: r = launch_wide_v<LA, LB, 5>(la, lb, M, N, K, e, splits, st); break;
-    case 6: r = launch_wide_v<LA, LB, 6>(la, lb, M, N, K, e, splits, st); break;
-    default: r = launch_wide_v<LA, LB, 3>(la, lb, M, N, K, e, splits, st); break;
-  }
+  const hipError_t r = launch_wide_v<LA, LB, 3>(la, lb, M, N, K, e, splits, st);
   if (r != hipSuccess || splits <= 1) return r;
   int ll = 0;
   while (ll < 4 && (splits >> ll) > 16) ++ll;
@@ -1974,10 +1769,9 @@ bool dgrad_phased(int stride, int dil) { return stride == 1 || dil == 1; }
 
 }  // namespace
 
-void set_gemm_paths(int wide, int variant) {
-  g_wide_override = wide;
-  if (variant >= 0) g_wide_variant = variant;
-}
+// (ping-pong schedules of the wide kernel — the two wave groups alternating MFMA and load sections —
+// measured slower on every plain GEMM and most convs: profiles/r3_wide_pingpong_DROPPED.jsonl)
+void set_gemm_paths(int wide) { g_wide_override = wide; }
 
 // slab sizing covers both the 128-tile plan and the wide tile's (possibly deeper) split
 int64_t split_slab_floats(int64_t M, int64_t N, int64_t K, const Plan& p) {

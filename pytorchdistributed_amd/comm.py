@@ -1,9 +1,10 @@
 """Native RCCL communicator (reference `init_process_group(backend="nccl")` at
 `02 DDP基本概念/ddp_gpus.py:20-22`, which torch serves with ProcessGroupNCCL).
 
-:class:`Communicator` owns an ``ncclComm_t`` over a process group and a high-priority HIP stream of
-its own (`csrc/comm/communicator.cpp`).  A collective is enqueued on that stream after an event-wait
-on the streams that produce its input and returns a :class:`Work`: ``wait()`` orders the current
+:class:`Communicator` owns an ``ncclComm_t`` over a process group and a HIP stream of its own
+(`csrc/comm/communicator.cpp`; default priority, ``PDA_COMM_PRIORITY=high`` for a high-priority
+one).  A collective is enqueued on that stream after an event-wait on the streams that produce its
+input and returns a :class:`Work`: ``wait()`` orders the current
 stream after the collective without blocking the host, ``is_completed()`` polls.  The bootstrap is
 the framework's own: group rank 0 calls ``ncclGetUniqueId`` and publishes the id in the rendezvous
 store (the native C++ store when the framework launched the job, the launcher's otherwise), every
@@ -80,8 +81,10 @@ class Communicator:
         self.rank = dist.get_rank(group)
         self.size = len(self.ranks)
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-        if high_priority is None:  # PDA_COMM_PRIORITY=normal: the comm stream at the default priority
-            high_priority = os.environ.get("PDA_COMM_PRIORITY", "high") != "normal"
+        if high_priority is None:
+            # default priority: a high-priority comm stream cost the one-rank headline step 0.6 %
+            # against the default (profiles/r3_comm_priority_ab.jsonl); PDA_COMM_PRIORITY=high
+            high_priority = os.environ.get("PDA_COMM_PRIORITY", "normal") == "high"
         key_ranks = tuple(self.ranks)
         seq = _created.get(key_ranks, 0)
         _created[key_ranks] = seq + 1

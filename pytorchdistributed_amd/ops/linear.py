@@ -6,9 +6,10 @@ K-major x MN-major, wgrad MN-major x MN-major via LDS transpose reads, split-K w
 small).  GPU otherwise (fp32 models, odd widths): the general-stride SIMT GEMM kernel.
 
 Plain (epilogue-free) large GEMMs go to the vendor library (hipBLASLt through ``torch.mm``) under
-``PDA_GEMM=auto`` (default): on the 4096^3 bf16 probe it runs 1.47 PF/s against 0.67 PF/s for the
-native 128x128 MFMA tile (profiles/r1_conv_gemm_microbench.md), and a plain GEMM is exactly the case
-the library is tuned for.  Fused cases (ReLU epilogue) and everything else stay native;
+``PDA_GEMM=auto`` (default): on 4096^3 bf16 it runs 1.48 PF/s against 1.13 PF/s for the native
+256x256 wide tile, and 1.22-1.49 vs 1.06-1.15 PF/s on the GPT-2-medium GEMM shapes (interleaved
+same-box rounds, profiles/r3_wide_pingpong_DROPPED.jsonl, whose ping-pong schedules were slower
+still); a plain GEMM is exactly the case the library is tuned for.  Fused cases (ReLU epilogue) and everything else stay native;
 ``PDA_GEMM=native`` forces the native kernel everywhere, ``PDA_GEMM=blas`` the library.
 """
 from __future__ import annotations

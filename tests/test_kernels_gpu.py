@@ -670,50 +670,6 @@ def test_conv_dgrad_masked_addend_paths(case, wide):
     assert rel_err(dx.cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("case", [(16, 56, 56, 64, 256, 1, 1, 0), (16, 56, 56, 256, 64, 1, 1, 0),
-                                  (8, 57, 57, 128, 128, 3, 1, 1), (4, 14, 14, 256, 512, 3, 1, 1),
-                                  (2, 7, 7, 512, 2048, 1, 1, 0), (3, 9, 13, 64, 256, 3, 2, 1)])
-def test_wide_pingpong_matches_wide(case):
-    """Ping-pong wide schedules (variants 4-6: the two wave groups alternate MFMA and load sections,
-    slots refilled as soon as their last reader is done) == the one-barrier-per-K-step schedule (3),
-    bit for bit (same per-accumulator k order): conv fwd (+bias/relu, +BN sums), dgrad with the masked
-    addend, wgrad through the split-K slabs (K ranges of 1..n K steps per split), and plain GEMMs whose
-    K step count is 1, 2, 3 and odd."""
-    N, H, W, Cin, Cout, k, s, p = case
-    torch.manual_seed(9)
-    x = torch.randn(N, H, W, Cin).to(torch.bfloat16).to(DEV)
-    w = (torch.randn(Cout, k, k, Cin) / math.sqrt(Cin * k * k)).to(torch.bfloat16).to(DEV)
-    b = torch.randn(Cout, device=DEV)
-    shift = torch.randn(Cout, device=DEV) * 0.1
-    P, Q = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-    dy = torch.randn(N, P, Q, Cout).to(torch.bfloat16).to(DEV)
-    add = torch.randn(N, H, W, Cin).to(torch.bfloat16).to(DEV)
-    bits = torch.randint(0, 256, (N * H * W * Cin // 8,), dtype=torch.uint8, device=DEV)
-    gemms = [(torch.randn(M_, K_, device=DEV).to(torch.bfloat16), torch.randn(N_, K_, device=DEV).to(torch.bfloat16))
-             for M_, N_, K_ in [(512, 256, 64), (300, 520, 128), (1000, 768, 192), (256, 512, 1000)]]
-    res = []
-    for var in (3, 4, 5, 6):
-        C().set_gemm_paths(2, var)
-        try:
-            table = torch.zeros(3, 2, Cout, device=DEV)
-            outs = [C().conv_fwd_stats(x, w, s, p, 1, shift, table), C().conv_fwd(x, w, s, p, 1, b, True),
-                    C().conv_dgrad(dy, w, H, W, s, p, 1, add, bits),
-                    C().conv_wgrad(dy, x, k, k, s, p, 1, True, None)]
-            for A_, B_ in gemms:
-                (M_, K_), N_ = A_.shape, B_.shape[0]
-                o = torch.empty(M_, N_, device=DEV, dtype=torch.bfloat16)
-                C().gemm(A_, True, K_, B_, True, K_, o, N_, M_, N_, K_, None, False, False)
-                outs.append(o)
-            torch.cuda.synchronize()
-        finally:
-            C().set_gemm_paths(-1, 3)
-        res.append((outs, table.sum(0)))
-    for r in res[1:]:
-        for a, c in zip(res[0][0], r[0]):
-            assert torch.equal(a, c)
-        assert rel_err(r[1].cpu(), res[0][1].cpu()) < 1e-5
-
-
 _WGRAD_BUDGET_SCRIPT = r"""
 import math, torch, torch.nn.functional as F
 from pytorchdistributed_amd._native import C
