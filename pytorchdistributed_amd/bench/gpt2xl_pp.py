@@ -63,6 +63,7 @@ def main(argv=None):
         # micro-batch's backward (overlapped with it and the drain); flat buffers -> one AdamW launch
         ddp = DistributedDataParallel(mod, device_ids=[device.index] if device.type == "cuda" else None,
                                       process_group=dp_group)
+        ddp.track_comm = True  # the JSON reports the DP all-reduce time the step could not hide
         pipe = Pipeline(mod, ranks, a.micro, schedule=a.schedule, loss_fn=mod.loss if stage == pp - 1 else None,
                         group=pp_group, device=device, dp_module=ddp)
     opt = AdamW(mod.parameters(), lr=1e-4, weight_decay=0.1)
