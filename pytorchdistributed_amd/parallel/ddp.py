@@ -334,21 +334,28 @@ class DistributedDataParallel(tnn.Module):
             task = torch._C._current_graph_task_id()
             if not self._callback_queued or self._callback_task != task:
                 if self._callback_queued:
-                    # the previous backward raised before its final callback ran: start this pass clean
-                    # (its side-stream weight gradients were never joined either)
-                    if p.is_cuda:
-                        _streams.join(p.device)
-                    self._works.clear()
-                    self._sweep_tickets(force=True)
-                    for grp in self.groups.values():
-                        grp.pending_comm = 0
-                    self.reducer.prepare()
+                    self._drain_aborted()
                 self._callback_queued = True
                 self._callback_task = task
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
             for b in self.reducer.mark_ready(i):
                 self._launch(b)
         return hook
+
+    def _drain_aborted(self):
+        """The previous backward raised before its final callback ran: finish what it left in flight
+        (bucket collectives still writing into the gradient buffers, side-stream weight gradients) and
+        start clean.  Runs at the next forward / zero_grad, or at the first hook of the next backward."""
+        if self._params and self._params[0].is_cuda:
+            _streams.join(self._params[0].device)
+        for work, _ in self._works:
+            work.wait()  # its result is stale, but it must not land in the buffers after this point
+        self._works.clear()
+        self._sweep_tickets(force=True)
+        for grp in self.groups.values():
+            grp.pending_comm = 0
+        self.reducer.prepare()
+        self._callback_queued = False
 
     def _finalize(self):
         self._callback_queued = False
@@ -422,6 +429,8 @@ class DistributedDataParallel(tnn.Module):
             self.xgmi.check(sync=False)
 
     def forward(self, *args, **kwargs):
+        if self._callback_queued and torch._C._current_graph_task_id() == -1:
+            self._drain_aborted()
         self._check_xgmi()
         if self._tickets:
             self._sweep_tickets()
@@ -442,6 +451,8 @@ class DistributedDataParallel(tnn.Module):
             self.require_backward_grad_sync = old
 
     def zero_grad(self, set_to_none: bool = True):
+        if self._callback_queued and torch._C._current_graph_task_id() == -1:
+            self._drain_aborted()
         for g in self.groups.values():
             g.zero_grad()
 

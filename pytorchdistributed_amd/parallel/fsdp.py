@@ -357,6 +357,9 @@ class FullyShardedDataParallel(tnn.Module):
         if self._callback_queued and self._callback_task == task:
             return
         if self._callback_queued:  # aborted pass: drop its partial arrivals / pending reduce-scatters
+            for _, work, _ in self._pending_rs:  # (their outputs are discarded, but let them finish first)
+                if work is not None:
+                    work.wait()
             self._pending_rs = []
             _join_side_streams(self.units)
             for u in self.units:
