@@ -1554,9 +1554,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm);
   m.def("gemm_act", &gemm_act);
   m.def("set_gemm_paths", &pda::set_gemm_paths,
-        "force a GEMM kernel path: wide=-1 env default, 0 off, 1 auto, 2 force; epi_direct (wide-tile bf16 "
-        "epilogue from registers): -2 keep, -1 env PDA_WIDE_EPI_DIRECT, 0 staged, 1 direct",
-        pybind11::arg("wide"), pybind11::arg("epi_direct") = -2);
+        "force a GEMM kernel path: wide=-1 env default, 0 off, 1 auto, 2 force", pybind11::arg("wide"));
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("bias") = py::none(), py::arg("relu") = false, py::arg("out_f32") = false);
   m.def("split_bf16", &split_bf16, py::arg("x"), py::arg("nseg"), py::arg("lo_mask"), py::arg("stack"));

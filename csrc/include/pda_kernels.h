@@ -187,7 +187,7 @@ hipError_t fill_randint(int64_t* out, int64_t n, uint64_t seed, uint64_t offset,
 // ---- gemm_conv.hip
 // path override for the GEMM family: wide = -1 env default (PDA_GEMM_WIDE), 0 off, 1 heuristic, 2 force;
 // variant >= 0 selects a wide-kernel schedule variant (bit 0 setprio, bit 1 MFMA/ds_read interleave)
-void set_gemm_paths(int wide, int epi_direct = -2);  // epi_direct: -2 keep, -1 env, 0/1
+void set_gemm_paths(int wide);
 int64_t gemm_slab_floats(int64_t M, int64_t N, int64_t K, bool allow_split);
 hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
                      void* C, bool c_f32, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,

@@ -429,9 +429,6 @@ struct Epi {
   // with the activation backward: no separate elementwise pass over two [tokens, 4d] tensors)
   int act;
   bf16_t* act_aux;
-  // wide kernel only: write the bf16 tile straight from the accumulators (8-byte stores, BN sums
-  // folded across lanes with shuffles) instead of staging it through LDS; set by launch_wide
-  int direct;
 };
 
 __device__ __forceinline__ void epi_act8(const Epi& e, int64_t crow, int64_t n, u16x8& v) {
@@ -1322,97 +1319,6 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
     return;
   }
 
-  if (epi.direct) {
-    // register-direct epilogue: each lane stores its 4-column runs (a wave's four j blocks make one
-    // 128-B row segment, merged in L2), no LDS round trip.  Rounding matches the staged path (bias /
-    // relu in fp32 -> bf16, then + addend -> bf16).  BN sums: a lane's 8 rows in registers, the 16
-    // lanes of a column group by shuffles, the two wave rows through LDS, one atomic per column.
-    const bool want_stats = epi.stats != nullptr;
-    float st1[4][4], st2[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) st1[j][r] = st2[j][r] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int64_t m = m0 + wr * 128 + 16 * i + (lane & 15);
-      if (m >= M) continue;
-      const int64_t crow = epi_row(epi, m);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
-        if (n >= N) continue;
-        f32x4 v = acc[i][j];
-        if (epi.bias) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
-        }
-        if (epi.relu) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-        }
-        u16x4 o;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
-        if (epi.addend) {
-          float a[4];
-          epi_addend4(epi, crow, n, a);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) o[q] = f2bf(bf2f(o[q]) + a[q]);
-        }
-        if (want_stats) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float d = bf2f(o[q]) - epi.stats_shift[n + q];
-            st1[j][q] += d;
-            st2[j][q] = fmaf(d, d, st2[j][q]);
-          }
-        }
-        *reinterpret_cast<u16x4*>((bf16_t*)epi.C + crow * epi.ldc + n) = o;
-      }
-    }
-    if (want_stats) {
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            st1[j][q] += __shfl_xor(st1[j][q], off, 64);
-            st2[j][q] += __shfl_xor(st2[j][q], off, 64);
-          }
-      // lanes 0, 16, 32, 48 hold their wave's sums for columns wc*64 + 16 j + 4 (lane >> 4) + q
-      float* red = reinterpret_cast<float*>(smem + W_STATS_OFF);  // [256 columns][2]
-      const bool owner = (lane & 15) == 0;
-      if (wr == 1 && owner) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int col = wc * 64 + 16 * j + 4 * (lane >> 4) + q;
-            red[2 * col] = st1[j][q];
-            red[2 * col + 1] = st2[j][q];
-          }
-      }
-      raw_barrier();
-      if (wr == 0 && owner) {
-        float* row = epi.stats + (int64_t)(tm % epi.stats_rows) * 2 * N;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int col = wc * 64 + 16 * j + 4 * (lane >> 4) + q;
-            if (n0 + col < N) {
-              unsafeAtomicAdd(row + n0 + col, st1[j][q] + red[2 * col]);
-              unsafeAtomicAdd(row + N + n0 + col, st2[j][q] + red[2 * col + 1]);
-            }
-          }
-      }
-    }
-    return;
-  }
-
   // epilogue (bf16 output): bias / relu in registers, stage through LDS, coalesced 16-B row stores
   bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
 #pragma unroll
@@ -1806,24 +1712,12 @@ hipError_t launch_wide_v(const LA& la, const LB& lb, int64_t M, int64_t N, int64
   return hipGetLastError();
 }
 
-// PDA_WIDE_EPI_DIRECT=1: the wide kernel's bf16 epilogue writes from the accumulators (no LDS staging)
-int g_epi_direct = -1;  // set_gemm_paths(): -1 = env, 0 staged, 1 direct
-
-bool wide_epi_direct() {
-  static const bool on = [] {
-    const char* e = getenv("PDA_WIDE_EPI_DIRECT");
-    return e && e[0] == '1';
-  }();
-  return g_epi_direct >= 0 ? g_epi_direct == 1 : on;
-}
-
 // splits > 1: epi.slab receives [splits][M][N] fp32 partials, reduced (with the caller's epilogue)
 // by splitk_reduce_kernel; the effective split count is recomputed from the per-split K tiles.
 template <class LA, class LB>
 hipError_t launch_wide(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st,
                        int splits = 1, float* slab = nullptr) {
   Epi e = epi;
-  e.direct = !epi.c_f32 && !epi.slab && !epi.act && splits <= 1 && wide_epi_direct();
   if (splits > 1) {
     const int ktiles = (int)((K + BK - 1) / BK);
     const int kps = (ktiles + splits - 1) / splits;
@@ -1877,10 +1771,10 @@ bool dgrad_phased(int stride, int dil) { return stride == 1 || dil == 1; }
 
 // (ping-pong schedules of the wide kernel — the two wave groups alternating MFMA and load sections —
 // measured slower on every plain GEMM and most convs: profiles/r3_wide_pingpong_DROPPED.jsonl)
-void set_gemm_paths(int wide, int epi_direct) {
-  g_wide_override = wide;
-  if (epi_direct >= -1) g_epi_direct = epi_direct;
-}
+// (a register-direct wide epilogue — 8-byte stores from the accumulators, no LDS staging — measured
+// 6 % slower on the headline step than the staged 16-byte row stores: profiles/
+// r3_epi_direct_DROPPED_and_transformers.jsonl)
+void set_gemm_paths(int wide) { g_wide_override = wide; }
 
 // slab sizing covers both the 128-tile plan and the wide tile's (possibly deeper) split
 int64_t split_slab_floats(int64_t M, int64_t N, int64_t K, const Plan& p) {

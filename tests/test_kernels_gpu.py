@@ -670,47 +670,6 @@ def test_conv_dgrad_masked_addend_paths(case, wide):
     assert rel_err(dx.cpu(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("case", [(16, 56, 56, 64, 256, 1, 1, 0), (16, 56, 56, 256, 64, 1, 1, 0),
-                                  (8, 57, 57, 128, 128, 3, 1, 1), (4, 14, 14, 256, 512, 3, 2, 1),
-                                  (5, 14, 14, 256, 1024, 1, 1, 0), (3, 9, 13, 64, 256, 3, 2, 1)])
-def test_wide_direct_epilogue_matches_staged(case):
-    """Wide-tile bf16 epilogue written straight from the accumulators (epi_direct=1) == the LDS-staged
-    epilogue, bit for bit: conv fwd (+bias/relu), fwd + BN sums (sums to summation-order rounding),
-    dgrad with the bit-masked addend (strided shapes: the phase row remap), plain GEMMs with ragged
-    M / N edges."""
-    N, H, W, Cin, Cout, k, s, p = case
-    torch.manual_seed(10)
-    x = torch.randn(N, H, W, Cin).to(torch.bfloat16).to(DEV)
-    w = (torch.randn(Cout, k, k, Cin) / math.sqrt(Cin * k * k)).to(torch.bfloat16).to(DEV)
-    b = torch.randn(Cout, device=DEV)
-    shift = torch.randn(Cout, device=DEV) * 0.1
-    P, Q = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-    dy = torch.randn(N, P, Q, Cout).to(torch.bfloat16).to(DEV)
-    add = torch.randn(N, H, W, Cin).to(torch.bfloat16).to(DEV)
-    bits = torch.randint(0, 256, (N * H * W * Cin // 8,), dtype=torch.uint8, device=DEV)
-    gemms = [(torch.randn(M_, K_, device=DEV).to(torch.bfloat16), torch.randn(N_, K_, device=DEV).to(torch.bfloat16))
-             for M_, N_, K_ in [(512, 256, 64), (300, 520, 128), (1000, 768, 192)]]
-    res = []
-    for direct in (0, 1):
-        C().set_gemm_paths(2, direct)
-        try:
-            table = torch.zeros(3, 2, Cout, device=DEV)
-            outs = [C().conv_fwd_stats(x, w, s, p, 1, shift, table), C().conv_fwd(x, w, s, p, 1, b, True),
-                    C().conv_dgrad(dy, w, H, W, s, p, 1, add, bits), C().conv_dgrad(dy, w, H, W, s, p, 1, None)]
-            for A_, B_ in gemms:
-                (M_, K_), N_ = A_.shape, B_.shape[0]
-                o = torch.empty(M_, N_, device=DEV, dtype=torch.bfloat16)
-                C().gemm(A_, True, K_, B_, True, K_, o, N_, M_, N_, K_, None, False, False)
-                outs.append(o)
-            torch.cuda.synchronize()
-        finally:
-            C().set_gemm_paths(-1, -1)
-        res.append((outs, table.sum(0)))
-    for a, c in zip(res[0][0], res[1][0]):
-        assert torch.equal(a, c)
-    assert rel_err(res[1][1].cpu(), res[0][1].cpu()) < 1e-5
-
-
 _WGRAD_BUDGET_SCRIPT = r"""
 import math, torch, torch.nn.functional as F
 from pytorchdistributed_amd._native import C
