@@ -33,6 +33,10 @@ RESNET_CONVS = [
 COUNT = [1, 1, 3, 4, 2, 1, 1, 4, 1, 3, 3, 1, 1, 6, 1, 5, 5, 1, 1, 3, 1, 2, 2]
 
 
+ROOF_PF = 2.2e15  # dense bf16 MFMA at the ~2.1 GHz the chip holds under MFMA load (1024 FLOP/clk/SIMD)
+ROOF_BW = 5.5e12  # HBM bytes/s a streaming kernel sustains (the BN kernels reach 5-6 TB/s)
+
+
 def time_fn(fn, iters):
     for _ in range(3):
         fn()
@@ -51,6 +55,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--torch", action="store_true", help="also time MIOpen / hipBLASLt")
+    ap.add_argument("--blas", action="store_true", help="1x1 stride-1 convs: also time the same GEMM on hipBLASLt")
     ap.add_argument("--wide", type=int, default=-1, help="wide-tile GEMM path: -1 env, 0 off, 1 auto, 2 force")
     ap.add_argument("--compare", action="store_true",
                     help="per shape and op, time the auto / 128-tile / wide-tile paths interleaved (min of 3)")
@@ -71,6 +76,7 @@ def main():
         print(json.dumps(rec), flush=True)
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     tot_t = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    tot_roof = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     for (H, Ci, Co, R, st), cnt in zip(RESNET_CONVS, COUNT):
         pad = 0 if R == 4 else R // 2
         P = (H + 2 * pad - R) // st + 1
@@ -98,11 +104,30 @@ def main():
                     rec[f"{k}_{name}_ms"] = round(ms, 4)
             print(json.dumps(rec), flush=True)
             continue
+        # roofline: minimum bytes (every operand read once, the output written once; bf16 activations,
+        # fp32 weight gradient) at ROOF_BW vs FLOPs at ROOF_PF — the lower bound on each launch
+        act_in, act_out = a.batch * H * H * Ci * 2, a.batch * P * P * Co * 2
+        wbytes = Co * R * R * Ci * 2
+        nbytes = {"fwd": act_in + act_out + wbytes, "dgrad": act_out + act_in + wbytes,
+                  "wgrad": act_in + act_out + 2 * wbytes}
         for k, fn in fns.items():
             ms = time_fn(fn, a.iters)
             tot[k] += ms * cnt
             rec[k + "_ms"] = round(ms, 4)
             rec[k + "_tflops"] = round(flops / ms / 1e9, 1)
+            roof = max(flops / ROOF_PF, nbytes[k] / ROOF_BW) * 1e3
+            rec[k + "_roof_ms"] = round(roof, 4)
+            rec[k + "_bound"] = "mfma" if flops / ROOF_PF > nbytes[k] / ROOF_BW else "hbm"
+            rec[k + "_of_roof"] = round(roof / ms, 3)
+            tot_roof[k] += roof * cnt
+        if a.blas and R == 1 and st == 1:
+            # the identical GEMMs on hipBLASLt (a 1x1 stride-1 conv IS a GEMM in NHWC): library class check
+            x2, w2, dy2 = x.view(-1, Ci), w.view(Co, Ci), dy.view(-1, Co)
+            bl = {"fwd": lambda: torch.mm(x2, w2.t()), "dgrad": lambda: torch.mm(dy2, w2),
+                  "wgrad": lambda: torch.mm(dy2.t(), x2)}
+            for k, fn in bl.items():
+                ms = time_fn(fn, a.iters)
+                rec["blas_" + k + "_ms"] = round(ms, 4)
         if a.torch:
             xt = x.permute(0, 3, 1, 2)
             wt = w.permute(0, 3, 1, 2)
@@ -116,6 +141,7 @@ def main():
                 rec["torch_" + k + "_ms"] = round(ms, 4)
         print(json.dumps(rec), flush=True)
     print(json.dumps({"op": "total_per_step_ms", "ours": {k: round(v, 3) for k, v in tot.items()},
+                      "roofline": {k: round(v, 3) for k, v in tot_roof.items()},
                       "torch": {k: round(v, 3) for k, v in tot_t.items()} if a.torch else None}), flush=True)
 
 
