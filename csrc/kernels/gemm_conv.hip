@@ -516,7 +516,8 @@ __device__ __forceinline__ void wait_vm() {
   else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else static_assert(N == 0 || N == 2 || N == 4 || N == 6 || N == 8, "add the literal");
+  else if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else static_assert(N == 0 || N == 2 || N == 4 || N == 6 || N == 8 || N == 16, "add the literal");
 }
 
 __device__ __forceinline__ void raw_barrier() {
@@ -528,7 +529,9 @@ __device__ __forceinline__ void raw_barrier() {
 // bf16 epilogue of a 4-wave (2x2) BM x BN tile whose accumulators are acc[i][j][r] =
 // C[m0 + wm*WM + 16 i + (lane & 15)][n0 + wn*WN + 16 j + 4 (lane >> 4) + r]; `smem` is the operand LDS
 // (>= BM * (BN + 8) * 2 bytes + the statistics scratch), free once every wave has left the K loop.
-template <int BM, int BN>
+// RAW: the staging barrier is an LDS-only one (lgkmcnt + s_barrier), so LDS-DMA loads of a later tile
+// that are in flight survive the epilogue (a __syncthreads() would wait for them with vmcnt(0)).
+template <int BM, int BN, bool RAW = false>
 __device__ __forceinline__ void tile_epilogue_bf16(const f32x4 (&acc)[BM / 32][BN / 32], char* smem, const Epi& epi,
                                                    int64_t m0, int64_t n0, int64_t M, int64_t N, int tm) {
   constexpr int WM = BM / 2, WN = BN / 2;
@@ -565,7 +568,8 @@ __device__ __forceinline__ void tile_epilogue_bf16(const f32x4 (&acc)[BM / 32][B
       *reinterpret_cast<u16x4*>(stg + r * SROW + cc) = o;
     }
   }
-  __syncthreads();
+  if constexpr (RAW) raw_barrier();
+  else __syncthreads();
   constexpr int CPR = BN / 8;
   static_assert(NT % CPR == 0, "a thread keeps one column chunk");
   // column chunk of this thread is fixed (NT % CPR == 0): BN statistics accumulate in registers
@@ -1011,6 +1015,216 @@ __global__ void __launch_bounds__(NT, 2) conv3x3_wgrad_kernel(const bf16_t* __re
     for (int t = 0; t < 9; ++t)
       *reinterpret_cast<f32x4*>(out + (int64_t)co * Nn + (int64_t)t * g.C + ci0 + 16 * w + 4 * (lane >> 4)) =
           acc[i][t];
+  }
+}
+
+// ------------------------------------------------------------------ stem forward (4x4 valid conv, 16 channels)
+// y[n,p,q,co] = sum_(r,s,ci) x[n,p+r,q+s,ci] w[co][r][s][ci] over the 2x2 space-to-depth image: K = 256,
+// N = 64, M = 8 M output pixels at batch 640.  The implicit GEMM re-gathers every input byte 16 times
+// through L2 and re-streams the 32 KB weight per 128-pixel tile (720 us at bs 640, 3x its HBM roofline,
+// on the critical path at the start of every step).  Here a workgroup keeps the weight resident in LDS
+// (four [64 co][64 k] K-major images) and walks output rows: a row's 4-input-row band (4 x W pixels x
+// 32 B, linear: the ds_read_b128 lane groups then read 16 distinct 16-B slots) is DMA'd once and the
+// A fragments (pixel q, k = (s, ci-half) chunks of tap row r) are read at band pixel r*W + q + s.  Two
+// band stages: row t+1 is in flight while row t is multiplied; after the MFMAs row t's stage becomes
+// the epilogue's staging tile (bf16 row stores + the BN column sums of the conv epilogue).
+struct StemGeom {
+  int N, H, W, P, Q, Cout;
+  int rows;        // N * P output rows (K-steps)
+  int rps;         // rows per split
+  int band_px;     // 512: four 128-pixel DMA rounds (4 W and every tap read fit)
+};
+
+__device__ __forceinline__ int stem_band_row(int b) { return b ^ (((b >> 3) & 1) << 2); }
+
+constexpr int STEMF_W_BYTES = 4 * 64 * BK * 2;  // resident weight: 4 x [64 co][64 k]
+constexpr int STEMF_STAGE = 20 * 1024;          // >= 512 band pixels, >= the 128 x 64 staging tile + sums
+
+// The weight and the two stages are separate __shared__ objects and the row loop is unrolled by two,
+// so every LDS access names one object: with one dynamic array, the compiler cannot prove that the
+// current stage's reads do not alias the next row's in-flight DMA and drains it (vmcnt(0)) before them.
+__global__ void __launch_bounds__(NT, 2) conv_stem_fwd_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                              StemGeom g, Epi epi) {
+  __shared__ __attribute__((aligned(16))) char s_w[STEMF_W_BYTES];
+  __shared__ __attribute__((aligned(16))) char s_b0[STEMF_STAGE];
+  __shared__ __attribute__((aligned(16))) char s_b1[STEMF_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int rb = blockIdx.x * g.rps, re = min(g.rows, rb + g.rps);
+  if (rb >= re) return;
+
+  {  // resident weight [Cout = 64][256] (OHWI flattened), K-major images per 64-deep k block
+    PlainK<64> lw;
+    lw.p = w;
+    lw.rows = 64;
+    lw.K = 256;
+    lw.ld = 256;
+    typename PlainK<64>::State sw;
+    lw.init(sw, 0, tid);
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) glds_tile(lw, sw, 64 * kb, s_w + kb * (64 * BK * 2), wid);
+  }
+  auto issue = [&](int row, char* band) {
+    const int n = row / g.P, p = row - n * g.P;
+    const int64_t xrow0 = ((int64_t)n * g.H + p) * g.W;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int b = k * 128 + (tid >> 1);
+      const bool ok = b < 4 * g.W;
+      const bf16_t* q = ok ? x + (xrow0 + b) * 16 + 8 * (tid & 1) : g_zero_page;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)q,
+                                       (void __attribute__((address_space(3)))*)(band + k * 4096 + wid * 1024), 16,
+                                       0, 0);
+    }
+  };
+  auto step = [&](int row, char* band, char* next) {
+    // row's band (and, first time round, the weight) landed for every wave; every wave is done with
+    // the previous row's epilogue, whose staging tile is `next`
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();
+    // unconditional (the last row re-fetches itself into the idle stage): a branch around the DMA
+    // makes the compiler's LDS-DMA tracking merge paths and drain it before the reads below
+    issue(min(row + 1, re - 1), next);
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 32) {
+        const int ch = (kk >> 3) + (lane >> 4);  // this lane's 8-wide k chunk: (s, ci half)
+        const int boff = (r * g.W + (ch >> 1)) * 32 + (ch & 1) * 16;
+        mfma_bf16x8 af[4], bw[2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[i] = *reinterpret_cast<const mfma_bf16x8*>(band + boff + (wm * 64 + 16 * i + (lane & 15)) * 32);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bw[j] = read_frag<true, 64>(s_w + r * (64 * BK * 2), wn * 32 + 16 * j, kk, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], af[i], acc[i][j], 0, 0, 0);
+      }
+    raw_barrier();  // every wave is done reading the band: it becomes the staging tile
+    const int64_t m0 = (int64_t)row * g.Q;
+    tile_epilogue_bf16<128, 64, true>(acc, band, epi, m0, 0, m0 + g.Q, 64, row);
+  };
+  issue(rb, s_b0);
+  for (int row = rb; row < re; row += 2) {
+    step(row, s_b0, s_b1);
+    if (row + 1 < re) step(row + 1, s_b1, s_b0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (redundant) band DMA lands before LDS is released
+}
+
+// ------------------------------------------------------------------ stem weight gradient (4x4 valid conv, 16 channels)
+// The ResNet-50 stem runs as a 4x4 / stride-1 / pad-0 conv over the 2x2 space-to-depth image (16
+// channels).  Its weight gradient dw[co][r][s][ci] = sum_(n,p,q) dy[n,p,q,co] x[n,p+r,q+s,ci] is a
+// 64 x 256 output with K = N*P*Q (8 M pixels at batch 640): the implicit GEMM gathers im2col(x), i.e.
+// every input byte 16 times through L2 (920 us at bs 640, the last — fully exposed — kernel of the
+// backward).  Here a K-step is ONE output row (n, p): its dy row ([Q px][64 co], MN-major, padded to
+// 128 px) and the 4 input rows it touches (a band of 4 x W pixels x 32 B) are DMA'd into LDS once, and
+// the 16 taps read the band at pixel offsets r*W + s — L2 traffic is dy once plus x ~4x (each input row
+// feeds 4 output rows, mostly from L2).  Wave w owns tap row r = w: acc[co group][s] over 64 co x 4 s
+// x 16 ci.  Band pixels are 32 B; pixel row b is stored at b ^ (((b >> 3) & 1) << 2) so the 8 pixels a
+// half-wave's ds_read_b64_tr_b16 touches (b0..b0+3, b0+8..b0+11) fill all 32 8-B slots of a bank row.
+
+constexpr int STEM_STAGE = 128 * 64 * 2 + 512 * 32;  // dy row [128 px][64 co] + the 512-pixel band
+
+// Two row stages as separate __shared__ objects with the row loop unrolled by two (every LDS access
+// names one object: see conv_stem_fwd_kernel), two workgroups per CU.  A 4-stage ring at one
+// workgroup per CU measured slower (586 vs 457 us, both with the next row's DMA drained by the
+// compiler before the reads): occupancy matters more than DMA depth here.
+__global__ void __launch_bounds__(NT, 2) conv_stem_wgrad_kernel(const bf16_t* __restrict__ dy,
+                                                                const bf16_t* __restrict__ x, StemGeom g,
+                                                                float* __restrict__ slab) {
+  constexpr int DY_BYTES = 128 * 64 * 2;  // [128 px][64 co]: two [64][64] MN-major images
+  __shared__ __attribute__((aligned(16))) char s_st0[STEM_STAGE];
+  __shared__ __attribute__((aligned(16))) char s_st1[STEM_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int co0 = blockIdx.x * 64;
+  const int rb = blockIdx.y * g.rps, re = min(g.rows, rb + g.rps);
+  if (rb >= re) return;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int row, char* base) {
+    const int n = row / g.P, p = row - n * g.P;
+    PlainMN<64> la;  // dy row: Q consecutive pixels x 64 output channels
+    la.p = dy + (int64_t)row * g.Q * g.Cout + co0;
+    la.K = g.Q;
+    la.cols = 64;
+    la.ld = g.Cout;
+    typename PlainMN<64>::State sa;
+    la.init(sa, 0, tid);
+    glds_tile(la, sa, 0, base, w);
+    glds_tile(la, sa, 64, base + DY_BYTES / 2, w);
+    // band: input rows p .. p+3, all W pixels, 16 channels (two 16-B chunks per pixel)
+    char* band = base + DY_BYTES;
+    const bf16_t* row0 = x + ((int64_t)n * g.H + p) * g.W * 16;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int b = stem_band_row(k * 128 + (tid >> 1));
+      const bf16_t* a = row0 + (int64_t)b * 16 + 8 * (tid & 1);  // formed unconditionally, then selected
+      const bf16_t* q = b < 4 * g.W ? a : g_zero_page;
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)q,
+                                       (void __attribute__((address_space(3)))*)(band + k * 4096 + w * 1024), 16,
+                                       0, 0);
+    }
+  };
+
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const int mcol = 4 * (lane & 3);  // ci of this lane's transposed reads
+  const int jl = 8 * (lane >> 4) + ((lane & 15) >> 2);
+  auto step = [&](int row, char* As, char* next) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();  // row landed for every wave; every wave is done with `next`
+    issue(min(row + 1, re - 1), next);  // unconditional: see conv_stem_fwd_kernel
+    const char* band = As + DY_BYTES;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {  // 32-pixel k-chunks of the (padded) output row
+      mfma_bf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<false, 64>(As + (c >> 1) * (DY_BYTES / 2), 16 * i, 32 * (c & 1), lane);
+      // pixels past Q read finite band data (their dy rows are zero)
+      const int j = 32 * c + jl + w * g.W;
+#pragma unroll
+      for (int sx = 0; sx < 4; ++sx) {
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)(band + stem_band_row(j + sx) * 32 + mcol * 2));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s16x4*)(band + stem_band_row(j + sx + 4) * 32 + mcol * 2));
+        s16x8 f;
+        f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+        f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+        const mfma_bf16x8 bf = __builtin_bit_cast(mfma_bf16x8, f);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i][sx] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf, af[i], acc[i][sx], 0, 0, 0);
+      }
+    }
+  };
+  issue(rb, s_st0);
+  for (int row = rb; row < re; row += 2) {
+    step(row, s_st0, s_st1);
+    if (row + 1 < re) step(row + 1, s_st1, s_st0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // fp32 partials: acc[i][s][q] = dw[co0 + 16 i + (lane & 15)][r = w][s][ci = 4 (lane >> 4) + q]
+  float* out = slab + (int64_t)blockIdx.y * g.Cout * 256;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = co0 + 16 * i + (lane & 15);
+#pragma unroll
+    for (int sx = 0; sx < 4; ++sx)
+      *reinterpret_cast<f32x4*>(out + (int64_t)co * 256 + (w * 4 + sx) * 16 + 4 * (lane >> 4)) = acc[i][sx];
   }
 }
 
@@ -1932,6 +2146,51 @@ bool wg3_geom(int N, int H, int W, int C, int Cout, int R, int S, int stride, in
 
 int wg3_splits(const Wg3Geom& g) { return (g.groups + g.gps - 1) / g.gps; }
 
+// stem weight-gradient path (conv_stem_wgrad_kernel): 4x4 / stride 1 / pad 0 / dil 1 over 16 channels,
+// Cout % 64 == 0, output rows of <= 128 pixels.  PDA_CONV_STEM_WG=0 disables it.
+bool stem_wg_mode_on() {
+  static const bool on = [] {
+    const char* e = getenv("PDA_CONV_STEM_WG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+bool stem_geom(int N, int H, int W, int C, int Cout, int R, int S, int P, int Q, int stride, int pad, int dil,
+               StemGeom& g) {
+  if (!stem_wg_mode_on() || C != 16 || R != 4 || S != 4 || stride != 1 || pad != 0 || dil != 1) return false;
+  if (Cout % 64 || Q > 128 || Q < 1 || P != H - 3 || Q != W - 3 || N < 1) return false;
+  g.N = N; g.H = H; g.W = W; g.P = P; g.Q = Q; g.Cout = Cout;
+  g.rows = N * P;
+  // the last lane's tap read reaches band pixel 127 + 3 + 4 + 3 W; the band is always 4 DMA rounds of
+  // 128 pixels (8 DMAs per row and thread: the counted waits assume it)
+  const int need = 4 * W > 135 + 3 * W ? 4 * W : 135 + 3 * W;
+  g.band_px = 512;
+  if (need > g.band_px) return false;
+  // two workgroups per CU over the whole chip: the stem's weight gradient is the last kernel of the
+  // backward (nothing on the compute stream to leave CUs for)
+  const int tiles = Cout / 64;
+  int splits = 512 / tiles;
+  if (splits < 1) splits = 1;
+  if (splits > g.rows / 4) splits = g.rows / 4 > 1 ? g.rows / 4 : 1;
+  const int64_t cap = ((int64_t)96 << 20) / ((int64_t)Cout * 256 * 4);
+  if (splits > cap) splits = cap > 1 ? (int)cap : 1;
+  g.rps = (g.rows + splits - 1) / splits;
+  return true;
+}
+
+int stem_splits(const StemGeom& g) { return (g.rows + g.rps - 1) / g.rps; }
+
+// stem forward path (conv_stem_fwd_kernel): the stem_geom shapes with Cout == 64 and a bf16 output.
+// PDA_CONV_STEM_FWD=0 disables it.
+bool stem_fwd_on(int Cout, bool y_f32, const StemGeom& g) {
+  static const bool on = [] {
+    const char* e = getenv("PDA_CONV_STEM_FWD");
+    return !(e && e[0] == '0');
+  }();
+  return on && Cout == 64 && !y_f32 && g.Q <= 128;
+}
+
 // y[N,P,Q,Cout] = conv(x[N,H,W,C], w[Cout,R,S,C]) (+bias, relu)
 hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int Cout,
                       int R, int S, int P, int Q, int stride, int pad, int dil, const void* bias, bool bias_f32,
@@ -1945,6 +2204,13 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int
   epi.stats_rows = stats_rows > 0 ? stats_rows : 1;
 
   if (use_halo(H, W, C, Cout, R, S, stride, pad, dil, epi)) return launch_halo(x, w, N, H, W, C, Cout, false, epi, st);
+  StemGeom sg;
+  if (stem_geom(N, H, W, C, Cout, R, S, P, Q, stride, pad, dil, sg) && stem_fwd_on(Cout, y_f32, sg)) {
+    sg.rps = (sg.rows + 511) / 512;  // two workgroups per CU, each walking a run of output rows
+    const int blocks = (sg.rows + sg.rps - 1) / sg.rps;
+    conv_stem_fwd_kernel<<<blocks, NT, 0, st>>>(x, w, sg, epi);
+    return hipGetLastError();
+  }
   ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
   auto mk_a = [&](auto t) { t.x = x; t.g = g; t.M = M; t.K = K; return t; };
   auto mk_b = [&](auto t) { t.p = w; t.rows = Nn; t.K = K; t.ld = K; return t; };
@@ -2033,6 +2299,11 @@ int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, 
     const int64_t w3 = (int64_t)wg3_splits(g) * M * Nn;
     if (w3 > n) n = w3;
   }
+  StemGeom sg;
+  if (stem_geom(N, H, W, C, Cout, R, S, P, Q, 1, 0, 1, sg)) {
+    const int64_t ws = (int64_t)stem_splits(sg) * M * Nn;
+    if (ws > n) n = ws;
+  }
   return n;
 }
 
@@ -2053,6 +2324,18 @@ hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32
     const int splits = wg3_splits(g3);
     const int lds = 2 * (64 * BK * 2 + g3.band_px * 128);
     conv3x3_wgrad_kernel<<<dim3((Cout / 64) * g3.tiles_ci, splits), NT, lds, st>>>(dy, x, g3, slab);
+    PDA_CHECK_HIP(hipGetLastError());
+    int ll = 0;
+    while (ll < 4 && (splits >> ll) > 16) ++ll;
+    const int64_t per_block = 256 >> ll;
+    const int64_t gr = (M * Nn / 4 + per_block - 1) / per_block;
+    splitk_reduce_kernel<<<(unsigned)gr, 256, 0, st>>>(slab, splits, M, Nn, ll, epi);
+    return hipGetLastError();
+  }
+  StemGeom sg;
+  if (slab && stem_geom(N, H, W, C, Cout, R, S, P, Q, stride, pad, dil, sg)) {
+    const int splits = stem_splits(sg);
+    conv_stem_wgrad_kernel<<<dim3(Cout / 64, splits), NT, 0, st>>>(dy, x, sg, slab);
     PDA_CHECK_HIP(hipGetLastError());
     int ll = 0;
     while (ll < 4 && (splits >> ll) > 16) ++ll;

@@ -224,6 +224,9 @@ CONV_CASES = [
     (3, 9, 13, 64, 128, 3, 1, 1),       # halo fwd (its dgrad, 64 out channels, stays implicit GEMM)
     (2, 5, 30, 64, 64, 3, 1, 1),        # all-taps 3x3 wgrad: 2 rows per K-step, a 1-row last group
     (3, 4, 56, 128, 64, 3, 1, 1),       # all-taps 3x3 wgrad: 1 row per K-step, 2 input-channel blocks
+    (2, 35, 35, 16, 64, 4, 1, 0),       # stem (4x4 valid over the space-to-depth image): band wgrad kernel
+    (2, 20, 40, 16, 128, 4, 1, 0),      # stem wgrad with two output-channel tiles, rows of 37 pixels
+    (2, 115, 115, 16, 64, 4, 1, 0),     # the ResNet-50 stem shape (112-pixel rows padded to 128)
 ]
 
 
@@ -261,7 +264,8 @@ def test_conv_fwd_dgrad_wgrad(case):
 
 
 @pytest.mark.parametrize("case", [(2, 16, 16, 64, 64, 1, 1, 0), (3, 15, 15, 32, 136, 3, 2, 1), (1, 7, 7, 64, 2048, 1, 1, 0),
-                                  (8, 28, 28, 64, 256, 1, 1, 0), (4, 14, 14, 256, 512, 3, 1, 1)])
+                                  (8, 28, 28, 64, 256, 1, 1, 0), (4, 14, 14, 256, 512, 3, 1, 1),
+                                  (2, 35, 35, 16, 64, 4, 1, 0), (3, 115, 115, 16, 64, 4, 1, 0)])  # stem kernels
 @pytest.mark.parametrize("wide", [-1, 0, 2])
 def test_conv_fwd_epilogue_bn_sums(case, wide):
     """BN statistics accumulated by the conv epilogue (128-tile, wide-tile and auto paths) == sums over
