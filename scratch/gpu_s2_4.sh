@@ -12,7 +12,7 @@ step() {
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread
 step conv_new 400 python tools/bench_conv.py --batch 640 --iters 10
 step bench_new 300 python bench.py
-PDA_CONV_STEM_WG=0 PDA_CONV_STEM_FWD=0 step bench_old 300 python bench.py
+PDA_CONV_STEM_WG=0 step bench_old 300 python bench.py
 step bench_new2 300 python bench.py
-PDA_CONV_STEM_WG=0 PDA_CONV_STEM_FWD=0 step bench_old2 300 python bench.py
+PDA_CONV_STEM_WG=0 step bench_old2 300 python bench.py
 step prof 400 rocprofv3 --kernel-trace --stats -d $D/prof -o run -- python bench.py --steps 10 --warmup 5

@@ -828,3 +828,39 @@ def test_rownorm_fused_bwd_path():
     r = subprocess.run([sys.executable, "-c", _ROWNORM_FUSED_SCRIPT], cwd=root,
                        env={**os.environ, "PDA_ROWNORM_FUSED_BWD": "1"}, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0 and "fused ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+_STEM_FWD_SCRIPT = r"""
+import torch, torch.nn.functional as F
+from pytorchdistributed_amd._native import C
+for N, H in [(2, 35), (16, 51), (13, 115)]:  # 1, 2 and 3 output rows per workgroup
+    torch.manual_seed(1)
+    x = torch.randn(N, H, H, 16).to(torch.bfloat16)
+    w = (torch.randn(64, 4, 4, 16) / 16).to(torch.bfloat16)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2)).permute(0, 2, 3, 1)
+    ys = [C().conv_fwd(x.cuda(), w.cuda(), 1, 0, 1, None, False).cpu() for _ in range(3)]
+    assert all(torch.equal(ys[0], y) for y in ys[1:]), (N, H)
+    err = ((ys[0].float() - ref).norm() / ref.norm()).item()
+    assert err < 1e-2, (N, H, err)
+    shift = torch.randn(64) * 0.1
+    table = torch.zeros(7, 2, 64, device="cuda")
+    y = C().conv_fwd_stats(x.cuda(), w.cuda(), 1, 0, 1, shift.cuda(), table)
+    d = y.float().cpu().reshape(-1, 64) - shift
+    s = torch.stack([d.sum(0), (d * d).sum(0)])
+    assert ((table.sum(0).cpu() - s).norm() / s.norm()).item() < 1e-4, (N, H)
+print("stem fwd ok")
+"""
+
+
+def test_stem_fwd_kernel_opt_in():
+    """The opt-in stem forward band kernel (PDA_CONV_STEM_FWD=1, read once per process: run in a
+    child): fp32-reference numerics, bit-exact repeats and the epilogue BN sums at 1-3 rows per
+    workgroup."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _STEM_FWD_SCRIPT], cwd=root,
+                       env={**os.environ, "PDA_CONV_STEM_FWD": "1"}, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "stem fwd ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
