@@ -531,9 +531,12 @@ __device__ __forceinline__ void raw_barrier() {
 // (>= BM * (BN + 8) * 2 bytes + the statistics scratch), free once every wave has left the K loop.
 // RAW: the staging barrier is an LDS-only one (lgkmcnt + s_barrier), so LDS-DMA loads of a later tile
 // that are in flight survive the epilogue (a __syncthreads() would wait for them with vmcnt(0)).
-template <int BM, int BN, bool RAW = false>
-__device__ __forceinline__ void tile_epilogue_bf16(const f32x4 (&acc)[BM / 32][BN / 32], char* smem, const Epi& epi,
-                                                   int64_t m0, int64_t n0, int64_t M, int64_t N, int tm) {
+// DEFER: the BN sums of this tile are ADDED into the caller's st1 / st2 (this thread's fixed column
+// chunk) instead of being flushed — a workgroup walking several tiles flushes once (epi_stats_flush).
+template <int BM, int BN, bool RAW = false, bool DEFER = false>
+__device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 32][BN / 32], char* smem,
+                                                        const Epi& epi, int64_t m0, int64_t n0, int64_t M, int64_t N,
+                                                        int tm, float (&st1)[8], float (&st2)[8]) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -573,15 +576,12 @@ __device__ __forceinline__ void tile_epilogue_bf16(const f32x4 (&acc)[BM / 32][B
   constexpr int CPR = BN / 8;
   static_assert(NT % CPR == 0, "a thread keeps one column chunk");
   // column chunk of this thread is fixed (NT % CPR == 0): BN statistics accumulate in registers
-  float st1[8], st2[8], kshift[8];
+  float kshift[8];
   const bool want_stats = epi.stats != nullptr;
   {
     const int64_t n = n0 + (tid % CPR) * 8;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      st1[q] = st2[q] = 0.f;
-      kshift[q] = (want_stats && n + q < N) ? epi.stats_shift[n + q] : 0.f;
-    }
+    for (int q = 0; q < 8; ++q) kshift[q] = (want_stats && n + q < N) ? epi.stats_shift[n + q] : 0.f;
   }
 #pragma unroll
   for (int c = tid; c < BM * CPR; c += NT) {
@@ -607,9 +607,18 @@ __device__ __forceinline__ void tile_epilogue_bf16(const f32x4 (&acc)[BM / 32][B
     }
     *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
   }
-  if (want_stats) {
+  if (!DEFER && want_stats) {
     epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + BM * SROW * 2), CPR, NT, tm, n0, N);
   }
+}
+
+template <int BM, int BN, bool RAW = false>
+__device__ __forceinline__ void tile_epilogue_bf16(const f32x4 (&acc)[BM / 32][BN / 32], char* smem, const Epi& epi,
+                                                   int64_t m0, int64_t n0, int64_t M, int64_t N, int tm) {
+  float st1[8], st2[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) st1[q] = st2[q] = 0.f;
+  tile_epilogue_bf16_impl<BM, BN, RAW, false>(acc, smem, epi, m0, n0, M, N, tm, st1, st2);
 }
 
 // ------------------------------------------------------------------ the kernel
@@ -1077,6 +1086,9 @@ __global__ void __launch_bounds__(NT, 2) conv_stem_fwd_kernel(const bf16_t* __re
                                        0, 0);
     }
   };
+  float st1[8], st2[8];  // this thread's BN column sums over all of the workgroup's rows
+#pragma unroll
+  for (int q = 0; q < 8; ++q) st1[q] = st2[q] = 0.f;
   auto step = [&](int row, char* band, char* next) {
     // row's band (and, first time round, the weight) landed for every wave; every wave is done with
     // the previous row's epilogue, whose staging tile is `next`
@@ -1109,13 +1121,16 @@ __global__ void __launch_bounds__(NT, 2) conv_stem_fwd_kernel(const bf16_t* __re
       }
     raw_barrier();  // every wave is done reading the band: it becomes the staging tile
     const int64_t m0 = (int64_t)row * g.Q;
-    tile_epilogue_bf16<128, 64, true>(acc, band, epi, m0, 0, m0 + g.Q, 64, row);
+    tile_epilogue_bf16_impl<128, 64, true, true>(acc, band, epi, m0, 0, m0 + g.Q, 64, row, st1, st2);
   };
   issue(rb, s_b0);
   for (int row = rb; row < re; row += 2) {
     step(row, s_b0, s_b1);
     if (row + 1 < re) step(row + 1, s_b1, s_b0);
   }
+  // one BN-sum flush per workgroup into table row blockIdx.x % R: with at most R workgroups (the host
+  // sizes small problems so) every row receives one atomic add and the sums are reproducible
+  if (epi.stats) epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(s_b0 + 128 * 72 * 2), 8, NT, blockIdx.x, 0, 64);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last (redundant) band DMA lands before LDS is released
 }
 
@@ -2182,14 +2197,11 @@ bool stem_geom(int N, int H, int W, int C, int Cout, int R, int S, int P, int Q,
 int stem_splits(const StemGeom& g) { return (g.rows + g.rps - 1) / g.rps; }
 
 // stem forward path (conv_stem_fwd_kernel): the stem_geom shapes with Cout == 64 and a bf16 output.
-// Opt-in (PDA_CONV_STEM_FWD=1): its outputs match the fp32 reference and repeat bit-exactly
-// (tools/stem_debug.py, conv and BN-sum tests), but with it the two ResNet-50 DDP-vs-replica /
-// side-stream gradient tests diverge O(1) in layer1/2 BN-bias gradients (profiles/r3_stem_kernels.jsonl)
-// — unexplained, so it stays off.
+// PDA_CONV_STEM_FWD=0 disables it.
 bool stem_fwd_on(int Cout, bool y_f32, const StemGeom& g) {
   static const bool on = [] {
     const char* e = getenv("PDA_CONV_STEM_FWD");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on && Cout == 64 && !y_f32 && g.Q <= 128;
 }
@@ -2209,7 +2221,10 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int
   if (use_halo(H, W, C, Cout, R, S, stride, pad, dil, epi)) return launch_halo(x, w, N, H, W, C, Cout, false, epi, st);
   StemGeom sg;
   if (stem_geom(N, H, W, C, Cout, R, S, P, Q, stride, pad, dil, sg) && stem_fwd_on(Cout, y_f32, sg)) {
-    sg.rps = (sg.rows + 511) / 512;  // two workgroups per CU, each walking a run of output rows
+    // two workgroups per CU, each walking a run of output rows; problems of <= 16 rows per table row
+    // use at most R (= stats_rows) workgroups, so their BN sums are reproducible (one add per row)
+    const int nb = (stats && sg.rows <= 16 * stats_rows) ? (stats_rows < 512 ? stats_rows : 512) : 512;
+    sg.rps = (sg.rows + nb - 1) / nb;
     const int blocks = (sg.rows + sg.rps - 1) / sg.rps;
     conv_stem_fwd_kernel<<<blocks, NT, 0, st>>>(x, w, sg, epi);
     return hipGetLastError();

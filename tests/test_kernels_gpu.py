@@ -852,10 +852,10 @@ print("stem fwd ok")
 """
 
 
-def test_stem_fwd_kernel_opt_in():
-    """The opt-in stem forward band kernel (PDA_CONV_STEM_FWD=1, read once per process: run in a
-    child): fp32-reference numerics, bit-exact repeats and the epilogue BN sums at 1-3 rows per
-    workgroup."""
+def test_stem_fwd_kernel_rows_per_workgroup():
+    """The stem forward band kernel (PDA_CONV_STEM_FWD=1 forced in a child: the flag is read once per
+    process): fp32-reference numerics, bit-exact repeats and the epilogue BN sums at 1-3 output rows
+    per workgroup (the conv tests above cover 1 only)."""
     import os
     import subprocess
     import sys
