@@ -729,7 +729,8 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
   TORCH_CHECK(w.size(0) == Cout && C % 8 == 0 && Cout % 8 == 0);
   c10::DeviceGuard g(dy.device());
   Tensor wt;
-  if (pda::conv_dgrad_needs_wt(R, S, (int)stride, (int)pad)) {
+  if (pda::conv_dgrad_needs_wt(R, S, (int)stride, (int)pad) ||
+      pda::conv_dgrad_1x1_wt(R, S, (int)stride, (int)pad, C, Cout)) {
     wt = at::empty({C, R, S, Cout}, w.options());
     CHECK_HIP_OK(pda::conv_weight_transpose(bp(w), bpm(wt), Cout, R, S, C, stride, pad, dil, stream_of(dy)));
   }

@@ -209,6 +209,8 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int
 // wt: the weight transposed by conv_weight_transpose — except for a 1x1 stride-1 unpadded conv
 // (conv_dgrad_needs_wt() false), whose dgrad is a plain GEMM that reads w [Cout][C] MN-major in place.
 bool conv_dgrad_needs_wt(int R, int S, int stride, int pad);
+// 1x1 stride-1 dgrads that read a transposed weight wt[C][Cout] (K-major) instead (MFMA-heavy shapes)
+bool conv_dgrad_1x1_wt(int R, int S, int stride, int pad, int C, int Cout);
 hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, void* dx, bool dx_f32, int N, int H, int W,
                         int C, int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,
                         const uint8_t* addend_bits, hipStream_t st);

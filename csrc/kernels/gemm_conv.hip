@@ -2239,6 +2239,19 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int
 // it (wt phase-packed by conv_weight_transpose); folded single launch when stride > 1 and dil > 1.
 bool conv_dgrad_needs_wt(int R, int S, int stride, int pad) { return !(R == 1 && S == 1 && stride == 1 && pad == 0); }
 
+// 1x1 stride-1 dgrad on a transposed weight wt[C][Cout] (K-major B operand) instead of reading w
+// [Cout][C] MN-major in place: the wide tile's K-major x K-major schedule avoids the two
+// ds_read_b64_tr_b16 per B fragment (plain GEMMs: dgrad layout 0.72-0.86x the fwd layout,
+// profiles/r3_wide_ring_DROPPED.jsonl two_stage arm).  Only where the GEMM is MFMA-heavy (C, Cout >= 256);
+// the transpose is one small launch.  PDA_DGRAD_1X1_WT=0 keeps the in-place read.
+bool conv_dgrad_1x1_wt(int R, int S, int stride, int pad, int C, int Cout) {
+  static const bool on = [] {
+    const char* e = getenv("PDA_DGRAD_1X1_WT");
+    return !(e && e[0] == '0');
+  }();
+  return on && R == 1 && S == 1 && stride == 1 && pad == 0 && C >= 256 && Cout >= 256;
+}
+
 hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, void* dx, bool dx_f32, int N, int H, int W,
                         int C, int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,
                         const uint8_t* addend_bits, hipStream_t st) {
@@ -2253,6 +2266,10 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
     epi.addend = addend;
     epi.addend_bits = addend_bits;
     auto mk_a = [&](auto t) { t.p = dy; t.rows = M; t.K = K; t.ld = Cout; return t; };
+    if (wt) {  // conv_dgrad_1x1_wt: B(k = co, n = ci) = wt[ci][co], K-major
+      auto mk_bt = [&](auto t) { t.p = wt; t.rows = Nn; t.K = K; t.ld = Cout; return t; };
+      return dispatch_bn<PlainK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_bt);
+    }
     auto mk_b = [&](auto t) { t.p = w; t.K = K; t.cols = Nn; t.ld = C; return t; };
     return dispatch_bn<PlainK, PlainMN>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
   }

@@ -227,6 +227,7 @@ CONV_CASES = [
     (2, 35, 35, 16, 64, 4, 1, 0),       # stem (4x4 valid over the space-to-depth image): band wgrad kernel
     (2, 20, 40, 16, 128, 4, 1, 0),      # stem wgrad with two output-channel tiles, rows of 37 pixels
     (2, 115, 115, 16, 64, 4, 1, 0),     # the ResNet-50 stem shape (112-pixel rows padded to 128)
+    (4, 14, 14, 1024, 256, 1, 1, 0),    # 1x1 dgrad on the transposed weight (K-major B), wide tile
 ]
 
 
