@@ -2206,6 +2206,18 @@ bool stem_fwd_on(int Cout, bool y_f32, const StemGeom& g) {
   return on && Cout == 64 && !y_f32 && g.Q <= 128;
 }
 
+// 1x1 / stride-1 / pad-0 convs are plain GEMMs in NHWC: fwd and wgrad read x through the plain loaders
+// (PlainK / PlainMN: a pointer add per row) instead of the im2col gathers (ConvFwdK / ConvWgradMN: two
+// fast divisions, bounds checks and 64-bit offsets per 16-B chunk — VALU work that competes with the
+// MFMA issue of the co-resident wave).  PDA_CONV_1X1_PLAIN=0 keeps the gathers.
+bool conv_1x1_plain(int R, int S, int stride, int pad, int dil) {
+  static const bool on = [] {
+    const char* e = getenv("PDA_CONV_1X1_PLAIN");
+    return !(e && e[0] == '0');
+  }();
+  return on && R == 1 && S == 1 && stride == 1 && pad == 0 && dil == 1;
+}
+
 // y[N,P,Q,Cout] = conv(x[N,H,W,C], w[Cout,R,S,C]) (+bias, relu)
 hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int N, int H, int W, int C, int Cout,
                       int R, int S, int P, int Q, int stride, int pad, int dil, const void* bias, bool bias_f32,
@@ -2229,9 +2241,13 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int
     conv_stem_fwd_kernel<<<blocks, NT, 0, st>>>(x, w, sg, epi);
     return hipGetLastError();
   }
+  auto mk_b = [&](auto t) { t.p = w; t.rows = Nn; t.K = K; t.ld = K; return t; };
+  if (conv_1x1_plain(R, S, stride, pad, dil)) {  // y[NHW, Cout] = x[NHW, C] w[Cout, C]^T
+    auto mk_ap = [&](auto t) { t.p = x; t.rows = M; t.K = K; t.ld = C; return t; };
+    return dispatch_bn<PlainK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_ap, mk_b);
+  }
   ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
   auto mk_a = [&](auto t) { t.x = x; t.g = g; t.M = M; t.K = K; return t; };
-  auto mk_b = [&](auto t) { t.p = w; t.rows = Nn; t.K = K; t.ld = K; return t; };
   return dispatch_bn<ConvFwdK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
 }
 
@@ -2380,8 +2396,12 @@ hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32
     return hipGetLastError();
   }
   Plan p = plan_wgrad(M, Nn, K, slab != nullptr);
-  ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
   auto mk_a = [&](auto t) { t.p = dy; t.K = K; t.cols = M; t.ld = Cout; return t; };
+  if (conv_1x1_plain(R, S, stride, pad, dil)) {  // dw[Cout, C] = dy[NHW, Cout]^T x[NHW, C]
+    auto mk_bp = [&](auto t) { t.p = x; t.K = K; t.cols = Nn; t.ld = C; return t; };
+    return dispatch_bn<PlainMN, PlainMN>(M, Nn, K, p, epi, slab, st, mk_a, mk_bp);
+  }
+  ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
   auto mk_b = [&](auto t) { t.x = x; t.g = g; t.K = K; t.cols = Nn; return t; };
   return dispatch_bn<PlainMN, ConvWgradMN>(M, Nn, K, p, epi, slab, st, mk_a, mk_b);
 }
