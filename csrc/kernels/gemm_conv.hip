@@ -195,6 +195,57 @@ struct ConvFwdK {
   }
 };
 
+// Conv fwd A operand when C % 64 == 0: a 64-deep K tile then lies inside ONE tap (r, s), so the tap
+// and the channel base are wave-uniform (scalar ALU) and each row keeps a pointer to its tap-(0, 0)
+// pixel: per K tile a row costs one 64-bit add of a uniform offset and two bounds compares, instead of
+// ConvFwdK's two fast divisions per 16-B chunk and a 64-bit multiply-add per row.
+template <int R>
+struct ConvFwdKU {
+  static constexpr bool kMajor = true;
+  static constexpr int NCH = R / 32;
+  const bf16_t* x;
+  ConvGeom g;
+  int64_t M, K;
+  struct State {
+    const bf16_t* base[NCH];  // x + pixel (n, p*st - pad, q*st - pad) * C + this thread's chunk
+    int ih0[NCH], iw0[NCH];   // (row invalid: ih0 = -2^20, never in range)
+    int kc;
+  };
+  __device__ void init(State& s, int64_t row0, int tid) const {
+    s.kc = kmaj_chunk(tid) * 8;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int64_t m = row0 + (tid >> 3) + 32 * i;
+      const bool ok = m < M;
+      const uint32_t mm = ok ? (uint32_t)m : 0u;
+      const uint32_t t = fdiv(mm, g.fQ);
+      const int q = (int)(mm - t * g.Q);
+      const uint32_t n = fdiv(t, g.fP);
+      const int p = (int)(t - n * g.P);
+      s.ih0[i] = ok ? p * g.st - g.pad : -(1 << 20);
+      s.iw0[i] = q * g.st - g.pad;
+      s.base[i] = x + (((int64_t)n * g.H + s.ih0[i]) * g.W + s.iw0[i]) * g.C + s.kc;
+    }
+  }
+  __device__ void src(const State& s, int64_t k0, const bf16_t* (&q)[NCH]) const {
+    const bool kok = k0 < K;  // K is a multiple of 64 here
+    const uint32_t kk = kok ? (uint32_t)k0 : 0u;
+    const uint32_t rs = fdiv(kk, g.fC);
+    const int cb = (int)(kk - rs * g.C);
+    const uint32_t r = fdiv(rs, g.fS);
+    const int sx = (int)(rs - r * g.S);
+    const int dr = (int)r * g.dil, ds = sx * g.dil;
+    const int64_t toff = ((int64_t)dr * g.W + ds) * g.C + cb;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int ih = s.ih0[i] + dr, iw = s.iw0[i] + ds;
+      const bool ok = kok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const bf16_t* a = s.base[i] + toff;  // formed unconditionally, then selected
+      q[i] = ok ? a : g_zero_page;
+    }
+  }
+};
+
 // Conv dgrad A operand, folded form (stride > 1 with dilation > 1 only): element (m = (n,h,w),
 // k = (r,s,co)) = dy[n, p, q, co] where p*st - pad + r*dil = h (zero when not integral / out of range).
 template <int R>
@@ -2206,6 +2257,15 @@ bool stem_fwd_on(int Cout, bool y_f32, const StemGeom& g) {
   return on && Cout == 64 && !y_f32 && g.Q <= 128;
 }
 
+// ConvFwdKU (tap-uniform K tiles) for C % 64 == 0.  PDA_CONV_TAP_UNIFORM=0 keeps ConvFwdK.
+bool tap_uniform_on() {
+  static const bool on = [] {
+    const char* e = getenv("PDA_CONV_TAP_UNIFORM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // 1x1 / stride-1 / pad-0 convs are plain GEMMs in NHWC: fwd and wgrad read x through the plain loaders
 // (PlainK / PlainMN: a pointer add per row) instead of the im2col gathers (ConvFwdK / ConvWgradMN: two
 // fast divisions, bounds checks and 64-bit offsets per 16-B chunk — VALU work that competes with the
@@ -2248,6 +2308,7 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int
   }
   ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
   auto mk_a = [&](auto t) { t.x = x; t.g = g; t.M = M; t.K = K; return t; };
+  if (C % 64 == 0 && tap_uniform_on()) return dispatch_bn<ConvFwdKU, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
   return dispatch_bn<ConvFwdK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
 }
 
