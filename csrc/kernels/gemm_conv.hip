@@ -962,6 +962,7 @@ struct Wg3Geom {
   int gps;        // row groups per split
   int band_px;    // band pixels (multiple of 32) >= (rk + 2) * (W + 2)
   int tiles_ci;   // C / 64
+  FastDiv fW2;    // W + 2
 };
 
 __device__ __forceinline__ int band_mn_off(int b, int m) {
@@ -969,12 +970,16 @@ __device__ __forceinline__ int band_mn_off(int b, int m) {
   return b * 128 + ((((m >> 4) ^ h) & 3) << 5) + ((m & 15) << 1);
 }
 
+constexpr int WG3_STAGE = 40 * 1024;  // [64 px][64 co] dy tile + a band of <= 256 pixels x 128 B
+
 __global__ void __launch_bounds__(NT, 2) conv3x3_wgrad_kernel(const bf16_t* __restrict__ dy,
                                                               const bf16_t* __restrict__ x, Wg3Geom g,
                                                               float* __restrict__ slab) {
   constexpr int A_BYTES = 64 * BK * 2;  // [64 px][64 co]
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int stage_bytes = A_BYTES + g.band_px * 128;
+  // two stages as separate __shared__ objects, loop unrolled by two (see conv_stem_fwd_kernel: with
+  // one dynamic array the compiler drained the next group's DMA before this group's reads)
+  __shared__ __attribute__((aligned(16))) char s_st0[WG3_STAGE];
+  __shared__ __attribute__((aligned(16))) char s_st1[WG3_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tco = blockIdx.x / g.tiles_ci, tci = blockIdx.x - tco * g.tiles_ci;
   const int co0 = tco * 64, ci0 = tci * 64;
@@ -1000,8 +1005,7 @@ __global__ void __launch_bounds__(NT, 2) conv3x3_wgrad_kernel(const bf16_t* __re
       pixj[h2][lh] = j < g.rk * W ? rj * W2 + cj : 0;  // past the group: any finite band pixel (dy = 0)
     }
 
-  auto issue = [&](int grp, int stg) {
-    char* base = smem + stg * stage_bytes;
+  auto issue = [&](int grp, char* base) {
     const int n = grp / g.gpi, p0 = (grp - n * g.gpi) * g.rk;
     const int rows = min(g.rk, H - p0);
     // dy rows p0 .. p0 + rows - 1: rows * W consecutive pixels, an MN-major [k = px][m = co] tile
@@ -1013,34 +1017,36 @@ __global__ void __launch_bounds__(NT, 2) conv3x3_wgrad_kernel(const bf16_t* __re
     typename PlainMN<64>::State sa;
     la.init(sa, 0, tid);
     glds_tile(la, sa, 0, base, w);
-    // x band: image rows p0 - 1 .. p0 + rk, cols -1 .. W (zero outside the image)
+    // x band: image rows p0 - 1 .. p0 + rk, cols -1 .. W (zero outside the image).  Always 8 DMA rounds
+    // (256 pixels, the stage's capacity; pixels past the band are zeros nobody reads) with the
+    // addresses selected, not branched around: a runtime-length loop / branch join made the compiler
+    // drain the DMA before the next reads
     char* band = base + A_BYTES;
     const int s16 = tid & 7;
-    for (int k = 0; k * 32 < g.band_px; ++k) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
       const int b = k * 32 + (tid >> 3);
-      const int rs = b / W2, cs = b - rs * W2;
-      const int ih = p0 - 1 + rs, iw = cs - 1;
+      const int rs = (int)fdiv((uint32_t)b, g.fW2), cs = b - rs * W2;
       const int hb = ((b >> 1) & 1) | (((b >> 3) & 1) << 1);
       const int ci = ci0 + 16 * ((s16 >> 1) ^ hb) + 8 * (s16 & 1);
+      const int ih = p0 - 1 + rs, iw = cs - 1;
       const bool ok = rs < g.rk + 2 && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-      const bf16_t* q = ok ? x + (((int64_t)n * H + ih) * W + iw) * g.C + ci : g_zero_page;
+      const bf16_t* a = x + (((int64_t)n * H + ih) * W + iw) * g.C + ci;  // formed unconditionally
+      const bf16_t* q = ok ? a : g_zero_page;
       __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)q,
                                        (void __attribute__((address_space(3)))*)(band + k * 4096 + w * 1024), 16,
                                        0, 0);
     }
   };
 
-  if (gb < ge) issue(gb, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   typedef short s16x4 __attribute__((ext_vector_type(4)));
   typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
   typedef short s16x8 __attribute__((ext_vector_type(8)));
   const int mcol = 16 * w + 4 * ((lane & 15) & 3);
-  for (int grp = gb; grp < ge; ++grp) {
-    const int stg = (grp - gb) & 1;
-    if (grp + 1 < ge) issue(grp + 1, stg ^ 1);
-    const char* As = smem + stg * stage_bytes;
+  auto step = [&](int grp, const char* As, char* next) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();  // this group landed for every wave; every wave is done with `next`
+    issue(min(grp + 1, ge - 1), next);  // unconditional: see conv_stem_fwd_kernel
     const char* band = As + A_BYTES;
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
@@ -1062,8 +1068,14 @@ __global__ void __launch_bounds__(NT, 2) conv3x3_wgrad_kernel(const bf16_t* __re
         for (int i = 0; i < 4; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf, af[i], acc[i][t], 0, 0, 0);
       }
     }
+  };
+  if (gb < ge) {  // (every split has groups: wg3_splits; an empty one would still write its zero slab)
+    issue(gb, s_st0);
+    for (int grp = gb; grp < ge; grp += 2) {
+      step(grp, s_st0, s_st1);
+      if (grp + 1 < ge) step(grp + 1, s_st1, s_st0);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
   // fp32 partials: acc[i][t][q] = dw[co0 + 16 i + (lane & 15)][t][ci0 + 16 w + 4 (lane >> 4) + q]
   const int64_t Nn = 9LL * g.C;
@@ -2197,6 +2209,7 @@ bool wg3_geom(int N, int H, int W, int C, int Cout, int R, int S, int stride, in
   g.gpi = (H + g.rk - 1) / g.rk;
   g.groups = N * g.gpi;
   g.band_px = ((g.rk + 2) * (W + 2) + 31) / 32 * 32;
+  g.fW2 = make_fastdiv((uint32_t)(W + 2));
   g.tiles_ci = C / 64;
   const int tiles = (Cout / 64) * g.tiles_ci;
   // ~512 workgroups (2 per CU), >= 4 row groups each, fp32 partial slabs capped at 96 MB
@@ -2207,7 +2220,7 @@ bool wg3_geom(int N, int H, int W, int C, int Cout, int R, int S, int stride, in
   const int64_t cap = ((int64_t)96 << 20) / (per * 4);
   if (splits > cap) splits = cap > 1 ? (int)cap : 1;
   g.gps = (g.groups + splits - 1) / splits;
-  return 2 * (64 * BK * 2 + g.band_px * 128) <= 80 * 1024;
+  return 64 * BK * 2 + g.band_px * 128 <= WG3_STAGE;  // two stages, two workgroups per CU
 }
 
 int wg3_splits(const Wg3Geom& g) { return (g.groups + g.gps - 1) / g.gps; }
@@ -2427,15 +2440,8 @@ hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32
   Epi epi{dw, Nn, dw_f32 ? 1 : 0, nullptr, 0, 0, nullptr};
   Wg3Geom g3;
   if (slab && P == H && Q == W && wg3_geom(N, H, W, C, Cout, R, S, stride, pad, dil, g3)) {
-    static bool attr = [] {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_wgrad_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-      return true;
-    }();
-    (void)attr;
     const int splits = wg3_splits(g3);
-    const int lds = 2 * (64 * BK * 2 + g3.band_px * 128);
-    conv3x3_wgrad_kernel<<<dim3((Cout / 64) * g3.tiles_ci, splits), NT, lds, st>>>(dy, x, g3, slab);
+    conv3x3_wgrad_kernel<<<dim3((Cout / 64) * g3.tiles_ci, splits), NT, 0, st>>>(dy, x, g3, slab);
     PDA_CHECK_HIP(hipGetLastError());
     int ll = 0;
     while (ll < 4 && (splits >> ll) > 16) ++ll;
