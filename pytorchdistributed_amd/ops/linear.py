@@ -184,10 +184,13 @@ class _MlpGeluFn(torch.autograd.Function):
         N = w2.shape[0]
         dy2 = dy.reshape(-1, N).contiguous()
         M, F_ = h.shape
-        # fc2 data gradient fused with the GELU backward: dh = (dy W2) * gelu'(h)
+        # fc2 data gradient fused with the GELU backward: dh = (dy W2) * gelu'(h), W2 read through its
+        # transpose (an 8 MB copy for GPT-2-medium) so both operands are K-major — the wide tile's fast
+        # layout (the in-place MN-major read of W2 costs the GEMM 15-25 %, profiles/r3_wide_ring_DROPPED.jsonl)
         dh = torch.empty_like(h)
         if M > 0:
-            C().gemm_act(dy2, True, N, w2, False, F_, dh, F_, M, F_, N, None, 2, h)
+            w2t = w2.t().contiguous()
+            C().gemm_act(dy2, True, N, w2t, True, N, dh, F_, M, F_, N, None, 2, h)
         dw2, db2 = _param_grads(dy2, g, pw2, pb2, ctx.needs_input_grad[3], pb2 is not None and ctx.needs_input_grad[4])
         dx = _gemm_dgrad(dh, w1).reshape(ctx.shape) if ctx.needs_input_grad[0] else None
         dw1, db1 = _param_grads(dh, x2, pw1, pb1, ctx.needs_input_grad[1], pb1 is not None and ctx.needs_input_grad[2])
@@ -199,7 +202,8 @@ def mlp_fused_ok(x, w1, w2) -> bool:
     on GPT-2-medium (32 x 1024 tokens) the native tile's fc1 forward / fc2 dgrad run at ~85 % of
     hipBLASLt's rate and the 256x256 tile's epilogue (one workgroup per CU, a second [tokens, 4d]
     stream in it) is exposed, which outweighs the two elementwise passes it removes: 303-305k vs
-    311-312k tokens/s same box (profiles/r2_gpt2_mlp_fused_ab.jsonl)."""
+    311-312k tokens/s same box (profiles/r2_gpt2_mlp_fused_ab.jsonl); still 300-302k vs 309-310k with
+    the fc2 dgrad on a K-major transposed weight (profiles/r3_gpt2_mlp_fused_wt_DROPPED.jsonl)."""
     return (x.is_cuda and x.dtype == torch.bfloat16 and _mfma_ok(x, w1) and _mfma_ok(x, w2)
             and os.environ.get("PDA_MLP_FUSED", "0") == "1")
 
