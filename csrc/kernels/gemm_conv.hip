@@ -1223,8 +1223,7 @@ __global__ void __launch_bounds__(NT, 2) conv_stem_wgrad_kernel(const bf16_t* __
   __shared__ __attribute__((aligned(16))) char s_st1[STEM_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int co0 = blockIdx.x * 64;
-  const int rb = blockIdx.y * g.rps, re = min(g.rows, rb + g.rps);
-  if (rb >= re) return;
+  const int rb = blockIdx.y * g.rps, re = min(g.rows, rb + g.rps);  // (stem_splits: never empty)
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -1289,12 +1288,14 @@ __global__ void __launch_bounds__(NT, 2) conv_stem_wgrad_kernel(const bf16_t* __
       }
     }
   };
-  issue(rb, s_st0);
-  for (int row = rb; row < re; row += 2) {
-    step(row, s_st0, s_st1);
-    if (row + 1 < re) step(row + 1, s_st1, s_st0);
+  if (rb < re) {  // an empty split would still write its zero slab
+    issue(rb, s_st0);
+    for (int row = rb; row < re; row += 2) {
+      step(row, s_st0, s_st1);
+      if (row + 1 < re) step(row + 1, s_st1, s_st0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // fp32 partials: acc[i][s][q] = dw[co0 + 16 i + (lane & 15)][r = w][s][ci = 4 (lane >> 4) + q]
   float* out = slab + (int64_t)blockIdx.y * g.Cout * 256;
 #pragma unroll
