@@ -352,6 +352,56 @@ struct ConvDgradPhaseK {
   }
 };
 
+// ConvDgradPhaseK when Cg % 64 == 0: tap-uniform K tiles as in ConvFwdKU (the tap (ri, si) and the
+// channel base are wave-uniform; each row keeps a pointer to its tap-(0, 0) source pixel).
+template <int R>
+struct ConvDgradPhaseKU {
+  static constexpr bool kMajor = true;
+  static constexpr int NCH = R / 32;
+  const bf16_t* dy;
+  ConvGeom g;
+  PhaseGeom ph;
+  int64_t M, K;
+  struct State {
+    const bf16_t* base[NCH];  // dy + pixel (n, hh, ww) * Cg + this thread's chunk
+    int hh[NCH], ww[NCH];     // (row invalid: hh = -2^20)
+    int kc;
+  };
+  __device__ void init(State& s, int64_t row0, int tid) const {
+    s.kc = kmaj_chunk(tid) * 8;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int64_t m = row0 + (tid >> 3) + 32 * i;
+      const bool ok = m < M;
+      const uint32_t mm = ok ? (uint32_t)m : 0u;
+      const uint32_t t = fdiv(mm, ph.fWh);
+      const int ww = (int)(mm - t * ph.Wh);
+      const uint32_t n = fdiv(t, ph.fHh);
+      const int hh = (int)(t - n * ph.Hh);
+      s.hh[i] = ok ? hh : -(1 << 20);
+      s.ww[i] = ww;
+      s.base[i] = dy + (((int64_t)n * g.P + s.hh[i]) * g.Q + ww) * g.Cg + s.kc;
+    }
+  }
+  __device__ void src(const State& s, int64_t k0, const bf16_t* (&q)[NCH]) const {
+    const bool kok = k0 < K;  // K is a multiple of 64 here
+    const uint32_t kk = kok ? (uint32_t)k0 : 0u;
+    const uint32_t t = fdiv(kk, g.fC);  // fC divides by Cg (= Cout) here
+    const int cb = (int)(kk - t * g.Cg);
+    const uint32_t ri = fdiv(t, ph.fSv);
+    const int si = (int)(t - ri * ph.Sv);
+    const int dr = ph.base_r - (int)ri * ph.step_r, ds = ph.base_s - si * ph.step_s;
+    const int64_t toff = ((int64_t)dr * g.Q + ds) * g.Cg + cb;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const int p = s.hh[i] + dr, qq = s.ww[i] + ds;
+      const bool ok = kok && (unsigned)p < (unsigned)g.P && (unsigned)qq < (unsigned)g.Q;
+      const bf16_t* a = s.base[i] + toff;  // formed unconditionally, then selected
+      q[i] = ok ? a : g_zero_page;
+    }
+  }
+};
+
 // Conv wgrad B operand (MN-major): element (k = (n,p,q), col = (r,s,ci)) = x[n, p*st-pad+r*dil, ...]
 template <int R>
 struct ConvWgradMN {
@@ -2271,7 +2321,8 @@ bool stem_fwd_on(int Cout, bool y_f32, const StemGeom& g) {
   return on && Cout == 64 && !y_f32 && g.Q <= 128;
 }
 
-// ConvFwdKU (tap-uniform K tiles) for C % 64 == 0.  PDA_CONV_TAP_UNIFORM=0 keeps ConvFwdK.
+// ConvFwdKU / ConvDgradPhaseKU (tap-uniform K tiles) for 64-multiple gathered channel counts.
+// PDA_CONV_TAP_UNIFORM=0 keeps ConvFwdK / ConvDgradPhaseK.
 bool tap_uniform_on() {
   static const bool on = [] {
     const char* e = getenv("PDA_CONV_TAP_UNIFORM");
@@ -2409,7 +2460,10 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
       }
       auto mk_a = [&](auto t) { t.dy = dy; t.g = g; t.ph = pg; t.M = M; t.K = K; return t; };
       auto mk_b = [&](auto t) { t.p = wph; t.rows = Nn; t.K = K; t.ld = K > 0 ? K : 8; return t; };
-      const hipError_t e = dispatch_bn<ConvDgradPhaseK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
+      const hipError_t e =
+          Cout % 64 == 0 && R * S > 1 && tap_uniform_on()  // (strided 1x1: measured +3 %, kept gathered)
+              ? dispatch_bn<ConvDgradPhaseKU, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b)
+              : dispatch_bn<ConvDgradPhaseK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
       if (e != hipSuccess) return e;
     }
   }
