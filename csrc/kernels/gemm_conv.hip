@@ -1834,6 +1834,49 @@ __global__ void __launch_bounds__(256) conv_wt_transpose_kernel(const bf16_t* __
   }
 }
 
+// ------------------------------------------------------------------ dgrad phases no tap reaches
+// A strided conv's dgrad runs one launch per stride phase (dx pixels (hh*st + ph, ww*st + pw)); a phase
+// that no tap reaches (3 of 4 for a stride-2 1x1 conv) is dx = addend (ReLU-bit masked) or 0.  One
+// streaming pass, 8 channels per thread, instead of a K = 0 GEMM launch whose 128-tile staged
+// epilogue wrote them at ~2.6 TB/s (56^2 256 -> 512 / 2: 3 x ~95 us).
+__global__ void __launch_bounds__(256) dgrad_fill_phase_kernel(void* __restrict__ dx, int dx_f32,
+                                                               const bf16_t* __restrict__ addend,
+                                                               const uint8_t* __restrict__ bits, int64_t total,
+                                                               FastDiv fC8, FastDiv fWh, FastDiv fHh, int H, int W,
+                                                               int C, int st, int ph, int pw) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t tt = (uint32_t)t;  // total < 2^31 (host-checked)
+    const uint32_t pix = fdiv(tt, fC8);
+    const int c8 = (int)(tt - pix * fC8.d);
+    const uint32_t r1 = fdiv(pix, fWh);
+    const int ww = (int)(pix - r1 * fWh.d);
+    const uint32_t n = fdiv(r1, fHh);
+    const int hh = (int)(r1 - n * fHh.d);
+    const int64_t row = ((int64_t)n * H + hh * st + ph) * W + ww * st + pw;
+    const int64_t off = row * C + c8 * 8;
+    float v[8];
+    if (addend) {
+      const u16x8 a = *reinterpret_cast<const u16x8*>(addend + off);
+      const uint32_t mb = bits ? bits[off >> 3] : 0xFFu;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = (mb >> q) & 1u ? bf2f(a[q]) : 0.f;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = 0.f;
+    }
+    if (dx_f32) {
+      float* d = (float*)dx + off;
+      *reinterpret_cast<f32x4*>(d) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(d + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    } else {
+      u16x8 o;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = f2bf(v[q]);
+      *reinterpret_cast<u16x8*>((bf16_t*)dx + off) = o;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ host-side dispatch
 struct Plan {
   int bm, bn;       // 64 or 128 each
@@ -2321,6 +2364,16 @@ bool stem_fwd_on(int Cout, bool y_f32, const StemGeom& g) {
   return on && Cout == 64 && !y_f32 && g.Q <= 128;
 }
 
+// dgrad phases without taps as a fill kernel (dgrad_fill_phase_kernel).  PDA_DGRAD_FILL_PHASE=0 keeps
+// the K = 0 GEMM launches.
+bool fill_phase_on() {
+  static const bool on = [] {
+    const char* e = getenv("PDA_DGRAD_FILL_PHASE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // ConvFwdKU / ConvDgradPhaseKU (tap-uniform K tiles) for 64-multiple gathered channel counts.
 // PDA_CONV_TAP_UNIFORM=0 keeps ConvFwdK / ConvDgradPhaseK.
 bool tap_uniform_on() {
@@ -2449,6 +2502,15 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
       pg.fHh = make_fastdiv((uint32_t)Hh);
       pg.fSv = make_fastdiv((uint32_t)pg.Sv);
       const int64_t M = (int64_t)N * Hh * Wh, Nn = C, K = (int64_t)a.n * b.n * Cout;
+      if (K == 0 && fill_phase_on() && M * (C / 8) < ((int64_t)1 << 31) && C % 8 == 0) {
+        const int64_t total = M * (C / 8);
+        const int64_t blocks = (total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096;
+        dgrad_fill_phase_kernel<<<(unsigned)blocks, 256, 0, st>>>(
+            dx, cf, addend, addend_bits, total, make_fastdiv((uint32_t)(C / 8)), make_fastdiv((uint32_t)Wh),
+            make_fastdiv((uint32_t)Hh), H, W, C, stride, ph, pw);
+        PDA_CHECK_HIP(hipGetLastError());
+        continue;
+      }
       const bf16_t* wph = wt + ((int64_t)a.cum * S + (int64_t)a.n * b.cum) * C * Cout;
       Plan p = plan_gemm(M, Nn, K, false, 512);
       Epi epi{dx, C, cf, nullptr, 0, 0, nullptr};
