@@ -2522,6 +2522,15 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
       }
       auto mk_a = [&](auto t) { t.dy = dy; t.g = g; t.ph = pg; t.M = M; t.K = K; return t; };
       auto mk_b = [&](auto t) { t.p = wph; t.rows = Nn; t.K = K; t.ld = K > 0 ? K : 8; return t; };
+      if (R == 1 && S == 1 && pad == 0 && Hh == P && Wh == Q && a.n * b.n == 1 && a.base == 0 && b.base == 0 &&
+          conv_1x1_plain(1, 1, 1, 0, 1)) {
+        // a strided 1x1 conv's one live phase: dx pixel (hh*st, ww*st) = dy[hh, ww] W, i.e. dy read as the
+        // plain K-major [N*P*Q][Cout] operand (no gather), rows remapped by the epilogue
+        auto mk_ap = [&](auto t) { t.p = dy; t.rows = M; t.K = K; t.ld = Cout; return t; };
+        const hipError_t e = dispatch_bn<PlainK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_ap, mk_b);
+        if (e != hipSuccess) return e;
+        continue;
+      }
       const hipError_t e =
           Cout % 64 == 0 && R * S > 1 && tap_uniform_on()  // (strided 1x1: measured +3 %, kept gathered)
               ? dispatch_bn<ConvDgradPhaseKU, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b)
