@@ -670,6 +670,23 @@ void gemm_act(Tensor A, bool a_kmajor, int64_t lda, Tensor B, bool b_kmajor, int
                                   bpm(aux), stream_of(A)));
 }
 
+// Pipelined 256x256 GEMM (gemm_pp.hip) lab entry: C[M,N] = A[M,K] B[N,K]^T (+ bias), bf16, K-major.
+void gemm_pp_lab(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> bias, int64_t variant) {
+  check_bf16(A, "A");
+  check_bf16(B, "B");
+  check_bf16(C, "C");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && A.is_contiguous() && B.is_contiguous() && C.is_contiguous());
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K && C.size(0) == M && C.size(1) == N && K % 8 == 0 && N % 8 == 0);
+  if (bias) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N);
+  }
+  c10::DeviceGuard g(A.device());
+  CHECK_HIP_OK(pda::gemm_pp_lab(bp(A), K, bp(B), K, bpm(C), N, M, N, K, bias ? bp(*bias) : nullptr, (int)variant,
+                                stream_of(A)));
+}
+
 void conv_check(const Tensor& x, const Tensor& w) {
   check_bf16(x, "x");
   check_bf16(w, "w");
@@ -1554,6 +1571,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("fill_randint", &fill_randint);
   m.def("gemm", &gemm);
   m.def("gemm_act", &gemm_act);
+  m.def("gemm_pp_lab", &gemm_pp_lab);
   m.def("set_gemm_paths", &pda::set_gemm_paths,
         "force a GEMM kernel path: wide=-1 env default, 0 off, 1 auto, 2 force", pybind11::arg("wide"));
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),

@@ -20,6 +20,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -146,6 +148,7 @@ class Work {
     return false;
   }
   void synchronize() { check_hip(hipEventSynchronize(ev_), "hipEventSynchronize"); }
+  uintptr_t event() const { return reinterpret_cast<uintptr_t>(ev_); }
 
  private:
   int device_;
@@ -185,13 +188,9 @@ class Communicator {
       g_live.erase(this);
     }
     DeviceGuard g(device_);
-    if (comm_) {
-      if (aborted_) {
-        (void)ncclCommDestroy(comm_);
-      } else {
-        (void)hipStreamSynchronize(stream_);
-        (void)ncclCommDestroy(comm_);
-      }
+    if (comm_ && !aborted_.load()) {  // an aborted comm was released by ncclCommAbort
+      (void)hipStreamSynchronize(stream_);
+      (void)ncclCommDestroy(comm_);
     }
     if (dep_) (void)hipEventDestroy(dep_);
     // stream_ is deliberately NOT destroyed: tensors the collectives used were record_stream()-ed on it
@@ -205,7 +204,7 @@ class Communicator {
   int size() const { return nranks_; }
   int device() const { return device_; }
   uintptr_t stream() const { return reinterpret_cast<uintptr_t>(stream_); }
-  bool aborted() const { return aborted_; }
+  bool aborted() const { return aborted_.load(); }
 
   // the comm stream waits for everything queued so far on `s` (the producers of the next input)
   void wait_stream(uintptr_t s) {
@@ -215,6 +214,7 @@ class Communicator {
   }
 
   std::shared_ptr<Work> all_reduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op) {
+    std::lock_guard<std::timed_mutex> l(op_mu_);
     live();
     DeviceGuard g(device_);
     check_nccl(ncclAllReduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), (size_t)count,
@@ -225,6 +225,7 @@ class Communicator {
 
   // recv[recvcount] = op over ranks of send[rank * recvcount : (rank + 1) * recvcount]
   std::shared_ptr<Work> reduce_scatter(uintptr_t send, uintptr_t recv, int64_t recvcount, int dtype, int op) {
+    std::lock_guard<std::timed_mutex> l(op_mu_);
     live();
     DeviceGuard g(device_);
     check_nccl(ncclReduceScatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv),
@@ -235,6 +236,7 @@ class Communicator {
 
   // recv[r * sendcount : (r + 1) * sendcount] = send of rank r
   std::shared_ptr<Work> all_gather(uintptr_t send, uintptr_t recv, int64_t sendcount, int dtype) {
+    std::lock_guard<std::timed_mutex> l(op_mu_);
     live();
     DeviceGuard g(device_);
     check_nccl(ncclAllGather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), (size_t)sendcount,
@@ -244,6 +246,7 @@ class Communicator {
   }
 
   std::shared_ptr<Work> broadcast(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int root) {
+    std::lock_guard<std::timed_mutex> l(op_mu_);
     live();
     DeviceGuard g(device_);
     check_nccl(ncclBroadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), (size_t)count,
@@ -254,6 +257,7 @@ class Communicator {
 
   // point-to-point: inside group_start / group_end they are fused into one launch (returns None then)
   std::shared_ptr<Work> send(uintptr_t buf, int64_t count, int dtype, int peer) {
+    std::lock_guard<std::timed_mutex> l(op_mu_);
     live();
     DeviceGuard g(device_);
     check_nccl(ncclSend(reinterpret_cast<const void*>(buf), (size_t)count, to_nccl_dtype(dtype), peer, comm_, stream_),
@@ -262,6 +266,7 @@ class Communicator {
   }
 
   std::shared_ptr<Work> recv(uintptr_t buf, int64_t count, int dtype, int peer) {
+    std::lock_guard<std::timed_mutex> l(op_mu_);
     live();
     DeviceGuard g(device_);
     check_nccl(ncclRecv(reinterpret_cast<void*>(buf), (size_t)count, to_nccl_dtype(dtype), peer, comm_, stream_),
@@ -276,22 +281,30 @@ class Communicator {
 
   std::shared_ptr<Work> group_end() {
     if (group_depth_ == 0) throw std::runtime_error("communicator: group_end without group_start");
+    std::lock_guard<std::timed_mutex> l(op_mu_);
+    live();
     DeviceGuard g(device_);
     check_nccl(ncclGroupEnd(), "ncclGroupEnd");
     --group_depth_;
     return group_depth_ ? nullptr : done();
   }
 
-  // abort: in-flight collectives exit, further calls raise (used by the watchdog hook)
+  // abort: in-flight collectives exit, further calls raise (used by the watchdog hook, which runs on
+  // its own thread).  The flag is atomic and set first, so no enqueue starts after it; an enqueue
+  // already past its check holds op_mu_, which abort waits for (bounded: an enqueue blocked inside
+  // RCCL, e.g. on a peer that never connects, is exactly what ncclCommAbort must release).  comm_
+  // itself never changes after construction, so no thread ever reads a nulled handle.
   void abort() {
-    if (aborted_ || !comm_) return;
-    aborted_ = true;
+    bool expected = false;
+    if (!comm_ || !aborted_.compare_exchange_strong(expected, true)) return;
+    std::unique_lock<std::timed_mutex> l(op_mu_, std::defer_lock);
+    (void)l.try_lock_for(std::chrono::seconds(2));
     (void)ncclCommAbort(comm_);
-    comm_ = nullptr;
   }
 
   std::string async_error() {
-    if (!comm_) return aborted_ ? "aborted" : "";
+    if (aborted_.load()) return "aborted";
+    if (!comm_) return "";
     ncclResult_t r = ncclSuccess;
     if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
     return r == ncclSuccess || r == ncclInProgress ? "" : ncclGetErrorString(r);
@@ -301,7 +314,7 @@ class Communicator {
     std::lock_guard<std::mutex> l(g_live_mu);
     int n = 0;
     for (Communicator* c : g_live) {
-      if (!c->aborted_) {
+      if (!c->aborted_.load()) {
         c->abort();
         ++n;
       }
@@ -311,7 +324,7 @@ class Communicator {
 
  private:
   void live() const {
-    if (aborted_) throw std::runtime_error("communicator was aborted (collective timeout / abort())");
+    if (aborted_.load()) throw std::runtime_error("communicator was aborted (collective timeout / abort())");
   }
   std::shared_ptr<Work> done() { return std::make_shared<Work>(device_, stream_, pool_); }
 
@@ -321,7 +334,8 @@ class Communicator {
   hipStream_t stream_ = nullptr;
   hipEvent_t dep_ = nullptr;
   int group_depth_ = 0;
-  bool aborted_ = false;
+  std::atomic<bool> aborted_{false};
+  std::timed_mutex op_mu_;  // held across the aborted check + enqueue of every RCCL call
 };
 
 void bind_comm(pybind11::module& m) {
@@ -340,6 +354,7 @@ void bind_comm(pybind11::module& m) {
   py::class_<Work, std::shared_ptr<Work>>(m, "RcclWork")
       .def("wait", &Work::wait, py::arg("stream"))
       .def("is_completed", &Work::is_completed)
+      .def_property_readonly("event", &Work::event)
       .def("synchronize", &Work::synchronize, py::call_guard<py::gil_scoped_release>());
   py::class_<Communicator>(m, "RcclComm")
       .def(py::init([](py::bytes uid, int nranks, int rank, int device, bool high_priority) {
@@ -366,6 +381,11 @@ void bind_comm(pybind11::module& m) {
       .def("async_error", &Communicator::async_error);
   // the watchdog aborts every communicator before it acts on a timed-out collective
   pda_rt::set_abort_hook([] { Communicator::abort_all(); });
+  // event-backed watchdog tickets (DDP / FSDP / pipeline collectives) retire on completion
+  pda_rt::set_event_query([](uintptr_t ev) -> int {
+    const hipError_t e = hipEventQuery(reinterpret_cast<hipEvent_t>(ev));
+    return e == hipSuccess ? 1 : (e == hipErrorNotReady ? 0 : -1);
+  });
 }
 
 }  // namespace pda_comm

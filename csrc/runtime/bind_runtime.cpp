@@ -68,6 +68,8 @@ void bind_runtime(pybind11::module& m) {
            py::arg("action") = "abort", py::arg("exit_code") = 17, py::arg("poll") = 0.5)
       .def("arm", &Watchdog::arm, py::arg("desc"), py::arg("timeout") = -1.0)
       .def("disarm", &Watchdog::disarm)
+      .def("attach_event", &Watchdog::attach_event, py::arg("ticket"), py::arg("event"))
+      .def_property_readonly("armed", &Watchdog::armed)
       .def("pending", &Watchdog::pending)
       .def("expired", &Watchdog::expired)
       .def_property_readonly("armed_total", &Watchdog::armed_total)

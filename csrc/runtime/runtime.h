@@ -127,6 +127,9 @@ class HostRing {
 // register ncclCommAbort of every live communicator here: csrc/comm/communicator.cpp).
 void set_abort_hook(void (*hook)());
 void run_abort_hook();
+// Completion query for event-backed tickets (registered by the HIP side, csrc/comm/communicator.cpp):
+// returns 1 when the GPU event has completed, 0 when not yet, -1 on error.
+void set_event_query(int (*query)(uintptr_t event));
 
 class Watchdog {
  public:
@@ -134,6 +137,10 @@ class Watchdog {
   ~Watchdog();
   int64_t arm(const std::string& desc, double timeout_s);
   bool disarm(int64_t id);
+  // attach the completion event of the armed collective: the watchdog thread disarms the ticket by
+  // itself once the event has completed (the caller must keep the event alive until it disarms)
+  bool attach_event(int64_t id, uintptr_t event);
+  size_t armed() const;
   std::vector<std::string> pending() const;
   std::vector<std::string> expired() const;
   int64_t armed_total() const;
@@ -145,6 +152,7 @@ class Watchdog {
     std::string desc;
     double start = 0, deadline = 0;
     bool reported = false;
+    uintptr_t event = 0;
   };
   void loop();
   double timeout_s_;

@@ -23,9 +23,11 @@ namespace pda_rt {
 
 namespace {
 std::atomic<void (*)()> g_abort_hook{nullptr};
+std::atomic<int (*)(uintptr_t)> g_event_query{nullptr};
 }  // namespace
 
 void set_abort_hook(void (*hook)()) { g_abort_hook.store(hook); }
+void set_event_query(int (*query)(uintptr_t)) { g_event_query.store(query); }
 
 void run_abort_hook() {
   if (auto h = g_abort_hook.load()) h();
@@ -71,6 +73,19 @@ bool Watchdog::disarm(int64_t id) {
   return tickets_.erase(id) > 0;
 }
 
+bool Watchdog::attach_event(int64_t id, uintptr_t event) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = tickets_.find(id);
+  if (it == tickets_.end()) return false;
+  it->second.event = event;
+  return true;
+}
+
+size_t Watchdog::armed() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return tickets_.size();
+}
+
 std::vector<std::string> Watchdog::pending() const {
   std::lock_guard<std::mutex> g(mu_);
   std::vector<std::string> out;
@@ -102,6 +117,15 @@ void Watchdog::loop() {
                            std::chrono::duration_cast<std::chrono::system_clock::duration>(
                                std::chrono::duration<double>(poll_s_)));
     if (stop_) break;
+    // event-backed tickets retire themselves: a collective whose completion event has fired is done
+    // whether or not its owner ever gets back to disarm it (e.g. a DDP stage driven by a pipeline
+    // schedule, whose forward never runs the owner's sweep)
+    if (auto q = g_event_query.load()) {
+      for (auto it = tickets_.begin(); it != tickets_.end();) {
+        if (it->second.event && !it->second.reported && q(it->second.event) == 1) it = tickets_.erase(it);
+        else ++it;
+      }
+    }
     const double t = now_s();
     bool fire = false;
     for (auto& kv : tickets_) {

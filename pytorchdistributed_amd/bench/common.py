@@ -2,6 +2,7 @@
 timed-window protocol (barrier + synchronize on both sides, MAX over ranks)."""
 from __future__ import annotations
 
+import datetime
 import json
 import os
 import sys
@@ -11,6 +12,9 @@ import torch.distributed as dist
 
 from .. import distributed as pdist
 from ..utils.timing import StepTimer
+
+
+_FORCE_ENVS = ("PDA_DDP_FORCE_COMM", "PDA_FSDP_FORCE_COMM", "PDA_PP_FORCE_COMM")
 
 
 def _self_command() -> list:
@@ -78,6 +82,14 @@ def setup(n_gpus: int, one_rank_group: bool = False):
     (rank r on GPU r % count) — the whole multi-rank DDP path (hooks, buckets, collectives, timing
     protocol) runs on the native kernels of a one-GPU box; RCCL itself refuses two ranks per GPU.
     """
+    # a hung collective must end the run with stacks and an ncclCommAbort well inside the driver's own
+    # limit on a benchmark (600 s): the collective watchdog fires at 180 s, c10d's own timeout at 300 s
+    if "PDA_COLLECTIVE_TIMEOUT_S" not in os.environ:
+        os.environ["PDA_COLLECTIVE_TIMEOUT_S"] = "180"
+        from .. import config as _config
+
+        _config.set_config(None)  # re-resolve if an earlier import already loaded the config
+    os.environ.setdefault("PDA_TRACK_COMM", "1")
     if n_gpus > 1 and "WORLD_SIZE" not in os.environ:
         launch_ranks(n_gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -101,26 +113,50 @@ def setup(n_gpus: int, one_rank_group: bool = False):
     # (``one_rank_group``: the headline bench defaults to it, so N=1 times the same DDP path as N>1)
     if one_rank_group and use_gpu:
         os.environ.setdefault("PDA_DDP_FORCE_COMM", "1")
-    force = os.environ.get("PDA_DDP_FORCE_COMM") == "1" and use_gpu and backend == "nccl"
+    # (PDA_FSDP_FORCE_COMM / PDA_PP_FORCE_COMM likewise run FSDP's and the pipeline's collectives over it)
+    force = any(os.environ.get(k) == "1" for k in _FORCE_ENVS) and use_gpu and backend == "nccl"
     if (world > 1 or force) and not dist.is_initialized():
         pdist.init_process_group(backend, rank=rank, world_size=world,
-                                 device_id=gpu if use_gpu and backend == "nccl" else None)
+                                 device_id=gpu if use_gpu and backend == "nccl" else None,
+                                 timeout=datetime.timedelta(seconds=_c10d_timeout_s()))
     device = torch.device("cuda", gpu) if use_gpu else torch.device("cpu")
     if dist.is_initialized():
         _verify_group(n_gpus, backend, device)
     return rank, world, local, device
 
 
-def timed(step_fn, steps: int, warmup: int) -> float:
-    """Run ``warmup`` untimed steps, then time exactly ``steps``; returns max-over-ranks seconds."""
+def _c10d_timeout_s() -> float:
+    return float(os.environ.get("PDA_BENCH_C10D_TIMEOUT_S", "300"))
+
+
+def timed(step_fn, steps: int, warmup: int, on_start=None) -> float:
+    """Run ``warmup`` untimed steps, then time exactly ``steps``; returns max-over-ranks seconds.
+    ``on_start`` runs between the two (e.g. resetting communication counters)."""
     for _ in range(warmup):
         step_fn()
+    if on_start is not None:
+        on_start()
     t = StepTimer()
     t.start()
     for _ in range(steps):
         step_fn()
     secs = t.stop()
     return t.max_over_ranks(secs)
+
+
+def comm_record(mod, steps: int) -> dict:
+    """Per-step communication figures of a DDP / FSDP module for the JSON line: bytes and
+    collective calls per step, and — tracking on (PDA_TRACK_COMM, default 1 in the benchmarks) — the
+    compute-stream time per step spent waiting on the collectives (``exposed_comm_ms``), so a multi-GPU
+    run separates exposed communication from kernel slowdown."""
+    if mod is None or not hasattr(mod, "comm_stats"):
+        return {}
+    st = mod.comm_stats(reset=True)
+    out = {"comm_mb_per_step": round(st.get("comm_bytes", 0) / 2 ** 20 / max(steps, 1), 2),
+           "comm_calls_per_step": round(st.get("comm_calls", 0) / max(steps, 1), 2)}
+    if "exposed_comm_ms" in st:
+        out["exposed_comm_ms_per_step"] = round(st["exposed_comm_ms"] / max(steps, 1), 3)
+    return out
 
 
 def emit(record: dict, rank: int):

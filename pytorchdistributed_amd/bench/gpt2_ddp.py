@@ -15,7 +15,7 @@ from ..models.gpt2 import GPT2, config
 from ..optim import AdamW
 from ..parallel.ddp import DistributedDataParallel
 from ..utils.tunable import use_tuned_gemms
-from .common import emit, setup, teardown, timed
+from .common import comm_record, emit, setup, teardown, timed
 
 
 def main(argv=None):
@@ -46,12 +46,13 @@ def main(argv=None):
         loss.backward()
         opt.step()
 
-    secs = timed(step, a.steps, a.warmup)
+    secs = timed(step, a.steps, a.warmup, on_start=lambda: ddp.comm_stats(reset=True))
+    comm = comm_record(ddp, a.steps)
     toks = a.batch * a.seq * world * a.steps / secs
     emit({"metric": "tokens/sec (whole job) GPT-2 DDP", "value": round(toks, 1), "unit": "tokens/sec",
           "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(secs / a.steps * 1e3, 3),
           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-          "data": "synthetic tokens (on-device), random-init weights", "gemm_table": gemm_table,
+          "data": "synthetic tokens (on-device), random-init weights", "gemm_table": gemm_table, "comm": comm,
           "config": {"model": a.model + ("" if a.layers is None else f"-{a.layers}L"),
                      "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": f"dp{world}",
                      "params": model.num_params()}}, rank)

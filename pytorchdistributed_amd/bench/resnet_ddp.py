@@ -18,7 +18,7 @@ from ..models.resnet import resnet50
 from ..ops import cross_entropy
 from ..optim import SGD
 from ..parallel.ddp import DistributedDataParallel
-from .common import emit, group_info, setup, teardown, timed
+from .common import comm_record, emit, group_info, setup, teardown, timed
 
 METRIC = "images/sec (whole node) ResNet-50 DDP at 1/2/4/8 MI355X; scaling efficiency"
 
@@ -68,9 +68,11 @@ def main(argv=None):
     if device.type == "cuda" and os.environ.get("PDA_MAIN_PRIO") == "high":
         ctx = torch.cuda.stream(torch.cuda.Stream(device=device, priority=-1))
     with ctx:
-        _, _, step = build(a.batch, a.image, device, rank, bucket_mb=a.bucket_mb)
+        model, _, step = build(a.batch, a.image, device, rank, bucket_mb=a.bucket_mb)
         losses = []
-        secs = timed(lambda: losses.append(step()), a.steps, a.warmup)
+        reset = (lambda: model.comm_stats(reset=True)) if hasattr(model, "comm_stats") else None
+        secs = timed(lambda: losses.append(step()), a.steps, a.warmup, on_start=reset)
+        comm = comm_record(model, a.steps)
     # (after the timed window) a benchmark that diverged would be measuring garbage
     last = float(losses[-1].item())
     if last != last or abs(last) == float("inf"):
@@ -88,6 +90,7 @@ def main(argv=None):
                    "image_size": a.image, "seq_len": None, "parallelism": f"dp{world}",
                    "optimizer": "SGD(momentum=0.9, wd=5e-5), fp32 master weights"},
         "final_loss": round(last, 4),
+        "comm": comm,
         "notes": "reference publishes no number for this metric (BASELINE.json published={}); per-GPU batch "
                  f"{a.batch} (640 = throughput-optimal on 288 GB HBM by a 512-768 sweep; --batch 256 gives "
                  "the round-1 setting); NB03 parity numbers are produced by pytorchdistributed_amd.bench.nb03",

@@ -46,6 +46,9 @@ def _store():
     return st
 
 
+_UID_FAILED = b"pda-rccl-unique-id-failed"
+
+
 class Work:
     """Completion handle of one enqueued collective; keeps its tensors alive until completion."""
 
@@ -68,6 +71,11 @@ class Work:
         self._w.synchronize()
         self._keep = ()
 
+    @property
+    def event(self) -> int:
+        """Raw handle of the completion event (watchdog tickets retire on it)."""
+        return self._w.event
+
 
 class Communicator:
     """RCCL communicator over ``group`` (default: the world) on this rank's GPU."""
@@ -82,9 +90,10 @@ class Communicator:
         self.size = len(self.ranks)
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         if high_priority is None:
-            # default priority: a high-priority comm stream cost the one-rank headline step 0.6 %
-            # against the default (profiles/r3_comm_priority_ab.jsonl); PDA_COMM_PRIORITY=high
-            high_priority = os.environ.get("PDA_COMM_PRIORITY", "normal") == "high"
+            # one switch for every comm stream of the process (distributed.comm_high_priority)
+            from .distributed import comm_high_priority
+
+            high_priority = comm_high_priority()
         key_ranks = tuple(self.ranks)
         seq = _created.get(key_ranks, 0)
         _created[key_ranks] = seq + 1
@@ -92,11 +101,24 @@ class Communicator:
         store = _store()
         C = _native.C()
         if self.rank == 0:
-            uid = C.rccl_unique_id()
+            try:
+                uid = C.rccl_unique_id()
+            except Exception:
+                # publish the failure, so the other ranks raise (and try_for_group falls back on
+                # every rank) instead of waiting in store.get until the store times out
+                store.set(key, _UID_FAILED)
+                raise
             store.set(key, uid)
         else:
             uid = store.get(key)
-        self._c = C.RcclComm(bytes(uid), self.size, self.rank, self.device.index, high_priority)
+            if bytes(uid) == _UID_FAILED:
+                raise RuntimeError("rank 0 of the group could not create the RCCL unique id")
+        from .utils import watchdog as _watchdog
+
+        # ncclCommInitRank blocks (GIL released) until every rank joined: a peer that never does turns
+        # into a watchdog report + abort with stacks, not a silent hang
+        with _watchdog.watch(f"rccl communicator init ranks={list(key_ranks)} seq={seq}"):
+            self._c = C.RcclComm(bytes(uid), self.size, self.rank, self.device.index, high_priority)
         self.stream = torch.cuda.ExternalStream(self._c.stream, device=self.device)
 
     # ---------------------------------------------------------------- ordering

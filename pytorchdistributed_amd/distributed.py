@@ -113,6 +113,19 @@ def _env_int(name: str, default: Optional[int] = None) -> Optional[int]:
     return int(v) if v not in (None, "") else default
 
 
+def comm_high_priority() -> bool:
+    """``PDA_COMM_PRIORITY``: ``high`` (or 1 / true) puts every communication stream of this process —
+    the native RCCL communicators' (comm.py) and torch's process group's — at high priority; ``normal``
+    (default, or 0 / false) leaves them at the default priority, which measured 0.6 % faster on the
+    one-rank headline step (profiles/r3_comm_priority_ab.jsonl)."""
+    v = os.environ.get("PDA_COMM_PRIORITY", "normal").strip().lower()
+    if v in ("high", "1", "true", "yes", "on"):
+        return True
+    if v in ("normal", "0", "false", "no", "off", "low", ""):
+        return False
+    raise ValueError(f"PDA_COMM_PRIORITY={v!r}: expected high | normal")
+
+
 def init_process_group(
     backend: str = "nccl",
     init_method: Optional[str] = None,
@@ -155,10 +168,9 @@ def init_process_group(
         kwargs["init_method"] = init_method
     if device_id is not None and backend == "nccl":
         kwargs["device_id"] = torch.device("cuda", device_id)
-    if backend == "nccl" and os.environ.get("PDA_COMM_PRIORITY", "1") != "0":
-        # RCCL's internal streams at high priority (SURVEY §2.3 N01, config.comm_priority): a bucket
-        # all-reduce's kernels are dispatched ahead of queued backward kernels, so communication
-        # starts as soon as its bucket is ready instead of behind the compute stream's backlog
+    if backend == "nccl" and comm_high_priority():
+        # PDA_COMM_PRIORITY=high: RCCL's internal streams at high priority as well,
+        # the same switch as the native communicators' (comm.py)
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
         kwargs["pg_options"] = opts

@@ -266,6 +266,7 @@ class DistributedDataParallel(tnn.Module):
             work = _EventWork(done)
             self._works.append((work, None))
             self._tickets.append((ticket, work))
+            _watchdog.attach(ticket, work)
             return
         ticket = _watchdog.arm(f"ddp all_reduce bucket {b} ({nbytes / 2**20:.1f} MB, {t.dtype})")
         up = self.reduce_fp32 and t.dtype != torch.float32
@@ -286,6 +287,7 @@ class DistributedDataParallel(tnn.Module):
                 else:
                     work = c.all_reduce(t, "avg", streams=producers)
                 self._works.append((work, None))
+                _watchdog.attach(ticket, work)
             elif self.backend == "nccl":
                 # RCCL orders its stream after the CURRENT stream: make that the side stream, itself
                 # ordered after the main stream, when weight gradients are still being produced there
@@ -397,6 +399,11 @@ class DistributedDataParallel(tnn.Module):
         self._works.clear()
         if self.backend != "nccl" and self.xgmi is None:
             self._sweep_tickets(force=True)  # gloo waits were blocking: all done
+        elif self._tickets:
+            # RCCL works complete asynchronously: drop the finished ones here as well as in forward(),
+            # so the list stays bounded when forward() is not this module's entry (pipeline stages
+            # call the wrapped module directly); event-backed tickets also retire on their own
+            self._sweep_tickets()
         self._check_xgmi()
         for g in self.groups.values():
             g.pending_comm = 0

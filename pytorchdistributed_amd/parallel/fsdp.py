@@ -101,7 +101,7 @@ class _Unit:
         for (owner, name, *_rest) in self.entries:
             del owner._parameters[name]
         # world 1 with a compute-dtype shard: the shard itself is the gathered buffer (no copy, never freed)
-        self.alias = W == 1 and fsdp.shard_dtype == fsdp.param_dtype
+        self.alias = not fsdp.comm_on and fsdp.shard_dtype == fsdp.param_dtype
         self.flat = self.shard.detach() if self.alias else torch.empty(self.numel, dtype=fsdp.param_dtype,
                                                                        device=self.device)
         # flat gradient buffer (every slot is fully rewritten each backward; the alignment padding is
@@ -194,7 +194,8 @@ class _Unit:
             self.flat.untyped_storage().resize_(self.numel * self.flat.element_size())
         with torch.no_grad():
             send = self._send_buffer()
-            if self.fsdp.world == 1:
+            self.fsdp._count(self.flat)
+            if not self.fsdp.comm_on:
                 self.flat.copy_(send)
                 self.gathered = True
             elif self.fsdp.xgmi is not None:
@@ -209,7 +210,8 @@ class _Unit:
 
     def finish_gather(self):
         if self.pending_ag is not None:
-            self.pending_ag.wait()
+            with self.fsdp._exposed():
+                self.pending_ag.wait()
             self.pending_ag = None
             self.gathered = True
         elif not self.gathered:
@@ -242,6 +244,16 @@ class FullyShardedDataParallel(tnn.Module):
         self.reshard_after_forward = reshard_after_forward
         self.prefetch = prefetch
         self.nccl = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
+        # PDA_FSDP_FORCE_COMM=1: run the unit all-gathers / reduce-scatters even at world size 1 (a
+        # one-rank RCCL group on a one-GPU box executes every ncclAllGather / ncclReduceScatter, stream
+        # wait and transient buffer of the multi-GPU path instead of aliasing the shard)
+        self.comm_on = self.world > 1 or (os.environ.get("PDA_FSDP_FORCE_COMM") == "1" and dist.is_initialized())
+        # communication accounting (comm_stats): bytes / calls, and with PDA_TRACK_COMM=1 (or
+        # PDA_METRICS_DIR) the compute-stream time spent waiting on the collectives (exposed comm)
+        self.track_comm = bool(os.environ.get("PDA_METRICS_DIR")) or os.environ.get("PDA_TRACK_COMM") == "1"
+        self._stats = {"comm_bytes": 0, "comm_calls": 0}
+        self._exposed_events: List = []
+        self._deferred_release: List = []
         # ---- build units: typed submodules first (outermost match), root takes the rest
         unit_mods, seen = [], set()
         for m in module.modules():
@@ -281,13 +293,13 @@ class FullyShardedDataParallel(tnn.Module):
         # one high-priority comm stream, so a unit's reduce-scatter never makes the compute stream wait:
         # the shard gradients are collected in the final callback).  PDA_COMM=c10d: ProcessGroupNCCL.
         self.ncomm = None
-        if self.nccl and all(u.device.type == "cuda" for u in self.units) and self.world > 1:
+        if self.nccl and all(u.device.type == "cuda" for u in self.units) and self.comm_on:
             from .. import comm as _comm
 
             if _comm.enabled():
                 self.ncomm = _comm.try_for_group(process_group, self.units[0].device)
         for u in self.units:
-            u.transient_grad = self.world > 1 and u is not self.root_unit
+            u.transient_grad = self.comm_on and u is not self.root_unit
             u.release_grad()
         # ---- optional direct xGMI collectives (PDA_FSDP_COMM=ipc, one node): the unit all-gathers pull
         # every peer's shard over its own link and the gradient reduce-scatters reduce chunk `rank` of
@@ -301,6 +313,38 @@ class FullyShardedDataParallel(tnn.Module):
                 cap = max(u.numel for u in self.units) * torch.tensor([], dtype=self.param_dtype).element_size()
                 self.xgmi = _xgmi.XgmiAllReduce(capacity_mb=cap / 2 ** 20 + 1, device=self.units[0].device)
                 self._ipc_stream = torch.cuda.Stream(self.units[0].device)
+
+    # ------------------------------------------------------------ communication accounting
+    def _count(self, t: torch.Tensor):
+        if self.comm_on:
+            self._stats["comm_bytes"] += t.numel() * t.element_size()
+            self._stats["comm_calls"] += 1
+
+    @contextlib.contextmanager
+    def _exposed(self):
+        """Brackets a compute-stream wait on a collective: with tracking on, the events' elapsed time
+        is how long the compute stream sat behind the communication (SURVEY §5.1 overlap ratio)."""
+        if not (self.track_comm and self.comm_on and torch.cuda.is_available() and self.units
+                and self.units[0].device.type == "cuda"):
+            yield
+            return
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        yield
+        b.record()
+        self._exposed_events.append((a, b))
+
+    def comm_stats(self, reset: bool = True) -> dict:
+        """Bytes / calls of the unit all-gathers + reduce-scatters since the last reset and, when
+        tracking is on, ``exposed_comm_ms``: compute-stream time spent waiting on them."""
+        out = dict(self._stats)
+        if self._exposed_events:
+            self._exposed_events[-1][1].synchronize()
+            out["exposed_comm_ms"] = round(sum(a.elapsed_time(b) for a, b in self._exposed_events), 3)
+        if reset:
+            self._stats = {"comm_bytes": 0, "comm_calls": 0}
+            self._exposed_events = []
+        return out
 
     def _ipc(self, fn, producers, tensors):
         """Run ``fn`` on the IPC stream after ``producers``; returns a work handle (wait = stream wait)."""
@@ -385,7 +429,7 @@ class FullyShardedDataParallel(tnn.Module):
     # ------------------------------------------------------------ gradient reduce-scatter
     def _grad_ready(self, u: _Unit):
         grad_full = u.grad_buffer
-        if self.world == 1:
+        if not self.comm_on:
             # the shard's gradient IS the flat gradient buffer (no copy); the slots were just rewritten,
             # so a gradient still held from an earlier backward cannot be accumulated into
             if u.shard.grad is not None and u.shard.grad.data_ptr() == grad_full.data_ptr():
@@ -419,8 +463,14 @@ class FullyShardedDataParallel(tnn.Module):
                                                       async_op=True)
                 else:
                     work = dist.reduce_scatter_tensor(out, grad_full, group=self.group, async_op=True)
+        self._count(grad_full)
         self._pending_rs.append((u, work, out))
-        u.release_grad()  # the collective's stream holds the storage until it has read it
+        if self.xgmi is not None or self.ncomm is not None:
+            u.release_grad()  # record_stream on the collective's stream holds the storage until it is read
+        else:
+            # c10d: with TORCH_NCCL_AVOID_RECORD_STREAMS=1 (and on gloo) nothing ties the storage to the
+            # in-flight collective, so the release waits until _finish_rs has waited on it
+            self._deferred_release.append(u)
         if u is not self.root_unit:
             u.reshard()
         self._queue_final()
@@ -429,9 +479,14 @@ class FullyShardedDataParallel(tnn.Module):
         """Collect every queued reduce-scatter into its shard's gradient (the compute stream waits on
         the collectives here, once, at the end of backward)."""
         pending, self._pending_rs = self._pending_rs, []
+        with self._exposed():
+            for _u, work, _out in pending:
+                if work is not None:
+                    work.wait()
+        deferred, self._deferred_release = self._deferred_release, []
+        for u in deferred:
+            u.release_grad()
         for u, work, out in pending:
-            if work is not None:
-                work.wait()
             if not self.nccl and self.xgmi is None and self.world > 1:
                 out.div_(self.world)
             g = out if out.dtype == u.shard.dtype else out.to(u.shard.dtype)
@@ -509,6 +564,11 @@ class FullyShardedDataParallel(tnn.Module):
                  "params": [{"name": nm, "shape": list(e[2]), "offset": e[3], "numel": e[4]}
                             for e, nm in zip(u.entries, names)]} for u, names in zip(self.units, self.names)]}
             if optimizer is not None:
+                # which param group each unit's shard belongs to (consolidate_snapshot maps every
+                # parameter of the unit to that group)
+                for um, u in zip(meta["units"], self.units):
+                    um["param_group"] = next((gi for gi, g in enumerate(optimizer.param_groups)
+                                              if any(q is u.shard for q in g["params"])), 0)
                 st0 = sd["optim"]["unit0"]
                 meta["optimizer"] = {
                     "type": type(optimizer).__name__,
@@ -562,7 +622,13 @@ def consolidate_snapshot(directory: str, path: Optional[str] = None) -> Dict[str
     shards = [torch.load(os.path.join(directory, f"shard_{r:05d}.pt"), map_location="cpu", weights_only=True)
               for r in range(W)]
     model, ostate, pi = {}, {}, 0
+    saved_groups = shards[0].get("param_groups", [{}]) or [{}]
+    group_params: List[List[int]] = [[] for _ in saved_groups]
+    if len(saved_groups) > 1 and any("param_group" not in u for u in meta["units"]):
+        raise ValueError("checkpoint has several optimizer param groups but meta.json does not record "
+                         "which group each unit belongs to (saved by an older version)")
     for i, u in enumerate(meta["units"]):
+        gi = int(u.get("param_group", 0))
         full = torch.cat([s_[f"unit{i}"] for s_ in shards])
         opt_full = {}
         if "optim" in shards[0]:
@@ -573,13 +639,16 @@ def consolidate_snapshot(directory: str, path: Optional[str] = None) -> Dict[str
             model[p["name"]] = full[sl].view(p["shape"]).clone()
             if opt_full:
                 ostate[pi] = {k: (v[sl].view(p["shape"]).clone() if v.dim() > 0 else v) for k, v in opt_full.items()}
+            group_params[gi].append(pi)
             pi += 1
     snap: Dict[str, object] = {"MODEL_STATE": model, "EPOCHS_RUN": 0}
     if ostate:
-        groups = [dict(g) for g in shards[0].get("param_groups", [{}])]
-        for g in groups:
-            g["params"] = list(range(pi))
-        snap["OPTIMIZER_STATE"] = {"state": ostate, "param_groups": groups[:1]}
+        groups = []
+        for g, params in zip(saved_groups, group_params):
+            g = dict(g)
+            g["params"] = params
+            groups.append(g)
+        snap["OPTIMIZER_STATE"] = {"state": ostate, "param_groups": groups}
     if path is not None:
         torch.save(snap, path)
     return snap

@@ -49,6 +49,27 @@ def arm(desc: str, timeout: float = -1.0) -> int:
     return wd.arm(desc, timeout) if wd is not None else 0
 
 
+def attach(ticket: int, work) -> None:
+    """Tie an armed ticket to ``work``'s completion event, when it has one (native RCCL works, event
+    works): the native thread then disarms the ticket by itself once the collective completed, so
+    a ticket never outlives its collective even when the owner's sweep does not run (a DDP stage
+    driven by a pipeline schedule) or the process idles after its last step.  The caller keeps
+    ``work`` alive until it calls :func:`disarm`."""
+    if not ticket or _WD is None:
+        return
+    ev = getattr(work, "event", None)
+    if ev is None:
+        return
+    handle = ev if isinstance(ev, int) else getattr(ev, "cuda_event", 0)
+    if handle:
+        _WD.attach_event(ticket, int(handle))
+
+
+def armed() -> int:
+    """Tickets currently armed in this process (0 when the watchdog is off)."""
+    return _WD.armed if _WD is not None else 0
+
+
 def disarm(ticket: int):
     if ticket and _WD is not None:
         _WD.disarm(ticket)
