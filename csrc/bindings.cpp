@@ -670,21 +670,26 @@ void gemm_act(Tensor A, bool a_kmajor, int64_t lda, Tensor B, bool b_kmajor, int
                                   bpm(aux), stream_of(A)));
 }
 
-// Pipelined 256x256 GEMM (gemm_pp.hip) lab entry: C[M,N] = A[M,K] B[N,K]^T (+ bias), bf16, K-major.
-void gemm_pp_lab(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> bias, int64_t variant) {
+// Pipelined 256x256 GEMM (gemm_pp.hip) lab entry: C[M,N] = A B (+ bias), bf16; operand majorness as
+// gemm(): A(m,k) = A[m*lda+k] (a_kmajor) or A[k*lda+m]; B(k,n) = B[n*ldb+k] (b_kmajor) or B[k*ldb+n].
+void gemm_pp_lab(Tensor A, bool a_kmajor, int64_t lda, Tensor B, bool b_kmajor, int64_t ldb, Tensor C, int64_t ldc,
+                 int64_t M, int64_t N, int64_t K, c10::optional<Tensor> bias, int64_t variant) {
   check_bf16(A, "A");
   check_bf16(B, "B");
   check_bf16(C, "C");
-  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && A.is_contiguous() && B.is_contiguous() && C.is_contiguous());
-  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
-  TORCH_CHECK(B.size(1) == K && C.size(0) == M && C.size(1) == N && K % 8 == 0 && N % 8 == 0);
+  TORCH_CHECK(N % 8 == 0 && K % 8 == 0 && (a_kmajor || M % 8 == 0), "gemm_pp needs N, K (and M-major M) % 8 == 0");
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 8 == 0, "leading dims must be 16-byte multiples");
+  TORCH_CHECK((a_kmajor ? (M - 1) * lda + K : (K - 1) * lda + M) <= A.numel(), "A too small");
+  TORCH_CHECK((b_kmajor ? (N - 1) * ldb + K : (K - 1) * ldb + N) <= B.numel(), "B too small");
+  TORCH_CHECK((M - 1) * ldc + N <= C.numel(), "C too small");
+  for (auto* t : {&A, &B, &C}) check_aligned16(*t, "gemm_pp operand");
   if (bias) {
     check_bf16(*bias, "bias");
     TORCH_CHECK(bias->numel() == N);
   }
   c10::DeviceGuard g(A.device());
-  CHECK_HIP_OK(pda::gemm_pp_lab(bp(A), K, bp(B), K, bpm(C), N, M, N, K, bias ? bp(*bias) : nullptr, (int)variant,
-                                stream_of(A)));
+  CHECK_HIP_OK(pda::gemm_pp_lab(bp(A), a_kmajor, lda, bp(B), b_kmajor, ldb, bpm(C), ldc, M, N, K,
+                                bias ? bp(*bias) : nullptr, (int)variant, stream_of(A)));
 }
 
 void conv_check(const Tensor& x, const Tensor& w) {

@@ -230,8 +230,9 @@ hipError_t swiglu_bwd(const void* dy, const void* gu, void* dgu, bool bf16, int6
 hipError_t colsum_unaligned(const void* x, bool bf16, float* out, int64_t rows, int64_t cols, hipStream_t st);
 
 // ---- gemm_pp.hip (pipelined 256x256 tile; lab entry)
-hipError_t gemm_pp_lab(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int64_t M,
-                       int64_t N, int64_t K, const bf16_t* bias, int variant, hipStream_t st);
+hipError_t gemm_pp_lab(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
+                       bf16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K, const bf16_t* bias, int variant,
+                       hipStream_t st);
 
 // ---- simt_gemm.hip (dtype codes 0 fp32 / 1 bf16; arbitrary strides)
 hipError_t simt_gemm(const void* A, int a_dt, int64_t sam, int64_t sak, const void* B, int b_dt, int64_t sbk,

@@ -24,10 +24,12 @@
 //   * Index math uses precomputed multiply-shift division (no integer divides in the K loop).
 #include "pda_common.h"
 #include "pda_kernels.h"
+#include "gemm_epi.h"
 
 #include <cmath>
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace pda {
 namespace {
@@ -500,111 +502,6 @@ __device__ __forceinline__ mfma_bf16x8 read_frag(const char* tile, int row0, int
   }
 }
 
-struct Epi {
-  void* C;           // output base
-  int64_t ldc;
-  int c_f32;         // 1: fp32 output, 0: bf16 output
-  const void* bias;  // per-column bias or null
-  int bias_f32;
-  int relu;
-  float* slab;       // split-K fp32 partial slabs [splits][M][N] (overrides C when non-null)
-  // row remap (dgrad phase launches): row m = (n, hh, ww) of a [N, Hh, Wh] phase grid is written to
-  // C row (n*H + hh*st + ph)*W + ww*st + pw
-  int rm_on, rm_Hh, rm_Wh, rm_st, rm_ph, rm_pw, rm_H, rm_W;
-  // optional bf16 addend with C's layout (gradient accumulation fused into the store: conv1's dgrad
-  // adds the residual-branch gradient of a bottleneck instead of a separate add kernel)
-  const bf16_t* addend;
-  // optional ReLU bit mask of the addend (bit j of byte v masks element 8v + j of C's layout): the
-  // addend is then dz * mask, i.e. a bottleneck's residual gradient read straight from the block's
-  // output gradient and the BN's forward bit mask, never materialised by the BN backward
-  const uint8_t* addend_bits;
-  // optional BatchNorm statistics of the (bf16-rounded) output: per-tile column sums of (y - K) and
-  // (y - K)^2 (K = stats_shift, e.g. the running mean) are atomically added to row (tile_m % stats_rows)
-  // of a zero-initialised stats[stats_rows][2][N] table, which the BN finalize reads and re-zeroes.
-  float* stats;
-  const float* stats_shift;
-  int stats_rows;
-  // optional fused activation of a bf16 output (staged epilogues; no split-K): 1 = GELU-tanh forward,
-  // the pre-activation written to act_aux (C's layout) for the backward; 2 = GELU-tanh backward,
-  // C = (A B) * gelu'(act_aux) with act_aux the forward's pre-activation (the MLP's fc2 dgrad fused
-  // with the activation backward: no separate elementwise pass over two [tokens, 4d] tensors)
-  int act;
-  bf16_t* act_aux;
-};
-
-__device__ __forceinline__ void epi_act8(const Epi& e, int64_t crow, int64_t n, u16x8& v) {
-  if (e.act == 1) {
-    *reinterpret_cast<u16x8*>(e.act_aux + crow * e.ldc + n) = v;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = f2bf(gelu_tanh(bf2f(v[q])));
-  } else if (e.act == 2) {
-    const u16x8 h = *reinterpret_cast<const u16x8*>(e.act_aux + crow * e.ldc + n);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) * gelu_tanh_grad(bf2f(h[q])));
-  }
-}
-
-// One workgroup's column partials (8 consecutive columns per thread, `cpr` column chunks per row,
-// `nt` threads): fold the lanes of a wave that share a chunk, then the waves through `red` (nt/64 x
-// 8*cpr x 2 floats of LDS that nothing else uses), then one atomic add per column and statistic.
-// The only barrier is LDS-only (lgkmcnt + s_barrier): a __syncthreads() here would also wait for the
-// tile's global stores to be acknowledged (vmcnt(0)) — measured at ~16 us per wide-tile conv, since a
-// 1-workgroup-per-CU kernel exposes every epilogue cycle.
-__device__ __forceinline__ void epi_stats_flush(const Epi& epi, float (&st1)[8], float (&st2)[8], float* red, int cpr,
-                                                int nt, int tm, int64_t n0, int64_t N) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, ncol = cpr * 8;
-  for (int off = cpr; off < 64; off <<= 1)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      st1[q] += __shfl_xor(st1[q], off, 64);
-      st2[q] += __shfl_xor(st2[q], off, 64);
-    }
-  if (lane < cpr) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      red[(wid * ncol + lane * 8 + q) * 2] = st1[q];
-      red[(wid * ncol + lane * 8 + q) * 2 + 1] = st2[q];
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (tid < ncol && n0 + tid < N) {
-    float a = 0.f, b = 0.f;
-    for (int w = 0; w < nt / 64; ++w) {
-      a += red[(w * ncol + tid) * 2];
-      b += red[(w * ncol + tid) * 2 + 1];
-    }
-    float* row = epi.stats + (int64_t)(tm % epi.stats_rows) * 2 * N;
-    unsafeAtomicAdd(row + n0 + tid, a);
-    unsafeAtomicAdd(row + N + n0 + tid, b);
-  }
-}
-
-// addend (optionally bit-masked) of the 8 (or 4) consecutive elements at (crow, n), n 8- (4-) aligned
-__device__ __forceinline__ void epi_addend8(const Epi& e, int64_t crow, int64_t n, float (&a)[8]) {
-  const int64_t off = crow * e.ldc + n;
-  const u16x8 v = *reinterpret_cast<const u16x8*>(e.addend + off);
-  const uint32_t mb = e.addend_bits ? e.addend_bits[off >> 3] : 0xFFu;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) a[q] = (mb >> q) & 1u ? bf2f(v[q]) : 0.f;
-}
-__device__ __forceinline__ void epi_addend4(const Epi& e, int64_t crow, int64_t n, float (&a)[4]) {
-  const int64_t off = crow * e.ldc + n;
-  const u16x4 v = *reinterpret_cast<const u16x4*>(e.addend + off);
-  const uint32_t mb = e.addend_bits ? (uint32_t)e.addend_bits[off >> 3] >> (off & 7) : 0xFu;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) a[q] = (mb >> q) & 1u ? bf2f(v[q]) : 0.f;
-}
-
-__device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
-  if (!e.rm_on) return m;
-  const int64_t t = m / e.rm_Wh;
-  const int ww = (int)(m - t * e.rm_Wh);
-  const int64_t n = t / e.rm_Hh;
-  const int hh = (int)(t - n * e.rm_Hh);
-  return (n * e.rm_H + (int64_t)hh * e.rm_st + e.rm_ph) * e.rm_W + (int64_t)ww * e.rm_st + e.rm_pw;
-}
 
 // Counted vmcnt waits and a barrier that does not drain outstanding LDS-DMA (multi-stage pipelines:
 // `__syncthreads()` would wait for every global_load_lds with vmcnt(0)).  A three-stage variant of
@@ -1624,107 +1521,7 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
   }
   }
   __syncthreads();  // every wave is done with the operand stages before they become the staging tile
-
-  if (epi.slab || epi.c_f32) {
-    // fp32 output (split-K slab partials or an fp32 C): 16-B stores straight from the accumulators
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int64_t m = m0 + wr * 128 + 16 * i + (lane & 15);
-      if (m >= M) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
-        if (n >= N) continue;
-        f32x4 v = acc[i][j];
-        if (epi.slab) {
-          *reinterpret_cast<f32x4*>(epi.slab + (int64_t)blockIdx.y * M * N + m * N + n) = v;
-          continue;
-        }
-        const int64_t crow = epi_row(epi, m);
-        if (epi.bias) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
-        }
-        if (epi.relu) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-        }
-        if (epi.addend) {
-          float a[4];
-          epi_addend4(epi, crow, n, a);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] += a[q];
-        }
-        *reinterpret_cast<f32x4*>((float*)epi.C + crow * epi.ldc + n) = v;
-      }
-    }
-    return;
-  }
-
-  // epilogue (bf16 output): bias / relu in registers, stage through LDS, coalesced 16-B row stores
-  bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int r = wr * 128 + 16 * i + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int cc = wc * 64 + 16 * j + 4 * (lane >> 4);
-      f32x4 v = acc[i][j];
-      if (epi.bias) {
-        const int64_t n = n0 + cc;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (n + q < N)
-            v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
-      }
-      if (epi.relu) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
-      }
-      u16x4 o;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
-      *reinterpret_cast<u16x4*>(stg + r * W_SROW + cc) = o;
-    }
-  }
-  __syncthreads();
-  constexpr int CPR = 256 / 8;
-  static_assert(W_NT % CPR == 0, "a thread keeps one column chunk");
-  const bool want_stats = epi.stats != nullptr;
-  float st1[8], st2[8], kshift[8];
-  {
-    const int64_t n = n0 + (tid % CPR) * 8;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      st1[q] = st2[q] = 0.f;
-      kshift[q] = (want_stats && n + q < N) ? epi.stats_shift[n + q] : 0.f;
-    }
-  }
-  for (int c = tid; c < 256 * CPR; c += W_NT) {
-    const int r = c / CPR, ch = c % CPR;
-    const int64_t m = m0 + r, n = n0 + ch * 8;
-    if (m >= M || n >= N) continue;
-    const int64_t crow = epi_row(epi, m);
-    u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * W_SROW + ch * 8);
-    if (epi.addend) {
-      float a[8];
-      epi_addend8(epi, crow, n, a);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
-    }
-    if (epi.act) epi_act8(epi, crow, n, v);
-    if (want_stats) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float d = bf2f(v[q]) - kshift[q];
-        st1[q] += d;
-        st2[q] = fmaf(d, d, st2[q]);
-      }
-    }
-    *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
-  }
-  if (want_stats) epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + W_STATS_OFF), CPR, W_NT, tm, n0, N);
+  wide_tile_epilogue(acc, smem, W_STATS_OFF, epi, m0, n0, M, N, tm, blockIdx.y);
 }
 
 // Split-K reduction: out[m, n] = act(sum_s slab[s, m, n] + bias[n]).  A workgroup is (256 / L) output
@@ -2120,9 +1917,52 @@ hipError_t launch_wide(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t
   return hipGetLastError();
 }
 
+// Plain-operand GEMMs that take the 256 x 256 tile run on the pipelined kernel of gemm_pp.hip
+// (PDA_GEMM_PP=0: the 2-stage wide kernel above, for A/B).  Conv gathers stay on the wide kernel.
+template <class L> struct IsPlain : std::false_type {};
+template <int R> struct IsPlain<PlainK<R>> : std::true_type {};
+template <int R> struct IsPlain<PlainMN<R>> : std::true_type {};
+
+bool pp_mode() {
+  static const bool on = [] {
+    const char* e = getenv("PDA_GEMM_PP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// returns hipErrorNotSupported when the pipelined kernel cannot take the shape (the caller falls back)
+template <class LA, class LB>
+hipError_t launch_pp_plain(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st,
+                           int splits, float* slab) {
+  Epi e = epi;
+  if (splits > 1) e.slab = slab;
+  int used = splits;
+  const hipError_t r = gemm_pp(la.p, LA::kMajor, la.ld, lb.p, LB::kMajor, lb.ld, M, N, K, e, splits, -1, st, &used);
+  if (r == hipErrorInvalidValue) return hipErrorNotSupported;
+  if (r != hipSuccess || used <= 1) return r;
+  int ll = 0;
+  while (ll < 4 && (used >> ll) > 16) ++ll;
+  const int64_t per_block = 256 >> ll;
+  const int64_t g = (M * N / 4 + per_block - 1) / per_block;
+  splitk_reduce_kernel<<<(unsigned)g, 256, 0, st>>>(slab, used, M, N, ll, epi);
+  return hipGetLastError();
+}
+
 template <template <int> class TA, template <int> class TB, class MakeA, class MakeB>
 hipError_t dispatch_bn(int64_t M, int64_t N, int64_t K, const Plan& p, Epi epi, float* slab, hipStream_t st,
                        MakeA make_a, MakeB make_b) {
+  if constexpr (IsPlain<TA<64>>::value && IsPlain<TB<64>>::value) {
+    if (pp_mode()) {
+      int ws = 0;
+      if (use_wide(M, N, K, p, epi)) ws = 1;
+      else if (slab) ws = wide_splits(M, N, K, p, epi);
+      if (ws > 0) {
+        const hipError_t r = launch_pp_plain(make_a(TA<64>{}), make_b(TB<64>{}), M, N, K, epi, st, ws, slab);
+        if (r != hipErrorNotSupported) return r;
+      }
+    }
+  }
   if (use_wide(M, N, K, p, epi)) return launch_wide(make_a(TA<64>{}), make_b(TB<64>{}), M, N, K, epi, st);
   if (slab) {
     const int ws = wide_splits(M, N, K, p, epi);

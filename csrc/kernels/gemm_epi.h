@@ -1,0 +1,240 @@
+// Shared GEMM epilogue of the 256 x 256 tiles (gemm_conv.hip wide kernel, gemm_pp.hip pipelined
+// kernel): the Epi descriptor (bias / ReLU / addend / GELU / BN statistics / fp32 and split-K slab
+// outputs / dgrad row remap) and the tile epilogue for the 8-wave (2 x 4) accumulator layout
+//   acc[i][j][r] = C[m0 + wr*128 + 16 i + (lane & 15)][n0 + wc*64 + 16 j + 4 (lane >> 4) + r].
+#pragma once
+#include "pda_common.h"
+
+namespace pda {
+
+struct Epi {
+  void* C;           // output base
+  int64_t ldc;
+  int c_f32;         // 1: fp32 output, 0: bf16 output
+  const void* bias;  // per-column bias or null
+  int bias_f32;
+  int relu;
+  float* slab;       // split-K fp32 partial slabs [splits][M][N] (overrides C when non-null)
+  // row remap (dgrad phase launches): row m = (n, hh, ww) of a [N, Hh, Wh] phase grid is written to
+  // C row (n*H + hh*st + ph)*W + ww*st + pw
+  int rm_on, rm_Hh, rm_Wh, rm_st, rm_ph, rm_pw, rm_H, rm_W;
+  // optional bf16 addend with C's layout (gradient accumulation fused into the store: conv1's dgrad
+  // adds the residual-branch gradient of a bottleneck instead of a separate add kernel)
+  const bf16_t* addend;
+  // optional ReLU bit mask of the addend (bit j of byte v masks element 8v + j of C's layout): the
+  // addend is then dz * mask, i.e. a bottleneck's residual gradient read straight from the block's
+  // output gradient and the BN's forward bit mask, never materialised by the BN backward
+  const uint8_t* addend_bits;
+  // optional BatchNorm statistics of the (bf16-rounded) output: per-tile column sums of (y - K) and
+  // (y - K)^2 (K = stats_shift, e.g. the running mean) are atomically added to row (tile_m % stats_rows)
+  // of a zero-initialised stats[stats_rows][2][N] table, which the BN finalize reads and re-zeroes.
+  float* stats;
+  const float* stats_shift;
+  int stats_rows;
+  // optional fused activation of a bf16 output (staged epilogues; no split-K): 1 = GELU-tanh forward,
+  // the pre-activation written to act_aux (C's layout) for the backward; 2 = GELU-tanh backward,
+  // C = (A B) * gelu'(act_aux) with act_aux the forward's pre-activation (the MLP's fc2 dgrad fused
+  // with the activation backward: no separate elementwise pass over two [tokens, 4d] tensors)
+  int act;
+  bf16_t* act_aux;
+};
+
+// The pipelined 256 x 256 GEMM (gemm_pp.hip); gemm_conv.hip routes plain GEMMs to it.
+hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
+                   int64_t M, int64_t N, int64_t K, const Epi& epi, int splits, int variant, hipStream_t st,
+                   int* used_splits);
+int pp_default_variant();
+
+namespace {
+
+
+__device__ __forceinline__ void epi_act8(const Epi& e, int64_t crow, int64_t n, u16x8& v) {
+  if (e.act == 1) {
+    *reinterpret_cast<u16x8*>(e.act_aux + crow * e.ldc + n) = v;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = f2bf(gelu_tanh(bf2f(v[q])));
+  } else if (e.act == 2) {
+    const u16x8 h = *reinterpret_cast<const u16x8*>(e.act_aux + crow * e.ldc + n);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) * gelu_tanh_grad(bf2f(h[q])));
+  }
+}
+
+// One workgroup's column partials (8 consecutive columns per thread, `cpr` column chunks per row,
+// `nt` threads): fold the lanes of a wave that share a chunk, then the waves through `red` (nt/64 x
+// 8*cpr x 2 floats of LDS that nothing else uses), then one atomic add per column and statistic.
+// The only barrier is LDS-only (lgkmcnt + s_barrier): a __syncthreads() here would also wait for the
+// tile's global stores to be acknowledged (vmcnt(0)) — measured at ~16 us per wide-tile conv, since a
+// 1-workgroup-per-CU kernel exposes every epilogue cycle.
+__device__ __forceinline__ void epi_stats_flush(const Epi& epi, float (&st1)[8], float (&st2)[8], float* red, int cpr,
+                                                int nt, int tm, int64_t n0, int64_t N) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, ncol = cpr * 8;
+  for (int off = cpr; off < 64; off <<= 1)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      st1[q] += __shfl_xor(st1[q], off, 64);
+      st2[q] += __shfl_xor(st2[q], off, 64);
+    }
+  if (lane < cpr) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      red[(wid * ncol + lane * 8 + q) * 2] = st1[q];
+      red[(wid * ncol + lane * 8 + q) * 2 + 1] = st2[q];
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (tid < ncol && n0 + tid < N) {
+    float a = 0.f, b = 0.f;
+    for (int w = 0; w < nt / 64; ++w) {
+      a += red[(w * ncol + tid) * 2];
+      b += red[(w * ncol + tid) * 2 + 1];
+    }
+    float* row = epi.stats + (int64_t)(tm % epi.stats_rows) * 2 * N;
+    unsafeAtomicAdd(row + n0 + tid, a);
+    unsafeAtomicAdd(row + N + n0 + tid, b);
+  }
+}
+
+// addend (optionally bit-masked) of the 8 (or 4) consecutive elements at (crow, n), n 8- (4-) aligned
+__device__ __forceinline__ void epi_addend8(const Epi& e, int64_t crow, int64_t n, float (&a)[8]) {
+  const int64_t off = crow * e.ldc + n;
+  const u16x8 v = *reinterpret_cast<const u16x8*>(e.addend + off);
+  const uint32_t mb = e.addend_bits ? e.addend_bits[off >> 3] : 0xFFu;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) a[q] = (mb >> q) & 1u ? bf2f(v[q]) : 0.f;
+}
+__device__ __forceinline__ void epi_addend4(const Epi& e, int64_t crow, int64_t n, float (&a)[4]) {
+  const int64_t off = crow * e.ldc + n;
+  const u16x4 v = *reinterpret_cast<const u16x4*>(e.addend + off);
+  const uint32_t mb = e.addend_bits ? (uint32_t)e.addend_bits[off >> 3] >> (off & 7) : 0xFu;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) a[q] = (mb >> q) & 1u ? bf2f(v[q]) : 0.f;
+}
+
+__device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
+  if (!e.rm_on) return m;
+  const int64_t t = m / e.rm_Wh;
+  const int ww = (int)(m - t * e.rm_Wh);
+  const int64_t n = t / e.rm_Hh;
+  const int hh = (int)(t - n * e.rm_Hh);
+  return (n * e.rm_H + (int64_t)hh * e.rm_st + e.rm_ph) * e.rm_W + (int64_t)ww * e.rm_st + e.rm_pw;
+}
+
+constexpr int WT_NT = 512;          // threads of a 256 x 256 tile workgroup
+constexpr int WT_SROW = 256 + 8;    // epilogue staging row (bf16 elements)
+constexpr int WT_STAGE_BYTES = 256 * WT_SROW * 2;
+constexpr int WT_STATS_BYTES = (WT_NT / 64) * 256 * 2 * 4;  // BN-statistics scratch
+
+// Epilogue of one 256 x 256 tile.  `smem` must hold WT_STAGE_BYTES (bf16 staging) and, at `stats_off`,
+// WT_STATS_BYTES; the caller guarantees every wave is done with the operand LDS (and no LDS-DMA is in
+// flight).  `split` = blockIdx.y of a split-K launch (slab index).
+__device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][4], char* smem, int stats_off, const Epi& epi,
+                                                   int64_t m0, int64_t n0, int64_t M, int64_t N, int tm, int split) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  if (epi.slab || epi.c_f32) {
+    // fp32 output (split-K slab partials or an fp32 C): 16-B stores straight from the accumulators
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t m = m0 + wr * 128 + 16 * i + (lane & 15);
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
+        if (n >= N) continue;
+        f32x4 v = acc[i][j];
+        if (epi.slab) {
+          *reinterpret_cast<f32x4*>(epi.slab + (int64_t)split * M * N + m * N + n) = v;
+          continue;
+        }
+        const int64_t crow = epi_row(epi, m);
+        if (epi.bias) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
+        }
+        if (epi.relu) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+        }
+        if (epi.addend) {
+          float a[4];
+          epi_addend4(epi, crow, n, a);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] += a[q];
+        }
+        *reinterpret_cast<f32x4*>((float*)epi.C + crow * epi.ldc + n) = v;
+      }
+    }
+    return;
+  }
+
+  // epilogue (bf16 output): bias / relu in registers, stage through LDS, coalesced 16-B row stores
+  bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = wr * 128 + 16 * i + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int cc = wc * 64 + 16 * j + 4 * (lane >> 4);
+      f32x4 v = acc[i][j];
+      if (epi.bias) {
+        const int64_t n = n0 + cc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (n + q < N)
+            v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
+      }
+      if (epi.relu) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+      }
+      u16x4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
+      *reinterpret_cast<u16x4*>(stg + r * WT_SROW + cc) = o;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = 256 / 8;
+  static_assert(WT_NT % CPR == 0, "a thread keeps one column chunk");
+  const bool want_stats = epi.stats != nullptr;
+  float st1[8], st2[8], kshift[8];
+  {
+    const int64_t n = n0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      st1[q] = st2[q] = 0.f;
+      kshift[q] = (want_stats && n + q < N) ? epi.stats_shift[n + q] : 0.f;
+    }
+  }
+  for (int c = tid; c < 256 * CPR; c += WT_NT) {
+    const int r = c / CPR, ch = c % CPR;
+    const int64_t m = m0 + r, n = n0 + ch * 8;
+    if (m >= M || n >= N) continue;
+    const int64_t crow = epi_row(epi, m);
+    u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * WT_SROW + ch * 8);
+    if (epi.addend) {
+      float a[8];
+      epi_addend8(epi, crow, n, a);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
+    }
+    if (epi.act) epi_act8(epi, crow, n, v);
+    if (want_stats) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float d = bf2f(v[q]) - kshift[q];
+        st1[q] += d;
+        st2[q] = fmaf(d, d, st2[q]);
+      }
+    }
+    *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
+  }
+  if (want_stats) epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + stats_off), CPR, WT_NT, tm, n0, N);
+}
+
+}  // namespace
+}  // namespace pda

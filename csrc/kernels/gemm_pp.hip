@@ -1,28 +1,34 @@
-// Pipelined 256 x 256 bf16 GEMM main loop for gfx950 (VERDICT r3 "what's next" #1).
+// Pipelined 256 x 256 bf16 GEMM for gfx950 (VERDICT r3 "next" #1).
 //
-// Why a new loop (profiles/r3_conv_roofline_bs640.md): the 2-stage wide kernel of gemm_conv.hip ends
-// every 64-deep K step with `vmcnt(0)` + a workgroup barrier and issues each K step's 64 KB of
-// LDS-DMA in one burst in lockstep on all 8 waves, so the matrix pipe idles while both waves of a
-// SIMD issue DMAs and while they wait: 53 % MFMA busy at 4096^3.
+// Why a new main loop (profiles/r3_conv_roofline_bs640.md): the 2-stage wide kernel of gemm_conv.hip
+// ends every 64-deep K step with `vmcnt(0)` + a workgroup barrier and issues each step's 64 KB of
+// LDS-DMA in one burst, in lockstep on all 8 waves, so the matrix pipe idles while both waves of a SIMD
+// issue DMAs and while they wait: 53 % MFMA busy at 4096^3.
 //
-// Structure here (cdna_hip_programming.md §5 "256^2 8-phase template", T2/T3/T4/T5):
-//   * 512 threads = 8 waves, 2 (M) x 4 (N); each wave owns a 128 x 64 output (acc[8][4], 16x16x32 MFMA).
+// Structure (cdna_hip_programming.md §5 "256^2 8-phase template", T2/T3/T4/T5):
+//   * 512 threads = 8 waves, 2 (M) x 4 (N); each wave owns a 128 x 64 output (acc[8][4], 16x16x32 MFMA),
+//     the accumulator layout of the shared 256 x 256 epilogue (gemm_epi.h).
 //   * The LDS holds two K-tile slots of four 16 KB "half" images each: Ah0 / Ah1 are the rows
 //     {0-63, 128-191} / {64-127, 192-255} of the A tile (every wave's first / second 64-row quadrant
-//     row), Bh0 / Bh1 the columns {32-wide first / second half of every wave's 64 columns}.
+//     row), Bh0 / Bh1 the columns {first / second 32 of every wave's 64 columns}.
 //   * A K tile is 4 phases of 16 MFMAs, quadrants (a0,b0) (a0,b1) (a1,b1) (a1,b0).  Each phase reads
-//     one operand quadrant into registers (8 or 4 ds_read_b128), so each half image is released after
-//     ONE phase: Bh0 after phase 3 of the previous tile (b0 is kept in registers), Ah0 after phase 0,
-//     Bh1 after 1, Ah1 after 2.  The very next phase refills it with K tile t+2 (2 LDS-DMA per thread),
-//     so 7 half images (~1.75 K tiles) stay in flight and every wait is the same counted `vmcnt(12)`
-//     — never 0 inside the loop.
+//     one operand quadrant into registers, so each half image is released after ONE phase: Bh0 after
+//     phase 3 of the previous tile (b0 stays in registers), Ah0 after phase 0, Bh1 after 1, Ah1 after 2.
+//     The very next phase refills it with K tile t+2 (2 LDS-DMA per thread), so 7 half images (~1.75 K
+//     tiles) stay in flight and every wait in the loop is the same counted `vmcnt(12)` — never 0.
 //   * Ping-pong: waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave issues its
-//     fragment reads + DMAs (load section) while its partner runs 16 MFMAs (compute section).
+//     fragment reads + DMAs (load section) while its partner runs its 16 MFMAs (compute section).
 //   * Operands come through buffer descriptors (`buffer_load_dwordx4 ... lds`): one 32-bit offset per
-//     lane and operand, rows past M / N and K past the end read as zero (hardware range check).
+//     lane and DMA; rows past M / N, K past the end and invalid columns read as zero.
+//   * K-major operands ([rows][K]) are [128][64] images read with ds_read_b128 (16-B chunks XOR-swizzled
+//     by row pair); MN-major operands ([K][rows], the weight gradient's dY^T and X) are [64 k][128]
+//     images read with ds_read_b64_tr_b16 (32-B slots XOR-swizzled by k) — no transpose pass.
 #include "pda_common.h"
 #include "pda_kernels.h"
+#include "gemm_epi.h"
 
+#include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace pda {
@@ -34,30 +40,63 @@ constexpr int PP_NT = 512;
 constexpr int PP_HALF = 128 * 64 * 2;  // one half image: 128 rows x 64 k, bf16
 constexpr int PP_SLOT = 4 * PP_HALF;   // Ah0 Ah1 Bh0 Bh1
 constexpr int PP_LDS_LOOP = 2 * PP_SLOT;
-constexpr int PP_SROW = 256 + 8;  // epilogue staging row (bf16 elements)
-constexpr int PP_LDS = PP_LDS_LOOP > 256 * PP_SROW * 2 ? PP_LDS_LOOP : 256 * PP_SROW * 2;
+constexpr int PP_STATS_OFF = WT_STAGE_BYTES > PP_LDS_LOOP ? WT_STAGE_BYTES : PP_LDS_LOOP;
+constexpr int PP_LDS = PP_STATS_OFF + WT_STATS_BYTES;
+static_assert(PP_LDS <= 160 * 1024, "LDS budget");
 constexpr uint32_t PP_OOB = 0x80000000u;  // an offset past every descriptor's range: reads zero
 
 enum { H_A0 = 0, H_A1 = 1, H_B0 = 2, H_B1 = 3 };
 
-// K-major [128][64] half image: 128-B rows, 16-B chunk XOR ((row >> 1) & 7) (conflict-free for the
-// 16-row x 4-chunk pattern of a 16x16x32 fragment read, see gemm_conv.hip kmaj_off)
-__device__ __forceinline__ int pp_off(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
-
-// Fragment of the 16 rows starting at row0 (a multiple of 16) for k-substep kk: lane l holds
-// (row0 + (l & 15), kk + 8 (l >> 4) + j).  For such rows the XOR key ((row >> 1) & 7) = (l >> 1) & 7
-// does not depend on row0, so the lane part of the address is one of two per-lane offsets (kk = 0 / 32)
-// and row0 / the half base fold into the instruction's immediate offset.
-__device__ __forceinline__ int pp_lane_off(int lane, int kk) {
+// ---- K-major [128][64] half image: 128-B rows, 16-B chunk XOR ((row >> 1) & 7) (gemm_conv.hip kmaj_off).
+// Fragment of the 16 rows from row0 (a multiple of 16), k-substep kk: lane l holds (row0 + (l & 15),
+// kk + 8 (l >> 4) + j).  For such rows the XOR key is (l >> 1) & 7 whatever row0 is, so the lane part of
+// the address is one of two per-lane offsets (kk = 0 / 32) and row0 folds into the immediate offset.
+__device__ __forceinline__ int pp_klane(int lane, int kk) {
   const int key = (lane >> 1) & 7, chunk = (kk >> 3) + (lane >> 4);
   return (lane & 15) * 128 + ((chunk ^ key) << 4);
 }
-__device__ __forceinline__ ppbf16x8 pp_frag(const char* half, int row0, int loff) {
+__device__ __forceinline__ ppbf16x8 pp_kfrag(const char* half, int row0, int loff) {
   return *reinterpret_cast<const ppbf16x8*>(half + row0 * 128 + loff);
+}
+
+// ---- MN-major [64 k][128] half image: 256-B k-rows, 32-B slots (16 rows) XOR-swizzled by k
+// (gemm_conv.hip mn_off<128>).  Thread t of a DMA round fills k-row t / 16 (+ 32 per round), slot t % 16.
+__device__ __forceinline__ int pp_mn_swz(int k) { return (k & 3) | (((k >> 3) & 1) << 2); }
+__device__ __forceinline__ int pp_mn_col(int t) {  // logical column (multiple of 8) that thread t fetches
+  const int p = t & 15, k = t >> 4;
+  return ((((p >> 1) ^ pp_mn_swz(k)) & 7) << 4) + (p & 1) * 8;
+}
+// Fragment (same register layout as the K-major one) by two transposing 8-byte reads: lane l = (g, i)
+// reads k-rows kk + 8 g + (i >> 2) (+ 4) at rows row0 + 4 (i & 3) .. + 3.  For row0 a multiple of 16 the
+// swizzle key depends on the lane only ((i >> 2) | ((g & 1) << 2)); the row group r = row0 / 16 enters
+// as (r ^ key) & 7.
+typedef short pp_s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) pp_s16x4 pp_lds_s16x4;
+__device__ __forceinline__ ppbf16x8 pp_mfrag(const char* half, int r, int kk, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const int key = (i >> 2) | ((g & 1) << 2);
+  const int k1 = kk + 8 * g + (i >> 2);
+  const int off = k1 * 256 + (((r ^ key) & 7) << 5) + ((i & 3) << 3);
+  const pp_s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((pp_lds_s16x4*)(half + off));
+  const pp_s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((pp_lds_s16x4*)(half + off + 4 * 256));
+  return __builtin_bit_cast(ppbf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 __device__ __forceinline__ void pp_glds(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+
+// The same DMA as inline asm, for kernels that read an MN-major image with ds_read_b64_tr_b16: beside
+// a compiler-visible LDS-DMA, hipcc (ROCm 7.2) puts `s_waitcnt vmcnt(0)` in front of every transposing
+// LDS read (it cannot tell them apart from the DMA's LDS range), which drains the whole pipeline each
+// phase.  Hidden in asm, the DMA is ordered by this kernel's own counted vmcnt waits only (no other
+// vector-memory op is in flight in the K loop; the loop drains with vmcnt(0) before the epilogue).
+typedef int pp_i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void pp_glds_asm(pp_i32x4 r, uint32_t lds, uint32_t voff) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+               :
+               : "v"(voff), "s"(r), "s"(lds)
+               : "memory", "m0");
 }
 
 __device__ __forceinline__ void pp_sync() {
@@ -80,17 +119,85 @@ __device__ __forceinline__ void pp_mma(f32x4 (&acc)[8][4], const ppbf16x8 (&a)[8
   if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
 }
 
-struct PPArgs {
-  const bf16_t* A;
-  const bf16_t* B;
-  bf16_t* C;
-  const bf16_t* bias;
-  int64_t lda, ldb, ldc;
-  int M, N, K, tiles_n;
+// One operand: element (row, k) = p[row * ld + k] (K-major) or p[k * ld + row] (MN-major); `rows` = M
+// (operand A) or N (operand B).
+struct PPOp {
+  const bf16_t* p;
+  int64_t ld, rows;
 };
 
+struct PPArgs {
+  PPOp a, b;
+  int64_t M, N, K;
+  int tiles_n, kt_per_split;
+  Epi epi;
+};
+
+// Per-lane DMA source of one operand for this workgroup: a buffer descriptor over its panel (from the
+// tile's first row and the split's first K element), the lane's offset for (half 0, round 0), and the
+// uniform offsets of half 1 / round 1 / one K tile.
+struct PPSrc {
+  __amdgpu_buffer_rsrc_t r;
+  pp_i32x4 rs;  // the same descriptor as four words (inline-asm DMA)
+  uint32_t v, dh, di, dk;
+  // K-major: the lane's chunk is in range for K tile t iff t * 64 < lim (rows past the operand lie past
+  // the descriptor's range).  MN-major: rows left from the lane's first column (half h is in range iff
+  // lim > h * half stride); K past the end lies past the descriptor's range.
+  int lim;
+};
+
+__device__ __forceinline__ pp_i32x4 pp_rsrc_words(const bf16_t* base, int64_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  pp_i32x4 w;
+  w[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  w[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));  // stride 0
+  w[2] = __builtin_amdgcn_readfirstlane((int)(bytes < 0x7fffffff ? bytes : 0x7fffffff));
+  w[3] = 0x00020000;
+  return w;
+}
+
+template <bool KMAJ, bool IS_A>
+__device__ __forceinline__ PPSrc pp_src(const PPOp& op, int64_t r0, int64_t k0, int64_t K, int wid, int lane) {
+  PPSrc s;
+  const int tid = wid * 64 + lane;
+  if constexpr (KMAJ) {
+    // image row R = round*64 + wid*8 + lane/8 holds logical chunk (lane & 7) ^ ((R >> 1) & 7); it is
+    // tile row (R/64)*128 + h*64 + R%64 (A) or (R/32)*64 + h*32 + R%32 (B)
+    const int chunk = (lane & 7) ^ ((wid * 4 + (lane >> 4)) & 7);
+    const int rr = IS_A ? wid * 8 + (lane >> 3) : (wid >> 2) * 64 + (wid & 3) * 8 + (lane >> 3);
+    const bf16_t* base = op.p + r0 * op.ld + k0;
+    const int64_t rem = (((op.rows - r0) - 1) * op.ld + (K - k0)) * 2;
+    s.r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(rem < 0x7fffffff ? rem : 0x7fffffff),
+                                            0x00020000);
+    s.rs = pp_rsrc_words(base, rem);
+    s.v = (uint32_t)((rr * op.ld + chunk * 8) * 2);
+    s.dh = (uint32_t)((IS_A ? 64 : 32) * op.ld * 2);
+    s.di = (uint32_t)(128 * op.ld * 2);
+    s.dk = 128u;
+    s.lim = (int)(K - k0) - chunk * 8;
+  } else {
+    // image k-row round*32 + tid/16 holds the 8 logical columns from pp_mn_col(tid): tile row
+    // (lc/64)*128 + h*64 + lc%64 (A) or (lc/32)*64 + h*32 + lc%32 (B)
+    const int lc = pp_mn_col(tid);
+    const int rr = IS_A ? (lc >> 6) * 128 + (lc & 63) : (lc >> 5) * 64 + (lc & 31);
+    const int kr = tid >> 4;
+    const bf16_t* base = op.p + k0 * op.ld + r0;
+    const int64_t rem = (((K - k0) - 1) * op.ld + (op.rows - r0)) * 2;
+    s.r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(rem < 0x7fffffff ? rem : 0x7fffffff),
+                                            0x00020000);
+    s.rs = pp_rsrc_words(base, rem);
+    s.v = (uint32_t)((kr * op.ld + rr) * 2);
+    s.dh = (uint32_t)((IS_A ? 64 : 32) * 2);
+    s.di = (uint32_t)(32 * op.ld * 2);
+    s.dk = (uint32_t)(64 * op.ld * 2);
+    const int64_t left = op.rows - r0 - rr;
+    s.lim = left > 0x7fffffff ? 0x7fffffff : (int)left;
+  }
+  return s;
+}
+
 // VAR bits: 1 = s_setprio(1) around each MFMA section, 2 = ping-pong stagger of the two wave groups
-template <int VAR>
+template <bool AK, bool BK, int VAR>
 __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -98,75 +205,83 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   const int wr = wid >> 2, wc = wid & 3;
   constexpr bool STAGGER = (VAR & 2) != 0;
   const bool lag = STAGGER && wr == 1;
+  constexpr bool EARLY = !AK;  // see ktile
+  constexpr bool ASM_DMA = !(AK && BK);  // see pp_glds_asm
 
   const int ntiles = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, ntiles);
   int tm, tn;
   grouped_tile(tile, ntiles / p.tiles_n, p.tiles_n, 8, tm, tn);
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int K = p.K;
-  const int nk = (K + 63) >> 6;
+  const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
+  const int ktiles = (int)((p.K + 63) >> 6);
+  const int kt0 = blockIdx.y * p.kt_per_split;
+  const int nk = min(ktiles, kt0 + p.kt_per_split) - kt0;  // K tiles of this split
+  const int64_t k0 = (int64_t)kt0 * 64;
 
-  // descriptors over this tile's row panels; num_records = bytes from the panel start to the end of
-  // the operand, so rows >= M (N) fall outside the range and read as zero
-  const int64_t a_rem = ((int64_t)(p.M - m0) - 1) * p.lda * 2 + (int64_t)K * 2;
-  const int64_t b_rem = ((int64_t)(p.N - n0) - 1) * p.ldb * 2 + (int64_t)K * 2;
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.A + (int64_t)m0 * p.lda), (short)0, (int)(a_rem < 0x7fffffff ? a_rem : 0x7fffffff), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(p.B + (int64_t)n0 * p.ldb), (short)0, (int)(b_rem < 0x7fffffff ? b_rem : 0x7fffffff), 0x00020000);
+  const PPSrc sa = pp_src<AK, true>(p.a, m0, k0, p.K, wid, lane);
+  const PPSrc sb = pp_src<BK, false>(p.b, n0, k0, p.K, wid, lane);
 
-  // this lane's source (row, chunk) for LDS-DMA round 0 of half 0: image row R = i*64 + wid*8 + lane/8
-  // holds logical chunk (lane & 7) ^ ((R >> 1) & 7) at slot lane & 7
-  const int chunk = (lane & 7) ^ ((wid * 4 + (lane >> 4)) & 7);
-  const int kc = chunk * 8;
-  const int klim = K - kc;  // K tile t is in range for this lane's chunk iff t * 64 < klim
-  // A image row R of half h -> tile row (R >> 6) * 128 + h * 64 + (R & 63)
-  const uint32_t a_v = (uint32_t)(((int64_t)(wid * 8 + (lane >> 3)) * p.lda + kc) * 2);
-  const uint32_t a_h = (uint32_t)(64 * p.lda * 2), a_i = (uint32_t)(128 * p.lda * 2);
-  // B image row R of half h -> tile column (R >> 5) * 64 + h * 32 + (R & 31)
-  const uint32_t b_v = (uint32_t)(((int64_t)((wid >> 2) * 64 + (wid & 3) * 8 + (lane >> 3)) * p.ldb + kc) * 2);
-  const uint32_t b_h = (uint32_t)(32 * p.ldb * 2), b_i = (uint32_t)(128 * p.ldb * 2);
-
-  auto issue = [&](auto hid_c, int t) {
+  // one half image of K tile t (of this split): 2 DMAs per thread; tiles past the split read zero
+  // (t & 1) == SLOT at every call site: the slot offsets fold into immediates
+  auto issue = [&](auto hid_c, auto slot_c, int t) {
     constexpr int hid = decltype(hid_c)::value;
-    char* dst = smem + (t & 1) * PP_SLOT + hid * PP_HALF + wid * 1024;
-    const bool kv = t * 64 < klim;
-    const uint32_t kb = (uint32_t)t * 128u;
-    if constexpr (hid < 2) {
-      const uint32_t o = a_v + (hid & 1) * a_h + kb;
-      pp_glds(ra, dst, kv ? o : PP_OOB);
-      pp_glds(ra, dst + 8192, kv ? o + a_i : PP_OOB);
+    constexpr int SLOT = decltype(slot_c)::value;
+    constexpr bool isA = hid < 2;
+    constexpr bool km = isA ? AK : BK;
+    const PPSrc& s = isA ? sa : sb;
+    char* dst = smem + SLOT * PP_SLOT + hid * PP_HALF + wid * 1024;
+    const uint32_t o = s.v + (hid & 1) * s.dh + (uint32_t)t * s.dk;
+    bool kv;
+    if constexpr (km) kv = t * 64 < s.lim && t < nk;
+    else kv = t < nk && s.lim > (hid & 1) * (isA ? 64 : 32);
+    if constexpr (ASM_DMA) {
+      const uint32_t l = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)dst);
+      pp_glds_asm(s.rs, l, kv ? o : PP_OOB);
+      pp_glds_asm(s.rs, l + 8192, kv ? o + s.di : PP_OOB);
     } else {
-      const uint32_t o = b_v + (hid & 1) * b_h + kb;
-      pp_glds(rb, dst, kv ? o : PP_OOB);
-      pp_glds(rb, dst + 8192, kv ? o + b_i : PP_OOB);
+      pp_glds(s.r, dst, kv ? o : PP_OOB);
+      pp_glds(s.r, dst + 8192, kv ? o + s.di : PP_OOB);
     }
   };
   using HA0 = std::integral_constant<int, H_A0>;
   using HA1 = std::integral_constant<int, H_A1>;
   using HB0 = std::integral_constant<int, H_B0>;
   using HB1 = std::integral_constant<int, H_B1>;
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
 
-  const int loff0 = pp_lane_off(lane, 0), loff1 = pp_lane_off(lane, 32);
+  const int kl0 = pp_klane(lane, 0), kl1 = pp_klane(lane, 32);
   auto rd_a = [&](const char* half, ppbf16x8 (&f)[8]) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) f[kk * 4 + i] = pp_frag(half, wr * 64 + 16 * i, kk ? loff1 : loff0);
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (AK) f[kk * 4 + i] = pp_kfrag(half, wr * 64 + 16 * i, kk ? kl1 : kl0);
+        else f[kk * 4 + i] = pp_mfrag(half, wr * 4 + i, kk * 32, lane);
+      }
   };
   auto rd_b = [&](const char* half, ppbf16x8 (&f)[4]) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) f[kk * 2 + j] = pp_frag(half, wc * 32 + 16 * j, kk ? loff1 : loff0);
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (BK) f[kk * 2 + j] = pp_kfrag(half, wc * 32 + 16 * j, kk ? kl1 : kl0);
+        else f[kk * 2 + j] = pp_mfrag(half, wc * 2 + j, kk * 32, lane);
+      }
   };
   // end of a load section: own DMAs of the half read next are done, own fragment reads are done
-  auto end_load = [&]() {
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  auto end_load = [&](auto vm_c) {
+    constexpr int VM = decltype(vm_c)::value;
+    if constexpr (VM == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if constexpr (VM == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else static_assert(VM == -1, "vmcnt literal");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     pp_sync();
   };
+  using VM10 = std::integral_constant<int, 10>;
+  using VM12 = std::integral_constant<int, 12>;
+  using VMNONE = std::integral_constant<int, -1>;
   auto end_mma = [&]() {
     if constexpr (STAGGER) pp_sync();
   };
@@ -179,116 +294,167 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
 
   ppbf16x8 fa[8], fb1[4], fb0e[4], fb0o[4];
   // prologue: K tiles 0 and 1 in the steady-state issue order (Bh0, Ah0, Bh1, Ah1)
-  issue(HB0{}, 0);
-  issue(HA0{}, 0);
-  issue(HB1{}, 0);
-  issue(HA1{}, 0);
-  issue(HB0{}, 1);
-  issue(HA0{}, 1);
-  issue(HB1{}, 1);
-  issue(HA1{}, 1);
+  issue(HB0{}, S0{}, 0);
+  issue(HA0{}, S0{}, 0);
+  issue(HB1{}, S0{}, 0);
+  issue(HA1{}, S0{}, 0);
+  issue(HB0{}, S1{}, 1);
+  issue(HA0{}, S1{}, 1);
+  issue(HB1{}, S1{}, 1);
+  issue(HA1{}, S1{}, 1);
   asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // Bh0(0), Ah0(0) landed
   pp_sync();
-  rd_b(smem + H_B0 * PP_HALF, fb0e);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  pp_sync();
+  if constexpr (!EARLY) {
+    rd_b(smem + H_B0 * PP_HALF, fb0e);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_sync();
+  }
   if (lag) pp_sync();
 
-  auto ktile = [&](int t, ppbf16x8 (&b0c)[4], ppbf16x8 (&b0n)[4]) {
-    const char* cs = smem + (t & 1) * PP_SLOT;
-    const char* ns = smem + ((t + 1) & 1) * PP_SLOT;
-    // phase 0: a0 x b0
-    rd_a(cs + H_A0 * PP_HALF, fa);
-    issue(HB0{}, t + 2);
-    end_load();
-    pp_mma<0, 0, VAR>(acc, fa, b0c);
-    end_mma();
-    // phase 1: a0 x b1
-    rd_b(cs + H_B1 * PP_HALF, fb1);
-    issue(HA0{}, t + 2);
-    end_load();
-    pp_mma<0, 1, VAR>(acc, fa, fb1);
-    end_mma();
-    // phase 2: a1 x b1
-    rd_a(cs + H_A1 * PP_HALF, fa);
-    issue(HB1{}, t + 2);
-    end_load();
-    pp_mma<1, 1, VAR>(acc, fa, fb1);
-    end_mma();
-    // phase 3: a1 x b0, next tile's b0 read
-    rd_b(ns + H_B0 * PP_HALF, b0n);
-    issue(HA1{}, t + 2);
-    end_load();
-    pp_mma<1, 0, VAR>(acc, fa, b0c);
-    end_mma();
+  // Default schedule: b0 of the next tile is read in phase 3 (a register copy per tile parity).
+  // EARLY (MN-major A, whose transposing fragment reads need more registers): b0 is read in phase 0
+  // beside a0 and Bh0 is refilled in phase 1 with Ah0 — one b0 register set, waits recounted:
+  //   issue order per tile Bh0 Ah0 | Bh1 | Ah1 (phases 1, 2, 3); vmcnt(10) after phase 0 (Bh1 of this
+  //   tile landed), 12 after phase 1 (Ah1), none after 2, 12 after 3 (Ah0 / Bh0 of the next tile).
+  auto ktile = [&](auto slot_c, int t, ppbf16x8 (&b0c)[4], ppbf16x8 (&b0n)[4]) {
+    constexpr int SLOT = decltype(slot_c)::value;
+    const char* cs = smem + SLOT * PP_SLOT;
+    const char* ns = smem + (SLOT ^ 1) * PP_SLOT;
+    if constexpr (EARLY) {
+      rd_a(cs + H_A0 * PP_HALF, fa);
+      rd_b(cs + H_B0 * PP_HALF, b0c);
+      end_load(VM10{});
+      pp_mma<0, 0, VAR>(acc, fa, b0c);
+      end_mma();
+      rd_b(cs + H_B1 * PP_HALF, fb1);
+      issue(HB0{}, slot_c, t + 2);
+      issue(HA0{}, slot_c, t + 2);
+      end_load(VM12{});
+      pp_mma<0, 1, VAR>(acc, fa, fb1);
+      end_mma();
+      rd_a(cs + H_A1 * PP_HALF, fa);
+      issue(HB1{}, slot_c, t + 2);
+      end_load(VMNONE{});
+      pp_mma<1, 1, VAR>(acc, fa, fb1);
+      end_mma();
+      issue(HA1{}, slot_c, t + 2);
+      end_load(VM12{});
+      pp_mma<1, 0, VAR>(acc, fa, b0c);
+      end_mma();
+      (void)ns;
+      (void)b0n;
+    } else {
+      // phase 0: a0 x b0 (refill Bh0 <- t+2)
+      rd_a(cs + H_A0 * PP_HALF, fa);
+      issue(HB0{}, slot_c, t + 2);
+      end_load(VM12{});
+      pp_mma<0, 0, VAR>(acc, fa, b0c);
+      end_mma();
+      // phase 1: a0 x b1 (refill Ah0)
+      rd_b(cs + H_B1 * PP_HALF, fb1);
+      issue(HA0{}, slot_c, t + 2);
+      end_load(VM12{});
+      pp_mma<0, 1, VAR>(acc, fa, fb1);
+      end_mma();
+      // phase 2: a1 x b1 (refill Bh1)
+      rd_a(cs + H_A1 * PP_HALF, fa);
+      issue(HB1{}, slot_c, t + 2);
+      end_load(VM12{});
+      pp_mma<1, 1, VAR>(acc, fa, fb1);
+      end_mma();
+      // phase 3: a1 x b0, next tile's b0 into registers (refill Ah1)
+      rd_b(ns + H_B0 * PP_HALF, b0n);
+      issue(HA1{}, slot_c, t + 2);
+      end_load(VM12{});
+      pp_mma<1, 0, VAR>(acc, fa, b0c);
+      end_mma();
+    }
   };
   int t = 0;
   for (; t + 1 < nk; t += 2) {
-    ktile(t, fb0e, fb0o);
-    ktile(t + 1, fb0o, fb0e);
+    ktile(S0{}, t, fb0e, fb0o);
+    ktile(S1{}, t + 1, fb0o, fb0e);
   }
-  if (t < nk) ktile(t, fb0e, fb0o);
+  if (t < nk) ktile(S0{}, t, fb0e, fb0o);
   if (STAGGER && !lag) pp_sync();
   // drain the (zero-filling) DMAs of the tiles past the end before the LDS becomes the staging tile
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-
-  // epilogue: bias in registers, bf16 rows staged through LDS, 16-B coalesced row stores
-  bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int r = wr * 128 + 16 * i + (lane & 15);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int cc = wc * 64 + 16 * j + 4 * (lane >> 4);
-      f32x4 v = acc[i][j];
-      if (p.bias) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (n0 + cc + q < p.N) v[q] += bf2f(p.bias[n0 + cc + q]);
-      }
-      u16x4 o;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
-      *reinterpret_cast<u16x4*>(stg + r * PP_SROW + cc) = o;
-    }
-  }
-  __syncthreads();
-  for (int c = tid; c < 256 * 32; c += PP_NT) {
-    const int r = c >> 5, ch = c & 31;
-    const int m = m0 + r, n = n0 + ch * 8;
-    if (m >= p.M || n >= p.N) continue;
-    *reinterpret_cast<u16x8*>(p.C + (int64_t)m * p.ldc + n) = *reinterpret_cast<const u16x8*>(stg + r * PP_SROW + ch * 8);
-  }
+  wide_tile_epilogue(acc, smem, PP_STATS_OFF, p.epi, m0, n0, p.M, p.N, tm, blockIdx.y);
 }
 
-template <int VAR>
-hipError_t launch_pp(const PPArgs& a, hipStream_t st) {
+template <bool AK, bool BK, int VAR>
+hipError_t launch_pp_v(const PPArgs& a, int splits, hipStream_t st) {
   static bool attr = [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<VAR>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<AK, BK, VAR>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
     return true;
   }();
   (void)attr;
-  const int tiles = ((a.M + 255) / 256) * a.tiles_n;
-  gemm_pp_kernel<VAR><<<tiles, PP_NT, PP_LDS, st>>>(a);
+  const int tiles = (int)((a.M + 255) / 256) * a.tiles_n;
+  gemm_pp_kernel<AK, BK, VAR><<<dim3(tiles, splits), PP_NT, PP_LDS, st>>>(a);
   return hipGetLastError();
+}
+
+template <int VAR>
+hipError_t launch_pp_var(bool ak, bool bk, const PPArgs& a, int splits, hipStream_t st) {
+  if (ak && bk) return launch_pp_v<true, true, VAR>(a, splits, st);
+  if (ak) return launch_pp_v<true, false, VAR>(a, splits, st);
+  if (bk) return launch_pp_v<false, true, VAR>(a, splits, st);
+  return launch_pp_v<false, false, VAR>(a, splits, st);
 }
 
 }  // namespace
 
-// Lab entry (tools/gemm_lab.py): C[M,N] = A[M,K] B[N,K]^T (+ bias), bf16, both operands K-major.
-hipError_t gemm_pp_lab(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, bf16_t* C, int64_t ldc, int64_t M,
-                       int64_t N, int64_t K, const bf16_t* bias, int variant, hipStream_t st) {
-  if (K % 8 || N % 8 || M <= 0 || N <= 0 || K <= 0) return hipErrorInvalidValue;
-  PPArgs a{A, B, C, bias, lda, ldb, ldc, (int)M, (int)N, (int)K, (int)((N + 255) / 256)};
-  switch (variant) {
-    case 0: return launch_pp<0>(a, st);
-    case 1: return launch_pp<1>(a, st);
-    case 2: return launch_pp<2>(a, st);
-    case 3: return launch_pp<3>(a, st);
-    default: return hipErrorInvalidValue;
+int pp_default_variant() {
+  static const int v = [] {
+    const char* e = getenv("PDA_PP_VAR");
+    return e ? (atoi(e) & 3) : 3;
+  }();
+  return v;
+}
+
+// C = A * B through the pipelined tile (see the header).  Operand conventions as gemm_bf16:
+// a_kmajor: A(m,k) = A[m*lda+k] else A[k*lda+m]; b_kmajor: B(k,n) = B[n*ldb+k] else B[k*ldb+n].
+// splits > 1: `epi.slab` receives [splits][M][N] fp32 partials (the caller reduces them); the split
+// count actually used (K tiles per split rounded) is returned through `*used_splits`.
+hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
+                   int64_t M, int64_t N, int64_t K, const Epi& epi, int splits, int variant, hipStream_t st,
+                   int* used_splits) {
+  if (M <= 0 || N <= 0 || K <= 0) return hipErrorInvalidValue;
+  if ((a_kmajor || b_kmajor) && K % 8) return hipErrorInvalidValue;
+  if ((!a_kmajor && M % 8) || N % 8) return hipErrorInvalidValue;
+  const int ktiles = (int)((K + 63) / 64);
+  if (splits < 1) splits = 1;
+  int kps = (ktiles + splits - 1) / splits;
+  // an MN-major operand addresses one split's K span with 32-bit offsets
+  const int64_t ld_mn = std::max(a_kmajor ? (int64_t)0 : lda, b_kmajor ? (int64_t)0 : ldb);
+  if (ld_mn > 0 && ((int64_t)kps * 64 + 64) * ld_mn * 2 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  splits = (ktiles + kps - 1) / kps;  // <= the requested count (the caller sized the slab for that)
+  if (splits > 1 && !epi.slab) return hipErrorInvalidValue;
+  // a K-major operand's 256-row panel must stay within 32-bit offsets
+  if ((a_kmajor && 257 * lda * 2 >= ((int64_t)1 << 31)) || (b_kmajor && 257 * ldb * 2 >= ((int64_t)1 << 31)))
+    return hipErrorInvalidValue;
+  if (used_splits) *used_splits = splits;
+  PPArgs a{{A, lda, M}, {B, ldb, N}, M, N, K, (int)((N + 255) / 256), kps, epi};
+  if (splits <= 1) a.epi.slab = nullptr;
+  switch (variant < 0 ? pp_default_variant() : variant) {
+    case 0: return launch_pp_var<0>(a_kmajor, b_kmajor, a, splits, st);
+    case 1: return launch_pp_var<1>(a_kmajor, b_kmajor, a, splits, st);
+    case 2: return launch_pp_var<2>(a_kmajor, b_kmajor, a, splits, st);
+    default: return launch_pp_var<3>(a_kmajor, b_kmajor, a, splits, st);
   }
+}
+
+// Lab entry (tools/gemm_lab.py): C[M,N] = A B (+ bf16 bias), bf16 output, the given operand majorness.
+hipError_t gemm_pp_lab(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
+                       bf16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K, const bf16_t* bias, int variant,
+                       hipStream_t st) {
+  Epi epi{};
+  epi.C = C;
+  epi.ldc = ldc;
+  epi.bias = bias;
+  return gemm_pp(A, a_kmajor, lda, B, b_kmajor, ldb, M, N, K, epi, 1, variant, st, nullptr);
 }
 
 }  // namespace pda

@@ -50,6 +50,7 @@ void bind_runtime(pybind11::module& m) {
       .def("mark_ready", &BucketReducer::mark_ready)
       .def("flush_unready", &BucketReducer::flush_unready)
       .def("all_launched", &BucketReducer::all_launched)
+      .def("any_marked", &BucketReducer::any_marked)
       .def("unready_params", &BucketReducer::unready_params)
       .def("ready_order", &BucketReducer::ready_order);
   py::class_<HostRing>(m, "HostRing")

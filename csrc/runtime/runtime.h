@@ -78,6 +78,7 @@ class BucketReducer {
   std::vector<int> mark_ready(int64_t p);
   std::vector<int> flush_unready();  // mark every unready parameter ready (unused params), return buckets
   bool all_launched() const { return next_launch_ == (int)buckets_.size(); }
+  bool any_marked() const { return !ready_order_.empty(); }
   std::vector<int64_t> unready_params() const;
   std::vector<int64_t> ready_order() const { return ready_order_; }
 

@@ -359,8 +359,18 @@ class DistributedDataParallel(tnn.Module):
         self.reducer.prepare()
         self._callback_queued = False
 
+    def set_multi_pass(self, on: bool = True):
+        """Gradient readiness spread over several backward passes (an interleaved pipeline's chunks each
+        finish in their own backward): a backward that leaves buckets unlaunched keeps the bucket state
+        and its in-flight collectives instead of treating the rest as unused; the pass that launches
+        the last bucket finalizes."""
+        self._multi_pass = bool(on)
+
     def _finalize(self):
         self._callback_queued = False
+        if getattr(self, "_multi_pass", False) and self.require_backward_grad_sync and \
+                not self.reducer.all_launched() and self.reducer.any_marked():
+            return  # later passes mark the remaining parameters
         if not self.reducer.all_launched():
             unready = self.reducer.unready_params()
             if not self.find_unused_parameters:

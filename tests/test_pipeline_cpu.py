@@ -125,6 +125,34 @@ def test_interleaved_pipeline_grads_match_single_process(tmp_path, world, chunks
                 assert torch.allclose(d["grads"][f"{c}.{n}"], p.grad, atol=1e-5, rtol=1e-4), (r, c, n)
 
 
+def test_interleaved_pipeline_ddp_grads_match_single_process(tmp_path):
+    """Interleaved schedule x DDP: 2 stages x 2 chunks x 2 DP replicas on gloo; the DP
+    average runs through each rank's DDP wrapper (multi-pass buckets), no dp_sync_grads."""
+    pp, dp, chunks, n_layers, n_micro = 2, 2, 2, 8, 4
+    spawn(_workers.pipeline_interleaved_ddp_worker, args=(pp * dp, pp, dp, chunks, n_layers, n_micro, str(tmp_path)),
+          nprocs=pp * dp, timeout=180)
+    full = _workers._tiny_stack(n_layers)
+    g = torch.Generator().manual_seed(1)
+    B = n_micro * 2
+    X = torch.randn(dp * B, 16, generator=g)
+    Y = torch.randn(dp * B, 16, generator=g)
+    # the replicas' losses are means over their own half: the DP-averaged gradient is that of the mean
+    # of the two half-batch means = the full-batch mean (equal halves)
+    loss = F.mse_loss(full(X), Y)
+    loss.backward()
+    per = n_layers // (pp * chunks)
+    blocks = [full[3 * i: 3 * i + 3] for i in range(n_layers)]
+    for r in range(pp * dp):
+        d = torch.load(tmp_path / f"{r}.pt", weights_only=True)
+        s = d["stage"]
+        assert d["stats"]["comm_calls"] > 0
+        for c in range(chunks):
+            vs = c * pp + s
+            ref = torch.nn.Sequential(*[m for b in blocks[vs * per:(vs + 1) * per] for m in b])
+            for n, p in ref.named_parameters():
+                assert torch.allclose(d["grads"][f"{c}.{n}"], p.grad, atol=1e-5, rtol=1e-4), (r, c, n)
+
+
 @pytest.mark.parametrize("world,chunks", [(2, 1), (2, 2), (4, 1)])
 def test_pipeline_checkpoint_roundtrip_and_consolidate(tmp_path, world, chunks):
     """PP checkpoint layout: stage files + partition map, reload, consolidation."""
