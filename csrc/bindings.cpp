@@ -642,6 +642,30 @@ void gemm(Tensor A, bool a_kmajor, int64_t lda, Tensor B, bool b_kmajor, int64_t
                               slab_n > 0 ? slab.data_ptr<float>() : nullptr, slab_n > 0, stream_of(A)));
 }
 
+// Weight + bias gradient of a Linear in one pipelined GEMM: dw[N, K] = dy^T x (dy [M, N], x [M, K]) and
+// db[N] = column sums of dy.  Returns whether db was written (false: the shape did not take the
+// 256 x 256 pipelined path; the caller reduces dy itself).
+bool gemm_wgrad_db(Tensor dy, Tensor x, Tensor dw, Tensor db) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  check_f32_or_bf16(dw, "dw");
+  check_f32_or_bf16(db, "db");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0) && dy.is_contiguous() && x.is_contiguous());
+  const int64_t T = dy.size(0), Nout = dy.size(1), Kin = x.size(1);
+  TORCH_CHECK(Nout % 8 == 0 && Kin % 8 == 0, "gemm_wgrad_db needs in / out features multiples of 8");
+  TORCH_CHECK(dw.numel() == Nout * Kin && dw.is_contiguous() && db.numel() == Nout && db.is_contiguous());
+  for (auto* t : {&dy, &x, &dw}) check_aligned16(*t, "gemm_wgrad_db operand");
+  c10::DeviceGuard g(dy.device());
+  const int64_t slab_n = pda::gemm_slab_floats(Nout, Kin, T, true);
+  Tensor scratch = at::empty({slab_n + Nout}, dy.options().dtype(at::kFloat));
+  int done = 0;
+  CHECK_HIP_OK(pda::gemm_bf16_wgrad_db(bp(dy), Nout, bp(x), Kin, dw.data_ptr(), dw.scalar_type() == at::kFloat, Kin,
+                                       Nout, Kin, T, db.data_ptr(), is_bf16(db),
+                                       slab_n > 0 ? scratch.data_ptr<float>() : nullptr,
+                                       scratch.data_ptr<float>() + slab_n, stream_of(dy), &done));
+  return done != 0;
+}
+
 // GEMM with a fused GELU-tanh epilogue (bf16 C [M, ldc]):
 //   act 1 (forward):  C = gelu(A B + bias) and aux = A B + bias (the pre-activation the backward needs)
 //   act 2 (backward): C = (A B) * gelu'(aux), aux = that pre-activation
@@ -1576,9 +1600,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("fill_randint", &fill_randint);
   m.def("gemm", &gemm);
   m.def("gemm_act", &gemm_act);
+  m.def("gemm_wgrad_db", &gemm_wgrad_db);
   m.def("gemm_pp_lab", &gemm_pp_lab);
   m.def("set_gemm_paths", &pda::set_gemm_paths,
         "force a GEMM kernel path: wide=-1 env default, 0 off, 1 auto, 2 force", pybind11::arg("wide"));
+  m.def("set_gemm_pp", &pda::set_gemm_pp,
+        "pipelined 256x256 kernel for plain wide GEMMs: -1 env default (PDA_GEMM_PP), 0 off, 1 on",
+        pybind11::arg("on"));
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("bias") = py::none(), py::arg("relu") = false, py::arg("out_f32") = false);
   m.def("split_bf16", &split_bf16, py::arg("x"), py::arg("nseg"), py::arg("lo_mask"), py::arg("stack"));

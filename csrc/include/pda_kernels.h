@@ -188,11 +188,15 @@ hipError_t fill_randint(int64_t* out, int64_t n, uint64_t seed, uint64_t offset,
 // path override for the GEMM family: wide = -1 env default (PDA_GEMM_WIDE), 0 off, 1 heuristic, 2 force;
 // variant >= 0 selects a wide-kernel schedule variant (bit 0 setprio, bit 1 MFMA/ds_read interleave)
 void set_gemm_paths(int wide);
+void set_gemm_pp(int on);  // -1: PDA_GEMM_PP (default on), 0 / 1: force
 int64_t gemm_slab_floats(int64_t M, int64_t N, int64_t K, bool allow_split);
 hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
                      void* C, bool c_f32, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,
                      bool bias_f32, bool relu, float* slab, bool allow_split, hipStream_t st);
 // act 1: C = gelu_tanh(A B + bias), act_aux = A B + bias (pre-activation); act 2: C = (A B) * gelu_tanh'(act_aux)
+hipError_t gemm_bf16_wgrad_db(const bf16_t* dy, int64_t ld_dy, const bf16_t* x, int64_t ld_x, void* dw, bool dw_f32,
+                              int64_t ldc, int64_t M, int64_t N, int64_t K, void* db, bool db_bf16, float* slab,
+                              float* rs_scratch, hipStream_t st, int* db_done);
 hipError_t gemm_bf16_act(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
                          bf16_t* C, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias, bool bias_f32,
                          int act, bf16_t* act_aux, hipStream_t st);

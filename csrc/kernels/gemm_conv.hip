@@ -1923,12 +1923,14 @@ template <class L> struct IsPlain : std::false_type {};
 template <int R> struct IsPlain<PlainK<R>> : std::true_type {};
 template <int R> struct IsPlain<PlainMN<R>> : std::true_type {};
 
+int g_pp_override = -1;  // set_gemm_pp(): tests force the pipelined kernel on / off at run time
+
 bool pp_mode() {
   static const bool on = [] {
     const char* e = getenv("PDA_GEMM_PP");
     return !(e && e[0] == '0');
   }();
-  return on;
+  return g_pp_override >= 0 ? g_pp_override != 0 : on;
 }
 
 // returns hipErrorNotSupported when the pipelined kernel cannot take the shape (the caller falls back)
@@ -2001,6 +2003,7 @@ bool dgrad_phased(int stride, int dil) { return stride == 1 || dil == 1; }
 // 6 % slower on the headline step than the staged 16-byte row stores: profiles/
 // r3_epi_direct_DROPPED_and_transformers.jsonl)
 void set_gemm_paths(int wide) { g_wide_override = wide; }
+void set_gemm_pp(int on) { g_pp_override = on; }
 
 // slab sizing covers both the 128-tile plan and the wide tile's (possibly deeper) split
 int64_t split_slab_floats(int64_t M, int64_t N, int64_t K, const Plan& p) {
@@ -2029,6 +2032,56 @@ hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* 
   if (a_kmajor && b_kmajor) return dispatch_bn<PlainK, PlainK>(M, N, K, p, epi, slab, st, mk_ak, mk_bk);
   if (a_kmajor) return dispatch_bn<PlainK, PlainMN>(M, N, K, p, epi, slab, st, mk_ak, mk_bmn);
   if (b_kmajor) return dispatch_bn<PlainMN, PlainK>(M, N, K, p, epi, slab, st, mk_amn, mk_bk);
+  return dispatch_bn<PlainMN, PlainMN>(M, N, K, p, epi, slab, st, mk_amn, mk_bmn);
+}
+
+__global__ void __launch_bounds__(256) rowsum_cast_kernel(const float* __restrict__ src, void* dst, int bf16_out,
+                                                          int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  if (bf16_out) ((bf16_t*)dst)[i] = f2bf(src[i]);
+  else ((float*)dst)[i] = src[i];
+}
+
+// Weight gradient with the bias gradient folded in: dw[M, N] = dy^T x with dy [K, M] and x
+// [K, N] (both MN-major, K = tokens), and db[M] = column sums of dy = row sums of the A operand, computed
+// by the pipelined kernel's extra MFMAs when the GEMM takes the 256 x 256 path (*db_done = 1); otherwise
+// *db_done = 0 and only dw is written.  Split-K launches add their partial sums into `rs_scratch`
+// (M floats, zeroed here) and a cast pass writes db.
+hipError_t gemm_bf16_wgrad_db(const bf16_t* dy, int64_t ld_dy, const bf16_t* x, int64_t ld_x, void* dw, bool dw_f32,
+                              int64_t ldc, int64_t M, int64_t N, int64_t K, void* db, bool db_bf16, float* slab,
+                              float* rs_scratch, hipStream_t st, int* db_done) {
+  *db_done = 0;
+  Plan p = plan_gemm(M, N, K, slab != nullptr, 512);
+  Epi epi{dw, ldc, dw_f32 ? 1 : 0, nullptr, 0, 0, nullptr};
+  auto mk_amn = [&](auto t) { t.p = dy; t.K = K; t.cols = M; t.ld = ld_dy; return t; };
+  auto mk_bmn = [&](auto t) { t.p = x; t.K = K; t.cols = N; t.ld = ld_x; return t; };
+  if (pp_mode()) {
+    int ws = 0;
+    if (use_wide(M, N, K, p, epi)) ws = 1;
+    else if (slab) ws = wide_splits(M, N, K, p, epi);
+    if (ws > 0) {
+      Epi e = epi;
+      if (ws > 1) {
+        PDA_CHECK_HIP(hipMemsetAsync(rs_scratch, 0, M * sizeof(float), st));
+        e.rowsum = rs_scratch;
+        e.rowsum_mode = 3;
+      } else {
+        e.rowsum = db;
+        e.rowsum_mode = db_bf16 ? 2 : 1;
+      }
+      const hipError_t r = launch_pp_plain(mk_amn(PlainMN<64>{}), mk_bmn(PlainMN<64>{}), M, N, K, e, st, ws, slab);
+      if (r != hipErrorNotSupported) {
+        if (r != hipSuccess) return r;
+        if (ws > 1) {
+          rowsum_cast_kernel<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(rs_scratch, db, db_bf16 ? 1 : 0, M);
+          PDA_CHECK_HIP(hipGetLastError());
+        }
+        *db_done = 1;
+        return hipSuccess;
+      }
+    }
+  }
   return dispatch_bn<PlainMN, PlainMN>(M, N, K, p, epi, slab, st, mk_amn, mk_bmn);
 }
 

@@ -37,6 +37,12 @@ struct Epi {
   // with the activation backward: no separate elementwise pass over two [tokens, 4d] tensors)
   int act;
   bf16_t* act_aux;
+  // optional row sums of operand A over this launch's K range (only the pipelined kernel, gemm_pp.hip,
+  // computes them): a Linear weight gradient dW = dY^T X has A = dY^T, so its row sums are the bias
+  // gradient (db folded into the dW GEMM).  mode 1: fp32 store, 2: bf16 store, 3: fp32
+  // atomic add (split-K launches; the caller zeroes the buffer)
+  void* rowsum;
+  int rowsum_mode;
 };
 
 // The pipelined 256 x 256 GEMM (gemm_pp.hip); gemm_conv.hip routes plain GEMMs to it.

@@ -196,8 +196,9 @@ __device__ __forceinline__ PPSrc pp_src(const PPOp& op, int64_t r0, int64_t k0, 
   return s;
 }
 
-// VAR bits: 1 = s_setprio(1) around each MFMA section, 2 = ping-pong stagger of the two wave groups
-template <bool AK, bool BK, int VAR>
+// VAR bits: 1 = s_setprio(1) around each MFMA section, 2 = ping-pong stagger of the two wave groups,
+// 4 = a load section issues its refill DMA before its fragment reads, 8 = two 32-MFMA phases per K tile
+template <bool AK, bool BK, int VAR, bool RS = false>
 __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -273,12 +274,14 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   // end of a load section: own DMAs of the half read next are done, own fragment reads are done
   auto end_load = [&](auto vm_c) {
     constexpr int VM = decltype(vm_c)::value;
-    if constexpr (VM == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    if constexpr (VM == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (VM == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     else if constexpr (VM == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
     else static_assert(VM == -1, "vmcnt literal");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     pp_sync();
   };
+  using VM8 = std::integral_constant<int, 8>;
   using VM10 = std::integral_constant<int, 10>;
   using VM12 = std::integral_constant<int, 12>;
   using VMNONE = std::integral_constant<int, -1>;
@@ -291,6 +294,102 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // RS: row sums of A (Epi::rowsum) by MFMA against a ones fragment — C = A * 1 puts every row's sum in
+  // each of its columns.  The 4 waves that share A rows split the row tiles (wave wc takes row tile wc
+  // of each 64-row quadrant): 2 MFMAs per A quadrant and K tile, +6 % matrix work, no VALU.
+  f32x4 rsacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  auto rs_mma = [&](auto qa_c, const ppbf16x8 (&a)[8]) {
+    if constexpr (RS) {
+      constexpr int QA = decltype(qa_c)::value;
+      typedef short s16x8 __attribute__((ext_vector_type(8)));
+      const ppbf16x8 ones = __builtin_bit_cast(ppbf16x8, s16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80,
+                                                               0x3F80, 0x3F80});
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        ppbf16x8 f = a[kk * 4];
+        if (wc == 1) f = a[kk * 4 + 1];
+        else if (wc == 2) f = a[kk * 4 + 2];
+        else if (wc == 3) f = a[kk * 4 + 3];
+        rsacc[QA] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f, rsacc[QA], 0, 0, 0);
+      }
+    } else {
+      (void)qa_c;
+      (void)a;
+    }
+  };
+  auto rs_store = [&]() {
+    if constexpr (RS) {
+      if ((lane >> 4) == 0) {
+#pragma unroll
+        for (int qa = 0; qa < 2; ++qa) {
+          const int64_t m = m0 + wr * 128 + qa * 64 + 16 * wc + (lane & 15);
+          if (m >= p.M) continue;
+          const float v = rsacc[qa][0];
+          if (p.epi.rowsum_mode == 3) unsafeAtomicAdd((float*)p.epi.rowsum + m, v);
+          else if (p.epi.rowsum_mode == 2) ((bf16_t*)p.epi.rowsum)[m] = f2bf(v);
+          else ((float*)p.epi.rowsum)[m] = v;
+        }
+      }
+    }
+  };
+  using Q0 = std::integral_constant<int, 0>;
+  using Q1 = std::integral_constant<int, 1>;
+
+  constexpr bool TWO = (VAR & 8) != 0;
+  if constexpr (TWO) {
+    // Two phases of 32 MFMAs per K tile: (a0 x b) then (a1 x b).  Phase 0 reads a0 and all of b (16
+    // fragments), phase 1 reads a1 (b stays in registers), so Ah0 / Bh0 / Bh1 are released after phase
+    // 0 and refilled with K tile t+2 in phase 1; Ah1 is released after phase 1 and refilled with t+1
+    // in the next tile's phase 0.  Issue order A0 B0 B1 (t+2) | A1 (t+1): every wait is vmcnt(8).
+    // Half the barriers of the 4-phase schedule per MFMA, 192 live registers for the operands.
+    ppbf16x8 ta[8], tb0[4], tb1[4];
+    issue(HA0{}, S0{}, 0);
+    issue(HB0{}, S0{}, 0);
+    issue(HB1{}, S0{}, 0);
+    issue(HA1{}, S0{}, 0);
+    issue(HA0{}, S1{}, 1);
+    issue(HB0{}, S1{}, 1);
+    issue(HB1{}, S1{}, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0 B0 B1 of tile 0 landed
+    pp_sync();
+    if (lag) pp_sync();
+    auto ktile2 = [&](auto slot_c, int t) {
+      constexpr int SLOT = decltype(slot_c)::value;
+      const char* cs = smem + SLOT * PP_SLOT;
+      rd_a(cs + H_A0 * PP_HALF, ta);
+      rd_b(cs + H_B0 * PP_HALF, tb0);
+      rd_b(cs + H_B1 * PP_HALF, tb1);
+      if constexpr (SLOT == 0) issue(HA1{}, S1{}, t + 1);
+      else issue(HA1{}, S0{}, t + 1);
+      end_load(VM8{});
+      pp_mma<0, 0, VAR>(acc, ta, tb0);
+      pp_mma<0, 1, VAR>(acc, ta, tb1);
+      rs_mma(Q0{}, ta);
+      end_mma();
+      rd_a(cs + H_A1 * PP_HALF, ta);
+      issue(HA0{}, slot_c, t + 2);
+      issue(HB0{}, slot_c, t + 2);
+      issue(HB1{}, slot_c, t + 2);
+      end_load(VM8{});
+      pp_mma<1, 0, VAR>(acc, ta, tb0);
+      pp_mma<1, 1, VAR>(acc, ta, tb1);
+      rs_mma(Q1{}, ta);
+      end_mma();
+    };
+    int t2 = 0;
+    for (; t2 + 1 < nk; t2 += 2) {
+      ktile2(S0{}, t2);
+      ktile2(S1{}, t2 + 1);
+    }
+    if (t2 < nk) ktile2(S0{}, t2);
+    if (STAGGER && !lag) pp_sync();
+    rs_store();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    wide_tile_epilogue(acc, smem, PP_STATS_OFF, p.epi, m0, n0, p.M, p.N, tm, blockIdx.y);
+    return;
+  }
 
   ppbf16x8 fa[8], fb1[4], fb0e[4], fb0o[4];
   // prologue: K tiles 0 and 1 in the steady-state issue order (Bh0, Ah0, Bh1, Ah1)
@@ -325,6 +424,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       rd_b(cs + H_B0 * PP_HALF, b0c);
       end_load(VM10{});
       pp_mma<0, 0, VAR>(acc, fa, b0c);
+      rs_mma(Q0{}, fa);
       end_mma();
       rd_b(cs + H_B1 * PP_HALF, fb1);
       issue(HB0{}, slot_c, t + 2);
@@ -336,6 +436,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       issue(HB1{}, slot_c, t + 2);
       end_load(VMNONE{});
       pp_mma<1, 1, VAR>(acc, fa, fb1);
+      rs_mma(Q1{}, fa);
       end_mma();
       issue(HA1{}, slot_c, t + 2);
       end_load(VM12{});
@@ -344,27 +445,34 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       (void)ns;
       (void)b0n;
     } else {
+      constexpr bool DMA_FIRST = (VAR & 4) != 0;
       // phase 0: a0 x b0 (refill Bh0 <- t+2)
+      if constexpr (DMA_FIRST) issue(HB0{}, slot_c, t + 2);
       rd_a(cs + H_A0 * PP_HALF, fa);
-      issue(HB0{}, slot_c, t + 2);
+      if constexpr (!DMA_FIRST) issue(HB0{}, slot_c, t + 2);
       end_load(VM12{});
       pp_mma<0, 0, VAR>(acc, fa, b0c);
+      rs_mma(Q0{}, fa);
       end_mma();
       // phase 1: a0 x b1 (refill Ah0)
+      if constexpr (DMA_FIRST) issue(HA0{}, slot_c, t + 2);
       rd_b(cs + H_B1 * PP_HALF, fb1);
-      issue(HA0{}, slot_c, t + 2);
+      if constexpr (!DMA_FIRST) issue(HA0{}, slot_c, t + 2);
       end_load(VM12{});
       pp_mma<0, 1, VAR>(acc, fa, fb1);
       end_mma();
       // phase 2: a1 x b1 (refill Bh1)
+      if constexpr (DMA_FIRST) issue(HB1{}, slot_c, t + 2);
       rd_a(cs + H_A1 * PP_HALF, fa);
-      issue(HB1{}, slot_c, t + 2);
+      if constexpr (!DMA_FIRST) issue(HB1{}, slot_c, t + 2);
       end_load(VM12{});
       pp_mma<1, 1, VAR>(acc, fa, fb1);
+      rs_mma(Q1{}, fa);
       end_mma();
       // phase 3: a1 x b0, next tile's b0 into registers (refill Ah1)
+      if constexpr (DMA_FIRST) issue(HA1{}, slot_c, t + 2);
       rd_b(ns + H_B0 * PP_HALF, b0n);
-      issue(HA1{}, slot_c, t + 2);
+      if constexpr (!DMA_FIRST) issue(HA1{}, slot_c, t + 2);
       end_load(VM12{});
       pp_mma<1, 0, VAR>(acc, fa, b0c);
       end_mma();
@@ -377,27 +485,32 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   }
   if (t < nk) ktile(S0{}, t, fb0e, fb0o);
   if (STAGGER && !lag) pp_sync();
+  rs_store();
   // drain the (zero-filling) DMAs of the tiles past the end before the LDS becomes the staging tile
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   wide_tile_epilogue(acc, smem, PP_STATS_OFF, p.epi, m0, n0, p.M, p.N, tm, blockIdx.y);
 }
 
-template <bool AK, bool BK, int VAR>
+template <bool AK, bool BK, int VAR, bool RS = false>
 hipError_t launch_pp_v(const PPArgs& a, int splits, hipStream_t st) {
   static bool attr = [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<AK, BK, VAR>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<AK, BK, VAR, RS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
     return true;
   }();
   (void)attr;
   const int tiles = (int)((a.M + 255) / 256) * a.tiles_n;
-  gemm_pp_kernel<AK, BK, VAR><<<dim3(tiles, splits), PP_NT, PP_LDS, st>>>(a);
+  gemm_pp_kernel<AK, BK, VAR, RS><<<dim3(tiles, splits), PP_NT, PP_LDS, st>>>(a);
   return hipGetLastError();
 }
 
 template <int VAR>
 hipError_t launch_pp_var(bool ak, bool bk, const PPArgs& a, int splits, hipStream_t st) {
+  if (a.epi.rowsum) {  // row sums of A: weight-gradient layout only (A = dY^T, MN-major)
+    if (ak || bk) return hipErrorInvalidValue;
+    return launch_pp_v<false, false, VAR, true>(a, splits, st);
+  }
   if (ak && bk) return launch_pp_v<true, true, VAR>(a, splits, st);
   if (ak) return launch_pp_v<true, false, VAR>(a, splits, st);
   if (bk) return launch_pp_v<false, true, VAR>(a, splits, st);
@@ -409,7 +522,7 @@ hipError_t launch_pp_var(bool ak, bool bk, const PPArgs& a, int splits, hipStrea
 int pp_default_variant() {
   static const int v = [] {
     const char* e = getenv("PDA_PP_VAR");
-    return e ? (atoi(e) & 3) : 3;
+    return e ? atoi(e) : 2;
   }();
   return v;
 }
@@ -441,8 +554,10 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
   switch (variant < 0 ? pp_default_variant() : variant) {
     case 0: return launch_pp_var<0>(a_kmajor, b_kmajor, a, splits, st);
     case 1: return launch_pp_var<1>(a_kmajor, b_kmajor, a, splits, st);
-    case 2: return launch_pp_var<2>(a_kmajor, b_kmajor, a, splits, st);
-    default: return launch_pp_var<3>(a_kmajor, b_kmajor, a, splits, st);
+    case 3: return launch_pp_var<3>(a_kmajor, b_kmajor, a, splits, st);
+    case 6: return launch_pp_var<6>(a_kmajor, b_kmajor, a, splits, st);
+    case 10: return launch_pp_var<10>(a_kmajor, b_kmajor, a, splits, st);
+    default: return launch_pp_var<2>(a_kmajor, b_kmajor, a, splits, st);
   }
 }
 

@@ -14,6 +14,7 @@ still); a plain GEMM is exactly the case the library is tuned for.  Fused cases 
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -98,10 +99,42 @@ def _gemm_wgrad(dy, x2, out_dtype, target=None):
     return dw
 
 
+def _fused_wgrad_db(dy2, x2, wparam, bparam, target):
+    """dW and db from ONE pipelined GEMM (db = row sums of its A operand dY^T), or None when
+    the shape does not take that kernel (the caller falls back to GEMM + column sum)."""
+    if os.environ.get("PDA_WGRAD_DB_FUSED", "1") != "1" or _use_blas(dy2, x2, *dy2.shape, x2.shape[1]):
+        return None
+    if not (dy2.dtype == x2.dtype == torch.bfloat16 and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0):
+        return None
+    N, K = dy2.shape[1], x2.shape[1]
+    dw = target if target is not None else torch.empty(N, K, device=dy2.device, dtype=wparam.dtype)
+    tb = grad_target(bparam)
+    db = tb if tb is not None else torch.empty(N, device=dy2.device, dtype=bparam.dtype)
+    if db.dtype not in (torch.bfloat16, torch.float32) or dw.dtype not in (torch.bfloat16, torch.float32):
+        return None
+    if not C().gemm_wgrad_db(dy2, x2, dw, db):
+        return dw, None  # dw written; the bias gradient still needs its column sum
+    return dw, db
+
+
 def _param_grads(dy2, x2, wparam, bparam, need_w, need_b):
     """Weight and bias gradients of ``y = x W^T + b`` (dy2 [M, N], x2 [M, K]), written into the flat
-    gradient buffers when the parameters have them."""
+    gradient buffers when the parameters have them.  With both needed, the native weight-gradient GEMM
+    also produces the bias gradient (its A operand's row sums) when it runs on the pipelined tile."""
     dw = db = None
+    if need_w and need_b and dy2.shape[0] > 0:
+        target = grad_target(wparam)
+        side = target is not None and _streams.side_ok(wparam) and target.numel() < _SIDE_MAX_NUMEL
+        with (_streams.wgrad_stream(dy2.device, dy2, x2) if side else contextlib.nullcontext()):
+            r = _fused_wgrad_db(dy2, x2, wparam, bparam, target)
+        if r is not None:
+            dw, db = r
+            if db is None:
+                tb = grad_target(bparam)
+                db = C().colsum(dy2, out=tb, out_bf16=bparam.dtype == torch.bfloat16)
+                if db.dtype != bparam.dtype:
+                    db = db.to(bparam.dtype)
+            return dw, db
     if need_w:
         target = grad_target(wparam)
         if target is not None and _streams.side_ok(wparam) and target.numel() < _SIDE_MAX_NUMEL:

@@ -543,7 +543,7 @@ def ddp_rccl_world1_worker(rank, world, outdir, mode="native"):
     pd.destroy_process_group()
 
 
-def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl"):
+def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl", force=False):
     """FSDP (bf16 shards, fused AdamW with fp32 masters, gradients written into the units' flat buffers)
     on a tiny Llama, `world` ranks sharing cuda:0 (gloo when world > 1): after 2 steps the consolidated
     parameters match an unsharded replica trained on the concatenated batch."""
@@ -556,6 +556,12 @@ def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl"):
     torch.cuda.set_device(0)
     if world > 1:
         pd.init_process_group("gloo")
+    elif force:
+        # a one-rank RCCL group with PDA_FSDP_FORCE_COMM=1: no aliasing, real ncclAllGather /
+        # ncclReduceScatter on the native communicator, transient gathered / gradient buffers
+        os.environ["PDA_FSDP_FORCE_COMM"] = "1"
+        os.environ["PDA_TRACK_COMM"] = "1"
+        pd.init_process_group("nccl", device_id=0)
     torch.manual_seed(0)
     cfg = config("llama3-tiny", dim=256, n_heads=2, n_kv_heads=1, ffn_dim=512)
     ref = Llama(cfg, device="cuda", dtype=torch.bfloat16)
@@ -563,6 +569,8 @@ def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl"):
     model.load_state_dict(ref.state_dict())
     fsdp = FullyShardedDataParallel(model, unit_types=(LlamaBlock,))
     assert (fsdp.xgmi is not None) == (comm == "ipc" and world > 1)
+    if force:
+        assert fsdp.comm_on and fsdp.ncomm is not None and not any(u.alias for u in fsdp.units)
     opt = AdamW(fsdp.parameters(), lr=1e-3, weight_decay=0.1)
     ropt = AdamW(ref.parameters(), lr=1e-3, weight_decay=0.1)
     g = torch.Generator().manual_seed(5)
@@ -581,10 +589,86 @@ def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl"):
         a, b = sd[n].float(), p.detach().float().cpu()
         worst = max(worst, (((a - b).norm() / b.norm()).item(), n))
     assert worst[0] < 2e-2, worst
+    extra = ""
+    if force:
+        st = fsdp.comm_stats()
+        assert st["comm_calls"] > 0 and "exposed_comm_ms" in st, st
+        extra = f" calls={st['comm_calls']} exposed_ms={st['exposed_comm_ms']}"
     with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
-        f.write(f"ok {worst[0]:.3e}")
-    if world > 1:
+        f.write(f"ok {worst[0]:.3e}{extra}")
+    if world > 1 or force:
         pd.destroy_process_group()
+
+
+def pipeline_ddp_watchdog_worker(rank, world, outdir, schedule="1f1b"):
+    """One-rank RCCL group: a Pipeline(S=1) stage driven with dp_module=DDP (PDA_DDP_FORCE_COMM=1, real
+    ncclAllReduce buckets) for longer than the collective timeout (PDA_COLLECTIVE_TIMEOUT_S=5, report
+    mode).  The stage's forward never goes through DDP.forward, so only the finalize sweep and the
+    event-backed tickets retire the bucket tickets: none may expire and the list must stay bounded.
+    ``schedule="interleaved"``: two chunks, hand-offs through RCCL send/recv to self (PDA_PP_FORCE_COMM)."""
+    import time
+
+    import torch.nn as nn
+
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+    from pytorchdistributed_amd.parallel.pipeline import Pipeline
+    from pytorchdistributed_amd.utils import watchdog as wd
+
+    os.environ["PDA_DDP_FORCE_COMM"] = "1"
+    os.environ["PDA_PP_FORCE_COMM"] = "1"
+    os.environ["PDA_COLLECTIVE_TIMEOUT_S"] = "5"
+    os.environ["PDA_WATCHDOG_ACTION"] = "report"
+    from pytorchdistributed_amd import config as _config
+
+    _config.set_config(None)
+    wd.reset_watchdog()
+    torch.cuda.set_device(0)
+    pd.init_process_group("nccl", device_id=0)
+    torch.manual_seed(0)
+    chunks = 2 if schedule == "interleaved" else 1
+    mods = [nn.Sequential(nn.Linear(64, 256), nn.GELU(), nn.Linear(256, 64)).cuda() for _ in range(chunks)]
+    ref = [nn.Sequential(nn.Linear(64, 256), nn.GELU(), nn.Linear(256, 64)).cuda() for _ in range(chunks)]
+    for a, b in zip(ref, mods):
+        a.load_state_dict(b.state_dict())
+    stage = mods[0] if chunks == 1 else nn.ModuleList(mods)
+    ddp = DistributedDataParallel(stage, device_ids=[0], bucket_cap_mb=0.05, first_bucket_mb=0.02)
+    pipe = Pipeline(mods[0] if chunks == 1 else mods, [0], num_microbatches=4, schedule=schedule,
+                    loss_fn=F.mse_loss, device=torch.device("cuda", 0), dp_module=ddp)
+    assert ddp._ncomm is not None
+    assert pipe._ncomm is not None
+    g = torch.Generator().manual_seed(3)
+    t0, steps, most = time.time(), 0, 0
+    while time.time() - t0 < 7.0 or steps < 3:
+        x = torch.randn(16, 64, generator=g).cuda()
+        y = torch.randn(16, 64, generator=g).cuda()
+        for m in mods:
+            m.zero_grad(set_to_none=True)
+        pipe.step(x, y)
+        if steps == 0:  # gradients of the first step vs one process without pipeline / DDP
+            for m in ref:
+                m.zero_grad(set_to_none=True)
+            h = x
+            for m in ref:
+                h = m(h)
+            F.mse_loss(h, y).backward()
+            for a, b in zip(mods, ref):
+                for pa, pb in zip(a.parameters(), b.parameters()):
+                    assert torch.allclose(pa.grad, pb.grad, atol=1e-5, rtol=1e-4)
+        torch.cuda.synchronize()
+        most = max(most, len(ddp._tickets))
+        steps += 1
+        time.sleep(0.3)
+    time.sleep(1.5)  # idle past the last step: the event-backed tickets retire on their own
+    w = wd.get_watchdog()
+    expired = list(w.expired())
+    assert not expired, expired
+    assert most <= 2 * ddp.reducer.num_buckets, (most, ddp.reducer.num_buckets)
+    assert wd.armed() == 0, w.pending()
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+        f.write(f"ok steps={steps} max_tickets={most} buckets={ddp.reducer.num_buckets}")
+    pd.destroy_process_group()
+    wd.reset_watchdog()
 
 
 class _PPFull(torch.nn.Module):

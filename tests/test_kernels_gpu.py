@@ -126,6 +126,70 @@ def test_gemm_wide_layouts(M, N, K, split, ak, bk, force_wide):
     assert rel_err(out.cpu(), ref) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(1000, 264, 136), (256, 520, 72), (296, 256, 1600), (8, 8, 8), (512, 768, 4096),
+                                   (2048, 2048, 1024)])
+@pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False)])
+@pytest.mark.parametrize("variant", [0, 3])
+def test_gemm_pp_variants(M, N, K, ak, bk, variant):
+    """Pipelined 256x256 GEMM (gemm_pp.hip) through its lab entry: every operand layout used in training
+    (fwd K x K, dgrad K x MN, wgrad MN x MN), ragged M / N / K (rows past the operand and K past the end
+    read zero through the buffer descriptors), the plain (0) and ping-pong + setprio (3) schedules, bias."""
+    torch.manual_seed(21)
+    A = torch.rand(M, K) * 2 - 1
+    B = torch.rand(K, N) * 2 - 1
+    bias = torch.rand(N) - 0.5
+    a_store = bf(A) if ak else bf(A.t().contiguous())
+    b_store = bf(B.t().contiguous()) if bk else bf(B)
+    out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    C().gemm_pp_lab(a_store, ak, K if ak else M, b_store, bk, K if bk else N, out, N, M, N, K, bf(bias), variant)
+    ref = A.to(torch.bfloat16).float() @ B.to(torch.bfloat16).float() + bias.to(torch.bfloat16).float()
+    assert torch.isfinite(out).all()
+    assert rel_err(out.cpu(), ref) < 1e-2
+
+
+def test_gemm_pp_matches_wide_kernel_bitwise_fp32_slabs():
+    """The pipelined and the 2-stage wide kernel accumulate every output in the same MFMA order over K
+    tiles, so with split-K fp32 slabs (no bf16 rounding of partials) both paths give the same fp32 C."""
+    M, N, K = 512, 512, 8192
+    torch.manual_seed(22)
+    A, B = bf(torch.randn(M, K)), bf(torch.randn(N, K))
+    outs = []
+    for pp in (1, 0):
+        C().set_gemm_pp(pp)
+        C().set_gemm_paths(2)
+        try:
+            o = torch.empty(M, N, device=DEV, dtype=torch.float32)
+            C().gemm(A, True, K, B, True, K, o, N, M, N, K, None, False, True)
+            outs.append(o)
+        finally:
+            C().set_gemm_paths(-1)
+            C().set_gemm_pp(-1)
+    ref = A.float().cpu() @ B.float().cpu().t()
+    assert rel_err(outs[0].cpu(), ref) < 1e-5 and rel_err(outs[1].cpu(), ref) < 1e-5
+    assert rel_err(outs[0], outs[1]) < 1e-6
+
+
+@pytest.mark.parametrize("T,Nout,Kin", [(4096, 1024, 1024), (2048, 512, 768), (3000, 296, 264), (64, 64, 64)])
+def test_gemm_wgrad_db_fused(T, Nout, Kin):
+    """Linear weight gradient with the bias gradient folded in: dW = dY^T X and db = sum_t dY
+    from one pipelined GEMM (split-K: fp32 atomics + cast; no split: direct bf16 store); small shapes
+    that do not take the 256x256 path report False and leave db to the caller."""
+    torch.manual_seed(23)
+    dy = torch.randn(T, Nout) * 0.1
+    x = torch.randn(T, Kin)
+    dw = torch.empty(Nout, Kin, device=DEV, dtype=torch.bfloat16)
+    db = torch.full((Nout,), float("nan"), device=DEV, dtype=torch.bfloat16)
+    done = C().gemm_wgrad_db(bf(dy), bf(x), dw, db)
+    dyb, xb = dy.to(torch.bfloat16).float(), x.to(torch.bfloat16).float()
+    assert rel_err(dw.cpu(), dyb.t() @ xb) < 1e-2
+    if (T, Nout, Kin) == (4096, 1024, 1024):
+        assert done  # 16 output tiles: split-K on the pipelined tile
+    if done:
+        assert rel_err(db.cpu(), dyb.sum(0)) < 1e-2
+    else:
+        assert torch.isnan(db.float()).all()
+
+
 def _gelu_grad_ref(h):
     k0, k1 = 0.7978845608028654, 0.044715
     t = torch.tanh(k0 * (h + k1 * h ** 3))

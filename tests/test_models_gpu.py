@@ -166,6 +166,29 @@ def test_native_rccl_communicator_one_rank(tmp_path):
     assert (tmp_path / "ok0").read_text().startswith("ok")
 
 
+def test_fsdp_forced_comm_one_rank_rccl(tmp_path):
+    """FSDP at world 1 over a one-rank RCCL group with PDA_FSDP_FORCE_COMM=1: the unit all-gathers and
+    gradient reduce-scatters run as real ncclAllGather / ncclReduceScatter on the native communicator
+    (no shard aliasing), the result matches an unsharded replica, and comm_stats reports exposed time."""
+    import _workers
+    from pytorchdistributed_amd.launch import spawn
+
+    spawn(_workers.fsdp_llama_gpu_worker, args=(1, str(tmp_path), "rccl", True), nprocs=1, timeout=300)
+    assert (tmp_path / "ok0").read_text().startswith("ok")
+
+
+@pytest.mark.parametrize("schedule", ["1f1b", "interleaved"])
+def test_pipeline_ddp_tickets_retire_one_rank_rccl(tmp_path, schedule):
+    """Pipeline(S=1) + DDP stage over a one-rank RCCL group, run past a 5 s collective timeout in report
+    mode: no expired ticket, bounded ticket list, nothing armed after an idle period;
+    interleaved: chunk hand-offs through RCCL send/recv to self."""
+    import _workers
+    from pytorchdistributed_amd.launch import spawn
+
+    spawn(_workers.pipeline_ddp_watchdog_worker, args=(1, str(tmp_path), schedule), nprocs=1, timeout=240)
+    assert (tmp_path / "ok0").read_text().startswith("ok")
+
+
 @pytest.mark.parametrize("world", [1, 2])
 def test_fsdp_llama_tiny_matches_unsharded(tmp_path, world):
     """FSDP on the native transformer path: world 1 (the shard aliases the gathered buffer) and world 2
