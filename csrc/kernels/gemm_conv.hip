@@ -1933,6 +1933,15 @@ bool pp_mode() {
   return g_pp_override >= 0 ? g_pp_override != 0 : on;
 }
 
+// PDA_GEMM_PP_CONV=0: implicit-GEMM convolutions stay on the 2-stage wide kernel (A/B knob)
+bool pp_conv_mode() {
+  static const bool on = [] {
+    const char* e = getenv("PDA_GEMM_PP_CONV");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // returns hipErrorNotSupported when the pipelined kernel cannot take the shape (the caller falls back)
 template <class LA, class LB>
 hipError_t launch_pp_plain(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st,
@@ -2319,7 +2328,15 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int
   }
   ConvGeom g = make_geom(H, W, C, P, Q, R, S, stride, pad, dil, C);
   auto mk_a = [&](auto t) { t.x = x; t.g = g; t.M = M; t.K = K; return t; };
-  if (C % 64 == 0 && tap_uniform_on()) return dispatch_bn<ConvFwdKU, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
+  if (C % 64 == 0 && tap_uniform_on()) {
+    // the 256 x 256 tile on the pipelined kernel (gathered A operand, gemm_pp.hip) where the wide tile
+    // would be chosen; PDA_GEMM_PP=0 keeps the 2-stage wide kernel
+    if (pp_mode() && pp_conv_mode() && use_wide(M, Nn, K, p, epi)) {
+      const hipError_t r = gemm_pp_conv_fwd(x, N, H, W, C, w, Cout, R, S, P, Q, stride, pad, dil, epi, st);
+      if (r != hipErrorInvalidValue) return r;
+    }
+    return dispatch_bn<ConvFwdKU, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
+  }
   return dispatch_bn<ConvFwdK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
 }
 

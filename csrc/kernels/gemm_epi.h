@@ -50,6 +50,8 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
                    int64_t M, int64_t N, int64_t K, const Epi& epi, int splits, int variant, hipStream_t st,
                    int* used_splits);
 int pp_default_variant();
+hipError_t gemm_pp_conv_fwd(const bf16_t* x, int Nimg, int H, int W, int C, const bf16_t* w, int Cout, int R, int S,
+                            int P, int Q, int stride, int pad, int dil, const Epi& epi, hipStream_t st);
 
 namespace {
 

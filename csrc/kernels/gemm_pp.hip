@@ -126,12 +126,25 @@ struct PPOp {
   int64_t ld, rows;
 };
 
+// Operand A as the implicit-GEMM gather of an NHWC convolution with C % 64 == 0 (gemm_conv.hip
+// ConvFwdKU semantics: element (m = (n, p, q), k = (r, s, c)) = x[n, p*st - pad + r*dil, q*st - pad +
+// s*dil, c]; a 64-deep K tile lies inside one tap, so the tap is uniform per K tile).
+struct PPGather {
+  int H, W, C, P, Q, S, st, pad, dil;
+  uint32_t mC, sC, mS, sS;  // k / C and rs / S as mul-hi + shift (fast_div)
+};
+
 struct PPArgs {
   PPOp a, b;
   int64_t M, N, K;
   int tiles_n, kt_per_split;
   Epi epi;
+  PPGather ga;
 };
+
+__device__ __forceinline__ uint32_t pp_fdiv(uint32_t n, uint32_t mul, uint32_t shr) {
+  return mul ? (__umulhi(n, mul) >> shr) : n;
+}
 
 // Per-lane DMA source of one operand for this workgroup: a buffer descriptor over its panel (from the
 // tile's first row and the split's first K element), the lane's offset for (half 0, round 0), and the
@@ -198,7 +211,7 @@ __device__ __forceinline__ PPSrc pp_src(const PPOp& op, int64_t r0, int64_t k0, 
 
 // VAR bits: 1 = s_setprio(1) around each MFMA section, 2 = ping-pong stagger of the two wave groups,
 // 4 = a load section issues its refill DMA before its fragment reads, 8 = two 32-MFMA phases per K tile
-template <bool AK, bool BK, int VAR, bool RS = false>
+template <bool AK, bool BK, int VAR, bool RS = false, bool GA = false>
 __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -221,6 +234,29 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
 
   const PPSrc sa = pp_src<AK, true>(p.a, m0, k0, p.K, wid, lane);
   const PPSrc sb = pp_src<BK, false>(p.b, n0, k0, p.K, wid, lane);
+  // GA: per-lane gather state of the 4 A rows this lane stages (half h, round i: tile row
+  // i*128 + h*64 + wid*8 + lane/8): the element offset of its tap-(0, 0) source pixel + chunk, and the
+  // pixel's (ih0, iw0) packed in 16 bits each (an invalid row never passes the bounds test)
+  int g_pb[4] = {0, 0, 0, 0}, g_hw[4] = {0, 0, 0, 0};
+  __amdgpu_buffer_rsrc_t g_r = sa.r;
+  if constexpr (GA) {
+    const int chunk = (lane & 7) ^ ((wid * 4 + (lane >> 4)) & 7);
+    const PPGather& g = p.ga;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t m = m0 + (j & 1) * 128 + (j >> 1) * 64 + wid * 8 + (lane >> 3);
+      const bool ok = m < p.M;
+      const int mm = ok ? (int)m : 0;
+      const int q = mm % g.Q, t1 = mm / g.Q;
+      const int pp = t1 % g.P, n = t1 / g.P;
+      const int ih0 = ok ? pp * g.st - g.pad : -16384, iw0 = q * g.st - g.pad;
+      g_pb[j] = ((n * g.H + ih0) * g.W + iw0) * g.C + chunk * 8;
+      g_hw[j] = (ih0 & 0xFFFF) | (iw0 << 16);
+    }
+    const int64_t bytes = p.a.rows * 2;  // a.rows carries the tensor's element count for a gather
+    g_r = __builtin_amdgcn_make_buffer_rsrc((void*)p.a.p, (short)0, (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff),
+                                            0x00020000);
+  }
 
   // one half image of K tile t (of this split): 2 DMAs per thread; tiles past the split read zero
   // (t & 1) == SLOT at every call site: the slot offsets fold into immediates
@@ -231,6 +267,31 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
     constexpr bool km = isA ? AK : BK;
     const PPSrc& s = isA ? sa : sb;
     char* dst = smem + SLOT * PP_SLOT + hid * PP_HALF + wid * 1024;
+    if constexpr (GA && isA) {
+      // tap of this K tile (uniform): k = (r, s, cb); rows whose shifted pixel leaves the image read zero
+      const PPGather& g = p.ga;
+      const uint32_t k = (uint32_t)(k0 + (int64_t)t * 64);
+      const uint32_t rs = pp_fdiv(k, g.mC, g.sC), cb = k - rs * (uint32_t)g.C;
+      const uint32_t r = pp_fdiv(rs, g.mS, g.sS), sx = rs - r * (uint32_t)g.S;
+      const int dr = (int)r * g.dil, ds = (int)sx * g.dil;
+      const int toff = (dr * g.W + ds) * g.C + (int)cb;
+      char* dst = smem + SLOT * PP_SLOT + hid * PP_HALF + wid * 1024;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int j = (hid & 1) * 2 + i;
+        const int ih = (int)(short)(g_hw[j] & 0xFFFF) + dr, iw = (g_hw[j] >> 16) + ds;
+        const bool ok = t < nk && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        const uint32_t off = ok ? (uint32_t)(g_pb[j] + toff) * 2u : PP_OOB;
+        if constexpr (ASM_DMA) {
+          const uint32_t l = __builtin_amdgcn_readfirstlane(
+              (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(dst + i * 8192));
+          pp_glds_asm(pp_rsrc_words(p.a.p, p.a.rows * 2), l, off);
+        } else {
+          pp_glds(g_r, dst + i * 8192, off);
+        }
+      }
+      return;
+    }
     const uint32_t o = s.v + (hid & 1) * s.dh + (uint32_t)t * s.dk;
     bool kv;
     if constexpr (km) kv = t * 64 < s.lim && t < nk;
@@ -492,16 +553,16 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   wide_tile_epilogue(acc, smem, PP_STATS_OFF, p.epi, m0, n0, p.M, p.N, tm, blockIdx.y);
 }
 
-template <bool AK, bool BK, int VAR, bool RS = false>
+template <bool AK, bool BK, int VAR, bool RS = false, bool GA = false>
 hipError_t launch_pp_v(const PPArgs& a, int splits, hipStream_t st) {
   static bool attr = [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<AK, BK, VAR, RS>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<AK, BK, VAR, RS, GA>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
     return true;
   }();
   (void)attr;
   const int tiles = (int)((a.M + 255) / 256) * a.tiles_n;
-  gemm_pp_kernel<AK, BK, VAR, RS><<<dim3(tiles, splits), PP_NT, PP_LDS, st>>>(a);
+  gemm_pp_kernel<AK, BK, VAR, RS, GA><<<dim3(tiles, splits), PP_NT, PP_LDS, st>>>(a);
   return hipGetLastError();
 }
 
@@ -549,7 +610,7 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
   if ((a_kmajor && 257 * lda * 2 >= ((int64_t)1 << 31)) || (b_kmajor && 257 * ldb * 2 >= ((int64_t)1 << 31)))
     return hipErrorInvalidValue;
   if (used_splits) *used_splits = splits;
-  PPArgs a{{A, lda, M}, {B, ldb, N}, M, N, K, (int)((N + 255) / 256), kps, epi};
+  PPArgs a{{A, lda, M}, {B, ldb, N}, M, N, K, (int)((N + 255) / 256), kps, epi, {}};
   if (splits <= 1) a.epi.slab = nullptr;
   switch (variant < 0 ? pp_default_variant() : variant) {
     case 0: return launch_pp_var<0>(a_kmajor, b_kmajor, a, splits, st);
@@ -559,6 +620,37 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
     case 10: return launch_pp_var<10>(a_kmajor, b_kmajor, a, splits, st);
     default: return launch_pp_var<2>(a_kmajor, b_kmajor, a, splits, st);
   }
+}
+
+static void pp_magic(uint32_t d, uint32_t& mul, uint32_t& shr) {
+  if (d <= 1) {
+    mul = 0;
+    shr = 0;
+    return;
+  }
+  uint32_t l = 0;
+  while ((1u << l) < d) ++l;
+  const uint32_t pw = 31 + l;
+  mul = (uint32_t)(((1ull << pw) + d - 1) / d);
+  shr = pw - 32;
+}
+
+// Implicit-GEMM convolution forward through the pipelined tile: y[NPQ, Cout] = im2col(x) W^T with
+// x NHWC [N, H, W, C] (C % 64 == 0), W [Cout, R*S*C] K-major (OHWI).  Returns hipErrorInvalidValue when
+// the shape does not fit the kernel's 32-bit offsets (the caller keeps its other paths).
+hipError_t gemm_pp_conv_fwd(const bf16_t* x, int Nimg, int H, int W, int C, const bf16_t* w, int Cout, int R, int S,
+                            int P, int Q, int stride, int pad, int dil, const Epi& epi, hipStream_t st) {
+  const int64_t M = (int64_t)Nimg * P * Q, K = (int64_t)R * S * C, xn = (int64_t)Nimg * H * W * C;
+  if (C % 64 || Cout % 8 || xn * 2 >= ((int64_t)1 << 31) || M >= ((int64_t)1 << 31) ||
+      257 * K * 2 >= ((int64_t)1 << 31) || H >= 16384 || W >= 16384)
+    return hipErrorInvalidValue;
+  PPArgs a{{x, 0, xn}, {w, K, Cout}, M, Cout, K, (int)((Cout + 255) / 256), (int)((K + 63) / 64), epi, {}};
+  a.epi.slab = nullptr;
+  PPGather& g = a.ga;
+  g.H = H; g.W = W; g.C = C; g.P = P; g.Q = Q; g.S = S; g.st = stride; g.pad = pad; g.dil = dil;
+  pp_magic((uint32_t)C, g.mC, g.sC);
+  pp_magic((uint32_t)S, g.mS, g.sS);
+  return launch_pp_v<true, true, 2, false, true>(a, 1, st);
 }
 
 // Lab entry (tools/gemm_lab.py): C[M,N] = A B (+ bf16 bias), bf16 output, the given operand majorness.

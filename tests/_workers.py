@@ -487,7 +487,7 @@ def xgmi_collectives_worker(rank, world, outdir):
     pd.destroy_process_group()
 
 
-def ddp_rccl_world1_worker(rank, world, outdir, mode="native"):
+def ddp_rccl_world1_worker(rank, world, outdir, mode="native", lr=1e-3):
     """A ONE-rank RCCL group (the only RCCL group a one-GPU box can form) with PDA_DDP_FORCE_COMM=1:
     every bucket goes through the nccl branch of DDP — high-priority RCCL streams, AVG all-reduces
     ordered after the main AND the weight-gradient side stream, watchdog tickets, buffer broadcasts —
@@ -503,6 +503,10 @@ def ddp_rccl_world1_worker(rank, world, outdir, mode="native"):
     os.environ["PDA_COMM"] = "c10d" if mode == "c10d" else "native"
     if mode == "native_fp32":
         os.environ["PDA_GRAD_REDUCE_DTYPE"] = "fp32"
+    if lr > 1e-3:
+        # the original well-conditioning-insensitive check: at lr 0.05 replicas only stay equal when
+        # every BN statistic is summed in a fixed order, i.e. without the stem band kernel's atomics
+        os.environ["PDA_CONV_STEM_FWD"] = "0"
     torch.cuda.set_device(0)
     pd.init_process_group("nccl", device_id=0)
     torch.manual_seed(3)
@@ -515,8 +519,8 @@ def ddp_rccl_world1_worker(rank, world, outdir, mode="native"):
     # 64-row table in nondeterministic order) grows to O(1) BN-bias gradient differences between the
     # two replicas by step 3 (seen with the stem band kernel: 256 row tiles -> 4 per table row; it
     # passed at 0.05 only because the implicit GEMM's 64 tiles hit the 64 rows one each)
-    opt = SGD(model.parameters(), lr=1e-3, momentum=0.9)
-    lopt = SGD(local.parameters(), lr=1e-3, momentum=0.9)
+    opt = SGD(model.parameters(), lr=lr, momentum=0.9)
+    lopt = SGD(local.parameters(), lr=lr, momentum=0.9)
     assert (model._ncomm is not None) == (mode != "c10d"), mode
     g = torch.Generator().manual_seed(11)
     worst = (0.0, "")

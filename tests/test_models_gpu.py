@@ -156,6 +156,16 @@ def test_ddp_rccl_one_rank_group_matches_local(tmp_path, mode):
     assert (tmp_path / "ok0").read_text().startswith("ok")
 
 
+def test_ddp_rccl_one_rank_group_lr005_stem_gemm(tmp_path):
+    """The original lr-0.05 replica check: with the stem on the implicit GEMM (its BN sums in a
+    fixed order, PDA_CONV_STEM_FWD=0) the DDP replica and a local one stay equal over three steps."""
+    import _workers
+    from pytorchdistributed_amd.launch import spawn
+
+    spawn(_workers.ddp_rccl_world1_worker, args=(1, str(tmp_path), "native", 0.05), nprocs=1, timeout=300)
+    assert (tmp_path / "ok0").read_text().startswith("ok")
+
+
 def test_native_rccl_communicator_one_rank(tmp_path):
     """csrc/comm/communicator.cpp through comm.py: all-reduce (sum / avg, fp32 / bf16), all-gather,
     reduce-scatter, broadcast, fused send/recv, work handles, stream ordering."""
