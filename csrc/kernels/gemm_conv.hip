@@ -2332,7 +2332,8 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int
     // the 256 x 256 tile on the pipelined kernel (gathered A operand, gemm_pp.hip) where the wide tile
     // would be chosen; PDA_GEMM_PP=0 keeps the 2-stage wide kernel
     if (pp_mode() && pp_conv_mode() && use_wide(M, Nn, K, p, epi)) {
-      const hipError_t r = gemm_pp_conv_fwd(x, N, H, W, C, w, Cout, R, S, P, Q, stride, pad, dil, epi, st);
+      const hipError_t r = gemm_pp_gather(x, N, H, W, C, P, Q, S, (int)K, stride, -pad, -pad, dil, dil, w, Cout, epi,
+                                          st);
       if (r != hipErrorInvalidValue) return r;
     }
     return dispatch_bn<ConvFwdKU, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
@@ -2441,10 +2442,18 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
         if (e != hipSuccess) return e;
         continue;
       }
-      const hipError_t e =
-          Cout % 64 == 0 && R * S > 1 && tap_uniform_on()  // (strided 1x1: measured +3 %, kept gathered)
-              ? dispatch_bn<ConvDgradPhaseKU, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b)
-              : dispatch_bn<ConvDgradPhaseK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
+      const bool ku = Cout % 64 == 0 && R * S > 1 && tap_uniform_on();  // (strided 1x1: +3 %, kept gathered)
+      if (ku && pp_mode() && pp_conv_mode() && use_wide(M, Nn, K, p, epi)) {
+        // the phase's gather on the pipelined tile: dy pixel (hh + base_r - ri*step_r, ww + ...)
+        const hipError_t r = gemm_pp_gather(dy, N, P, Q, Cout, Hh, Wh, pg.Sv, (int)K, 1, pg.base_r, pg.base_s,
+                                            -pg.step_r, -pg.step_s, wph, C, epi, st);
+        if (r != hipErrorInvalidValue) {
+          if (r != hipSuccess) return r;
+          continue;
+        }
+      }
+      const hipError_t e = ku ? dispatch_bn<ConvDgradPhaseKU, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b)
+                              : dispatch_bn<ConvDgradPhaseK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
       if (e != hipSuccess) return e;
     }
   }

@@ -126,11 +126,15 @@ struct PPOp {
   int64_t ld, rows;
 };
 
-// Operand A as the implicit-GEMM gather of an NHWC convolution with C % 64 == 0 (gemm_conv.hip
-// ConvFwdKU semantics: element (m = (n, p, q), k = (r, s, c)) = x[n, p*st - pad + r*dil, q*st - pad +
-// s*dil, c]; a 64-deep K tile lies inside one tap, so the tap is uniform per K tile).
+// Operand A as the implicit-GEMM gather of an NHWC tensor [N, H, W, C] with C % 64 == 0 (a 64-deep K
+// tile lies inside one tap, so the tap is uniform per K tile):
+//   element (m = (n, a, b) of an [N, P, Q] row grid, k = (r, s, c)) = src[n, a*st + o_r + r*tr,
+//   b*st + o_c + s*ts, c], zero outside the image.
+// Convolution forward (gemm_conv.hip ConvFwdKU): grid = output pixels, st = stride, o = -pad, t = dil.
+// Stride-phase data gradient (ConvDgradPhaseKU): src = dy, grid = one phase's dx pixels, st = 1,
+// o = the phase's base offsets, t = -tap step, S = taps per row of that phase.
 struct PPGather {
-  int H, W, C, P, Q, S, st, pad, dil;
+  int H, W, C, P, Q, S, st, o_r, o_c, tr, ts;
   uint32_t mC, sC, mS, sS;  // k / C and rs / S as mul-hi + shift (fast_div)
 };
 
@@ -249,7 +253,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       const int mm = ok ? (int)m : 0;
       const int q = mm % g.Q, t1 = mm / g.Q;
       const int pp = t1 % g.P, n = t1 / g.P;
-      const int ih0 = ok ? pp * g.st - g.pad : -16384, iw0 = q * g.st - g.pad;
+      const int ih0 = ok ? pp * g.st + g.o_r : -16384, iw0 = q * g.st + g.o_c;
       g_pb[j] = ((n * g.H + ih0) * g.W + iw0) * g.C + chunk * 8;
       g_hw[j] = (ih0 & 0xFFFF) | (iw0 << 16);
     }
@@ -273,7 +277,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       const uint32_t k = (uint32_t)(k0 + (int64_t)t * 64);
       const uint32_t rs = pp_fdiv(k, g.mC, g.sC), cb = k - rs * (uint32_t)g.C;
       const uint32_t r = pp_fdiv(rs, g.mS, g.sS), sx = rs - r * (uint32_t)g.S;
-      const int dr = (int)r * g.dil, ds = (int)sx * g.dil;
+      const int dr = (int)r * g.tr, ds = (int)sx * g.ts;
       const int toff = (dr * g.W + ds) * g.C + (int)cb;
       char* dst = smem + SLOT * PP_SLOT + hid * PP_HALF + wid * 1024;
 #pragma unroll
@@ -635,22 +639,22 @@ static void pp_magic(uint32_t d, uint32_t& mul, uint32_t& shr) {
   shr = pw - 32;
 }
 
-// Implicit-GEMM convolution forward through the pipelined tile: y[NPQ, Cout] = im2col(x) W^T with
-// x NHWC [N, H, W, C] (C % 64 == 0), W [Cout, R*S*C] K-major (OHWI).  Returns hipErrorInvalidValue when
-// the shape does not fit the kernel's 32-bit offsets (the caller keeps its other paths).
-hipError_t gemm_pp_conv_fwd(const bf16_t* x, int Nimg, int H, int W, int C, const bf16_t* w, int Cout, int R, int S,
-                            int P, int Q, int stride, int pad, int dil, const Epi& epi, hipStream_t st) {
-  const int64_t M = (int64_t)Nimg * P * Q, K = (int64_t)R * S * C, xn = (int64_t)Nimg * H * W * C;
-  if (C % 64 || Cout % 8 || xn * 2 >= ((int64_t)1 << 31) || M >= ((int64_t)1 << 31) ||
-      257 * K * 2 >= ((int64_t)1 << 31) || H >= 16384 || W >= 16384)
+// Implicit GEMM through the pipelined tile: C[N*P*Q, Cout] = gather(src) W^T (PPGather above) with
+// W [Cout][K] K-major.  Returns hipErrorInvalidValue when the shape does not fit the kernel's 32-bit
+// offsets (the caller keeps its other paths).
+hipError_t gemm_pp_gather(const bf16_t* src, int Nimg, int H, int W, int C, int P, int Q, int S, int K, int st,
+                          int o_r, int o_c, int tr, int ts, const bf16_t* w, int Cout, const Epi& epi, hipStream_t stream) {
+  const int64_t M = (int64_t)Nimg * P * Q, xn = (int64_t)Nimg * H * W * C;
+  if (C % 64 || Cout % 8 || K % 64 || K <= 0 || xn * 2 >= ((int64_t)1 << 31) || M >= ((int64_t)1 << 31) ||
+      257 * (int64_t)K * 2 >= ((int64_t)1 << 31) || H >= 16384 || W >= 16384)
     return hipErrorInvalidValue;
-  PPArgs a{{x, 0, xn}, {w, K, Cout}, M, Cout, K, (int)((Cout + 255) / 256), (int)((K + 63) / 64), epi, {}};
+  PPArgs a{{src, 0, xn}, {w, K, Cout}, M, Cout, K, (int)((Cout + 255) / 256), (int)((K + 63) / 64), epi, {}};
   a.epi.slab = nullptr;
   PPGather& g = a.ga;
-  g.H = H; g.W = W; g.C = C; g.P = P; g.Q = Q; g.S = S; g.st = stride; g.pad = pad; g.dil = dil;
+  g.H = H; g.W = W; g.C = C; g.P = P; g.Q = Q; g.S = S; g.st = st; g.o_r = o_r; g.o_c = o_c; g.tr = tr; g.ts = ts;
   pp_magic((uint32_t)C, g.mC, g.sC);
   pp_magic((uint32_t)S, g.mS, g.sS);
-  return launch_pp_v<true, true, 2, false, true>(a, 1, st);
+  return launch_pp_v<true, true, 2, false, true>(a, 1, stream);
 }
 
 // Lab entry (tools/gemm_lab.py): C[M,N] = A B (+ bf16 bias), bf16 output, the given operand majorness.
