@@ -244,5 +244,102 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][4], cha
   if (want_stats) epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + stats_off), CPR, WT_NT, tm, n0, N);
 }
 
+// Persistent-kernel variant of the bf16 epilogue (gemm_pp.hip): the next tile's operand DMAs are in
+// flight, so (1) no barrier may wait on vmcnt (LDS-only barriers: lgkmcnt(0) + s_barrier), and (2) only
+// 32 KB of LDS beside the operand ring is free: the tile is staged in four 64-row bands through
+// `stage` ([64][256] bf16, 16-B chunks XOR-swizzled by row so both the 8-B fragment writes and the
+// 16-B row reads are bank-conflict free).  The BN-statistics scratch reuses `stage` after the bands.
+// fp32 / slab outputs go straight from the accumulators (wide_tile_epilogue's path, no LDS).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ int band_off(int r, int c) { return r * 256 + (c ^ ((r & 15) << 3)); }
+
+__device__ __forceinline__ void wide_tile_epilogue_banded(const f32x4 (&acc)[8][4], char* stage, const Epi& epi,
+                                                          int64_t m0, int64_t n0, int64_t M, int64_t N, int tm) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  if (epi.slab || epi.c_f32) {
+    wide_tile_epilogue(acc, stage, 0, epi, m0, n0, M, N, tm, 0);  // register path only (no LDS, no barrier)
+    return;
+  }
+  bf16_t* stg = reinterpret_cast<bf16_t*>(stage);
+  constexpr int CPR = 256 / 8;
+  const bool want_stats = epi.stats != nullptr;
+  float st1[8], st2[8], kshift[8];
+  {
+    const int64_t n = n0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      st1[q] = st2[q] = 0.f;
+      kshift[q] = (want_stats && n + q < N) ? epi.stats_shift[n + q] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    if (wr == (b >> 1)) {
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii) {
+        const int i = (b & 1) * 4 + ii;
+        const int r = 16 * ii + (lane & 15);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cc = wc * 64 + 16 * j + 4 * (lane >> 4);
+          f32x4 v = acc[i][j];
+          if (epi.bias) {
+            const int64_t n = n0 + cc;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (n + q < N)
+                v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
+          }
+          if (epi.relu) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+          }
+          u16x4 o;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = f2bf(v[q]);
+          *reinterpret_cast<u16x4*>(stg + band_off(r, cc)) = o;
+        }
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int c = tid; c < 64 * CPR; c += WT_NT) {
+      const int r = c / CPR, ch = c % CPR;
+      const int64_t m = m0 + b * 64 + r, n = n0 + ch * 8;
+      if (m >= M || n >= N) continue;
+      const int64_t crow = epi_row(epi, m);
+      u16x8 v = *reinterpret_cast<const u16x8*>(stg + band_off(r, ch * 8));
+      if (epi.addend) {
+        float a[8];
+        epi_addend8(epi, crow, n, a);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
+      }
+      if (epi.act) epi_act8(epi, crow, n, v);
+      if (want_stats) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float d = bf2f(v[q]) - kshift[q];
+          st1[q] += d;
+          st2[q] = fmaf(d, d, st2[q]);
+        }
+      }
+      *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
+    }
+    lds_barrier();
+  }
+  if (want_stats) {
+    epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(stage), CPR, WT_NT, tm, n0, N);
+    lds_barrier();  // the scratch is the next tile's staging band
+  }
+}
+
 }  // namespace
 }  // namespace pda

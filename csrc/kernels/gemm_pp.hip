@@ -557,6 +557,273 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   wide_tile_epilogue(acc, smem, PP_STATS_OFF, p.epi, m0, n0, p.M, p.N, tm, blockIdx.y);
 }
 
+// ---------------------------------------------------------------- persistent variant
+// One workgroup per CU walks tiles L = slot + i*G (G = grid size, slot = the XCD-aware rank of the
+// block, so each round of G tiles is the same tile set as one wave of the non-persistent launch).  The
+// K-tile stream does not stop at tile boundaries: the refills issued during a tile's last two K tiles
+// already fetch the next tile's first two, and its epilogue (the banded, LDS-only-barrier form) runs
+// while those are in flight — the prologue / epilogue gap that costs the non-persistent kernel ~15 %
+// at K = 1024 (gemm_lab: 32768 x 3072 x 1024 vs x 4096) overlaps the next tile's loads.  Operand
+// descriptors span whole matrices here (32-bit offsets: the host checks the operand sizes), so the
+// per-tile source state is uniform (m0, n0) and any tile's DMA source costs a few scalar ops.
+constexpr int PPP_LDS = PP_LDS_LOOP + 64 * 256 * 2;  // ring + one 64-row staging band
+static_assert(PPP_LDS <= 160 * 1024, "LDS budget");
+
+struct PPPArgs {
+  PPOp a, b;
+  int64_t M, N, K;
+  int tiles_m, tiles_n, ntiles, nk;
+  uint32_t nk_mul, nk_shr;  // u / nk
+  Epi epi;
+};
+
+template <bool AK, bool BK, bool RS>
+__global__ void __launch_bounds__(PP_NT, 1) gemm_pp_persist_kernel(PPPArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const bool lag = wr == 1;  // ping-pong stagger (variant 2 of the non-persistent kernel)
+  constexpr bool EARLY = !AK;
+  constexpr bool ASM_DMA = !(AK && BK);
+  const int G = gridDim.x;
+  const int slot_id = xcd_remap(blockIdx.x, G);
+  const int my_tiles = slot_id < p.ntiles ? (p.ntiles - slot_id + G - 1) / G : 0;
+  const int nk = p.nk;
+  const int64_t K = p.K;
+
+  // whole-matrix descriptors and the lane's fixed offsets
+  const int64_t a_bytes = AK ? p.M * p.a.ld * 2 : ((K - 1) * p.a.ld + p.M) * 2;
+  const int64_t b_bytes = BK ? p.N * p.b.ld * 2 : ((K - 1) * p.b.ld + p.N) * 2;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.a.p, (short)0, (int)a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)p.b.p, (short)0, (int)b_bytes, 0x00020000);
+  const pp_i32x4 ras = pp_rsrc_words(p.a.p, a_bytes), rbs = pp_rsrc_words(p.b.p, b_bytes);
+  // K-major: lane row rr (image row round*64 + wid*8 + lane/8) and logical chunk; MN-major: k-row and column
+  const int kchunk = (lane & 7) ^ ((wid * 4 + (lane >> 4)) & 7);
+  const int a_rr = AK ? wid * 8 + (lane >> 3) : ((pp_mn_col(tid) >> 6) * 128 + (pp_mn_col(tid) & 63));
+  const int b_rr = BK ? (wid >> 2) * 64 + (wid & 3) * 8 + (lane >> 3) : ((pp_mn_col(tid) >> 5) * 64 + (pp_mn_col(tid) & 31));
+  const uint32_t a_lane = AK ? (uint32_t)((a_rr * p.a.ld + kchunk * 8) * 2) : (uint32_t)(((tid >> 4) * p.a.ld + a_rr) * 2);
+  const uint32_t b_lane = BK ? (uint32_t)((b_rr * p.b.ld + kchunk * 8) * 2) : (uint32_t)(((tid >> 4) * p.b.ld + b_rr) * 2);
+  const int klim = (int)K - kchunk * 8;
+
+  auto tile_of = [&](int i, int& m0, int& n0) {
+    const int L = slot_id + i * G;
+    int tm, tn;
+    grouped_tile(L, p.tiles_m, p.tiles_n, 8, tm, tn);
+    m0 = tm * 256;
+    n0 = tn * 256;
+  };
+
+  // the DMA stream's position (the unit being refilled, two ahead of the one computed): tile coordinates
+  // of its tile, its K tile and whether the tile exists — uniform values advanced once per unit
+  struct Pos {
+    int m0, n0, kt, ti;
+  };
+  auto pos_at = [&](int ti, int kt) {
+    Pos q;
+    q.ti = ti;
+    q.kt = kt;
+    q.m0 = q.n0 = 0;
+    if (ti < my_tiles) tile_of(ti, q.m0, q.n0);
+    q.m0 = __builtin_amdgcn_readfirstlane(q.m0);
+    q.n0 = __builtin_amdgcn_readfirstlane(q.n0);
+    return q;
+  };
+  auto advance = [&](Pos& q) {
+    if (++q.kt == nk) q = pos_at(q.ti + 1, 0);
+  };
+  // one half image of the unit at `q` into slot `slot`
+  auto issue = [&](auto hid_c, int slot, const Pos& q) {
+    constexpr int hid = decltype(hid_c)::value;
+    constexpr bool isA = hid < 2;
+    constexpr bool km = isA ? AK : BK;
+    char* dst = smem + slot * PP_SLOT + hid * PP_HALF + wid * 1024;
+    const bool live = q.ti < my_tiles;
+    const int kt = q.kt;
+    const int r0 = isA ? q.m0 : q.n0;
+    const int64_t ld = isA ? p.a.ld : p.b.ld;
+    const uint32_t lane_off = isA ? a_lane : b_lane;
+    uint32_t o0, o1;
+    bool ok;
+    if constexpr (km) {
+      const uint32_t ub = (uint32_t)(((int64_t)r0 * ld + (int64_t)kt * 64) * 2) + (hid & 1) * (uint32_t)((isA ? 64 : 32) * ld * 2);
+      o0 = ub + lane_off;
+      o1 = o0 + (uint32_t)(128 * ld * 2);
+      ok = live && kt * 64 < klim;
+    } else {
+      const int rows = (int)(isA ? p.M : p.N);
+      const int rr = (isA ? a_rr : b_rr) + (hid & 1) * (isA ? 64 : 32);
+      const uint32_t ub = (uint32_t)(((int64_t)kt * 64 * ld + r0) * 2) + (hid & 1) * (uint32_t)((isA ? 64 : 32) * 2);
+      o0 = ub + lane_off;
+      o1 = o0 + (uint32_t)(32 * ld * 2);
+      ok = live && r0 + rr < rows;
+    }
+    if constexpr (ASM_DMA) {
+      const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)dst);
+      pp_glds_asm(isA ? ras : rbs, l, ok ? o0 : PP_OOB);
+      pp_glds_asm(isA ? ras : rbs, l + 8192, ok ? o1 : PP_OOB);
+    } else {
+      pp_glds(isA ? ra : rb, dst, ok ? o0 : PP_OOB);
+      pp_glds(isA ? ra : rb, dst + 8192, ok ? o1 : PP_OOB);
+    }
+  };
+  using HA0 = std::integral_constant<int, H_A0>;
+  using HA1 = std::integral_constant<int, H_A1>;
+  using HB0 = std::integral_constant<int, H_B0>;
+  using HB1 = std::integral_constant<int, H_B1>;
+
+  const int kl0 = pp_klane(lane, 0), kl1 = pp_klane(lane, 32);
+  auto rd_a = [&](const char* half, ppbf16x8 (&f)[8]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (AK) f[kk * 4 + i] = pp_kfrag(half, wr * 64 + 16 * i, kk ? kl1 : kl0);
+        else f[kk * 4 + i] = pp_mfrag(half, wr * 4 + i, kk * 32, lane);
+      }
+  };
+  auto rd_b = [&](const char* half, ppbf16x8 (&f)[4]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (BK) f[kk * 2 + j] = pp_kfrag(half, wc * 32 + 16 * j, kk ? kl1 : kl0);
+        else f[kk * 2 + j] = pp_mfrag(half, wc * 2 + j, kk * 32, lane);
+      }
+  };
+  auto end_load = [&](auto vm_c) {
+    constexpr int VM = decltype(vm_c)::value;
+    if constexpr (VM == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if constexpr (VM == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_sync();
+  };
+  using VM10 = std::integral_constant<int, 10>;
+  using VM12 = std::integral_constant<int, 12>;
+  using VMNONE = std::integral_constant<int, -1>;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 rsacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  auto rs_mma = [&](auto qa_c, const ppbf16x8 (&a)[8]) {
+    if constexpr (RS) {
+      constexpr int QA = decltype(qa_c)::value;
+      const ppbf16x8 ones = __builtin_bit_cast(ppbf16x8, s16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80,
+                                                               0x3F80, 0x3F80});
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        ppbf16x8 f = a[kk * 4];
+        if (wc == 1) f = a[kk * 4 + 1];
+        else if (wc == 2) f = a[kk * 4 + 2];
+        else if (wc == 3) f = a[kk * 4 + 3];
+        rsacc[QA] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f, rsacc[QA], 0, 0, 0);
+      }
+    } else {
+      (void)qa_c;
+      (void)a;
+    }
+  };
+  using Q0 = std::integral_constant<int, 0>;
+  using Q1 = std::integral_constant<int, 1>;
+
+  ppbf16x8 fa[8], fb0[4], fb1[4];
+  // prologue: units 0 and 1 in the issue order of the loop below (Bh0 Ah0 | Bh1 | Ah1 per unit)
+  Pos ip = pos_at(0, 0);
+  issue(HB0{}, 0, ip);
+  issue(HA0{}, 0, ip);
+  issue(HB1{}, 0, ip);
+  issue(HA1{}, 0, ip);
+  advance(ip);
+  issue(HB0{}, 1, ip);
+  issue(HA0{}, 1, ip);
+  issue(HB1{}, 1, ip);
+  issue(HA1{}, 1, ip);
+  advance(ip);  // ip: the unit two ahead of the first computed one
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // Bh0(0), Ah0(0) landed
+  pp_sync();
+  if (lag) pp_sync();
+
+  // One K unit in the EARLY schedule of the per-tile kernel (b0 read beside a0 in phase 0, Bh0 and Ah0
+  // refilled in phase 1): a single b0 register set, so the unit loop needs no parity unroll and the
+  // tile epilogue has one call site (one copy of its code and register live ranges).
+  auto kunit = [&](int slot) {
+    const char* cs = smem + slot * PP_SLOT;
+    rd_a(cs + H_A0 * PP_HALF, fa);
+    rd_b(cs + H_B0 * PP_HALF, fb0);
+    end_load(VM10{});
+    pp_mma<0, 0, 2>(acc, fa, fb0);
+    rs_mma(Q0{}, fa);
+    pp_sync();
+    rd_b(cs + H_B1 * PP_HALF, fb1);
+    issue(HB0{}, slot, ip);
+    issue(HA0{}, slot, ip);
+    end_load(VM12{});
+    pp_mma<0, 1, 2>(acc, fa, fb1);
+    pp_sync();
+    rd_a(cs + H_A1 * PP_HALF, fa);
+    issue(HB1{}, slot, ip);
+    end_load(VMNONE{});
+    pp_mma<1, 1, 2>(acc, fa, fb1);
+    rs_mma(Q1{}, fa);
+    pp_sync();
+    issue(HA1{}, slot, ip);
+    end_load(VM12{});
+    pp_mma<1, 0, 2>(acc, fa, fb0);
+    pp_sync();
+  };
+
+  int u = 0;
+  for (int ti = 0; ti < my_tiles; ++ti) {
+    for (int kt = 0; kt < nk; ++kt, ++u) {
+      kunit(u & 1);
+      advance(ip);
+    }
+    // align the two wave groups, epilogue (the next tile's first two units are in flight), restagger
+    int m0, n0;
+    tile_of(ti, m0, n0);
+    if (!lag) pp_sync();
+    if constexpr (RS) {
+      if ((lane >> 4) == 0) {
+#pragma unroll
+        for (int qa = 0; qa < 2; ++qa) {
+          const int64_t m = m0 + wr * 128 + qa * 64 + 16 * wc + (lane & 15);
+          if (m >= p.M) continue;
+          const float v = rsacc[qa][0];
+          if (p.epi.rowsum_mode == 3) unsafeAtomicAdd((float*)p.epi.rowsum + m, v);
+          else if (p.epi.rowsum_mode == 2) ((bf16_t*)p.epi.rowsum)[m] = f2bf(v);
+          else ((float*)p.epi.rowsum)[m] = v;
+        }
+      }
+      rsacc[0] = rsacc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    wide_tile_epilogue_banded(acc, smem + PP_LDS_LOOP, p.epi, m0, n0, p.M, p.N, m0 / 256);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (lag) pp_sync();
+  }
+  if (!lag) pp_sync();
+  // the refills issued past the last unit (zero-filling) must land before the workgroup exits
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool AK, bool BK, bool RS>
+hipError_t launch_ppp(const PPPArgs& a, int grid, hipStream_t st) {
+  static bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_persist_kernel<AK, BK, RS>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, PPP_LDS);
+    return true;
+  }();
+  (void)attr;
+  gemm_pp_persist_kernel<AK, BK, RS><<<grid, PP_NT, PPP_LDS, st>>>(a);
+  return hipGetLastError();
+}
+
 template <bool AK, bool BK, int VAR, bool RS = false, bool GA = false>
 hipError_t launch_pp_v(const PPArgs& a, int splits, hipStream_t st) {
   static bool attr = [] {
@@ -583,6 +850,54 @@ hipError_t launch_pp_var(bool ak, bool bk, const PPArgs& a, int splits, hipStrea
 }
 
 }  // namespace
+
+// PDA_PP_PERSIST=0: one workgroup per tile (A/B knob for the persistent walk)
+bool pp_persist_mode() {
+  static const bool on = [] {
+    const char* e = getenv("PDA_PP_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+static void pp_magic(uint32_t d, uint32_t& mul, uint32_t& shr);
+
+// Persistent pipelined GEMM (no split-K): hipErrorInvalidValue when the operands do not fit its
+// whole-matrix 32-bit offsets (the caller launches the per-tile kernel instead).
+hipError_t gemm_pp_persistent(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor,
+                              int64_t ldb, int64_t M, int64_t N, int64_t K, const Epi& epi, hipStream_t st) {
+  const int64_t lim = ((int64_t)1 << 31) - 4096;
+  const int64_t a_bytes = a_kmajor ? (M + 256) * lda * 2 : (K + 64) * lda * 2;
+  const int64_t b_bytes = b_kmajor ? (N + 256) * ldb * 2 : (K + 64) * ldb * 2;
+  if (a_bytes >= lim || b_bytes >= lim) return hipErrorInvalidValue;
+  static const int cus = [] {
+    int dev = 0, n = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  PPPArgs a{};
+  a.a = {A, lda, M};
+  a.b = {B, ldb, N};
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.tiles_m = (int)((M + 255) / 256);
+  a.tiles_n = (int)((N + 255) / 256);
+  a.ntiles = a.tiles_m * a.tiles_n;
+  a.nk = (int)((K + 63) / 64);
+  pp_magic((uint32_t)a.nk, a.nk_mul, a.nk_shr);
+  a.epi = epi;
+  a.epi.slab = nullptr;
+  const int grid = a.ntiles < cus ? a.ntiles : cus;
+  if (epi.rowsum) {
+    if (a_kmajor || b_kmajor) return hipErrorInvalidValue;
+    return launch_ppp<false, false, true>(a, grid, st);
+  }
+  if (a_kmajor && b_kmajor) return launch_ppp<true, true, false>(a, grid, st);
+  if (a_kmajor) return launch_ppp<true, false, false>(a, grid, st);
+  if (b_kmajor) return launch_ppp<false, true, false>(a, grid, st);
+  return launch_ppp<false, false, false>(a, grid, st);
+}
 
 int pp_default_variant() {
   static const int v = [] {
@@ -614,6 +929,10 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
   if ((a_kmajor && 257 * lda * 2 >= ((int64_t)1 << 31)) || (b_kmajor && 257 * ldb * 2 >= ((int64_t)1 << 31)))
     return hipErrorInvalidValue;
   if (used_splits) *used_splits = splits;
+  if (splits == 1 && variant < 0 && pp_persist_mode()) {
+    const hipError_t r = gemm_pp_persistent(A, a_kmajor, lda, B, b_kmajor, ldb, M, N, K, epi, st);
+    if (r != hipErrorInvalidValue) return r;
+  }
   PPArgs a{{A, lda, M}, {B, ldb, N}, M, N, K, (int)((N + 255) / 256), kps, epi, {}};
   if (splits <= 1) a.epi.slab = nullptr;
   switch (variant < 0 ? pp_default_variant() : variant) {
@@ -665,6 +984,7 @@ hipError_t gemm_pp_lab(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t
   epi.C = C;
   epi.ldc = ldc;
   epi.bias = bias;
+  if (variant == 100) return gemm_pp_persistent(A, a_kmajor, lda, B, b_kmajor, ldb, M, N, K, epi, st);
   return gemm_pp(A, a_kmajor, lda, B, b_kmajor, ldb, M, N, K, epi, 1, variant, st, nullptr);
 }
 
