@@ -135,6 +135,24 @@ constexpr int WT_SROW = 256 + 8;    // epilogue staging row (bf16 elements)
 constexpr int WT_STAGE_BYTES = 256 * WT_SROW * 2;
 constexpr int WT_STATS_BYTES = (WT_NT / 64) * 256 * 2 * 4;  // BN-statistics scratch
 
+// the wave's bias values, loaded once per tile: column n0 + wc*64 + 16*j + 4*(lane>>4) + q -> bv[j][q]
+// (zero past N or without a bias): 16 loads a thread instead of one per accumulator element (128).
+__device__ __forceinline__ void epi_bias_cols(const Epi& epi, int64_t n0, int64_t N, int wc, int lane,
+                                              float (&bv)[4][4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bv[j][q] = 0.f;
+    if (!epi.bias) continue;
+    // element loads: a bias may be a view into a flat parameter buffer at any element offset
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (n + q < N)
+        bv[j][q] = epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
+  }
+}
+
 // Epilogue of one 256 x 256 tile.  `smem` must hold WT_STAGE_BYTES (bf16 staging) and, at `stats_off`,
 // WT_STATS_BYTES; the caller guarantees every wave is done with the operand LDS (and no LDS-DMA is in
 // flight).  `split` = blockIdx.y of a split-K launch (slab index).
@@ -181,6 +199,8 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][4], cha
 
   // epilogue (bf16 output): bias / relu in registers, stage through LDS, coalesced 16-B row stores
   bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
+  float bv[4][4];
+  epi_bias_cols(epi, n0, N, wc, lane, bv);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int r = wr * 128 + 16 * i + (lane & 15);
@@ -188,13 +208,8 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][4], cha
     for (int j = 0; j < 4; ++j) {
       const int cc = wc * 64 + 16 * j + 4 * (lane >> 4);
       f32x4 v = acc[i][j];
-      if (epi.bias) {
-        const int64_t n = n0 + cc;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (n + q < N)
-            v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
-      }
+      for (int q = 0; q < 4; ++q) v[q] += bv[j][q];
       if (epi.relu) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
@@ -268,6 +283,8 @@ __device__ __forceinline__ void wide_tile_epilogue_banded(const f32x4 (&acc)[8][
     return;
   }
   bf16_t* stg = reinterpret_cast<bf16_t*>(stage);
+  float bv[4][4];
+  epi_bias_cols(epi, n0, N, wc, lane, bv);
   constexpr int CPR = 256 / 8;
   const bool want_stats = epi.stats != nullptr;
   float st1[8], st2[8], kshift[8];
@@ -290,13 +307,8 @@ __device__ __forceinline__ void wide_tile_epilogue_banded(const f32x4 (&acc)[8][
         for (int j = 0; j < 4; ++j) {
           const int cc = wc * 64 + 16 * j + 4 * (lane >> 4);
           f32x4 v = acc[i][j];
-          if (epi.bias) {
-            const int64_t n = n0 + cc;
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-              if (n + q < N)
-                v[q] += epi.bias_f32 ? ((const float*)epi.bias)[n + q] : bf2f(((const bf16_t*)epi.bias)[n + q]);
-          }
+          for (int q = 0; q < 4; ++q) v[q] += bv[j][q];
           if (epi.relu) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);

@@ -82,8 +82,8 @@ __device__ __forceinline__ ppbf16x8 pp_mfrag(const char* half, int r, int kk, in
   return __builtin_bit_cast(ppbf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-__device__ __forceinline__ void pp_glds(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+__device__ __forceinline__ void pp_glds(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff, uint32_t soff = 0) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
 }
 
 // The same DMA as inline asm, for kernels that read an MN-major image with ds_read_b64_tr_b16: beside
@@ -96,6 +96,13 @@ __device__ __forceinline__ void pp_glds_asm(pp_i32x4 r, uint32_t lds, uint32_t v
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
                :
                : "v"(voff), "s"(r), "s"(lds)
+               : "memory", "m0");
+}
+// ... with a uniform byte offset in soffset (the per-lane offset stays one loop-invariant register)
+__device__ __forceinline__ void pp_glds_asm(pp_i32x4 r, uint32_t lds, uint32_t voff, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+               :
+               : "v"(voff), "s"(r), "s"(lds), "s"(soff)
                : "memory", "m0");
 }
 
@@ -156,11 +163,14 @@ __device__ __forceinline__ uint32_t pp_fdiv(uint32_t n, uint32_t mul, uint32_t s
 struct PPSrc {
   __amdgpu_buffer_rsrc_t r;
   pp_i32x4 rs;  // the same descriptor as four words (inline-asm DMA)
+  // per-lane byte offset v (the only per-lane address register); uniform strides dh (half 1), di (the
+  // second DMA of a half), dk (one K tile) travel in soffset.  Validity is explicit per DMA — a lane
+  // out of the operand gets PP_OOB — so no element depends on how the hardware range check treats
+  // soffset:
+  //   K-major: chunk in range for K tile t iff t * 64 < lim; row in range iff rows > h * hr + i * 128
+  //   MN-major: column chunk in range iff lim > h * half stride; k-row t * 64 + kr (+32) < rows
   uint32_t v, dh, di, dk;
-  // K-major: the lane's chunk is in range for K tile t iff t * 64 < lim (rows past the operand lie past
-  // the descriptor's range).  MN-major: rows left from the lane's first column (half h is in range iff
-  // lim > h * half stride); K past the end lies past the descriptor's range.
-  int lim;
+  int lim, rows;
 };
 
 __device__ __forceinline__ pp_i32x4 pp_rsrc_words(const bf16_t* base, int64_t bytes) {
@@ -192,6 +202,8 @@ __device__ __forceinline__ PPSrc pp_src(const PPOp& op, int64_t r0, int64_t k0, 
     s.di = (uint32_t)(128 * op.ld * 2);
     s.dk = 128u;
     s.lim = (int)(K - k0) - chunk * 8;
+    const int64_t rl = op.rows - r0 - rr;  // rows of the operand from the lane's first row
+    s.rows = rl > 0x7fffffff ? 0x7fffffff : (int)rl;
   } else {
     // image k-row round*32 + tid/16 holds the 8 logical columns from pp_mn_col(tid): tile row
     // (lc/64)*128 + h*64 + lc%64 (A) or (lc/32)*64 + h*32 + lc%32 (B)
@@ -209,12 +221,47 @@ __device__ __forceinline__ PPSrc pp_src(const PPOp& op, int64_t r0, int64_t k0, 
     s.dk = (uint32_t)(64 * op.ld * 2);
     const int64_t left = op.rows - r0 - rr;
     s.lim = left > 0x7fffffff ? 0x7fffffff : (int)left;
+    const int64_t kl = (K - k0) - kr;  // k-rows from the lane's first
+    s.rows = kl > 0x7fffffff ? 0x7fffffff : (int)kl;
   }
   return s;
 }
 
 // VAR bits: 1 = s_setprio(1) around each MFMA section, 2 = ping-pong stagger of the two wave groups,
 // 4 = a load section issues its refill DMA before its fragment reads, 8 = two 32-MFMA phases per K tile
+// Row sums of one 16-row tile of A over a K tile (its two 32-deep k-halves) by MFMA against a ones
+// fragment: C = 1 * A^T puts every row's sum in each row of C; lane l (< 16) gets row m = l in c[0].
+// The ones operand is rematerialised per call (opaque moves) and C starts at zero, so only the caller's
+// running float per quadrant lives across the main loop — the persistent-accumulator form (8 registers
+// + 4 for the constant) pushed the MN x MN tile into scratch.
+__device__ __forceinline__ float pp_rowsum_pair(const ppbf16x8& f0, const ppbf16x8& f1) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 o;
+  asm volatile("v_mov_b32 %0, 0x3f803f80\n\tv_mov_b32 %1, 0x3f803f80\n\tv_mov_b32 %2, 0x3f803f80\n\t"
+               "v_mov_b32 %3, 0x3f803f80"
+               : "=v"(o[0]), "=v"(o[1]), "=v"(o[2]), "=v"(o[3]));
+  const ppbf16x8 ones = __builtin_bit_cast(ppbf16x8, o);
+  f32x4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f0, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f1, c, 0, 0, 0);
+  return c[0];
+}
+
+// row sums of wave WC's row tile of a quadrant (a[kk*4 + i]: k-half kk, row tile i).  WC is a template
+// argument: the RS kernels run one copy of the main loop per wave column (a runtime select copies two
+// fragments — 8 registers — and a branch splits the loop's scheduling region; either spilled the MN x MN
+// loop into scratch)
+template <int WC>
+__device__ __forceinline__ float pp_rs_tile(const ppbf16x8 (&a)[8]) {
+  return pp_rowsum_pair(a[WC], a[WC + 4]);
+}
+__device__ __forceinline__ float pp_rs_tile(const ppbf16x8 (&a)[8], int wc) {  // runtime-select form
+  ppbf16x8 f0 = a[0], f1 = a[4];
+  if (wc == 1) { f0 = a[1]; f1 = a[5]; }
+  else if (wc == 2) { f0 = a[2]; f1 = a[6]; }
+  else if (wc == 3) { f0 = a[3]; f1 = a[7]; }
+  return pp_rowsum_pair(f0, f1);
+}
+
 template <bool AK, bool BK, int VAR, bool RS = false, bool GA = false>
 __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -296,18 +343,26 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       }
       return;
     }
-    const uint32_t o = s.v + (hid & 1) * s.dh + (uint32_t)t * s.dk;
-    bool kv;
-    if constexpr (km) kv = t * 64 < s.lim && t < nk;
-    else kv = t < nk && s.lim > (hid & 1) * (isA ? 64 : 32);
+    const uint32_t su = __builtin_amdgcn_readfirstlane((hid & 1) * s.dh + (uint32_t)t * s.dk);
+    bool ok0, ok1;
+    if constexpr (km) {
+      constexpr int hr = (hid & 1) * (isA ? 64 : 32);
+      const bool kv = t < nk && t * 64 < s.lim;
+      ok0 = kv && s.rows > hr;
+      ok1 = kv && s.rows > hr + 128;
+    } else {
+      const bool cv = t < nk && s.lim > (hid & 1) * (isA ? 64 : 32);
+      ok0 = cv && t * 64 < s.rows;
+      ok1 = cv && t * 64 + 32 < s.rows;
+    }
     if constexpr (ASM_DMA) {
       const uint32_t l = __builtin_amdgcn_readfirstlane(
           (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)dst);
-      pp_glds_asm(s.rs, l, kv ? o : PP_OOB);
-      pp_glds_asm(s.rs, l + 8192, kv ? o + s.di : PP_OOB);
+      pp_glds_asm(s.rs, l, ok0 ? s.v : PP_OOB, su);
+      pp_glds_asm(s.rs, l + 8192, ok1 ? s.v : PP_OOB, su + s.di);
     } else {
-      pp_glds(s.r, dst, kv ? o : PP_OOB);
-      pp_glds(s.r, dst + 8192, kv ? o + s.di : PP_OOB);
+      pp_glds(s.r, dst, ok0 ? s.v : PP_OOB, su);
+      pp_glds(s.r, dst + 8192, ok1 ? s.v : PP_OOB, su + s.di);
     }
   };
   using HA0 = std::integral_constant<int, H_A0>;
@@ -363,34 +418,42 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   // RS: row sums of A (Epi::rowsum) by MFMA against a ones fragment — C = A * 1 puts every row's sum in
   // each of its columns.  The 4 waves that share A rows split the row tiles (wave wc takes row tile wc
   // of each 64-row quadrant): 2 MFMAs per A quadrant and K tile, +6 % matrix work, no VALU.
-  f32x4 rsacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  auto rs_mma = [&](auto qa_c, const ppbf16x8 (&a)[8]) {
+  float rsacc[2] = {0.f, 0.f};
+  // only tile column 0 sums (every column tile sees the same A rows: the split-K atomics would count
+  // them tiles_n times)
+  const bool rs_on = RS && n0 == 0;
+  auto rs_mma = [&](auto qa_c, const ppbf16x8 (&a)[8], auto wc_c) {
     if constexpr (RS) {
+      if (!rs_on) return;
       constexpr int QA = decltype(qa_c)::value;
-      typedef short s16x8 __attribute__((ext_vector_type(8)));
-      const ppbf16x8 ones = __builtin_bit_cast(ppbf16x8, s16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80,
-                                                               0x3F80, 0x3F80});
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        ppbf16x8 f = a[kk * 4];
-        if (wc == 1) f = a[kk * 4 + 1];
-        else if (wc == 2) f = a[kk * 4 + 2];
-        else if (wc == 3) f = a[kk * 4 + 3];
-        rsacc[QA] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f, rsacc[QA], 0, 0, 0);
-      }
+      rsacc[QA] += pp_rs_tile<decltype(wc_c)::value>(a);
     } else {
       (void)qa_c;
       (void)a;
+      (void)wc_c;
+    }
+  };
+  // the main loop, instantiated per wave column for RS (pp_rs_tile) and once otherwise
+  auto per_wc = [&](auto body) {
+    if constexpr (RS) {
+      switch (__builtin_amdgcn_readfirstlane(wc)) {
+        case 0: body(std::integral_constant<int, 0>{}); break;
+        case 1: body(std::integral_constant<int, 1>{}); break;
+        case 2: body(std::integral_constant<int, 2>{}); break;
+        default: body(std::integral_constant<int, 3>{}); break;
+      }
+    } else {
+      body(std::integral_constant<int, 0>{});
     }
   };
   auto rs_store = [&]() {
     if constexpr (RS) {
-      if ((lane >> 4) == 0) {
+      if (rs_on && (lane >> 4) == 0) {
 #pragma unroll
         for (int qa = 0; qa < 2; ++qa) {
           const int64_t m = m0 + wr * 128 + qa * 64 + 16 * wc + (lane & 15);
           if (m >= p.M) continue;
-          const float v = rsacc[qa][0];
+          const float v = rsacc[qa];
           if (p.epi.rowsum_mode == 3) unsafeAtomicAdd((float*)p.epi.rowsum + m, v);
           else if (p.epi.rowsum_mode == 2) ((bf16_t*)p.epi.rowsum)[m] = f2bf(v);
           else ((float*)p.epi.rowsum)[m] = v;
@@ -419,7 +482,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0 B0 B1 of tile 0 landed
     pp_sync();
     if (lag) pp_sync();
-    auto ktile2 = [&](auto slot_c, int t) {
+    auto ktile2 = [&](auto slot_c, int t, auto wc_c) {
       constexpr int SLOT = decltype(slot_c)::value;
       const char* cs = smem + SLOT * PP_SLOT;
       rd_a(cs + H_A0 * PP_HALF, ta);
@@ -430,7 +493,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       end_load(VM8{});
       pp_mma<0, 0, VAR>(acc, ta, tb0);
       pp_mma<0, 1, VAR>(acc, ta, tb1);
-      rs_mma(Q0{}, ta);
+      rs_mma(Q0{}, ta, wc_c);
       end_mma();
       rd_a(cs + H_A1 * PP_HALF, ta);
       issue(HA0{}, slot_c, t + 2);
@@ -439,15 +502,17 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       end_load(VM8{});
       pp_mma<1, 0, VAR>(acc, ta, tb0);
       pp_mma<1, 1, VAR>(acc, ta, tb1);
-      rs_mma(Q1{}, ta);
+      rs_mma(Q1{}, ta, wc_c);
       end_mma();
     };
-    int t2 = 0;
-    for (; t2 + 1 < nk; t2 += 2) {
-      ktile2(S0{}, t2);
-      ktile2(S1{}, t2 + 1);
-    }
-    if (t2 < nk) ktile2(S0{}, t2);
+    per_wc([&](auto wc_c) {
+      int t2 = 0;
+      for (; t2 + 1 < nk; t2 += 2) {
+        ktile2(S0{}, t2, wc_c);
+        ktile2(S1{}, t2 + 1, wc_c);
+      }
+      if (t2 < nk) ktile2(S0{}, t2, wc_c);
+    });
     if (STAGGER && !lag) pp_sync();
     rs_store();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -480,7 +545,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   // beside a0 and Bh0 is refilled in phase 1 with Ah0 — one b0 register set, waits recounted:
   //   issue order per tile Bh0 Ah0 | Bh1 | Ah1 (phases 1, 2, 3); vmcnt(10) after phase 0 (Bh1 of this
   //   tile landed), 12 after phase 1 (Ah1), none after 2, 12 after 3 (Ah0 / Bh0 of the next tile).
-  auto ktile = [&](auto slot_c, int t, ppbf16x8 (&b0c)[4], ppbf16x8 (&b0n)[4]) {
+  auto ktile = [&](auto slot_c, int t, ppbf16x8 (&b0c)[4], ppbf16x8 (&b0n)[4], auto wc_c) {
     constexpr int SLOT = decltype(slot_c)::value;
     const char* cs = smem + SLOT * PP_SLOT;
     const char* ns = smem + (SLOT ^ 1) * PP_SLOT;
@@ -489,7 +554,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       rd_b(cs + H_B0 * PP_HALF, b0c);
       end_load(VM10{});
       pp_mma<0, 0, VAR>(acc, fa, b0c);
-      rs_mma(Q0{}, fa);
+      rs_mma(Q0{}, fa, wc_c);
       end_mma();
       rd_b(cs + H_B1 * PP_HALF, fb1);
       issue(HB0{}, slot_c, t + 2);
@@ -501,7 +566,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       issue(HB1{}, slot_c, t + 2);
       end_load(VMNONE{});
       pp_mma<1, 1, VAR>(acc, fa, fb1);
-      rs_mma(Q1{}, fa);
+      rs_mma(Q1{}, fa, wc_c);
       end_mma();
       issue(HA1{}, slot_c, t + 2);
       end_load(VM12{});
@@ -517,7 +582,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       if constexpr (!DMA_FIRST) issue(HB0{}, slot_c, t + 2);
       end_load(VM12{});
       pp_mma<0, 0, VAR>(acc, fa, b0c);
-      rs_mma(Q0{}, fa);
+      rs_mma(Q0{}, fa, wc_c);
       end_mma();
       // phase 1: a0 x b1 (refill Ah0)
       if constexpr (DMA_FIRST) issue(HA0{}, slot_c, t + 2);
@@ -532,7 +597,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       if constexpr (!DMA_FIRST) issue(HB1{}, slot_c, t + 2);
       end_load(VM12{});
       pp_mma<1, 1, VAR>(acc, fa, fb1);
-      rs_mma(Q1{}, fa);
+      rs_mma(Q1{}, fa, wc_c);
       end_mma();
       // phase 3: a1 x b0, next tile's b0 into registers (refill Ah1)
       if constexpr (DMA_FIRST) issue(HA1{}, slot_c, t + 2);
@@ -543,12 +608,14 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       end_mma();
     }
   };
-  int t = 0;
-  for (; t + 1 < nk; t += 2) {
-    ktile(S0{}, t, fb0e, fb0o);
-    ktile(S1{}, t + 1, fb0o, fb0e);
-  }
-  if (t < nk) ktile(S0{}, t, fb0e, fb0o);
+  per_wc([&](auto wc_c) {
+    int t = 0;
+    for (; t + 1 < nk; t += 2) {
+      ktile(S0{}, t, fb0e, fb0o, wc_c);
+      ktile(S1{}, t + 1, fb0o, fb0e, wc_c);
+    }
+    if (t < nk) ktile(S0{}, t, fb0e, fb0o, wc_c);
+  });
   if (STAGGER && !lag) pp_sync();
   rs_store();
   // drain the (zero-filling) DMAs of the tiles past the end before the LDS becomes the staging tile
@@ -707,21 +774,11 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_persist_kernel(PPPArgs p) {
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 rsacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  float rsacc[2] = {0.f, 0.f};
   auto rs_mma = [&](auto qa_c, const ppbf16x8 (&a)[8]) {
     if constexpr (RS) {
       constexpr int QA = decltype(qa_c)::value;
-      const ppbf16x8 ones = __builtin_bit_cast(ppbf16x8, s16x8{0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80,
-                                                               0x3F80, 0x3F80});
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        ppbf16x8 f = a[kk * 4];
-        if (wc == 1) f = a[kk * 4 + 1];
-        else if (wc == 2) f = a[kk * 4 + 2];
-        else if (wc == 3) f = a[kk * 4 + 3];
-        rsacc[QA] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, f, rsacc[QA], 0, 0, 0);
-      }
+      rsacc[QA] += pp_rs_tile(a, wc);
     } else {
       (void)qa_c;
       (void)a;
@@ -787,18 +844,18 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_persist_kernel(PPPArgs p) {
     tile_of(ti, m0, n0);
     if (!lag) pp_sync();
     if constexpr (RS) {
-      if ((lane >> 4) == 0) {
+      if (n0 == 0 && (lane >> 4) == 0) {  // tile column 0 only (see gemm_pp_kernel)
 #pragma unroll
         for (int qa = 0; qa < 2; ++qa) {
           const int64_t m = m0 + wr * 128 + qa * 64 + 16 * wc + (lane & 15);
           if (m >= p.M) continue;
-          const float v = rsacc[qa][0];
+          const float v = rsacc[qa];
           if (p.epi.rowsum_mode == 3) unsafeAtomicAdd((float*)p.epi.rowsum + m, v);
           else if (p.epi.rowsum_mode == 2) ((bf16_t*)p.epi.rowsum)[m] = f2bf(v);
           else ((float*)p.epi.rowsum)[m] = v;
         }
       }
-      rsacc[0] = rsacc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      rsacc[0] = rsacc[1] = 0.f;
     }
     wide_tile_epilogue_banded(acc, smem + PP_LDS_LOOP, p.epi, m0, n0, p.M, p.N, m0 / 256);
 #pragma unroll
@@ -854,8 +911,8 @@ hipError_t launch_pp_var(bool ak, bool bk, const PPArgs& a, int splits, hipStrea
 // PDA_PP_PERSIST=0: one workgroup per tile (A/B knob for the persistent walk)
 bool pp_persist_mode() {
   static const bool on = [] {
-    const char* e = getenv("PDA_PP_PERSIST");
-    return !(e && e[0] == '0');
+    const char* e = getenv("PDA_PP_PERSIST");  // opt-in: measured slower than the per-tile grid so far
+    return e && e[0] == '1';
   }();
   return on;
 }

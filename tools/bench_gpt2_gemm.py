@@ -1,10 +1,13 @@
-"""hipBLASLt (torch.mm) vs the native MFMA GEMM (auto path and forced 256x256 wide tile) on the
-GPT-2-medium training GEMMs (32 x 1024 tokens per GPU): forward, dgrad and wgrad layouts of the
-qkv / proj / fc1 / fc2 projections.  Decides whether a fused-epilogue native GEMM (bias + GELU, GELU
-backward) can replace the library call plus a separate elementwise pass.
+"""hipBLASLt (torch.mm) vs the native GEMMs on the transformer training GEMMs: forward, dgrad and wgrad
+layouts of each projection (GPT-2-medium at 32 x 1024 tokens per GPU by default; ``--model llama``
+for Llama-3-8B's projections at 16 x 1024 tokens).  Native arms: the production dispatch with the
+pipelined 256x256 kernel (``pp``), the same with the pipelined kernel off (the 2-stage wide tile,
+``wide``), and for the weight gradient the fused dW + db entry (``wgrad_db``).  Arms interleave per
+round in one process; the median round is reported.
 
-    python tools/bench_gpt2_gemm.py [tokens] > out.jsonl
+    python tools/bench_gpt2_gemm.py [--tokens T] [--model gpt2|llama] [--kinds fwd,dgrad,wgrad] > out.jsonl
 """
+import argparse
 import json
 import sys
 
@@ -13,53 +16,81 @@ import torch
 sys.path.insert(0, __file__.rsplit("/tools/", 1)[0])
 from pytorchdistributed_amd._native import C  # noqa: E402
 
+MODELS = {
+    "gpt2": [("qkv", 3072, 1024), ("proj", 1024, 1024), ("fc1", 4096, 1024), ("fc2", 1024, 4096),
+             ("lm_head", 50304, 1024)],
+    "llama": [("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336)],
+}
 
-def t(fn, it=20):
-    for _ in range(3):
-        fn()
+
+def t(fn, it):
+    fn()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(it):
         fn()
     e.record()
-    torch.cuda.synchronize()
+    e.synchronize()
     return s.elapsed_time(e) / it
 
 
 def main():
-    T = int(sys.argv[1]) if len(sys.argv) > 1 else 32 * 1024
-    d, f = 1024, 4096
-    for name, N, K in [("qkv", 3 * d, d), ("proj", d, d), ("fc1", f, d), ("fc2", d, f)]:
-        x = torch.randn(T, K, device="cuda").to(torch.bfloat16)
-        w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
-        dy = torch.randn(T, N, device="cuda").to(torch.bfloat16)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tokens", type=int, default=0)
+    ap.add_argument("--model", default="gpt2")
+    ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    T = a.tokens or (32 * 1024 if a.model == "gpt2" else 16 * 1024)
+    kinds = a.kinds.split(",")
+    for name, N, K in MODELS[a.model]:
+        if a.only and name not in a.only.split(","):
+            continue
+        x = (torch.rand(T, K, device="cuda") * 2 - 1).to(torch.bfloat16)
+        w = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).to(torch.bfloat16)
+        dy = (torch.rand(T, N, device="cuda") * 2 - 1).to(torch.bfloat16)
+        bias = torch.zeros(N, device="cuda", dtype=torch.bfloat16)
         y = torch.empty(T, N, device="cuda", dtype=torch.bfloat16)
         dx = torch.empty(T, K, device="cuda", dtype=torch.bfloat16)
         dw = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
+        db = torch.empty(N, device="cuda", dtype=torch.bfloat16)
+
+        def pp(on, fn):
+            def run():
+                C().set_gemm_pp(on)
+                fn()
+            return run
+
         cases = {
-            # forward y = x W^T
-            "fwd": (lambda: torch.mm(x, w.t(), out=y),
-                    lambda: C().gemm(x, True, K, w, True, K, y, N, T, N, K, None, False, True)),
-            # dgrad dx = dy W
-            "dgrad": (lambda: torch.mm(dy, w, out=dx),
-                      lambda: C().gemm(dy, True, N, w, False, K, dx, K, T, K, N, None, False, True)),
-            # wgrad dw = dy^T x
-            "wgrad": (lambda: torch.mm(dy.t(), x, out=dw),
-                      lambda: C().gemm(dy, False, N, x, False, K, dw, K, N, K, T, None, False, True)),
+            "fwd": {"blas": lambda: torch.addmm(bias, x, w.t(), out=y),
+                    "pp": pp(1, lambda: C().gemm(x, True, K, w, True, K, y, N, T, N, K, bias, False, True)),
+                    "wide": pp(0, lambda: C().gemm(x, True, K, w, True, K, y, N, T, N, K, bias, False, True))},
+            "dgrad": {"blas": lambda: torch.mm(dy, w, out=dx),
+                      "pp": pp(1, lambda: C().gemm(dy, True, N, w, False, K, dx, K, T, K, N, None, False, True)),
+                      "wide": pp(0, lambda: C().gemm(dy, True, N, w, False, K, dx, K, T, K, N, None, False, True))},
+            "wgrad": {"blas": lambda: (torch.mm(dy.t(), x, out=dw), torch.sum(dy, 0, out=db)),
+                      "pp": pp(1, lambda: C().gemm(dy, False, N, x, False, K, dw, K, N, K, T, None, False, True)),
+                      "wgrad_db": pp(1, lambda: C().gemm_wgrad_db(dy, x, dw, db)),
+                      "wide": pp(0, lambda: C().gemm(dy, False, N, x, False, K, dw, K, N, K, T, None, False, True))},
         }
-        fl = 2 * T * N * K
-        for kind, (blas, native) in cases.items():
-            tb = t(blas)
-            C().set_gemm_paths(-1)
-            ta = t(native)
-            C().set_gemm_paths(2)
-            tw = t(native)
-            C().set_gemm_paths(-1)
-            print(json.dumps({"gemm": name, "kind": kind, "M": T, "N": N, "K": K,
-                              "blas_ms": round(tb, 4), "blas_tflops": round(fl / tb / 1e9, 1),
-                              "native_auto_ms": round(ta, 4), "native_auto_tflops": round(fl / ta / 1e9, 1),
-                              "native_wide_ms": round(tw, 4), "native_wide_tflops": round(fl / tw / 1e9, 1)}),
-                  flush=True)
+        fl = 2.0 * T * N * K
+        for kind in kinds:
+            arms = cases[kind]
+            times = {k: [] for k in arms}
+            for _ in range(a.rounds):
+                for k, fn in arms.items():
+                    times[k].append(t(fn, a.iters))
+            C().set_gemm_pp(-1)
+            rec = {"gemm": name, "kind": kind, "T": T, "N": N, "K": K}
+            for k, ts in times.items():
+                ms = sorted(ts)[len(ts) // 2]
+                rec[f"{k}_ms"] = round(ms, 4)
+                rec[f"{k}_tflops"] = round(fl / ms / 1e9, 1)
+            print(json.dumps(rec), flush=True)
+        del x, w, dy, y, dx, dw
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
