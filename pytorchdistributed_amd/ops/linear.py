@@ -5,12 +5,13 @@ GPU, bf16 with in/out features multiples of 8: the MFMA GEMM (forward K-major x 
 K-major x MN-major, wgrad MN-major x MN-major via LDS transpose reads, split-K when the tile grid is
 small).  GPU otherwise (fp32 models, odd widths): the general-stride SIMT GEMM kernel.
 
-Plain (epilogue-free) large GEMMs go to the vendor library (hipBLASLt through ``torch.mm``) under
-``PDA_GEMM=auto`` (default): on 4096^3 bf16 it runs 1.48 PF/s against 1.13 PF/s for the native
-256x256 wide tile, and 1.22-1.49 vs 1.06-1.15 PF/s on the GPT-2-medium GEMM shapes (interleaved
-same-box rounds, profiles/r3_wide_pingpong_DROPPED.jsonl, whose ping-pong schedules were slower
-still); a plain GEMM is exactly the case the library is tuned for.  Fused cases (ReLU epilogue) and everything else stay native;
-``PDA_GEMM=native`` forces the native kernel everywhere, ``PDA_GEMM=blas`` the library.
+Every bf16 GEMM runs on the native kernels: the pipelined 256x256 tile (csrc/kernels/gemm_pp.hip) takes
+the large ones in all three operand layouts — on the GPT-2-medium / Llama-3-8B training shapes it is
+within 85-95 % of hipBLASLt on the forward (both operands K-major), at parity on the data gradient and
+1.1-2.7x faster on the weight gradient, whose bias gradient it produces in the same pass
+(profiles/r4_gpt2_gemm_shapes_pp.jsonl, r4_llama_gemm_shapes_pp.jsonl); whole steps: GPT-2-medium 300k
+vs 286k tok/s, Llama-3-8B FSDP 18.8k vs 18.6k (profiles/r4_gpt2_native_ab.jsonl, r4_llama_native_ab.jsonl).
+There is no vendor-library path.
 """
 from __future__ import annotations
 
@@ -30,24 +31,11 @@ def _mfma_ok(x2, w):
 
 
 _SIDE_MAX_NUMEL = 256 * 256 * 256  # 256 CUs x one 256x256 tile
-_BLAS_MIN_WORK = 1 << 27  # M*N*K below this: launch-latency bound, the native kernel is as good
-_WGRAD_BLAS_MIN_OUT = int(os.environ.get("PDA_WGRAD_BLAS_MIN_OUT", "0"))
-
-
-def _use_blas(a, b, M, N, K) -> bool:
-    mode = os.environ.get("PDA_GEMM", "auto")
-    if mode == "native" or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
-        return False
-    return mode == "blas" or M * N * K >= _BLAS_MIN_WORK
 
 
 def _gemm_fwd(x2, w, b, relu):
     M, K = x2.shape
     N = w.shape[0]
-    if not relu and M > 0 and _use_blas(x2, w, M, N, K):
-        if b is not None:
-            return torch.addmm(b.to(x2.dtype), x2, w.t())
-        return torch.mm(x2, w.t())
     if _mfma_ok(x2, w):
         y = torch.empty(M, N, device=x2.device, dtype=x2.dtype)
         if M > 0:
@@ -67,8 +55,6 @@ def _gemm_dgrad(dy, w):
     dx = torch.empty(M, K, device=dy.device, dtype=dy.dtype)
     if M == 0:
         return dx
-    if _use_blas(dy, w, M, N, K):
-        return torch.mm(dy, w, out=dx)
     if _mfma_ok(dy, w):
         # dx[M,K] = dy[M,N] W[N,K]:  A = dy (K-major, lda N), B(k=n, col=kk) = W[n*K + kk] (MN-major, ldb K)
         C().gemm(dy, True, N, w, False, K, dx, K, M, K, N, None, False, True)
@@ -83,14 +69,6 @@ def _gemm_wgrad(dy, x2, out_dtype, target=None):
     dw = target if target is not None else torch.empty(N, K, device=dy.device, dtype=out_dtype)
     if M == 0:
         return dw.zero_()
-    # PDA_WGRAD_BLAS_MIN_OUT > 0: hipBLASLt only for weight gradients with at least that many outputs.
-    # In isolation the native tile wins below 4M outputs (GPT-2-medium proj / qkv at 32K tokens: 660 /
-    # 694 vs 350 / 584 TFLOP/s, profiles/r2_gpt2_gemm_shapes.jsonl), but inside the step, beside the
-    # critical-path kernels on the side stream, it cost 1 % (profiles/r2_gpt2_mlp_fused_ab.jsonl); with
-    # the native split-K grids sized for 192 CUs: 4M -> +0.15 % (noise), every wgrad native -> -4.9 %
-    # (profiles/r2_gpt2_wgrad_native_vs_blas_v27.jsonl): default 0 = the library for every large plain GEMM
-    if dw.dtype == dy.dtype and N * K >= _WGRAD_BLAS_MIN_OUT and _use_blas(dy, x2, M, N, K):
-        return torch.mm(dy.t(), x2, out=dw)
     if dy.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and N % 8 == 0 and K % 8 == 0:
         # dw[N,K] = dy^T x: A(m=n, k=r) = dy[r*N + n] (MN-major), B(k=r, col) = x[r*K + col] (MN-major)
         C().gemm(dy, False, N, x2, False, K, dw, K, N, K, M, None, False, True)
@@ -102,7 +80,7 @@ def _gemm_wgrad(dy, x2, out_dtype, target=None):
 def _fused_wgrad_db(dy2, x2, wparam, bparam, target):
     """dW and db from ONE pipelined GEMM (db = row sums of its A operand dY^T), or None when
     the shape does not take that kernel (the caller falls back to GEMM + column sum)."""
-    if os.environ.get("PDA_WGRAD_DB_FUSED", "1") != "1" or _use_blas(dy2, x2, *dy2.shape, x2.shape[1]):
+    if os.environ.get("PDA_WGRAD_DB_FUSED", "1") != "1":
         return None
     if not (dy2.dtype == x2.dtype == torch.bfloat16 and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0):
         return None
@@ -231,14 +209,12 @@ class _MlpGeluFn(torch.autograd.Function):
 
 
 def mlp_fused_ok(x, w1, w2) -> bool:
-    """The fused GELU MLP applies: GPU bf16, widths multiples of 8, ``PDA_MLP_FUSED=1``.  Off by default:
-    on GPT-2-medium (32 x 1024 tokens) the native tile's fc1 forward / fc2 dgrad run at ~85 % of
-    hipBLASLt's rate and the 256x256 tile's epilogue (one workgroup per CU, a second [tokens, 4d]
-    stream in it) is exposed, which outweighs the two elementwise passes it removes: 303-305k vs
-    311-312k tokens/s same box (profiles/r2_gpt2_mlp_fused_ab.jsonl); still 300-302k vs 309-310k with
-    the fc2 dgrad on a K-major transposed weight (profiles/r3_gpt2_mlp_fused_wt_DROPPED.jsonl)."""
+    """The fused GELU MLP applies: GPU bf16, widths multiples of 8, ``PDA_MLP_FUSED`` not ``0``.  On by
+    default since the pipelined tile carries the forward / backward GEMMs: GPT-2-medium 308.7k vs 300.4k
+    tok/s unfused (profiles/r4_gpt2_native_ab.jsonl; it lost to hipBLASLt + two elementwise passes while
+    the GEMMs were the 2-stage wide tile, r2_gpt2_mlp_fused_ab.jsonl / r3_gpt2_mlp_fused_wt_DROPPED.jsonl)."""
     return (x.is_cuda and x.dtype == torch.bfloat16 and _mfma_ok(x, w1) and _mfma_ok(x, w2)
-            and os.environ.get("PDA_MLP_FUSED", "0") == "1")
+            and os.environ.get("PDA_MLP_FUSED", "1") != "0")
 
 
 def mlp_gelu(x, w1, b1, w2, b2):

@@ -685,12 +685,13 @@ def test_linear_op_all_paths():
             assert rel_err(a.cpu(), r.detach()) < tol
 
 
-@pytest.mark.parametrize("mode", ["native", "blas"])
-def test_linear_gemm_backends(mode, monkeypatch):
-    """Plain bf16 Linear through the native MFMA kernel and through hipBLASLt, fwd + bwd vs fp32."""
+@pytest.mark.parametrize("fused_db", ["1", "0"])
+def test_linear_gemm_native(fused_db, monkeypatch):
+    """Plain bf16 Linear on the native MFMA kernels (no vendor-library path), fwd + bwd vs fp32, with the
+    bias gradient from the weight-gradient GEMM (PDA_WGRAD_DB_FUSED=1) and from the column-sum kernel."""
     from pytorchdistributed_amd.ops import linear
 
-    monkeypatch.setenv("PDA_GEMM", mode)
+    monkeypatch.setenv("PDA_WGRAD_DB_FUSED", fused_db)
     torch.manual_seed(9)
     x = torch.randn(300, 256).to(torch.bfloat16).float()
     w = (torch.randn(136, 256) * 0.05).to(torch.bfloat16).float()
