@@ -135,13 +135,14 @@ constexpr int WT_SROW = 256 + 8;    // epilogue staging row (bf16 elements)
 constexpr int WT_STAGE_BYTES = 256 * WT_SROW * 2;
 constexpr int WT_STATS_BYTES = (WT_NT / 64) * 256 * 2 * 4;  // BN-statistics scratch
 
-// the wave's bias values, loaded once per tile: column n0 + wc*64 + 16*j + 4*(lane>>4) + q -> bv[j][q]
-// (zero past N or without a bias): 16 loads a thread instead of one per accumulator element (128).
+// the wave's bias values, loaded once per tile: column n0 + wc*(16*JT) + 16*j + 4*(lane>>4) + q -> bv[j][q]
+// (zero past N or without a bias): 4*JT loads a thread instead of one per accumulator element.
+template <int JT = 4>
 __device__ __forceinline__ void epi_bias_cols(const Epi& epi, int64_t n0, int64_t N, int wc, int lane,
-                                              float (&bv)[4][4]) {
+                                              float (&bv)[JT][4]) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
+  for (int j = 0; j < JT; ++j) {
+    const int64_t n = n0 + wc * 16 * JT + 16 * j + 4 * (lane >> 4);
 #pragma unroll
     for (int q = 0; q < 4; ++q) bv[j][q] = 0.f;
     if (!epi.bias) continue;
@@ -153,13 +154,16 @@ __device__ __forceinline__ void epi_bias_cols(const Epi& epi, int64_t n0, int64_
   }
 }
 
-// Epilogue of one 256 x 256 tile.  `smem` must hold WT_STAGE_BYTES (bf16 staging) and, at `stats_off`,
-// WT_STATS_BYTES; the caller guarantees every wave is done with the operand LDS (and no LDS-DMA is in
-// flight).  `split` = blockIdx.y of a split-K launch (slab index).
-__device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][4], char* smem, int stats_off, const Epi& epi,
-                                                   int64_t m0, int64_t n0, int64_t M, int64_t N, int tm, int split) {
+// Shared epilogue of the 256 x 256 tiles.  WCOLS = wave columns: 4 (8 waves of 128 x 64, acc[8][4]: the
+// wide kernel of gemm_conv.hip and gemm_pp.hip) or 2 (4 waves of 128 x 128, acc[8][8]: gemm_pp4.hip).
+// acc[i][j][q] is C(row wr*128 + 16 i + (lane & 15), col wc*(16*JT) + 16 j + 4 (lane >> 4) + q).
+template <int WCOLS = 4>
+__device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][16 / WCOLS], char* smem, int stats_off,
+                                                   const Epi& epi, int64_t m0, int64_t n0, int64_t M, int64_t N, int tm,
+                                                   int split) {
+  constexpr int JT = 16 / WCOLS, NT = 128 * WCOLS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
+  const int wr = wid / WCOLS, wc = wid % WCOLS;
   if (epi.slab || epi.c_f32) {
     // fp32 output (split-K slab partials or an fp32 C): 16-B stores straight from the accumulators
 #pragma unroll
@@ -167,8 +171,8 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][4], cha
       const int64_t m = m0 + wr * 128 + 16 * i + (lane & 15);
       if (m >= M) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
+      for (int j = 0; j < JT; ++j) {
+        const int64_t n = n0 + wc * 16 * JT + 16 * j + 4 * (lane >> 4);
         if (n >= N) continue;
         f32x4 v = acc[i][j];
         if (epi.slab) {
@@ -199,14 +203,14 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][4], cha
 
   // epilogue (bf16 output): bias / relu in registers, stage through LDS, coalesced 16-B row stores
   bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
-  float bv[4][4];
-  epi_bias_cols(epi, n0, N, wc, lane, bv);
+  float bv[JT][4];
+  epi_bias_cols<JT>(epi, n0, N, wc, lane, bv);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int r = wr * 128 + 16 * i + (lane & 15);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int cc = wc * 64 + 16 * j + 4 * (lane >> 4);
+    for (int j = 0; j < JT; ++j) {
+      const int cc = wc * 16 * JT + 16 * j + 4 * (lane >> 4);
       f32x4 v = acc[i][j];
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] += bv[j][q];
@@ -222,7 +226,7 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][4], cha
   }
   __syncthreads();
   constexpr int CPR = 256 / 8;
-  static_assert(WT_NT % CPR == 0, "a thread keeps one column chunk");
+  static_assert(NT % CPR == 0, "a thread keeps one column chunk");
   const bool want_stats = epi.stats != nullptr;
   float st1[8], st2[8], kshift[8];
   {
@@ -233,7 +237,7 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][4], cha
       kshift[q] = (want_stats && n + q < N) ? epi.stats_shift[n + q] : 0.f;
     }
   }
-  for (int c = tid; c < 256 * CPR; c += WT_NT) {
+  for (int c = tid; c < 256 * CPR; c += NT) {
     const int r = c / CPR, ch = c % CPR;
     const int64_t m = m0 + r, n = n0 + ch * 8;
     if (m >= M || n >= N) continue;
@@ -256,7 +260,7 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][4], cha
     }
     *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
   }
-  if (want_stats) epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + stats_off), CPR, WT_NT, tm, n0, N);
+  if (want_stats) epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + stats_off), CPR, NT, tm, n0, N);
 }
 
 // Persistent-kernel variant of the bf16 epilogue (gemm_pp.hip): the next tile's operand DMAs are in

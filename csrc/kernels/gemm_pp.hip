@@ -881,6 +881,180 @@ hipError_t launch_ppp(const PPPArgs& a, int grid, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------------------
+// 4-wave variant (one wave per SIMD): 256 threads, 2 x 2 waves of 128 x 128 (acc[8][8] = 256 registers,
+// the accumulator file), so each fragment read feeds 8 MFMAs instead of 4 / 2 — 32 ds_read_b128 per 128
+// MFMAs per K tile, 2/3 of the 8-wave tile's LDS traffic per MFMA.  With no partner wave on the SIMD
+// the latency hiding is all software: the two 32-deep k halves of a K tile are double-buffered in
+// registers (fragments of half kk+1 are read while half kk multiplies), the LDS holds two K-tile
+// stages (tile t+2 is DMA'd into t's stage as soon as every wave has read it), and the DMA / fragment
+// reads are interleaved with the MFMAs by sched_group_barrier so the matrix pipe never waits on an
+// issue burst.  Two barriers per K tile: (B1) stage t fully read -> refill it; (B2) tile t+1 landed.
+// Stage = four [128][64] K-major half images: A rows 0-127 / 128-255, B rows 0-127 / 128-255.
+constexpr int P4_NT = 256;
+constexpr int P4_STAGE = 4 * PP_HALF;
+constexpr int P4_LOOP = 2 * P4_STAGE;
+constexpr int P4_STATS_OFF = WT_STAGE_BYTES > P4_LOOP ? WT_STAGE_BYTES : P4_LOOP;
+constexpr int P4_LDS = P4_STATS_OFF + 4 * 256 * 2 * 4;
+static_assert(P4_LDS <= 160 * 1024, "LDS budget");
+
+// K-major DMA source for the 4-wave tile: a 128-row half image is 4 rounds of 32 rows; lane l of wave w
+// fills image row R = round*32 + w*8 + l/8, physical chunk l & 7 = logical chunk (l & 7) ^ ((R >> 1) & 7).
+struct P4Src {
+  __amdgpu_buffer_rsrc_t r;
+  uint32_t v, ld2;  // per-lane byte offset; row stride in bytes
+  int lim, rows;    // K left from the lane's chunk; rows left from the lane's round-0 row
+};
+
+__device__ __forceinline__ P4Src p4_src(const PPOp& op, int64_t r0, int64_t k0, int64_t K, int wid, int lane) {
+  P4Src s;
+  const int chunk = (lane & 7) ^ ((wid * 4 + (lane >> 4)) & 7);
+  const int rr = wid * 8 + (lane >> 3);
+  const bf16_t* base = op.p + r0 * op.ld + k0;
+  const int64_t rem = (((op.rows - r0) - 1) * op.ld + (K - k0)) * 2;
+  s.r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(rem < 0x7fffffff ? rem : 0x7fffffff),
+                                          0x00020000);
+  s.v = (uint32_t)((rr * op.ld + chunk * 8) * 2);
+  s.ld2 = (uint32_t)(op.ld * 2);
+  s.lim = (int)(K - k0) - chunk * 8;
+  const int64_t rl = op.rows - r0 - rr;
+  s.rows = rl > 0x7fffffff ? 0x7fffffff : (int)rl;
+  return s;
+}
+
+template <bool AK, bool BK>
+__global__ void __launch_bounds__(P4_NT) gemm_pp4_kernel(PPArgs p) {
+  static_assert(AK && BK, "4-wave tile: K-major operands");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+
+  const int ntiles = gridDim.x;
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  int tm, tn;
+  grouped_tile(tile, ntiles / p.tiles_n, p.tiles_n, 8, tm, tn);
+  const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
+  const int ktiles = (int)((p.K + 63) >> 6);
+  const int kt0 = blockIdx.y * p.kt_per_split;
+  const int nk = min(ktiles, kt0 + p.kt_per_split) - kt0;
+  const int64_t k0 = (int64_t)kt0 * 64;
+
+  const P4Src sa = p4_src(p.a, m0, k0, p.K, wid, lane);
+  const P4Src sb = p4_src(p.b, n0, k0, p.K, wid, lane);
+
+  // K tile t into stage (t & 1): 8 DMAs per operand and thread (2 halves x 4 rounds); tiles past the
+  // split and rows / K past the operand read zero
+  auto issue_op = [&](const P4Src& s, int hbase, int t, int stage) {
+    const bool kv = t < nk && t * 64 < s.lim;
+    char* dst = smem + stage * P4_STAGE + hbase * PP_HALF + wid * 1024;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = h * 128 + i * 32;
+        const uint32_t su = __builtin_amdgcn_readfirstlane((uint32_t)row * s.ld2 + (uint32_t)t * 128u);
+        pp_glds(s.r, dst + h * PP_HALF + i * 4096, kv && s.rows > row ? s.v : PP_OOB, su);
+      }
+  };
+  auto issue = [&](int t, int stage) {
+    issue_op(sa, 0, t, stage);
+    issue_op(sb, 2, t, stage);
+  };
+
+  const int kl0 = pp_klane(lane, 0), kl1 = pp_klane(lane, 32);
+  // fragment x of a k half in the order the MFMAs (row-major over acc) first use them: a0, b0..b7, a1..a7
+  auto rd1 = [&](const char* stg, int kl, int x, ppbf16x8 (&fa)[8], ppbf16x8 (&fb)[8]) {
+    if (x == 0) fa[0] = pp_kfrag(stg + wr * PP_HALF, 0, kl);
+    else if (x <= 8) fb[x - 1] = pp_kfrag(stg + (2 + wc) * PP_HALF, 16 * (x - 1), kl);
+    else fa[x - 8] = pp_kfrag(stg + wr * PP_HALF, 16 * (x - 8), kl);
+  };
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // The MFMAs are inline asm with the accumulator pinned to the AGPR file ("+a"): with the builtin,
+  // hipcc keeps the 256-register accumulator in the mixed class and shuffles it between the files
+  // (~200 v_accvgpr moves per K tile) once the fragments and addresses need their VGPRs.  asm MFMAs
+  // are invisible to sched_group_barrier, so the interleave is spelled out: each step is one extra
+  // instruction (a fragment read or an LDS-DMA) then a group of MFMAs, fenced by sched_barrier.
+  auto mfma = [&](int i, int j, const ppbf16x8 (&fa)[8], const ppbf16x8 (&fb)[8]) {
+    asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][j]) : "v"(fb[j]), "v"(fa[i]));
+  };
+  ppbf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  issue(0, 0);
+  issue(1, 1);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  pp_sync();
+#pragma unroll
+  for (int x = 0; x < 16; ++x) rd1(smem, kl0, x, fa0, fb0);
+  auto ktile = [&](auto st_c, int t) {
+    constexpr int ST = decltype(st_c)::value;
+    const char* cur = smem + ST * P4_STAGE;
+    const char* nxt = smem + (ST ^ 1) * P4_STAGE;
+    // (1) k half 0 multiplies (64 MFMAs); k half 1's 16 fragments are read one per 4 MFMAs
+#pragma unroll
+    for (int x = 0; x < 16; ++x) {
+      rd1(cur, kl1, x, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int y = 0; y < 4; ++y) mfma(x >> 1, (x & 1) * 4 + y, fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_sync();  // B1: every wave has read stage t
+    // (2) stage t <- tile t+2 (16 DMAs, one per 2 MFMAs) under rows 0-3 of k half 1
+#pragma unroll
+    for (int x = 0; x < 16; ++x) {
+      const P4Src& s = x < 8 ? sa : sb;
+      const int h = (x >> 2) & 1, i = x & 3, row = h * 128 + i * 32;
+      const bool kv = t + 2 < nk && (t + 2) * 64 < s.lim;
+      const uint32_t su = __builtin_amdgcn_readfirstlane((uint32_t)row * s.ld2 + (uint32_t)(t + 2) * 128u);
+      pp_glds(s.r, smem + ST * P4_STAGE + ((x < 8 ? 0 : 2) + h) * PP_HALF + i * 4096 + wid * 1024,
+              kv && s.rows > row ? s.v : PP_OOB, su);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma(x >> 2, (x & 3) * 2, fa1, fb1);
+      mfma(x >> 2, (x & 3) * 2 + 1, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    pp_sync();  // B2: tile t+1 landed for every wave
+    // (3) k half 0 of tile t+1 read (one fragment per 2 MFMAs) under rows 4-7 of k half 1
+#pragma unroll
+    for (int x = 0; x < 16; ++x) {
+      rd1(nxt, kl0, x, fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma(4 + (x >> 2), (x & 3) * 2, fa1, fb1);
+      mfma(4 + (x >> 2), (x & 3) * 2 + 1, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  int t = 0;
+  for (; t + 1 < nk; t += 2) {
+    ktile(std::integral_constant<int, 0>{}, t);
+    ktile(std::integral_constant<int, 1>{}, t + 1);
+  }
+  if (t < nk) ktile(std::integral_constant<int, 0>{}, t);
+  asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA's result -> the epilogue's accumulator reads
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  wide_tile_epilogue<2>(acc, smem, P4_STATS_OFF, p.epi, m0, n0, p.M, p.N, tm, blockIdx.y);
+}
+
+template <bool AK, bool BK>
+hipError_t launch_pp4(const PPArgs& a, int splits, hipStream_t st) {
+  static bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp4_kernel<AK, BK>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, P4_LDS);
+    return true;
+  }();
+  (void)attr;
+  const int tiles = (int)((a.M + 255) / 256) * a.tiles_n;
+  gemm_pp4_kernel<AK, BK><<<dim3(tiles, splits), P4_NT, P4_LDS, st>>>(a);
+  return hipGetLastError();
+}
+
 template <bool AK, bool BK, int VAR, bool RS = false, bool GA = false>
 hipError_t launch_pp_v(const PPArgs& a, int splits, hipStream_t st) {
   static bool attr = [] {
@@ -992,7 +1166,9 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
   }
   PPArgs a{{A, lda, M}, {B, ldb, N}, M, N, K, (int)((N + 255) / 256), kps, epi, {}};
   if (splits <= 1) a.epi.slab = nullptr;
-  switch (variant < 0 ? pp_default_variant() : variant) {
+  const int var = variant < 0 ? pp_default_variant() : variant;
+  if (var == 200 && a_kmajor && b_kmajor && !epi.rowsum) return launch_pp4<true, true>(a, splits, st);
+  switch (var) {
     case 0: return launch_pp_var<0>(a_kmajor, b_kmajor, a, splits, st);
     case 1: return launch_pp_var<1>(a_kmajor, b_kmajor, a, splits, st);
     case 3: return launch_pp_var<3>(a_kmajor, b_kmajor, a, splits, st);

@@ -129,12 +129,13 @@ def test_gemm_wide_layouts(M, N, K, split, ak, bk, force_wide):
 @pytest.mark.parametrize("M,N,K", [(1000, 264, 136), (256, 520, 72), (296, 256, 1600), (8, 8, 8), (512, 768, 4096),
                                    (2048, 2048, 1024)])
 @pytest.mark.parametrize("ak,bk", [(True, True), (True, False), (False, False)])
-@pytest.mark.parametrize("variant", [0, 3, 6, 10, 100])
+@pytest.mark.parametrize("variant", [0, 3, 6, 10, 100, 200])
 def test_gemm_pp_variants(M, N, K, ak, bk, variant):
     """Pipelined 256x256 GEMM (gemm_pp.hip) through its lab entry: every operand layout used in training
     (fwd K x K, dgrad K x MN, wgrad MN x MN), ragged M / N / K (rows past the operand and K past the end
     read zero through the buffer descriptors), the plain (0), ping-pong + setprio (3), DMA-first (6),
-    two-phase (10) schedules and the persistent tile walk (100), bias."""
+    two-phase (10) schedules, the persistent tile walk (100) and the 4-wave 128x128-per-wave tile (200,
+    K-major x K-major; the other layouts fall back to the default schedule), bias."""
     torch.manual_seed(21)
     A = torch.rand(M, K) * 2 - 1
     B = torch.rand(K, N) * 2 - 1
