@@ -657,7 +657,9 @@ bool gemm_wgrad_db(Tensor dy, Tensor x, Tensor dw, Tensor db) {
   for (auto* t : {&dy, &x, &dw}) check_aligned16(*t, "gemm_wgrad_db operand");
   c10::DeviceGuard g(dy.device());
   const int64_t slab_n = pda::gemm_slab_floats(Nout, Kin, T, true);
-  Tensor scratch = at::empty({slab_n + Nout}, dy.options().dtype(at::kFloat));
+  // [splits][Nout] split-K row sums after the slab (its split count bounds the launch's)
+  const int64_t rs_n = slab_n > 0 ? slab_n / Kin : Nout;
+  Tensor scratch = at::empty({slab_n + rs_n}, dy.options().dtype(at::kFloat));
   int done = 0;
   CHECK_HIP_OK(pda::gemm_bf16_wgrad_db(bp(dy), Nout, bp(x), Kin, dw.data_ptr(), dw.scalar_type() == at::kFloat, Kin,
                                        Nout, Kin, T, db.data_ptr(), is_bf16(db),

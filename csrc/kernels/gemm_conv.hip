@@ -1945,11 +1945,12 @@ bool pp_conv_mode() {
 // returns hipErrorNotSupported when the pipelined kernel cannot take the shape (the caller falls back)
 template <class LA, class LB>
 hipError_t launch_pp_plain(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st,
-                           int splits, float* slab) {
+                           int splits, float* slab, int* used_out = nullptr) {
   Epi e = epi;
   if (splits > 1) e.slab = slab;
   int used = splits;
   const hipError_t r = gemm_pp(la.p, LA::kMajor, la.ld, lb.p, LB::kMajor, lb.ld, M, N, K, e, splits, -1, st, &used);
+  if (used_out) *used_out = used;
   if (r == hipErrorInvalidValue) return hipErrorNotSupported;
   if (r != hipSuccess || used <= 1) return r;
   int ll = 0;
@@ -2044,19 +2045,23 @@ hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* 
   return dispatch_bn<PlainMN, PlainMN>(M, N, K, p, epi, slab, st, mk_amn, mk_bmn);
 }
 
+// db[i] = sum over the split-K launches' row sums src[s][i]
 __global__ void __launch_bounds__(256) rowsum_cast_kernel(const float* __restrict__ src, void* dst, int bf16_out,
-                                                          int64_t n) {
+                                                          int64_t n, int splits) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  if (bf16_out) ((bf16_t*)dst)[i] = f2bf(src[i]);
-  else ((float*)dst)[i] = src[i];
+  float v = 0.f;
+  for (int s = 0; s < splits; ++s) v += src[(int64_t)s * n + i];
+  if (bf16_out) ((bf16_t*)dst)[i] = f2bf(v);
+  else ((float*)dst)[i] = v;
 }
 
 // Weight gradient with the bias gradient folded in: dw[M, N] = dy^T x with dy [K, M] and x
 // [K, N] (both MN-major, K = tokens), and db[M] = column sums of dy = row sums of the A operand, computed
 // by the pipelined kernel's extra MFMAs when the GEMM takes the 256 x 256 path (*db_done = 1); otherwise
-// *db_done = 0 and only dw is written.  Split-K launches add their partial sums into `rs_scratch`
-// (M floats, zeroed here) and a cast pass writes db.
+// *db_done = 0 and only dw is written.  Split-K launches store their partial sums at `rs_scratch`
+// [split][M] (sized by the caller for the slab's split count; no zeroing pass) and a pass sums them
+// into db.
 hipError_t gemm_bf16_wgrad_db(const bf16_t* dy, int64_t ld_dy, const bf16_t* x, int64_t ld_x, void* dw, bool dw_f32,
                               int64_t ldc, int64_t M, int64_t N, int64_t K, void* db, bool db_bf16, float* slab,
                               float* rs_scratch, hipStream_t st, int* db_done) {
@@ -2072,18 +2077,20 @@ hipError_t gemm_bf16_wgrad_db(const bf16_t* dy, int64_t ld_dy, const bf16_t* x, 
     if (ws > 0) {
       Epi e = epi;
       if (ws > 1) {
-        PDA_CHECK_HIP(hipMemsetAsync(rs_scratch, 0, M * sizeof(float), st));
         e.rowsum = rs_scratch;
-        e.rowsum_mode = 3;
+        e.rowsum_mode = 4;
       } else {
         e.rowsum = db;
         e.rowsum_mode = db_bf16 ? 2 : 1;
       }
-      const hipError_t r = launch_pp_plain(mk_amn(PlainMN<64>{}), mk_bmn(PlainMN<64>{}), M, N, K, e, st, ws, slab);
+      int used = 1;
+      const hipError_t r =
+          launch_pp_plain(mk_amn(PlainMN<64>{}), mk_bmn(PlainMN<64>{}), M, N, K, e, st, ws, slab, &used);
       if (r != hipErrorNotSupported) {
         if (r != hipSuccess) return r;
         if (ws > 1) {
-          rowsum_cast_kernel<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(rs_scratch, db, db_bf16 ? 1 : 0, M);
+          rowsum_cast_kernel<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(rs_scratch, db, db_bf16 ? 1 : 0, M,
+                                                                          used);
           PDA_CHECK_HIP(hipGetLastError());
         }
         *db_done = 1;

@@ -42,7 +42,7 @@ struct Epi {
   // gradient (db folded into the dW GEMM).  mode 1: fp32 store, 2: bf16 store, 3: fp32
   // atomic add (split-K launches; the caller zeroes the buffer)
   void* rowsum;
-  int rowsum_mode;
+  int rowsum_mode;  // 1 fp32 store, 2 bf16 store, 3 fp32 atomic add, 4 fp32 store at [split][M]
 };
 
 // The pipelined 256 x 256 GEMM (gemm_pp.hip); gemm_conv.hip routes plain GEMMs to it.

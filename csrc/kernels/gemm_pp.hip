@@ -151,6 +151,10 @@ struct PPArgs {
   int tiles_n, kt_per_split;
   Epi epi;
   PPGather ga;
+  // MN-major operands: the descriptor base advances every 2^rb_shift K tiles, so the per-DMA offsets
+  // (t * 64 k-rows * ld) stay 32-bit on K spans of any length (the LM head's weight gradient: ld 50304,
+  // K = 32768 tokens is 3.3 GB of k-rows)
+  int rb_shift = 30;
 };
 
 __device__ __forceinline__ uint32_t pp_fdiv(uint32_t n, uint32_t mul, uint32_t shr) {
@@ -171,6 +175,7 @@ struct PPSrc {
   //   MN-major: column chunk in range iff lim > h * half stride; k-row t * 64 + kr (+32) < rows
   uint32_t v, dh, di, dk;
   int lim, rows;
+  int64_t rem;  // bytes from the descriptor base to the operand's end (uncapped)
 };
 
 __device__ __forceinline__ pp_i32x4 pp_rsrc_words(const bf16_t* base, int64_t bytes) {
@@ -197,6 +202,7 @@ __device__ __forceinline__ PPSrc pp_src(const PPOp& op, int64_t r0, int64_t k0, 
     s.r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(rem < 0x7fffffff ? rem : 0x7fffffff),
                                             0x00020000);
     s.rs = pp_rsrc_words(base, rem);
+    s.rem = rem;
     s.v = (uint32_t)((rr * op.ld + chunk * 8) * 2);
     s.dh = (uint32_t)((IS_A ? 64 : 32) * op.ld * 2);
     s.di = (uint32_t)(128 * op.ld * 2);
@@ -215,6 +221,7 @@ __device__ __forceinline__ PPSrc pp_src(const PPOp& op, int64_t r0, int64_t k0, 
     s.r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(rem < 0x7fffffff ? rem : 0x7fffffff),
                                             0x00020000);
     s.rs = pp_rsrc_words(base, rem);
+    s.rem = rem;
     s.v = (uint32_t)((kr * op.ld + rr) * 2);
     s.dh = (uint32_t)((IS_A ? 64 : 32) * 2);
     s.di = (uint32_t)(32 * op.ld * 2);
@@ -343,7 +350,20 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
       }
       return;
     }
-    const uint32_t su = __builtin_amdgcn_readfirstlane((hid & 1) * s.dh + (uint32_t)t * s.dk);
+    uint32_t su;
+    pp_i32x4 rs = s.rs;
+    if constexpr (!km) {
+      const uint32_t blk = (uint32_t)t >> p.rb_shift;  // uniform; 0 unless K spans past 2^31 bytes
+      su = __builtin_amdgcn_readfirstlane((hid & 1) * s.dh + ((uint32_t)t - (blk << p.rb_shift)) * s.dk);
+      const uint64_t adv = (uint64_t)blk * ((uint64_t)s.dk << p.rb_shift);
+      const uint64_t b = ((uint64_t)(uint32_t)rs[1] << 32 | (uint32_t)rs[0]) + adv;
+      rs[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+      rs[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
+      const int64_t left = s.rem - (int64_t)adv;
+      rs[2] = __builtin_amdgcn_readfirstlane(left <= 0 ? 0 : (int)(left < 0x7fffffff ? left : 0x7fffffff));
+    } else {
+      su = __builtin_amdgcn_readfirstlane((hid & 1) * s.dh + (uint32_t)t * s.dk);
+    }
     bool ok0, ok1;
     if constexpr (km) {
       constexpr int hr = (hid & 1) * (isA ? 64 : 32);
@@ -358,8 +378,8 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
     if constexpr (ASM_DMA) {
       const uint32_t l = __builtin_amdgcn_readfirstlane(
           (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)dst);
-      pp_glds_asm(s.rs, l, ok0 ? s.v : PP_OOB, su);
-      pp_glds_asm(s.rs, l + 8192, ok1 ? s.v : PP_OOB, su + s.di);
+      pp_glds_asm(rs, l, ok0 ? s.v : PP_OOB, su);
+      pp_glds_asm(rs, l + 8192, ok1 ? s.v : PP_OOB, su + s.di);
     } else {
       pp_glds(s.r, dst, ok0 ? s.v : PP_OOB, su);
       pp_glds(s.r, dst + 8192, ok1 ? s.v : PP_OOB, su + s.di);
@@ -454,7 +474,8 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
           const int64_t m = m0 + wr * 128 + qa * 64 + 16 * wc + (lane & 15);
           if (m >= p.M) continue;
           const float v = rsacc[qa];
-          if (p.epi.rowsum_mode == 3) unsafeAtomicAdd((float*)p.epi.rowsum + m, v);
+          if (p.epi.rowsum_mode == 4) ((float*)p.epi.rowsum)[(int64_t)blockIdx.y * p.M + m] = v;
+          else if (p.epi.rowsum_mode == 3) unsafeAtomicAdd((float*)p.epi.rowsum + m, v);
           else if (p.epi.rowsum_mode == 2) ((bf16_t*)p.epi.rowsum)[m] = f2bf(v);
           else ((float*)p.epi.rowsum)[m] = v;
         }
@@ -898,33 +919,73 @@ constexpr int P4_STATS_OFF = WT_STAGE_BYTES > P4_LOOP ? WT_STAGE_BYTES : P4_LOOP
 constexpr int P4_LDS = P4_STATS_OFF + 4 * 256 * 2 * 4;
 static_assert(P4_LDS <= 160 * 1024, "LDS budget");
 
-// K-major DMA source for the 4-wave tile: a 128-row half image is 4 rounds of 32 rows; lane l of wave w
-// fills image row R = round*32 + w*8 + l/8, physical chunk l & 7 = logical chunk (l & 7) ^ ((R >> 1) & 7).
+// DMA source of one operand for the 4-wave tile.  An operand stage is two [128]-row half images (rows
+// 0-127 / 128-255 of the tile); each half is 4 DMA rounds of 1 KB per wave.
+//   K-major ([128][64] image, gemm_pp's K-major half): round i, wave w, lane l fills image row
+//     R = i*32 + w*8 + l/8, physical chunk l & 7 = logical chunk (l & 7) ^ ((R >> 1) & 7).
+//   MN-major ([64 k][128] image, gemm_pp's MN-major half): round i fills k-rows i*16 + t/16 (t = thread),
+//     the 8 columns pp_mn_col(t) (the swizzle key only sees k bits 0, 1, 3: rounds of 16 keep it).
+// Every per-round / per-half / per-K-tile step is uniform (soffset); validity is explicit per lane.
 struct P4Src {
   __amdgpu_buffer_rsrc_t r;
-  uint32_t v, ld2;  // per-lane byte offset; row stride in bytes
-  int lim, rows;    // K left from the lane's chunk; rows left from the lane's round-0 row
+  pp_i32x4 rs;
+  uint32_t v, ld2;  // per-lane byte offset; row (K-major) or k-row (MN-major) stride in bytes
+  int lim, rows;    // K-major: K left from the lane's chunk, rows left from its round-0 row
+                    // MN-major: columns left from the lane's first column, k-rows left from its first
 };
 
+template <bool KM>
 __device__ __forceinline__ P4Src p4_src(const PPOp& op, int64_t r0, int64_t k0, int64_t K, int wid, int lane) {
   P4Src s;
-  const int chunk = (lane & 7) ^ ((wid * 4 + (lane >> 4)) & 7);
-  const int rr = wid * 8 + (lane >> 3);
-  const bf16_t* base = op.p + r0 * op.ld + k0;
-  const int64_t rem = (((op.rows - r0) - 1) * op.ld + (K - k0)) * 2;
+  const int tid = wid * 64 + lane;
+  const bf16_t* base;
+  int64_t rem;
+  if constexpr (KM) {
+    const int chunk = (lane & 7) ^ ((wid * 4 + (lane >> 4)) & 7);
+    const int rr = wid * 8 + (lane >> 3);
+    base = op.p + r0 * op.ld + k0;
+    rem = (((op.rows - r0) - 1) * op.ld + (K - k0)) * 2;
+    s.v = (uint32_t)((rr * op.ld + chunk * 8) * 2);
+    s.lim = (int)(K - k0) - chunk * 8;
+    const int64_t rl = op.rows - r0 - rr;
+    s.rows = rl > 0x7fffffff ? 0x7fffffff : (int)rl;
+  } else {
+    const int col = pp_mn_col(tid), kr = tid >> 4;
+    base = op.p + k0 * op.ld + r0;
+    rem = (((K - k0) - 1) * op.ld + (op.rows - r0)) * 2;
+    s.v = (uint32_t)((kr * op.ld + col) * 2);
+    const int64_t cl = op.rows - r0 - col;
+    s.lim = cl > 0x7fffffff ? 0x7fffffff : (int)cl;
+    const int64_t kl = (K - k0) - kr;
+    s.rows = kl > 0x7fffffff ? 0x7fffffff : (int)kl;
+  }
   s.r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)(rem < 0x7fffffff ? rem : 0x7fffffff),
                                           0x00020000);
-  s.v = (uint32_t)((rr * op.ld + chunk * 8) * 2);
+  s.rs = pp_rsrc_words(base, rem);
   s.ld2 = (uint32_t)(op.ld * 2);
-  s.lim = (int)(K - k0) - chunk * 8;
-  const int64_t rl = op.rows - r0 - rr;
-  s.rows = rl > 0x7fffffff ? 0x7fffffff : (int)rl;
   return s;
+}
+
+// DMA x (0..7: half x >> 2, round x & 3) of K tile t: uniform soffset and the lane's voffset / validity
+template <bool KM>
+__device__ __forceinline__ void p4_dma_args(const P4Src& s, int x, int t, int nk, uint32_t& su, uint32_t& vo) {
+  const int h = x >> 2, i = x & 3;
+  bool ok;
+  if constexpr (KM) {
+    const int row = h * 128 + i * 32;
+    su = (uint32_t)row * s.ld2 + (uint32_t)t * 128u;
+    ok = t < nk && t * 64 < s.lim && s.rows > row;
+  } else {
+    su = (uint32_t)h * 256u + (uint32_t)(i * 16) * s.ld2 + (uint32_t)(t * 64) * s.ld2;
+    ok = t < nk && s.lim > h * 128 && t * 64 + i * 16 < s.rows;
+  }
+  su = __builtin_amdgcn_readfirstlane(su);
+  vo = ok ? s.v : PP_OOB;
 }
 
 template <bool AK, bool BK>
 __global__ void __launch_bounds__(P4_NT) gemm_pp4_kernel(PPArgs p) {
-  static_assert(AK && BK, "4-wave tile: K-major operands");
+  constexpr bool ASM_DMA = !(AK && BK);  // see pp_glds_asm
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -940,34 +1001,42 @@ __global__ void __launch_bounds__(P4_NT) gemm_pp4_kernel(PPArgs p) {
   const int nk = min(ktiles, kt0 + p.kt_per_split) - kt0;
   const int64_t k0 = (int64_t)kt0 * 64;
 
-  const P4Src sa = p4_src(p.a, m0, k0, p.K, wid, lane);
-  const P4Src sb = p4_src(p.b, n0, k0, p.K, wid, lane);
+  const P4Src sa = p4_src<AK>(p.a, m0, k0, p.K, wid, lane);
+  const P4Src sb = p4_src<BK>(p.b, n0, k0, p.K, wid, lane);
 
-  // K tile t into stage (t & 1): 8 DMAs per operand and thread (2 halves x 4 rounds); tiles past the
-  // split and rows / K past the operand read zero
-  auto issue_op = [&](const P4Src& s, int hbase, int t, int stage) {
-    const bool kv = t < nk && t * 64 < s.lim;
-    char* dst = smem + stage * P4_STAGE + hbase * PP_HALF + wid * 1024;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = h * 128 + i * 32;
-        const uint32_t su = __builtin_amdgcn_readfirstlane((uint32_t)row * s.ld2 + (uint32_t)t * 128u);
-        pp_glds(s.r, dst + h * PP_HALF + i * 4096, kv && s.rows > row ? s.v : PP_OOB, su);
-      }
+  // DMA x (0..15: A halves / rounds, then B) of K tile t into stage (t & 1); tiles past the split and
+  // rows / columns / K past the operands read zero
+  auto dma = [&](int x, int t, int stage) {
+    const bool isA = x < 8;
+    uint32_t su, vo;
+    if (isA) p4_dma_args<AK>(sa, x & 7, t, nk, su, vo);
+    else p4_dma_args<BK>(sb, x & 7, t, nk, su, vo);
+    char* dst = smem + stage * P4_STAGE + ((isA ? 0 : 2) + ((x >> 2) & 1)) * PP_HALF + (x & 3) * 4096 + wid * 1024;
+    if constexpr (ASM_DMA) {
+      const uint32_t l = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)dst);
+      pp_glds_asm(isA ? sa.rs : sb.rs, l, vo, su);
+    } else {
+      pp_glds(isA ? sa.r : sb.r, dst, vo, su);
+    }
   };
   auto issue = [&](int t, int stage) {
-    issue_op(sa, 0, t, stage);
-    issue_op(sb, 2, t, stage);
+#pragma unroll
+    for (int x = 0; x < 16; ++x) dma(x, t, stage);
   };
 
   const int kl0 = pp_klane(lane, 0), kl1 = pp_klane(lane, 32);
   // fragment x of a k half in the order the MFMAs (row-major over acc) first use them: a0, b0..b7, a1..a7
-  auto rd1 = [&](const char* stg, int kl, int x, ppbf16x8 (&fa)[8], ppbf16x8 (&fb)[8]) {
-    if (x == 0) fa[0] = pp_kfrag(stg + wr * PP_HALF, 0, kl);
-    else if (x <= 8) fb[x - 1] = pp_kfrag(stg + (2 + wc) * PP_HALF, 16 * (x - 1), kl);
-    else fa[x - 8] = pp_kfrag(stg + wr * PP_HALF, 16 * (x - 8), kl);
+  auto frag = [&](auto km_c, const char* half, int g, int kk) {
+    if constexpr (decltype(km_c)::value) return pp_kfrag(half, 16 * g, kk ? kl1 : kl0);
+    else return pp_mfrag(half, g, kk * 32, lane);
+  };
+  auto rd1 = [&](const char* stg, int kk, int x, ppbf16x8 (&fa)[8], ppbf16x8 (&fb)[8]) {
+    const char* ha = stg + wr * PP_HALF;
+    const char* hb = stg + (2 + wc) * PP_HALF;
+    if (x == 0) fa[0] = frag(std::integral_constant<bool, AK>{}, ha, 0, kk);
+    else if (x <= 8) fb[x - 1] = frag(std::integral_constant<bool, BK>{}, hb, x - 1, kk);
+    else fa[x - 8] = frag(std::integral_constant<bool, AK>{}, ha, x - 8, kk);
   };
   f32x4 acc[8][8];
 #pragma unroll
@@ -988,7 +1057,7 @@ __global__ void __launch_bounds__(P4_NT) gemm_pp4_kernel(PPArgs p) {
   asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   pp_sync();
 #pragma unroll
-  for (int x = 0; x < 16; ++x) rd1(smem, kl0, x, fa0, fb0);
+  for (int x = 0; x < 16; ++x) rd1(smem, 0, x, fa0, fb0);
   auto ktile = [&](auto st_c, int t) {
     constexpr int ST = decltype(st_c)::value;
     const char* cur = smem + ST * P4_STAGE;
@@ -996,7 +1065,7 @@ __global__ void __launch_bounds__(P4_NT) gemm_pp4_kernel(PPArgs p) {
     // (1) k half 0 multiplies (64 MFMAs); k half 1's 16 fragments are read one per 4 MFMAs
 #pragma unroll
     for (int x = 0; x < 16; ++x) {
-      rd1(cur, kl1, x, fa1, fb1);
+      rd1(cur, 1, x, fa1, fb1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int y = 0; y < 4; ++y) mfma(x >> 1, (x & 1) * 4 + y, fa0, fb0);
@@ -1007,12 +1076,7 @@ __global__ void __launch_bounds__(P4_NT) gemm_pp4_kernel(PPArgs p) {
     // (2) stage t <- tile t+2 (16 DMAs, one per 2 MFMAs) under rows 0-3 of k half 1
 #pragma unroll
     for (int x = 0; x < 16; ++x) {
-      const P4Src& s = x < 8 ? sa : sb;
-      const int h = (x >> 2) & 1, i = x & 3, row = h * 128 + i * 32;
-      const bool kv = t + 2 < nk && (t + 2) * 64 < s.lim;
-      const uint32_t su = __builtin_amdgcn_readfirstlane((uint32_t)row * s.ld2 + (uint32_t)(t + 2) * 128u);
-      pp_glds(s.r, smem + ST * P4_STAGE + ((x < 8 ? 0 : 2) + h) * PP_HALF + i * 4096 + wid * 1024,
-              kv && s.rows > row ? s.v : PP_OOB, su);
+      dma(x, t + 2, ST);
       __builtin_amdgcn_sched_barrier(0);
       mfma(x >> 2, (x & 3) * 2, fa1, fb1);
       mfma(x >> 2, (x & 3) * 2 + 1, fa1, fb1);
@@ -1023,7 +1087,7 @@ __global__ void __launch_bounds__(P4_NT) gemm_pp4_kernel(PPArgs p) {
     // (3) k half 0 of tile t+1 read (one fragment per 2 MFMAs) under rows 4-7 of k half 1
 #pragma unroll
     for (int x = 0; x < 16; ++x) {
-      rd1(nxt, kl0, x, fa0, fb0);
+      rd1(nxt, 0, x, fa0, fb0);
       __builtin_amdgcn_sched_barrier(0);
       mfma(4 + (x >> 2), (x & 3) * 2, fa1, fb1);
       mfma(4 + (x >> 2), (x & 3) * 2 + 1, fa1, fb1);
@@ -1151,9 +1215,13 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
   const int ktiles = (int)((K + 63) / 64);
   if (splits < 1) splits = 1;
   int kps = (ktiles + splits - 1) / splits;
-  // an MN-major operand addresses one split's K span with 32-bit offsets
+  // an MN-major operand addresses 2^rb_shift K tiles from each descriptor base with 32-bit offsets
   const int64_t ld_mn = std::max(a_kmajor ? (int64_t)0 : lda, b_kmajor ? (int64_t)0 : ldb);
-  if (ld_mn > 0 && ((int64_t)kps * 64 + 64) * ld_mn * 2 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  int rb_shift = 30;
+  if (ld_mn > 0) {
+    while (rb_shift > 0 && (((int64_t)64 << rb_shift) + 128) * ld_mn * 2 >= ((int64_t)1 << 31)) --rb_shift;
+    if ((64 + 128) * ld_mn * 2 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
+  }
   splits = (ktiles + kps - 1) / kps;  // <= the requested count (the caller sized the slab for that)
   if (splits > 1 && !epi.slab) return hipErrorInvalidValue;
   // a K-major operand's 256-row panel must stay within 32-bit offsets
@@ -1165,9 +1233,15 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
     if (r != hipErrorInvalidValue) return r;
   }
   PPArgs a{{A, lda, M}, {B, ldb, N}, M, N, K, (int)((N + 255) / 256), kps, epi, {}};
+  a.rb_shift = rb_shift;
   if (splits <= 1) a.epi.slab = nullptr;
   const int var = variant < 0 ? pp_default_variant() : variant;
-  if (var == 200 && a_kmajor && b_kmajor && !epi.rowsum) return launch_pp4<true, true>(a, splits, st);
+  if (var == 200 && !epi.rowsum) {
+    if (a_kmajor && b_kmajor) return launch_pp4<true, true>(a, splits, st);
+    if (a_kmajor) return launch_pp4<true, false>(a, splits, st);
+    if (b_kmajor) return launch_pp4<false, true>(a, splits, st);
+    return launch_pp4<false, false>(a, splits, st);
+  }
   switch (var) {
     case 0: return launch_pp_var<0>(a_kmajor, b_kmajor, a, splits, st);
     case 1: return launch_pp_var<1>(a_kmajor, b_kmajor, a, splits, st);

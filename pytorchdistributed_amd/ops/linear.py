@@ -195,13 +195,12 @@ class _MlpGeluFn(torch.autograd.Function):
         N = w2.shape[0]
         dy2 = dy.reshape(-1, N).contiguous()
         M, F_ = h.shape
-        # fc2 data gradient fused with the GELU backward: dh = (dy W2) * gelu'(h), W2 read through its
-        # transpose (an 8 MB copy for GPT-2-medium) so both operands are K-major — the wide tile's fast
-        # layout (the in-place MN-major read of W2 costs the GEMM 15-25 %, profiles/r3_wide_ring_DROPPED.jsonl)
+        # fc2 data gradient fused with the GELU backward: dh = (dy W2) * gelu'(h), W2 read in place as the
+        # MN-major B operand (B(k, f) = W2[k * F + f]): the pipelined tile runs that layout at the K-major
+        # rate (profiles/r4_gpt2_gemm_shapes_pp.jsonl dgrad rows), so no per-step transposed copy
         dh = torch.empty_like(h)
         if M > 0:
-            w2t = w2.t().contiguous()
-            C().gemm_act(dy2, True, N, w2t, True, N, dh, F_, M, F_, N, None, 2, h)
+            C().gemm_act(dy2, True, N, w2, False, F_, dh, F_, M, F_, N, None, 2, h)
         dw2, db2 = _param_grads(dy2, g, pw2, pb2, ctx.needs_input_grad[3], pb2 is not None and ctx.needs_input_grad[4])
         dx = _gemm_dgrad(dh, w1).reshape(ctx.shape) if ctx.needs_input_grad[0] else None
         dw1, db1 = _param_grads(dh, x2, pw1, pb1, ctx.needs_input_grad[1], pb1 is not None and ctx.needs_input_grad[2])

@@ -22,6 +22,13 @@ for step in "$@"; do
     resnet_ab) run resnet_ab 900 bash tools/ab_env.sh "$out/resnet_ab.jsonl" 2 "PDA_GEMM_PP=1" "PDA_GEMM_PP=0" -- python -u bench.py --steps 20 --warmup 5 ;;
     gpt2_ab) run gpt2_ab 900 bash tools/ab_env.sh "$out/gpt2_ab.jsonl" 1 "PDA_MLP_FUSED=1" "PDA_MLP_FUSED=0" -- python -u -m pytorchdistributed_amd.bench.gpt2_ddp --steps 8 --warmup 3 ;;
     bench) run bench 600 python -u bench.py ;;
+    conv_table) run conv_table 600 python -u tools/bench_conv.py --batch 640 --iters 10 ;;
+    gpt2) run gpt2 300 python -u -m pytorchdistributed_amd.bench.gpt2_ddp --steps 8 --warmup 3 ;;
+    llama) run llama 400 python -u -m pytorchdistributed_amd.bench.llama_fsdp --steps 4 --warmup 2 ;;
+    lab4) run lab4 400 python -u tools/gemm_lab.py --variants 2,200 --layouts nt,nn,tn --shapes 4096x4096x4096,8192x8192x8192,32768x3072x1024,32768x1024x4096,16384x4096x4096,16384x28672x4096 ;;
+    gpt2_prof) export TMPDIR=/tmp; run gpt2_prof 600 rocprofv3 --kernel-trace --output-format csv -d "$out/gpt2_prof" -o run -- python -u -m pytorchdistributed_amd.bench.gpt2_ddp --steps 3 --warmup 2 ;;
+    llama_prof) export TMPDIR=/tmp; run llama_prof 600 rocprofv3 --kernel-trace --output-format csv -d "$out/llama_prof" -o run -- python -u -m pytorchdistributed_amd.bench.llama_fsdp --steps 2 --warmup 2 ;;
+    resnet_prof) export TMPDIR=/tmp; PDA_WGRAD_STREAM=0 run resnet_prof 600 rocprofv3 --kernel-trace --output-format csv -d "$out/resnet_prof" -o run -- python -u -m pytorchdistributed_amd.bench.resnet_ddp --steps 3 --warmup 3 ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     *) echo "[session] unknown step $step" ;;
   esac
