@@ -2190,6 +2190,16 @@ hipError_t launch_halo(const bf16_t* src, const bf16_t* B, int Nimg, int H, int 
   return launch_halo_bn<128>(src, B, Nimg, H, W, Cg, Nout, flip, epi, st);
 }
 
+// PDA_WGRAD_PP_MIN_COUT: smallest Cout whose gathered weight gradient takes the pipelined tile (0: off)
+int wgrad_pp_min_cout() {
+  static const int v = [] {
+    const char* e = getenv("PDA_WGRAD_PP_MIN_COUT");
+    const int x = e ? atoi(e) : 0;  // off by default until measured (the MN x MN gather tile spills)
+    return x <= 0 ? (1 << 30) : x;
+  }();
+  return v;
+}
+
 // 3x3 all-taps weight gradient (conv3x3_wgrad_kernel): stride 1, pad 1, dil 1, C and Cout multiples of
 // 64, W <= 64.  PDA_CONV_WG3=0 disables it.
 bool wg3_mode_on() {
@@ -2515,6 +2525,25 @@ hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32
     return hipGetLastError();
   }
   Plan p = plan_wgrad(M, Nn, K, slab != nullptr);
+  // gathered convs with >= 256 output channels (a full 256-row tile): the pipelined tile with the
+  // input gathered per k-row (gemm_pp.hip PPWg) instead of the 2-stage wide kernel's gather
+  if (slab && pp_conv_mode() && wgrad_pp_min_cout() <= Cout && !conv_1x1_plain(R, S, stride, pad, dil)) {
+    const int ws = wide_split_count(M, Nn, K);
+    Epi e = epi;
+    e.slab = slab;
+    int used = 1;
+    const hipError_t r = gemm_pp_wgrad(dy, x, N, H, W, C, Cout, R, S, P, Q, stride, pad, dil, e, ws, st, &used);
+    if (r == hipSuccess) {
+      if (used <= 1) return hipGetLastError();
+      int ll = 0;
+      while (ll < 4 && (used >> ll) > 16) ++ll;
+      const int64_t per_block = 256 >> ll;
+      const int64_t gr = (M * Nn / 4 + per_block - 1) / per_block;
+      splitk_reduce_kernel<<<(unsigned)gr, 256, 0, st>>>(slab, used, M, Nn, ll, epi);
+      return hipGetLastError();
+    }
+    if (r != hipErrorInvalidValue) return r;
+  }
   auto mk_a = [&](auto t) { t.p = dy; t.K = K; t.cols = M; t.ld = Cout; return t; };
   if (conv_1x1_plain(R, S, stride, pad, dil)) {  // dw[Cout, C] = dy[NHW, Cout]^T x[NHW, C]
     auto mk_bp = [&](auto t) { t.p = x; t.K = K; t.cols = Nn; t.ld = C; return t; };

@@ -50,6 +50,9 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
                    int64_t M, int64_t N, int64_t K, const Epi& epi, int splits, int variant, hipStream_t st,
                    int* used_splits);
 int pp_default_variant();
+hipError_t gemm_pp_wgrad(const bf16_t* dy, const bf16_t* x, int Nimg, int H, int W, int C, int Cout, int R, int S,
+                         int P, int Q, int stride, int pad, int dil, const Epi& epi, int splits, hipStream_t stream,
+                         int* used_splits);
 hipError_t gemm_pp_gather(const bf16_t* src, int Nimg, int H, int W, int C, int P, int Q, int S, int K, int st,
                           int o_r, int o_c, int tr, int ts, const bf16_t* w, int Cout, const Epi& epi, hipStream_t stream);
 

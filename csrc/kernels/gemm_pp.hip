@@ -145,12 +145,22 @@ struct PPGather {
   uint32_t mC, sC, mS, sS;  // k / C and rs / S as mul-hi + shift (fast_div)
 };
 
+// Operand B of a convolution's weight gradient as the gather of its input x [N, H, W, C]: element
+// (k = output pixel (n, p, q) of the [N, P, Q] grid, col = (r, s, c)) = x[n, p*st + r*dil - pad,
+// q*st + s*dil - pad, c], zero outside the image (gemm_conv.hip ConvWgradMN).  MN-major, so a lane's
+// 8 columns (one (r, s) tap, 8 channels) are fixed for the kernel and only its k-rows (pixels) move.
+struct PPWg {
+  int H, W, C, P, Q, st, pad, dil, S;
+  uint32_t mQ, sQ, mP, sP, mC, sC, mS, sS;
+};
+
 struct PPArgs {
   PPOp a, b;
   int64_t M, N, K;
   int tiles_n, kt_per_split;
   Epi epi;
   PPGather ga;
+  PPWg gb;
   // MN-major operands: the descriptor base advances every 2^rb_shift K tiles, so the per-DMA offsets
   // (t * 64 k-rows * ld) stay 32-bit on K spans of any length (the LM head's weight gradient: ld 50304,
   // K = 32768 tokens is 3.3 GB of k-rows)
@@ -159,6 +169,10 @@ struct PPArgs {
 
 __device__ __forceinline__ uint32_t pp_fdiv(uint32_t n, uint32_t mul, uint32_t shr) {
   return mul ? (__umulhi(n, mul) >> shr) : n;
+}
+// branch-free form for per-DMA use inside the K loop (mul == 0 encodes d == 1: the n term passes through)
+__device__ __forceinline__ uint32_t pp_fdiv_nb(uint32_t n, uint32_t mul, uint32_t shr) {
+  return (__umulhi(n, mul) + (n & (mul ? 0u : 0xFFFFFFFFu))) >> shr;
 }
 
 // Per-lane DMA source of one operand for this workgroup: a buffer descriptor over its panel (from the
@@ -269,8 +283,11 @@ __device__ __forceinline__ float pp_rs_tile(const ppbf16x8 (&a)[8], int wc) {  /
   return pp_rowsum_pair(f0, f1);
 }
 
-template <bool AK, bool BK, int VAR, bool RS = false, bool GA = false>
+template <bool AK, bool BK, int VAR, bool RS = false, int GM = 0>
 __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
+  constexpr bool GA = GM == 1;  // A = implicit-GEMM gather (PPGather)
+  constexpr bool GB = GM == 2;  // B = weight-gradient gather (PPWg)
+  static_assert(!GB || (!AK && !BK), "weight-gradient gather: MN-major operands");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -316,6 +333,13 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
                                             0x00020000);
   }
 
+  // GB: the lane's two column contexts (B half h: tile column (lc / 32) * 64 + h * 32 + lc % 32) — tap
+  // offsets packed in 16 bits each and channel (-1: column past N) — and its first k-row
+  // (no per-lane gather state is kept across the loop: the MN x MN tile has no registers to spare, so
+  // each issue recomputes its column's tap and channel — two multiply-high divisions)
+  pp_i32x4 gb_rs = sb.rs;
+  if constexpr (GB) gb_rs = pp_rsrc_words(p.b.p, p.b.rows * 2);  // b.rows carries x's element count
+
   // one half image of K tile t (of this split): 2 DMAs per thread; tiles past the split read zero
   // (t & 1) == SLOT at every call site: the slot offsets fold into immediates
   auto issue = [&](auto hid_c, auto slot_c, int t) {
@@ -347,6 +371,32 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
         } else {
           pp_glds(g_r, dst + i * 8192, off);
         }
+      }
+      return;
+    }
+    if constexpr (GB && !isA) {
+      // pixel k of each DMA's k-row (round i: +32), its tap-shifted source pixel; zero outside the image
+      const PPWg& g = p.gb;
+      const int lc = pp_mn_col((int)threadIdx.x);
+      const uint32_t col = (uint32_t)n0 + (uint32_t)((lc >> 5) * 64 + (hid & 1) * 32 + (lc & 31));
+      const uint32_t rs = pp_fdiv_nb(col, g.mC, g.sC);
+      const uint32_t r = pp_fdiv_nb(rs, g.mS, g.sS);
+      const uint32_t c = col - rs * (uint32_t)g.C;
+      const int dr = (int)r * g.dil - g.pad, ds = (int)(rs - r * (uint32_t)g.S) * g.dil - g.pad;
+      const bool cok = col < (uint32_t)p.N;
+      const uint32_t kbase = (uint32_t)k0 + (uint32_t)t * 64u + ((uint32_t)threadIdx.x >> 4);
+      const uint32_t kend = (uint32_t)p.K;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t kk = kbase + (uint32_t)(i * 32);
+        const uint32_t nq = pp_fdiv_nb(kk, g.mQ, g.sQ), q = kk - nq * (uint32_t)g.Q;
+        const uint32_t n = pp_fdiv_nb(nq, g.mP, g.sP), pp = nq - n * (uint32_t)g.P;
+        const int ih = (int)pp * g.st + dr, iw = (int)q * g.st + ds;
+        const bool ok = t < nk && kk < kend && cok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        const uint32_t off = ok ? (uint32_t)((((int)n * g.H + ih) * g.W + iw) * g.C + (int)c) * 2u : PP_OOB;
+        const uint32_t l = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(dst + i * 8192));
+        pp_glds_asm(gb_rs, l, off);
       }
       return;
     }
@@ -1119,16 +1169,16 @@ hipError_t launch_pp4(const PPArgs& a, int splits, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <bool AK, bool BK, int VAR, bool RS = false, bool GA = false>
+template <bool AK, bool BK, int VAR, bool RS = false, int GM = 0>
 hipError_t launch_pp_v(const PPArgs& a, int splits, hipStream_t st) {
   static bool attr = [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<AK, BK, VAR, RS, GA>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_pp_kernel<AK, BK, VAR, RS, GM>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, PP_LDS);
     return true;
   }();
   (void)attr;
   const int tiles = (int)((a.M + 255) / 256) * a.tiles_n;
-  gemm_pp_kernel<AK, BK, VAR, RS, GA><<<dim3(tiles, splits), PP_NT, PP_LDS, st>>>(a);
+  gemm_pp_kernel<AK, BK, VAR, RS, GM><<<dim3(tiles, splits), PP_NT, PP_LDS, st>>>(a);
   return hipGetLastError();
 }
 
@@ -1280,7 +1330,35 @@ hipError_t gemm_pp_gather(const bf16_t* src, int Nimg, int H, int W, int C, int 
   g.H = H; g.W = W; g.C = C; g.P = P; g.Q = Q; g.S = S; g.st = st; g.o_r = o_r; g.o_c = o_c; g.tr = tr; g.ts = ts;
   pp_magic((uint32_t)C, g.mC, g.sC);
   pp_magic((uint32_t)S, g.mS, g.sS);
-  return launch_pp_v<true, true, 2, false, true>(a, 1, stream);
+  return launch_pp_v<true, true, 2, false, 1>(a, 1, stream);
+}
+
+// Convolution weight gradient through the pipelined tile: dw[Cout, R*S*C] = dy[N*P*Q, Cout]^T gather(x)
+// (PPWg), both operands MN-major, split-K into `slab` ([splits][Cout][R*S*C] fp32, reduced by the
+// caller).  hipErrorInvalidValue when the shape does not fit (the caller keeps its other paths).
+hipError_t gemm_pp_wgrad(const bf16_t* dy, const bf16_t* x, int Nimg, int H, int W, int C, int Cout, int R, int S,
+                         int P, int Q, int stride, int pad, int dil, const Epi& epi, int splits, hipStream_t stream,
+                         int* used_splits) {
+  const int64_t K = (int64_t)Nimg * P * Q, Nn = (int64_t)R * S * C, xn = (int64_t)Nimg * H * W * C;
+  if (C % 8 || Cout % 8 || xn * 2 >= ((int64_t)1 << 31) || K >= ((int64_t)1 << 31) - 256) return hipErrorInvalidValue;
+  const int ktiles = (int)((K + 63) / 64);
+  if (splits < 1) splits = 1;
+  const int kps = (ktiles + splits - 1) / splits;
+  splits = (ktiles + kps - 1) / kps;
+  if (splits > 1 && !epi.slab) return hipErrorInvalidValue;
+  int rb_shift = 30;
+  while (rb_shift > 0 && (((int64_t)64 << rb_shift) + 128) * Cout * 2 >= ((int64_t)1 << 31)) --rb_shift;
+  PPArgs a{{dy, Cout, Cout}, {x, 0, xn}, Cout, Nn, K, (int)((Nn + 255) / 256), kps, epi, {}};
+  a.rb_shift = rb_shift;
+  if (splits <= 1) a.epi.slab = nullptr;
+  PPWg& g = a.gb;
+  g.H = H; g.W = W; g.C = C; g.P = P; g.Q = Q; g.st = stride; g.pad = pad; g.dil = dil; g.S = S;
+  pp_magic((uint32_t)Q, g.mQ, g.sQ);
+  pp_magic((uint32_t)P, g.mP, g.sP);
+  pp_magic((uint32_t)C, g.mC, g.sC);
+  pp_magic((uint32_t)S, g.mS, g.sS);
+  if (used_splits) *used_splits = splits;
+  return launch_pp_v<false, false, 2, false, 2>(a, splits, stream);
 }
 
 // Lab entry (tools/gemm_lab.py): C[M,N] = A B (+ bf16 bias), bf16 output, the given operand majorness.
