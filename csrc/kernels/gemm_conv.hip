@@ -2194,7 +2194,9 @@ hipError_t launch_halo(const bf16_t* src, const bf16_t* B, int Nimg, int H, int 
 int wgrad_pp_min_cout() {
   static const int v = [] {
     const char* e = getenv("PDA_WGRAD_PP_MIN_COUT");
-    const int x = e ? atoi(e) : 0;  // off by default until measured (the MN x MN gather tile spills)
+    // off by default: 1.4-1.9x slower than the wide kernel's gather on every shape (the MN x MN gather
+    // tile spills its LDS-read addresses inside the K loop; profiles/r4_wgrad_pp_gather_DROPPED.jsonl)
+    const int x = e ? atoi(e) : 0;
     return x <= 0 ? (1 << 30) : x;
   }();
   return v;
