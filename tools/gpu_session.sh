@@ -17,7 +17,7 @@ run() {  # name seconds cmd...
 for step in "$@"; do
   case $step in
     gemm_tests) run gemm_tests 300 python -u -m pytest tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "gemm or conv" ;;
-    gpu_tests) run gpu_tests 1500 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ;;
+    gpu_tests) run gpu_tests 1050 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread ;;
     lab) run lab 400 python -u tools/gemm_lab.py --variants 2,6,10,100 --layouts nt,tn --no-native --shapes 4096x4096x4096,8192x8192x8192,32768x3072x1024,32768x1024x4096,16384x4096x4096 ;;
     resnet_ab) run resnet_ab 900 bash tools/ab_env.sh "$out/resnet_ab.jsonl" 2 "PDA_GEMM_PP=1" "PDA_GEMM_PP=0" -- python -u bench.py --steps 20 --warmup 5 ;;
     gpt2_ab) run gpt2_ab 900 bash tools/ab_env.sh "$out/gpt2_ab.jsonl" 1 "PDA_MLP_FUSED=1" "PDA_MLP_FUSED=0" -- python -u -m pytorchdistributed_amd.bench.gpt2_ddp --steps 8 --warmup 3 ;;
