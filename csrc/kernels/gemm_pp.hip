@@ -1244,6 +1244,17 @@ hipError_t gemm_pp_persistent(const bf16_t* A, bool a_kmajor, int64_t lda, const
   return launch_ppp<false, false, false>(a, grid, st);
 }
 
+// PDA_PP_RB_SHIFT (tests): cap on the descriptor-rebase period of MN-major operands (2^s K tiles), so
+// small GEMMs exercise the rebase that only K spans past 2 GB need
+int pp_rb_shift_cap() {
+  static const int v = [] {
+    const char* e = getenv("PDA_PP_RB_SHIFT");
+    const int x = e ? atoi(e) : 30;
+    return x < 0 ? 0 : (x > 30 ? 30 : x);
+  }();
+  return v;
+}
+
 int pp_default_variant() {
   static const int v = [] {
     const char* e = getenv("PDA_PP_VAR");
@@ -1267,7 +1278,7 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
   int kps = (ktiles + splits - 1) / splits;
   // an MN-major operand addresses 2^rb_shift K tiles from each descriptor base with 32-bit offsets
   const int64_t ld_mn = std::max(a_kmajor ? (int64_t)0 : lda, b_kmajor ? (int64_t)0 : ldb);
-  int rb_shift = 30;
+  int rb_shift = pp_rb_shift_cap();
   if (ld_mn > 0) {
     while (rb_shift > 0 && (((int64_t)64 << rb_shift) + 128) * ld_mn * 2 >= ((int64_t)1 << 31)) --rb_shift;
     if ((64 + 128) * ld_mn * 2 >= ((int64_t)1 << 31)) return hipErrorInvalidValue;

@@ -775,6 +775,51 @@ def test_conv_wgrad_cu_budgets(env):
     assert r.returncode == 0 and "budget ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
+_PP_REBASE_SCRIPT = r"""
+import torch
+from pytorchdistributed_amd._native import C
+torch.manual_seed(5)
+dev = "cuda"
+def rel(a, b):
+    return ((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12)).item()
+# K = 40 K tiles (not a multiple of the 2-tile rebase period), every MN-major layout, split and unsplit
+for M, N, K in [(512, 520, 2560), (264, 256, 2600)]:
+    for lay in ("nn", "tn", "mn"):
+        ak, bk = lay == "nn", lay == "mn"
+        a = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16() if ak else (torch.rand(K, M, device=dev) * 2 - 1).bfloat16()
+        b = (torch.rand(N, K, device=dev) * 2 - 1).bfloat16() if bk else (torch.rand(K, N, device=dev) * 2 - 1).bfloat16()
+        ref = (a.float() if ak else a.float().t()) @ (b.float().t() if bk else b.float())
+        for split in (False, True):
+            o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)  # bf16 C: the pipelined tile's output
+            C().gemm(a, ak, K if ak else M, b, bk, K if bk else N, o, N, M, N, K, None, False, split)
+            assert rel(o, ref) < 5e-3, (M, N, K, lay, split, rel(o, ref))
+# the fused weight + bias gradient (row sums) across rebases
+dy = (torch.rand(2560, 512, device=dev) * 2 - 1).bfloat16()
+x = (torch.rand(2560, 768, device=dev) * 2 - 1).bfloat16()
+dw = torch.empty(512, 768, device=dev, dtype=torch.bfloat16)
+db = torch.empty(512, device=dev, dtype=torch.float32)
+done = C().gemm_wgrad_db(dy, x, dw, db)
+assert rel(dw, dy.float().t() @ x.float()) < 5e-3
+assert done and rel(db, dy.float().sum(0)) < 1e-5
+print("rebase ok")
+"""
+
+
+def test_gemm_pp_descriptor_rebase():
+    """MN-major operands re-base their buffer descriptor every 2^s K tiles so K spans past 2 GB (the LM-head
+    weight gradients) keep 32-bit offsets; PDA_PP_RB_SHIFT=1 (read once per process: a child) forces a
+    rebase every 2 K tiles on small GEMMs: every MN-major layout, split-K on and off, and the fused
+    weight + bias gradient, against fp32."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _PP_REBASE_SCRIPT], cwd=root, env={**os.environ, "PDA_PP_RB_SHIFT": "1"},
+                       capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and "rebase ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 @pytest.mark.parametrize("dual_bwd", [True, False])
 # (768, 384): C = 1536 has no register-table layout -> the guard (bn_dual_ok) takes the separate-BN path
 @pytest.mark.parametrize("inplanes,planes,stride", [(64, 64, 1), (256, 128, 2), (512, 256, 2), (1024, 512, 2),
