@@ -794,10 +794,10 @@ for M, N, K in [(512, 520, 2560), (264, 256, 2600)]:
             C().gemm(a, ak, K if ak else M, b, bk, K if bk else N, o, N, M, N, K, None, False, split)
             assert rel(o, ref) < 5e-3, (M, N, K, lay, split, rel(o, ref))
 # the fused weight + bias gradient (row sums) across rebases
-dy = (torch.rand(2560, 512, device=dev) * 2 - 1).bfloat16()
-x = (torch.rand(2560, 768, device=dev) * 2 - 1).bfloat16()
-dw = torch.empty(512, 768, device=dev, dtype=torch.bfloat16)
-db = torch.empty(512, device=dev, dtype=torch.float32)
+dy = (torch.rand(4096, 1024, device=dev) * 2 - 1).bfloat16()  # the shape test_gemm_wgrad_db_fused pins to the tile
+x = (torch.rand(4096, 1024, device=dev) * 2 - 1).bfloat16()
+dw = torch.empty(1024, 1024, device=dev, dtype=torch.bfloat16)
+db = torch.empty(1024, device=dev, dtype=torch.float32)
 done = C().gemm_wgrad_db(dy, x, dw, db)
 assert rel(dw, dy.float().t() @ x.float()) < 5e-3
 assert done and rel(db, dy.float().sum(0)) < 1e-5
