@@ -723,7 +723,9 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_persist_kernel(PPPArgs p) {
   const int wr = wid >> 2, wc = wid & 3;
   const bool lag = wr == 1;  // ping-pong stagger (variant 2 of the non-persistent kernel)
   constexpr bool EARLY = !AK;
-  constexpr bool ASM_DMA = !(AK && BK);
+  // inline-asm DMA for every layout: the unit's LDS slot is a runtime value here, so beside a visible
+  // LDS-DMA hipcc drains vmcnt(0) before every fragment read it cannot prove disjoint from the DMA
+  constexpr bool ASM_DMA = true;
   const int G = gridDim.x;
   const int slot_id = xcd_remap(blockIdx.x, G);
   const int my_tiles = slot_id < p.ntiles ? (p.ntiles - slot_id + G - 1) / G : 0;
@@ -781,28 +783,33 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_persist_kernel(PPPArgs p) {
     const int r0 = isA ? q.m0 : q.n0;
     const int64_t ld = isA ? p.a.ld : p.b.ld;
     const uint32_t lane_off = isA ? a_lane : b_lane;
-    uint32_t o0, o1;
-    bool ok;
+    const int rows = (int)(isA ? p.M : p.N);
+    const int rr = (isA ? a_rr : b_rr) + (hid & 1) * (isA ? 64 : 32);
+    // the tile origin, half and K tile are uniform (soffset); validity explicit per lane as gemm_pp_kernel
+    uint32_t su, s1;
+    bool ok0, ok1;
     if constexpr (km) {
-      const uint32_t ub = (uint32_t)(((int64_t)r0 * ld + (int64_t)kt * 64) * 2) + (hid & 1) * (uint32_t)((isA ? 64 : 32) * ld * 2);
-      o0 = ub + lane_off;
-      o1 = o0 + (uint32_t)(128 * ld * 2);
-      ok = live && kt * 64 < klim;
+      su = (uint32_t)(((int64_t)(r0 + (hid & 1) * (isA ? 64 : 32)) * ld + (int64_t)kt * 64) * 2);
+      s1 = su + (uint32_t)(128 * ld * 2);
+      const bool kv = live && kt * 64 < klim;
+      ok0 = kv && r0 + rr < rows;
+      ok1 = kv && r0 + rr + 128 < rows;
     } else {
-      const int rows = (int)(isA ? p.M : p.N);
-      const int rr = (isA ? a_rr : b_rr) + (hid & 1) * (isA ? 64 : 32);
-      const uint32_t ub = (uint32_t)(((int64_t)kt * 64 * ld + r0) * 2) + (hid & 1) * (uint32_t)((isA ? 64 : 32) * 2);
-      o0 = ub + lane_off;
-      o1 = o0 + (uint32_t)(32 * ld * 2);
-      ok = live && r0 + rr < rows;
+      su = (uint32_t)(((int64_t)kt * 64 * ld + r0 + (hid & 1) * (isA ? 64 : 32)) * 2);
+      s1 = su + (uint32_t)(32 * ld * 2);
+      const bool cv = live && r0 + rr < rows;
+      ok0 = cv && kt * 64 + (tid >> 4) < (int)K;
+      ok1 = cv && kt * 64 + (tid >> 4) + 32 < (int)K;
     }
+    su = __builtin_amdgcn_readfirstlane(su);
+    s1 = __builtin_amdgcn_readfirstlane(s1);
     if constexpr (ASM_DMA) {
       const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)dst);
-      pp_glds_asm(isA ? ras : rbs, l, ok ? o0 : PP_OOB);
-      pp_glds_asm(isA ? ras : rbs, l + 8192, ok ? o1 : PP_OOB);
+      pp_glds_asm(isA ? ras : rbs, l, ok0 ? lane_off : PP_OOB, su);
+      pp_glds_asm(isA ? ras : rbs, l + 8192, ok1 ? lane_off : PP_OOB, s1);
     } else {
-      pp_glds(isA ? ra : rb, dst, ok ? o0 : PP_OOB);
-      pp_glds(isA ? ra : rb, dst + 8192, ok ? o1 : PP_OOB);
+      pp_glds(isA ? ra : rb, dst, ok0 ? lane_off : PP_OOB, su);
+      pp_glds(isA ? ra : rb, dst + 8192, ok1 ? lane_off : PP_OOB, s1);
     }
   };
   using HA0 = std::integral_constant<int, H_A0>;
@@ -929,6 +936,10 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_persist_kernel(PPPArgs p) {
       rsacc[0] = rsacc[1] = 0.f;
     }
     wide_tile_epilogue_banded(acc, smem + PP_LDS_LOOP, p.epi, m0, n0, p.M, p.N, m0 / 256);
+    // retire the tile's C stores where hipcc can see it (vmcnt(0), once per tile): otherwise its wait
+    // for the store data registers merges into the unit loop's header and drains every unit's in-flight
+    // DMAs (vmcnt(0) before a fragment read, per unit)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
