@@ -43,6 +43,7 @@ struct Epi {
   // atomic add (split-K launches; the caller zeroes the buffer)
   void* rowsum;
   int rowsum_mode;  // 1 fp32 store, 2 bf16 store, 3 fp32 atomic add, 4 fp32 store at [split][M]
+  int nt_store;     // bf16 C rows written with nontemporal stores (streamed past the caches)
 };
 
 // The pipelined 256 x 256 GEMM (gemm_pp.hip); gemm_conv.hip routes plain GEMMs to it.
@@ -261,7 +262,9 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][16 / WC
         st2[q] = fmaf(d, d, st2[q]);
       }
     }
-    *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
+    u16x8* dst = reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n);
+    if (epi.nt_store) __builtin_nontemporal_store(v, dst);
+    else *dst = v;
   }
   if (want_stats) epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + stats_off), CPR, NT, tm, n0, N);
 }

@@ -1266,6 +1266,15 @@ int pp_rb_shift_cap() {
   return v;
 }
 
+// PDA_EPI_NT=1: the pipelined tile writes bf16 C with nontemporal stores (A/B knob)
+int pp_epi_nt() {
+  static const int v = [] {
+    const char* e = getenv("PDA_EPI_NT");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return v;
+}
+
 int pp_default_variant() {
   static const int v = [] {
     const char* e = getenv("PDA_PP_VAR");
@@ -1306,6 +1315,7 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
   }
   PPArgs a{{A, lda, M}, {B, ldb, N}, M, N, K, (int)((N + 255) / 256), kps, epi, {}};
   a.rb_shift = rb_shift;
+  a.epi.nt_store = pp_epi_nt();
   if (splits <= 1) a.epi.slab = nullptr;
   const int var = variant < 0 ? pp_default_variant() : variant;
   if (var == 200 && !epi.rowsum) {
@@ -1348,6 +1358,7 @@ hipError_t gemm_pp_gather(const bf16_t* src, int Nimg, int H, int W, int C, int 
     return hipErrorInvalidValue;
   PPArgs a{{src, 0, xn}, {w, K, Cout}, M, Cout, K, (int)((Cout + 255) / 256), (int)((K + 63) / 64), epi, {}};
   a.epi.slab = nullptr;
+  a.epi.nt_store = pp_epi_nt();
   PPGather& g = a.ga;
   g.H = H; g.W = W; g.C = C; g.P = P; g.Q = Q; g.S = S; g.st = st; g.o_r = o_r; g.o_c = o_c; g.tr = tr; g.ts = ts;
   pp_magic((uint32_t)C, g.mC, g.sC);
