@@ -87,6 +87,8 @@ class DistributedDataParallel(tnn.Module):
 
         params = [p for p in module.parameters() if p.requires_grad]
         self._params = params
+        if self.world > 1 and dist.is_initialized():
+            self._verify_model_across_ranks(params)
         self._bucket_caps = (int(bucket_cap_mb * 2 ** 20), int(first_bucket_mb * 2 ** 20))
         # bucket order: reverse registration until the first backward has shown the real gradient order,
         # then (PDA_DDP_REBUILD=1, default) the buckets are rebuilt once in that order (torch's Reducer
@@ -222,6 +224,28 @@ class DistributedDataParallel(tnn.Module):
     # ------------------------------------------------------------------ communication
     def _use_ring(self):
         return self.backend == "ring"
+
+    def _verify_model_across_ranks(self, params):
+        """torch DDP's construction-time check (the [1] all-gather and the small metadata
+        broadcasts behind `ddp_gpus.py:35`), as ONE all-gather of a 4-int64 signature — parameter count,
+        total elements, a CRC of the (shape, dtype) sequence and of the requires_grad layout — so a rank
+        whose model differs fails here with a clear error instead of hanging in a bucket all-reduce."""
+        import zlib
+
+        desc = ";".join(f"{tuple(p.shape)}:{p.dtype}" for p in params).encode()
+        full = ";".join(f"{tuple(p.shape)}:{int(p.requires_grad)}" for p in self.module.parameters()).encode()
+        dev = params[0].device if params and params[0].is_cuda and self.backend == "nccl" else torch.device("cpu")
+        sig = torch.tensor([len(params), sum(p.numel() for p in params), zlib.crc32(desc), zlib.crc32(full)],
+                           dtype=torch.int64, device=dev)
+        outs = [torch.empty_like(sig) for _ in range(self.world)]
+        dist.all_gather(outs, sig, group=self.process_group)
+        bad = [r for r, o in enumerate(outs) if not torch.equal(o, sig)]
+        if bad:
+            raise RuntimeError(
+                f"DistributedDataParallel: rank {self.rank}'s model (params={len(params)}, "
+                f"numel={int(sig[1])}) differs from rank(s) {bad} "
+                f"({[tuple(int(v) for v in outs[r][:2]) for r in bad]} as (params, numel)); every rank must "
+                "construct the same module")
 
     def _src0(self) -> int:
         """Global rank of the group's rank 0 (torch's broadcast takes a global source rank)."""

@@ -74,6 +74,28 @@ def ddp_mlp(rank, world, backend, outdir, steps, abort_first=False):
     pd.destroy_process_group()
 
 
+def ddp_mismatch_worker(rank, world, outdir):
+    """Rank 1 builds a different MLP: DDP construction must raise on every rank instead
+    of hanging in the first bucket all-reduce; the error names the other rank and its sizes."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.models.mlp import MnistMLP
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+
+    pd.init_process_group("gloo")
+    model = MnistMLP((16, 32, 24, 10) if rank == 0 else (16, 32, 28, 10))
+    try:
+        DistributedDataParallel(model)
+        raise AssertionError("mismatched models were accepted")
+    except RuntimeError as e:
+        msg = str(e)
+        assert "differs from rank(s) [" + str(1 - rank) + "]" in msg, msg
+    # matching models on every rank pass the same check
+    DistributedDataParallel(MnistMLP((16, 32, 24, 10)))
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+        f.write("ok")
+    pd.destroy_process_group()
+
+
 def reference_ddp_demo(rank, world, max_epochs, batch_size, outdir):
     """The reference's ddp_gpus.py main() (Linear(20,1), SGD, F.cross_entropy on float targets) on gloo."""
     import contextlib

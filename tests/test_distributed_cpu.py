@@ -62,6 +62,12 @@ def test_reference_ddp_demo_parity(tmp_path):
         assert d["loss"].abs().item() == 0.0
 
 
+def test_ddp_rejects_mismatched_models(tmp_path):
+    """DDP's construction-time cross-rank model check (torch semantics behind `ddp_gpus.py:35`)."""
+    spawn(_workers.ddp_mismatch_worker, args=(2, str(tmp_path)), nprocs=2, timeout=120)
+    assert (tmp_path / "ok0").exists() and (tmp_path / "ok1").exists()
+
+
 def test_spawn_propagates_child_exception():
     with pytest.raises(ProcessRaisedException) as ei:
         spawn(_workers.failing_worker, args=(2,), nprocs=2, timeout=60)
