@@ -165,6 +165,7 @@ struct PPArgs {
   // (t * 64 k-rows * ld) stay 32-bit on K spans of any length (the LM head's weight gradient: ld 50304,
   // K = 32768 tokens is 3.3 GB of k-rows)
   int rb_shift = 30;
+  int group_m = 8;  // grouped tile order: tile rows per group (PDA_PP_GROUP, A/B knob)
 };
 
 __device__ __forceinline__ uint32_t pp_fdiv(uint32_t n, uint32_t mul, uint32_t shr) {
@@ -300,7 +301,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   const int ntiles = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, ntiles);
   int tm, tn;
-  grouped_tile(tile, ntiles / p.tiles_n, p.tiles_n, 8, tm, tn);
+  grouped_tile(tile, ntiles / p.tiles_n, p.tiles_n, p.group_m, tm, tn);
   const int64_t m0 = (int64_t)tm * 256, n0 = (int64_t)tn * 256;
   const int ktiles = (int)((p.K + 63) >> 6);
   const int kt0 = blockIdx.y * p.kt_per_split;
@@ -1275,6 +1276,15 @@ int pp_epi_nt() {
   return v;
 }
 
+int pp_group_m() {
+  static const int v = [] {
+    const char* e = getenv("PDA_PP_GROUP");
+    const int x = e ? atoi(e) : 8;
+    return x < 1 ? 1 : x;
+  }();
+  return v;
+}
+
 int pp_default_variant() {
   static const int v = [] {
     const char* e = getenv("PDA_PP_VAR");
@@ -1315,6 +1325,7 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
   }
   PPArgs a{{A, lda, M}, {B, ldb, N}, M, N, K, (int)((N + 255) / 256), kps, epi, {}};
   a.rb_shift = rb_shift;
+  a.group_m = pp_group_m();
   a.epi.nt_store = pp_epi_nt();
   if (splits <= 1) a.epi.slab = nullptr;
   const int var = variant < 0 ? pp_default_variant() : variant;
