@@ -16,7 +16,7 @@ from ..data.device import DeviceSyntheticTokens
 from ..models.gpt2 import GPT2Stage, config
 from ..optim import AdamW
 from ..parallel.ddp import DistributedDataParallel
-from ..parallel.pipeline import Pipeline, dp_sync_grads, partition_layers, pp_dp_groups
+from ..parallel.pipeline import Pipeline, partition_layers, pp_dp_groups
 from ..utils.tunable import use_tuned_gemms
 from .common import emit, setup, teardown, timed
 
@@ -53,9 +53,14 @@ def main(argv=None):
         chunks = [GPT2Stage(cfg, *parts[c * pp + stage], c * pp + stage == 0, c * pp + stage == pp * v - 1,
                             device=device, dtype=torch.bfloat16) for c in range(v)]
         mod = torch.nn.ModuleList(chunks)
+        # the chunks' DP gradient average: one DDP over the DP group whose buckets launch in the backward
+        # of each chunk's last micro-batch (multi-pass buckets; no blocking post-flush all-reduce)
+        ddp = DistributedDataParallel(mod, device_ids=[device.index] if device.type == "cuda" else None,
+                                      process_group=dp_group)
+        ddp.track_comm = True
         pipe = Pipeline(chunks, ranks, a.micro, schedule="interleaved",
-                        loss_fn=chunks[-1].loss if stage == pp - 1 else None, group=pp_group, device=device)
-        ddp = None
+                        loss_fn=chunks[-1].loss if stage == pp - 1 else None, group=pp_group, device=device,
+                        dp_module=ddp)
     else:
         lo, hi = partition_layers(cfg.n_layer, pp)[stage]
         mod = GPT2Stage(cfg, lo, hi, stage == 0, stage == pp - 1, device=device, dtype=torch.bfloat16)
@@ -73,12 +78,10 @@ def main(argv=None):
         x, y = data.next()
         opt.zero_grad(set_to_none=True)
         pipe.step(x, y)
-        if ddp is None:
-            dp_sync_grads(mod, dp_group)
         opt.step()
 
     secs = timed(step, a.steps, a.warmup)
-    comm = ddp.comm_stats() if ddp is not None else {}
+    comm = ddp.comm_stats()
     toks = a.micro * a.micro_batch * a.seq * dp * a.steps / secs
     emit({"metric": "tokens/sec (whole job) GPT-2-XL pipeline x DDP", "value": round(toks, 1),
           "unit": "tokens/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,

@@ -21,8 +21,7 @@ neighbours never wait on each other's opposite-direction transfer (the classic b
 (e.g. 4 stages x 2 replicas: PP {0-3},{4-7}; DP {0,4},{1,5},{2,6},{3,7}).  The DP gradient average
 runs through the stage's :class:`~.ddp.DistributedDataParallel` over the DP group (``dp_module``):
 bucketed, launched during the last micro-batch's backward (interleaved: each chunk's last), overlapped
-with it and with the drain.  :func:`dp_sync_grads` (blocking, after the flush) is kept for modules
-without a DDP wrapper.
+with it and with the drain (there is no blocking post-flush gradient all-reduce).
 """
 from __future__ import annotations
 
@@ -173,42 +172,6 @@ def pp_dp_groups(pp: int, dp: int):
         if rank in ranks:
             dp_group = g
     return pp_group, dp_group, rank % pp, rank // pp, my_pp_ranks
-
-
-@torch.no_grad()
-def dp_sync_grads(module: tnn.Module, group, bucket_mb: float = 64.0):
-    """Average ``module``'s gradients over ``group`` with coalesced all-reduces (one per bucket)."""
-    if group is None or dist.get_world_size(group) == 1:
-        return
-    grads = [p.grad for p in module.parameters() if p.grad is not None]
-    if not grads:
-        return
-    nccl = dist.get_backend(group) == "nccl"
-    cap = int(bucket_mb * 2 ** 20)
-    bucket: List[torch.Tensor] = []
-    size = 0
-
-    def flush():
-        if not bucket:
-            return
-        flat = torch.cat([g.reshape(-1) for g in bucket])
-        if nccl:
-            dist.all_reduce(flat, op=dist.ReduceOp.AVG, group=group)
-        else:
-            dist.all_reduce(flat, group=group)
-            flat.div_(dist.get_world_size(group))
-        off = 0
-        for g in bucket:
-            g.copy_(flat[off: off + g.numel()].view_as(g))
-            off += g.numel()
-
-    for g in grads:
-        if size + g.numel() * g.element_size() > cap and bucket:
-            flush()
-            bucket, size = [], 0
-        bucket.append(g)
-        size += g.numel() * g.element_size()
-    flush()
 
 
 # ------------------------------------------------------------------ the pipeline engine

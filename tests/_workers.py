@@ -143,13 +143,15 @@ def _tiny_stack(n_layers=4, d=16, seed=0):
     return nn.Sequential(*layers)
 
 
-def pipeline_worker(rank, world, pp, dp, schedule, recompute, outdir, dp_mode="sync"):
+def pipeline_worker(rank, world, pp, dp, schedule, recompute, outdir, dp_mode="none"):
     """PP x DP on gloo: stage grads after one pipeline step must equal the single-process grads.
-    ``dp_mode``: "sync" = dp_sync_grads after the flush; "ddp" = the stage wrapped in DDP over its DP group
+    ``dp_mode``: "none" = no DP average (dp == 1 only); "ddp" = the stage wrapped in DDP over its DP group
     (buckets launched during the last micro-batch's backward)."""
     import pytorchdistributed_amd.distributed as pd
     from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
-    from pytorchdistributed_amd.parallel.pipeline import Pipeline, dp_sync_grads, partition_layers, pp_dp_groups
+    from pytorchdistributed_amd.parallel.pipeline import Pipeline, partition_layers, pp_dp_groups
+
+    assert dp_mode == "ddp" or dp == 1, "DP > 1 averages through the stage's DDP"
 
     pd.init_process_group("gloo")
     pp_group, dp_group, stage, dp_rank, ranks = pp_dp_groups(pp, dp)
@@ -169,9 +171,7 @@ def pipeline_worker(rank, world, pp, dp, schedule, recompute, outdir, dp_mode="s
                     loss_fn=F.mse_loss, recompute=recompute, device=torch.device("cpu"), dp_module=ddp)
     loss = pipe.step(xs, ys)
     stats = None
-    if ddp is None:
-        dp_sync_grads(stage_mod, dp_group)
-    else:
+    if ddp is not None:
         stats = ddp.comm_stats()
         assert stats["comm_calls"] == ddp.reducer.num_buckets or stats["comm_calls"] > 0, stats
     torch.save({"grads": {n: p.grad.clone() for n, p in stage_mod.named_parameters()}, "lo": lo,

@@ -49,8 +49,8 @@ def _reference_grads(dp):
 
 
 @pytest.mark.parametrize("pp,dp,schedule,recompute,dp_mode", [
-    (2, 1, "gpipe", False, "sync"), (2, 1, "1f1b", False, "sync"), (4, 1, "1f1b", True, "sync"),
-    (2, 2, "1f1b", False, "sync"), (2, 2, "1f1b", False, "ddp"), (2, 2, "gpipe", True, "ddp")])
+    (2, 1, "gpipe", False, "none"), (2, 1, "1f1b", False, "none"), (4, 1, "1f1b", True, "none"),
+    (2, 2, "1f1b", True, "ddp"), (2, 2, "1f1b", False, "ddp"), (2, 2, "gpipe", True, "ddp")])
 def test_pipeline_grads_match_single_process(tmp_path, pp, dp, schedule, recompute, dp_mode):
     """``dp_mode="ddp"``: the DP average runs through the stage's DDP over its DP group, launched during
     the last micro-batch's backward (no_sync before), reporting the exposed communication time."""
@@ -127,7 +127,7 @@ def test_interleaved_pipeline_grads_match_single_process(tmp_path, world, chunks
 
 def test_interleaved_pipeline_ddp_grads_match_single_process(tmp_path):
     """Interleaved schedule x DDP: 2 stages x 2 chunks x 2 DP replicas on gloo; the DP
-    average runs through each rank's DDP wrapper (multi-pass buckets), no dp_sync_grads."""
+    average runs through each rank's DDP wrapper (multi-pass buckets)."""
     pp, dp, chunks, n_layers, n_micro = 2, 2, 2, 8, 4
     spawn(_workers.pipeline_interleaved_ddp_worker, args=(pp * dp, pp, dp, chunks, n_layers, n_micro, str(tmp_path)),
           nprocs=pp * dp, timeout=180)
