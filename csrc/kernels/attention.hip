@@ -1214,11 +1214,24 @@ hipError_t attention_bwd(const AttnParams& p, hipStream_t st) {
       if (db & 2) attn_bwd_dkdv2_kernel<128, 1, true><<<gk, NT, 0, st>>>(p);
       else attn_bwd_dkdv2_kernel<128, 1><<<gk, NT, 0, st>>>(p);
     } else {
-      if (db & 1) attn_bwd_dq2_kernel<64, 2, true><<<gq2, NT, 0, st>>>(p);
-      else attn_bwd_dq2_kernel<64, 2><<<gq2, NT, 0, st>>>(p);
-      const dim3 gk((p.T + 2 * BKV - 1) / (2 * BKV), p.Hq, p.B);
-      if (db & 2) attn_bwd_dkdv2_kernel<64, 2, true><<<gk, NT, 0, st>>>(p);
-      else attn_bwd_dkdv2_kernel<64, 2><<<gk, NT, 0, st>>>(p);
+      // PDA_ATTN_BWD_G64=1: one query / key group per wave at D = 64 (140 / 159 VGPRs: 3 waves per SIMD
+      // instead of 2, half the fragment reuse) — GPT-2-medium 323.3-324.6k vs 323.1-323.6k tok/s, a tie
+      // (profiles/r4_attn_bwd_g64_ab.jsonl); A/B knob
+      static const int g1 = [] {
+        const char* e = getenv("PDA_ATTN_BWD_G64");
+        return e && e[0] == '1' ? 1 : 0;
+      }();
+      if (g1) {
+        attn_bwd_dq2_kernel<64, 1><<<gq, NT, 0, st>>>(p);
+        const dim3 gk1((p.T + BKV - 1) / BKV, p.Hq, p.B);
+        attn_bwd_dkdv2_kernel<64, 1><<<gk1, NT, 0, st>>>(p);
+      } else {
+        if (db & 1) attn_bwd_dq2_kernel<64, 2, true><<<gq2, NT, 0, st>>>(p);
+        else attn_bwd_dq2_kernel<64, 2><<<gq2, NT, 0, st>>>(p);
+        const dim3 gk((p.T + 2 * BKV - 1) / (2 * BKV), p.Hq, p.B);
+        if (db & 2) attn_bwd_dkdv2_kernel<64, 2, true><<<gk, NT, 0, st>>>(p);
+        else attn_bwd_dkdv2_kernel<64, 2><<<gk, NT, 0, st>>>(p);
+      }
     }
     PDA_CHECK_HIP(hipGetLastError());
     if (p.Hq > p.Hkv) {
