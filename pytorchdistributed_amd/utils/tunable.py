@@ -1,12 +1,12 @@
-"""Per-shape selection of the vendor library GEMM solutions (PyTorch TunableOp over hipBLASLt/rocBLAS).
+"""Per-shape selection of vendor-library GEMM solutions (PyTorch TunableOp over hipBLASLt/rocBLAS).
 
-Plain linear GEMMs of the transformer models go to hipBLASLt through ``torch.mm`` (ops/linear.py).
-The library's default heuristic pick is weak on some training shapes — e.g. the GPT-2-medium weight
-gradient 1024 x 1024 x 16384 runs at ~350 TFLOP/s with it — so each model's GEMM shapes were timed
-over all candidate solutions once on an MI355X and the winners are committed under
-``pytorchdistributed_amd/tuning/tunableop_<model>.csv``; a run only reads that table (no tuning).
+Since round 4 no framework GEMM goes to the vendor library: every bf16 Linear / conv GEMM runs on the
+native kernels (ops/linear.py, csrc/kernels/gemm_pp.hip), so this only matters for PyTorch ops a user
+script calls directly (``torch.mm`` / ``F.linear`` on GPU tensors).  The tables tuned on MI355X for the
+transformer configs while their Linears still used hipBLASLt stay under
+``pytorchdistributed_amd/tuning/tunableop_<model>.csv``; a run only reads a table (no tuning).
 
-``PDA_TUNABLEOP``: ``1`` (default) use the table when it exists, ``0`` off, ``tune`` re-tune and write
+``PDA_TUNABLEOP``: ``0`` (default) off, ``1`` use the table when it exists, ``tune`` re-tune and write
 ``PDA_TUNABLEOP_OUT`` (torch appends the device ordinal to the file name).
 """
 from __future__ import annotations
@@ -20,7 +20,7 @@ TABLE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file_
 
 def use_tuned_gemms(tag: str) -> str:
     """Enable TunableOp for this process with the committed table of ``tag``; returns the mode used."""
-    mode = os.environ.get("PDA_TUNABLEOP", "1")
+    mode = os.environ.get("PDA_TUNABLEOP", "0")
     if mode == "0" or not torch.cuda.is_available():
         return "off"
     from torch.cuda import tunable
