@@ -22,6 +22,8 @@
 
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
+#include <thread>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -40,6 +42,12 @@ namespace {
 void check_nccl(ncclResult_t r, const char* what) {
   if (r != ncclSuccess && r != ncclInProgress)
     throw std::runtime_error(std::string("RCCL ") + what + " failed: " + ncclGetErrorString(r));
+}
+
+bool comm_nonblocking() {
+  // PDA_COMM_NONBLOCKING=0: the blocking communicator (ncclCommInitRank) as before round 5
+  const char* v = std::getenv("PDA_COMM_NONBLOCKING");
+  return !(v && v[0] == '0');
 }
 
 void check_hip(hipError_t e, const char* what) {
@@ -177,9 +185,43 @@ class Communicator {
     check_hip(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, high_priority ? hi : lo),
               "hipStreamCreateWithPriority");
     check_hip(hipEventCreateWithFlags(&dep_, hipEventDisableTiming), "hipEventCreate");
-    check_nccl(ncclCommInitRank(&comm_, nranks, id, rank), "ncclCommInitRank");
-    std::lock_guard<std::mutex> l(g_live_mu);
-    g_live.insert(this);
+    nonblocking_ = comm_nonblocking();
+    if (!nonblocking_) {
+      check_nccl(ncclCommInitRank(&comm_, nranks, id, rank), "ncclCommInitRank");
+      inited_.store(true);
+      std::lock_guard<std::mutex> l(g_live_mu);
+      g_live.insert(this);
+      return;
+    }
+    // Non-blocking init (ncclConfig_t.blocking = 0): the communicator is visible to the abort hook
+    // BEFORE it has connected, and this thread polls its state instead of blocking inside RCCL, so a
+    // peer that never joins ends in a watchdog abort that releases the init
+    // instead of a SIGABRT while stuck in ncclCommInitRank.
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    check_nccl(ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg), "ncclCommInitRankConfig");
+    {
+      std::lock_guard<std::mutex> l(g_live_mu);
+      g_live.insert(this);
+    }
+    ncclResult_t st = ncclInProgress;
+    while (true) {
+      if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) st = ncclInternalError;
+      if (st != ncclInProgress || aborted_.load()) break;
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    if (st == ncclSuccess && !aborted_.load()) {
+      inited_.store(true);
+      if (!aborted_.load()) return;  // abort() raced in after the check: release the comm below
+    }
+    do_abort();
+    {
+      std::lock_guard<std::mutex> l(g_live_mu);
+      g_live.erase(this);
+    }
+    (void)hipEventDestroy(dep_);
+    throw std::runtime_error(std::string("RCCL communicator init ") +
+                             (aborted_.load() ? "aborted" : std::string("failed: ") + ncclGetErrorString(st)));
   }
 
   ~Communicator() {
@@ -188,10 +230,7 @@ class Communicator {
       g_live.erase(this);
     }
     DeviceGuard g(device_);
-    if (comm_ && !aborted_.load()) {  // an aborted comm was released by ncclCommAbort
-      (void)hipStreamSynchronize(stream_);
-      (void)ncclCommDestroy(comm_);
-    }
+    release();
     if (dep_) (void)hipEventDestroy(dep_);
     // stream_ is deliberately NOT destroyed: tensors the collectives used were record_stream()-ed on it
     // (comm.py _hold), and the caching allocator records an event on that stream when such a tensor
@@ -200,17 +239,36 @@ class Communicator {
     // communicator ever created is the price.
   }
 
+  // explicit teardown (destroy_process_group): drain the stream, then ncclCommDestroy,
+  // while the peers and the store still exist; later calls on this communicator raise
+  void close() {
+    {
+      std::lock_guard<std::mutex> l(g_live_mu);
+      g_live.erase(this);
+    }
+    DeviceGuard g(device_);
+    release();
+  }
+
   int rank() const { return rank_; }
   int size() const { return nranks_; }
   int device() const { return device_; }
   uintptr_t stream() const { return reinterpret_cast<uintptr_t>(stream_); }
   bool aborted() const { return aborted_.load(); }
+  bool closed() const { return closed_.load(); }
+  bool nonblocking() const { return nonblocking_; }
 
   // the comm stream waits for everything queued so far on `s` (the producers of the next input)
   void wait_stream(uintptr_t s) {
     DeviceGuard g(device_);
     check_hip(hipEventRecord(dep_, reinterpret_cast<hipStream_t>(s)), "hipEventRecord");
     check_hip(hipStreamWaitEvent(stream_, dep_, 0), "hipStreamWaitEvent");
+  }
+
+  // the comm stream waits for a recorded event (cross-communicator ordering, comm.py:_order)
+  void wait_event(uintptr_t ev) {
+    DeviceGuard g(device_);
+    check_hip(hipStreamWaitEvent(stream_, reinterpret_cast<hipEvent_t>(ev), 0), "hipStreamWaitEvent");
   }
 
   std::shared_ptr<Work> all_reduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op) {
@@ -220,6 +278,7 @@ class Communicator {
     check_nccl(ncclAllReduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), (size_t)count,
                              to_nccl_dtype(dtype), to_nccl_op(op), comm_, stream_),
                "ncclAllReduce");
+    settle("ncclAllReduce");
     return done();
   }
 
@@ -231,6 +290,7 @@ class Communicator {
     check_nccl(ncclReduceScatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv),
                                  (size_t)recvcount, to_nccl_dtype(dtype), to_nccl_op(op), comm_, stream_),
                "ncclReduceScatter");
+    settle("ncclReduceScatter");
     return done();
   }
 
@@ -242,6 +302,7 @@ class Communicator {
     check_nccl(ncclAllGather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), (size_t)sendcount,
                              to_nccl_dtype(dtype), comm_, stream_),
                "ncclAllGather");
+    settle("ncclAllGather");
     return done();
   }
 
@@ -252,6 +313,7 @@ class Communicator {
     check_nccl(ncclBroadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), (size_t)count,
                              to_nccl_dtype(dtype), root, comm_, stream_),
                "ncclBroadcast");
+    settle("ncclBroadcast");
     return done();
   }
 
@@ -262,6 +324,7 @@ class Communicator {
     DeviceGuard g(device_);
     check_nccl(ncclSend(reinterpret_cast<const void*>(buf), (size_t)count, to_nccl_dtype(dtype), peer, comm_, stream_),
                "ncclSend");
+    if (!group_depth_) settle("ncclSend");
     return group_depth_ ? nullptr : done();
   }
 
@@ -271,10 +334,12 @@ class Communicator {
     DeviceGuard g(device_);
     check_nccl(ncclRecv(reinterpret_cast<void*>(buf), (size_t)count, to_nccl_dtype(dtype), peer, comm_, stream_),
                "ncclRecv");
+    if (!group_depth_) settle("ncclRecv");
     return group_depth_ ? nullptr : done();
   }
 
   void group_start() {
+    live();
     check_nccl(ncclGroupStart(), "ncclGroupStart");
     ++group_depth_;
   }
@@ -282,10 +347,14 @@ class Communicator {
   std::shared_ptr<Work> group_end() {
     if (group_depth_ == 0) throw std::runtime_error("communicator: group_end without group_start");
     std::lock_guard<std::timed_mutex> l(op_mu_);
-    live();
     DeviceGuard g(device_);
-    check_nccl(ncclGroupEnd(), "ncclGroupEnd");
+    // RCCL group state is thread-local: close the group even after an abort (ignoring its result),
+    // or every later NCCL call of this thread — c10d's included — would be deferred into it and hang
+    const ncclResult_t r = ncclGroupEnd();
     --group_depth_;
+    live();
+    check_nccl(r, "ncclGroupEnd");
+    if (!group_depth_) settle("ncclGroupEnd");
     return group_depth_ ? nullptr : done();
   }
 
@@ -293,13 +362,13 @@ class Communicator {
   // its own thread).  The flag is atomic and set first, so no enqueue starts after it; an enqueue
   // already past its check holds op_mu_, which abort waits for (bounded: an enqueue blocked inside
   // RCCL, e.g. on a peer that never connects, is exactly what ncclCommAbort must release).  comm_
-  // itself never changes after construction, so no thread ever reads a nulled handle.
+  // itself never changes after construction, so no thread ever reads a nulled handle.  During a
+  // non-blocking init only the flag is set: the initialising thread sees it and aborts the comm itself
+  // (no second thread touches a half-built communicator).
   void abort() {
-    bool expected = false;
-    if (!comm_ || !aborted_.compare_exchange_strong(expected, true)) return;
-    std::unique_lock<std::timed_mutex> l(op_mu_, std::defer_lock);
-    (void)l.try_lock_for(std::chrono::seconds(2));
-    (void)ncclCommAbort(comm_);
+    aborted_.store(true);
+    if (!inited_.load()) return;
+    do_abort();
   }
 
   std::string async_error() {
@@ -325,6 +394,51 @@ class Communicator {
  private:
   void live() const {
     if (aborted_.load()) throw std::runtime_error("communicator was aborted (collective timeout / abort())");
+    if (closed_.load()) throw std::runtime_error("communicator was closed (destroy_process_group)");
+  }
+
+  void do_abort() {
+    bool expected = false;
+    if (!comm_ || !abort_done_.compare_exchange_strong(expected, true)) return;
+    std::unique_lock<std::timed_mutex> l(op_mu_, std::defer_lock);
+    (void)l.try_lock_for(std::chrono::seconds(2));
+    (void)ncclCommAbort(comm_);
+  }
+
+  // non-blocking communicator: an enqueue may return ncclInProgress; RCCL needs the state to reach
+  // ncclSuccess before the next call on the comm (polled; an abort ends the wait)
+  void settle(const char* what) {
+    if (!nonblocking_) return;
+    ncclResult_t st = ncclInProgress;
+    while (true) {
+      if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) st = ncclInternalError;
+      if (st != ncclInProgress) break;
+      if (aborted_.load()) throw std::runtime_error(std::string(what) + ": communicator aborted");
+      std::this_thread::yield();
+    }
+    check_nccl(st, what);
+  }
+
+  // ncclCommDestroy once (close() or the destructor); an aborted comm was released by ncclCommAbort
+  void release() {
+    bool expected = false;
+    if (!comm_ || !closed_.compare_exchange_strong(expected, true)) return;
+    if (aborted_.load() || !inited_.load()) return;
+    std::lock_guard<std::timed_mutex> l(op_mu_);
+    (void)hipStreamSynchronize(stream_);
+    if (nonblocking_) {
+      ncclResult_t st = ncclCommFinalize(comm_);
+      // bounded (~20 s): a finalize only waits for work already in flight
+      for (int i = 0; st == ncclInProgress && i < 200000; ++i) {
+        std::this_thread::sleep_for(std::chrono::microseconds(100));
+        if (ncclCommGetAsyncError(comm_, &st) != ncclSuccess) st = ncclInternalError;
+      }
+      if (st == ncclInProgress) {
+        (void)ncclCommAbort(comm_);
+        return;
+      }
+    }
+    (void)ncclCommDestroy(comm_);
   }
   std::shared_ptr<Work> done() { return std::make_shared<Work>(device_, stream_, pool_); }
 
@@ -334,6 +448,8 @@ class Communicator {
   hipStream_t stream_ = nullptr;
   hipEvent_t dep_ = nullptr;
   int group_depth_ = 0;
+  bool nonblocking_ = false;
+  std::atomic<bool> inited_{false}, abort_done_{false}, closed_{false};
   std::atomic<bool> aborted_{false};
   std::timed_mutex op_mu_;  // held across the aborted check + enqueue of every RCCL call
 };
@@ -368,7 +484,11 @@ void bind_comm(pybind11::module& m) {
       .def_property_readonly("device", &Communicator::device)
       .def_property_readonly("stream", &Communicator::stream)
       .def_property_readonly("aborted", &Communicator::aborted)
+      .def_property_readonly("closed", &Communicator::closed)
+      .def_property_readonly("nonblocking", &Communicator::nonblocking)
+      .def("close", &Communicator::close, py::call_guard<py::gil_scoped_release>())
       .def("wait_stream", &Communicator::wait_stream)
+      .def("wait_event", &Communicator::wait_event)
       .def("all_reduce", &Communicator::all_reduce)
       .def("reduce_scatter", &Communicator::reduce_scatter)
       .def("all_gather", &Communicator::all_gather)
@@ -381,11 +501,31 @@ void bind_comm(pybind11::module& m) {
       .def("async_error", &Communicator::async_error);
   // the watchdog aborts every communicator before it acts on a timed-out collective
   pda_rt::set_abort_hook([] { Communicator::abort_all(); });
-  // event-backed watchdog tickets (DDP / FSDP / pipeline collectives) retire on completion
-  pda_rt::set_event_query([](uintptr_t ev) -> int {
+  // event-backed watchdog tickets (DDP / FSDP / pipeline collectives) retire on completion; each
+  // ticket records and owns its own event on the collective's stream
+  pda_rt::EventOps ops;
+  ops.record = [](uintptr_t stream) -> uintptr_t {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int dev = -1;
+    if (hipStreamGetDevice(s, &dev) != hipSuccess) return 0;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    if (prev != dev) (void)hipSetDevice(dev);
+    hipEvent_t e = nullptr;
+    uintptr_t out = 0;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
+      if (hipEventRecord(e, s) == hipSuccess) out = reinterpret_cast<uintptr_t>(e);
+      else (void)hipEventDestroy(e);
+    }
+    if (prev != dev && prev >= 0) (void)hipSetDevice(prev);
+    return out;
+  };
+  ops.query = [](uintptr_t ev) -> int {
     const hipError_t e = hipEventQuery(reinterpret_cast<hipEvent_t>(ev));
     return e == hipSuccess ? 1 : (e == hipErrorNotReady ? 0 : -1);
-  });
+  };
+  ops.destroy = [](uintptr_t ev) { (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(ev)); };
+  pda_rt::set_event_ops(ops);
 }
 
 }  // namespace pda_comm

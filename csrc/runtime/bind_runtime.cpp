@@ -69,7 +69,7 @@ void bind_runtime(pybind11::module& m) {
            py::arg("action") = "abort", py::arg("exit_code") = 17, py::arg("poll") = 0.5)
       .def("arm", &Watchdog::arm, py::arg("desc"), py::arg("timeout") = -1.0)
       .def("disarm", &Watchdog::disarm)
-      .def("attach_event", &Watchdog::attach_event, py::arg("ticket"), py::arg("event"))
+      .def("attach_stream", &Watchdog::attach_stream, py::arg("ticket"), py::arg("stream"))
       .def_property_readonly("armed", &Watchdog::armed)
       .def("pending", &Watchdog::pending)
       .def("expired", &Watchdog::expired)

@@ -128,9 +128,18 @@ class HostRing {
 // register ncclCommAbort of every live communicator here: csrc/comm/communicator.cpp).
 void set_abort_hook(void (*hook)());
 void run_abort_hook();
-// Completion query for event-backed tickets (registered by the HIP side, csrc/comm/communicator.cpp):
-// returns 1 when the GPU event has completed, 0 when not yet, -1 on error.
-void set_event_query(int (*query)(uintptr_t event));
+// GPU event operations for event-backed tickets (registered by the HIP side, csrc/comm/communicator.cpp):
+//   record(stream) -> a NEW event recorded on `stream`, owned by the ticket (0 on failure);
+//   query(event)   -> 1 when the event has completed, 0 when not yet, -1 on error;
+//   destroy(event) -> releases an event that record() returned.
+// A ticket owns its event, so it never queries a handle whose owner (a Python work object, a DDP
+// module) was garbage-collected while the ticket was still armed.
+struct EventOps {
+  uintptr_t (*record)(uintptr_t stream) = nullptr;
+  int (*query)(uintptr_t event) = nullptr;
+  void (*destroy)(uintptr_t event) = nullptr;
+};
+void set_event_ops(const EventOps& ops);
 
 class Watchdog {
  public:
@@ -138,9 +147,10 @@ class Watchdog {
   ~Watchdog();
   int64_t arm(const std::string& desc, double timeout_s);
   bool disarm(int64_t id);
-  // attach the completion event of the armed collective: the watchdog thread disarms the ticket by
-  // itself once the event has completed (the caller must keep the event alive until it disarms)
-  bool attach_event(int64_t id, uintptr_t event);
+  // attach the completion point of the armed collective: an event owned by the ticket is recorded on
+  // `stream` right behind the collective, and the watchdog thread disarms the ticket by itself once
+  // that event has completed.  Returns false when the ticket is gone or no event ops are registered.
+  bool attach_stream(int64_t id, uintptr_t stream);
   size_t armed() const;
   std::vector<std::string> pending() const;
   std::vector<std::string> expired() const;
@@ -153,8 +163,9 @@ class Watchdog {
     std::string desc;
     double start = 0, deadline = 0;
     bool reported = false;
-    uintptr_t event = 0;
+    uintptr_t event = 0;  // owned: destroyed when the ticket is erased
   };
+  void erase_locked(std::map<int64_t, Ticket>::iterator it);
   void loop();
   double timeout_s_;
   int rank_;

@@ -23,11 +23,20 @@ namespace pda_rt {
 
 namespace {
 std::atomic<void (*)()> g_abort_hook{nullptr};
-std::atomic<int (*)(uintptr_t)> g_event_query{nullptr};
+std::mutex g_ops_mu;
+EventOps g_ops;  // set once at module load, read under g_ops_mu
+
+EventOps event_ops() {
+  std::lock_guard<std::mutex> g(g_ops_mu);
+  return g_ops;
+}
 }  // namespace
 
 void set_abort_hook(void (*hook)()) { g_abort_hook.store(hook); }
-void set_event_query(int (*query)(uintptr_t)) { g_event_query.store(query); }
+void set_event_ops(const EventOps& ops) {
+  std::lock_guard<std::mutex> g(g_ops_mu);
+  g_ops = ops;
+}
 
 void run_abort_hook() {
   if (auto h = g_abort_hook.load()) h();
@@ -68,16 +77,34 @@ int64_t Watchdog::arm(const std::string& desc, double timeout_s) {
   return id;
 }
 
-bool Watchdog::disarm(int64_t id) {
-  std::lock_guard<std::mutex> g(mu_);
-  return tickets_.erase(id) > 0;
+void Watchdog::erase_locked(std::map<int64_t, Ticket>::iterator it) {
+  if (it->second.event) {
+    const EventOps ops = event_ops();
+    if (ops.destroy) ops.destroy(it->second.event);
+  }
+  tickets_.erase(it);
 }
 
-bool Watchdog::attach_event(int64_t id, uintptr_t event) {
+bool Watchdog::disarm(int64_t id) {
   std::lock_guard<std::mutex> g(mu_);
   auto it = tickets_.find(id);
   if (it == tickets_.end()) return false;
-  it->second.event = event;
+  erase_locked(it);
+  return true;
+}
+
+bool Watchdog::attach_stream(int64_t id, uintptr_t stream) {
+  const EventOps ops = event_ops();
+  if (!ops.record || !ops.query || !ops.destroy) return false;
+  const uintptr_t ev = ops.record(stream);  // outside the lock: a HIP call
+  if (!ev) return false;
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = tickets_.find(id);
+  if (it == tickets_.end() || it->second.event) {
+    ops.destroy(ev);
+    return false;
+  }
+  it->second.event = ev;
   return true;
 }
 
@@ -120,10 +147,10 @@ void Watchdog::loop() {
     // event-backed tickets retire themselves: a collective whose completion event has fired is done
     // whether or not its owner ever gets back to disarm it (e.g. a DDP stage driven by a pipeline
     // schedule, whose forward never runs the owner's sweep)
-    if (auto q = g_event_query.load()) {
+    if (auto q = event_ops().query) {
       for (auto it = tickets_.begin(); it != tickets_.end();) {
-        if (it->second.event && !it->second.reported && q(it->second.event) == 1) it = tickets_.erase(it);
-        else ++it;
+        auto cur = it++;
+        if (cur->second.event && !cur->second.reported && q(cur->second.event) == 1) erase_locked(cur);
       }
     }
     const double t = now_s();

@@ -14,7 +14,6 @@ from ..data.device import DeviceSyntheticTokens
 from ..models.gpt2 import GPT2, config
 from ..optim import AdamW
 from ..parallel.ddp import DistributedDataParallel
-from ..utils.tunable import use_tuned_gemms
 from .common import comm_record, emit, setup, teardown, timed
 
 
@@ -31,7 +30,6 @@ def main(argv=None):
     ap.add_argument("--layers", type=int, default=None, help="override depth (smoke runs only)")
     a = ap.parse_args(argv)
     rank, world, local, device = setup(a.gpus)
-    gemm_table = use_tuned_gemms("gpt2")
     over = {} if a.layers is None else {"n_layer": a.layers}
     torch.manual_seed(0)
     model = GPT2(config(a.model, n_positions=max(1024, a.seq), **over), device=device, dtype=torch.bfloat16)
@@ -52,7 +50,7 @@ def main(argv=None):
     emit({"metric": "tokens/sec (whole job) GPT-2 DDP", "value": round(toks, 1), "unit": "tokens/sec",
           "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(secs / a.steps * 1e3, 3),
           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-          "data": "synthetic tokens (on-device), random-init weights", "gemm_table": gemm_table, "comm": comm,
+          "data": "synthetic tokens (on-device), random-init weights", "comm": comm,
           "config": {"model": a.model + ("" if a.layers is None else f"-{a.layers}L"),
                      "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": f"dp{world}",
                      "params": model.num_params()}}, rank)

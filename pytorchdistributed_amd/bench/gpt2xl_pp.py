@@ -17,7 +17,6 @@ from ..models.gpt2 import GPT2Stage, config
 from ..optim import AdamW
 from ..parallel.ddp import DistributedDataParallel
 from ..parallel.pipeline import Pipeline, partition_layers, pp_dp_groups
-from ..utils.tunable import use_tuned_gemms
 from .common import emit, setup, teardown, timed
 
 
@@ -37,7 +36,6 @@ def main(argv=None):
     ap.add_argument("--layers", type=int, default=None)
     a = ap.parse_args(argv)
     rank, world, local, device = setup(a.gpus)
-    gemm_table = use_tuned_gemms("gpt2xl")
     pp = a.pp or min(4, world)
     dp = world // pp
     cfg = config(a.model, **({} if a.layers is None else {"n_layer": a.layers}))
@@ -86,7 +84,7 @@ def main(argv=None):
     emit({"metric": "tokens/sec (whole job) GPT-2-XL pipeline x DDP", "value": round(toks, 1),
           "unit": "tokens/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
           "ms_per_step": round(secs / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-          "vs_baseline": None, "dtype": "bf16", "dp_comm": comm, "data": "synthetic tokens (on-device), random-init weights", "gemm_table": gemm_table,
+          "vs_baseline": None, "dtype": "bf16", "dp_comm": comm, "data": "synthetic tokens (on-device), random-init weights",
           "config": {"model": a.model, "global_batch": a.micro * a.micro_batch * dp, "seq_len": a.seq,
                      "parallelism": f"pp{pp}xdp{dp}", "schedule": a.schedule, "microbatches": a.micro,
                      **({"chunks": a.chunks} if a.schedule == "interleaved" else {})}}, rank)

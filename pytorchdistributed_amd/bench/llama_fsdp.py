@@ -14,7 +14,6 @@ from ..data.device import DeviceSyntheticTokens
 from ..models.llama import Llama, LlamaBlock, config
 from ..optim import AdamW
 from ..parallel.fsdp import FullyShardedDataParallel
-from ..utils.tunable import use_tuned_gemms
 from .common import comm_record, emit, setup, teardown, timed
 
 
@@ -31,7 +30,6 @@ def main(argv=None):
     ap.add_argument("--layers", type=int, default=None, help="override depth (smoke runs only)")
     a = ap.parse_args(argv)
     rank, world, local, device = setup(a.gpus)
-    gemm_table = use_tuned_gemms("llama3")
     over = {} if a.layers is None else {"n_layers": a.layers}
     torch.manual_seed(0)
     model = Llama(config(a.model, **over), device=device, dtype=torch.bfloat16)
@@ -53,7 +51,7 @@ def main(argv=None):
     emit({"metric": "tokens/sec (whole job) Llama-3 FSDP full-shard", "value": round(toks, 1),
           "unit": "tokens/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
           "ms_per_step": round(secs / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-          "vs_baseline": None, "dtype": "bf16", "data": "synthetic tokens (on-device), random-init weights", "gemm_table": gemm_table, "comm": comm,
+          "vs_baseline": None, "dtype": "bf16", "data": "synthetic tokens (on-device), random-init weights", "comm": comm,
           "config": {"model": a.model + ("" if a.layers is None else f"-{a.layers}L"),
                      "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": f"fsdp{world}",
                      "params": n_params}}, rank)

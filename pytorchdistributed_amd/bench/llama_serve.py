@@ -14,7 +14,6 @@ import torch
 
 from ..models.llama import Llama, config
 from ..serving import KVCache, generate
-from ..utils.tunable import use_tuned_gemms
 
 
 def main(argv=None):
@@ -32,7 +31,6 @@ def main(argv=None):
     a = ap.parse_args(argv)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    table = use_tuned_gemms("llama3")
     over = {} if a.layers is None else {"n_layers": a.layers}
     torch.manual_seed(0)
     model = Llama(config(a.model, **over), device=dev, dtype=torch.bfloat16).eval()
@@ -68,7 +66,7 @@ def main(argv=None):
         "metric": "Llama-3 KV-cached generation (1 GPU)", "model": a.model + ("" if a.layers is None else f"-{a.layers}L"),
         "batch": a.batch, "decode_graph": a.graph, "weights": f"int8 (per-row scale): {a.int8_names}" if a.int8 else "bf16",
         "int8_head": a.int8_head, "prompt": a.prompt, "new_tokens": a.new, "dtype": "bf16",
-        "data": "synthetic prompts, random-init weights", "gemm_table": table,
+        "data": "synthetic prompts, random-init weights",
         "prefill_ms": round(t_pre * 1e3, 2), "prefill_tokens_per_s": round(a.batch * a.prompt / t_pre, 1),
         "decode_ms_per_step": round(t_dec / steps * 1e3, 3),
         "decode_tokens_per_s": round(a.batch * steps / t_dec, 1),

@@ -30,6 +30,22 @@ _DTYPE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 
 _OPS = {"sum": 0, "avg": 1, "max": 2, "min": 3, "prod": 4}
 _created: Dict[Tuple[int, ...], int] = {}
 _cache: Dict[Tuple[Tuple[int, ...], int], "Communicator"] = {}
+# last enqueued native operation per device: (communicator, Work) — the cross-communicator order rule
+_LAST: Dict[int, tuple] = {}
+_ORDER_STATS = {"order_waits": 0}
+
+
+def ordered() -> bool:
+    """One global order for every native communicator of a process (``PDA_COMM_ORDER``, default on).
+
+    Each communicator owns a stream, so a rank driving two of them — PP x DP: the pipeline's P2P group
+    and the stage's DP all-reduce group — could otherwise run their RCCL kernels in either order on the
+    GPU.  With the rule on, an operation on communicator B is stream-ordered after the last operation
+    enqueued on any other communicator A of the same device, so each rank executes its collectives in
+    exactly its host enqueue order.  Ranks sharing a communicator enqueue identical sequences on it
+    (same schedule), and the DP groups only join ranks of the same pipeline stage, so no two ranks can
+    wait on each other's communicators in opposite orders."""
+    return os.environ.get("PDA_COMM_ORDER", "1") != "0"
 
 
 def enabled() -> bool:
@@ -125,6 +141,23 @@ class Communicator:
     def _after(self, streams: Optional[Iterable[torch.cuda.Stream]]):
         for s in (streams if streams is not None else [torch.cuda.current_stream(self.device)]):
             self._c.wait_stream(s.cuda_stream)
+        if ordered():
+            last = _LAST.get(self.device.index)
+            if last is not None and last[0] is not self and not last[0].closed and not last[1].is_completed():
+                self._c.wait_event(last[1].event)
+                _ORDER_STATS["order_waits"] += 1
+
+    def _done(self, work: "Work") -> "Work":
+        _LAST[self.device.index] = (self, work)
+        return work
+
+    @property
+    def closed(self) -> bool:
+        return self._c.closed
+
+    def close(self):
+        """ncclCommDestroy now (after draining the comm stream); later operations raise."""
+        self._c.close()
 
     def _check(self, name: str, *ts, **kw):
         """``PDA_DEBUG=collectives``: the cross-rank fingerprint check (parallel/debug.py) covers the
@@ -146,7 +179,8 @@ class Communicator:
         self._check("all_reduce", t, op=op)
         self._after(streams)
         self._hold(t)
-        return Work(self._c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPE[t.dtype], _OPS[op]), (t,))
+        return self._done(Work(self._c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPE[t.dtype], _OPS[op]),
+                               (t,)))
 
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum", streams=None) -> Work:
         """``out`` = op over ranks of this rank's ``out.numel()`` chunk of ``inp``."""
@@ -155,8 +189,8 @@ class Communicator:
         self._check("reduce_scatter", out, inp, op=op)
         self._after(streams)
         self._hold(out, inp)
-        return Work(self._c.reduce_scatter(inp.data_ptr(), out.data_ptr(), out.numel(), _DTYPE[out.dtype], _OPS[op]),
-                    (out, inp))
+        return self._done(Work(self._c.reduce_scatter(inp.data_ptr(), out.data_ptr(), out.numel(), _DTYPE[out.dtype],
+                                                      _OPS[op]), (out, inp)))
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor, streams=None) -> Work:
         """``out`` = concatenation over ranks of ``inp``."""
@@ -165,7 +199,8 @@ class Communicator:
         self._check("all_gather", out, inp)
         self._after(streams)
         self._hold(out, inp)
-        return Work(self._c.all_gather(inp.data_ptr(), out.data_ptr(), inp.numel(), _DTYPE[inp.dtype]), (out, inp))
+        return self._done(Work(self._c.all_gather(inp.data_ptr(), out.data_ptr(), inp.numel(), _DTYPE[inp.dtype]),
+                               (out, inp)))
 
     def broadcast(self, t: torch.Tensor, root: int = 0, streams=None) -> Work:
         """In place from group rank ``root``."""
@@ -173,7 +208,7 @@ class Communicator:
         self._check("broadcast", t, src=root)
         self._after(streams)
         self._hold(t)
-        return Work(self._c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPE[t.dtype], root), (t,))
+        return self._done(Work(self._c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPE[t.dtype], root), (t,)))
 
     def send_recv(self, sends: List[Tuple[torch.Tensor, int]], recvs: List[Tuple[torch.Tensor, int]],
                   streams=None) -> Work:
@@ -191,7 +226,7 @@ class Communicator:
                 self._c.recv(t.data_ptr(), t.numel(), _DTYPE[t.dtype], peer)
         finally:
             w = self._c.group_end()
-        return Work(w, tuple(t for t, _ in sends) + tuple(t for t, _ in recvs))
+        return self._done(Work(w, tuple(t for t, _ in sends) + tuple(t for t, _ in recvs)))
 
     # ---------------------------------------------------------------- failure handling
     def abort(self):
@@ -212,7 +247,7 @@ def for_group(group=None, device: Optional[torch.device] = None) -> Communicator
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     key = (ranks, dev.index)
     c = _cache.get(key)
-    if c is None or c.aborted:
+    if c is None or c.aborted or c.closed:
         c = _cache[key] = Communicator(group, dev)
     return c
 
@@ -238,5 +273,20 @@ def try_for_group(group=None, device: Optional[torch.device] = None) -> Optional
 
 
 def reset():
-    """Drop cached communicators (destroy_process_group)."""
+    """Close and drop every cached communicator (destroy_process_group): ncclCommDestroy
+    runs here, explicitly, while c10d's process group and the store still exist — not whenever the
+    DDP / FSDP objects holding a communicator happen to be garbage-collected."""
+    for c in list(_cache.values()):
+        try:
+            if not c.aborted:
+                c.close()
+        except Exception as e:  # noqa: BLE001 - teardown must reach c10d's destroy
+            import warnings
+
+            warnings.warn(f"closing a native RCCL communicator failed: {e}")
     _cache.clear()
+    _LAST.clear()
+
+
+def order_stats() -> dict:
+    return dict(_ORDER_STATS)

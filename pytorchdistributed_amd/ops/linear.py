@@ -77,16 +77,16 @@ def _gemm_wgrad(dy, x2, out_dtype, target=None):
     return dw
 
 
-def _fused_wgrad_db(dy2, x2, wparam, bparam, target):
+def _fused_wgrad_db(dy2, x2, wparam, bparam, target, tb):
     """dW and db from ONE pipelined GEMM (db = row sums of its A operand dY^T), or None when
-    the shape does not take that kernel (the caller falls back to GEMM + column sum)."""
+    the shape does not take that kernel (the caller falls back to GEMM + column sum).  ``target`` / ``tb``
+    are the flat-buffer slots the caller claimed (each slot is claimed exactly once per backward)."""
     if os.environ.get("PDA_WGRAD_DB_FUSED", "1") != "1":
         return None
     if not (dy2.dtype == x2.dtype == torch.bfloat16 and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0):
         return None
     N, K = dy2.shape[1], x2.shape[1]
     dw = target if target is not None else torch.empty(N, K, device=dy2.device, dtype=wparam.dtype)
-    tb = grad_target(bparam)
     db = tb if tb is not None else torch.empty(N, device=dy2.device, dtype=bparam.dtype)
     if db.dtype not in (torch.bfloat16, torch.float32) or dw.dtype not in (torch.bfloat16, torch.float32):
         return None
@@ -100,22 +100,23 @@ def _param_grads(dy2, x2, wparam, bparam, need_w, need_b):
     gradient buffers when the parameters have them.  With both needed, the native weight-gradient GEMM
     also produces the bias gradient (its A operand's row sums) when it runs on the pipelined tile."""
     dw = db = None
+    # claim each flat slot ONCE: a second grad_target() on the same parameter reads as a tied weight
+    # (flat.py), which would push the parameter off the side stream for good
+    target = grad_target(wparam) if need_w else None
+    tb = grad_target(bparam) if need_b else None
+    side = target is not None and _streams.side_ok(wparam) and target.numel() < _SIDE_MAX_NUMEL
     if need_w and need_b and dy2.shape[0] > 0:
-        target = grad_target(wparam)
-        side = target is not None and _streams.side_ok(wparam) and target.numel() < _SIDE_MAX_NUMEL
         with (_streams.wgrad_stream(dy2.device, dy2, x2) if side else contextlib.nullcontext()):
-            r = _fused_wgrad_db(dy2, x2, wparam, bparam, target)
+            r = _fused_wgrad_db(dy2, x2, wparam, bparam, target, tb)
         if r is not None:
             dw, db = r
             if db is None:
-                tb = grad_target(bparam)
                 db = C().colsum(dy2, out=tb, out_bf16=bparam.dtype == torch.bfloat16)
                 if db.dtype != bparam.dtype:
                     db = db.to(bparam.dtype)
             return dw, db
     if need_w:
-        target = grad_target(wparam)
-        if target is not None and _streams.side_ok(wparam) and target.numel() < _SIDE_MAX_NUMEL:
+        if side:
             # written straight into the flat gradient slot: run it beside the critical path
             # (ops/streams.py; same contract as the conv weight gradient).  A dW with a full wave
             # of 256x256 output tiles per CU fills the chip by itself; beside other work it only
@@ -130,7 +131,6 @@ def _param_grads(dy2, x2, wparam, bparam, need_w, need_b):
             dw = _gemm_wgrad(dy2, x2, wparam.dtype, target)
     if need_b:
         # written in the parameter dtype, straight into its flat-buffer slot when it has one
-        tb = grad_target(bparam)
         db = C().colsum(dy2, out=tb, out_bf16=bparam.dtype == torch.bfloat16)
         if db.dtype != bparam.dtype:
             db = db.to(bparam.dtype)

@@ -39,6 +39,8 @@ from ..utils import watchdog as _watchdog
 from .flat import FlatGroup, flatten_buffers
 
 _DTYPE_IDS = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}
+_NATIVE_DTYPES = (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64, torch.int32,
+                  torch.uint8, torch.int8)
 
 
 def _mb(env, default):
@@ -102,6 +104,15 @@ class DistributedDataParallel(tnn.Module):
         # fp32 ring, one rounding back) instead of accumulating bf16 partial sums over N ranks
         self.reduce_fp32 = os.environ.get("PDA_GRAD_REDUCE_DTYPE", "") in ("fp32", "float32")
         self._f32: Dict[int, torch.Tensor] = {}
+        # ---- native RCCL communicator for the bucket all-reduces AND the state / buffer /
+        # rebuild-order broadcasts, so the step drives one communicator (comm.py; PDA_COMM=c10d: ProcessGroupNCCL)
+        self._ncomm = None
+        on_gpu0 = bool(params) and all(p.is_cuda for p in params)
+        if self._comm and self.backend == "nccl" and on_gpu0:
+            from .. import comm as _comm
+
+            if _comm.enabled():
+                self._ncomm = _comm.try_for_group(process_group, params[0].device)
         # ---- rank-0 state broadcast (X04) as one collective per flat buffer
         self._buffer_flats = flatten_buffers(module)
         if self._comm:
@@ -118,14 +129,6 @@ class DistributedDataParallel(tnn.Module):
         self._callback_task = -1
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
         self.reducer.prepare()
-        # ---- native RCCL communicator for the bucket all-reduces (comm.py; PDA_COMM=c10d: ProcessGroupNCCL)
-        self._ncomm = None
-        on_gpu0 = bool(params) and all(p.is_cuda for p in params)
-        if self._comm and self.backend == "nccl" and on_gpu0:
-            from .. import comm as _comm
-
-            if _comm.enabled():
-                self._ncomm = _comm.try_for_group(process_group, params[0].device)
         # ---- optional IPC all-reduce over xGMI for buckets (PDA_ALLREDUCE=ipc|oneshot|twoshot, single node)
         self.xgmi = None
         on_gpu = bool(params) and all(p.is_cuda for p in params)
@@ -188,7 +191,7 @@ class DistributedDataParallel(tnn.Module):
         if self.world > 1 and dist.is_initialized():
             dev = self._params[0].device if self.backend == "nccl" else torch.device("cpu")
             t = torch.tensor(order, dtype=torch.int64, device=dev)
-            dist.broadcast(t, self._src0(), group=self.process_group)
+            self._bcast(t)
             order = t.tolist()
         current = [pi for b in range(self.reducer.num_buckets) for pi in self.reducer.bucket_params(b)]
         if order == current:
@@ -252,8 +255,12 @@ class DistributedDataParallel(tnn.Module):
         return dist.get_global_rank(self.process_group, 0) if self.process_group is not None else 0
 
     def _bcast(self, t: torch.Tensor):
+        """Broadcast from the group's rank 0 in place.  On the native communicator it is enqueued on the
+        comm stream after the current stream, and the current stream waits on it (no host block)."""
         if self._use_ring() and t.device.type == "cpu":
             pdist.host_ring().broadcast(t.data_ptr(), t.numel() * t.element_size(), 0)
+        elif self._ncomm is not None and t.is_cuda and t.dtype in _NATIVE_DTYPES:
+            self._ncomm.broadcast(t, 0).wait()
         else:
             dist.broadcast(t, self._src0(), group=self.process_group)
 
@@ -290,7 +297,7 @@ class DistributedDataParallel(tnn.Module):
             work = _EventWork(done)
             self._works.append((work, None))
             self._tickets.append((ticket, work))
-            _watchdog.attach(ticket, work)
+            _watchdog.attach(ticket, self._ipc_stream)
             return
         ticket = _watchdog.arm(f"ddp all_reduce bucket {b} ({nbytes / 2**20:.1f} MB, {t.dtype})")
         up = self.reduce_fp32 and t.dtype != torch.float32
@@ -311,7 +318,7 @@ class DistributedDataParallel(tnn.Module):
                 else:
                     work = c.all_reduce(t, "avg", streams=producers)
                 self._works.append((work, None))
-                _watchdog.attach(ticket, work)
+                _watchdog.attach(ticket, c.stream)
             elif self.backend == "nccl":
                 # RCCL orders its stream after the CURRENT stream: make that the side stream, itself
                 # ordered after the main stream, when weight gradients are still being produced there
@@ -387,14 +394,26 @@ class DistributedDataParallel(tnn.Module):
         """Gradient readiness spread over several backward passes (an interleaved pipeline's chunks each
         finish in their own backward): a backward that leaves buckets unlaunched keeps the bucket state
         and its in-flight collectives instead of treating the rest as unused; the pass that launches
-        the last bucket finalizes."""
+        the last bucket finalizes.  The driver of the passes calls :meth:`finish_multi_pass` after the
+        last one, which runs the normal end-of-backward checks if no pass did."""
         self._multi_pass = bool(on)
+        self._multi_pass_open = False
 
-    def _finalize(self):
+    def finish_multi_pass(self):
+        """End of a multi-pass step: if some parameter never received a gradient (so no pass launched
+        every bucket and each one deferred), finalize now — the unused-parameter error, or with
+        ``find_unused_parameters`` the zero-filled flush — instead of leaving buckets unlaunched,
+        collectives un-waited and ``pending_comm`` set for the optimizer."""
+        if getattr(self, "_multi_pass_open", False):
+            self._finalize(force=True)
+
+    def _finalize(self, force: bool = False):
         self._callback_queued = False
-        if getattr(self, "_multi_pass", False) and self.require_backward_grad_sync and \
+        if not force and getattr(self, "_multi_pass", False) and self.require_backward_grad_sync and \
                 not self.reducer.all_launched() and self.reducer.any_marked():
-            return  # later passes mark the remaining parameters
+            self._multi_pass_open = True
+            return  # later passes mark the remaining parameters (finish_multi_pass closes the step)
+        self._multi_pass_open = False
         if not self.reducer.all_launched():
             unready = self.reducer.unready_params()
             if not self.find_unused_parameters:

@@ -47,6 +47,7 @@ import torch.nn as tnn
 
 from .. import distributed as pdist
 from ..ops import streams as _streams
+from ..utils import watchdog as _watchdog
 
 ALIGN = 8
 
@@ -202,15 +203,17 @@ class _Unit:
                 flat = self.flat
                 self.pending_ag = self.fsdp._ipc(lambda: self.fsdp.xgmi.all_gather_into_tensor(flat, send),
                                                  [torch.cuda.current_stream(self.device)], [send, flat])
+                self.fsdp._track("xgmi all_gather", self, self.fsdp._ipc_stream)
             elif self.fsdp.ncomm is not None:
                 self.pending_ag = self.fsdp.ncomm.all_gather(self.flat, send)
+                self.fsdp._track("all_gather", self, self.fsdp.ncomm.stream)
             else:
                 self.pending_ag = dist.all_gather_into_tensor(self.flat, send, group=self.fsdp.group,
                                                               async_op=True)
 
     def finish_gather(self):
         if self.pending_ag is not None:
-            with self.fsdp._exposed():
+            with self.fsdp._exposed(), self.fsdp._watch_c10d(f"all_gather unit {self.index}"):
                 self.pending_ag.wait()
             self.pending_ag = None
             self.gathered = True
@@ -346,6 +349,32 @@ class FullyShardedDataParallel(tnn.Module):
             self._exposed_events = []
         return out
 
+    def _release_completed(self):
+        """c10d path: release the transient gradient storage of units whose reduce-scatter finished."""
+        keep = []
+        for u, work in self._deferred_release:
+            if work is None or work.is_completed():
+                u.release_grad()
+            else:
+                keep.append((u, work))
+        self._deferred_release = keep
+
+    def _watch_c10d(self, what: str):
+        """Deadline for a c10d wait (gloo blocks the host there); native / IPC collectives already carry a
+        ticket from their enqueue (:meth:`_track`)."""
+        if not self.comm_on or self.ncomm is not None or self.xgmi is not None:
+            return contextlib.nullcontext()
+        return _watchdog.watch(f"fsdp c10d {what}")
+
+    def _track(self, what: str, u: "_Unit", stream):
+        """Watchdog ticket for a unit collective just enqueued on ``stream``: it retires on
+        an event the native thread records behind the collective, so a peer that never joins the
+        all-gather / reduce-scatter ends in a report + ncclCommAbort + stack dump, not a silent hang in the
+        next synchronize."""
+        nbytes = (u.numel if "gather" in what else u.shard_numel) * u.flat.element_size()
+        _watchdog.track(f"fsdp {what} unit {u.index} ({nbytes / 2**20:.1f} MB)", stream)
+        self._stats["tickets"] = self._stats.get("tickets", 0) + 1
+
     def _ipc(self, fn, producers, tensors):
         """Run ``fn`` on the IPC stream after ``producers``; returns a work handle (wait = stream wait)."""
         s = self._ipc_stream
@@ -405,6 +434,9 @@ class FullyShardedDataParallel(tnn.Module):
                 if work is not None:
                     work.wait()
             self._pending_rs = []
+            deferred, self._deferred_release = self._deferred_release, []
+            for du, _work in deferred:
+                du.release_grad()
             _join_side_streams(self.units)
             for u in self.units:
                 u.arrived = 0
@@ -445,8 +477,10 @@ class FullyShardedDataParallel(tnn.Module):
         if self.xgmi is not None:
             work = self._ipc(lambda: self.xgmi.reduce_scatter_tensor(out, grad_full, average=True), producers,
                              [out, grad_full])
+            self._track("xgmi reduce_scatter", u, self._ipc_stream)
         elif self.ncomm is not None:
             work = self.ncomm.reduce_scatter(out, grad_full, "avg", streams=producers)
+            self._track("reduce_scatter", u, self.ncomm.stream)
         else:
             ctx = contextlib.nullcontext()
             if len(producers) > 1:
@@ -469,8 +503,11 @@ class FullyShardedDataParallel(tnn.Module):
             u.release_grad()  # record_stream on the collective's stream holds the storage until it is read
         else:
             # c10d: with TORCH_NCCL_AVOID_RECORD_STREAMS=1 (and on gloo) nothing ties the storage to the
-            # in-flight collective, so the release waits until _finish_rs has waited on it
-            self._deferred_release.append(u)
+            # in-flight collective, so a unit's storage is released once ITS collective has completed
+            # (polled here at every later unit, the rest in _finish_rs) — never the whole unsharded
+            # gradient held to the end of backward
+            self._release_completed()
+            self._deferred_release.append((u, work))
         if u is not self.root_unit:
             u.reshard()
         self._queue_final()
@@ -479,12 +516,12 @@ class FullyShardedDataParallel(tnn.Module):
         """Collect every queued reduce-scatter into its shard's gradient (the compute stream waits on
         the collectives here, once, at the end of backward)."""
         pending, self._pending_rs = self._pending_rs, []
-        with self._exposed():
+        with self._exposed(), self._watch_c10d(f"reduce_scatter x{len(pending)}"):
             for _u, work, _out in pending:
                 if work is not None:
                     work.wait()
         deferred, self._deferred_release = self._deferred_release, []
-        for u in deferred:
+        for u, _work in deferred:
             u.release_grad()
         for u, work, out in pending:
             if not self.nccl and self.xgmi is None and self.world > 1:

@@ -36,6 +36,7 @@ import torch.nn as tnn
 from torch.utils.checkpoint import checkpoint
 
 from .. import distributed as pdist
+from ..utils import watchdog as _watchdog
 
 _nullctx = contextlib.nullcontext
 
@@ -175,6 +176,24 @@ def pp_dp_groups(pp: int, dp: int):
 
 
 # ------------------------------------------------------------------ the pipeline engine
+class _P2PWork:
+    """Completion of a P2P group that received buffers: ``wait()`` orders the current stream after it
+    (native: a stream-event wait; c10d: the works' own wait)."""
+
+    def __init__(self, native=None, c10d=None, desc: str = "pp p2p"):
+        self.native, self.c10d, self.desc = native, c10d, desc
+
+    def wait(self):
+        if self.native is not None:
+            self.native.wait()  # the native group's watchdog ticket was armed at enqueue
+        if self.c10d:
+            # c10d (gloo: the wait blocks the host) under a deadline of its own
+            with _watchdog.watch(f"{self.desc} (c10d wait)"):
+                for w in self.c10d:
+                    w.wait()
+        self.native, self.c10d = None, None
+
+
 class Pipeline:
     """Drive one pipeline stage.
 
@@ -221,6 +240,8 @@ class Pipeline:
         # PDA_COMM=c10d.  PDA_PP_FORCE_COMM=1 at one stage: the interleaved schedule's chunk-to-chunk
         # hand-offs go through RCCL send/recv to this same rank (a one-GPU box runs the P2P path).
         self._ncomm = None
+        self._send_works: List = []
+        self._tickets = 0  # watchdog tickets armed for native P2P groups (tests / stats)
         force = os.environ.get("PDA_PP_FORCE_COMM") == "1"
         if (self.device.type == "cuda" and dist.is_initialized() and dist.get_backend(group) == "nccl"
                 and (self.S > 1 or force)):
@@ -238,56 +259,74 @@ class Pipeline:
         return self.stage == self.S - 1
 
     # ---------------- shape handshake (once) and p2p helpers
+    # Transfers never make the compute stream wait for a SEND: a send is enqueued on the P2P stream after
+    # the producing kernels, its tensor is held for the allocator by record_stream on that stream
+    # (comm.py _hold), and the next micro-batch's forward runs while it is in flight (the reference's
+    # point, "B can run concurrently with A", NB03 raw lines 551-556).  The compute stream waits only
+    # before it CONSUMES a received buffer (:class:`_P2PWork`).  Every native P2P group is armed on the
+    # collective watchdog and retires on the GPU's own completion.
+    def _peer(self, r: int) -> int:
+        return dist.get_group_rank(self.group, r) if self.group is not None else r
+
+    def _native_group(self, sends, recvs, what: str):
+        w = self._ncomm.send_recv([(t.contiguous(), self._peer(r)) for t, r in sends],
+                                  [(t, self._peer(r)) for t, r in recvs])
+        nbytes = sum(t.numel() * t.element_size() for t, _ in list(sends) + list(recvs))
+        _watchdog.track(f"pp {what} stage {self.stage} ({len(sends)} send / {len(recvs)} recv, "
+                        f"{nbytes / 2**20:.2f} MB)", self._ncomm.stream)
+        self._tickets += 1
+        return w
+
     def _send_meta(self, t: torch.Tensor, dst: int):
-        meta = torch.zeros(10, dtype=torch.long, device=self.device)
-        meta[0] = t.dim()
-        meta[1] = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}[t.dtype]
-        meta[2: 2 + t.dim()] = torch.tensor(t.shape, dtype=torch.long)
-        dist.send(meta, dst, group=self.group)
+        meta = self._meta_tensor(t)
+        if self._ncomm is not None:
+            self._native_group([(meta, dst)], [], "shape send")
+        else:
+            dist.send(meta, dst, group=self.group)
 
     def _recv_meta(self, src: int):
         meta = torch.zeros(10, dtype=torch.long, device=self.device)
-        dist.recv(meta, src, group=self.group)
+        if self._ncomm is not None:
+            self._native_group([], [(meta, src)], "shape recv").synchronize()  # host needs the shape
+        else:
+            with _watchdog.watch(f"pp shape recv stage {self.stage} from {src}"):
+                dist.recv(meta, src, group=self.group)
         nd = int(meta[0])
         dtype = [torch.float32, torch.bfloat16, torch.float16][int(meta[1])]
         return tuple(int(v) for v in meta[2: 2 + nd]), dtype
 
-    def _p2p(self, send: Optional[Tuple[torch.Tensor, int]] = None, recv: Optional[Tuple[torch.Tensor, int]] = None):
-        if self._ncomm is not None and (send is not None or recv is not None):
-            g = self.group
-
-            def peer(r):
-                return dist.get_group_rank(g, r) if g is not None else r
-            sends = [(send[0].contiguous(), peer(send[1]))] if send is not None else []
-            recvs = [(recv[0], peer(recv[1]))] if recv is not None else []
-            self._ncomm.send_recv(sends, recvs).wait()
-            return
-        ops = []
-        if send is not None:
-            ops.append(dist.P2POp(dist.isend, send[0].contiguous(), send[1], group=self.group))
-        if recv is not None:
-            ops.append(dist.P2POp(dist.irecv, recv[0], recv[1], group=self.group))
-        if ops:
-            for r in dist.batch_isend_irecv(ops):
-                r.wait()
-
-    def _p2p_group(self, sends: List[Tuple[torch.Tensor, int]], recvs: List[Tuple[torch.Tensor, int]]):
-        """One fused group of transfers (global ranks as peers): native RCCL send/recv (stream wait, no
-        host block) or c10d batch_isend_irecv."""
+    def _p2p_group(self, sends: List[Tuple[torch.Tensor, int]], recvs: List[Tuple[torch.Tensor, int]],
+                   what: str = "p2p") -> Optional["_P2PWork"]:
+        """One fused group of transfers (global ranks as peers): native RCCL send/recv on the P2P stream,
+        or c10d batch_isend_irecv.  Returns the work to wait on before consuming the received buffers
+        (None when there are none); send-only groups are never waited on by the compute stream (c10d
+        send works are kept and retired by :meth:`_drain_sends` at the end of the step)."""
         if not sends and not recvs:
-            return
+            return None
         if self._ncomm is not None:
-            g = self.group
-
-            def peer(r):
-                return dist.get_group_rank(g, r) if g is not None else r
-            self._ncomm.send_recv([(t.contiguous(), peer(r)) for t, r in sends],
-                                  [(t, peer(r)) for t, r in recvs]).wait()
-            return
+            w = self._native_group(sends, recvs, what)
+            return _P2PWork(native=w) if recvs else None
         ops = [dist.P2POp(dist.isend, t.contiguous(), r, group=self.group) for t, r in sends]
         ops += [dist.P2POp(dist.irecv, t, r, group=self.group) for t, r in recvs]
-        for w in dist.batch_isend_irecv(ops):
+        works = dist.batch_isend_irecv(ops)
+        if not recvs:
+            self._send_works.extend(works)
+            return None
+        return _P2PWork(c10d=works, desc=f"pp {what} stage {self.stage}")
+
+    def _p2p(self, send: Optional[Tuple[torch.Tensor, int]] = None, recv: Optional[Tuple[torch.Tensor, int]] = None):
+        """Blocking-for-the-consumer transfer pair: the current stream waits for the receive (if any)."""
+        w = self._p2p_group([send] if send is not None else [], [recv] if recv is not None else [],
+                            "send+recv" if send is not None and recv is not None else ("recv" if recv is not None else "send"))
+        if w is not None:
             w.wait()
+
+    def _drain_sends(self):
+        if self._send_works:
+            with _watchdog.watch(f"pp sends stage {self.stage} (c10d wait, {len(self._send_works)} ops)"):
+                for w in self._send_works:
+                    w.wait()
+        self._send_works = []
 
     def _empty(self, meta):
         shape, dtype = meta
@@ -312,6 +351,14 @@ class Pipeline:
         acts_in, acts_out, inbox = {}, {}, {}
         losses = []
 
+        def take(key):
+            # a received buffer is waited on only here, when it is consumed: the hand-off of tick t
+            # overlaps whatever this rank runs before it needs the data
+            buf, work = inbox.pop(key)
+            if work is not None:
+                work.wait()
+            return buf
+
         def fwd(c, x):
             m = self.chunks[c]
             if self.recompute and torch.is_grad_enabled():
@@ -324,7 +371,7 @@ class Pipeline:
                 kind, c, mb = run[self.stage]
                 g = c * S + self.stage
                 if kind == "F":
-                    x = in_mb[mb].to(self.device) if g == 0 else inbox.pop(("F", c, mb))
+                    x = in_mb[mb].to(self.device) if g == 0 else take(("F", c, mb))
                     if g > 0:
                         x.requires_grad_()
                     acts_in[(c, mb)] = x
@@ -346,7 +393,7 @@ class Pipeline:
                         if g == G - 1:
                             out.backward()
                         else:
-                            torch.autograd.backward(out, inbox.pop(("B", c, mb)))
+                            torch.autograd.backward(out, take(("B", c, mb)))
                     x = acts_in.pop((c, mb))
                     if g > 0:
                         out_t[("B", g, mb)] = x.grad
@@ -358,29 +405,39 @@ class Pipeline:
                 key = (kind, tgt // S, mb)
                 if src == dst:  # S == 1: hand over within the rank (through RCCL under PDA_PP_FORCE_COMM)
                     t = out_t[(kind, g, mb)]
+                    w = None
                     if self._ncomm is not None:
                         buf = torch.empty_like(t)
-                        self._p2p_group([(t, self.rank)], [(buf, self.rank)])
+                        w = self._p2p_group([(t, self.rank)], [(buf, self.rank)], "loopback")
                         t = buf
-                    local.append((key, t))
+                    local.append((key, t, w))
                     continue
                 if src == self.stage:
                     t = out_t[(kind, g, mb)].contiguous()
                     if kind == "F" and ("sent", g) not in self._vmeta:
                         self._vmeta[("sent", g)] = True
-                        meta_ops.append(dist.P2POp(dist.isend, self._meta_tensor(t), self.ranks[dst], group=self.group))
+                        meta_ops.append((self._meta_tensor(t), self.ranks[dst]))
                     ops.append((t, self.ranks[dst]))
                 else:
                     if kind == "F" and g not in self._vmeta:
                         mt = torch.zeros(10, dtype=torch.long, device=self.device)
-                        meta_ops.append(dist.P2POp(dist.irecv, mt, self.ranks[src], group=self.group))
-                        meta_in.append((g, mt))
+                        meta_ops.append((None, -1))  # marks that this tick has a shape exchange
+                        meta_in.append((g, mt, self.ranks[src]))
                     # shape of what arrives: virtual stage g's output (F) or input (B, = output of tgt)
                     ops.append((key, src, g if kind == "F" else tgt))
             if meta_ops:
-                for r in dist.batch_isend_irecv(meta_ops):
-                    r.wait()
-                for g, mt in meta_in:
+                if self._ncomm is not None:  # first-use shapes on the same native communicator
+                    w = self._native_group([(t, r) for t, r in meta_ops if t is not None and r >= 0],
+                                           [(mt, r) for _g, mt, r in meta_in], "shapes")
+                    if meta_in:
+                        w.synchronize()  # the host allocates the receive buffers from them
+                else:
+                    ops_ = [dist.P2POp(dist.isend, t, r, group=self.group) for t, r in meta_ops if t is not None]
+                    ops_ += [dist.P2POp(dist.irecv, mt, r, group=self.group) for _g, mt, r in meta_in]
+                    with _watchdog.watch(f"pp shapes stage {self.stage} (c10d wait)"):
+                        for r in dist.batch_isend_irecv(ops_):
+                            r.wait()
+                for g, mt, _r in meta_in:
                     nd = int(mt[0])
                     self._vmeta[g] = (tuple(int(q) for q in mt[2: 2 + nd]),
                                       [torch.float32, torch.bfloat16, torch.float16][int(mt[1])])
@@ -393,9 +450,14 @@ class Pipeline:
                     recvd.append((key, buf))
                 else:
                     sends.append(op)
-            self._p2p_group(sends, recvs)
-            for key, buf in recvd + local:
-                inbox[key] = buf
+            w = self._p2p_group(sends, recvs, "tick")
+            for key, buf in recvd:
+                inbox[key] = (buf, w)
+            for key, buf, lw in local:
+                inbox[key] = (buf, lw)
+        self._drain_sends()
+        if self.dp_module is not None:
+            self.dp_module.finish_multi_pass()
         if last:
             return torch.stack(losses).sum()
         return None
@@ -512,6 +574,7 @@ class Pipeline:
                     self._p2p(send=(dx, self.prev))
         else:
             raise ValueError(f"unknown schedule {sched!r}")
+        self._drain_sends()
         if self.is_last:
             return torch.stack(losses).sum()
         return None

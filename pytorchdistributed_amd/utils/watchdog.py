@@ -1,6 +1,8 @@
 """Collective watchdog front end.  The native thread lives in ``_C.Watchdog``
 (`csrc/runtime/watchdog.cpp`); this module owns the per-process instance and the ``watch`` helper
-used by DDP (bucket all-reduces), FSDP (all-gather / reduce-scatter) and the pipeline (P2P waits).
+used by DDP (bucket all-reduces), FSDP (parameter all-gathers / gradient reduce-scatters, ``track``) and
+the pipeline (native P2P groups, ``track``; c10d P2P waits, ``watch``).  Tickets of GPU collectives
+retire on an event the native thread records behind the collective on its stream.
 
 Config: ``PDA_WATCHDOG`` (default on), ``PDA_COLLECTIVE_TIMEOUT_S`` (default 600 s),
 ``PDA_WATCHDOG_ACTION`` = abort | exit | report.
@@ -49,20 +51,28 @@ def arm(desc: str, timeout: float = -1.0) -> int:
     return wd.arm(desc, timeout) if wd is not None else 0
 
 
-def attach(ticket: int, work) -> None:
-    """Tie an armed ticket to ``work``'s completion event, when it has one (native RCCL works, event
-    works): the native thread then disarms the ticket by itself once the collective completed, so
-    a ticket never outlives its collective even when the owner's sweep does not run (a DDP stage
-    driven by a pipeline schedule) or the process idles after its last step.  The caller keeps
-    ``work`` alive until it calls :func:`disarm`."""
-    if not ticket or _WD is None:
-        return
-    ev = getattr(work, "event", None)
-    if ev is None:
-        return
-    handle = ev if isinstance(ev, int) else getattr(ev, "cuda_event", 0)
-    if handle:
-        _WD.attach_event(ticket, int(handle))
+def attach(ticket: int, stream) -> bool:
+    """Tie an armed ticket to the completion of everything queued so far on ``stream`` (a
+    ``torch.cuda.Stream`` or a raw handle — the stream the collective was just enqueued on): the native
+    thread records an event of its own there and disarms the ticket once that event has completed, so a
+    ticket never outlives its collective even when the owner's sweep does not run (a DDP stage driven by
+    a pipeline schedule, an FSDP unit whose work is waited on by a stream only) or the process idles after
+    its last step.  The ticket owns the event: nothing the caller frees can leave the watchdog querying a
+    dead handle.  Returns False when the watchdog is off or has no GPU event support."""
+    if not ticket or _WD is None or stream is None:
+        return False
+    handle = stream if isinstance(stream, int) else getattr(stream, "cuda_stream", 0)
+    return bool(_WD.attach_stream(ticket, int(handle)))
+
+
+def track(desc: str, stream, timeout: float = -1.0) -> int:
+    """Arm a ticket for a collective just enqueued on ``stream`` and let it retire on the GPU's own
+    completion (:func:`attach`).  Returns the ticket (0 when the watchdog is off)."""
+    t = arm(desc, timeout)
+    if t and not attach(t, stream):
+        disarm(t)  # no event support: nothing would ever retire it
+        return 0
+    return t
 
 
 def armed() -> int:

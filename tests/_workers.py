@@ -619,7 +619,16 @@ def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl", force=False):
     if force:
         st = fsdp.comm_stats()
         assert st["comm_calls"] > 0 and "exposed_comm_ms" in st, st
-        extra = f" calls={st['comm_calls']} exposed_ms={st['exposed_comm_ms']}"
+        # every native all-gather / reduce-scatter carried a watchdog ticket that retired by itself
+        from pytorchdistributed_amd.utils import watchdog as wd
+
+        torch.cuda.synchronize()
+        import time
+
+        time.sleep(1.5)
+        assert st.get("tickets", 0) == st["comm_calls"], st
+        assert wd.armed() == 0 and not wd.get_watchdog().expired(), wd.get_watchdog().pending()
+        extra = f" calls={st['comm_calls']} tickets={st['tickets']} exposed_ms={st['exposed_comm_ms']}"
     with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
         f.write(f"ok {worst[0]:.3e}{extra}")
     if world > 1 or force:
@@ -691,6 +700,8 @@ def pipeline_ddp_watchdog_worker(rank, world, outdir, schedule="1f1b"):
     assert not expired, expired
     assert most <= 2 * ddp.reducer.num_buckets, (most, ddp.reducer.num_buckets)
     assert wd.armed() == 0, w.pending()
+    if schedule == "interleaved":  # the RCCL loopback hand-offs were armed (and retired) too
+        assert pipe._tickets >= 2 * steps, (pipe._tickets, steps)
     with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
         f.write(f"ok steps={steps} max_tickets={most} buckets={ddp.reducer.num_buckets}")
     pd.destroy_process_group()
@@ -1086,9 +1097,29 @@ def rccl_comm_world1_worker(rank, world, outdir):
     w = c.all_reduce(t, "sum")
     w.synchronize()
     assert w.is_completed() and c.async_error() == ""
+    assert c._c.nonblocking == (os.environ.get("PDA_COMM_NONBLOCKING", "1") != "0")
+    # cross-communicator order rule (comm.py:ordered): a second communicator's op enqueued while the
+    # first one's is still in flight is stream-ordered after it
+    c2 = comm.Communicator(None, torch.device("cuda", 0))
+    big = torch.randn(1 << 26, device="cuda")
+    before = comm.order_stats()["order_waits"]
+    w1 = c.all_reduce(big, "sum")
+    x2 = torch.randn(1 << 10, device="cuda")
+    c2.all_reduce(x2, "sum").wait()
+    assert comm.order_stats()["order_waits"] >= before + (0 if w1.is_completed() else 1)
+    torch.cuda.synchronize()
+    # explicit close: later operations raise, the cache hands out a fresh communicator
+    c2.close()
+    assert c2.closed
+    try:
+        c2.all_reduce(x2, "sum")
+        raise AssertionError("closed communicator accepted an operation")
+    except RuntimeError as e:
+        assert "closed" in str(e)
     with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
         f.write("ok")
     pd.destroy_process_group()
+    assert c.closed  # destroy_process_group closed the cached communicator before c10d's teardown
 
 
 def fsdp_resume_worker(rank, world, outdir, phase):
@@ -1124,4 +1155,46 @@ def fsdp_resume_worker(rank, world, outdir, phase):
     if phase == "first":
         model.save_sharded(ckpt, opt)
     torch.save({"losses": losses, "state": model.full_state_dict()}, os.path.join(outdir, f"{phase}{rank}.pt"))
+    pd.destroy_process_group()
+
+
+class _UnusedChunk(torch.nn.Module):
+    """A pipeline chunk with a parameter its forward never touches."""
+
+    def __init__(self, inner):
+        super().__init__()
+        self.inner = inner
+        self.unused = torch.nn.Linear(16, 16)
+
+    def forward(self, x):
+        return self.inner(x)
+
+
+def pipeline_interleaved_unused_worker(rank, world, find_unused, outdir):
+    """Interleaved schedule x DDP multi-pass with an unused parameter in one chunk: the step
+    must end in DDP's unused-parameter error (or, with find_unused_parameters, a complete finalize with a
+    zero gradient), never with buckets silently left unlaunched."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+    from pytorchdistributed_amd.parallel.pipeline import Pipeline
+
+    pd.init_process_group("gloo")
+    full = _tiny_stack(4)
+    blocks = [full[3 * i: 3 * i + 3] for i in range(4)]
+    mine = [torch.nn.Sequential(*blocks[0], *blocks[1]), _UnusedChunk(torch.nn.Sequential(*blocks[2], *blocks[3]))]
+    ddp = DistributedDataParallel(torch.nn.ModuleList(mine), bucket_cap_mb=0.002, first_bucket_mb=0.001,
+                                  find_unused_parameters=find_unused)
+    pipe = Pipeline(mine, [0], num_microbatches=2, schedule="interleaved", loss_fn=F.mse_loss,
+                    device=torch.device("cpu"), dp_module=ddp)
+    g = torch.Generator().manual_seed(1)
+    X, Y = torch.randn(4, 16, generator=g), torch.randn(4, 16, generator=g)
+    out = {"error": None}
+    try:
+        pipe.step(X, Y)
+        out["unused_grad_zero"] = bool((mine[1].unused.weight.grad == 0).all())
+        out["pending"] = [grp.pending_comm for grp in ddp.groups.values()]
+        out["open"] = ddp._multi_pass_open
+    except RuntimeError as e:
+        out["error"] = str(e)
+    torch.save(out, os.path.join(outdir, f"{rank}.pt"))
     pd.destroy_process_group()

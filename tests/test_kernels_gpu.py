@@ -977,3 +977,32 @@ def test_stem_fwd_kernel_rows_per_workgroup():
     r = subprocess.run([sys.executable, "-c", _STEM_FWD_SCRIPT], cwd=root,
                        env={**os.environ, "PDA_CONV_STEM_FWD": "1"}, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0 and "stem fwd ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("M,K,N", [(64, 40, 24), (300, 136, 200), (2048, 512, 512)])
+def test_linear_grads_land_in_flat_slots_once(monkeypatch, fused, M, K, N):
+    """each flat-buffer slot is claimed once per backward.  With the fused wgrad+db path off
+    and on small shapes (db from a column sum) the weight / bias gradients must alias the flat buffer and
+    the parameter must NOT be marked shared (a second claim reads as a tied weight and pushes the
+    parameter off the side stream for good)."""
+    monkeypatch.setenv("PDA_WGRAD_DB_FUSED", fused)
+    from pytorchdistributed_amd.ops.linear import linear
+    from pytorchdistributed_amd.parallel.flat import FlatGroup
+
+    torch.manual_seed(0)
+    w = torch.nn.Parameter((torch.randn(N, K) * 0.1).to(DEV, torch.bfloat16))
+    b = torch.nn.Parameter((torch.randn(N) * 0.1).to(DEV, torch.bfloat16))
+    fg = FlatGroup([w, b])
+    x = bf(torch.randn(M, K))
+    dy = bf(torch.randn(M, N))
+    for _ in range(2):
+        w.grad = b.grad = None
+        w._pda_claimed = b._pda_claimed = False
+        linear(x, w, b).backward(dy)
+        torch.cuda.synchronize()
+        assert not getattr(w, "_pda_shared", False) and not getattr(b, "_pda_shared", False)
+        assert w.grad.data_ptr() == fg.grad_view(0).data_ptr()
+        assert b.grad.data_ptr() == fg.grad_view(1).data_ptr()
+    assert rel_err(w.grad, dy.float().t() @ x.float()) < 1e-2
+    assert rel_err(b.grad, dy.float().sum(0)) < 1e-2

@@ -161,3 +161,17 @@ def test_pipeline_checkpoint_roundtrip_and_consolidate(tmp_path, world, chunks):
         assert (tmp_path / f"ok{r}").read_text() == "ok"
     assert sorted(p.name for p in (tmp_path / "ckpt").iterdir()) == \
         ["pipeline.json"] + [f"stage_{s:03d}.pt" for s in range(world)]
+
+
+@pytest.mark.parametrize("find_unused", [False, True])
+def test_interleaved_ddp_unused_parameter_is_reported(tmp_path, find_unused):
+    """a chunk parameter that gets no gradient must not leave the multi-pass DDP step with
+    unlaunched buckets; Pipeline finalizes through DDP.finish_multi_pass after its last backward."""
+    import os
+
+    spawn(_workers.pipeline_interleaved_unused_worker, args=(1, find_unused, str(tmp_path)), nprocs=1, timeout=120)
+    out = torch.load(os.path.join(tmp_path, "0.pt"), weights_only=False)
+    if find_unused:
+        assert out["error"] is None and out["unused_grad_zero"] and out["pending"] == [0] and not out["open"]
+    else:
+        assert out["error"] is not None and "received no gradient" in out["error"]
