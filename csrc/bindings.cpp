@@ -462,6 +462,52 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::op
   return {dx, dres, dgamma, dbeta};
 }
 
+// BN backward from the sums a dgrad epilogue accumulated into `table` (conv_dgrad bst_*): finalize (re-zeroes
+// the table) + apply; y = the forward's ReLU bit mask (uint8) or None with ss = scale / shift
+std::vector<Tensor> bn_bwd_table(Tensor dy, Tensor x, c10::optional<Tensor> bits, c10::optional<Tensor> ss,
+                                 Tensor mean, Tensor invstd, c10::optional<Tensor> gamma, bool relu, bool want_dres,
+                                 Tensor table, c10::optional<Tensor> dgamma_out, c10::optional<Tensor> dbeta_out) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  TORCH_CHECK(dy.sizes() == x.sizes());
+  const int64_t C = x.size(-1), M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0 && C <= 2048, "channels must be a multiple of 8 and <= 2048");
+  check_f32(table, "table");
+  TORCH_CHECK(table.dim() == 3 && table.size(1) == 2 && table.size(2) == C && table.is_contiguous());
+  if (relu) {
+    TORCH_CHECK(bits.has_value() || ss.has_value(), "relu backward needs the bit mask or scale/shift");
+    if (bits.has_value()) {
+      check_gpu(*bits, "bits");
+      TORCH_CHECK(bits->scalar_type() == at::kByte && bits->is_contiguous() && bits->numel() * 8 == x.numel());
+    } else {
+      check_f32(*ss, "ss");
+      TORCH_CHECK(ss->numel() == 2 * C);
+    }
+  }
+  check_f32(mean, "mean");
+  check_f32(invstd, "invstd");
+  const float* gf;
+  const pda::bf16_t* gb;
+  bn_param_ptrs(gamma, &gf, &gb, C);
+  c10::DeviceGuard g(x.device());
+  Tensor dx = at::empty_like(x);
+  Tensor dres = want_dres ? at::empty_like(x) : Tensor();
+  const auto pdt = gamma.has_value() ? gamma->scalar_type() : at::kFloat;
+  Tensor dgamma = dgamma_out.has_value() ? *dgamma_out : at::empty({C}, x.options().dtype(pdt));
+  Tensor dbeta = dbeta_out.has_value() ? *dbeta_out : at::empty({C}, x.options().dtype(pdt));
+  TORCH_CHECK(dgamma.numel() == C && dbeta.numel() == C && dgamma.scalar_type() == pdt && dbeta.scalar_type() == pdt);
+  const bool pb = pdt == at::kBFloat16;
+  Tensor coef = at::empty({3 * C}, x.options().dtype(at::kFloat));
+  CHECK_HIP_OK(pda::bn_bwd_table(bp(dy), bp(x), (relu && bits.has_value()) ? bits->data_ptr<uint8_t>() : nullptr,
+                                 (relu && !bits.has_value()) ? ss->data_ptr<float>() : nullptr, M, C,
+                                 mean.data_ptr<float>(), invstd.data_ptr<float>(), gf, gb, relu, bpm(dx),
+                                 want_dres ? bpm(dres) : nullptr, pb ? nullptr : dgamma.data_ptr<float>(),
+                                 pb ? bpm(dgamma) : nullptr, pb ? nullptr : dbeta.data_ptr<float>(),
+                                 pb ? bpm(dbeta) : nullptr, table.data_ptr<float>(), (int)table.size(0),
+                                 coef.data_ptr<float>(), stream_of(x)));
+  return {dx, dres, dgamma, dbeta};
+}
+
 // ------------------------------------------------------------------ pooling (NHWC)
 std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t pad) {
   check_bf16(x, "x");
@@ -768,8 +814,13 @@ Tensor conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t d
 }
 
 // addend_bits: optional ReLU bit mask of the addend (numel/8 bytes): dx = dgrad + addend * mask
+// bst_*: the BN-backward statistics of dx accumulated in the epilogue (pda::BnBwdStats): z = the BN's input
+// (dx's shape), ss = its [2][C] scale / shift (ReLU mask recomputed) or bits = its forward ReLU bit mask,
+// mean = its saved batch mean, table = [R][2][C] fp32 zero on entry (bn_bwd_table re-zeroes it)
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad, int64_t dil,
-                  c10::optional<Tensor> addend, c10::optional<Tensor> addend_bits, bool out_f32) {
+                  c10::optional<Tensor> addend, c10::optional<Tensor> addend_bits, bool out_f32,
+                  c10::optional<Tensor> bst_z, c10::optional<Tensor> bst_ss, c10::optional<Tensor> bst_bits,
+                  c10::optional<Tensor> bst_mean, c10::optional<Tensor> bst_table) {
   check_bf16(dy, "dy");
   check_bf16(w, "w");
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), Cout = dy.size(3);
@@ -795,9 +846,38 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
                     addend_bits->numel() * 8 == dx.numel(),
                 "addend_bits must be numel/8 contiguous bytes");
   }
+  pda::BnBwdStats bst{};
+  const bool want_bst = bst_z.has_value();
+  if (want_bst) {
+    TORCH_CHECK(!out_f32 && !(addend.has_value() && stride > 1),
+                "conv_dgrad: BN-backward statistics need a bf16 dx (and no addend on a strided dgrad)");
+    check_bf16(*bst_z, "bst_z");
+    TORCH_CHECK(bst_z->sizes() == dx.sizes() && bst_z->is_contiguous(), "bst_z must have dx's shape");
+    TORCH_CHECK(bst_mean.has_value() && bst_table.has_value(), "bst_z needs bst_mean and bst_table");
+    check_f32(*bst_mean, "bst_mean");
+    check_f32(*bst_table, "bst_table");
+    TORCH_CHECK(bst_mean->numel() == C && bst_table->dim() == 3 && bst_table->size(1) == 2 && bst_table->size(2) == C &&
+                    bst_table->is_contiguous(),
+                "bst_table must be a contiguous [R, 2, C] fp32 table");
+    TORCH_CHECK(bst_ss.has_value() != bst_bits.has_value(), "exactly one of bst_ss / bst_bits");
+    bst.z = bp(*bst_z);
+    bst.mean = bst_mean->data_ptr<float>();
+    bst.table = bst_table->data_ptr<float>();
+    bst.rows = (int)bst_table->size(0);
+    if (bst_ss.has_value()) {
+      check_f32(*bst_ss, "bst_ss");
+      TORCH_CHECK(bst_ss->numel() == 2 * C);
+      bst.ss = bst_ss->data_ptr<float>();
+    } else {
+      check_gpu(*bst_bits, "bst_bits");
+      TORCH_CHECK(bst_bits->scalar_type() == at::kByte && bst_bits->is_contiguous() && bst_bits->numel() * 8 == dx.numel());
+      bst.bits = bst_bits->data_ptr<uint8_t>();
+    }
+  }
   CHECK_HIP_OK(pda::conv2d_dgrad(bp(dy), bp(w), wt.defined() ? bp(wt) : nullptr, dx.data_ptr(), out_f32, N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
                                  addend.has_value() ? bp(*addend) : nullptr,
-                                 addend_bits.has_value() ? addend_bits->data_ptr<uint8_t>() : nullptr, stream_of(dy)));
+                                 addend_bits.has_value() ? addend_bits->data_ptr<uint8_t>() : nullptr, stream_of(dy),
+                                 want_bst ? &bst : nullptr));
   return dx;
 }
 
@@ -1588,6 +1668,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd_train", &bn_fwd_train);
   m.def("bn_fwd_eval", &bn_fwd_eval);
   m.def("bn_bwd", &bn_bwd);
+  m.def("bn_bwd_table", &bn_bwd_table);
   m.def("set_bn_bwd_fused_max_c", &set_bn_bwd_fused_max_c);
   m.def("bn_bwd_fused_max_c", []() { return bn_bwd_fused_max_c(); });
   m.def("maxpool_fwd", &maxpool_fwd);
@@ -1627,7 +1708,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_dual_ok", &bn_bwd_dual_ok);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"),
         py::arg("pad"), py::arg("dil"), py::arg("addend") = py::none(), py::arg("addend_bits") = py::none(),
-        py::arg("out_f32") = false);
+        py::arg("out_f32") = false, py::arg("bst_z") = py::none(), py::arg("bst_ss") = py::none(),
+        py::arg("bst_bits") = py::none(), py::arg("bst_mean") = py::none(), py::arg("bst_table") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);

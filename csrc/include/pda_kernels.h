@@ -160,6 +160,12 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint
                   bool relu, bf16_t* dx, bf16_t* dres, float* dgamma_f, bf16_t* dgamma_b, float* dbeta_f,
                   bf16_t* dbeta_b, float* ws, float* fin_table, unsigned* fin_ticket, int fin_rows,
                   hipStream_t st);
+// BN backward whose reduction sums were accumulated by the producing dgrad's epilogue (BnBwdStats): a
+// finalize from `table` ([rows][2][C], re-zeroed) and the apply pass; no reduce pass over dy and x
+hipError_t bn_bwd_table(const bf16_t* dy, const bf16_t* x, const uint8_t* relu_bits, const float* ss, int64_t M,
+                        int64_t C, const float* save_mean, const float* save_invstd, const float* gamma_f,
+                        const bf16_t* gamma_b, bool relu, bf16_t* dx, bf16_t* dres, float* dgamma_f, bf16_t* dgamma_b,
+                        float* dbeta_f, bf16_t* dbeta_b, float* table, int rows, float* coef, hipStream_t st);
 // fused finalize (fin_table != nullptr): the reduce kernel's last block finalizes in-launch from a
 // persistent zeroed [fin_rows][2][C] table + ticket (left zero); rows for C channels:
 int bn_bwd_table_rows(int64_t C);
@@ -215,9 +221,21 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int
 bool conv_dgrad_needs_wt(int R, int S, int stride, int pad);
 // 1x1 stride-1 dgrads that read a transposed weight wt[C][Cout] (K-major) instead (MFMA-heavy shapes)
 bool conv_dgrad_1x1_wt(int R, int S, int stride, int pad, int C, int Cout);
+// BatchNorm-backward statistics fused into the dgrad epilogue (bst, optional): dx is the dy of the BN whose
+// ReLU output the conv consumed; the epilogues add sum(g) and sum(g (z - mean)), g = dx * relu_mask(z),
+// into table[tile % rows][2][C] (zero on entry; bn_bwd_table reads and re-zeroes it).  Mask from
+// ss = [2][C] scale / shift or from the forward's bit mask.  Not with an fp32 dx or an addend.
+struct BnBwdStats {
+  const bf16_t* z;
+  const float* ss;
+  const uint8_t* bits;
+  const float* mean;
+  float* table;
+  int rows;
+};
 hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, void* dx, bool dx_f32, int N, int H, int W,
                         int C, int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,
-                        const uint8_t* addend_bits, hipStream_t st);
+                        const uint8_t* addend_bits, hipStream_t st, const BnBwdStats* bst = nullptr);
 hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32, int N, int H, int W, int C,
                         int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, float* slab,
                         hipStream_t st);

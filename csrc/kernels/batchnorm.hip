@@ -703,7 +703,9 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_reduce_dual_kernel(
   block_col_reduce_store(sa2, sb2, tx, ty, cols, rpi, vcol, C, slab2, slab2 + (int64_t)gridDim.x * C);
 }
 
-// dgamma = invstd * sum(dz (x-mean)), dbeta = sum(dz);  coefficients for dx = A*dz + B*x + Cc
+// dgamma = invstd * sum(dz (x-mean)), dbeta = sum(dz);  coefficients for dx = A*dz + B*x + Cc.
+// TABLE: the sums come from a dgrad epilogue's [nrb][2][C] table (gemm_epi.h bst_*), re-zeroed here.
+template <bool TABLE = false>
 __global__ void __launch_bounds__(kFinThreads) bn_bwd_finalize_kernel(
     float* __restrict__ slab, int nrb, int64_t M, int C, const float* __restrict__ mean,
     const float* __restrict__ invstd, const float* __restrict__ gamma_f, const bf16_t* __restrict__ gamma_b,
@@ -711,7 +713,8 @@ __global__ void __launch_bounds__(kFinThreads) bn_bwd_finalize_kernel(
     bf16_t* __restrict__ dbeta_b, float* __restrict__ coef) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   float sdz, sdx;
-  slab_sum(slab, slab + (int64_t)nrb * C, nrb, C, C, c, sdz, sdx);
+  if (TABLE) slab_sum<true>(slab, slab + C, nrb, 2 * (int64_t)C, C, c, sdz, sdx);
+  else slab_sum(slab, slab + (int64_t)nrb * C, nrb, C, C, c, sdz, sdx);
   if (threadIdx.x >= 64 || c >= C) return;
   const float is = invstd[c], mu = mean[c];
   const float g = param_at(gamma_f, gamma_b, c, 1.f);
@@ -1187,6 +1190,9 @@ hipError_t bn_fwd_eval(const bf16_t* x, const bf16_t* res, bf16_t* y, int64_t M,
   return launch_apply(x, res, y, M, (int)C, scale, shift, relu, nullptr, st);
 }
 
+hipError_t bwd_apply(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* ss, int64_t M, int64_t C,
+                     const float* coef, bf16_t* dx, bf16_t* dres, int mask, hipStream_t st);
+
 hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint8_t* relu_bits, const float* ss,
                   int64_t M, int64_t C,
                   const float* save_mean, const float* save_invstd, const float* gamma_f, const bf16_t* gamma_b,
@@ -1220,11 +1226,17 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint
 #undef BWD_REDUCE
   PDA_CHECK_HIP(hipGetLastError());
   if (!fused) {
-    bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(ws, g.nrb, M, (int)C, save_mean,
+    bn_bwd_finalize_kernel<false><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(ws, g.nrb, M, (int)C, save_mean,
                                                                            save_invstd, gamma_f, gamma_b, dgamma_f,
                                                                            dgamma_b, dbeta_f, dbeta_b, coef);
     PDA_CHECK_HIP(hipGetLastError());
   }
+  return bwd_apply(dy, x, y, ss, M, C, coef, dx, dres, mask, st);
+}
+
+// the BN backward apply pass: dx = A dz + B x + Cc (dz = dy * ReLU mask), optionally dres = dz
+hipError_t bwd_apply(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const float* ss, int64_t M, int64_t C,
+                     const float* coef, bf16_t* dx, bf16_t* dres, int mask, hipStream_t st) {
   int ns = lds_tables_forced() ? 0 : wave_sets((int)(C / 8));
   if (ns == 3 || ns > 4) ns = 0;
   const int grid = ns ? wave_grid(M * C / 8) : ew_grid(M * C / 8);
@@ -1242,6 +1254,20 @@ hipError_t bn_bwd(const bf16_t* dy, const bf16_t* x, const bf16_t* y, const uint
   else { if (dres) BWD_APPLY(3, true); else BWD_APPLY(3, false); }
 #undef BWD_APPLY
   return hipGetLastError();
+}
+
+hipError_t bn_bwd_table(const bf16_t* dy, const bf16_t* x, const uint8_t* relu_bits, const float* ss, int64_t M,
+                        int64_t C, const float* save_mean, const float* save_invstd, const float* gamma_f,
+                        const bf16_t* gamma_b, bool relu, bf16_t* dx, bf16_t* dres, float* dgamma_f, bf16_t* dgamma_b,
+                        float* dbeta_f, bf16_t* dbeta_b, float* table, int rows, float* coef, hipStream_t st) {
+  if (C > kMaxC || C % 8 || rows < 1 || !table) return hipErrorInvalidValue;
+  if (relu && !ss && !relu_bits) return hipErrorInvalidValue;
+  bn_bwd_finalize_kernel<true><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
+      table, rows, M, (int)C, save_mean, save_invstd, gamma_f, gamma_b, dgamma_f, dgamma_b, dbeta_f, dbeta_b, coef);
+  PDA_CHECK_HIP(hipGetLastError());
+  const int mask = !relu ? 0 : (relu_bits ? 3 : 2);
+  const bf16_t* y = mask == 3 ? reinterpret_cast<const bf16_t*>(relu_bits) : nullptr;
+  return bwd_apply(dy, x, y, ss, M, C, coef, dx, dres, mask, st);
 }
 
 bool bn_bwd_dual_ok(int64_t C) {
@@ -1263,7 +1289,7 @@ hipError_t bn_bwd_dual(const bf16_t* dy, const uint8_t* relu_bits, int64_t M, in
   float* coefs[2] = {coef, coef2};
   for (int i = 0; i < 2; ++i) {
     const BnBwdSide& p = *sides[i];
-    bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
+    bn_bwd_finalize_kernel<false><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
         p.ws, g.nrb, M, (int)C, p.mean, p.invstd, p.gamma_f, p.gamma_b, p.dgamma_f, p.dgamma_b, p.dbeta_f, p.dbeta_b,
         coefs[i]);
     PDA_CHECK_HIP(hipGetLastError());
@@ -1295,7 +1321,7 @@ hipError_t stem_pool_bn_bwd(const bf16_t* dp, const uint8_t* idx, const bf16_t* 
   stem_pool_bn_bwd_kernel<0><<<kStemBlocks, kThreads, 0, st>>>(dp, idx, z, ss, mean, nullptr, N, H, W, C, P, Q, ws,
                                                               nullptr);
   PDA_CHECK_HIP(hipGetLastError());
-  bn_bwd_finalize_kernel<<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(ws, kStemBlocks, M, C, mean, invstd,
+  bn_bwd_finalize_kernel<false><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(ws, kStemBlocks, M, C, mean, invstd,
                                                                            gamma_f, gamma_b, dgamma_f, dgamma_b,
                                                                            dbeta_f, dbeta_b, coef);
   PDA_CHECK_HIP(hipGetLastError());

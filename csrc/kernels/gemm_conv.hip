@@ -574,13 +574,14 @@ __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 
   constexpr int CPR = BN / 8;
   static_assert(NT % CPR == 0, "a thread keeps one column chunk");
   // column chunk of this thread is fixed (NT % CPR == 0): BN statistics accumulate in registers
-  float kshift[8];
   const bool want_stats = epi.stats != nullptr;
-  {
-    const int64_t n = n0 + (tid % CPR) * 8;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) kshift[q] = (want_stats && n + q < N) ? epi.stats_shift[n + q] : 0.f;
-  }
+  EpiStatCols scol;
+  epi_stat_cols(epi, want_stats, n0 + (tid % CPR) * 8, N, scol);
+  if (epi.bst_z) {
+    epi_bst_chunks<BM, CPR, NT>(
+        epi, scol, [&](int r, int ch) { return *reinterpret_cast<const u16x8*>(stg + r * SROW + ch * 8); }, m0, n0,
+        M, N, st1, st2);
+  } else
 #pragma unroll
   for (int c = tid; c < BM * CPR; c += NT) {
     const int r = c / CPR, ch = c % CPR;
@@ -595,14 +596,7 @@ __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 
       for (int q = 0; q < 8; ++q) v[q] = f2bf(bf2f(v[q]) + a[q]);
     }
     if (epi.act) epi_act8(epi, crow, n, v);
-    if (want_stats) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float d = bf2f(v[q]) - kshift[q];
-        st1[q] += d;
-        st2[q] += d * d;
-      }
-    }
+    if (want_stats) epi_stats8(epi, scol, crow, n, v, st1, st2);
     *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
   }
   if (!DEFER && want_stats) {
@@ -1428,6 +1422,12 @@ __device__ __forceinline__ mfma_bf16x8 wide_frag(const char* half, int row, int 
 }
 
 // blockIdx.y = K split (ktiles_per_split K tiles each); split launches write fp32 slabs.
+// the wide kernel compiles the BN-backward statistics epilogue only for plain-operand launches (a dgrad
+// with statistics never takes a gathered wide tile: dispatch_bn routes it to the 128 tile)
+template <class L> struct WideBst : std::false_type {};
+template <int R> struct WideBst<PlainK<R>> : std::true_type {};
+template <int R> struct WideBst<PlainMN<R>> : std::true_type {};
+
 template <class LA, class LB, int VAR>
 __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K,
                                                            int tiles_n, int ktiles_per_split, Epi epi) {
@@ -1521,7 +1521,7 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
   }
   }
   __syncthreads();  // every wave is done with the operand stages before they become the staging tile
-  wide_tile_epilogue(acc, smem, W_STATS_OFF, epi, m0, n0, M, N, tm, blockIdx.y);
+  wide_tile_epilogue<4, WideBst<LA>::value && WideBst<LB>::value>(acc, smem, W_STATS_OFF, epi, m0, n0, M, N, tm, blockIdx.y);
 }
 
 // Split-K reduction: out[m, n] = act(sum_s slab[s, m, n] + bias[n]).  A workgroup is (256 / L) output
@@ -1975,7 +1975,8 @@ hipError_t dispatch_bn(int64_t M, int64_t N, int64_t K, const Plan& p, Epi epi, 
       }
     }
   }
-  if (use_wide(M, N, K, p, epi)) return launch_wide(make_a(TA<64>{}), make_b(TB<64>{}), M, N, K, epi, st);
+  if (use_wide(M, N, K, p, epi) && ((WideBst<TA<64>>::value && WideBst<TB<64>>::value) || !epi.bst_z))
+    return launch_wide(make_a(TA<64>{}), make_b(TB<64>{}), M, N, K, epi, st);
   if (slab) {
     const int ws = wide_splits(M, N, K, p, epi);
     if (ws > 0) return launch_wide(make_a(TA<64>{}), make_b(TB<64>{}), M, N, K, epi, st, ws, slab);
@@ -2379,17 +2380,35 @@ bool conv_dgrad_1x1_wt(int R, int S, int stride, int pad, int C, int Cout) {
 
 hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, void* dx, bool dx_f32, int N, int H, int W,
                         int C, int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,
-                        const uint8_t* addend_bits, hipStream_t st) {
+                        const uint8_t* addend_bits, hipStream_t st, const BnBwdStats* bst) {
   const int cf = dx_f32 ? 1 : 0;
+  // (a strided dgrad's fill-phase kernel writes the addend where no tap reaches: those elements would be
+  // missing from the sums, so the statistics take an addend only at stride 1)
+  if (bst && (dx_f32 || (addend && stride > 1) || !bst->z || !bst->mean || !bst->table || bst->rows < 1 ||
+              (!bst->ss && !bst->bits)))
+    return hipErrorInvalidValue;
+  // every Epi below starts from this one: bf16 dx, the optional addend and the optional BN-backward sums
+  auto base_epi = [&]() {
+    Epi e{dx, C, cf, nullptr, 0, 0, nullptr};
+    e.addend = addend;
+    e.addend_bits = addend_bits;
+    if (bst) {
+      e.stats = bst->table;
+      e.stats_shift = bst->mean;
+      e.stats_rows = bst->rows;
+      e.bst_z = bst->z;
+      e.bst_ss = bst->ss;
+      e.bst_bits = bst->bits;
+    }
+    return e;
+  };
   if (!conv_dgrad_needs_wt(R, S, stride, pad)) {
     // 1x1 stride 1: dx[NHW, C] = dy[NHW, Cout] * w[Cout, C] — dy rows are the K-major A operand and the
     // OHWI weight is already the MN-major B operand (k = co rows of C contiguous channels): no weight
     // transpose launch (36 of ResNet-50's 53 convs are 1x1, 32 of them stride 1)
     const int64_t M = (int64_t)N * H * W, Nn = C, K = Cout;
     Plan p = plan_gemm(M, Nn, K, false, 512);
-    Epi epi{dx, C, cf, nullptr, 0, 0, nullptr};
-    epi.addend = addend;
-    epi.addend_bits = addend_bits;
+    Epi epi = base_epi();
     auto mk_a = [&](auto t) { t.p = dy; t.rows = M; t.K = K; t.ld = Cout; return t; };
     if (wt) {  // conv_dgrad_1x1_wt: B(k = co, n = ci) = wt[ci][co], K-major
       auto mk_bt = [&](auto t) { t.p = wt; t.rows = Nn; t.K = K; t.ld = Cout; return t; };
@@ -2402,18 +2421,14 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
   if (!dgrad_phased(stride, dil)) {
     const int64_t M = (int64_t)N * H * W, Nn = C, K = (int64_t)R * S * Cout;
     Plan p = plan_gemm(M, Nn, K, false, 512);
-    Epi epi{dx, C, cf, nullptr, 0, 0, nullptr};
-    epi.addend = addend;
-    epi.addend_bits = addend_bits;
+    Epi epi = base_epi();
     auto mk_a = [&](auto t) { t.dy = dy; t.g = g; t.M = M; t.K = K; return t; };
     auto mk_b = [&](auto t) { t.p = wt; t.rows = Nn; t.K = K; t.ld = K; return t; };
     return dispatch_bn<ConvDgradK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_a, mk_b);
   }
   if (stride == 1) {
     // stride-1 dgrad = the 3x3 conv of dy with the rotated transposed weights (halo path)
-    Epi epi{dx, C, cf, nullptr, 0, 0, nullptr};
-    epi.addend = addend;
-    epi.addend_bits = addend_bits;
+    Epi epi = base_epi();
     if (use_halo(H, W, Cout, C, R, S, stride, pad, dil, epi)) return launch_halo(dy, wt, N, H, W, Cout, C, true, epi, st);
   }
   const int nph = stride;  // phases per dim (1 for stride 1)
@@ -2443,9 +2458,7 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
       }
       const bf16_t* wph = wt + ((int64_t)a.cum * S + (int64_t)a.n * b.cum) * C * Cout;
       Plan p = plan_gemm(M, Nn, K, false, 512);
-      Epi epi{dx, C, cf, nullptr, 0, 0, nullptr};
-      epi.addend = addend;
-      epi.addend_bits = addend_bits;
+      Epi epi = base_epi();
       if (stride > 1) {
         epi.rm_on = 1; epi.rm_Hh = Hh; epi.rm_Wh = Wh; epi.rm_st = stride; epi.rm_ph = ph; epi.rm_pw = pw;
         epi.rm_H = H; epi.rm_W = W;

@@ -1165,7 +1165,7 @@ __global__ void __launch_bounds__(P4_NT) gemm_pp4_kernel(PPArgs p) {
   asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");  // last MFMA's result -> the epilogue's accumulator reads
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
-  wide_tile_epilogue<2>(acc, smem, P4_STATS_OFF, p.epi, m0, n0, p.M, p.N, tm, blockIdx.y);
+  wide_tile_epilogue<2, false>(acc, smem, P4_STATS_OFF, p.epi, m0, n0, p.M, p.N, tm, blockIdx.y);  // (lab: no BN-bwd sums)
 }
 
 template <bool AK, bool BK>
@@ -1319,7 +1319,8 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
   if ((a_kmajor && 257 * lda * 2 >= ((int64_t)1 << 31)) || (b_kmajor && 257 * ldb * 2 >= ((int64_t)1 << 31)))
     return hipErrorInvalidValue;
   if (used_splits) *used_splits = splits;
-  if (splits == 1 && variant < 0 && pp_persist_mode()) {
+  // (the persistent walk's banded epilogue has no BN-backward statistics path)
+  if (splits == 1 && variant < 0 && pp_persist_mode() && !epi.bst_z) {
     const hipError_t r = gemm_pp_persistent(A, a_kmajor, lda, B, b_kmajor, ldb, M, N, K, epi, st);
     if (r != hipErrorInvalidValue) return r;
   }
@@ -1329,7 +1330,7 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
   a.epi.nt_store = pp_epi_nt();
   if (splits <= 1) a.epi.slab = nullptr;
   const int var = variant < 0 ? pp_default_variant() : variant;
-  if (var == 200 && !epi.rowsum) {
+  if (var == 200 && !epi.rowsum && !epi.bst_z) {
     if (a_kmajor && b_kmajor) return launch_pp4<true, true>(a, splits, st);
     if (a_kmajor) return launch_pp4<true, false>(a, splits, st);
     if (b_kmajor) return launch_pp4<false, true>(a, splits, st);
@@ -1413,6 +1414,7 @@ hipError_t gemm_pp_lab(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t
   epi.C = C;
   epi.ldc = ldc;
   epi.bias = bias;
+  if (variant == 100 && epi.bst_z) return hipErrorInvalidValue;
   if (variant == 100) return gemm_pp_persistent(A, a_kmajor, lda, B, b_kmajor, ldb, M, N, K, epi, st);
   return gemm_pp(A, a_kmajor, lda, B, b_kmajor, ldb, M, N, K, epi, 1, variant, st, nullptr);
 }

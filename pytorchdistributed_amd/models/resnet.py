@@ -51,8 +51,10 @@ class Bottleneck(tnn.Module):
         # Every conv also reduces the batch statistics of the BN it feeds in its epilogue (bn=...).
         join = (GradJoin(2) if (x.is_cuda and x.dtype == torch.bfloat16 and x.requires_grad and torch.is_grad_enabled())
                 else None)
-        out = self.bn1(self.conv1(x, grad_join=join, bn=self.bn1), relu=True)
-        out = self.bn2(self.conv2(out, bn=self.bn2), relu=True)
+        # bn1 / bn2 outputs feed exactly one conv each: their backward reductions run in conv2's / conv3's
+        # dgrad epilogues (fuse_bwd_stats); bn3's output feeds the next block's gradient join
+        out = self.bn1(self.conv1(x, grad_join=join, bn=self.bn1), relu=True, fuse_bwd_stats=True)
+        out = self.bn2(self.conv2(out, bn=self.bn2), relu=True, fuse_bwd_stats=True)
         if self.downsample is not None:
             conv_ds, bn_ds = self.downsample
             zd = conv_ds(x, grad_join=join, bn=bn_ds)
@@ -63,12 +65,16 @@ class Bottleneck(tnn.Module):
                 # are never stored (PDA_DUAL_BN=0: the separate shortcut BN apply)
                 return ops.batch_norm_dual(z3[0], self.bn3, zd[0], bn_ds, z3[1], zd[1])
             return self.bn3(z3, residual=bn_ds(zd), relu=True)
-        return self.bn3(self.conv3(out, bn=self.bn3), residual=x, relu=True, residual_join=join)
+        return self.bn3(self.conv3(out, bn=self.bn3), residual=x, relu=True, residual_join=join,
+                        fuse_bwd_stats=_BN3_BWD_JOIN)
 
 
 _STEM_S2D = os.environ.get("PDA_STEM_S2D", "1") == "1"
 _DUAL_BN = os.environ.get("PDA_DUAL_BN", "1") == "1"
 _STEM_BN_POOL = os.environ.get("PDA_STEM_BN_POOL", "1") == "1"
+# an identity block's output BN: its backward sums from the next block's conv1 dgrad (the gradient join's
+# last contributor, whose epilogue adds the shortcut gradient) — PDA_BN3_BWD_JOIN=0: the reduce pass
+_BN3_BWD_JOIN = os.environ.get("PDA_BN3_BWD_JOIN", "1") == "1"
 
 
 def space_to_depth_stem(x: torch.Tensor, w: torch.Tensor):

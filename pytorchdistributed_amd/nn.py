@@ -109,6 +109,20 @@ class BatchNorm2d(tnn.Module):
             self._stat_table = t
         return t
 
+    def bwd_table(self, device):
+        """(table, token) for the backward reduction fused into the consuming conv's dgrad epilogue
+        (ops/grad_join.py:BnBwdStats): a zeroed [R, 2, C] fp32 table the epilogue accumulates into and the BN
+        backward finalize re-zeroes, and the [filled] flag; a table some dgrad filled without a BN backward
+        consuming it (aborted backward) is re-zeroed here before it is handed out again."""
+        t = getattr(self, "_bwd_table", None)
+        if t is None or t.device != torch.device(device):
+            t = torch.zeros(_STAT_ROWS, 2, self.num_features, device=device)
+            self._bwd_table, self._bwd_token = t, [False]
+        elif self._bwd_token[0]:
+            t.zero_()
+            self._bwd_token[0] = False
+        return t, self._bwd_token
+
     def _apply(self, fn, recurse=True):
         # keep running stats in fp32 when the module is cast to bf16
         rm, rv = self.running_mean, self.running_var
@@ -118,12 +132,17 @@ class BatchNorm2d(tnn.Module):
             self.running_var = fn(rv).float()
         return self
 
-    def forward(self, x, residual=None, relu=False, residual_join=None, stats=None):
+    def forward(self, x, residual=None, relu=False, residual_join=None, stats=None, fuse_bwd_stats=False):
+        """``fuse_bwd_stats``: the output's consumers are known to be one conv (or, with a residual, the next
+        block's gradient join): that conv's dgrad epilogue then reduces this BN's backward sums."""
         if isinstance(x, tuple):  # (y, stats) from Conv2d(..., bn=self)
             x, stats = x
+        bt = None
+        if fuse_bwd_stats and self.training and x.is_cuda and x.dtype == torch.bfloat16 and relu:
+            bt = self.bwd_table(x.device)
         return ops.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
                               self.momentum, self.eps, residual=residual, relu=relu, residual_join=residual_join,
-                              stats=stats, num_batches_tracked=self.num_batches_tracked)
+                              stats=stats, num_batches_tracked=self.num_batches_tracked, bwd_table=bt)
 
 
 class ReLU(tnn.Module):

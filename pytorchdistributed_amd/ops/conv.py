@@ -30,7 +30,7 @@ def _ref_conv(x, w, stride, padding, dilation, bias=None):
 
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, bias, stride, padding, dilation, relu, join):
+    def forward(ctx, x, w, bias, stride, padding, dilation, relu, join, bnb=None):
         x = x.contiguous()
         w = w.contiguous()
         y = C().conv_fwd(x, w, stride, padding, dilation, bias, relu)
@@ -38,6 +38,7 @@ class _Conv2dFn(torch.autograd.Function):
         ctx.cfg = (stride, padding, dilation, relu, bias is not None)
         ctx.wparam = w
         ctx.join = join
+        ctx.bnb = bnb
         return y
 
     @staticmethod
@@ -57,11 +58,22 @@ class _Conv2dFn(torch.autograd.Function):
             if join is not None and not join.is_last():
                 join.stash(C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation, None))
             else:
+                # the BN that produced x: its backward sums come out of this dgrad's epilogue (its dy = dx);
+                # with a join, only as its last contributor (checked before take() resets the join)
+                bnb = getattr(ctx, "bnb", None)
+                join_last = join is not None and join.is_last()
                 addend = join.take() if join is not None else None
                 bits = None
                 if isinstance(addend, MaskedGrad):  # residual gradient = dz * ReLU mask, applied in the epilogue
                     addend, bits = addend.grad, addend.bits
-                dx = C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation, addend, bits)
+                kw = {}
+                if bnb is not None and bnb.usable(join_last, join is not None, stride, addend) and \
+                        bnb.z.shape == x.shape:
+                    kw = bnb.dgrad_kwargs()
+                dx = C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation, addend, bits, **kw)
+                if kw:
+                    bnb.filled = True
+        ctx.bnb = None
         if ctx.needs_input_grad[1]:
             target = grad_target(ctx.wparam)
             args = (dy, x, w.shape[1], w.shape[2], stride, padding, dilation, w.dtype == torch.float32, target)
@@ -76,7 +88,7 @@ class _Conv2dFn(torch.autograd.Function):
                 dw = C().conv_wgrad(*args)
         if has_bias and ctx.needs_input_grad[2]:
             db = dy.reshape(-1, dy.shape[-1]).sum(0, dtype=torch.float32).to(dy.dtype)
-        return dx, dw, db, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 class _Conv2dStatsFn(torch.autograd.Function):
@@ -86,7 +98,7 @@ class _Conv2dStatsFn(torch.autograd.Function):
     the plain conv backward."""
 
     @staticmethod
-    def forward(ctx, x, w, stride, padding, dilation, shift, table, join):
+    def forward(ctx, x, w, stride, padding, dilation, shift, table, join, bnb=None):
         x = x.contiguous()
         w = w.contiguous()
         y = C().conv_fwd_stats(x, w, stride, padding, dilation, shift, table)
@@ -94,12 +106,13 @@ class _Conv2dStatsFn(torch.autograd.Function):
         ctx.cfg = (stride, padding, dilation, False, False)
         ctx.wparam = w
         ctx.join = join
+        ctx.bnb = bnb
         return y
 
     @staticmethod
     def backward(ctx, dy):
         dx, dw, _db, *_ = _Conv2dFn._backward(ctx, dy)
-        return dx, dw, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None
 
 
 def conv2d_bn_stats(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padding: int = 0, dilation: int = 1,
@@ -108,7 +121,8 @@ def conv2d_bn_stats(x: torch.Tensor, weight: torch.Tensor, stride: int = 1, padd
     ``table`` ([R, 2, C_out] fp32, zero on entry; the consuming BN finalize re-zeroes it)."""
     if weight.shape[-1] != x.shape[-1]:
         weight = F.pad(weight, (0, x.shape[-1] - weight.shape[-1]))
-    return _Conv2dStatsFn.apply(x, weight, stride, padding, dilation, shift, table, grad_join)
+    return _Conv2dStatsFn.apply(x, weight, stride, padding, dilation, shift, table, grad_join,
+                                getattr(x, "_pda_bnb", None))
 
 
 def conv2d(x: torch.Tensor, weight: torch.Tensor, bias=None, stride: int = 1, padding: int = 0, dilation: int = 1,
@@ -123,7 +137,8 @@ def conv2d(x: torch.Tensor, weight: torch.Tensor, bias=None, stride: int = 1, pa
             from . import fp32
 
             return fp32.conv2d(x, weight, bias, stride, padding, dilation, relu)
-        return _Conv2dFn.apply(x, weight, bias, stride, padding, dilation, relu, grad_join)
+        return _Conv2dFn.apply(x, weight, bias, stride, padding, dilation, relu, grad_join,
+                               getattr(x, "_pda_bnb", None))
     if weight.shape[-1] != x.shape[-1]:
         x = x[..., : weight.shape[-1]]
     y = _ref_conv(x, weight, stride, padding, dilation, bias)

@@ -70,3 +70,53 @@ class GradJoin:
         if p is None:
             return _dense(g)
         return _dense(p) if g is None else _dense(g) + _dense(p)
+
+
+class BnBwdStats:
+    """Hand-off of a BatchNorm's backward reduction to the data gradient of the conv that consumes the
+    BN's ReLU output.  The BN forward creates it and attaches it to its output tensor
+    (``y._pda_bnb``); the consuming conv picks it up in its forward, and in backward its dgrad epilogue
+    accumulates sum(g) and sum(g (z - mean)) with g = dx * relu_mask into ``table`` — dx IS the BN's dy —
+    and sets ``filled``.  The BN backward then finalizes from the table instead of re-reading dy and z
+    in a reduce pass.
+
+    ``needs_join``: the BN output has a second consumer (the residual shortcut), so its gradient is only
+    complete in the dgrad of the LAST consumer of the shared gradient join (the one whose epilogue adds
+    the other consumers' stashed gradients)."""
+
+    __slots__ = ("z", "ss", "bits", "mean", "table", "needs_join", "token")
+
+    def __init__(self, z, ss, bits, mean, table, needs_join: bool, token=None):
+        self.z, self.ss, self.bits, self.mean, self.table = z, ss, bits, mean, table
+        self.needs_join = needs_join
+        # [filled]: shared with the table's owner (BatchNorm2d), which re-zeroes a table a dgrad filled but
+        # no BN backward consumed (an aborted backward) before handing it out again
+        self.token = token if token is not None else [False]
+        self.token[0] = False
+
+    @property
+    def filled(self) -> bool:
+        return self.token[0]
+
+    @filled.setter
+    def filled(self, v: bool):
+        self.token[0] = bool(v)
+
+    def usable(self, join_last: bool, has_join: bool, stride: int, addend) -> bool:
+        """May the dgrad of a conv (the last contributor of its gradient join or not, stride, epilogue
+        addend) fill the table?"""
+        if self.z is None:
+            return False
+        if self.needs_join and not (has_join and join_last):
+            return False
+        # a strided dgrad writes the phases no tap reaches with a fill kernel: with an addend those
+        # elements are nonzero and would be missing from the sums
+        return stride == 1 or addend is None
+
+    def dgrad_kwargs(self) -> dict:
+        kw = dict(bst_z=self.z, bst_mean=self.mean, bst_table=self.table)
+        if self.bits is not None:
+            kw["bst_bits"] = self.bits
+        else:
+            kw["bst_ss"] = self.ss
+        return kw

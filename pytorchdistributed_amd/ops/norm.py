@@ -17,13 +17,13 @@ import torch.nn.functional as F
 
 from .._native import C
 from ..parallel.flat import grad_target
-from .grad_join import MaskedGrad
+from .grad_join import BnBwdStats, MaskedGrad
 
 
 class _BatchNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu, join,
-                table=None, shift=None, num_batches=None):
+                table=None, shift=None, num_batches=None, bwd_table=None):
         x = x.contiguous()
         if residual is not None:
             residual = residual.contiguous()
@@ -48,6 +48,12 @@ class _BatchNormFn(torch.autograd.Function):
         ctx.cfg = (relu, residual is not None, training)
         ctx.beta = beta
         ctx.join = join
+        # backward reduction handed to the consuming conv's dgrad epilogue (ops/grad_join.py:BnBwdStats):
+        # ReLU outputs only (the mask source: scale/shift or the residual path's bit mask)
+        ctx.bnb = None
+        if bwd_table is not None and training and relu and (bits is not None or ss is not None):
+            table_, token = bwd_table
+            ctx.bnb = BnBwdStats(x, ss if bits is None else None, bits, mean, table_, residual is not None, token)
         return y
 
     @staticmethod
@@ -65,8 +71,16 @@ class _BatchNormFn(torch.autograd.Function):
         # contributor): dres = dy * relu_mask is handed over as (dy, bits) and applied in that conv's
         # epilogue, so the backward apply kernel never stores it
         masked = has_res and ctx.join is not None and bits is not None and not ctx.join.is_last()
-        dx, dres, dgamma, dbeta = C().bn_bwd(dy, x, bits, ss, mean, invstd, gamma, relu, has_res and not masked, tg,
-                                             tb)
+        bnb = ctx.bnb
+        if bnb is not None and bnb.filled:
+            # the sums were accumulated by the dgrad that produced dy: finalize + apply only
+            bnb.filled = False
+            dx, dres, dgamma, dbeta = C().bn_bwd_table(dy, x, bits, ss if bits is None else None, mean, invstd, gamma,
+                                                       relu, has_res and not masked, bnb.table, tg, tb)
+        else:
+            dx, dres, dgamma, dbeta = C().bn_bwd(dy, x, bits, ss, mean, invstd, gamma, relu, has_res and not masked,
+                                                 tg, tb)
+        ctx.bnb = None
         dg = dgamma if gamma is not None and ctx.needs_input_grad[1] else None
         db = dbeta if ctx.needs_input_grad[2] else None
         if masked:
@@ -74,7 +88,7 @@ class _BatchNormFn(torch.autograd.Function):
             dres = None
         elif has_res and ctx.join is not None:
             dres = ctx.join.contribute(dres)  # usually stashed for the consumer conv's dgrad epilogue
-        return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None, None, None, None, None
+        return dx, dg, db, (dres if has_res else None), None, None, None, None, None, None, None, None, None, None, None
 
 
 def _param_targets(ctx, gamma, beta, ig, ib):
@@ -151,18 +165,30 @@ def _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, trainin
     return y.to(x.dtype)
 
 
+_BWD_EPILOGUE = os.environ.get("PDA_BN_BWD_EPILOGUE", "1") == "1"
+
+
 def batch_norm(x, gamma, beta, running_mean=None, running_var=None, training=True, momentum=0.1, eps=1e-5,
-               residual=None, relu=False, residual_join=None, stats=None, num_batches_tracked=None):
+               residual=None, relu=False, residual_join=None, stats=None, num_batches_tracked=None, bwd_table=None):
     """BatchNorm over the last (channel) dim of ``x`` (any leading dims), then ``+residual``, then ReLU.
     ``residual_join``: the residual's gradient is handed to the join instead of autograd's add.
     ``stats``: ``(table, shift)`` — the statistics table filled by :func:`~.conv.conv2d_bn_stats`
     (``BatchNorm2d.stat_table``; re-zeroed by the finalize) — skips the statistics pass.
     ``num_batches_tracked``: int64 counter incremented in training mode (inside the finalize kernel on
-    the native path, so it costs no launch of its own)."""
+    the native path, so it costs no launch of its own).
+    ``bwd_table``: (zeroed [R, 2, C] fp32 table, token) (``BatchNorm2d.bwd_table``) — the caller guarantees that the
+    output's only consumer is a conv (or, with a residual, the gradient join of the next block), whose
+    dgrad epilogue then reduces this BN's backward sums (``PDA_BN_BWD_EPILOGUE=0``: the reduce pass)."""
     if x.is_cuda and x.dtype == torch.bfloat16:
         table, shift = stats if stats is not None else (None, None)
-        return _BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
-                                  relu, residual_join, table, shift, num_batches_tracked if training else None)
+        bt = bwd_table if (_BWD_EPILOGUE and training and torch.is_grad_enabled()) else None
+        y = _BatchNormFn.apply(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps,
+                               relu, residual_join, table, shift, num_batches_tracked if training else None, bt)
+        if bt is not None and y.grad_fn is not None:
+            bnb = getattr(y.grad_fn, "bnb", None)
+            if bnb is not None:
+                y._pda_bnb = bnb
+        return y
     if x.is_cuda and x.dtype == torch.float32 and x.shape[-1] % 4 == 0 and residual_join is None:
         from . import fp32
 

@@ -288,3 +288,105 @@ def test_tied_embedding_side_stream_matches_single_stream():
     for a, b in zip(got, ref):
         assert rel_err(a, b) < 1e-2, rel_err(a, b)
 
+
+
+@pytest.mark.parametrize("case", [
+    # N, H, W, Cin(dx channels), Cout(dy channels), R, stride, pad, mask source, addend
+    (4, 14, 14, 64, 256, 1, 1, 0, "ss", False),      # 1x1 dgrad, MN-major weight read in place (128 tile)
+    (32, 28, 28, 256, 256, 1, 1, 0, "ss", False),    # 1x1 dgrad on a transposed weight (256 x 256 tile)
+    (8, 28, 28, 128, 128, 3, 1, 1, "ss", False),     # 3x3 stride-1 dgrad (halo kernel)
+    (32, 28, 28, 64, 64, 3, 1, 1, "ss", False),      # 3x3 stride-1, 64 channels
+    (8, 28, 28, 128, 128, 3, 2, 1, "ss", False),     # 3x3 stride-2: phase launches + fill phases
+    (32, 14, 14, 256, 1024, 1, 1, 0, "bits", True),  # next block's conv1: addend (shortcut) + bit mask
+    (4, 14, 14, 64, 256, 1, 1, 0, "bits", True),
+])
+def test_conv_dgrad_bn_bwd_stats(case):
+    """The dgrad epilogue's BN-backward sums (gemm_epi.h bst_*) equal fp32 sums over the dx the same
+    launch stored: sum(g) and sum(g (z - mean)), g = dx * relu_mask; dx itself is unchanged."""
+    from pytorchdistributed_amd._native import C
+
+    N, H, W, Cin, Cout, R, st, pad, src, with_add = case
+    P, Q = (H + 2 * pad - R) // st + 1, (W + 2 * pad - R) // st + 1
+    torch.manual_seed(0)
+    dev = "cuda"
+    dy = torch.randn(N, P, Q, Cout).to(dev, torch.bfloat16)
+    w = (torch.randn(Cout, R, R, Cin) * 0.05).to(dev, torch.bfloat16)
+    z = torch.randn(N, H, W, Cin).to(dev, torch.bfloat16)
+    mean = (torch.randn(Cin) * 0.1).to(dev)
+    addend = torch.randn(N, H, W, Cin).to(dev, torch.bfloat16) if with_add else None
+    table = torch.zeros(64, 2, Cin, device=dev)
+    kw = dict(bst_z=z, bst_mean=mean, bst_table=table)
+    if src == "ss":
+        scale, shift = torch.rand(Cin) + 0.5, torch.randn(Cin) * 0.2
+        kw["bst_ss"] = torch.cat([scale, shift]).to(dev)
+        keep = (z.float() * scale.to(dev) + shift.to(dev)) > 0
+    else:
+        bits = torch.randint(0, 256, (N * H * W * Cin // 8,), dtype=torch.uint8, device=dev)
+        kw["bst_bits"] = bits
+        shifts = torch.arange(8, device=dev, dtype=torch.uint8)
+        keep = ((bits.reshape(-1, 1) >> shifts) & 1).bool().reshape(z.shape)
+    dx = C().conv_dgrad(dy, w, H, W, st, pad, 1, addend, None, **kw)
+    dx_ref = C().conv_dgrad(dy, w, H, W, st, pad, 1, addend, None)
+    assert torch.equal(dx, dx_ref)
+    g = torch.where(keep, dx.float(), torch.zeros((), device=dev)).reshape(-1, Cin)
+    s1 = g.sum(0)
+    s2 = (g * (z.float().reshape(-1, Cin) - mean)).sum(0)
+    tab = table.sum(0)
+    scale1 = g.abs().sum(0) + 1e-3
+    scale2 = (g * (z.float().reshape(-1, Cin) - mean)).abs().sum(0) + 1e-3
+    assert ((tab[0] - s1).abs() / scale1).max().item() < 1e-4
+    assert ((tab[1] - s2).abs() / scale2).max().item() < 1e-4
+
+
+def test_bottleneck_bwd_stats_from_dgrad_epilogue(monkeypatch):
+    """Two identity bottlenecks: bn1 / bn2 of both blocks and the first block's output BN (through the
+    second block's conv1 gradient join) take their backward sums from the dgrad epilogues — every BN
+    backward but the last block's bn3 (whose output has no conv consumer) finalizes from a table.  The
+    gradients match the reduce-pass path and the fp32 CPU reference (to 1.5x plain bf16 rounding)."""
+    from pytorchdistributed_amd._native import C as _C
+    from pytorchdistributed_amd.models.resnet import resnet50
+    from pytorchdistributed_amd.ops import norm as _norm
+
+    torch.manual_seed(0)
+    ref = resnet50(dtype=torch.bfloat16)
+    pair_ref = torch.nn.Sequential(ref.layer1[1], ref.layer1[2]).float().train()
+    xin = torch.randn(8, 16, 16, 256).to(torch.bfloat16).float().requires_grad_()
+    out_r = pair_ref(xin)
+    dy = torch.randn_like(out_r).to(torch.bfloat16).float()
+    out_r.backward(dy)
+    pair_b16 = copy.deepcopy(pair_ref).to(torch.bfloat16)
+    xb = xin.detach().to(torch.bfloat16).requires_grad_()
+    pair_b16(xb).backward(dy.to(torch.bfloat16))
+
+    calls = {"table": 0, "reduce": 0}
+    mod = _C()
+    real_t, real_r = mod.bn_bwd_table, mod.bn_bwd
+
+    def t_(*a, **k):
+        calls["table"] += 1
+        return real_t(*a, **k)
+
+    def r_(*a, **k):
+        calls["reduce"] += 1
+        return real_r(*a, **k)
+
+    monkeypatch.setattr(mod, "bn_bwd_table", t_)
+    monkeypatch.setattr(mod, "bn_bwd", r_)
+    grads = {}
+    for fused in (True, False):
+        monkeypatch.setattr(_norm, "_BWD_EPILOGUE", fused)
+        calls.update(table=0, reduce=0)
+        pair_g = copy.deepcopy(pair_ref).to("cuda", torch.bfloat16)
+        xg = xin.detach().to("cuda", torch.bfloat16).requires_grad_()
+        pair_g(xg).backward(dy.to("cuda", torch.bfloat16))
+        torch.cuda.synchronize()
+        if fused:
+            assert calls == {"table": 5, "reduce": 1}, calls
+        else:
+            assert calls == {"table": 0, "reduce": 6}, calls
+        grads[fused] = [xg.grad.cpu()] + [p.grad.cpu() for p in pair_g.parameters()]
+    bound_x = max(2e-2, 1.5 * rel_err(xb.grad, xin.grad))
+    assert rel_err(grads[True][0], xin.grad) < bound_x
+    for (n, pr), pb, gf, gu in zip(pair_ref.named_parameters(), pair_b16.parameters(), grads[True][1:], grads[False][1:]):
+        assert rel_err(gf, pr.grad) < max(2e-2, 1.5 * rel_err(pb.grad, pr.grad)), n
+        assert rel_err(gf, gu) < 1e-2, n
