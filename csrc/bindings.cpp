@@ -315,7 +315,8 @@ std::vector<Tensor> bn_bwd_dual(Tensor dy, Tensor bits, Tensor x, Tensor mean, T
                                 c10::optional<Tensor> gamma, Tensor x2, Tensor mean2, Tensor invstd2,
                                 c10::optional<Tensor> gamma2, c10::optional<Tensor> dgamma_out,
                                 c10::optional<Tensor> dbeta_out, c10::optional<Tensor> dgamma2_out,
-                                c10::optional<Tensor> dbeta2_out) {
+                                c10::optional<Tensor> dbeta2_out, c10::optional<Tensor> table,
+                                c10::optional<Tensor> table2) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   check_bf16(x2, "x2");
@@ -329,8 +330,16 @@ std::vector<Tensor> bn_bwd_dual(Tensor dy, Tensor bits, Tensor x, Tensor mean, T
   Tensor xs[2] = {x, x2}, means[2] = {mean, mean2}, invs[2] = {invstd, invstd2};
   c10::optional<Tensor> gam[2] = {gamma, gamma2}, dgo[2] = {dgamma_out, dgamma2_out}, dbo[2] = {dbeta_out, dbeta2_out};
   Tensor dxs[2], dgs[2], dbs[2], wss[2];
-  pda::BnBwdSide side[2];
+  pda::BnBwdSide side[2] = {};
+  TORCH_CHECK(table.has_value() == table2.has_value(), "bn_bwd_dual: both tables or none");
+  c10::optional<Tensor> tabs[2] = {table, table2};
   for (int i = 0; i < 2; ++i) {
+    if (tabs[i].has_value()) {
+      check_f32(*tabs[i], "table");
+      TORCH_CHECK(tabs[i]->dim() == 3 && tabs[i]->size(1) == 2 && tabs[i]->size(2) == C && tabs[i]->is_contiguous());
+      side[i].table = tabs[i]->data_ptr<float>();
+      side[i].rows = (int)tabs[i]->size(0);
+    }
     check_f32(means[i], "mean");
     check_f32(invs[i], "invstd");
     bn_param_ptrs(gam[i], &side[i].gamma_f, &side[i].gamma_b, C);
@@ -820,7 +829,8 @@ Tensor conv_fwd_stats(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t d
 Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int64_t pad, int64_t dil,
                   c10::optional<Tensor> addend, c10::optional<Tensor> addend_bits, bool out_f32,
                   c10::optional<Tensor> bst_z, c10::optional<Tensor> bst_ss, c10::optional<Tensor> bst_bits,
-                  c10::optional<Tensor> bst_mean, c10::optional<Tensor> bst_table) {
+                  c10::optional<Tensor> bst_mean, c10::optional<Tensor> bst_table, c10::optional<Tensor> bst_z2,
+                  c10::optional<Tensor> bst_mean2, c10::optional<Tensor> bst_table2) {
   check_bf16(dy, "dy");
   check_bf16(w, "w");
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), Cout = dy.size(3);
@@ -872,6 +882,17 @@ Tensor conv_dgrad(Tensor dy, Tensor w, int64_t H, int64_t W, int64_t stride, int
       check_gpu(*bst_bits, "bst_bits");
       TORCH_CHECK(bst_bits->scalar_type() == at::kByte && bst_bits->is_contiguous() && bst_bits->numel() * 8 == dx.numel());
       bst.bits = bst_bits->data_ptr<uint8_t>();
+    }
+    if (bst_z2.has_value()) {
+      check_bf16(*bst_z2, "bst_z2");
+      TORCH_CHECK(bst_z2->sizes() == dx.sizes() && bst_z2->is_contiguous(), "bst_z2 must have dx's shape");
+      TORCH_CHECK(bst_mean2.has_value() && bst_table2.has_value(), "bst_z2 needs bst_mean2 and bst_table2");
+      check_f32(*bst_mean2, "bst_mean2");
+      check_f32(*bst_table2, "bst_table2");
+      TORCH_CHECK(bst_mean2->numel() == C && bst_table2->sizes() == bst_table->sizes() && bst_table2->is_contiguous());
+      bst.z2 = bp(*bst_z2);
+      bst.mean2 = bst_mean2->data_ptr<float>();
+      bst.table2 = bst_table2->data_ptr<float>();
     }
   }
   CHECK_HIP_OK(pda::conv2d_dgrad(bp(dy), bp(w), wt.defined() ? bp(wt) : nullptr, dx.data_ptr(), out_f32, N, H, W, C, Cout, R, S, P, Q, stride, pad, dil,
@@ -1704,12 +1725,16 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd_train_sums", &bn_fwd_train_sums);
   m.def("bn_fwd_train_sums_dual", &bn_fwd_train_sums_dual);
   m.def("bn_dual_ok", &bn_dual_ok);
-  m.def("bn_bwd_dual", &bn_bwd_dual);
+  m.def("bn_bwd_dual", &bn_bwd_dual, py::arg("dy"), py::arg("bits"), py::arg("x"), py::arg("mean"), py::arg("invstd"),
+        py::arg("gamma"), py::arg("x2"), py::arg("mean2"), py::arg("invstd2"), py::arg("gamma2"),
+        py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(), py::arg("dgamma2_out") = py::none(),
+        py::arg("dbeta2_out") = py::none(), py::arg("table") = py::none(), py::arg("table2") = py::none());
   m.def("bn_bwd_dual_ok", &bn_bwd_dual_ok);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("w"), py::arg("H"), py::arg("W"), py::arg("stride"),
         py::arg("pad"), py::arg("dil"), py::arg("addend") = py::none(), py::arg("addend_bits") = py::none(),
         py::arg("out_f32") = false, py::arg("bst_z") = py::none(), py::arg("bst_ss") = py::none(),
-        py::arg("bst_bits") = py::none(), py::arg("bst_mean") = py::none(), py::arg("bst_table") = py::none());
+        py::arg("bst_bits") = py::none(), py::arg("bst_mean") = py::none(), py::arg("bst_table") = py::none(),
+        py::arg("bst_z2") = py::none(), py::arg("bst_mean2") = py::none(), py::arg("bst_table2") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("act_fwd", &act_fwd);
   m.def("act_bwd", &act_bwd);

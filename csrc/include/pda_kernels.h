@@ -128,6 +128,8 @@ hipError_t stem_pool_bn_bwd(const bf16_t* dp, const uint8_t* idx, const bf16_t* 
 bool bn_dual_ok(int64_t C);
 // one BN of bn_bwd_dual: input, saved statistics, affine weight, outputs, workspace (bn_workspace_floats)
 struct BnBwdSide {
+  float* table;  // optional: [rows][2][C] sums from a dgrad epilogue (no reduce pass; re-zeroed)
+  int rows;
   const bf16_t* x;
   const float* mean;
   const float* invstd;
@@ -232,6 +234,10 @@ struct BnBwdStats {
   const float* mean;
   float* table;
   int rows;
+  // optional second BN of the same masked gradient (relu(bn(z) + bn2(z2))): its input, mean and table
+  const bf16_t* z2;
+  const float* mean2;
+  float* table2;
 };
 hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, void* dx, bool dx_f32, int N, int H, int W,
                         int C, int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,

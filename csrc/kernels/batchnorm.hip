@@ -1282,16 +1282,26 @@ hipError_t bn_bwd_dual(const bf16_t* dy, const uint8_t* relu_bits, int64_t M, in
   BnGeom g = bn_geom(M, C);
   float* coef = a.ws + 2 * (int64_t)g.nrb * C;
   float* coef2 = b.ws + 2 * (int64_t)g.nrb * C;
-  bn_bwd_reduce_dual_kernel<<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(dy, a.x, b.x, relu_bits, a.mean, b.mean, M, (int)C,
-                                                                   g.cols, g.rpi, g.rpb, a.ws, b.ws);
-  PDA_CHECK_HIP(hipGetLastError());
+  // both sums from a dgrad epilogue (BnBwdStats z / z2): no reduce pass, finalize from the tables
+  const bool tables = a.table && b.table;
+  if ((a.table != nullptr) != (b.table != nullptr) || (tables && (a.rows < 1 || b.rows < 1))) return hipErrorInvalidValue;
+  if (!tables) {
+    bn_bwd_reduce_dual_kernel<<<dim3(g.nrb, g.gy), kThreads, 0, st>>>(dy, a.x, b.x, relu_bits, a.mean, b.mean, M,
+                                                                     (int)C, g.cols, g.rpi, g.rpb, a.ws, b.ws);
+    PDA_CHECK_HIP(hipGetLastError());
+  }
   const BnBwdSide* sides[2] = {&a, &b};
   float* coefs[2] = {coef, coef2};
   for (int i = 0; i < 2; ++i) {
     const BnBwdSide& p = *sides[i];
-    bn_bwd_finalize_kernel<false><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
-        p.ws, g.nrb, M, (int)C, p.mean, p.invstd, p.gamma_f, p.gamma_b, p.dgamma_f, p.dgamma_b, p.dbeta_f, p.dbeta_b,
-        coefs[i]);
+    if (tables)
+      bn_bwd_finalize_kernel<true><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
+          p.table, p.rows, M, (int)C, p.mean, p.invstd, p.gamma_f, p.gamma_b, p.dgamma_f, p.dgamma_b, p.dbeta_f,
+          p.dbeta_b, coefs[i]);
+    else
+      bn_bwd_finalize_kernel<false><<<(unsigned)((C + 63) / 64), kFinThreads, 0, st>>>(
+          p.ws, g.nrb, M, (int)C, p.mean, p.invstd, p.gamma_f, p.gamma_b, p.dgamma_f, p.dgamma_b, p.dbeta_f,
+          p.dbeta_b, coefs[i]);
     PDA_CHECK_HIP(hipGetLastError());
   }
   const int grid = wave_grid(M * C / 8);

@@ -577,10 +577,13 @@ __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 
   const bool want_stats = epi.stats != nullptr;
   EpiStatCols scol;
   epi_stat_cols(epi, want_stats, n0 + (tid % CPR) * 8, N, scol);
+  float st3[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) st3[q] = 0.f;
   if (epi.bst_z) {
     epi_bst_chunks<BM, CPR, NT>(
         epi, scol, [&](int r, int ch) { return *reinterpret_cast<const u16x8*>(stg + r * SROW + ch * 8); }, m0, n0,
-        M, N, st1, st2);
+        M, N, st1, st2, st3);
   } else
 #pragma unroll
   for (int c = tid; c < BM * CPR; c += NT) {
@@ -600,7 +603,7 @@ __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 
     *reinterpret_cast<u16x8*>((bf16_t*)epi.C + crow * epi.ldc + n) = v;
   }
   if (!DEFER && want_stats) {
-    epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + BM * SROW * 2), CPR, NT, tm, n0, N);
+    epi_stats_flush_all(epi, st1, st2, st3, reinterpret_cast<float*>(smem + BM * SROW * 2), CPR, NT, tm, n0, N);
   }
 }
 
@@ -2385,7 +2388,7 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
   // (a strided dgrad's fill-phase kernel writes the addend where no tap reaches: those elements would be
   // missing from the sums, so the statistics take an addend only at stride 1)
   if (bst && (dx_f32 || (addend && stride > 1) || !bst->z || !bst->mean || !bst->table || bst->rows < 1 ||
-              (!bst->ss && !bst->bits)))
+              (!bst->ss && !bst->bits) || (bst->z2 && (!bst->mean2 || !bst->table2))))
     return hipErrorInvalidValue;
   // every Epi below starts from this one: bf16 dx, the optional addend and the optional BN-backward sums
   auto base_epi = [&]() {
@@ -2399,6 +2402,9 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
       e.bst_z = bst->z;
       e.bst_ss = bst->ss;
       e.bst_bits = bst->bits;
+      e.bst_z2 = bst->z2;
+      e.bst_mean2 = bst->mean2;
+      e.bst_table2 = bst->table2;
     }
     return e;
   };

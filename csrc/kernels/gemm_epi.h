@@ -53,6 +53,11 @@ struct Epi {
   const bf16_t* bst_z;
   const float* bst_ss;
   const uint8_t* bst_bits;
+  // second BN fed by the same masked gradient (a downsample bottleneck's relu(bn(z) + bn2(z2))): its sums
+  // sum(g) and sum(g (z2 - mean2)) go to bst_table2 (same row layout)
+  const bf16_t* bst_z2;
+  const float* bst_mean2;
+  float* bst_table2;
 };
 
 // The pipelined 256 x 256 GEMM (gemm_pp.hip); gemm_conv.hip routes plain GEMMs to it.
@@ -88,7 +93,7 @@ __device__ __forceinline__ void epi_act8(const Epi& e, int64_t crow, int64_t n, 
 // tile's global stores to be acknowledged (vmcnt(0)) — measured at ~16 us per wide-tile conv, since a
 // 1-workgroup-per-CU kernel exposes every epilogue cycle.
 __device__ __forceinline__ void epi_stats_flush(const Epi& epi, float (&st1)[8], float (&st2)[8], float* red, int cpr,
-                                                int nt, int tm, int64_t n0, int64_t N) {
+                                                int nt, int tm, int64_t n0, int64_t N, float* table = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, ncol = cpr * 8;
   for (int off = cpr; off < 64; off <<= 1)
 #pragma unroll
@@ -112,7 +117,7 @@ __device__ __forceinline__ void epi_stats_flush(const Epi& epi, float (&st1)[8],
       a += red[(w * ncol + tid) * 2];
       b += red[(w * ncol + tid) * 2 + 1];
     }
-    float* row = epi.stats + (int64_t)(tm % epi.stats_rows) * 2 * N;
+    float* row = (table ? table : epi.stats) + (int64_t)(tm % epi.stats_rows) * 2 * N;
     unsafeAtomicAdd(row + n0 + tid, a);
     unsafeAtomicAdd(row + N + n0 + tid, b);
   }
@@ -160,7 +165,8 @@ __device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
 //   stg_read(r, ch): the staged bf16 values of tile row r, column chunk ch.
 template <int ROWS, int CPR, int NT, class StgRead>
 __device__ __forceinline__ void epi_bst_chunks(const Epi& e, const EpiStatCols& sc, StgRead stg_read, int64_t m0,
-                                               int64_t n0, int64_t M, int64_t N, float (&st1)[8], float (&st2)[8]) {
+                                               int64_t n0, int64_t M, int64_t N, float (&st1)[8], float (&st2)[8],
+                                               float (&st3)[8]) {
   constexpr int ITERS = ROWS * CPR / NT;
   constexpr int G = ITERS < 4 ? ITERS : 4;  // (8 pushed the gathered wide-tile kernels into scratch)
   static_assert(ITERS % G == 0, "groups cover the tile");
@@ -170,6 +176,14 @@ __device__ __forceinline__ void epi_bst_chunks(const Epi& e, const EpiStatCols& 
   const uint8_t* abp = e.addend_bits ? e.addend_bits : reinterpret_cast<const uint8_t*>(e.bst_z);
   const uint32_t ab_or = e.addend_bits ? 0u : 0xFFu;
   const uint8_t* zbp = use_bits ? e.bst_bits : reinterpret_cast<const uint8_t*>(e.bst_z);
+  const bool dual = e.bst_z2 != nullptr;
+  const bf16_t* z2p = dual ? e.bst_z2 : e.bst_z;
+  float mu2[8];
+  {
+    const int64_t n = n0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) mu2[q] = (dual && n + q < N) ? e.bst_mean2[n + q] : 0.f;
+  }
   float scl[8], shf[8];  // the BN's scale / shift of this thread's (fixed) column chunk: the recomputed mask
   {
     const int64_t n = n0 + (tid % CPR) * 8;
@@ -182,7 +196,7 @@ __device__ __forceinline__ void epi_bst_chunks(const Epi& e, const EpiStatCols& 
   }
 #pragma unroll 1
   for (int c0 = tid; c0 < ROWS * CPR; c0 += G * NT) {
-    u16x8 z[G], a[G];
+    u16x8 z[G], a[G], z2[G];
     uint32_t ab[G], zb[G];
     int64_t off[G];
     bool ok[G];
@@ -194,6 +208,7 @@ __device__ __forceinline__ void epi_bst_chunks(const Epi& e, const EpiStatCols& 
       ok[u] = m < M && n < N;
       off[u] = ok[u] ? epi_row(e, m) * e.ldc + n : 0;
       z[u] = *reinterpret_cast<const u16x8*>(e.bst_z + off[u]);
+      z2[u] = *reinterpret_cast<const u16x8*>(z2p + off[u]);
       a[u] = *reinterpret_cast<const u16x8*>(adp + off[u]);
       ab[u] = (uint32_t)abp[off[u] >> 3] | ab_or;
       zb[u] = zbp[off[u] >> 3];
@@ -214,9 +229,27 @@ __device__ __forceinline__ void epi_bst_chunks(const Epi& e, const EpiStatCols& 
         const float g = keep ? bf2f(o[q]) : 0.f;
         st1[q] += g;
         st2[q] = fmaf(g, zf - sc.k[q], st2[q]);
+        st3[q] = fmaf(g, bf2f(z2[u][q]) - mu2[q], st3[q]);
       }
       *reinterpret_cast<u16x8*>((bf16_t*)e.C + off[u]) = o;
     }
+  }
+}
+
+// flush of a tile's statistics; with a second BN (bst_z2) also (sum g, sum g (z2 - mean2)) into bst_table2
+// (st1 is reduced in place by a flush, so the second one gets a copy; an LDS-only barrier separates the
+// two uses of the scratch)
+__device__ __forceinline__ void epi_stats_flush_all(const Epi& epi, float (&st1)[8], float (&st2)[8], float (&st3)[8],
+                                                    float* red, int cpr, int nt, int tm, int64_t n0, int64_t N) {
+  float g1[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) g1[q] = st1[q];
+  epi_stats_flush(epi, st1, st2, red, cpr, nt, tm, n0, N);
+  if (epi.bst_z2) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    epi_stats_flush(epi, g1, st3, red, cpr, nt, tm, n0, N, epi.bst_table2);
   }
 }
 
@@ -343,10 +376,13 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][16 / WC
   epi_stat_cols(epi, want_stats, n0 + (tid % CPR) * 8, N, scol);
 #pragma unroll
   for (int q = 0; q < 8; ++q) st1[q] = st2[q] = 0.f;
+  float st3[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) st3[q] = 0.f;
   if (BST && epi.bst_z) {
     epi_bst_chunks<256, CPR, NT>(
         epi, scol, [&](int r, int ch) { return *reinterpret_cast<const u16x8*>(stg + r * WT_SROW + ch * 8); }, m0,
-        n0, M, N, st1, st2);
+        n0, M, N, st1, st2, st3);
   } else
   for (int c = tid; c < 256 * CPR; c += NT) {
     const int r = c / CPR, ch = c % CPR;
@@ -366,7 +402,10 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][16 / WC
     if (epi.nt_store) __builtin_nontemporal_store(v, dst);
     else *dst = v;
   }
-  if (want_stats) epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + stats_off), CPR, NT, tm, n0, N);
+  if (want_stats) {
+    if (BST) epi_stats_flush_all(epi, st1, st2, st3, reinterpret_cast<float*>(smem + stats_off), CPR, NT, tm, n0, N);
+    else epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + stats_off), CPR, NT, tm, n0, N);
+  }
 }
 
 // Persistent-kernel variant of the bf16 epilogue (gemm_pp.hip): the next tile's operand DMAs are in

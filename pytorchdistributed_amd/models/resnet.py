@@ -63,7 +63,7 @@ class Bottleneck(tnn.Module):
                     and (bn_ds.eps, bn_ds.momentum) == (self.bn3.eps, self.bn3.momentum)):
                 # relu(bn3(z3) + bn_ds(zd)) in one kernel: the shortcut's BN output and its gradient
                 # are never stored (PDA_DUAL_BN=0: the separate shortcut BN apply)
-                return ops.batch_norm_dual(z3[0], self.bn3, zd[0], bn_ds, z3[1], zd[1])
+                return ops.batch_norm_dual(z3[0], self.bn3, zd[0], bn_ds, z3[1], zd[1], fuse_bwd_stats=_BN3_BWD_JOIN)
             return self.bn3(z3, residual=bn_ds(zd), relu=True)
         return self.bn3(self.conv3(out, bn=self.bn3), residual=x, relu=True, residual_join=join,
                         fuse_bwd_stats=_BN3_BWD_JOIN)

@@ -84,23 +84,28 @@ class BnBwdStats:
     complete in the dgrad of the LAST consumer of the shared gradient join (the one whose epilogue adds
     the other consumers' stashed gradients)."""
 
-    __slots__ = ("z", "ss", "bits", "mean", "table", "needs_join", "token")
+    __slots__ = ("z", "ss", "bits", "mean", "table", "needs_join", "token", "z2", "mean2", "table2")
 
-    def __init__(self, z, ss, bits, mean, table, needs_join: bool, token=None):
+    def __init__(self, z, ss, bits, mean, table, needs_join: bool, token=None, second=None):
         self.z, self.ss, self.bits, self.mean, self.table = z, ss, bits, mean, table
         self.needs_join = needs_join
-        # [filled]: shared with the table's owner (BatchNorm2d), which re-zeroes a table a dgrad filled but
-        # no BN backward consumed (an aborted backward) before handing it out again
-        self.token = token if token is not None else [False]
-        self.token[0] = False
+        # second BN fed by the same masked gradient (relu(bn(z) + bn2(z2))): (z2, mean2, table2)
+        self.z2, self.mean2, self.table2 = second if second is not None else (None, None, None)
+        # [filled] flags shared with the tables' owners (BatchNorm2d), which re-zero a table a dgrad filled
+        # but no BN backward consumed (an aborted backward) before handing it out again (one per table)
+        if token is None:
+            token = [False]
+        self.token = list(token) if isinstance(token, tuple) else [token]
+        self.filled = False
 
     @property
     def filled(self) -> bool:
-        return self.token[0]
+        return self.token[0][0]
 
     @filled.setter
     def filled(self, v: bool):
-        self.token[0] = bool(v)
+        for t in self.token:
+            t[0] = bool(v)
 
     def usable(self, join_last: bool, has_join: bool, stride: int, addend) -> bool:
         """May the dgrad of a conv (the last contributor of its gradient join or not, stride, epilogue
@@ -119,4 +124,6 @@ class BnBwdStats:
             kw["bst_bits"] = self.bits
         else:
             kw["bst_ss"] = self.ss
+        if self.z2 is not None:
+            kw.update(bst_z2=self.z2, bst_mean2=self.mean2, bst_table2=self.table2)
         return kw

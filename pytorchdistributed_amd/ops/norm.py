@@ -108,13 +108,19 @@ class _DualBatchNormFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gamma, beta, x2, gamma2, beta2, rm, rv, rm2, rv2, table, shift, table2, shift2, nbt, nbt2,
-                momentum, eps):
+                momentum, eps, bwd_tables=None):
         x, x2 = x.contiguous(), x2.contiguous()
         y, bits, mean, invstd, mean2, invstd2 = C().bn_fwd_train_sums_dual(
             x, table, shift, gamma, beta, rm, rv, nbt, x2, table2, shift2, gamma2, beta2, rm2, rv2, nbt2, momentum,
             eps)
         ctx.save_for_backward(x, x2, bits, mean, invstd, mean2, invstd2, gamma, gamma2)
         ctx.betas = (beta, beta2)
+        # both BNs' backward sums from the next block's conv1 dgrad epilogue (the gradient join's last
+        # contributor): (bt1, token), (bt2, token2) = bwd_tables
+        ctx.bnb = None
+        if bwd_tables is not None:
+            (bt1, tok), (bt2, tok2) = bwd_tables
+            ctx.bnb = BnBwdStats(x, None, bits, mean, bt1, True, (tok, tok2), second=(x2, mean2, bt2))
         return y
 
     @staticmethod
@@ -124,7 +130,19 @@ class _DualBatchNormFn(torch.autograd.Function):
         dy = dy.contiguous()
         tg, tb = _param_targets(ctx, gamma, beta, 1, 2)
         tg2, tb2 = _param_targets(ctx, gamma2, beta2, 4, 5)
-        if _DUAL_BWD and C().bn_bwd_dual_ok(x.shape[-1]):
+        bnb, ctx.bnb = ctx.bnb, None
+        if bnb is not None and bnb.filled:
+            # both reductions were accumulated by the dgrad that produced dy: finalizes + the apply pass(es)
+            bnb.filled = False
+            if C().bn_bwd_dual_ok(x.shape[-1]):
+                dx, dx2, dg, db, dg2, db2 = C().bn_bwd_dual(dy, bits, x, mean, invstd, gamma, x2, mean2, invstd2,
+                                                            gamma2, tg, tb, tg2, tb2, bnb.table, bnb.table2)
+            else:
+                dx, _, dg, db = C().bn_bwd_table(dy, x, bits, None, mean, invstd, gamma, True, False, bnb.table, tg,
+                                                 tb)
+                dx2, _, dg2, db2 = C().bn_bwd_table(dy, x2, bits, None, mean2, invstd2, gamma2, True, False,
+                                                    bnb.table2, tg2, tb2)
+        elif _DUAL_BWD and C().bn_bwd_dual_ok(x.shape[-1]):
             # one reduce pass over (dy, bits, x, x2) and one apply pass writing dx and dx2
             dx, dx2, dg, db, dg2, db2 = C().bn_bwd_dual(dy, bits, x, mean, invstd, gamma, x2, mean2, invstd2, gamma2,
                                                         tg, tb, tg2, tb2)
@@ -134,7 +152,7 @@ class _DualBatchNormFn(torch.autograd.Function):
         ng = ctx.needs_input_grad
         return (dx, dg if gamma is not None and ng[1] else None, db if beta is not None and ng[2] else None,
                 dx2, dg2 if gamma2 is not None and ng[4] else None, db2 if beta2 is not None and ng[5] else None) \
-            + (None,) * 12
+            + (None,) * 13
 
 
 def dual_bn_ok(x: torch.Tensor, training: bool) -> bool:
@@ -142,13 +160,21 @@ def dual_bn_ok(x: torch.Tensor, training: bool) -> bool:
     return training and x.is_cuda and x.dtype == torch.bfloat16 and C().bn_dual_ok(x.shape[-1])
 
 
-def batch_norm_dual(x, bn, x2, bn2, stats, stats2):
+def batch_norm_dual(x, bn, x2, bn2, stats, stats2, fuse_bwd_stats: bool = False):
     """``relu(bn(x) + bn2(x2))`` for two training-mode ``BatchNorm2d`` modules whose batch statistics
-    were accumulated by the producing convs (``stats = (table, shift)`` from ``Conv2d(..., bn=...)``)."""
+    were accumulated by the producing convs (``stats = (table, shift)`` from ``Conv2d(..., bn=...)``).
+    ``fuse_bwd_stats``: the output feeds the next block's gradient join, whose last contributing conv
+    reduces both BNs' backward sums in its dgrad epilogue (``PDA_BN_BWD_EPILOGUE=0``: the reduce pass)."""
     (t1, s1), (t2, s2) = stats, stats2
-    return _DualBatchNormFn.apply(x, bn.weight, bn.bias, x2, bn2.weight, bn2.bias, bn.running_mean, bn.running_var,
-                                  bn2.running_mean, bn2.running_var, t1, s1, t2, s2, bn.num_batches_tracked,
-                                  bn2.num_batches_tracked, bn.momentum, bn.eps)
+    bt = None
+    if fuse_bwd_stats and _BWD_EPILOGUE and torch.is_grad_enabled():
+        bt = (bn.bwd_table(x.device), bn2.bwd_table(x.device))
+    y = _DualBatchNormFn.apply(x, bn.weight, bn.bias, x2, bn2.weight, bn2.bias, bn.running_mean, bn.running_var,
+                               bn2.running_mean, bn2.running_var, t1, s1, t2, s2, bn.num_batches_tracked,
+                               bn2.num_batches_tracked, bn.momentum, bn.eps, bt)
+    if bt is not None and y.grad_fn is not None and getattr(y.grad_fn, "bnb", None) is not None:
+        y._pda_bnb = y.grad_fn.bnb
+    return y
 
 
 def _ref_batch_norm(x, gamma, beta, residual, running_mean, running_var, training, momentum, eps, relu):

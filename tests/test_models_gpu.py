@@ -299,6 +299,8 @@ def test_tied_embedding_side_stream_matches_single_stream():
     (8, 28, 28, 128, 128, 3, 2, 1, "ss", False),     # 3x3 stride-2: phase launches + fill phases
     (32, 14, 14, 256, 1024, 1, 1, 0, "bits", True),  # next block's conv1: addend (shortcut) + bit mask
     (4, 14, 14, 64, 256, 1, 1, 0, "bits", True),
+    (32, 14, 14, 256, 1024, 1, 1, 0, "dual", True),  # after a downsample block: two BNs, one masked dy
+    (4, 14, 14, 64, 256, 1, 1, 0, "dual", True),
 ])
 def test_conv_dgrad_bn_bwd_stats(case):
     """The dgrad epilogue's BN-backward sums (gemm_epi.h bst_*) equal fp32 sums over the dx the same
@@ -321,6 +323,11 @@ def test_conv_dgrad_bn_bwd_stats(case):
         kw["bst_ss"] = torch.cat([scale, shift]).to(dev)
         keep = (z.float() * scale.to(dev) + shift.to(dev)) > 0
     else:
+        if src == "dual":
+            z2 = torch.randn(N, H, W, Cin).to(dev, torch.bfloat16)
+            mean2 = (torch.randn(Cin) * 0.1).to(dev)
+            table2 = torch.zeros(64, 2, Cin, device=dev)
+            kw.update(bst_z2=z2, bst_mean2=mean2, bst_table2=table2)
         bits = torch.randint(0, 256, (N * H * W * Cin // 8,), dtype=torch.uint8, device=dev)
         kw["bst_bits"] = bits
         shifts = torch.arange(8, device=dev, dtype=torch.uint8)
@@ -336,21 +343,28 @@ def test_conv_dgrad_bn_bwd_stats(case):
     scale2 = (g * (z.float().reshape(-1, Cin) - mean)).abs().sum(0) + 1e-3
     assert ((tab[0] - s1).abs() / scale1).max().item() < 1e-4
     assert ((tab[1] - s2).abs() / scale2).max().item() < 1e-4
+    if src == "dual":
+        t2 = table2.sum(0)
+        s3 = (g * (z2.float().reshape(-1, Cin) - mean2)).sum(0)
+        scale3 = (g * (z2.float().reshape(-1, Cin) - mean2)).abs().sum(0) + 1e-3
+        assert ((t2[0] - s1).abs() / scale1).max().item() < 1e-4
+        assert ((t2[1] - s3).abs() / scale3).max().item() < 1e-4
 
 
 def test_bottleneck_bwd_stats_from_dgrad_epilogue(monkeypatch):
-    """Two identity bottlenecks: bn1 / bn2 of both blocks and the first block's output BN (through the
-    second block's conv1 gradient join) take their backward sums from the dgrad epilogues — every BN
-    backward but the last block's bn3 (whose output has no conv consumer) finalizes from a table.  The
-    gradients match the reduce-pass path and the fp32 CPU reference (to 1.5x plain bf16 rounding)."""
+    """layer1 (a downsample bottleneck + two identity ones): bn1 / bn2 of every block, the identity block's
+    output BN and the downsample block's dual output BN pair (both through the next block's conv1 gradient
+    join) take their backward sums from the dgrad epilogues — every BN backward but the last block's bn3
+    (whose output has no conv consumer) finalizes from a table.  The gradients match the reduce-pass
+    path and the fp32 CPU reference (to 1.5x plain bf16 rounding)."""
     from pytorchdistributed_amd._native import C as _C
     from pytorchdistributed_amd.models.resnet import resnet50
     from pytorchdistributed_amd.ops import norm as _norm
 
     torch.manual_seed(0)
     ref = resnet50(dtype=torch.bfloat16)
-    pair_ref = torch.nn.Sequential(ref.layer1[1], ref.layer1[2]).float().train()
-    xin = torch.randn(8, 16, 16, 256).to(torch.bfloat16).float().requires_grad_()
+    pair_ref = torch.nn.Sequential(ref.layer1[0], ref.layer1[1], ref.layer1[2]).float().train()
+    xin = torch.randn(8, 16, 16, 64).to(torch.bfloat16).float().requires_grad_()
     out_r = pair_ref(xin)
     dy = torch.randn_like(out_r).to(torch.bfloat16).float()
     out_r.backward(dy)
@@ -358,9 +372,9 @@ def test_bottleneck_bwd_stats_from_dgrad_epilogue(monkeypatch):
     xb = xin.detach().to(torch.bfloat16).requires_grad_()
     pair_b16(xb).backward(dy.to(torch.bfloat16))
 
-    calls = {"table": 0, "reduce": 0}
+    calls = {"table": 0, "reduce": 0, "dual_table": 0, "dual": 0}
     mod = _C()
-    real_t, real_r = mod.bn_bwd_table, mod.bn_bwd
+    real_t, real_r, real_d = mod.bn_bwd_table, mod.bn_bwd, mod.bn_bwd_dual
 
     def t_(*a, **k):
         calls["table"] += 1
@@ -370,20 +384,25 @@ def test_bottleneck_bwd_stats_from_dgrad_epilogue(monkeypatch):
         calls["reduce"] += 1
         return real_r(*a, **k)
 
+    def d_(*a, **k):
+        calls["dual_table" if len(a) == 16 else "dual"] += 1
+        return real_d(*a, **k)
+
     monkeypatch.setattr(mod, "bn_bwd_table", t_)
     monkeypatch.setattr(mod, "bn_bwd", r_)
+    monkeypatch.setattr(mod, "bn_bwd_dual", d_)
     grads = {}
     for fused in (True, False):
         monkeypatch.setattr(_norm, "_BWD_EPILOGUE", fused)
-        calls.update(table=0, reduce=0)
+        calls.update(table=0, reduce=0, dual_table=0, dual=0)
         pair_g = copy.deepcopy(pair_ref).to("cuda", torch.bfloat16)
         xg = xin.detach().to("cuda", torch.bfloat16).requires_grad_()
         pair_g(xg).backward(dy.to("cuda", torch.bfloat16))
         torch.cuda.synchronize()
         if fused:
-            assert calls == {"table": 5, "reduce": 1}, calls
+            assert calls == {"table": 7, "reduce": 1, "dual_table": 1, "dual": 0}, calls
         else:
-            assert calls == {"table": 0, "reduce": 6}, calls
+            assert calls == {"table": 0, "reduce": 8, "dual_table": 0, "dual": 1}, calls
         grads[fused] = [xg.grad.cpu()] + [p.grad.cpu() for p in pair_g.parameters()]
     bound_x = max(2e-2, 1.5 * rel_err(xb.grad, xin.grad))
     assert rel_err(grads[True][0], xin.grad) < bound_x
