@@ -1034,6 +1034,205 @@ __global__ void __launch_bounds__(NT, 2) conv3x3_wgrad_kernel(const bf16_t* __re
   }
 }
 
+// ------------------------------------------------------------------ 3x3 weight gradient v2 (all layers)
+// dw[co][r][s][ci] = sum over output pixels of dy[px][co] * x[st*px + (r-1, s-1)][ci], stride 1 or 2, for
+// every 3x3 layer of ResNet-50 (56^2 .. 7^2, the three strided ones included).  The round-4 kernels left
+// these at 0.22-0.34 of their roofline: the 64 x 576 all-taps kernel above moves one 64-pixel row group
+// per barrier with a single DMA stage of cover at two 4-wave workgroups per CU (latency-bound, and
+// each x row is fetched 3 times), and the 14^2 / 7^2 / strided layers took the implicit GEMM whose
+// im2col gather re-reads every x pixel per tap through L2.
+// Here one 8-wave workgroup (one per CU, 144 KB of LDS in two 72 KB stages) owns CO_T output channels x
+// 64 input channels x 9 taps and walks K in row groups of ONE image: rk output rows (<= 128 pixels,
+// in 32-pixel halves) per step.  A step DMAs the dy rows (MN-major [px][CO_T] images) and the x BAND
+// those rows touch — (rk - 1) st + 3 input rows of W + 2 pixels (zero outside the image) — and the 9
+// taps are 9 views of the band at pixel offsets r (W + 2) + s from the output pixel's (st rj, st cj):
+// x crosses the L2 once per row group instead of once per tap.  Waves: ci block w & 3 (16 channels)
+// x (CO_T = 128) the co half w >> 2, or (CO_T = 64, KSPLIT) the pixel-half parity w >> 2 with its own
+// slab (two slabs per split): every wave multiplies 4 co blocks x 9 taps against one ci block, so an
+// A fragment serves 9 MFMAs and a B (band) fragment 4.  Split-K over row groups; fp32 slabs summed by
+// splitk_reduce_kernel.
+struct Wg3v2Geom {
+  int N, H, W, P, Q, C, Cout, st;
+  int rk;        // output rows per K-step (rk * Q <= 128)
+  int gpi;       // row groups per image = ceil(P / rk)
+  int groups;    // N * gpi
+  int gps;       // row groups per split
+  int band_rows; // (rk - 1) * st + 3
+  int w2l;       // log2 of the band row pitch in pixels (>= W + 2, >= 16)
+  int tiles_ci;  // C / 64
+  int tiles_co;  // Cout / CO_T
+  FastDiv fQ;
+};
+
+constexpr int WG3V2_NT = 512;
+constexpr int WG3V2_DY = 32 * 1024;    // dy: two [64 px][<= 128 co] MN-major images
+constexpr int WG3V2_BAND = 40 * 1024;  // band: <= 320 pixels x 64 channels (128-B rows)
+constexpr int WG3V2_STAGE = WG3V2_DY + WG3V2_BAND;
+
+// LDS-DMA of one 16-B chunk per lane (wave-uniform LDS base + lane x 16 B) as inline asm, as gemm_pp.hip
+// pp_glds_asm: beside a compiler-visible global_load_lds, hipcc (ROCm 7.2) waits vmcnt(0) in front of
+// every ds_read_b64_tr_b16 (it cannot tell the read from the DMA's LDS range), which drained the next
+// group's DMA before this group's first read.  Hidden in asm, the DMA is ordered by the kernel's own
+// s_waitcnt only (no other vector-memory op is in flight in its K loop).
+__device__ __forceinline__ void glds_asm(const bf16_t* src, char* lds_wave_base) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(l) : "memory", "m0");
+}
+
+template <int CO_T, int W2L>
+__global__ void __launch_bounds__(WG3V2_NT, 1) conv3x3_wg_kernel(const bf16_t* __restrict__ dy,
+                                                                 const bf16_t* __restrict__ x, Wg3v2Geom g,
+                                                                 float* __restrict__ slab) {
+  constexpr bool KSPLIT = CO_T == 64;   // 8 waves = 4 ci blocks x 2 pixel-half parities
+  constexpr int NCB = 4;                // co blocks per wave
+  constexpr int IMG = 64 * CO_T * 2;    // one [64 px][CO_T] dy image
+  // two stages as separate __shared__ objects, loop unrolled by two (conv_stem_fwd_kernel: with one
+  // dynamic array hipcc drains the next group's DMA before this group's reads)
+  __shared__ __attribute__((aligned(16))) char s_st0[WG3V2_STAGE];
+  __shared__ __attribute__((aligned(16))) char s_st1[WG3V2_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cb = w & 3, wh = w >> 2;
+  const int tco = blockIdx.x / g.tiles_ci, tci = blockIdx.x - tco * g.tiles_ci;
+  const int co0 = tco * CO_T, ci0 = tci * 64;
+  const int cow = KSPLIT ? 0 : wh * 64;  // this wave's first co within the tile
+  // band rows are W2P = 2^W2L >= W + 2 pixels (>= 16): the swizzle key (pixel bits 1 and 3) then depends on
+  // the column only, so a tap's row step r W2P is a constant LDS offset and only the 3 column shifts need
+  // their swizzled addresses computed (the per-tap address arithmetic had made the loop VALU-bound)
+  constexpr int W2P = 1 << W2L;
+  const int W = g.W, H = g.H, Q = g.Q, st = g.st;
+  const int gb = blockIdx.y * g.gps;
+  const int ge = min(g.groups, gb + g.gps);
+
+  f32x4 acc[NCB][9];
+#pragma unroll
+  for (int i = 0; i < NCB; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // per-lane band pixel (tap (0,0)) of k row j of the transposed B reads, j = 32 h + 8 (lane >> 4) +
+  // ((lane & 15) >> 2) (+ 4): output pixel (rj, cj) -> (st rj) W2 + st cj (computed per half: a table of
+  // all 8 stays live across the MFMAs)
+  const int jl = 8 * (lane >> 4) + ((lane & 15) >> 2);
+  const int jmax = g.rk * Q;
+  auto band_px = [&](int j) {
+    const int rj = (int)fdiv((uint32_t)j, g.fQ), cj = j - rj * Q;
+    return j < jmax ? ((rj * st) << W2L) + cj * st : 0;  // past the group: dy = 0 there
+  };
+
+  // dy DMA mapping of [64 px][CO_T co] images: round i of thread t writes byte i*8192 + t*16 = mn_off<CO_T>(k, m)
+  // with k = i * PXR + t / TPR; the swizzle key of k (k & 63's low bits) does not depend on i, so the
+  // thread's column m is the same in every round
+  constexpr int RB = CO_T * 2;               // image row bytes
+  constexpr int TPR = RB / 16;               // threads per pixel row
+  constexpr int PXR = WG3V2_NT / TPR;        // pixels per DMA round: 32 (CO_T = 128) or 64 (CO_T = 64)
+  constexpr int DY_ROUNDS = 128 / PXR;
+  const int dy_k0 = tid / TPR;
+  int dy_m;
+  {
+    const int kl = dy_k0 & 63, rb = (tid % TPR) * 16;
+    int hsw;
+    if constexpr (CO_T == 128) hsw = (kl & 3) | (((kl >> 3) & 1) << 2);
+    else hsw = ((kl >> 1) & 1) | (((kl >> 3) & 1) << 1);
+    dy_m = ((((rb >> 5) ^ hsw) & (CO_T / 16 - 1)) << 4) + ((rb >> 4) & 1) * 8;
+  }
+  const int s16 = tid & 7;
+
+  auto issue = [&](int grp, char* base) {
+    const int n = grp / g.gpi, p0 = (grp - n * g.gpi) * g.rk;
+    const int rows = min(g.rk, g.P - p0);
+    const int npx = rows * Q;
+    // dy rows p0 .. p0 + rows - 1 of image n: npx consecutive pixels (zero past them)
+    const bf16_t* dyb = dy + ((int64_t)n * g.P + p0) * Q * g.Cout + co0 + dy_m;
+#pragma unroll
+    for (int i = 0; i < DY_ROUNDS; ++i) {
+      const int k = dy_k0 + i * PXR;
+      const bf16_t* a = dyb + (int64_t)k * g.Cout;  // formed unconditionally, then selected
+      glds_asm(k < npx ? a : g_zero_page, base + i * 8192 + w * 1024);
+    }
+    // x band: input rows st*p0 - 1 .. + band_rows - 1, cols -1 .. W (zero outside the image); always 5 DMA
+    // rounds of 64 pixels (the band capacity; pixels past the band are zeros nobody reads), addresses
+    // selected, not branched around
+    char* band = base + WG3V2_DY;
+    const int ih0 = st * p0 - 1;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int b = k * 64 + (tid >> 3);
+      const int rs = b >> W2L, cs = b & (W2P - 1);
+      const int hb = ((b >> 1) & 1) | (((b >> 3) & 1) << 1);
+      const int ci = ci0 + 16 * ((s16 >> 1) ^ hb) + 8 * (s16 & 1);
+      const int ih = ih0 + rs, iw = cs - 1;
+      const bool ok = rs < g.band_rows && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W && cs < W + 2;
+      const bf16_t* a = x + (((int64_t)n * H + ih) * W + iw) * g.C + ci;
+      glds_asm(ok ? a : g_zero_page, band + k * 8192 + w * 1024);
+    }
+  };
+
+  typedef short s16x4 __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const int mcol = 16 * cb + 4 * ((lane & 15) & 3);
+  auto half = [&](const char* As, const char* band, int h) {
+    const int pj0 = band_px(32 * h + jl), pj1 = band_px(32 * h + jl + 4);
+    int alo[3], ahi[3];  // swizzled addresses of the three column shifts (tap row r adds r W2P 128 B)
+#pragma unroll
+    for (int sx = 0; sx < 3; ++sx) {
+      alo[sx] = band_mn_off(pj0 + sx, mcol);
+      ahi[sx] = band_mn_off(pj1 + sx, mcol);
+    }
+    mfma_bf16x8 af[NCB];
+#pragma unroll
+    for (int i = 0; i < NCB; ++i) af[i] = read_frag<false, CO_T>(As + (h >> 1) * IMG, cow + 16 * i, 32 * (h & 1), lane);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      constexpr int RB = W2P * 128;
+      const int roff = (t / 3) * RB;
+      const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(band + alo[t % 3] + roff));
+      const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(band + ahi[t % 3] + roff));
+      s16x8 f;
+      f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+      f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+      const mfma_bf16x8 bf = __builtin_bit_cast(mfma_bf16x8, f);
+#pragma unroll
+      for (int i = 0; i < NCB; ++i) acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf, af[i], acc[i][t], 0, 0, 0);
+    }
+  };
+  // the halves with data of this group (a runtime count; one loop body, so its fragments do not pile up
+  // in registers across halves); the asm DMA keeps hipcc from draining the next group's loads here
+  auto step = [&](int grp, const char* As, char* next) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    raw_barrier();  // this group landed for every wave; every wave is done with `next`
+    issue(min(grp + 1, ge - 1), next);
+    const int n = grp / g.gpi, p0 = (grp - n * g.gpi) * g.rk;
+    const int nh = (min(g.rk, g.P - p0) * Q + 31) >> 5;
+    const char* band = As + WG3V2_DY;
+    const int h0 = KSPLIT ? wh : 0, hs = KSPLIT ? 2 : 1;
+#pragma unroll 1
+    for (int h = h0; h < nh; h += hs) half(As, band, h);
+  };
+  if (gb < ge) {
+    issue(gb, s_st0);
+    for (int grp = gb; grp < ge; grp += 2) {
+      step(grp, s_st0, s_st1);
+      if (grp + 1 < ge) step(grp + 1, s_st1, s_st0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  // fp32 partials: acc[i][t][q] = dw[co0 + cow + 16 i + (lane & 15)][t][ci0 + 16 cb + 4 (lane >> 4) + q]
+  const int64_t Nn = 9LL * g.C;
+  const int sl = KSPLIT ? 2 * blockIdx.y + wh : blockIdx.y;
+  float* out = slab + (int64_t)sl * g.Cout * Nn;
+#pragma unroll
+  for (int i = 0; i < NCB; ++i) {
+    const int co = co0 + cow + 16 * i + (lane & 15);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      *reinterpret_cast<f32x4*>(out + (int64_t)co * Nn + (int64_t)t * g.C + ci0 + 16 * cb + 4 * (lane >> 4)) =
+          acc[i][t];
+  }
+}
+
 // ------------------------------------------------------------------ stem forward (4x4 valid conv, 16 channels)
 // y[n,p,q,co] = sum_(r,s,ci) x[n,p+r,q+s,ci] w[co][r][s][ci] over the 2x2 space-to-depth image: K = 256,
 // N = 64, M = 8 M output pixels at batch 640.  The implicit GEMM re-gathers every input byte 16 times
@@ -2244,6 +2443,69 @@ bool wg3_geom(int N, int H, int W, int C, int Cout, int R, int S, int stride, in
 
 int wg3_splits(const Wg3Geom& g) { return (g.groups + g.gps - 1) / g.gps; }
 
+// conv3x3_wg_kernel (v2): every 3x3 / pad 1 / dil 1 layer with stride 1 or 2, C and Cout multiples of 64.
+// PDA_CONV_WG3V2=0 keeps the round-4 kernels.
+bool wg3v2_mode_on() {
+  static const bool on = [] {
+    const char* e = getenv("PDA_CONV_WG3V2");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+int wg3v2_co_tile(int Cout) { return Cout % 128 == 0 ? 128 : 64; }
+
+bool wg3v2_geom(int N, int H, int W, int C, int Cout, int R, int S, int P, int Q, int stride, int pad, int dil,
+                Wg3v2Geom& g) {
+  if (!wg3v2_mode_on() || R != 3 || S != 3 || pad != 1 || dil != 1 || (stride != 1 && stride != 2)) return false;
+  if (C % 64 || Cout % 64 || Q > 128 || H < 1 || W < 1) return false;
+  if (P != (H - 1) / stride + 1 || Q != (W - 1) / stride + 1) return false;
+  // rows per K-step: the fewest 32-pixel halves per image among the rk whose dy (<= 128 px) and band
+  // (<= 320 px) fit a stage; every step runs NH = ceil(rk Q / 32) halves (even for the 64-channel tile,
+  // whose two wave groups take alternate halves)
+  int w2p = 16;
+  while (w2p < W + 2) w2p *= 2;
+  if (w2p > 128) return false;
+  int best = 0, best_halves = 1 << 30;
+  for (int rk = 1; rk <= P && rk * Q <= 128; ++rk) {
+    const int brows = (rk - 1) * stride + 3;
+    if (brows * w2p > 320) break;
+    const int full = P / rk, rem = P - full * rk;
+    const int halves = full * ((rk * Q + 31) / 32) + (rem ? (rem * Q + 31) / 32 : 0);
+    if (halves < best_halves || (halves == best_halves && rk > best)) {
+      best_halves = halves;
+      best = rk;
+    }
+  }
+  if (best == 0) return false;
+  g.N = N; g.H = H; g.W = W; g.P = P; g.Q = Q; g.C = C; g.Cout = Cout; g.st = stride;
+  g.rk = best;
+  g.gpi = (P + g.rk - 1) / g.rk;
+  g.groups = N * g.gpi;
+  g.band_rows = (g.rk - 1) * stride + 3;
+  g.w2l = w2p == 16 ? 4 : (w2p == 32 ? 5 : (w2p == 64 ? 6 : 7));
+  g.tiles_ci = C / 64;
+  g.tiles_co = Cout / wg3v2_co_tile(Cout);
+  g.fQ = make_fastdiv((uint32_t)Q);
+  // one workgroup per CU: ~wgrad_cus() workgroups, >= 4 row groups each, fp32 slabs capped at 96 MB
+  const int tiles = g.tiles_co * g.tiles_ci;
+  const int per_split_slabs = wg3v2_co_tile(Cout) == 64 ? 2 : 1;
+  int splits = wg3_wgrad_cus() / tiles;
+  if (splits < 1) splits = 1;
+  if (splits > g.groups / 4) splits = g.groups / 4 > 1 ? g.groups / 4 : 1;
+  const int64_t per = (int64_t)Cout * 9 * C * per_split_slabs;
+  const int64_t cap = ((int64_t)96 << 20) / (per * 4);
+  if (splits > cap) splits = cap > 1 ? (int)cap : 1;
+  g.gps = (g.groups + splits - 1) / splits;
+  return true;
+}
+
+// slabs written by a v2 launch (the 64-channel tile's two pixel-half parities each write their own)
+int wg3v2_slabs(const Wg3v2Geom& g) {
+  const int splits = (g.groups + g.gps - 1) / g.gps;
+  return wg3v2_co_tile(g.Cout) == 64 ? 2 * splits : splits;
+}
+
 // stem weight-gradient path (conv_stem_wgrad_kernel): 4x4 / stride 1 / pad 0 / dil 1 over 16 channels,
 // Cout % 64 == 0, output rows of <= 128 pixels.  PDA_CONV_STEM_WG=0 disables it.
 bool stem_wg_mode_on() {
@@ -2512,6 +2774,13 @@ int64_t conv_slab_floats(int mode, int N, int H, int W, int C, int Cout, int R, 
     const int64_t ws = (int64_t)stem_splits(sg) * M * Nn;
     if (ws > n) n = ws;
   }
+  Wg3v2Geom gv;
+  for (int sv = 1; sv <= 2; ++sv) {  // (the stride is not an argument: wg3v2_geom accepts at most one)
+    if (wg3v2_geom(N, H, W, C, Cout, R, S, P, Q, sv, 1, 1, gv)) {
+      const int64_t wv = (int64_t)wg3v2_slabs(gv) * M * Nn;
+      if (wv > n) n = wv;
+    }
+  }
   return n;
 }
 
@@ -2521,6 +2790,29 @@ hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32
                         hipStream_t st) {
   const int64_t M = Cout, Nn = (int64_t)R * S * C, K = (int64_t)N * P * Q;
   Epi epi{dw, Nn, dw_f32 ? 1 : 0, nullptr, 0, 0, nullptr};
+  Wg3v2Geom gv;
+  if (slab && wg3v2_geom(N, H, W, C, Cout, R, S, P, Q, stride, pad, dil, gv)) {
+    const int splits = (gv.groups + gv.gps - 1) / gv.gps;
+    const dim3 grid(gv.tiles_co * gv.tiles_ci, splits);
+#define WG3V2_LAUNCH(CO)                                                                        \
+  do {                                                                                          \
+    if (gv.w2l == 4) conv3x3_wg_kernel<CO, 4><<<grid, WG3V2_NT, 0, st>>>(dy, x, gv, slab);      \
+    else if (gv.w2l == 5) conv3x3_wg_kernel<CO, 5><<<grid, WG3V2_NT, 0, st>>>(dy, x, gv, slab); \
+    else if (gv.w2l == 6) conv3x3_wg_kernel<CO, 6><<<grid, WG3V2_NT, 0, st>>>(dy, x, gv, slab); \
+    else conv3x3_wg_kernel<CO, 7><<<grid, WG3V2_NT, 0, st>>>(dy, x, gv, slab);                 \
+  } while (0)
+    if (wg3v2_co_tile(Cout) == 128) WG3V2_LAUNCH(128);
+    else WG3V2_LAUNCH(64);
+#undef WG3V2_LAUNCH
+    PDA_CHECK_HIP(hipGetLastError());
+    const int slabs = wg3v2_slabs(gv);
+    int ll = 0;
+    while (ll < 4 && (slabs >> ll) > 16) ++ll;
+    const int64_t per_block = 256 >> ll;
+    const int64_t gr = (M * Nn / 4 + per_block - 1) / per_block;
+    splitk_reduce_kernel<<<(unsigned)gr, 256, 0, st>>>(slab, slabs, M, Nn, ll, epi);
+    return hipGetLastError();
+  }
   Wg3Geom g3;
   if (slab && P == H && Q == W && wg3_geom(N, H, W, C, Cout, R, S, stride, pad, dil, g3)) {
     const int splits = wg3_splits(g3);

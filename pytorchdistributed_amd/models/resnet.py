@@ -127,7 +127,7 @@ class Stem(tnn.Module):
             # (the space-to-depth image is sized so the 4x4 valid conv yields exactly ceil(H/2) x ceil(W/2))
             bn = self.bn1
             if pnn._EPILOGUE_STATS and bn.training and x2.dtype == torch.bfloat16:
-                table = bn.stat_table(x2.device)
+                table = bn.stat_table(x2.device, x2.shape[0] * (x2.shape[1] - 3) * (x2.shape[2] - 3))
                 y = ops.conv2d_bn_stats(x2, w2, 1, 0, 1, bn.running_mean, table)
                 mp = self.maxpool
                 if _STEM_BN_POOL:  # BN + ReLU applied inside the pool's loads: the BN output is never stored

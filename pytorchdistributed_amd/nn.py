@@ -20,6 +20,23 @@ _EPILOGUE_STATS = os.environ.get("PDA_BN_EPILOGUE_STATS", "1") == "1"
 _STAT_ROWS = int(os.environ.get("PDA_BN_STAT_ROWS", "64"))
 
 
+def deterministic() -> bool:
+    """``PDA_DETERMINISTIC=1``: bit-reproducible training steps.  The only order-dependent reductions of
+    the ResNet path are the BatchNorm sums the conv epilogues add atomically into a statistics table
+    (forward) and the dgrad epilogues into the backward table: tile t adds into row t % R.  With R at
+    least the number of output-row tiles (64-row tiles are the smallest), every row receives exactly one
+    add per column (0 + v is exact) and the finalize sums the rows in a fixed order.  Split-K weight
+    gradients already reduce fp32 slabs in a fixed order; everything else is elementwise or slab-based."""
+    return os.environ.get("PDA_DETERMINISTIC", "0") == "1"
+
+
+def stat_rows(m_rows: int) -> int:
+    """Rows of a BN sums table for a conv output of ``m_rows`` pixels (see :func:`deterministic`)."""
+    if deterministic():
+        return max(_STAT_ROWS, (int(m_rows) + 63) // 64)
+    return _STAT_ROWS
+
+
 def _kaiming_uniform_(w: torch.Tensor, fan_in: int):
     bound = 1.0 / math.sqrt(fan_in) * math.sqrt(3.0) * math.sqrt(2.0 / (1 + 5))
     with torch.no_grad():
@@ -70,7 +87,10 @@ class Conv2d(tnn.Module):
         if bn is not None:
             if (_EPILOGUE_STATS and x.is_cuda and bn.training and self.bias is None and not relu
                     and x.dtype == torch.bfloat16):
-                table = bn.stat_table(x.device)
+                k, st_, pd = self.kernel_size, self.stride, self.padding
+                P = (x.shape[1] + 2 * pd - self.dilation * (k - 1) - 1) // st_ + 1
+                Q = (x.shape[2] + 2 * pd - self.dilation * (k - 1) - 1) // st_ + 1
+                table = bn.stat_table(x.device, x.shape[0] * P * Q)
                 y = ops.conv2d_bn_stats(x, self.weight, self.stride, self.padding, self.dilation,
                                         bn.running_mean, table, grad_join)
                 return y, (table, bn.running_mean)
@@ -98,25 +118,27 @@ class BatchNorm2d(tnn.Module):
         self.register_buffer("running_var", torch.ones(num_features, device=device))
         self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long, device=device))
 
-    def stat_table(self, device) -> torch.Tensor:
+    def stat_table(self, device, m_rows: int = 0) -> torch.Tensor:
         """Zeroed [R, 2, C] fp32 table that the producing conv's epilogue accumulates this BN's batch
         sums into (output tile t adds into row t % R, spreading the atomics over R rows) and that the
         BN finalize reads and re-zeroes — so it is zero between uses and needs no per-step memset.
         Not a registered buffer: never saved, broadcast or all-reduced."""
         t = getattr(self, "_stat_table", None)
-        if t is None or t.device != torch.device(device):
-            t = torch.zeros(_STAT_ROWS, 2, self.num_features, device=device)
+        rows = stat_rows(m_rows)
+        if t is None or t.device != torch.device(device) or t.shape[0] != rows:
+            t = torch.zeros(rows, 2, self.num_features, device=device)
             self._stat_table = t
         return t
 
-    def bwd_table(self, device):
+    def bwd_table(self, device, m_rows: int = 0):
         """(table, token) for the backward reduction fused into the consuming conv's dgrad epilogue
         (ops/grad_join.py:BnBwdStats): a zeroed [R, 2, C] fp32 table the epilogue accumulates into and the BN
         backward finalize re-zeroes, and the [filled] flag; a table some dgrad filled without a BN backward
         consuming it (aborted backward) is re-zeroed here before it is handed out again."""
         t = getattr(self, "_bwd_table", None)
-        if t is None or t.device != torch.device(device):
-            t = torch.zeros(_STAT_ROWS, 2, self.num_features, device=device)
+        rows = stat_rows(m_rows)
+        if t is None or t.device != torch.device(device) or t.shape[0] != rows:
+            t = torch.zeros(rows, 2, self.num_features, device=device)
             self._bwd_table, self._bwd_token = t, [False]
         elif self._bwd_token[0]:
             t.zero_()
@@ -139,7 +161,7 @@ class BatchNorm2d(tnn.Module):
             x, stats = x
         bt = None
         if fuse_bwd_stats and self.training and x.is_cuda and x.dtype == torch.bfloat16 and relu:
-            bt = self.bwd_table(x.device)
+            bt = self.bwd_table(x.device, x.numel() // x.shape[-1])
         return ops.batch_norm(x, self.weight, self.bias, self.running_mean, self.running_var, self.training,
                               self.momentum, self.eps, residual=residual, relu=relu, residual_join=residual_join,
                               stats=stats, num_batches_tracked=self.num_batches_tracked, bwd_table=bt)

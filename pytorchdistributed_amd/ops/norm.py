@@ -168,7 +168,8 @@ def batch_norm_dual(x, bn, x2, bn2, stats, stats2, fuse_bwd_stats: bool = False)
     (t1, s1), (t2, s2) = stats, stats2
     bt = None
     if fuse_bwd_stats and _BWD_EPILOGUE and torch.is_grad_enabled():
-        bt = (bn.bwd_table(x.device), bn2.bwd_table(x.device))
+        m = x.numel() // x.shape[-1]
+        bt = (bn.bwd_table(x.device, m), bn2.bwd_table(x.device, m))
     y = _DualBatchNormFn.apply(x, bn.weight, bn.bias, x2, bn2.weight, bn2.bias, bn.running_mean, bn.running_var,
                                bn2.running_mean, bn2.running_var, t1, s1, t2, s2, bn.num_batches_tracked,
                                bn2.num_batches_tracked, bn.momentum, bn.eps, bt)

@@ -294,6 +294,16 @@ CONV_CASES = [
     (2, 20, 40, 16, 128, 4, 1, 0),      # stem wgrad with two output-channel tiles, rows of 37 pixels
     (2, 115, 115, 16, 64, 4, 1, 0),     # the ResNet-50 stem shape (112-pixel rows padded to 128)
     (4, 14, 14, 1024, 256, 1, 1, 0),    # 1x1 dgrad on the transposed weight (K-major B), wide tile
+    # 3x3 weight gradient v2 (conv3x3_wg_kernel): every ResNet-50 3x3 layer shape (small batch), the
+    # strided ones included, 64- and 128-channel output tiles, ragged last row groups
+    (3, 56, 56, 64, 64, 3, 1, 1),       # 2 rows (112 px) per K-step, 64-channel tile (pixel-half parities)
+    (2, 28, 28, 128, 128, 3, 1, 1),     # 4 rows per step, 128-channel tile, 2 ci blocks
+    (3, 14, 14, 256, 256, 3, 1, 1),     # 9 + 5 rows per image
+    (4, 7, 7, 512, 512, 3, 1, 1),       # one image per step (49 px)
+    (2, 56, 56, 128, 128, 3, 2, 1),     # stride 2: 2 output rows, a 5-row band of 58 pixels
+    (2, 28, 28, 256, 256, 3, 2, 1),
+    (3, 14, 14, 512, 512, 3, 2, 1),
+    (2, 9, 13, 64, 192, 3, 2, 1),       # odd sizes, 64-channel output tiles x 3
 ]
 
 
