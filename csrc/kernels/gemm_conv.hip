@@ -2458,7 +2458,10 @@ int wg3v2_co_tile(int Cout) { return Cout % 128 == 0 ? 128 : 64; }
 bool wg3v2_geom(int N, int H, int W, int C, int Cout, int R, int S, int P, int Q, int stride, int pad, int dil,
                 Wg3v2Geom& g) {
   if (!wg3v2_mode_on() || R != 3 || S != 3 || pad != 1 || dil != 1 || (stride != 1 && stride != 2)) return false;
-  if (C % 64 || Cout % 64 || Q > 128 || H < 1 || W < 1) return false;
+  // Q >= 14: at 7-pixel output rows (7^2, and 14^2 -> 7^2 strided) a 49-pixel row group wastes 23 % of its
+  // two halves and the implicit GEMM's split-K 256 x 256 tile measured 9 % faster
+  // (profiles/r5_conv_wgrad_v2_table.jsonl)
+  if (C % 64 || Cout % 64 || Q > 128 || Q < 14 || H < 1 || W < 1) return false;
   if (P != (H - 1) / stride + 1 || Q != (W - 1) / stride + 1) return false;
   // rows per K-step: the fewest 32-pixel halves per image among the rk whose dy (<= 128 px) and band
   // (<= 320 px) fit a stage; every step runs NH = ceil(rk Q / 32) halves (even for the 64-channel tile,

@@ -39,6 +39,9 @@ from .. import distributed as pdist
 from ..utils import watchdog as _watchdog
 
 _nullctx = contextlib.nullcontext
+# PDA_PP_SYNC_P2P=1: every native P2P group is waited on by the compute stream right after it is enqueued
+# (round-4 behaviour, for A/B traces: tools/overlap_report.py)
+_SYNC_P2P = os.environ.get("PDA_PP_SYNC_P2P") == "1"
 
 
 # ------------------------------------------------------------------ schedules (pure functions)
@@ -305,6 +308,9 @@ class Pipeline:
             return None
         if self._ncomm is not None:
             w = self._native_group(sends, recvs, what)
+            if _SYNC_P2P:  # A/B knob: the round-4 behaviour (the compute stream waits on every group at once)
+                w.wait()
+                return None
             return _P2PWork(native=w) if recvs else None
         ops = [dist.P2POp(dist.isend, t.contiguous(), r, group=self.group) for t, r in sends]
         ops += [dist.P2POp(dist.irecv, t, r, group=self.group) for t, r in recvs]

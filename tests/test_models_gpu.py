@@ -409,3 +409,41 @@ def test_bottleneck_bwd_stats_from_dgrad_epilogue(monkeypatch):
     for (n, pr), pb, gf, gu in zip(pair_ref.named_parameters(), pair_b16.parameters(), grads[True][1:], grads[False][1:]):
         assert rel_err(gf, pr.grad) < max(2e-2, 1.5 * rel_err(pb.grad, pr.grad)), n
         assert rel_err(gf, gu) < 1e-2, n
+
+
+def test_deterministic_mode_bit_identical(monkeypatch):
+    """PDA_DETERMINISTIC=1: two runs of the same ResNet-50 steps (DDP flat buffers,
+    fused SGD, BN sums from the conv / dgrad epilogues, side-stream split-K weight gradients) end with
+    bit-identical parameters and losses — every BN sums table gets one row per output tile, so no two
+    atomic adds meet in one element."""
+    from pytorchdistributed_amd.models.resnet import resnet50
+    from pytorchdistributed_amd.ops import cross_entropy
+    from pytorchdistributed_amd.optim import SGD
+    from pytorchdistributed_amd.parallel.ddp import DistributedDataParallel
+
+    monkeypatch.setenv("PDA_DETERMINISTIC", "1")
+
+    def run():
+        torch.manual_seed(0)
+        base = resnet50(device="cuda", dtype=torch.bfloat16)
+        model = DistributedDataParallel(base, device_ids=[0])
+        opt = SGD(model.parameters(), lr=0.05, momentum=0.9, weight_decay=5e-5)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        x = torch.randn(24, 112, 112, 3, device="cuda", generator=g).to(torch.bfloat16)
+        y = torch.randint(0, 1000, (24,), device="cuda", generator=g)
+        losses = []
+        for _ in range(3):
+            opt.zero_grad()
+            loss = cross_entropy(model(x), y)
+            loss.backward()
+            opt.step()
+            losses.append(loss.detach().float().clone())
+        torch.cuda.synchronize()
+        return [p.detach().clone() for p in base.parameters()], torch.stack(losses), \
+            [b.detach().clone() for b in base.buffers()]
+
+    p1, l1, b1 = run()
+    p2, l2, b2 = run()
+    assert torch.equal(l1, l2), (l1, l2)
+    assert all(torch.equal(a, b) for a, b in zip(p1, p2))
+    assert all(torch.equal(a, b) for a, b in zip(b1, b2))

@@ -15,7 +15,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-COPY_OPS = {"aten::copy_", "aten::_to_copy", "aten::clone", "aten::contiguous", "aten::to", "aten::cat"}
+COPY_OPS = {"aten::copy_", "aten::_to_copy", "aten::clone", "aten::contiguous", "aten::to", "aten::cat",
+            "aten::zero_", "aten::fill_", "aten::zeros", "aten::zeros_like", "aten::new_zeros"}
 
 
 def gpt2_step(batch):
@@ -76,7 +77,7 @@ def main():
         print(f"{n / a.steps:8.1f}  {name:18s} {site}")
     kern = collections.Counter()
     for ev in prof.events():
-        if ev.device_type == torch.autograd.DeviceType.CUDA and ("copy" in ev.name.lower() or "Copy" in ev.name):
+        if ev.device_type == torch.autograd.DeviceType.CUDA and any(t in ev.name.lower() for t in ("copy", "fill")):
             kern[ev.name[:90]] += 1
     print("device copy kernels per step:")
     for k, n in kern.most_common(10):
