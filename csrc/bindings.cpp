@@ -1183,10 +1183,12 @@ void attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, T
   p.dv = bpm(dv); p.dv_sb = dv.stride(0); p.dv_st = dv.stride(1); p.dv_sh = dv.stride(2);
   rope_tables(p, rope_cos, rope_sin, T, D);
   const int64_t wsn = pda::attention_bwd_ws_floats(B, T, Hq, Hkv, D, rope_cos.has_value());
+  const int64_t dqn = pda::attention_bwd_fused(D, rope_cos.has_value()) ? (int64_t)B * Hq * T * D : 0;
   Tensor ws;
-  if (wsn > 0) {
-    ws = at::empty({wsn}, q.options().dtype(at::kFloat));
-    p.dkv_part = ws.data_ptr<float>();
+  if (wsn + dqn > 0) {
+    ws = at::empty({wsn + dqn}, q.options().dtype(at::kFloat));
+    if (wsn > 0) p.dkv_part = ws.data_ptr<float>();
+    if (dqn > 0) p.dq_acc = ws.data_ptr<float>() + wsn;
   }
   CHECK_HIP_OK(pda::attention_bwd(p, stream_of(q)));
 }
@@ -1691,6 +1693,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd", &bn_bwd);
   m.def("bn_bwd_table", &bn_bwd_table);
   m.def("set_bn_bwd_fused_max_c", &set_bn_bwd_fused_max_c);
+  m.def("set_attn_bwd_fused", [](int64_t m) { pda::attention_bwd_fused_mode() = (int)m; });
+  m.def("attn_bwd_fused_mode", []() { return (int64_t)pda::attention_bwd_fused_mode(); });
   m.def("bn_bwd_fused_max_c", []() { return bn_bwd_fused_max_c(); });
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);

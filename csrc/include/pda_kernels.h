@@ -26,6 +26,8 @@ struct AttnParams {
   int64_t dq_sb, dq_st, dq_sh, dk_sb, dk_st, dk_sh, dv_sb, dv_st, dv_sh;
   // GQA dK/dV partials per query head, fp32 [2][B][Hq][T][D] (only when Hq > Hkv; attn_bwd_ws_floats)
   float* dkv_part;
+  // fused dK/dV/dQ backward: fp32 dQ accumulator [B][Hq][T][D] (attention_bwd_fused), else null
+  float* dq_acc;
 };
 
 // ---- xgmi.hip (one-shot / two-shot all-reduce over IPC-mapped peer buffers)
@@ -285,6 +287,8 @@ int64_t colreduce_ws_floats(int64_t rows, int64_t D, int nout);
 hipError_t attention_fwd(const AttnParams& p, hipStream_t st);
 hipError_t attention_bwd(const AttnParams& p, hipStream_t st);
 int64_t attention_bwd_ws_floats(int B, int T, int Hq, int Hkv, int D, bool rope);
+bool attention_bwd_fused(int D, bool rope);
+int& attention_bwd_fused_mode();  // PDA_ATTN_BWD_FUSED bits (set_attn_bwd_fused)
 
 // ---- decode_attn.hip (serving: one query token per sequence vs a bf16 KV cache, split over the sequence)
 struct DecodeAttnParams {

@@ -13,8 +13,9 @@
 //    k-step permuted to match the S layout; V is the A operand, read with ds_read_b64_tr_b16 (T10) from
 //    an LDS image swizzled per 32-B slot so the 8 rows a half-wave reads hit distinct banks.
 //  * K tiles for the row-wise reads use a 16-B-chunk XOR swizzle (T2) -> conflict-free ds_read_b128.
-// Backward = FA2 with recomputation, split into a dQ kernel (query-stationary) and a dK/dV kernel
-// (key-stationary, looping over the query heads of its GQA group), so no atomics are needed.
+// Backward = FA2 with recomputation: at D = 64 one key-stationary kernel computes dK, dV and dQ from a
+// single P / dS per tile (dQ through an fp32 atomic accumulator, attn_bwd_dkdv2_kernel<..., FQ>); at
+// D = 128 a dQ kernel (query-stationary) plus the dK/dV kernel, no atomics.
 #include "pda_common.h"
 #include "pda_kernels.h"
 
@@ -298,26 +299,77 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_kernel(AttnParams p) {
 }
 
 // ---------------------------------------------------------------- backward: delta = rowsum(dO * O)
+// DRPT rows per thread group, all loads issued before the first use (one-shot threads are latency
+// bound: a lone 16-B load pair per thread kept this pass near 2 TB/s).  With the fused dQ path it also
+// zeroes the rows of the fp32 dQ accumulator.
+constexpr int DRPT = 4;
 template <int D>
 __global__ void __launch_bounds__(NT) attn_bwd_delta_kernel(AttnParams p) {
   constexpr int TPR = D / 8;  // threads per row
+  constexpr int RPB = NT / TPR;  // rows per block per pass
   const int64_t rows = (int64_t)p.B * p.Hq * p.T;
-  const int64_t row = (int64_t)blockIdx.x * (NT / TPR) + threadIdx.x / TPR;
   const int part = threadIdx.x % TPR;
-  float acc = 0.f;
-  if (row < rows) {
-    const int t = (int)(row % p.T);
-    const int h = (int)((row / p.T) % p.Hq);
-    const int b = (int)(row / ((int64_t)p.T * p.Hq));
-    float a[8], o[8];
-    load8(p.dout + b * p.do_sb + (int64_t)t * p.do_st + h * p.do_sh + part * 8, a);
-    load8(p.o + b * p.o_sb + (int64_t)t * p.o_st + h * p.o_sh + part * 8, o);
+  float a[DRPT][8], o[DRPT][8];
+  int64_t rr[DRPT];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc += a[j] * o[j];
+  for (int i = 0; i < DRPT; ++i) {
+    const int64_t row = ((int64_t)blockIdx.x * DRPT + i) * RPB + threadIdx.x / TPR;
+    rr[i] = row;
+    if (row < rows) {
+      const int t = (int)(row % p.T);
+      const int h = (int)((row / p.T) % p.Hq);
+      const int b = (int)(row / ((int64_t)p.T * p.Hq));
+      load8(p.dout + b * p.do_sb + (int64_t)t * p.do_st + h * p.do_sh + part * 8, a[i]);
+      load8(p.o + b * p.o_sb + (int64_t)t * p.o_st + h * p.o_sh + part * 8, o[i]);
+    }
+  }
+  if (p.dq_acc != nullptr) {  // fused-dQ accumulator rows start at zero
+#pragma unroll
+    for (int i = 0; i < DRPT; ++i)
+      if (rr[i] < rows) {
+        float4* z = reinterpret_cast<float4*>(p.dq_acc + rr[i] * D + part * 8);
+        z[0] = z[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
   }
 #pragma unroll
-  for (int off = TPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  if (row < rows && part == 0) p.delta[row] = acc;
+  for (int i = 0; i < DRPT; ++i) {
+    float acc = 0.f;
+    if (rr[i] < rows) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += a[i][j] * o[i][j];
+    }
+#pragma unroll
+    for (int off = TPR / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (rr[i] < rows && part == 0) p.delta[rr[i]] = acc;
+  }
+}
+
+// dq = scale * dq_acc ([B][Hq][T][D] fp32 from the fused dK/dV/dQ kernel), 8 columns per thread
+__global__ void __launch_bounds__(NT) attn_dq_convert_kernel(AttnParams p) {
+  const int D = p.D, T = p.T;
+  const int64_t n8 = (int64_t)p.B * p.Hq * T * (D / 8);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  constexpr int U = 4;  // chunks in flight per thread
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n8; i0 += U * stride) {
+    float v[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * stride < n8) load8(p.dq_acc + (i0 + u * stride) * 8, v[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n8) break;
+      const int c8 = (int)(i % (D / 8));
+      int64_t r = i / (D / 8);
+      const int t = (int)(r % T);
+      r /= T;
+      const int h = (int)(r % p.Hq);
+      const int b = (int)(r / p.Hq);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[u][j] *= p.scale;
+      store8(p.dq + b * p.dq_sb + (int64_t)t * p.dq_st + h * p.dq_sh + c8 * 8, v[u]);
+    }
+  }
 }
 
 // ---------------------------------------------------------------- backward: dQ (query-stationary)
@@ -917,15 +969,58 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
   }
 }
 
+// Fused-dQ step of attn_bwd_dkdv2_kernel<..., FQ>: barrier (the dS image is complete), then wave w adds
+// dS[q0 + 16 w .. +15][keys 0 .. kmax) * K into dq_acc.  kmax < BK only for causal diagonal tiles.
+template <int D, int BK, bool ATOMIC>
+__device__ __forceinline__ void fused_dq(const AttnParams& p, const char* DSt, const char* Kt, float* dqa, int q0,
+                                         int kmax, int w, int lane) {
+  constexpr int DT = D / 16;
+  __syncthreads();
+  const int nk = (kmax < BK ? kmax : BK) / 32;
+  f32x4 acc[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) acc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int kc = 0; kc < nk; ++kc) {
+    const mbf16x8 af = frag_tr<BQ>(DSt, 32 * kc, 16 * w, lane);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) acc[dt] = mfma(af, frag_tr<D>(Kt, 32 * kc, 16 * dt, lane), acc[dt]);
+  }
+  const int qb = q0 + 16 * w + 4 * (lane >> 4);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (qb + r >= p.T) break;
+    float* row = dqa + (int64_t)(qb + r) * D + (lane & 15);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      if constexpr (ATOMIC) unsafeAtomicAdd(row + 16 * dt, acc[dt][r]);
+      else row[16 * dt] = acc[dt][r];  // lab only (PDA_ATTN_BWD_FUSED bit 4): prices the atomics, wrong dQ
+    }
+  }
+}
+
 // dK / dV for one (key tile, query head): prefetched Q / dO tiles; output bf16 directly (no GQA) or
 // fp32 partials [2][B][Hq][T][D] summed over the group by attn_dkv_reduce_kernel.
 // KG key groups of 16 per wave (key tile = 64 * KG): every Q / dO fragment read from LDS and every
 // transposed Q / dO fragment feeds KG MFMAs, and each staged Q / dO tile serves 64 * KG keys.
-template <int D, int KG, bool DB = false>
+//
+// FQ (fused dQ, single-stage only): the workgroup also adds its keys' share of dQ = dS K for every query
+// tile it visits, so no query-stationary dQ kernel recomputes S and dP.  The waves' dS fragments go to
+// an LDS image transposed to [key][query] (4 consecutive queries per 8-byte store), the key tile sits in
+// LDS once as a transposed-read image, and after one extra barrier wave w multiplies query rows
+// 16 w .. 16 w + 15 of dS by K (A and B both by ds_read_b64_tr_b16, the key order permuted alike) and
+// adds the fp32 result into p.dq_acc ([B][Hq][T][D], zeroed by the delta kernel) with no-return
+// atomics; attn_dq_convert_kernel scales it into dq.  Causal: a query tile only reads the key rows
+// below its last query, which are exactly the rows of the waves that did not skip it.
+template <int D, int KG, bool DB = false, int FQ = 0>
 __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
+  static_assert(!(DB && FQ), "fused dQ is single-stage");
   constexpr int KS = D / 32, DT = D / 16, IMG = BQ * D * 2, BK = BKV * KG;
   constexpr int STAGE = 4 * IMG + 2 * BQ * 4;  // Q row / Q tr / dO row / dO tr images + lse / delta
-  __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * STAGE];
+  constexpr int KIMG = FQ ? BK * D * 2 : 0, DSIMG = FQ ? BK * BQ * 2 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * STAGE + KIMG + DSIMG];
+  char* const Kt = smem + STAGE;        // [BK keys][D] transposed-read image (FQ)
+  char* const DSt = smem + STAGE + KIMG;  // [BK keys][BQ queries] transposed-read image of dS (FQ)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int kt = blockIdx.x, hq = blockIdx.y, b = blockIdx.z;
   const int T = p.T, G = p.Hq / p.Hkv, hk = hq / G;
@@ -940,6 +1035,10 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
       kf[kg][ks] = load_frag_global(kb, p.k_st, kvbase + 16 * kg + (lane & 15), T, ks, lane);
       vf[kg][ks] = load_frag_global(vb, p.v_st, kvbase + 16 * kg + (lane & 15), T, ks, lane);
     }
+  if constexpr (FQ) {  // visible after the first loop barrier
+#pragma unroll
+    for (int h = 0; h < KG; ++h) stage_tile<D, false, true>(kb, p.k_st, kt * BK + 64 * h, T, nullptr, Kt + h * 64 * D * 2);
+  }
   const float c = p.scale * LOG2E;
   f32x4 dk[KG][DT], dv[KG][DT];
 #pragma unroll
@@ -947,6 +1046,7 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) dk[kg][dt] = dv[kg][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int q_begin = p.causal ? kt * BK : 0;
+  float* const dqa = FQ ? p.dq_acc + ((int64_t)b * p.Hq + hq) * T * D : nullptr;
   const bf16_t* qb = p.q + b * p.q_sb + hq * p.q_sh;
   const bf16_t* dob = p.dout + b * p.do_sb + hq * p.do_sh;
   const float* lse = p.lse + ((int64_t)b * p.Hq + hq) * T;
@@ -1009,6 +1109,10 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
     }
     // every query of this tile is before all of this wave's keys: nothing to add (wave-uniform)
     if (p.causal && q0 + BQ - 1 < kvbase) {
+      if constexpr (FQ) {
+        fused_dq<D, BK, FQ == 1>(p, DSt, Kt, dqa, q0, q0 + BQ - kt * BK, w, lane);
+        continue;
+      }
       if constexpr (DB) __syncthreads();
       continue;
     }
@@ -1055,6 +1159,23 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
         pf[cc][kg] = pack_p(s[kg][2 * cc], s[kg][2 * cc + 1]);
         sf[cc][kg] = pack_p(dp[kg][2 * cc], dp[kg][2 * cc + 1]);
       }
+    if constexpr (FQ) {  // dS^T -> LDS: key row kl, queries 16 t + 4 g .. +3 (one 8-byte store each)
+      const int kl = w * 16 * KG + (lane & 15);
+      const int sw = (kl >> 1) & 3;
+      char* const rowp = DSt + kl * (BQ * 2) + 8 * g;
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          char* const a = rowp + (((2 * cc + h) ^ sw) << 5);
+#pragma unroll
+          for (int kg = 0; kg < KG; ++kg) {
+            const s16x8 v = __builtin_bit_cast(s16x8, sf[cc][kg]);
+            *reinterpret_cast<s16x4*>(a + kg * 16 * (BQ * 2)) =
+                h ? s16x4{v[4], v[5], v[6], v[7]} : s16x4{v[0], v[1], v[2], v[3]};
+          }
+        }
+    }
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
 #pragma unroll
@@ -1068,6 +1189,7 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
         }
       }
     }
+    if constexpr (FQ) fused_dq<D, BK, FQ == 1>(p, DSt, Kt, dqa, q0, p.causal ? q0 + BQ - kt * BK : BK, w, lane);
     if constexpr (DB) __syncthreads();
   }
 #pragma unroll
@@ -1190,11 +1312,25 @@ int64_t attention_bwd_ws_floats(int B, int T, int Hq, int Hkv, int D, bool rope)
   return (!rope && Hq > Hkv) ? (int64_t)2 * B * Hq * T * D : 0;
 }
 
+// PDA_ATTN_BWD_FUSED bit 0: fused dK/dV/dQ kernel at D = 64, bit 1: at D = 128 (else the dQ kernel +
+// dK/dV kernel pair); bit 4: lab store mode (plain stores instead of the dQ atomics — wrong dQ, prices
+// the atomics).  Measured (profiles/r5_attn_bwd_fused.jsonl): GPT-2-medium 326.1 / 321.8 k vs 315.3 /
+// 318.1 k tok/s on one box; microbench backward 0.4065 vs 0.4176 ms (atomics ~0.05 ms of it).  At
+// D = 128 the fused kernel needs 88.5 KB of LDS (one workgroup per CU): Llama-3-8B 16.9 k vs 18.6 k, off.
+int& attention_bwd_fused_mode() {
+  static int mode = [] {
+    const char* e = getenv("PDA_ATTN_BWD_FUSED");
+    return e ? atoi(e) : 1;
+  }();
+  return mode;
+}
+bool attention_bwd_fused(int D, bool rope) { return !rope && (attention_bwd_fused_mode() & (D == 64 ? 1 : 2)) != 0; }
+
 hipError_t attention_bwd(const AttnParams& p, hipStream_t st) {
   if (p.D != 64 && p.D != 128) return hipErrorInvalidValue;
   if (p.Hkv <= 0 || p.Hq % p.Hkv) return hipErrorInvalidValue;
   const int64_t rows = (int64_t)p.B * p.Hq * p.T;
-  const int rows_per_block = NT / (p.D / 8);
+  const int rows_per_block = DRPT * NT / (p.D / 8);
   const unsigned dgrid = (unsigned)((rows + rows_per_block - 1) / rows_per_block);
   if (p.D == 128) attn_bwd_delta_kernel<128><<<dgrid, NT, 0, st>>>(p);
   else attn_bwd_delta_kernel<64><<<dgrid, NT, 0, st>>>(p);
@@ -1203,6 +1339,30 @@ hipError_t attention_bwd(const AttnParams& p, hipStream_t st) {
   if (p.rope_cos == nullptr) {
     dim3 gq2((p.T + 2 * BQ - 1) / (2 * BQ), p.Hq, p.B);
     if (p.Hq > p.Hkv && p.dkv_part == nullptr) return hipErrorInvalidValue;
+    if (p.dq_acc != nullptr) {  // fused dK / dV / dQ (attention_bwd_fused)
+      const bool lab_store = (attention_bwd_fused_mode() & 16) != 0;
+      if (p.D == 128) {
+        const dim3 gk((p.T + BKV - 1) / BKV, p.Hq, p.B);
+        attn_bwd_dkdv2_kernel<128, 1, false, 1><<<gk, NT, 0, st>>>(p);
+      } else {
+        const dim3 gk((p.T + 2 * BKV - 1) / (2 * BKV), p.Hq, p.B);
+        if (lab_store) attn_bwd_dkdv2_kernel<64, 2, false, 2><<<gk, NT, 0, st>>>(p);
+        else attn_bwd_dkdv2_kernel<64, 2, false, 1><<<gk, NT, 0, st>>>(p);
+      }
+      PDA_CHECK_HIP(hipGetLastError());
+      const int64_t n8 = (int64_t)p.B * p.Hq * p.T * (p.D / 8);
+      int64_t g = (n8 + 4 * NT - 1) / (4 * NT);
+      if (g > 4096) g = 4096;
+      attn_dq_convert_kernel<<<(unsigned)g, NT, 0, st>>>(p);
+      PDA_CHECK_HIP(hipGetLastError());
+      if (p.Hq > p.Hkv) {
+        const int64_t m8 = (int64_t)2 * p.B * p.Hkv * p.T * (p.D / 8);
+        int64_t gm = (m8 + NT - 1) / NT;
+        if (gm > 8192) gm = 8192;
+        attn_dkv_reduce_kernel<<<(unsigned)gm, NT, 0, st>>>(p);
+      }
+      return hipGetLastError();
+    }
     static const int db = [] {  // bit 0: dQ kernel double-buffered, bit 1: dK/dV kernel
       const char* e = getenv("PDA_ATTN_BWD_DB");
       return e ? atoi(e) : 0;

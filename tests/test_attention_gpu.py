@@ -41,6 +41,42 @@ def test_flash_attention_fwd_bwd(B, T, Hq, Hkv, D, causal, use_rope):
     assert rel_err(g[:, :, Hq + Hkv:], r[:, :, Hq + Hkv:]) < 3e-2      # dv
 
 
+@pytest.mark.parametrize("B,T,Hq,Hkv,D,causal", [(2, 128, 4, 4, 64, True), (1, 200, 4, 2, 128, True),
+                                                  (2, 64, 2, 2, 128, False), (1, 256, 8, 1, 64, True),
+                                                  (1, 96, 2, 2, 64, False), (1, 200, 4, 2, 64, True),
+                                                  (2, 72, 2, 1, 64, True), (1, 330, 2, 2, 64, False),
+                                                  (1, 520, 4, 1, 128, True), (2, 384, 4, 4, 64, True)])
+def test_flash_attention_bwd_fused_dq(B, T, Hq, Hkv, D, causal):
+    """Fused key-stationary backward (dQ through the fp32 atomic accumulator, PDA_ATTN_BWD_FUSED) vs
+    the fp32 reference and vs the two-kernel path."""
+    from pytorchdistributed_amd._native import C
+    from pytorchdistributed_amd.ops.attention import attention_qkv, attention_ref
+
+    torch.manual_seed(1)
+    qkv = torch.randn(B, T, Hq + 2 * Hkv, D).to(torch.bfloat16)
+    ref_in = qkv.float().clone().requires_grad_()
+    q, k, v = ref_in[:, :, :Hq], ref_in[:, :, Hq:Hq + Hkv], ref_in[:, :, Hq + Hkv:]
+    o_ref = attention_ref(q, k, v, causal, 1 / math.sqrt(D), None)
+    do = torch.randn_like(o_ref)
+    o_ref.backward(do)
+    grads = {}
+    old = C().attn_bwd_fused_mode()
+    try:
+        for mode in (0, 3):
+            C().set_attn_bwd_fused(mode)
+            g_in = qkv.cuda().requires_grad_()
+            o = attention_qkv(g_in, Hq, Hkv, causal=causal)
+            o.backward(do.cuda().to(torch.bfloat16))
+            grads[mode] = g_in.grad.cpu().float()
+    finally:
+        C().set_attn_bwd_fused(old)
+    g, r = grads[3], ref_in.grad
+    assert torch.isfinite(g).all()
+    for sl in (slice(0, Hq), slice(Hq, Hq + Hkv), slice(Hq + Hkv, Hq + 2 * Hkv)):  # dq, dk, dv
+        assert rel_err(g[:, :, sl], r[:, :, sl]) < 3e-2
+        assert rel_err(g[:, :, sl], grads[0][:, :, sl]) < 1e-2
+
+
 def test_embedding_and_rope_kernels():
     from pytorchdistributed_amd._native import C
     from pytorchdistributed_amd.ops import embedding
