@@ -531,7 +531,10 @@ __device__ __forceinline__ void raw_barrier() {
 // that are in flight survive the epilogue (a __syncthreads() would wait for them with vmcnt(0)).
 // DEFER: the BN sums of this tile are ADDED into the caller's st1 / st2 (this thread's fixed column
 // chunk) instead of being flushed — a workgroup walking several tiles flushes once (epi_stats_flush).
-template <int BM, int BN, bool RAW = false, bool DEFER = false>
+// BST: compile the BN-backward sums path (epi.bst_z).  Off, the epilogue's register peak stays below the
+// K loop's: the 128x64 tile keeps 114 VGPRs and 3 workgroups per CU (173 and 2 with the path compiled
+// in: the 56^2 64-channel convs ran 20-25 % slower, profiles/r5_conv_table_bs640.jsonl).
+template <int BM, int BN, bool RAW = false, bool DEFER = false, bool BST = true>
 __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 32][BN / 32], char* smem,
                                                         const Epi& epi, int64_t m0, int64_t n0, int64_t M, int64_t N,
                                                         int tm, float (&st1)[8], float (&st2)[8]) {
@@ -580,10 +583,9 @@ __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 
   float st3[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) st3[q] = 0.f;
-  if (epi.bst_z) {
-    epi_bst_chunks<BM, CPR, NT>(
-        epi, scol, [&](int r, int ch) { return *reinterpret_cast<const u16x8*>(stg + r * SROW + ch * 8); }, m0, n0,
-        M, N, st1, st2, st3);
+  if (BST && epi.bst_z) {
+    auto rd = [&](int r, int ch) { return *reinterpret_cast<const u16x8*>(stg + r * SROW + ch * 8); };
+    epi_bst_chunks<BM, CPR, NT, decltype(rd), BN == 64 ? 2 : 4>(epi, scol, rd, m0, n0, M, N, st1, st2, st3);
   } else
 #pragma unroll
   for (int c = tid; c < BM * CPR; c += NT) {
@@ -607,17 +609,17 @@ __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 
   }
 }
 
-template <int BM, int BN, bool RAW = false>
+template <int BM, int BN, bool RAW = false, bool BST = true>
 __device__ __forceinline__ void tile_epilogue_bf16(const f32x4 (&acc)[BM / 32][BN / 32], char* smem, const Epi& epi,
                                                    int64_t m0, int64_t n0, int64_t M, int64_t N, int tm) {
   float st1[8], st2[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) st1[q] = st2[q] = 0.f;
-  tile_epilogue_bf16_impl<BM, BN, RAW, false>(acc, smem, epi, m0, n0, M, N, tm, st1, st2);
+  tile_epilogue_bf16_impl<BM, BN, RAW, false, BST>(acc, smem, epi, m0, n0, M, N, tm, st1, st2);
 }
 
 // ------------------------------------------------------------------ the kernel
-template <int BM, int BN, class LA, class LB>
+template <int BM, int BN, class LA, class LB, bool BST = false>
 __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, int64_t N, int64_t K, int tiles_n,
                                                      int ktiles_per_split, Epi epi) {
   constexpr int WM = BM / 2, WN = BN / 2;
@@ -690,7 +692,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
   if (!epi.slab && !epi.c_f32) {
     static_assert(BM * (BN + 8) * 2 + (NT / 64) * BN * 2 * 4 <= 2 * (A_BYTES + B_BYTES),
                   "staging tile + stats scratch must fit the operand LDS");
-    tile_epilogue_bf16<BM, BN>(acc, smem, epi, m0, n0, M, N, tm);
+    tile_epilogue_bf16<BM, BN, false, BST>(acc, smem, epi, m0, n0, M, N, tm);
     return;
   }
 #pragma unroll
@@ -1327,7 +1329,7 @@ __global__ void __launch_bounds__(NT, 2) conv_stem_fwd_kernel(const bf16_t* __re
       }
     raw_barrier();  // every wave is done reading the band: it becomes the staging tile
     const int64_t m0 = (int64_t)row * g.Q;
-    tile_epilogue_bf16_impl<128, 64, true, true>(acc, band, epi, m0, 0, m0 + g.Q, 64, row, st1, st2);
+    tile_epilogue_bf16_impl<128, 64, true, true, false>(acc, band, epi, m0, 0, m0 + g.Q, 64, row, st1, st2);
   };
   issue(rb, s_b0);
   for (int row = rb; row < re; row += 2) {
@@ -1948,14 +1950,37 @@ Plan plan_wgrad(int64_t M, int64_t N, int64_t K, bool allow_split) {
   return plan_gemm(M, N, K, allow_split, 2 * wgrad_cus(), (int)cap);
 }
 
+// loaders whose GEMM can be a conv data gradient (the only producers of BN-backward sums; a stride-1
+// 3x3 dgrad is a forward conv over flipped weights)
+template <class L> struct BstLoader : std::false_type {};
+template <int R> struct BstLoader<ConvFwdK<R>> : std::true_type {};
+template <int R> struct BstLoader<ConvFwdKU<R>> : std::true_type {};
+template <int R> struct BstLoader<PlainK<R>> : std::true_type {};
+template <int R> struct BstLoader<PlainMN<R>> : std::true_type {};
+template <int R> struct BstLoader<ConvDgradK<R>> : std::true_type {};
+template <int R> struct BstLoader<ConvDgradPhaseK<R>> : std::true_type {};
+template <int R> struct BstLoader<ConvDgradPhaseKU<R>> : std::true_type {};
+
 template <int BM, int BN, class LA, class LB>
 hipError_t launch(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, const Plan& p, Epi epi,
                   float* slab, hipStream_t st) {
   const int ntiles = p.tiles_m * p.tiles_n;
   Epi e = epi;
   if (p.splits > 1) e.slab = slab;
-  gemm_kernel<BM, BN, LA, LB><<<dim3(ntiles, p.splits), NT, 0, st>>>(la, lb, M, N, K, p.tiles_n,
-                                                                     p.ktiles_per_split, e);
+  static const bool lean = [] {  // PDA_EPI_BST_LEAN=0: every launch takes the BN-backward-sums build (A/B)
+    const char* v = getenv("PDA_EPI_BST_LEAN");
+    return !(v && v[0] == '0');
+  }();
+  if (e.bst_z || (!lean && BstLoader<LA>::value)) {  // BN-backward sums: only the data-gradient loaders produce a BN input's gradient
+    if constexpr (BstLoader<LA>::value)
+      gemm_kernel<BM, BN, LA, LB, true><<<dim3(ntiles, p.splits), NT, 0, st>>>(la, lb, M, N, K, p.tiles_n,
+                                                                               p.ktiles_per_split, e);
+    else
+      return hipErrorNotSupported;
+  } else {
+    gemm_kernel<BM, BN, LA, LB><<<dim3(ntiles, p.splits), NT, 0, st>>>(la, lb, M, N, K, p.tiles_n,
+                                                                       p.ktiles_per_split, e);
+  }
   PDA_CHECK_HIP(hipGetLastError());
   if (p.splits > 1) {
     int ll = 0;  // split lanes per output: ~16 slabs per lane, at most 16 lanes

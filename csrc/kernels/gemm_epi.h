@@ -163,12 +163,14 @@ __device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
 // out-of-range chunks; the flags and pointers are selected once, not per load: a per-element "load or not"
 // branch would wait vmcnt(0) per element), and then the G chunks are finished and stored.
 //   stg_read(r, ch): the staged bf16 values of tile row r, column chunk ch.
-template <int ROWS, int CPR, int NT, class StgRead>
+//   GMAX: chunks per load group (a 64-column tile takes 2: its kernel then stays within 168 VGPRs, three
+//   workgroups per CU)
+template <int ROWS, int CPR, int NT, class StgRead, int GMAX = 4>
 __device__ __forceinline__ void epi_bst_chunks(const Epi& e, const EpiStatCols& sc, StgRead stg_read, int64_t m0,
                                                int64_t n0, int64_t M, int64_t N, float (&st1)[8], float (&st2)[8],
                                                float (&st3)[8]) {
   constexpr int ITERS = ROWS * CPR / NT;
-  constexpr int G = ITERS < 4 ? ITERS : 4;  // (8 pushed the gathered wide-tile kernels into scratch)
+  constexpr int G = ITERS < GMAX ? ITERS : GMAX;  // (8 pushed the gathered wide-tile kernels into scratch)
   static_assert(ITERS % G == 0, "groups cover the tile");
   const int tid = threadIdx.x;
   const bool has_add = e.addend != nullptr, use_bits = e.bst_bits != nullptr;

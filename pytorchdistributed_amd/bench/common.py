@@ -159,6 +159,19 @@ def comm_record(mod, steps: int) -> dict:
     return out
 
 
+def mem_record(device) -> dict:
+    """Caching-allocator figures for the JSON line: peak allocated / reserved GiB and the number of
+    allocation retries (a retry frees the cache and synchronises the device: a step that needs them
+    is allocator-bound, not compute- or comm-bound)."""
+    if device is None or getattr(device, "type", "cpu") != "cuda":
+        return {}
+    st = torch.cuda.memory_stats(device)
+    gib = 2 ** 30
+    return {"peak_alloc_gib": round(st.get("allocated_bytes.all.peak", 0) / gib, 1),
+            "peak_reserved_gib": round(st.get("reserved_bytes.all.peak", 0) / gib, 1),
+            "alloc_retries": int(st.get("num_alloc_retries", 0))}
+
+
 def emit(record: dict, rank: int):
     if rank == 0:
         print(json.dumps(record), flush=True)

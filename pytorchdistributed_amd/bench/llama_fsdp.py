@@ -14,7 +14,7 @@ from ..data.device import DeviceSyntheticTokens
 from ..models.llama import Llama, LlamaBlock, config
 from ..optim import AdamW
 from ..parallel.fsdp import FullyShardedDataParallel
-from .common import comm_record, emit, setup, teardown, timed
+from .common import comm_record, emit, mem_record, setup, teardown, timed
 
 
 def main(argv=None):
@@ -52,6 +52,7 @@ def main(argv=None):
           "unit": "tokens/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
           "ms_per_step": round(secs / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
           "vs_baseline": None, "dtype": "bf16", "data": "synthetic tokens (on-device), random-init weights", "comm": comm,
+          "mem": mem_record(device),
           "config": {"model": a.model + ("" if a.layers is None else f"-{a.layers}L"),
                      "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": f"fsdp{world}",
                      "params": n_params}}, rank)
