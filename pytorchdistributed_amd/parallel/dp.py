@@ -4,9 +4,12 @@ forward at 139-145: replicate -> scatter -> parallel_apply -> gather).
 
 MI355X version:
 * the module is explicitly moved to ``device_ids[0]`` (the reference never moves it, SURVEY A12);
-* replication is a functional call with per-device parameter copies (peer copies over xGMI issued
-  on per-device streams); autograd's copy-backward reduce-adds every replica's gradient into the
-  master parameters on ``device_ids[0]`` (the reference's PS-style "reduce grads to master");
+* replication is a functional call with coalesced per-device parameter copies: the parameters of one
+  dtype are concatenated once on ``device_ids[0]`` and each other device receives ONE peer copy over
+  xGMI (buffers likewise, without autograd), which it views as its replica's tensors — not one copy per
+  tensor (torch's ``Broadcast`` / ``broadcast_coalesced`` idea); autograd's copy- and cat-backward
+  reduce-add every replica's gradient into the master parameters on ``device_ids[0]`` (the
+  reference's PS-style "reduce grads to master");
 * the per-device forwards run in one Python thread per device, each on its own device/stream;
 * outputs are gathered (concatenated) on ``output_device``.
 ``device_ids`` may also list CPU devices (used by the CPU tests to exercise the same code path).
@@ -66,13 +69,36 @@ class DataParallel(tnn.Module):
         self.dim = dim
         self.module = module.to(self.devices[0])
 
-    def _replica_state(self, dev: torch.device):
-        state = {}
-        for name, p in self.module.named_parameters():
-            state[name] = p if p.device == dev else p.to(dev, non_blocking=True)
-        for name, b in self.module.named_buffers():
-            state[name] = b if b.device == dev else b.to(dev, non_blocking=True)
-        return state
+    # tests set this to copy even to the master's own device (the CPU tier has one device type)
+    _force_copy = False
+
+    def _replica_states(self, devs: Sequence[torch.device]) -> List[dict]:
+        """Parameter / buffer dicts for functional_call on every device: the master's tensors on
+        ``devs[0]``; elsewhere views of one coalesced copy per dtype (parameters through autograd, so
+        gradients flow back to the master; buffers without)."""
+        states = [dict() for _ in devs]
+        named = [(n, p, True) for n, p in self.module.named_parameters()] + \
+                [(n, b, False) for n, b in self.module.named_buffers()]
+        for n, t, _ in named:
+            states[0][n] = t
+        targets = [i for i in range(1, len(devs)) if self._force_copy or devs[i] != devs[0]]
+        for i in range(1, len(devs)):
+            if i not in targets:
+                states[i] = dict(states[0])
+        if not targets:
+            return states
+        groups = {}
+        for n, t, is_param in named:
+            groups.setdefault((t.dtype, t.device, is_param), []).append((n, t))
+        for (_dt, _dev, is_param), items in groups.items():
+            with torch.set_grad_enabled(is_param and torch.is_grad_enabled()):
+                flat = torch.cat([t.reshape(-1) for _, t in items]) if len(items) > 1 else items[0][1].reshape(-1)
+                sizes = [t.numel() for _, t in items]
+                for i in targets:
+                    rep = flat.to(devs[i], non_blocking=True) if devs[i] != flat.device else flat.clone()
+                    for (n, t), piece in zip(items, rep.split(sizes)):
+                        states[i][n] = piece.view_as(t)
+        return states
 
     def forward(self, *inputs, **kwargs):
         if len(self.devices) == 1:
@@ -81,7 +107,7 @@ class DataParallel(tnn.Module):
         n = min(len(self.devices), inputs[0].shape[self.dim] if isinstance(inputs[0], torch.Tensor) else len(self.devices))
         devs = self.devices[:n]
         scattered = scatter(list(inputs), devs, self.dim)
-        states = [self._replica_state(d) for d in devs]
+        states = self._replica_states(devs)
         results: List = [None] * n
         errors: List = [None] * n
         grad_enabled = torch.is_grad_enabled()

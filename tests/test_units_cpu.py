@@ -386,3 +386,31 @@ def test_resnet_snapshot_in_torchvision_layout(tmp_path):
     assert load_snapshot(path, m2) == 1
     for (k, a), (_, b) in zip(m.state_dict().items(), m2.state_dict().items()):
         assert torch.equal(a, b), k
+
+
+def test_data_parallel_coalesced_replicas_match_single_device():
+    """DataParallel replicas built from one coalesced copy per dtype (forced copy on the CPU tier):
+    outputs and master gradients equal the plain module's; the replica state views one flat copy."""
+    import torch.nn as tnn
+
+    from pytorchdistributed_amd.parallel.dp import DataParallel
+
+    torch.manual_seed(0)
+    net = tnn.Sequential(tnn.Linear(6, 8), tnn.BatchNorm1d(8), tnn.ReLU(), tnn.Linear(8, 3))
+    ref = tnn.Sequential(tnn.Linear(6, 8), tnn.BatchNorm1d(8), tnn.ReLU(), tnn.Linear(8, 3))
+    ref.load_state_dict(net.state_dict())
+    dp = DataParallel(net, device_ids=["cpu", "cpu"])
+    dp._force_copy = True
+    st = dp._replica_states([torch.device("cpu"), torch.device("cpu")])
+    w0, b0 = st[1]["0.weight"], st[1]["0.bias"]
+    assert w0.untyped_storage().data_ptr() == b0.untyped_storage().data_ptr()  # one flat copy
+    assert w0.data_ptr() != net[0].weight.data_ptr()
+    x = torch.randn(10, 6)
+    out = dp(x)
+    # reference: the two halves through the module separately (per-replica BN batch statistics)
+    ref_out = torch.cat([ref(x[:5]), ref(x[5:])])
+    assert torch.allclose(out, ref_out, atol=1e-6)
+    out.square().sum().backward()
+    ref_out.square().sum().backward()
+    for (n, p), (_, q) in zip(net.named_parameters(), ref.named_parameters()):
+        assert torch.allclose(p.grad, q.grad, atol=1e-5), n
