@@ -518,6 +518,17 @@ __device__ __forceinline__ void wait_vm() {
   else static_assert(N == 0 || N == 2 || N == 4 || N == 6 || N == 8 || N == 16, "add the literal");
 }
 
+// LDS-DMA of one 16-B chunk per lane (wave-uniform LDS base + lane x 16 B) as inline asm, as gemm_pp.hip
+// pp_glds_asm: beside a compiler-visible global_load_lds, hipcc (ROCm 7.2) waits vmcnt(0) in front of
+// every ds_read_b64_tr_b16 (it cannot tell the read from the DMA's LDS range), which drained the next
+// group's DMA before this group's first read.  Hidden in asm, the DMA is ordered by the kernel's own
+// s_waitcnt only (no other vector-memory op is in flight in its K loop).
+__device__ __forceinline__ void glds_asm(const bf16_t* src, char* lds_wave_base) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(l) : "memory", "m0");
+}
+
 __device__ __forceinline__ void raw_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -534,7 +545,7 @@ __device__ __forceinline__ void raw_barrier() {
 // BST: compile the BN-backward sums path (epi.bst_z).  Off, the epilogue's register peak stays below the
 // K loop's: the 128x64 tile keeps 114 VGPRs and 3 workgroups per CU (173 and 2 with the path compiled
 // in: the 56^2 64-channel convs ran 20-25 % slower, profiles/r5_conv_table_bs640.jsonl).
-template <int BM, int BN, bool RAW = false, bool DEFER = false, bool BST = true>
+template <int BM, int BN, bool RAW = false, bool DEFER = false, bool BST = true, int GM = 0>
 __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 32][BN / 32], char* smem,
                                                         const Epi& epi, int64_t m0, int64_t n0, int64_t M, int64_t N,
                                                         int tm, float (&st1)[8], float (&st2)[8]) {
@@ -585,7 +596,7 @@ __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 
   for (int q = 0; q < 8; ++q) st3[q] = 0.f;
   if (BST && epi.bst_z) {
     auto rd = [&](int r, int ch) { return *reinterpret_cast<const u16x8*>(stg + r * SROW + ch * 8); };
-    epi_bst_chunks<BM, CPR, NT, decltype(rd), BN == 64 ? 2 : 4>(epi, scol, rd, m0, n0, M, N, st1, st2, st3);
+    epi_bst_chunks<BM, CPR, NT, decltype(rd), GM ? GM : (BN == 64 ? 2 : 4)>(epi, scol, rd, m0, n0, M, N, st1, st2, st3);
   } else
 #pragma unroll
   for (int c = tid; c < BM * CPR; c += NT) {
@@ -609,13 +620,13 @@ __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 
   }
 }
 
-template <int BM, int BN, bool RAW = false, bool BST = true>
+template <int BM, int BN, bool RAW = false, bool BST = true, int GM = 0>
 __device__ __forceinline__ void tile_epilogue_bf16(const f32x4 (&acc)[BM / 32][BN / 32], char* smem, const Epi& epi,
                                                    int64_t m0, int64_t n0, int64_t M, int64_t N, int tm) {
   float st1[8], st2[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) st1[q] = st2[q] = 0.f;
-  tile_epilogue_bf16_impl<BM, BN, RAW, false, BST>(acc, smem, epi, m0, n0, M, N, tm, st1, st2);
+  tile_epilogue_bf16_impl<BM, BN, RAW, false, BST, GM>(acc, smem, epi, m0, n0, M, N, tm, st1, st2);
 }
 
 // ------------------------------------------------------------------ the kernel
@@ -887,6 +898,131 @@ __global__ void __launch_bounds__(NT, 2) conv3x3_halo_kernel(const bf16_t* __res
   tile_epilogue_bf16<BM, BN>(acc, smem, epi, m0, n0, M, N, tm);
 }
 
+// ------------------------------------------------------------------ 3x3 / stride-1, 64 -> 64 channels
+// The 56^2 layer of ResNet-50 (forward, and the stride-1 dgrad as the conv of dy with the rotated
+// weights).  The implicit GEMM is bound by its 9x im2col re-reads through L2 (0.28 ms vs a 0.09 ms HBM
+// roof at bs 640), and the halo kernel's one-tile-per-workgroup at 64 output channels is ~1 us of MFMAs
+// behind a ~2 us band load.  This kernel:
+//  * tiles = 4 whole image rows (224 pixels, W = 56): a band is the 4 rows + 1 halo row each side;
+//  * the band is stored with a 64-pixel row pitch, column -1 and columns >= 56 and out-of-image rows
+//    zero-filled by the DMA, so every tap reads a real band pixel (no validity selects) and a tap's row
+//    step is +-64 pixels, which keeps the (pixel >> 1) & 7 chunk swizzle unchanged: a lane's 42 fragment
+//    addresses (7 pixel groups x 3 column offsets x 2 channel halves) are computed ONCE per kernel (tile
+//    rows are aligned, so they are the same for every tile) and every tap is ds_read_b128 at an
+//    immediate row offset — the per-tap address math had made the first version VALU-bound (5.9 VALU per
+//    MFMA, rocprofv3 pmc);
+//  * the 9 x 2 x 2 weight fragments of a wave's 32 output channels live in VGPRs (one wave per SIMD:
+//    512 VGPRs), loaded once; the LDS holds only two band stages (2 x 48 KB);
+//  * workgroups are persistent over a contiguous run of tiles; the next tile's band is DMA'd (inline
+//    asm: hipcc adds no vmcnt(0) before the band reads) while this tile multiplies; the finished stage is
+//    the epilogue's staging tile (LDS-only barriers, so the other stage's DMA stays in flight).
+constexpr int R64_QW = 56;                        // image width this kernel is built for
+constexpr int R64_PITCH = 64;                     // band pixels per row
+constexpr int R64_ROWS = 6;                       // 4 tile rows + 2 halo rows
+constexpr int R64_BAND = R64_ROWS * R64_PITCH * 128;  // 49,152 B per band stage
+constexpr int R64_LDS = 2 * R64_BAND;             // 98,304 B
+
+template <bool BST>
+__global__ void __launch_bounds__(NT, 1) conv3x3_res64_kernel(const bf16_t* __restrict__ src,
+                                                               const bf16_t* __restrict__ wts, int H, int flip,
+                                                               int64_t M, int ntiles, Epi epi) {
+  constexpr int TMW = 7, BM = 32 * TMW, BN = 64, WM = 16 * TMW, WN = 32;
+  constexpr int TM = TMW, TN = WN / 16;
+  static_assert(BM == 4 * R64_QW, "a tile is 4 image rows");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1, g = lane >> 4;
+  const int per = (ntiles + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int t_begin = (int)blockIdx.x * per;
+  const int t_end = min(ntiles, t_begin + per);
+  if (t_begin >= t_end) return;
+
+  // weight fragments: B(k = ci, n = co) of tap t (flip: the rotated tap 8 - t), half h, column group j:
+  // lane holds w[co = wn*32 + 16 j + (lane & 15)][tap][ci = 32 h + 8 g .. + 7]
+  mfma_bf16x8 wf[9][2][TN];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int co = wn * WN + 16 * j + (lane & 15);
+        const int tb = flip ? 8 - t : t;
+        wf[t][h][j] = *reinterpret_cast<const mfma_bf16x8*>(wts + (int64_t)co * 576 + tb * 64 + 32 * h + 8 * g);
+      }
+  // band byte offsets (row 0 of the band, column offset ds = -1, 0, +1) of this lane's 7 pixel groups
+  int aoff[TM][3][2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int loc = wm * WM + 16 * i + (lane & 15);  // pixel within the 4-row tile
+    const int lr = loc / R64_QW, q = loc - lr * R64_QW;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const int b = lr * R64_PITCH + q + d;  // band column = image column + 1; ds = d - 1
+#pragma unroll
+      for (int h = 0; h < 2; ++h) aoff[i][d][h] = b * 128 + ((((4 * h + g) ^ ((b >> 1) & 7))) << 4);  // NOLINT
+    }
+  }
+  // band of tile tm: rows p0 - 1 .. p0 + 4 of image n, 64 pixel slots each (slot s = column s - 1)
+  auto load_band = [&](int tm, char* band) {
+    const int r0 = tm * 4;           // flattened (n * H + p) row of the tile's first row
+    const int n = r0 / H, p0 = r0 - n * H;
+    const bf16_t* img = src + (int64_t)n * H * R64_QW * 64;
+    const int slot = tid & 7;
+#pragma unroll
+    for (int k = 0; k < R64_ROWS * R64_PITCH / 32; ++k) {
+      const int b = k * 32 + (tid >> 3);
+      const int r = b >> 6, sc = b & 63;
+      const int ph = p0 - 1 + r, qc = sc - 1;
+      const int lc = slot ^ ((b >> 1) & 7);
+      const bool ok = (unsigned)ph < (unsigned)H && (unsigned)qc < (unsigned)R64_QW;
+      const bf16_t* a = img + ((int64_t)ph * R64_QW + qc) * 64 + lc * 8;  // formed unconditionally, selected
+      glds_asm(ok ? a : g_zero_page, band + k * 4096 + wid * 1024);
+    }
+  };
+
+  auto tile = [&](int tm, char* band, char* nband) {
+    if (tm + 1 < t_end) load_band(tm + 1, nband);
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dr = t / 3, d = t % 3;  // band row offset (dr - 1 + 1) and column variant
+      mfma_bf16x8 af[2][TM];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[h][i] = *reinterpret_cast<const mfma_bf16x8*>(band + aoff[i][d][h] + dr * R64_PITCH * 128);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][h][j], af[h][i], acc[i][j], 0, 0, 0);
+    }
+    raw_barrier();  // every wave is done with this band: it becomes the staging tile
+    tile_epilogue_bf16<BM, BN, true, BST, 7>(acc, band, epi, (int64_t)tm * BM, 0, M, BN, tm);
+    // the next band has landed (and this tile's stores).  The builtin, not asm: hipcc's waitcnt pass sees
+    // the counters drained here, so it adds no vmcnt(0) of its own at the top of the next tile — after
+    // that tile's band DMA has been issued
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+    raw_barrier();
+  };
+
+  char* const b0 = smem;
+  char* const b1 = smem + R64_BAND;
+  load_band(t_begin, b0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  __syncthreads();
+#pragma unroll 1
+  for (int tm = t_begin, it = 0; tm < t_end; ++tm, ++it) tile(tm, (it & 1) ? b1 : b0, (it & 1) ? b0 : b1);
+}
+
 // ------------------------------------------------------------------ 3x3 / stride-1 weight gradient, all taps
 // dw[co][r][s][ci] = sum over output pixels of dy[px][co] * x[px + (r-1, s-1)][ci].  The implicit GEMM
 // (M = Cout, N = 9 C, K = pixels) gathers im2col(x) per N tile: every x pixel is fetched from L2 once
@@ -1070,17 +1206,6 @@ constexpr int WG3V2_NT = 512;
 constexpr int WG3V2_DY = 32 * 1024;    // dy: two [64 px][<= 128 co] MN-major images
 constexpr int WG3V2_BAND = 40 * 1024;  // band: <= 320 pixels x 64 channels (128-B rows)
 constexpr int WG3V2_STAGE = WG3V2_DY + WG3V2_BAND;
-
-// LDS-DMA of one 16-B chunk per lane (wave-uniform LDS base + lane x 16 B) as inline asm, as gemm_pp.hip
-// pp_glds_asm: beside a compiler-visible global_load_lds, hipcc (ROCm 7.2) waits vmcnt(0) in front of
-// every ds_read_b64_tr_b16 (it cannot tell the read from the DMA's LDS range), which drained the next
-// group's DMA before this group's first read.  Hidden in asm, the DMA is ordered by the kernel's own
-// s_waitcnt only (no other vector-memory op is in flight in its K loop).
-__device__ __forceinline__ void glds_asm(const bf16_t* src, char* lds_wave_base) {
-  const uint32_t l = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)lds_wave_base);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(src), "s"(l) : "memory", "m0");
-}
 
 template <int CO_T, int W2L>
 __global__ void __launch_bounds__(WG3V2_NT, 1) conv3x3_wg_kernel(const bf16_t* __restrict__ dy,
@@ -2413,6 +2538,44 @@ hipError_t launch_halo_bn(const bf16_t* src, const bf16_t* B, int Nimg, int H, i
   return hipGetLastError();
 }
 
+// PDA_CONV_RES64=0: the 64 -> 64 channel 3x3 convs stay on the implicit GEMM (A/B)
+bool res64_mode_on() {
+  static const bool on = [] {
+    const char* e = getenv("PDA_CONV_RES64");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+bool use_res64(int H, int W, int Cg, int Nout, int R, int S, int stride, int pad, int dil, const Epi& epi) {
+  if (!res64_mode_on() || R != 3 || S != 3 || stride != 1 || pad != 1 || dil != 1) return false;
+  if (Cg != 64 || Nout != 64 || W != R64_QW || H % 4 != 0) return false;
+  if (epi.slab || epi.c_f32 || epi.act || epi.rm_on) return false;
+  return true;
+}
+
+hipError_t launch_res64(const bf16_t* src, const bf16_t* B, int Nimg, int H, int W, bool flip, const Epi& epi,
+                        hipStream_t st) {
+  static bool attr = [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_res64_kernel<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, R64_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_res64_kernel<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, R64_LDS);
+    return true;
+  }();
+  (void)attr;
+  (void)W;
+  const int64_t M = (int64_t)Nimg * H * R64_QW;
+  const int ntiles = Nimg * H / 4;
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = ntiles < cus ? ntiles : cus;
+  if (epi.bst_z) conv3x3_res64_kernel<true><<<grid, NT, R64_LDS, st>>>(src, B, H, flip ? 1 : 0, M, ntiles, epi);
+  else conv3x3_res64_kernel<false><<<grid, NT, R64_LDS, st>>>(src, B, H, flip ? 1 : 0, M, ntiles, epi);
+  return hipGetLastError();
+}
+
 hipError_t launch_halo(const bf16_t* src, const bf16_t* B, int Nimg, int H, int W, int Cg, int Nout, bool flip,
                        const Epi& epi, hipStream_t st) {
   return launch_halo_bn<128>(src, B, Nimg, H, W, Cg, Nout, flip, epi, st);
@@ -2623,6 +2786,7 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int
   epi.stats_shift = stats_shift;
   epi.stats_rows = stats_rows > 0 ? stats_rows : 1;
 
+  if (use_res64(H, W, C, Cout, R, S, stride, pad, dil, epi)) return launch_res64(x, w, N, H, W, false, epi, st);
   if (use_halo(H, W, C, Cout, R, S, stride, pad, dil, epi)) return launch_halo(x, w, N, H, W, C, Cout, false, epi, st);
   StemGeom sg;
   if (stem_geom(N, H, W, C, Cout, R, S, P, Q, stride, pad, dil, sg) && stem_fwd_on(Cout, y_f32, sg)) {
@@ -2725,6 +2889,7 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
   if (stride == 1) {
     // stride-1 dgrad = the 3x3 conv of dy with the rotated transposed weights (halo path)
     Epi epi = base_epi();
+    if (use_res64(H, W, Cout, C, R, S, stride, pad, dil, epi)) return launch_res64(dy, wt, N, H, W, true, epi, st);
     if (use_halo(H, W, Cout, C, R, S, stride, pad, dil, epi)) return launch_halo(dy, wt, N, H, W, Cout, C, true, epi, st);
   }
   const int nph = stride;  // phases per dim (1 for stride 1)

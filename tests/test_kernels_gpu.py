@@ -297,6 +297,10 @@ CONV_CASES = [
     # 3x3 weight gradient v2 (conv3x3_wg_kernel): every ResNet-50 3x3 layer shape (small batch), the
     # strided ones included, 64- and 128-channel output tiles, ragged last row groups
     (3, 56, 56, 64, 64, 3, 1, 1),       # 2 rows (112 px) per K-step, 64-channel tile (pixel-half parities)
+    # persistent 64 -> 64 3x3 fwd / dgrad (conv3x3_res64_kernel): > 256 tiles so workgroups walk several
+    # tiles with the next band in flight; bands crossing image boundaries; ragged last tile
+    (16, 56, 56, 64, 64, 3, 1, 1),
+    (70, 17, 29, 64, 64, 3, 1, 1),
     (2, 28, 28, 128, 128, 3, 1, 1),     # 4 rows per step, 128-channel tile, 2 ci blocks
     (3, 14, 14, 256, 256, 3, 1, 1),     # 9 + 5 rows per image
     (4, 7, 7, 512, 512, 3, 1, 1),       # one image per step (49 px)

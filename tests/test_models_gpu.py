@@ -295,7 +295,8 @@ def test_tied_embedding_side_stream_matches_single_stream():
     (4, 14, 14, 64, 256, 1, 1, 0, "ss", False),      # 1x1 dgrad, MN-major weight read in place (128 tile)
     (32, 28, 28, 256, 256, 1, 1, 0, "ss", False),    # 1x1 dgrad on a transposed weight (256 x 256 tile)
     (8, 28, 28, 128, 128, 3, 1, 1, "ss", False),     # 3x3 stride-1 dgrad (halo kernel)
-    (32, 28, 28, 64, 64, 3, 1, 1, "ss", False),      # 3x3 stride-1, 64 channels
+    (32, 28, 28, 64, 64, 3, 1, 1, "ss", False),      # 3x3 stride-1, 64 channels (persistent res64 kernel)
+    (48, 28, 28, 64, 64, 3, 1, 1, "ss", False),      # ... with 2 tiles per workgroup (next band in flight)
     (8, 28, 28, 128, 128, 3, 2, 1, "ss", False),     # 3x3 stride-2: phase launches + fill phases
     (32, 14, 14, 256, 1024, 1, 1, 0, "bits", True),  # next block's conv1: addend (shortcut) + bit mask
     (4, 14, 14, 64, 256, 1, 1, 0, "bits", True),
