@@ -48,7 +48,9 @@ def main():
     a, rest = ap.parse_known_args()
     mod = importlib.import_module(a.module)
     rec = _Rec(set(a.ops.split(",")))
-    with rec:
+    # backward on the calling thread, so the mode also sees the ops autograd runs (a dispatch mode is
+    # not active on the engine's device threads)
+    with rec, torch.autograd.set_multithreading_enabled(False):
         mod.main(rest)
     rows = sorted(rec.hits.items(), key=lambda kv: -kv[1][1])
     for (name, dt, site), (n, b) in rows[: a.top]:
