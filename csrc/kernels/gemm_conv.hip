@@ -545,7 +545,7 @@ __device__ __forceinline__ void raw_barrier() {
 // BST: compile the BN-backward sums path (epi.bst_z).  Off, the epilogue's register peak stays below the
 // K loop's: the 128x64 tile keeps 114 VGPRs and 3 workgroups per CU (173 and 2 with the path compiled
 // in: the 56^2 64-channel convs ran 20-25 % slower, profiles/r5_conv_table_bs640.jsonl).
-template <int BM, int BN, bool RAW = false, bool DEFER = false, bool BST = true, int GM = 0>
+template <int BM, int BN, bool RAW = false, bool DEFER = false, bool BST = true, int GM = 0, bool LEAN = false>
 __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 32][BN / 32], char* smem,
                                                         const Epi& epi, int64_t m0, int64_t n0, int64_t M, int64_t N,
                                                         int tm, float (&st1)[8], float (&st2)[8]) {
@@ -596,7 +596,8 @@ __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 
   for (int q = 0; q < 8; ++q) st3[q] = 0.f;
   if (BST && epi.bst_z) {
     auto rd = [&](int r, int ch) { return *reinterpret_cast<const u16x8*>(stg + r * SROW + ch * 8); };
-    epi_bst_chunks<BM, CPR, NT, decltype(rd), GM ? GM : (BN == 64 ? 2 : 4)>(epi, scol, rd, m0, n0, M, N, st1, st2, st3);
+    epi_bst_chunks<BM, CPR, NT, decltype(rd), GM ? GM : (BN == 64 ? 2 : 4), LEAN>(epi, scol, rd, m0, n0, M, N, st1,
+                                                                                 st2, st3);
   } else
 #pragma unroll
   for (int c = tid; c < BM * CPR; c += NT) {
@@ -620,13 +621,13 @@ __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 
   }
 }
 
-template <int BM, int BN, bool RAW = false, bool BST = true, int GM = 0>
+template <int BM, int BN, bool RAW = false, bool BST = true, int GM = 0, bool LEAN = false>
 __device__ __forceinline__ void tile_epilogue_bf16(const f32x4 (&acc)[BM / 32][BN / 32], char* smem, const Epi& epi,
                                                    int64_t m0, int64_t n0, int64_t M, int64_t N, int tm) {
   float st1[8], st2[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) st1[q] = st2[q] = 0.f;
-  tile_epilogue_bf16_impl<BM, BN, RAW, false, BST, GM>(acc, smem, epi, m0, n0, M, N, tm, st1, st2);
+  tile_epilogue_bf16_impl<BM, BN, RAW, false, BST, GM, LEAN>(acc, smem, epi, m0, n0, M, N, tm, st1, st2);
 }
 
 // ------------------------------------------------------------------ the kernel
@@ -922,7 +923,8 @@ constexpr int R64_ROWS = 6;                       // 4 tile rows + 2 halo rows
 constexpr int R64_BAND = R64_ROWS * R64_PITCH * 128;  // 49,152 B per band stage
 constexpr int R64_LDS = 2 * R64_BAND;             // 98,304 B
 
-template <bool BST>
+// BSTM: 0 no BN-backward sums, 1 the generic sums epilogue, 2 lean (z only: no addend / bits / second BN)
+template <int BSTM>
 __global__ void __launch_bounds__(NT, 1) conv3x3_res64_kernel(const bf16_t* __restrict__ src,
                                                                const bf16_t* __restrict__ wts, int H, int flip,
                                                                int64_t M, int ntiles, Epi epi) {
@@ -1006,7 +1008,7 @@ __global__ void __launch_bounds__(NT, 1) conv3x3_res64_kernel(const bf16_t* __re
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][h][j], af[h][i], acc[i][j], 0, 0, 0);
     }
     raw_barrier();  // every wave is done with this band: it becomes the staging tile
-    tile_epilogue_bf16<BM, BN, true, BST, 7>(acc, band, epi, (int64_t)tm * BM, 0, M, BN, tm);
+    tile_epilogue_bf16<BM, BN, true, BSTM != 0, 7, BSTM == 2>(acc, band, epi, (int64_t)tm * BM, 0, M, BN, tm);
     // the next band has landed (and this tile's stores).  The builtin, not asm: hipcc's waitcnt pass sees
     // the counters drained here, so it adds no vmcnt(0) of its own at the top of the next tile — after
     // that tile's band DMA has been issued
@@ -2557,9 +2559,11 @@ bool use_res64(int H, int W, int Cg, int Nout, int R, int S, int stride, int pad
 hipError_t launch_res64(const bf16_t* src, const bf16_t* B, int Nimg, int H, int W, bool flip, const Epi& epi,
                         hipStream_t st) {
   static bool attr = [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_res64_kernel<false>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_res64_kernel<0>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, R64_LDS);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_res64_kernel<true>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_res64_kernel<1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, R64_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&conv3x3_res64_kernel<2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, R64_LDS);
     return true;
   }();
@@ -2571,8 +2575,10 @@ hipError_t launch_res64(const bf16_t* src, const bf16_t* B, int Nimg, int H, int
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int grid = ntiles < cus ? ntiles : cus;
-  if (epi.bst_z) conv3x3_res64_kernel<true><<<grid, NT, R64_LDS, st>>>(src, B, H, flip ? 1 : 0, M, ntiles, epi);
-  else conv3x3_res64_kernel<false><<<grid, NT, R64_LDS, st>>>(src, B, H, flip ? 1 : 0, M, ntiles, epi);
+  if (!epi.bst_z) conv3x3_res64_kernel<0><<<grid, NT, R64_LDS, st>>>(src, B, H, flip ? 1 : 0, M, ntiles, epi);
+  else if (epi.addend || epi.bst_bits || epi.bst_z2)
+    conv3x3_res64_kernel<1><<<grid, NT, R64_LDS, st>>>(src, B, H, flip ? 1 : 0, M, ntiles, epi);
+  else conv3x3_res64_kernel<2><<<grid, NT, R64_LDS, st>>>(src, B, H, flip ? 1 : 0, M, ntiles, epi);
   return hipGetLastError();
 }
 

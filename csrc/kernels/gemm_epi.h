@@ -165,7 +165,9 @@ __device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
 //   stg_read(r, ch): the staged bf16 values of tile row r, column chunk ch.
 //   GMAX: chunks per load group (a 64-column tile takes 2: its kernel then stays within 168 VGPRs, three
 //   workgroups per CU)
-template <int ROWS, int CPR, int NT, class StgRead, int GMAX = 4>
+//   LEAN: the launch has no addend, no second BN and no bit mask (the caller checked): only z is loaded
+//   (the generic path loads z2 / addend / mask bytes from always-valid aliases of z when they are absent)
+template <int ROWS, int CPR, int NT, class StgRead, int GMAX = 4, bool LEAN = false>
 __device__ __forceinline__ void epi_bst_chunks(const Epi& e, const EpiStatCols& sc, StgRead stg_read, int64_t m0,
                                                int64_t n0, int64_t M, int64_t N, float (&st1)[8], float (&st2)[8],
                                                float (&st3)[8]) {
@@ -173,12 +175,12 @@ __device__ __forceinline__ void epi_bst_chunks(const Epi& e, const EpiStatCols& 
   constexpr int G = ITERS < GMAX ? ITERS : GMAX;  // (8 pushed the gathered wide-tile kernels into scratch)
   static_assert(ITERS % G == 0, "groups cover the tile");
   const int tid = threadIdx.x;
-  const bool has_add = e.addend != nullptr, use_bits = e.bst_bits != nullptr;
+  const bool has_add = !LEAN && e.addend != nullptr, use_bits = !LEAN && e.bst_bits != nullptr;
   const bf16_t* adp = has_add ? e.addend : e.bst_z;
   const uint8_t* abp = e.addend_bits ? e.addend_bits : reinterpret_cast<const uint8_t*>(e.bst_z);
   const uint32_t ab_or = e.addend_bits ? 0u : 0xFFu;
   const uint8_t* zbp = use_bits ? e.bst_bits : reinterpret_cast<const uint8_t*>(e.bst_z);
-  const bool dual = e.bst_z2 != nullptr;
+  const bool dual = !LEAN && e.bst_z2 != nullptr;
   const bf16_t* z2p = dual ? e.bst_z2 : e.bst_z;
   float mu2[8];
   {
@@ -210,10 +212,15 @@ __device__ __forceinline__ void epi_bst_chunks(const Epi& e, const EpiStatCols& 
       ok[u] = m < M && n < N;
       off[u] = ok[u] ? epi_row(e, m) * e.ldc + n : 0;
       z[u] = *reinterpret_cast<const u16x8*>(e.bst_z + off[u]);
-      z2[u] = *reinterpret_cast<const u16x8*>(z2p + off[u]);
-      a[u] = *reinterpret_cast<const u16x8*>(adp + off[u]);
-      ab[u] = (uint32_t)abp[off[u] >> 3] | ab_or;
-      zb[u] = zbp[off[u] >> 3];
+      if constexpr (LEAN) {
+        z2[u] = a[u] = z[u];
+        ab[u] = zb[u] = 0u;
+      } else {
+        z2[u] = *reinterpret_cast<const u16x8*>(z2p + off[u]);
+        a[u] = *reinterpret_cast<const u16x8*>(adp + off[u]);
+        ab[u] = (uint32_t)abp[off[u] >> 3] | ab_or;
+        zb[u] = zbp[off[u] >> 3];
+      }
     }
 #pragma unroll
     for (int u = 0; u < G; ++u) {
@@ -231,7 +238,7 @@ __device__ __forceinline__ void epi_bst_chunks(const Epi& e, const EpiStatCols& 
         const float g = keep ? bf2f(o[q]) : 0.f;
         st1[q] += g;
         st2[q] = fmaf(g, zf - sc.k[q], st2[q]);
-        st3[q] = fmaf(g, bf2f(z2[u][q]) - mu2[q], st3[q]);
+        if (!LEAN) st3[q] = fmaf(g, bf2f(z2[u][q]) - mu2[q], st3[q]);
       }
       *reinterpret_cast<u16x8*>((bf16_t*)e.C + off[u]) = o;
     }
