@@ -938,6 +938,12 @@ __global__ void __launch_bounds__(NT, 1) conv3x3_res64_kernel(const bf16_t* __re
   const int t_begin = (int)blockIdx.x * per;
   const int t_end = min(ntiles, t_begin + per);
   if (t_begin >= t_end) return;
+  // BN sums (forward statistics, or the lean backward sums) accumulate in registers over the whole run
+  // of tiles and are flushed once (table row = workgroup): no per-tile LDS reduction + atomics
+  constexpr bool DEFER = BSTM != 1;
+  float st1[8], st2[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) st1[q] = st2[q] = 0.f;
 
   // weight fragments: B(k = ci, n = co) of tap t (flip: the rotated tap 8 - t), half h, column group j:
   // lane holds w[co = wn*32 + 16 j + (lane & 15)][tap][ci = 32 h + 8 g .. + 7]
@@ -1008,7 +1014,12 @@ __global__ void __launch_bounds__(NT, 1) conv3x3_res64_kernel(const bf16_t* __re
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[t][h][j], af[h][i], acc[i][j], 0, 0, 0);
     }
     raw_barrier();  // every wave is done with this band: it becomes the staging tile
-    tile_epilogue_bf16<BM, BN, true, BSTM != 0, 7, BSTM == 2>(acc, band, epi, (int64_t)tm * BM, 0, M, BN, tm);
+    if constexpr (DEFER) {
+      tile_epilogue_bf16_impl<BM, BN, true, true, BSTM != 0, 7, BSTM == 2>(acc, band, epi, (int64_t)tm * BM, 0, M, BN,
+                                                                           tm, st1, st2);
+    } else {
+      tile_epilogue_bf16<BM, BN, true, BSTM != 0, 7, BSTM == 2>(acc, band, epi, (int64_t)tm * BM, 0, M, BN, tm);
+    }
     // the next band has landed (and this tile's stores).  The builtin, not asm: hipcc's waitcnt pass sees
     // the counters drained here, so it adds no vmcnt(0) of its own at the top of the next tile — after
     // that tile's band DMA has been issued
@@ -1023,6 +1034,7 @@ __global__ void __launch_bounds__(NT, 1) conv3x3_res64_kernel(const bf16_t* __re
   __syncthreads();
 #pragma unroll 1
   for (int tm = t_begin, it = 0; tm < t_end; ++tm, ++it) tile(tm, (it & 1) ? b1 : b0, (it & 1) ? b0 : b1);
+  if (DEFER && epi.stats) epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem), BN / 8, NT, blockIdx.x, 0, BN);
 }
 
 // ------------------------------------------------------------------ 3x3 / stride-1 weight gradient, all taps
