@@ -3,6 +3,9 @@
 // outputs / dgrad row remap) and the tile epilogue for the 8-wave (2 x 4) accumulator layout
 //   acc[i][j][r] = C[m0 + wr*128 + 16 i + (lane & 15)][n0 + wc*64 + 16 j + 4 (lane >> 4) + r].
 #pragma once
+#ifndef PDA_BSTG
+#define PDA_BSTG 8
+#endif
 #include "pda_common.h"
 
 namespace pda {
@@ -308,8 +311,10 @@ __device__ __forceinline__ void epi_bias_cols(const Epi& epi, int64_t n0, int64_
 // acc[i][j][q] is C(row wr*128 + 16 i + (lane & 15), col wc*(16*JT) + 16 j + 4 (lane >> 4) + q).
 // BST: compile the BN-backward statistics path (epi_bst_chunks).  Off for the kernels that never produce a
 // BN's dy (gathered forward / weight-gradient loaders of the wide kernel): the extra epilogue code pushed
-// their main loops into scratch spills.
-template <int WCOLS = 4, bool BST = true>
+// their main loops into scratch spills.  BSTG: chunks per load group of the BN-backward sums (each group
+// is one exposed z-load latency; a short-K tile — the 56^2 1x1 dgrads, K = 64 — has nothing else to hide
+// it behind).
+template <int WCOLS = 4, bool BST = true, int BSTG = PDA_BSTG>
 __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][16 / WCOLS], char* smem, int stats_off,
                                                    const Epi& epi, int64_t m0, int64_t n0, int64_t M, int64_t N, int tm,
                                                    int split) {
@@ -389,9 +394,8 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][16 / WC
 #pragma unroll
   for (int q = 0; q < 8; ++q) st3[q] = 0.f;
   if (BST && epi.bst_z) {
-    epi_bst_chunks<256, CPR, NT>(
-        epi, scol, [&](int r, int ch) { return *reinterpret_cast<const u16x8*>(stg + r * WT_SROW + ch * 8); }, m0,
-        n0, M, N, st1, st2, st3);
+    auto rd = [&](int r, int ch) { return *reinterpret_cast<const u16x8*>(stg + r * WT_SROW + ch * 8); };
+    epi_bst_chunks<256, CPR, NT, decltype(rd), BSTG>(epi, scol, rd, m0, n0, M, N, st1, st2, st3);
   } else
   for (int c = tid; c < 256 * CPR; c += NT) {
     const int r = c / CPR, ch = c % CPR;
