@@ -1020,6 +1020,19 @@ __global__ void __launch_bounds__(kThreads) stem_pool_bn_bwd_kernel(
     pix /= Wb;
     const int p = pix % Hb;
     const int n = pix / Hb;
+    const int h = 2 * p, w = 2 * q;
+    // the block's 4 z vectors are loaded up front, beside the pooled gradients: their addresses do not
+    // depend on the argmax bytes, and in phase 1 a z load issued after the previous pixel's dz store
+    // cannot be hoisted above it (the compiler cannot rule out aliasing), which serialised 4 memory
+    // latencies per block
+    u16x8 zr[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int hh = h + (e >> 1), ww = w + (e & 1);
+      const bool ok = hh < H && ww < W;
+      const int64_t off = ok ? (((int64_t)n * H + hh) * W + ww) * C + c8 * 8 : (int64_t)c8 * 8;
+      zr[e] = *reinterpret_cast<const u16x8*>(z + off);
+    }
     float g[4][8];
     uint64_t id[4];
 #pragma unroll
@@ -1045,14 +1058,14 @@ __global__ void __launch_bounds__(kThreads) stem_pool_bn_bwd_kernel(
       d[2][j] = (i0 == 7 ? g[0][j] : 0.f) + (i2 == 1 ? g[2][j] : 0.f);
       d[3][j] = ((i0 == 8 ? g[0][j] : 0.f) + (i1 == 6 ? g[1][j] : 0.f)) + ((i2 == 2 ? g[2][j] : 0.f) + (i3 == 0 ? g[3][j] : 0.f));
     }
-    const int h = 2 * p, w = 2 * q;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int hh = h + (e >> 1), ww = w + (e & 1);
       if (hh >= H || ww >= W) continue;
       const int64_t off = (((int64_t)n * H + hh) * W + ww) * C + c8 * 8;
       float zv[8];
-      load8(z + off, zv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) zv[j] = bf2f(zr[e][j]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float gm = fmaf(zv[j], sc[j], sh[j]) > 0.f ? d[e][j] : 0.f;
