@@ -202,7 +202,8 @@ class _Unit:
             elif self.fsdp.xgmi is not None:
                 flat = self.flat
                 self.pending_ag = self.fsdp._ipc(lambda: self.fsdp.xgmi.all_gather_into_tensor(flat, send),
-                                                 [torch.cuda.current_stream(self.device)], [send, flat])
+                                                 [torch.cuda.current_stream(self.device)], [send, flat],
+                                                 ("ag", self.index))
                 self.fsdp._track("xgmi all_gather", self, self.fsdp._ipc_stream)
             elif self.fsdp.ncomm is not None:
                 self.pending_ag = self.fsdp.ncomm.all_gather(self.flat, send)
@@ -255,6 +256,7 @@ class FullyShardedDataParallel(tnn.Module):
         # PDA_METRICS_DIR) the compute-stream time spent waiting on the collectives (exposed comm)
         self.track_comm = bool(os.environ.get("PDA_METRICS_DIR")) or os.environ.get("PDA_TRACK_COMM") == "1"
         self._stats = {"comm_bytes": 0, "comm_calls": 0}
+        self._ipc_log: List = []  # (kind, unit) of every IPC collective in issue order (debugging)
         self._exposed_events: List = []
         self._deferred_release: List = []
         # ---- build units: typed submodules first (outermost match), root takes the rest
@@ -375,8 +377,10 @@ class FullyShardedDataParallel(tnn.Module):
         _watchdog.track(f"fsdp {what} unit {u.index} ({nbytes / 2**20:.1f} MB)", stream)
         self._stats["tickets"] = self._stats.get("tickets", 0) + 1
 
-    def _ipc(self, fn, producers, tensors):
+    def _ipc(self, fn, producers, tensors, tag=None):
         """Run ``fn`` on the IPC stream after ``producers``; returns a work handle (wait = stream wait)."""
+        if tag is not None:
+            self._ipc_log.append(tag)
         s = self._ipc_stream
         for p in producers:
             s.wait_stream(p)
@@ -476,7 +480,7 @@ class FullyShardedDataParallel(tnn.Module):
         producers = _streams.producer_streams(grad_full.device) if grad_full.is_cuda else []
         if self.xgmi is not None:
             work = self._ipc(lambda: self.xgmi.reduce_scatter_tensor(out, grad_full, average=True), producers,
-                             [out, grad_full])
+                             [out, grad_full], ("rs", u.index))
             self._track("xgmi reduce_scatter", u, self._ipc_stream)
         elif self.ncomm is not None:
             work = self.ncomm.reduce_scatter(out, grad_full, "avg", streams=producers)
@@ -537,6 +541,10 @@ class FullyShardedDataParallel(tnn.Module):
         for u in self.units:
             u.flush_missing()
         self._finish_rs()
+        if self.xgmi is not None and self.xgmi.poll():
+            # a peer barrier of an IPC gather / reduce-scatter timed out: that call's output is garbage
+            # (the kernels give up instead of hanging) — fail the step rather than train on it
+            self.xgmi.check(sync=False)
         for u in self.units:
             u.reshard()
             u.arrived = 0

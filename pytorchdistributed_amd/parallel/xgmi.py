@@ -86,8 +86,13 @@ def table_from_sweep(records: List[dict], world: int) -> dict:
 
 
 class XgmiAllReduce:
-    def __init__(self, capacity_mb: float = 64.0, device: Optional[torch.device] = None, timeout_s: float = 10.0,
+    def __init__(self, capacity_mb: float = 64.0, device: Optional[torch.device] = None, timeout_s: Optional[float] = None,
                  store=None, rank: Optional[int] = None, world: Optional[int] = None):
+        # peer-barrier deadline inside the kernels (PDA_XGMI_TIMEOUT_S, default 60 s): long enough that a
+        # peer whose first launch waits on a cold code-object load is not taken for a dead one (the
+        # collective watchdog, PDA_COLLECTIVE_TIMEOUT_S, is what ends real hangs)
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("PDA_XGMI_TIMEOUT_S", "60"))
         self.rank = dist.get_rank() if rank is None else rank
         self.world = dist.get_world_size() if world is None else world
         if device is None:

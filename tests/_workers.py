@@ -593,6 +593,11 @@ def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl", force=False):
     ref = Llama(cfg, device="cuda", dtype=torch.bfloat16)
     model = Llama(cfg, device="cuda", dtype=torch.bfloat16)
     model.load_state_dict(ref.state_dict())
+    skew = float(os.environ.get("PDA_TEST_SKEW_S", "0"))
+    if skew and rank == 1:  # debugging aid: start one rank late
+        import time
+
+        time.sleep(skew)
     fsdp = FullyShardedDataParallel(model, unit_types=(LlamaBlock,))
     assert (fsdp.xgmi is not None) == (comm == "ipc" and world > 1)
     if force:
@@ -600,20 +605,36 @@ def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl", force=False):
     opt = AdamW(fsdp.parameters(), lr=1e-3, weight_decay=0.1)
     ropt = AdamW(ref.parameters(), lr=1e-3, weight_decay=0.1)
     g = torch.Generator().manual_seed(5)
-    for _ in range(2):
+    dbg = os.environ.get("PDA_TEST_DEBUG") == "1"
+    for step in range(2):
         idx = torch.randint(0, cfg.vocab_size, (world * 2, 64), generator=g).cuda()
         tgt = torch.randint(0, cfg.vocab_size, (world * 2, 64), generator=g).cuda()
         opt.zero_grad(set_to_none=True)
-        fsdp(idx[rank * 2:(rank + 1) * 2], tgt[rank * 2:(rank + 1) * 2]).backward()
+        loss = fsdp(idx[rank * 2:(rank + 1) * 2], tgt[rank * 2:(rank + 1) * 2])
+        loss.backward()
+        if dbg:
+            gsum = [float(u.grad_buffer.float().norm()) if u.grad_buffer.untyped_storage().size() else -1.0
+                    for u in fsdp.units]
+            print(f"[rank {rank}] step {step} loss {float(loss):.6f} unit grad norms {gsum}", flush=True)
         opt.step()
         ropt.zero_grad(set_to_none=True)
-        ref(idx, tgt).backward()
+        rl = ref(idx, tgt)
+        rl.backward()
+        if dbg and rank == 0:
+            print(f"[ref] step {step} loss {float(rl):.6f}", flush=True)
         ropt.step()
     sd = fsdp.full_state_dict()
     worst = (0.0, "")
+    errs = []
     for n, p in ref.named_parameters():
         a, b = sd[n].float(), p.detach().float().cpu()
-        worst = max(worst, (((a - b).norm() / b.norm()).item(), n))
+        e = ((a - b).norm() / b.norm()).item()
+        errs.append((round(e, 4), n))
+        worst = max(worst, (e, n))
+    if dbg or worst[0] >= 2e-2:
+        print(f"[rank {rank}] errors {sorted(errs, reverse=True)[:8]}", flush=True)
+        print(f"[rank {rank}] ipc order {getattr(fsdp, '_ipc_log', None)} xgmi error word "
+              f"{fsdp.xgmi.poll() if fsdp.xgmi is not None else None}", flush=True)
     assert worst[0] < 2e-2, worst
     extra = ""
     if force:
