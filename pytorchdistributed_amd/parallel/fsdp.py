@@ -256,7 +256,9 @@ class FullyShardedDataParallel(tnn.Module):
         # PDA_METRICS_DIR) the compute-stream time spent waiting on the collectives (exposed comm)
         self.track_comm = bool(os.environ.get("PDA_METRICS_DIR")) or os.environ.get("PDA_TRACK_COMM") == "1"
         self._stats = {"comm_bytes": 0, "comm_calls": 0}
-        self._ipc_log: List = []  # (kind, unit) of every IPC collective in issue order (debugging)
+        # PDA_FSDP_IPC_LOG=1: record (kind, unit) of every IPC collective in issue order (debugging the
+        # cross-rank op order; unbounded, so off by default)
+        self._ipc_log: Optional[List] = [] if os.environ.get("PDA_FSDP_IPC_LOG") == "1" else None
         self._exposed_events: List = []
         self._deferred_release: List = []
         # ---- build units: typed submodules first (outermost match), root takes the rest
@@ -379,7 +381,7 @@ class FullyShardedDataParallel(tnn.Module):
 
     def _ipc(self, fn, producers, tensors, tag=None):
         """Run ``fn`` on the IPC stream after ``producers``; returns a work handle (wait = stream wait)."""
-        if tag is not None:
+        if tag is not None and self._ipc_log is not None:
             self._ipc_log.append(tag)
         s = self._ipc_stream
         for p in producers:
