@@ -1874,6 +1874,21 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
 __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t M,
                                                             int64_t N, int lanes_log2, Epi epi) {
   __shared__ f32x4 red[256];
+  if (epi.rowsum_out && epi.rowsum_mode == 4) {  // trailing workgroups: the bias gradient's split sums
+    const int rb = (int)((M + 255) / 256);
+    const int b = (int)blockIdx.x - ((int)gridDim.x - rb);
+    if (b >= 0) {
+      const int64_t i = (int64_t)b * 256 + threadIdx.x;
+      if (i < M) {
+        const float* rs = (const float*)epi.rowsum;
+        float v = 0.f;
+        for (int s = 0; s < splits; ++s) v += rs[(int64_t)s * M + i];
+        if (epi.rowsum_out_bf16) ((bf16_t*)epi.rowsum_out)[i] = f2bf(v);
+        else ((float*)epi.rowsum_out)[i] = v;
+      }
+      return;
+    }
+  }
   const int L = 1 << lanes_log2;
   const int lane = threadIdx.x & (L - 1), o = threadIdx.x >> lanes_log2;
   const int64_t total4 = M * N / 4;
@@ -2323,7 +2338,8 @@ hipError_t launch_pp_plain(const LA& la, const LB& lb, int64_t M, int64_t N, int
   while (ll < 4 && (used >> ll) > 16) ++ll;
   const int64_t per_block = 256 >> ll;
   const int64_t g = (M * N / 4 + per_block - 1) / per_block;
-  splitk_reduce_kernel<<<(unsigned)g, 256, 0, st>>>(slab, used, M, N, ll, epi);
+  const int64_t rb = (epi.rowsum_out && epi.rowsum_mode == 4) ? (M + 255) / 256 : 0;
+  splitk_reduce_kernel<<<(unsigned)(g + rb), 256, 0, st>>>(slab, used, M, N, ll, epi);
   return hipGetLastError();
 }
 
@@ -2443,9 +2459,17 @@ hipError_t gemm_bf16_wgrad_db(const bf16_t* dy, int64_t ld_dy, const bf16_t* x, 
     else if (slab) ws = wide_splits(M, N, K, p, epi);
     if (ws > 0) {
       Epi e = epi;
+      static const bool fused_cast = [] {  // PDA_ROWSUM_FUSED=0: the separate rowsum_cast launch (A/B)
+        const char* v = getenv("PDA_ROWSUM_FUSED");
+        return !(v && v[0] == '0');
+      }();
       if (ws > 1) {
         e.rowsum = rs_scratch;
         e.rowsum_mode = 4;
+        if (fused_cast) {
+          e.rowsum_out = db;
+          e.rowsum_out_bf16 = db_bf16 ? 1 : 0;
+        }
       } else {
         e.rowsum = db;
         e.rowsum_mode = db_bf16 ? 2 : 1;
@@ -2455,7 +2479,7 @@ hipError_t gemm_bf16_wgrad_db(const bf16_t* dy, int64_t ld_dy, const bf16_t* x, 
           launch_pp_plain(mk_amn(PlainMN<64>{}), mk_bmn(PlainMN<64>{}), M, N, K, e, st, ws, slab, &used);
       if (r != hipErrorNotSupported) {
         if (r != hipSuccess) return r;
-        if (ws > 1) {
+        if (ws > 1 && (!e.rowsum_out || used <= 1)) {  // (used == 1: no reduce launch carried the sums)
           rowsum_cast_kernel<<<(unsigned)((M + 255) / 256), 256, 0, st>>>(rs_scratch, db, db_bf16 ? 1 : 0, M,
                                                                           used);
           PDA_CHECK_HIP(hipGetLastError());

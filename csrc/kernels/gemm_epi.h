@@ -46,6 +46,10 @@ struct Epi {
   // atomic add (split-K launches; the caller zeroes the buffer)
   void* rowsum;
   int rowsum_mode;  // 1 fp32 store, 2 bf16 store, 3 fp32 atomic add, 4 fp32 store at [split][M]
+  // mode 4 + rowsum_out: the split-K reduce launch also sums the [split][M] row sums into rowsum_out (its
+  // last ceil(M / 256) workgroups; bf16 when rowsum_out_bf16) — no separate cast launch
+  void* rowsum_out;
+  int rowsum_out_bf16;
   int nt_store;     // bf16 C rows written with nontemporal stores (streamed past the caches)
   // optional BatchNorm-BACKWARD statistics of the produced gradient (the data gradient of the
   // conv that consumed relu(bn(z)) IS that BN's dy).  With bst_z set, the stats path above accumulates
