@@ -2963,6 +2963,7 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
       Plan p = plan_gemm(M, Nn, K, false, 512);
       Epi epi = base_epi();
       if (stride > 1) {
+        if (M >= ((int64_t)1 << 32)) return hipErrorInvalidValue;  // epi_row's 32-bit row remap
         epi.rm_on = 1; epi.rm_Hh = Hh; epi.rm_Wh = Wh; epi.rm_st = stride; epi.rm_ph = ph; epi.rm_pw = pw;
         epi.rm_H = H; epi.rm_W = W;
       }

@@ -155,11 +155,14 @@ __device__ __forceinline__ void epi_stats8(const Epi& e, const EpiStatCols& c, i
 
 __device__ __forceinline__ int64_t epi_row(const Epi& e, int64_t m) {
   if (!e.rm_on) return m;
-  const int64_t t = m / e.rm_Wh;
-  const int ww = (int)(m - t * e.rm_Wh);
-  const int64_t n = t / e.rm_Hh;
-  const int hh = (int)(t - n * e.rm_Hh);
-  return (n * e.rm_H + (int64_t)hh * e.rm_st + e.rm_ph) * e.rm_W + (int64_t)ww * e.rm_st + e.rm_pw;
+  // 32-bit divisions (a phase GEMM's rows and the phase grid fit easily; the int64 divide is a ~100-instruction
+  // software sequence, paid per 16-B chunk of every strided-dgrad epilogue)
+  const uint32_t mm = (uint32_t)m, wh = (uint32_t)e.rm_Wh, hh_ = (uint32_t)e.rm_Hh;
+  const uint32_t t = mm / wh;
+  const int ww = (int)(mm - t * wh);
+  const uint32_t n = t / hh_;
+  const int hh = (int)(t - n * hh_);
+  return ((int64_t)n * e.rm_H + (int64_t)hh * e.rm_st + e.rm_ph) * e.rm_W + (int64_t)ww * e.rm_st + e.rm_pw;
 }
 
 // The staged-chunk loop of a bf16 epilogue WITH BN-backward statistics (bst_z set; no act / nontemporal
