@@ -1,7 +1,7 @@
 set -o pipefail
 export TMPDIR=/tmp
-out=gpurun_out/s29; mkdir -p $out
-timeout -k 10 600 python -u -m pytest tests/test_models_gpu.py tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "resnet or bottleneck or conv or bn" > $out/t.log 2>&1 || { tail -30 $out/t.log; exit 1; }
+out=gpurun_out/s30; mkdir -p $out
+timeout -k 10 600 python -u -m pytest tests/test_models_gpu.py tests/test_kernels_gpu.py -x -q --timeout 120 --timeout-method thread -k "resnet or bottleneck or conv or bn or determin or stats" > $out/t.log 2>&1 || { tail -30 $out/t.log; exit 1; }
 tail -1 $out/t.log
 for r in 1 2; do
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $out/rn_$r.log 2>&1 || exit 1
