@@ -1219,3 +1219,27 @@ def pipeline_interleaved_unused_worker(rank, world, find_unused, outdir):
         out["error"] = str(e)
     torch.save(out, os.path.join(outdir, f"{rank}.pt"))
     pd.destroy_process_group()
+
+
+def param_server_worker(rank, world, outdir, steps):
+    """Synchronous parameter server on an MLP: after `steps` server SGD steps every rank's params equal
+    single-process full-batch training from the server's initial weights; workers hold no optimizer."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.models.mlp import MnistMLP
+    from pytorchdistributed_amd.optim import SGD
+    from pytorchdistributed_amd.parallel.param_server import ParameterServer
+
+    pd.init_process_group("gloo")
+    torch.manual_seed(123 + rank)  # different init per rank: the server's state must win
+    model = MnistMLP((16, 32, 24, 10))
+    ps = ParameterServer(model, lambda params: SGD(params, lr=0.1, momentum=0.9), server=0)
+    assert (ps.optimizer is None) == (rank != 0)
+    g = torch.Generator().manual_seed(7)
+    X = torch.randn(steps, world * 4, 16, generator=g)
+    Y = torch.randint(0, 10, (steps, world * 4), generator=g)
+    for s in range(steps):
+        ps.zero_grad()
+        F.cross_entropy(ps(X[s, rank * 4:(rank + 1) * 4]), Y[s, rank * 4:(rank + 1) * 4]).backward()
+        ps.step()
+    torch.save({k: v.clone() for k, v in model.state_dict().items()}, os.path.join(outdir, f"{rank}.pt"))
+    pd.destroy_process_group()

@@ -332,3 +332,28 @@ def test_watchdog_fault_injection_ends_run(tmp_path, kind, schedule):
     want = "fsdp c10d all_gather" if kind == "fsdp" else "pp "
     assert want in r.stderr, r.stderr[-3000:]
     assert "File " in r.stderr  # faulthandler stack dump
+
+
+def test_parameter_server_matches_single_process(tmp_path):
+    """SURVEY X17 (PS-worker concept, NB02:28-31): reduce-to-server + server-side SGD + broadcast
+    equals full-batch single-process SGD; every rank ends with the server's parameters."""
+    world, steps = 2, 3
+    spawn(_workers.param_server_worker, args=(world, str(tmp_path), steps), nprocs=world, timeout=120)
+    import torch.nn.functional as F
+    from pytorchdistributed_amd.models.mlp import MnistMLP
+
+    torch.manual_seed(123)
+    ref = MnistMLP((16, 32, 24, 10))
+    opt = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(7)
+    X = torch.randn(steps, world * 4, 16, generator=g)
+    Y = torch.randint(0, 10, (steps, world * 4), generator=g)
+    for s in range(steps):
+        opt.zero_grad()
+        F.cross_entropy(ref(X[s]), Y[s]).backward()
+        opt.step()
+    s0 = torch.load(tmp_path / "0.pt", weights_only=True)
+    s1 = torch.load(tmp_path / "1.pt", weights_only=True)
+    for k, v in ref.state_dict().items():
+        assert torch.allclose(s0[k], v, atol=1e-5), k
+        assert torch.equal(s0[k], s1[k]), k
