@@ -166,6 +166,16 @@ def test_ddp_rccl_one_rank_group_lr005_stem_gemm(tmp_path):
     assert (tmp_path / "ok0").read_text().startswith("ok")
 
 
+def test_parameter_server_rccl_one_rank_group(tmp_path):
+    """parallel/param_server.py over a one-rank RCCL group: gradients reduced to the server and
+    parameters broadcast back through RCCL on device tensors; three steps equal a local replica's."""
+    import _workers
+    from pytorchdistributed_amd.launch import spawn
+
+    spawn(_workers.ps_rccl_world1_worker, args=(1, str(tmp_path)), nprocs=1, timeout=300)
+    assert (tmp_path / "ok0").read_text().startswith("ok")
+
+
 def test_native_rccl_communicator_one_rank(tmp_path):
     """csrc/comm/communicator.cpp through comm.py: all-reduce (sum / avg, fp32 / bf16), all-gather,
     reduce-scatter, broadcast, fused send/recv, work handles, stream ordering."""
