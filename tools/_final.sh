@@ -1,6 +1,6 @@
 set -o pipefail
 export TMPDIR=/tmp
-out=gpurun_out/final3; mkdir -p $out
+out=gpurun_out/final4; mkdir -p $out
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $out/pytest_gpu.txt 2>&1 || { tail -30 $out/pytest_gpu.txt; exit 1; }
 tail -2 $out/pytest_gpu.txt
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
