@@ -107,6 +107,10 @@ def test_examples_run_on_cpu(tmp_path):
     assert out.returncode == 0
     rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["n_ranks"] == 2 and rec["value"] > 0
+    out = subprocess.run([sys.executable, "-m", "pytorchdistributed_amd.run", "--standalone", "--nproc-per-node", "2",
+                          "examples/04_parameter_server.py", "--epochs", "1"], cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and "server] epoch 0 | steps 32" in out.stdout and "worker] epoch 0 | steps 32" in out.stdout
 
 
 def test_merge_rank_traces_and_overlap(tmp_path):
