@@ -1327,8 +1327,16 @@ Tensor embedding_bwd(Tensor idx, Tensor dy, int64_t V, c10::optional<Tensor> out
   const int64_t D = dy.size(-1);
   c10::DeviceGuard g(dy.device());
   Tensor acc = at::zeros({V, D}, dy.options().dtype(at::kFloat));
-  CHECK_HIP_OK(pda::embedding_bwd(idx.data_ptr<int64_t>(), bp(dy), acc.data_ptr<float>(), idx.numel(), D,
-                                  stream_of(dy)));
+  const char* det = getenv("PDA_DETERMINISTIC");
+  if (det != nullptr && det[0] == '1') {  // fixed-order sums: stable sort by token id, one lane per run
+    auto sorted = at::sort(idx.reshape({-1}), /*stable=*/true, /*dim=*/0, /*descending=*/false);
+    Tensor sidx = std::get<0>(sorted).contiguous(), order = std::get<1>(sorted).contiguous();
+    CHECK_HIP_OK(pda::embedding_bwd_sorted(sidx.data_ptr<int64_t>(), order.data_ptr<int64_t>(), bp(dy),
+                                           acc.data_ptr<float>(), idx.numel(), D, stream_of(dy)));
+  } else {
+    CHECK_HIP_OK(pda::embedding_bwd(idx.data_ptr<int64_t>(), bp(dy), acc.data_ptr<float>(), idx.numel(), D,
+                                    stream_of(dy)));
+  }
   Tensor res = out.has_value() ? *out : at::empty({V, D}, dy.options());
   TORCH_CHECK(res.numel() == V * D);
   CHECK_HIP_OK(pda::cast_scale(acc.data_ptr(), false, res.data_ptr(), is_bf16(res), V * D, 1.f, nullptr,
@@ -1693,6 +1701,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd", &bn_bwd);
   m.def("bn_bwd_table", &bn_bwd_table);
   m.def("set_bn_bwd_fused_max_c", &set_bn_bwd_fused_max_c);
+  m.def("set_dgrad_stream", [](int64_t m) { pda::set_dgrad_stream((int)m); });
   m.def("set_attn_bwd_fused", [](int64_t m) { pda::attention_bwd_fused_mode() = (int)m; });
   m.def("attn_bwd_fused_mode", []() { return (int64_t)pda::attention_bwd_fused_mode(); });
   m.def("bn_bwd_fused_max_c", []() { return bn_bwd_fused_max_c(); });

@@ -50,6 +50,34 @@ bool comm_nonblocking() {
   return !(v && v[0] == '0');
 }
 
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v && *v) ? std::atoi(v) : dflt;
+}
+
+// PDA_COMM_CUS: CUs the comm stream may use (0 = all, no mask)
+int comm_cu_budget() { return env_int("PDA_COMM_CUS", 0); }
+
+// PDA_COMM_MAX_CTAS: RCCL blocks per collective (default: the CU budget when one is set, else RCCL's own)
+int comm_max_ctas(int cu_budget) { return env_int("PDA_COMM_MAX_CTAS", cu_budget > 0 ? cu_budget : 0); }
+
+// n CU bits out of ncu, spread so that they land evenly on the 8 XCDs whether the logical CU ids run
+// XCD-major (CU i on XCD i / (ncu / 8)) or round-robin (CU i on XCD i % 8): bit k sits in block k % 8 of
+// ncu / 8 CUs at offset (k % 8 + 8 j + j / 4) mod (ncu / 8), j = k / 8 — distinct blocks and residues.
+std::vector<uint32_t> cu_mask_spread(int n, int ncu) {
+  std::vector<uint32_t> m((ncu + 31) / 32, 0u);
+  const int blk = ncu / 8 > 0 ? ncu / 8 : 1;
+  int placed = 0;
+  for (int k = 0; placed < n && k < 64 * ncu; ++k) {
+    const int r = k % 8, j = k / 8;
+    const int bit = (r * blk + (r + 8 * j + j / 4) % blk) % ncu;
+    if (m[bit / 32] & (1u << (bit % 32))) continue;
+    m[bit / 32] |= 1u << (bit % 32);
+    ++placed;
+  }
+  return m;
+}
+
 void check_hip(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP ") + what + " failed: " + hipGetErrorString(e));
 }
@@ -180,14 +208,36 @@ class Communicator {
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
     DeviceGuard g(device_);
-    int lo = 0, hi = 0;
-    check_hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
-    check_hip(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, high_priority ? hi : lo),
-              "hipStreamCreateWithPriority");
+    // CU budget (PDA_COMM_CUS = n > 0): the comm stream's hardware queue may only dispatch to n CUs,
+    // spread evenly over the 8 XCDs, and RCCL launches at most n blocks (ncclConfig_t.maxCTAs), so
+    // collective kernels — and the D2D blits of a one-rank group — never take more than n of the 256
+    // CUs from the compute streams' one-workgroup-per-CU GEMM tiles.  n = 0: an unmasked stream.
+    cu_budget_ = comm_cu_budget();
+    if (cu_budget_ > 0) {
+      int ncu = 0;
+      check_hip(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_), "hipDeviceGetAttribute");
+      if (ncu <= 0) ncu = 256;
+      if (cu_budget_ > ncu) cu_budget_ = ncu;
+      std::vector<uint32_t> mask = cu_mask_spread(cu_budget_, ncu);
+      check_hip(hipExtStreamCreateWithCUMask(&stream_, (uint32_t)mask.size(), mask.data()),
+                "hipExtStreamCreateWithCUMask");
+    } else {
+      int lo = 0, hi = 0;
+      check_hip(hipDeviceGetStreamPriorityRange(&lo, &hi), "hipDeviceGetStreamPriorityRange");
+      check_hip(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, high_priority ? hi : lo),
+                "hipStreamCreateWithPriority");
+    }
     check_hip(hipEventCreateWithFlags(&dep_, hipEventDisableTiming), "hipEventCreate");
     nonblocking_ = comm_nonblocking();
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    const int max_ctas = comm_max_ctas(cu_budget_);
+    if (max_ctas > 0) {
+      cfg.maxCTAs = max_ctas;
+      cfg.minCTAs = 1;
+    }
     if (!nonblocking_) {
-      check_nccl(ncclCommInitRank(&comm_, nranks, id, rank), "ncclCommInitRank");
+      cfg.blocking = 1;
+      check_nccl(ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg), "ncclCommInitRankConfig");
       inited_.store(true);
       std::lock_guard<std::mutex> l(g_live_mu);
       g_live.insert(this);
@@ -197,7 +247,6 @@ class Communicator {
     // BEFORE it has connected, and this thread polls its state instead of blocking inside RCCL, so a
     // peer that never joins ends in a watchdog abort that releases the init
     // instead of a SIGABRT while stuck in ncclCommInitRank.
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.blocking = 0;
     check_nccl(ncclCommInitRankConfig(&comm_, nranks, id, rank, &cfg), "ncclCommInitRankConfig");
     {
@@ -257,6 +306,7 @@ class Communicator {
   bool aborted() const { return aborted_.load(); }
   bool closed() const { return closed_.load(); }
   bool nonblocking() const { return nonblocking_; }
+  int cu_budget() const { return cu_budget_; }
 
   // the comm stream waits for everything queued so far on `s` (the producers of the next input)
   void wait_stream(uintptr_t s) {
@@ -303,6 +353,18 @@ class Communicator {
                              to_nccl_dtype(dtype), comm_, stream_),
                "ncclAllGather");
     settle("ncclAllGather");
+    return done();
+  }
+
+  // recv (root only) = op over ranks of send; parameter-server gradients (parallel/param_server.py)
+  std::shared_ptr<Work> reduce(uintptr_t send, uintptr_t recv, int64_t count, int dtype, int op, int root) {
+    std::lock_guard<std::timed_mutex> l(op_mu_);
+    live();
+    DeviceGuard g(device_);
+    check_nccl(ncclReduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), (size_t)count,
+                          to_nccl_dtype(dtype), to_nccl_op(op), root, comm_, stream_),
+               "ncclReduce");
+    settle("ncclReduce");
     return done();
   }
 
@@ -448,6 +510,7 @@ class Communicator {
   hipStream_t stream_ = nullptr;
   hipEvent_t dep_ = nullptr;
   int group_depth_ = 0;
+  int cu_budget_ = 0;
   bool nonblocking_ = false;
   std::atomic<bool> inited_{false}, abort_done_{false}, closed_{false};
   std::atomic<bool> aborted_{false};
@@ -467,6 +530,7 @@ void bind_comm(pybind11::module& m) {
     return v;
   });
   m.def("rccl_abort_all", &Communicator::abort_all, "ncclCommAbort every live communicator of this process");
+  m.def("cu_mask_spread", &cu_mask_spread, "the comm stream's CU mask words for a budget of n of ncu CUs");
   py::class_<Work, std::shared_ptr<Work>>(m, "RcclWork")
       .def("wait", &Work::wait, py::arg("stream"))
       .def("is_completed", &Work::is_completed)
@@ -486,6 +550,7 @@ void bind_comm(pybind11::module& m) {
       .def_property_readonly("aborted", &Communicator::aborted)
       .def_property_readonly("closed", &Communicator::closed)
       .def_property_readonly("nonblocking", &Communicator::nonblocking)
+      .def_property_readonly("cu_budget", &Communicator::cu_budget)
       .def("close", &Communicator::close, py::call_guard<py::gil_scoped_release>())
       .def("wait_stream", &Communicator::wait_stream)
       .def("wait_event", &Communicator::wait_event)
@@ -493,6 +558,7 @@ void bind_comm(pybind11::module& m) {
       .def("reduce_scatter", &Communicator::reduce_scatter)
       .def("all_gather", &Communicator::all_gather)
       .def("broadcast", &Communicator::broadcast)
+      .def("reduce", &Communicator::reduce)
       .def("send", &Communicator::send)
       .def("recv", &Communicator::recv)
       .def("group_start", &Communicator::group_start)

@@ -244,6 +244,8 @@ struct BnBwdStats {
 hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, void* dx, bool dx_f32, int N, int H, int W,
                         int C, int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, const bf16_t* addend,
                         const uint8_t* addend_bits, hipStream_t st, const BnBwdStats* bst = nullptr);
+// PDA_DGRAD_STREAM at run time (-1: back to the environment's value): 0 off, 1 BN-sums dgrads, 2 all short-K
+void set_dgrad_stream(int mode);
 hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32, int N, int H, int W, int C,
                         int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, float* slab,
                         hipStream_t st);
@@ -335,6 +337,8 @@ hipError_t decode_attention(DecodeAttnParams p, hipStream_t st);
 // ---- embed.hip
 hipError_t embedding_fwd(const int64_t* idx, const bf16_t* table, bf16_t* out, int64_t n, int64_t D, hipStream_t st);
 hipError_t embedding_bwd(const int64_t* idx, const bf16_t* dy, float* acc, int64_t n, int64_t D, hipStream_t st);
+hipError_t embedding_bwd_sorted(const int64_t* sidx, const int64_t* order, const bf16_t* dy, float* acc, int64_t n,
+                                int64_t D, hipStream_t st);
 hipError_t rope_apply(const bf16_t* x, bf16_t* y, const float* cos, const float* sin, int B, int T, int H, int D,
                       int64_t sb, int64_t st_, int64_t sh, int64_t yb, int64_t yt, int64_t yh, bool inverse,
                       hipStream_t st);

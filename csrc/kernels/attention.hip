@@ -1324,7 +1324,15 @@ int& attention_bwd_fused_mode() {
   }();
   return mode;
 }
-bool attention_bwd_fused(int D, bool rope) { return !rope && (attention_bwd_fused_mode() & (D == 64 ? 1 : 2)) != 0; }
+// PDA_DETERMINISTIC=1 (nn.py:deterministic, read per call so a process can switch) turns the fused kernel
+// off: its dQ is summed by fp32 atomics in key-tile arrival order, the dQ + dK/dV pair has no atomics.
+static bool deterministic_mode() {
+  const char* e = getenv("PDA_DETERMINISTIC");
+  return e != nullptr && e[0] == '1';
+}
+bool attention_bwd_fused(int D, bool rope) {
+  return !rope && (attention_bwd_fused_mode() & (D == 64 ? 1 : 2)) != 0 && !deterministic_mode();
+}
 
 hipError_t attention_bwd(const AttnParams& p, hipStream_t st) {
   if (p.D != 64 && p.D != 128) return hipErrorInvalidValue;

@@ -4,6 +4,7 @@
 // into an fp32 accumulator of the table with float atomics (no sort); rows are 2-8 KB so every wave
 // instruction adds 1 KB of contiguous bytes (the full-rate atomic shape, guide §6 G12), and only
 // repeated tokens contend.  The fp32 accumulator is cast to the parameter dtype afterwards.
+// (PDA_DETERMINISTIC=1: a sorted, atomic-free variant.)
 // RoPE (rotate-half convention) is normally fused into the attention kernels; `rope_apply` is the
 // standalone form (e.g. for KV-cache writes / tests).
 #include "pda_common.h"
@@ -41,6 +42,33 @@ __global__ void __launch_bounds__(kThreads) embedding_bwd_kernel(const int64_t* 
     float* dst = acc + row * D + c * 8;
 #pragma unroll
     for (int j = 0; j < 8; ++j) atomicAdd(dst + j, g[j]);
+  }
+}
+
+// PDA_DETERMINISTIC=1: the same gradient without atomics.  The tokens come sorted by id (stable sort:
+// `sidx`, with `order` mapping a sorted position back to its token); the lane at the first position of a
+// run of equal ids sums the run's dy rows in token order and stores the table row once.
+__global__ void __launch_bounds__(kThreads) embedding_bwd_sorted_kernel(const int64_t* __restrict__ sidx,
+                                                                        const int64_t* __restrict__ order,
+                                                                        const bf16_t* __restrict__ dy,
+                                                                        float* __restrict__ acc, int64_t n, int64_t D) {
+  const int64_t cv = D / 8;
+  const int64_t total = n * cv;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+    const int64_t j = t / cv, c = t % cv;
+    const int64_t row = sidx[j];
+    if (j > 0 && sidx[j - 1] == row) continue;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int64_t k = j; k < n && sidx[k] == row; ++k) {
+      float g[8];
+      load8(dy + order[k] * D + c * 8, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += g[e];
+    }
+    float* dst = acc + row * D + c * 8;
+    *reinterpret_cast<float4*>(dst) = make_float4(s[0], s[1], s[2], s[3]);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(s[4], s[5], s[6], s[7]);
   }
 }
 
@@ -92,6 +120,12 @@ hipError_t embedding_fwd(const int64_t* idx, const bf16_t* table, bf16_t* out, i
 
 hipError_t embedding_bwd(const int64_t* idx, const bf16_t* dy, float* acc, int64_t n, int64_t D, hipStream_t st) {
   embedding_bwd_kernel<<<grid_for(n * D / 8), kThreads, 0, st>>>(idx, dy, acc, n, D);
+  return hipGetLastError();
+}
+
+hipError_t embedding_bwd_sorted(const int64_t* sidx, const int64_t* order, const bf16_t* dy, float* acc, int64_t n,
+                                int64_t D, hipStream_t st) {
+  embedding_bwd_sorted_kernel<<<grid_for(n * D / 8), kThreads, 0, st>>>(sidx, order, dy, acc, n, D);
   return hipGetLastError();
 }
 

@@ -2911,6 +2911,8 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
     const int64_t M = (int64_t)N * H * W, Nn = C, K = Cout;
     Plan p = plan_gemm(M, Nn, K, false, 512);
     Epi epi = base_epi();
+    // short K (64 / 128) with BN-backward sums: the streaming kernel (HBM-bound shape, dgrad_stream.hip)
+    if (dgrad_stream_ok(M, Nn, K, epi)) return dgrad_stream(dy, w, M, Nn, K, epi, st);
     auto mk_a = [&](auto t) { t.p = dy; t.rows = M; t.K = K; t.ld = Cout; return t; };
     if (wt) {  // conv_dgrad_1x1_wt: B(k = co, n = ci) = wt[ci][co], K-major
       auto mk_bt = [&](auto t) { t.p = wt; t.rows = Nn; t.K = K; t.ld = Cout; return t; };

@@ -72,6 +72,10 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
                    int64_t M, int64_t N, int64_t K, const Epi& epi, int splits, int variant, hipStream_t st,
                    int* used_splits);
 int pp_default_variant();
+// Streaming short-K (64 / 128) 1x1 stride-1 dgrad with the BN-backward sums (dgrad_stream.hip)
+bool dgrad_stream_ok(int64_t M, int64_t N, int64_t K, const Epi& epi);
+hipError_t dgrad_stream(const bf16_t* dy, const bf16_t* w, int64_t M, int64_t N, int64_t K, const Epi& epi,
+                        hipStream_t st);
 hipError_t gemm_pp_wgrad(const bf16_t* dy, const bf16_t* x, int Nimg, int H, int W, int C, int Cout, int R, int S,
                          int P, int Q, int stride, int pad, int dil, const Epi& epi, int splits, hipStream_t stream,
                          int* used_splits);

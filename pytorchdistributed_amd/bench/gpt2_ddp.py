@@ -14,7 +14,7 @@ from ..data.device import DeviceSyntheticTokens
 from ..models.gpt2 import GPT2, config
 from ..optim import AdamW
 from ..parallel.ddp import DistributedDataParallel
-from .common import comm_record, emit, setup, teardown, timed
+from .common import comm_record, emit, group_info, mem_record, setup, teardown, timed
 
 
 def main(argv=None):
@@ -29,7 +29,9 @@ def main(argv=None):
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--layers", type=int, default=None, help="override depth (smoke runs only)")
     a = ap.parse_args(argv)
-    rank, world, local, device = setup(a.gpus)
+    # N = 1 runs the DDP path over a one-rank RCCL group (bucket all-reduces timed, as at N > 1; the
+    # ResNet headline does the same): PDA_DDP_FORCE_COMM=0 skips it
+    rank, world, local, device = setup(a.gpus, one_rank_group=True)
     over = {} if a.layers is None else {"n_layer": a.layers}
     torch.manual_seed(0)
     model = GPT2(config(a.model, n_positions=max(1024, a.seq), **over), device=device, dtype=torch.bfloat16)
@@ -51,6 +53,7 @@ def main(argv=None):
           "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(secs / a.steps * 1e3, 3),
           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
           "data": "synthetic tokens (on-device), random-init weights", "comm": comm,
+          **group_info(device), "mem": mem_record(device),
           "config": {"model": a.model + ("" if a.layers is None else f"-{a.layers}L"),
                      "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": f"dp{world}",
                      "params": model.num_params()}}, rank)

@@ -17,7 +17,7 @@ from ..models.gpt2 import GPT2Stage, config
 from ..optim import AdamW
 from ..parallel.ddp import DistributedDataParallel
 from ..parallel.pipeline import Pipeline, partition_layers, pp_dp_groups
-from .common import emit, setup, teardown, timed
+from .common import comm_record, emit, group_info, setup, teardown, timed
 
 
 def main(argv=None):
@@ -35,7 +35,8 @@ def main(argv=None):
     ap.add_argument("--chunks", type=int, default=2, help="model chunks per rank (interleaved)")
     ap.add_argument("--layers", type=int, default=None)
     a = ap.parse_args(argv)
-    rank, world, local, device = setup(a.gpus)
+    # N = 1: the stage's DDP all-reduce runs over a one-rank RCCL group (timed, as at N > 1)
+    rank, world, local, device = setup(a.gpus, one_rank_group=True)
     pp = a.pp or min(4, world)
     dp = world // pp
     cfg = config(a.model, **({} if a.layers is None else {"n_layer": a.layers}))
@@ -78,13 +79,13 @@ def main(argv=None):
         pipe.step(x, y)
         opt.step()
 
-    secs = timed(step, a.steps, a.warmup)
-    comm = ddp.comm_stats()
+    secs = timed(step, a.steps, a.warmup, on_start=lambda: ddp.comm_stats(reset=True))
+    comm = comm_record(ddp, a.steps)
     toks = a.micro * a.micro_batch * a.seq * dp * a.steps / secs
     emit({"metric": "tokens/sec (whole job) GPT-2-XL pipeline x DDP", "value": round(toks, 1),
           "unit": "tokens/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
           "ms_per_step": round(secs / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-          "vs_baseline": None, "dtype": "bf16", "dp_comm": comm, "data": "synthetic tokens (on-device), random-init weights",
+          "vs_baseline": None, "dtype": "bf16", "dp_comm": comm, **group_info(device), "data": "synthetic tokens (on-device), random-init weights",
           "config": {"model": a.model, "global_batch": a.micro * a.micro_batch * dp, "seq_len": a.seq,
                      "parallelism": f"pp{pp}xdp{dp}", "schedule": a.schedule, "microbatches": a.micro,
                      **({"chunks": a.chunks} if a.schedule == "interleaved" else {})}}, rank)

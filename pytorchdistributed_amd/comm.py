@@ -202,6 +202,20 @@ class Communicator:
         return self._done(Work(self._c.all_gather(inp.data_ptr(), out.data_ptr(), inp.numel(), _DTYPE[inp.dtype]),
                                (out, inp)))
 
+    def reduce(self, t: torch.Tensor, root: int = 0, op: str = "sum", streams=None) -> Work:
+        """In place: group rank ``root``'s ``t`` becomes op over ranks (the others' ``t`` is unchanged)."""
+        assert t.is_contiguous() and t.device == self.device
+        self._check("reduce", t, op=op, dst=root)
+        self._after(streams)
+        self._hold(t)
+        return self._done(Work(self._c.reduce(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPE[t.dtype], _OPS[op], root),
+                               (t,)))
+
+    @property
+    def cu_budget(self) -> int:
+        """CUs the comm stream may dispatch to (``PDA_COMM_CUS``; 0 = unmasked)."""
+        return self._c.cu_budget
+
     def broadcast(self, t: torch.Tensor, root: int = 0, streams=None) -> Work:
         """In place from group rank ``root``."""
         assert t.is_contiguous()

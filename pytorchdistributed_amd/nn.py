@@ -26,7 +26,10 @@ def deterministic() -> bool:
     (forward) and the dgrad epilogues into the backward table: tile t adds into row t % R.  With R at
     least the number of output-row tiles (64-row tiles are the smallest), every row receives exactly one
     add per column (0 + v is exact) and the finalize sums the rows in a fixed order.  Split-K weight
-    gradients already reduce fp32 slabs in a fixed order; everything else is elementwise or slab-based."""
+    gradients already reduce fp32 slabs in a fixed order; everything else is elementwise or slab-based.
+    The transformer path's two atomic reductions switch too (read per call by the native layer): the
+    fused attention backward (dQ by fp32 atomics) gives way to the dQ + dK/dV kernel pair, and the
+    embedding backward sums each token id's rows in sorted order (`embed.hip:embedding_bwd_sorted_kernel`)."""
     return os.environ.get("PDA_DETERMINISTIC", "0") == "1"
 
 

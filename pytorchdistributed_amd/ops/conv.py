@@ -72,7 +72,7 @@ class _Conv2dFn(torch.autograd.Function):
                     kw = bnb.dgrad_kwargs()
                 dx = C().conv_dgrad(dy, w, x.shape[1], x.shape[2], stride, padding, dilation, addend, bits, **kw)
                 if kw:
-                    bnb.filled = True
+                    bnb.mark_filled(dx)
         ctx.bnb = None
         if ctx.needs_input_grad[1]:
             target = grad_target(ctx.wparam)

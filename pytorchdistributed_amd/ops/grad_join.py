@@ -84,7 +84,7 @@ class BnBwdStats:
     complete in the dgrad of the LAST consumer of the shared gradient join (the one whose epilogue adds
     the other consumers' stashed gradients)."""
 
-    __slots__ = ("z", "ss", "bits", "mean", "table", "needs_join", "token", "z2", "mean2", "table2")
+    __slots__ = ("z", "ss", "bits", "mean", "table", "needs_join", "token", "z2", "mean2", "table2", "dx", "dx_ver")
 
     def __init__(self, z, ss, bits, mean, table, needs_join: bool, token=None, second=None):
         self.z, self.ss, self.bits, self.mean, self.table = z, ss, bits, mean, table
@@ -97,6 +97,31 @@ class BnBwdStats:
             token = [False]
         self.token = list(token) if isinstance(token, tuple) else [token]
         self.filled = False
+        self.dx, self.dx_ver = None, -1
+
+    def mark_filled(self, dx: torch.Tensor):
+        """The dgrad that produced ``dx`` filled the table(s) from it.  ``dx`` is held so the BN backward
+        can check that its incoming gradient IS this tensor, unmodified (:meth:`take_if_matches`)."""
+        self.dx, self.dx_ver = dx, dx._version
+        self.filled = True
+
+    def take_if_matches(self, dy: torch.Tensor) -> bool:
+        """BN backward: True when the tables hold the sums of exactly ``dy``.  If the BN output had a
+        consumer besides the fused conv (an auxiliary head, a hook, a user model reusing the block),
+        autograd summed its gradient into a different tensor or bumped dx's version in place: the tables
+        then miss that contribution, so they are re-zeroed and False sends the caller to the reduce pass.
+        Either way the flag is cleared and the hold on dx released."""
+        if not self.filled:
+            return False
+        dx, ver = self.dx, self.dx_ver
+        self.dx, self.dx_ver = None, -1
+        self.filled = False
+        if (dx is not None and dy.data_ptr() == dx.data_ptr() and dy.shape == dx.shape and dy._version == ver):
+            return True
+        self.table.zero_()
+        if self.table2 is not None:
+            self.table2.zero_()
+        return False
 
     @property
     def filled(self) -> bool:

@@ -72,9 +72,8 @@ class _BatchNormFn(torch.autograd.Function):
         # epilogue, so the backward apply kernel never stores it
         masked = has_res and ctx.join is not None and bits is not None and not ctx.join.is_last()
         bnb = ctx.bnb
-        if bnb is not None and bnb.filled:
+        if bnb is not None and bnb.take_if_matches(dy):
             # the sums were accumulated by the dgrad that produced dy: finalize + apply only
-            bnb.filled = False
             dx, dres, dgamma, dbeta = C().bn_bwd_table(dy, x, bits, ss if bits is None else None, mean, invstd, gamma,
                                                        relu, has_res and not masked, bnb.table, tg, tb)
         else:
@@ -131,9 +130,8 @@ class _DualBatchNormFn(torch.autograd.Function):
         tg, tb = _param_targets(ctx, gamma, beta, 1, 2)
         tg2, tb2 = _param_targets(ctx, gamma2, beta2, 4, 5)
         bnb, ctx.bnb = ctx.bnb, None
-        if bnb is not None and bnb.filled:
+        if bnb is not None and bnb.take_if_matches(dy):
             # both reductions were accumulated by the dgrad that produced dy: finalizes + the apply pass(es)
-            bnb.filled = False
             if C().bn_bwd_dual_ok(x.shape[-1]):
                 dx, dx2, dg, db, dg2, db2 = C().bn_bwd_dual(dy, bits, x, mean, invstd, gamma, x2, mean2, invstd2,
                                                             gamma2, tg, tb, tg2, tb2, bnb.table, bnb.table2)

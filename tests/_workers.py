@@ -1248,6 +1248,8 @@ def param_server_worker(rank, world, outdir, steps):
 def ps_rccl_world1_worker(rank, world, outdir):
     """ParameterServer over a ONE-rank RCCL group on the GPU (reduce / broadcast are real RCCL launches on
     device tensors): three steps equal a local replica's; the optimizer lives on the server only."""
+    import torch.distributed as dist
+
     import pytorchdistributed_amd.distributed as pd
     from pytorchdistributed_amd.models.mlp import MnistMLP
     from pytorchdistributed_amd.parallel.param_server import ParameterServer
@@ -1259,14 +1261,26 @@ def ps_rccl_world1_worker(rank, world, outdir):
     local = MnistMLP((64, 256, 128, 10)).cuda()
     local.load_state_dict(model.state_dict())
     ps = ParameterServer(model, lambda params: torch.optim.SGD(params, lr=0.05, momentum=0.9))
+    assert ps.native, "parameter server must run on the native RCCL communicator on GPU tensors"
     lopt = torch.optim.SGD(local.parameters(), lr=0.05, momentum=0.9)
     g = torch.Generator().manual_seed(13)
+
+    def no_c10d(*a, **k):
+        raise AssertionError("c10d collective inside ParameterServer.step() on GPU")
+
+    real = {n: getattr(dist, n) for n in ("reduce", "broadcast", "all_reduce")}
     for _ in range(3):
         x = torch.randn(32, 64, generator=g).cuda()
         y = torch.randint(0, 10, (32,), generator=g).cuda()
         ps.zero_grad()
         F.cross_entropy(ps(x), y).backward()
-        ps.step()
+        for n in real:
+            setattr(dist, n, no_c10d)
+        try:
+            ps.step()
+        finally:
+            for n, f in real.items():
+                setattr(dist, n, f)
         lopt.zero_grad()
         F.cross_entropy(local(x), y).backward()
         lopt.step()
@@ -1275,4 +1289,39 @@ def ps_rccl_world1_worker(rank, world, outdir):
     assert ps.comm_bytes > 0 and ps.steps == 3
     with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
         f.write(f"ok {worst:.3e} comm_bytes={ps.comm_bytes}")
+    pd.destroy_process_group()
+
+
+def param_server_unused_frozen_worker(rank, world, outdir):
+    """frozen parameters follow the server at construction, and a parameter no rank
+    produced a gradient for is left alone by the server's optimizer (grad None: no weight decay /
+    momentum step), as in single-process training."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.param_server import ParameterServer
+
+    pd.init_process_group("gloo")
+    torch.manual_seed(100 + rank)  # different init per rank
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.used = torch.nn.Linear(8, 4)
+            self.unused = torch.nn.Linear(8, 4)
+            self.frozen = torch.nn.Linear(8, 8)
+            self.frozen.requires_grad_(False)
+
+        def forward(self, x):
+            return self.used(self.frozen(x))
+
+    m = M()
+    ps = ParameterServer(m, lambda params: torch.optim.SGD(params, lr=0.1, momentum=0.9, weight_decay=0.1))
+    start = {k: v.clone() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(3)
+    for _ in range(2):
+        x = torch.randn(4, 8, generator=g)
+        ps.zero_grad()
+        m(x).square().mean().backward()
+        ps.step()
+    out = {"start": start, "end": {k: v.clone() for k, v in m.state_dict().items()}}
+    torch.save(out, os.path.join(outdir, f"{rank}.pt"))
     pd.destroy_process_group()

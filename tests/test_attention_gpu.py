@@ -162,3 +162,43 @@ def test_llama_tiny_native_vs_reference():
         g = dict(gpu.named_parameters())[n].grad.float().cpu().flatten()
         r = dict(ref.named_parameters())[n].grad.float().flatten()
         assert torch.nn.functional.cosine_similarity(g, r, dim=0) > 0.98, n
+
+
+def test_deterministic_mode_transformer_bit_identical(monkeypatch):
+    """PDA_DETERMINISTIC=1 also covers the transformer path — the fused attention backward (dQ
+    by fp32 atomics) gives way to the atomic-free dQ + dK/dV pair and the embedding backward sums each
+    token's rows in sorted order.  Two GPT-2 training steps from the same state are bit-identical, and the
+    deterministic embedding gradient equals the fp32 reference."""
+    import copy
+
+    from pytorchdistributed_amd.models.gpt2 import GPT2, config
+
+    monkeypatch.setenv("PDA_DETERMINISTIC", "1")
+    torch.manual_seed(0)
+    cfg = config("gpt2", n_layer=2, n_embd=256, n_head=4, n_positions=512, vocab_size=1000)
+    base = GPT2(cfg, dtype=torch.bfloat16).cuda()
+    idx = torch.randint(0, 50, (4, 512), device="cuda")  # many repeated tokens: contended embedding rows
+    tgt = torch.randint(0, 1000, (4, 512), device="cuda")
+
+    def run():
+        m = copy.deepcopy(base)
+        loss = m(idx, tgt)
+        loss.backward()
+        torch.cuda.synchronize()
+        return loss.detach().clone(), [p.grad.detach().clone() for p in m.parameters()]
+
+    l1, g1 = run()
+    l2, g2 = run()
+    assert torch.equal(l1, l2)
+    assert all(torch.equal(a, b) for a, b in zip(g1, g2))
+    # the sorted embedding backward against fp32 index_add
+    from pytorchdistributed_amd.ops import embedding
+
+    table = torch.randn(100, 64).to(torch.bfloat16)
+    ids = torch.randint(0, 7, (5, 33))
+    dy = torch.randn(5, 33, 64).to(torch.bfloat16)
+    tg = table.cuda().requires_grad_()
+    embedding(ids.cuda(), tg).backward(dy.cuda())
+    ref = torch.zeros(100, 64).index_add_(0, ids.reshape(-1), dy.float().reshape(-1, 64))
+    assert rel_err(tg.grad.cpu(), ref) < 1e-2
+    assert tg.grad[7:].abs().sum().item() == 0

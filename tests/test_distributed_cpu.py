@@ -357,3 +357,17 @@ def test_parameter_server_matches_single_process(tmp_path):
     for k, v in ref.state_dict().items():
         assert torch.allclose(s0[k], v, atol=1e-5), k
         assert torch.equal(s0[k], s1[k]), k
+
+
+def test_parameter_server_frozen_and_unused_params(tmp_path):
+    """Frozen parameters are synced from the server at construction; a parameter without a gradient on
+    every rank is not stepped by the server's optimizer (weight decay / momentum would move it)."""
+    spawn(_workers.param_server_unused_frozen_worker, args=(2, str(tmp_path)), nprocs=2, timeout=120)
+    s0 = torch.load(tmp_path / "0.pt", weights_only=True)
+    s1 = torch.load(tmp_path / "1.pt", weights_only=True)
+    for k in s0["start"]:
+        assert torch.equal(s0["start"][k], s1["start"][k]), k  # every rank starts from the server's state
+        assert torch.equal(s0["end"][k], s1["end"][k]), k
+    for k in ("unused.weight", "unused.bias", "frozen.weight", "frozen.bias"):
+        assert torch.equal(s0["start"][k], s0["end"][k]), k
+    assert not torch.equal(s0["start"]["used.weight"], s0["end"]["used.weight"])

@@ -312,6 +312,14 @@ def test_tied_embedding_side_stream_matches_single_stream():
     (4, 14, 14, 64, 256, 1, 1, 0, "bits", True),
     (32, 14, 14, 256, 1024, 1, 1, 0, "dual", True),  # after a downsample block: two BNs, one masked dy
     (4, 14, 14, 64, 256, 1, 1, 0, "dual", True),
+    # short K (64 / 128): the streaming kernel (dgrad_stream.hip), with M not a multiple of its 16-row tile
+    (8, 28, 28, 256, 64, 1, 1, 0, "ss", False),
+    (6, 15, 15, 256, 64, 1, 1, 0, "bits", True),
+    (8, 28, 28, 256, 64, 1, 1, 0, "dual", True),
+    (4, 14, 14, 512, 128, 1, 1, 0, "bits", True),
+    (5, 13, 13, 512, 128, 1, 1, 0, "dual", True),
+    (4, 14, 14, 256, 128, 1, 1, 0, "ss", False),
+    (4, 14, 14, 128, 64, 1, 1, 0, "bits", False),   # N = 128: two waves per workgroup
 ])
 def test_conv_dgrad_bn_bwd_stats(case):
     """The dgrad epilogue's BN-backward sums (gemm_epi.h bst_*) equal fp32 sums over the dx the same
@@ -343,23 +351,49 @@ def test_conv_dgrad_bn_bwd_stats(case):
         kw["bst_bits"] = bits
         shifts = torch.arange(8, device=dev, dtype=torch.uint8)
         keep = ((bits.reshape(-1, 1) >> shifts) & 1).bool().reshape(z.shape)
-    dx = C().conv_dgrad(dy, w, H, W, st, pad, 1, addend, None, **kw)
     dx_ref = C().conv_dgrad(dy, w, H, W, st, pad, 1, addend, None)
-    assert torch.equal(dx, dx_ref)
-    g = torch.where(keep, dx.float(), torch.zeros((), device=dev)).reshape(-1, Cin)
-    s1 = g.sum(0)
-    s2 = (g * (z.float().reshape(-1, Cin) - mean)).sum(0)
-    tab = table.sum(0)
-    scale1 = g.abs().sum(0) + 1e-3
-    scale2 = (g * (z.float().reshape(-1, Cin) - mean)).abs().sum(0) + 1e-3
-    assert ((tab[0] - s1).abs() / scale1).max().item() < 1e-4
-    assert ((tab[1] - s2).abs() / scale2).max().item() < 1e-4
-    if src == "dual":
-        t2 = table2.sum(0)
-        s3 = (g * (z2.float().reshape(-1, Cin) - mean2)).sum(0)
-        scale3 = (g * (z2.float().reshape(-1, Cin) - mean2)).abs().sum(0) + 1e-3
-        assert ((t2[0] - s1).abs() / scale1).max().item() < 1e-4
-        assert ((t2[1] - s3).abs() / scale3).max().item() < 1e-4
+
+    def run(mode):
+        t1 = torch.zeros_like(table)
+        k = dict(kw, bst_table=t1)
+        t2 = None
+        if src == "dual":
+            t2 = torch.zeros_like(table2)
+            k["bst_table2"] = t2
+        C().set_dgrad_stream(mode)
+        try:
+            return C().conv_dgrad(dy, w, H, W, st, pad, 1, addend, None, **k), t1, t2
+        finally:
+            C().set_dgrad_stream(-1)
+
+    # default routing; and for short K (64 / 128) the streaming kernel on every launch vs the 256 x 256 tile
+    modes = [-1] + ([3, 0] if R == 1 and Cout in (64, 128) else [])
+    for mode in modes:
+        dx, tab1, tab2 = run(mode)
+        assert torch.equal(dx, dx_ref), mode
+        g = torch.where(keep, dx.float(), torch.zeros((), device=dev)).reshape(-1, Cin)
+        s1 = g.sum(0)
+        s2 = (g * (z.float().reshape(-1, Cin) - mean)).sum(0)
+        tab = tab1.sum(0)
+        scale1 = g.abs().sum(0) + 1e-3
+        scale2 = (g * (z.float().reshape(-1, Cin) - mean)).abs().sum(0) + 1e-3
+        assert ((tab[0] - s1).abs() / scale1).max().item() < 1e-4, mode
+        assert ((tab[1] - s2).abs() / scale2).max().item() < 1e-4, mode
+        if src == "dual":
+            t2 = tab2.sum(0)
+            s3 = (g * (z2.float().reshape(-1, Cin) - mean2)).sum(0)
+            scale3 = (g * (z2.float().reshape(-1, Cin) - mean2)).abs().sum(0) + 1e-3
+            assert ((t2[0] - s1).abs() / scale1).max().item() < 1e-4, mode
+            assert ((t2[1] - s3).abs() / scale3).max().item() < 1e-4, mode
+    if R == 1 and Cout in (64, 128):  # plain short-K dgrads on the streaming kernel (mode 2), with / without addend
+        C().set_dgrad_stream(2)
+        try:
+            dx_plain = C().conv_dgrad(dy, w, H, W, st, pad, 1, addend, None)
+            dx_noadd = C().conv_dgrad(dy, w, H, W, st, pad, 1, None, None)
+        finally:
+            C().set_dgrad_stream(-1)
+        assert torch.equal(dx_plain, dx_ref)
+        assert torch.equal(dx_noadd, C().conv_dgrad(dy, w, H, W, st, pad, 1, None, None))
 
 
 def test_bottleneck_bwd_stats_from_dgrad_epilogue(monkeypatch):
@@ -420,6 +454,46 @@ def test_bottleneck_bwd_stats_from_dgrad_epilogue(monkeypatch):
     for (n, pr), pb, gf, gu in zip(pair_ref.named_parameters(), pair_b16.parameters(), grads[True][1:], grads[False][1:]):
         assert rel_err(gf, pr.grad) < max(2e-2, 1.5 * rel_err(pb.grad, pr.grad)), n
         assert rel_err(gf, gu) < 1e-2, n
+
+
+@pytest.mark.parametrize("tap", [0, 1])
+def test_bn_bwd_table_skipped_for_extra_consumer(monkeypatch, tap):
+    """a block output that also feeds a second loss term (an auxiliary head) gets its gradient
+    summed by autograd, so the next block's conv1 dgrad epilogue saw only part of it.  The BN backward must
+    notice (dy is not the dgrad's dx) and fall back to the reduce pass: the gradients equal the path with
+    the epilogue sums off, for the dual output BN (tap 0, downsample block) and an identity bn3 (tap 1)."""
+    from pytorchdistributed_amd.models.resnet import resnet50
+    from pytorchdistributed_amd.ops import norm as _norm
+
+    torch.manual_seed(0)
+    ref = resnet50(dtype=torch.bfloat16)
+    blocks = [ref.layer1[0], ref.layer1[1], ref.layer1[2]]
+    xin = torch.randn(8, 16, 16, 64).to(torch.bfloat16)
+    dy = torch.randn(8, 16, 16, 256).to(torch.bfloat16)
+    grads = {}
+    for fused in (True, False):
+        monkeypatch.setattr(_norm, "_BWD_EPILOGUE", fused)
+        bs = [copy.deepcopy(b).to("cuda") for b in blocks]
+        xg = xin.to("cuda").requires_grad_()
+        h = xg
+        aux = None
+        for i, b in enumerate(bs):
+            h = b(h)
+            if i == tap:
+                aux = h
+        loss = (h.float() * dy.to("cuda").float()).sum() + 0.5 * (aux.float() ** 2).sum()
+        loss.backward()
+        torch.cuda.synchronize()
+        grads[fused] = [xg.grad.cpu()] + [p.grad.cpu() for b in bs for p in b.parameters()]
+        # every table handed out was consumed or re-zeroed: nothing stays filled for the next step
+        for b in bs:
+            for m in b.modules():
+                tok = getattr(m, "_bwd_token", None)
+                if tok is not None:
+                    assert not tok[0]
+                    assert m._bwd_table.abs().sum().item() == 0
+    for gf, gu in zip(grads[True], grads[False]):
+        assert rel_err(gf, gu) < 1e-2
 
 
 def test_deterministic_mode_bit_identical(monkeypatch):

@@ -30,6 +30,12 @@ for step in "$@"; do
     llama_prof) export TMPDIR=/tmp; run llama_prof 600 rocprofv3 --kernel-trace --output-format csv -d "$out/llama_prof" -o run -- python -u -m pytorchdistributed_amd.bench.llama_fsdp --steps 2 --warmup 2 ;;
     resnet_prof) export TMPDIR=/tmp; PDA_WGRAD_STREAM=0 run resnet_prof 600 rocprofv3 --kernel-trace --output-format csv -d "$out/resnet_prof" -o run -- python -u -m pytorchdistributed_amd.bench.resnet_ddp --steps 3 --warmup 3 ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    # multi-rank rehearsal on a one-GPU box: ranks share the GPU over gloo (RCCL refuses two ranks per
+    # device), so the DDP and pipeline x DDP paths run with world > 1 on the native kernels
+    rehearse_dp) PDA_DIST_BACKEND=gloo run rehearse_dp2 300 python -u bench.py --gpus 2 --steps 5 --warmup 2 --batch 256
+                 PDA_DIST_BACKEND=gloo run rehearse_dp4 300 python -u bench.py --gpus 4 --steps 5 --warmup 2 --batch 128 ;;
+    rehearse_pp) PDA_DIST_BACKEND=gloo run rehearse_pp 400 python -u -m pytorchdistributed_amd.bench.gpt2xl_pp --gpus 4 --pp 2 --micro 4 --micro-batch 4 --steps 3 --warmup 1 ;;
+    gpt2xl_pp) run gpt2xl_pp 600 python -u -m pytorchdistributed_amd.bench.gpt2xl_pp --steps 4 --warmup 2 ;;
     *) echo "[session] unknown step $step" ;;
   esac
 done

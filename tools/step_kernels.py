@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--out", default="")
     ap.add_argument("--title", default="")
+    ap.add_argument("--stream", default="", help="only the dispatches of this Stream_Id / Queue_Id ('list': "
+                                                  "print each stream's kernel time in the step)")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     marks = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
@@ -24,6 +26,21 @@ def main():
         raise SystemExit(f"fewer than two '{a.marker}' dispatches in the trace")
     lo, hi = marks[a.step - 1], marks[a.step]
     step = rows[lo + 1: hi + 1]
+
+    def sid(r):
+        return r.get("Stream_Id") or r.get("Queue_Id") or "0"
+
+    if a.stream == "list":
+        per = collections.defaultdict(float)
+        cnt = collections.Counter()
+        for r in step:
+            per[sid(r)] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+            cnt[sid(r)] += 1
+        for k, v in sorted(per.items(), key=lambda kv: -kv[1]):
+            print(f"stream {k}: {v:.3f} ms of kernels in {cnt[k]} dispatches")
+        return
+    if a.stream:
+        step = [r for r in step if sid(r) == a.stream]
     t = collections.defaultdict(float)
     n = collections.Counter()
     for r in step:
