@@ -1517,6 +1517,17 @@ int64_t stream_create(int64_t device, int64_t priority) {
   return reinterpret_cast<int64_t>(s);
 }
 
+// a stream whose hardware queue dispatches only to `ncu` CUs spread over the XCDs (invert: all the others)
+int64_t stream_create_cumask(int64_t device, int64_t ncu, bool invert) {
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  int total = 0;
+  CHECK_HIP_OK(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, (int)device));
+  std::vector<uint32_t> mask = pda_rt::cu_mask_spread((int)ncu, total, invert);
+  hipStream_t s = nullptr;
+  CHECK_HIP_OK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+  return reinterpret_cast<int64_t>(s);
+}
+
 std::vector<int64_t> stream_priority_range(int64_t device) {
   c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
   int least = 0, greatest = 0;
@@ -1689,6 +1700,7 @@ Tensor avgpool_f32_bwd(Tensor dy, int64_t H, int64_t W) {
 PYBIND11_MODULE(_C, m) {
   m.def("stream_create", &stream_create, py::arg("device"), py::arg("priority"));
   m.def("stream_priority_range", &stream_priority_range, py::arg("device"));
+  m.def("stream_create_cumask", &stream_create_cumask, py::arg("device"), py::arg("ncu"), py::arg("invert") = false);
   m.doc() = "pytorchdistributed_amd native layer: CDNA4 HIP kernels + C++ runtime";
   m.def("sgd_step", &sgd_step);
   m.def("adam_step", &adam_step);

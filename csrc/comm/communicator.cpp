@@ -61,23 +61,6 @@ int comm_cu_budget() { return env_int("PDA_COMM_CUS", 0); }
 // PDA_COMM_MAX_CTAS: RCCL blocks per collective (default: the CU budget when one is set, else RCCL's own)
 int comm_max_ctas(int cu_budget) { return env_int("PDA_COMM_MAX_CTAS", cu_budget > 0 ? cu_budget : 0); }
 
-// n CU bits out of ncu, spread so that they land evenly on the 8 XCDs whether the logical CU ids run
-// XCD-major (CU i on XCD i / (ncu / 8)) or round-robin (CU i on XCD i % 8): bit k sits in block k % 8 of
-// ncu / 8 CUs at offset (k % 8 + 8 j + j / 4) mod (ncu / 8), j = k / 8 — distinct blocks and residues.
-std::vector<uint32_t> cu_mask_spread(int n, int ncu) {
-  std::vector<uint32_t> m((ncu + 31) / 32, 0u);
-  const int blk = ncu / 8 > 0 ? ncu / 8 : 1;
-  int placed = 0;
-  for (int k = 0; placed < n && k < 64 * ncu; ++k) {
-    const int r = k % 8, j = k / 8;
-    const int bit = (r * blk + (r + 8 * j + j / 4) % blk) % ncu;
-    if (m[bit / 32] & (1u << (bit % 32))) continue;
-    m[bit / 32] |= 1u << (bit % 32);
-    ++placed;
-  }
-  return m;
-}
-
 void check_hip(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("HIP ") + what + " failed: " + hipGetErrorString(e));
 }
@@ -218,7 +201,7 @@ class Communicator {
       check_hip(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device_), "hipDeviceGetAttribute");
       if (ncu <= 0) ncu = 256;
       if (cu_budget_ > ncu) cu_budget_ = ncu;
-      std::vector<uint32_t> mask = cu_mask_spread(cu_budget_, ncu);
+      std::vector<uint32_t> mask = pda_rt::cu_mask_spread(cu_budget_, ncu);
       check_hip(hipExtStreamCreateWithCUMask(&stream_, (uint32_t)mask.size(), mask.data()),
                 "hipExtStreamCreateWithCUMask");
     } else {
@@ -530,7 +513,8 @@ void bind_comm(pybind11::module& m) {
     return v;
   });
   m.def("rccl_abort_all", &Communicator::abort_all, "ncclCommAbort every live communicator of this process");
-  m.def("cu_mask_spread", &cu_mask_spread, "the comm stream's CU mask words for a budget of n of ncu CUs");
+  m.def("cu_mask_spread", &pda_rt::cu_mask_spread, py::arg("n"), py::arg("ncu"), py::arg("invert") = false,
+        "CU mask words: n of ncu CUs spread over the XCDs (the comm stream's budget; invert = the rest)");
   py::class_<Work, std::shared_ptr<Work>>(m, "RcclWork")
       .def("wait", &Work::wait, py::arg("stream"))
       .def("is_completed", &Work::is_completed)

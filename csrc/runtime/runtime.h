@@ -13,6 +13,28 @@
 
 namespace pda_rt {
 
+// ------------------------------------------------------------------ CU masks
+// n of ncu CU bits (the hipExtStreamCreateWithCUMask word array), spread so that they land evenly on the 8
+// XCDs whether the logical CU ids run XCD-major (CU i on XCD i / (ncu / 8)) or round-robin (CU i on XCD
+// i % 8): bit k sits in block k % 8 of ncu / 8 CUs at offset (k % 8 + 8 j + j / 4) mod (ncu / 8), j = k / 8.
+// invert: the complement (the CUs a mask of n leaves to everything else).
+inline std::vector<uint32_t> cu_mask_spread(int n, int ncu, bool invert = false) {
+  std::vector<uint32_t> m((ncu + 31) / 32, 0u);
+  const int blk = ncu / 8 > 0 ? ncu / 8 : 1;
+  int placed = 0;
+  for (int k = 0; placed < n && k < 64 * ncu; ++k) {
+    const int r = k % 8, j = k / 8;
+    const int bit = (r * blk + (r + 8 * j + j / 4) % blk) % ncu;
+    if (m[bit / 32] & (1u << (bit % 32))) continue;
+    m[bit / 32] |= 1u << (bit % 32);
+    ++placed;
+  }
+  if (invert) {
+    for (int b = 0; b < ncu; ++b) m[b / 32] ^= 1u << (b % 32);
+  }
+  return m;
+}
+
 // ------------------------------------------------------------------ sockets
 int tcp_listen(const std::string& host, int port, int* bound_port);
 int tcp_connect(const std::string& host, int port, double timeout_s);

@@ -32,9 +32,11 @@ def main(argv=None):
     rank, world, local, device = setup(a.gpus)
     over = {} if a.layers is None else {"n_layers": a.layers}
     torch.manual_seed(0)
-    model = Llama(config(a.model, **over), device=device, dtype=torch.bfloat16)
+    # built on the meta device: FSDP materialises one block at a time and keeps this rank's shard (deferred
+    # initialisation: a rank never holds the full 8 B-parameter model, only 1/world of it plus one unit)
+    model = Llama(config(a.model, **over), device="meta", dtype=torch.bfloat16)
     n_params = sum(p.numel() for p in model.parameters())
-    fsdp = FullyShardedDataParallel(model, unit_types=(LlamaBlock,))
+    fsdp = FullyShardedDataParallel(model, unit_types=(LlamaBlock,), device=device)
     opt = AdamW(fsdp.parameters(), lr=3e-4, weight_decay=0.1)
     data = DeviceSyntheticTokens(a.batch, a.seq, model.cfg.vocab_size, device=device, rank=rank)
 
@@ -52,7 +54,7 @@ def main(argv=None):
           "unit": "tokens/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
           "ms_per_step": round(secs / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
           "vs_baseline": None, "dtype": "bf16", "data": "synthetic tokens (on-device), random-init weights", "comm": comm,
-          "mem": mem_record(device),
+          "mem": dict(mem_record(device), init_peak_gib=round(fsdp.init_peak_bytes / 2 ** 30, 2)),
           "config": {"model": a.model + ("" if a.layers is None else f"-{a.layers}L"),
                      "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": f"fsdp{world}",
                      "params": n_params}}, rank)

@@ -92,10 +92,14 @@ class LlamaBlock(tnn.Module):
 
 
 class Llama(tnn.Module):
-    def __init__(self, cfg: LlamaConfig, device=None, dtype=None):
+    def __init__(self, cfg: LlamaConfig, device=None, dtype=None, seed=None):
+        """``device="meta"``: no storage is allocated — FSDP then builds each unit directly as a shard
+        (:meth:`init_unit` fills one unit at a time, parallel/fsdp.py).  ``seed``: base of the per-unit
+        initialisation streams (default: drawn from the global RNG, so ``torch.manual_seed`` fixes it)."""
         super().__init__()
         self.cfg = cfg
         kw = dict(device=device, dtype=dtype)
+        self.init_seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if seed is None else int(seed)
         self.tok_embeddings = tnn.Parameter(torch.empty(cfg.vocab_size, cfg.dim, **kw))
         self.layers = tnn.ModuleList([LlamaBlock(cfg, **kw) for _ in range(cfg.n_layers)])
         self.norm = pnn.RMSNorm(cfg.dim, cfg.norm_eps, **kw)
@@ -105,14 +109,39 @@ class Llama(tnn.Module):
 
     @torch.no_grad()
     def reset_parameters(self):
+        if self.tok_embeddings.is_meta:
+            return
+        for i, blk in enumerate(self.layers):
+            self.init_unit(blk, i)
+        self.init_unit(self, len(self.layers))
+
+    @torch.no_grad()
+    def init_unit(self, module: tnn.Module, index: int):
+        """Initialise one FSDP unit's parameters — block ``index``, or (``module`` is the model, index =
+        n_layers) the embedding, final norm and head — from its own generator seeded by (init_seed, index).
+        Eager construction and FSDP's deferred one run exactly this, unit by unit, so they produce the same
+        bits (test_fsdp_cpu.py::test_fsdp_deferred_init_matches_eager)."""
         std = 0.02
-        self.tok_embeddings.normal_(0, std)
-        for blk in self.layers:
-            for lin in (blk.wqkv, blk.w13):
-                lin.weight.normal_(0, std)
-            for lin in (blk.wo, blk.w2):
-                lin.weight.normal_(0, std / math.sqrt(2 * self.cfg.n_layers))
-        self.output.weight.normal_(0, std)
+        std_out = std / math.sqrt(2 * self.cfg.n_layers)
+
+        def gen(t):
+            g = torch.Generator(device=t.device)
+            g.manual_seed(self.init_seed * 1000003 + index)
+            return g
+
+        if isinstance(module, LlamaBlock):
+            g = gen(module.wqkv.weight)
+            module.attention_norm.weight.fill_(1.0)
+            module.wqkv.weight.normal_(0, std, generator=g)
+            module.wo.weight.normal_(0, std_out, generator=g)
+            module.ffn_norm.weight.fill_(1.0)
+            module.w13.weight.normal_(0, std, generator=g)
+            module.w2.weight.normal_(0, std_out, generator=g)
+        else:
+            g = gen(self.tok_embeddings)
+            self.tok_embeddings.normal_(0, std, generator=g)
+            self.norm.weight.fill_(1.0)
+            self.output.weight.normal_(0, std, generator=g)
 
     def rope(self, T: int, device):
         key = (T, str(device))
@@ -158,5 +187,5 @@ class Llama(tnn.Module):
         return self.output(n)
 
 
-def llama(name: str = "llama3-8b", device=None, dtype=None, **overrides) -> Llama:
-    return Llama(config(name, **overrides), device=device, dtype=dtype)
+def llama(name: str = "llama3-8b", device=None, dtype=None, seed=None, **overrides) -> Llama:
+    return Llama(config(name, **overrides), device=device, dtype=dtype, seed=seed)

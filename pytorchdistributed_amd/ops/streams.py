@@ -57,11 +57,22 @@ def side_priority() -> str:
     return os.environ.get("PDA_WGRAD_PRIO", "normal")
 
 
+def side_cus() -> int:
+    """``PDA_WGRAD_CU_MASK=n``: the side stream's hardware queue dispatches to n CUs only (spread over the 8
+    XCDs), so weight-gradient tiles can never occupy more than n CUs beside the critical-path kernels of
+    the compute stream (0 = unmasked, the default)."""
+    return int(os.environ.get("PDA_WGRAD_CU_MASK", "0"))
+
+
 def side_stream(device: torch.device) -> torch.cuda.Stream:
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _streams.get(idx)
     if s is None:
-        if side_priority() == "low":
+        if side_cus() > 0:
+            from .._native import C
+
+            s = torch.cuda.ExternalStream(C().stream_create_cumask(idx, side_cus()), device=torch.device("cuda", idx))
+        elif side_priority() == "low":
             from .._native import C
 
             lo, _hi = C().stream_priority_range(idx)

@@ -4,11 +4,13 @@ forward at 139-145: replicate -> scatter -> parallel_apply -> gather).
 
 MI355X version:
 * the module is explicitly moved to ``device_ids[0]`` (the reference never moves it, SURVEY A12);
-* replication is a functional call with coalesced per-device parameter copies: the parameters of one
-  dtype are concatenated once on ``device_ids[0]`` and each other device receives ONE peer copy over
-  xGMI (buffers likewise, without autograd), which it views as its replica's tensors — not one copy per
-  tensor (torch's ``Broadcast`` / ``broadcast_coalesced`` idea); autograd's copy- and cat-backward
-  reduce-add every replica's gradient into the master parameters on ``device_ids[0]`` (the
+* the master's parameters (and buffers) live as views of ONE flat buffer per dtype on ``device_ids[0]``
+  (re-homed once at construction), and every other device keeps a persistent flat replica of it: a
+  forward refreshes each replica with ONE peer copy per dtype over xGMI (``copy_`` into the existing
+  buffer: no per-forward concatenation, no per-forward allocation) and the replica's module runs on
+  views of it through a functional call — torch's ``Broadcast`` / ``broadcast_coalesced`` idea without
+  the flatten.  Backward: each replica's flat gradient comes back to ``device_ids[0]`` as one copy and
+  autograd sums them with the master's own gradient before one split into per-parameter views (the
   reference's PS-style "reduce grads to master");
 * the per-device forwards run in one Python thread per device, each on its own device/stream;
 * outputs are gathered (concatenated) on ``output_device``.
@@ -57,6 +59,44 @@ def gather(outs, device: torch.device, dim: int = 0):
     return first
 
 
+class _FlatOf(torch.autograd.Function):
+    """The master's flat parameter buffer as one differentiable tensor of its parameters (which are views
+    of it): forward returns the buffer itself (no copy); backward splits the summed flat gradient into
+    per-parameter views."""
+
+    @staticmethod
+    def forward(ctx, flat, *params):
+        ctx.shapes = [(off, p.shape) for off, p in zip(_offsets(params), params)]
+        return flat.view(-1)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (None,) + tuple(g[off: off + sh.numel()].view(sh) for off, sh in ctx.shapes)
+
+
+def _offsets(ts):
+    out, o = [], 0
+    for t in ts:
+        out.append(o)
+        o += t.numel()
+    return out
+
+
+class _CopyInto(torch.autograd.Function):
+    """``buf.copy_(src)`` (one peer copy into a persistent replica buffer); backward: the gradient goes back
+    to ``src``'s device as one copy."""
+
+    @staticmethod
+    def forward(ctx, src, buf):
+        buf.copy_(src, non_blocking=True)
+        ctx.src_device = src.device
+        return buf.view_as(buf)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(ctx.src_device, non_blocking=True), None
+
+
 class DataParallel(tnn.Module):
     def __init__(self, module: tnn.Module, device_ids: Optional[Sequence] = None, output_device=None, dim: int = 0):
         super().__init__()
@@ -68,36 +108,92 @@ class DataParallel(tnn.Module):
         self.output_device = _as_devices([output_device])[0] if output_device is not None else self.devices[0]
         self.dim = dim
         self.module = module.to(self.devices[0])
+        self._groups: List[tuple] = []   # (flat, [(name, param)], is_param)
+        self._replicas: dict = {}        # (group index, device index) -> persistent replica buffer
+        self.replica_copies = 0          # peer copies issued by forwards (one per dtype group and device)
+        if len(self.devices) > 1:
+            self._flatten()
 
     # tests set this to copy even to the master's own device (the CPU tier has one device type)
     _force_copy = False
 
+    @torch.no_grad()
+    def _flatten(self):
+        """Re-home the master's parameters and buffers as views of one flat buffer per (dtype, kind)."""
+        self._groups, self._replicas = [], {}
+        groups = {}
+        for n, p in self.module.named_parameters():
+            groups.setdefault((p.dtype, True), []).append((n, p))
+        owners = {}
+        for mod_name, mod in self.module.named_modules():
+            for bn, b in mod._buffers.items():
+                if b is not None:
+                    owners.setdefault((b.dtype, False), []).append((f"{mod_name}.{bn}" if mod_name else bn, mod, bn, b))
+        for (dt, _), items in groups.items():
+            flat = torch.empty(sum(p.numel() for _, p in items), dtype=dt, device=self.devices[0])
+            o = 0
+            for _, p in items:
+                flat[o: o + p.numel()].copy_(p.detach().reshape(-1))
+                p.data = flat[o: o + p.numel()].view_as(p)
+                o += p.numel()
+            self._groups.append((flat, items, True))
+        for (dt, _), items in owners.items():
+            flat = torch.empty(sum(b.numel() for *_, b in items), dtype=dt, device=self.devices[0])
+            o = 0
+            named = []
+            for name, mod, bn, b in items:
+                view = flat[o: o + b.numel()].view_as(b)
+                view.copy_(b)
+                mod._buffers[bn] = view
+                named.append((name, view))
+                o += b.numel()
+            self._groups.append((flat, named, False))
+
+    def _stale(self) -> bool:
+        """A parameter / buffer replaced since the flattening (not a view of its group's buffer any more)."""
+        for flat, items, _ in self._groups:
+            lo = flat.data_ptr()
+            hi = lo + flat.numel() * flat.element_size()
+            for _, t in items:
+                if not (lo <= t.data_ptr() < hi):
+                    return True
+        named = dict(self.module.named_parameters())
+        return any(is_p and any(named.get(n) is not t for n, t in items) for _, items, is_p in self._groups)
+
     def _replica_states(self, devs: Sequence[torch.device]) -> List[dict]:
         """Parameter / buffer dicts for functional_call on every device: the master's tensors on
-        ``devs[0]``; elsewhere views of one coalesced copy per dtype (parameters through autograd, so
-        gradients flow back to the master; buffers without)."""
+        ``devs[0]``; elsewhere views of the device's persistent flat replica, refreshed by one copy per
+        group (parameters through autograd, so gradients flow back to the master; buffers without)."""
+        if not self._groups or self._stale():
+            self._flatten()
         states = [dict() for _ in devs]
-        named = [(n, p, True) for n, p in self.module.named_parameters()] + \
-                [(n, b, False) for n, b in self.module.named_buffers()]
-        for n, t, _ in named:
-            states[0][n] = t
+        for _, items, _ in self._groups:
+            for n, t in items:
+                states[0][n] = t
         targets = [i for i in range(1, len(devs)) if self._force_copy or devs[i] != devs[0]]
         for i in range(1, len(devs)):
             if i not in targets:
                 states[i] = dict(states[0])
         if not targets:
             return states
-        groups = {}
-        for n, t, is_param in named:
-            groups.setdefault((t.dtype, t.device, is_param), []).append((n, t))
-        for (_dt, _dev, is_param), items in groups.items():
-            with torch.set_grad_enabled(is_param and torch.is_grad_enabled()):
-                flat = torch.cat([t.reshape(-1) for _, t in items]) if len(items) > 1 else items[0][1].reshape(-1)
-                sizes = [t.numel() for _, t in items]
-                for i in targets:
-                    rep = flat.to(devs[i], non_blocking=True) if devs[i] != flat.device else flat.clone()
-                    for (n, t), piece in zip(items, rep.split(sizes)):
-                        states[i][n] = piece.view_as(t)
+        grad = torch.is_grad_enabled()
+        for gi, (flat, items, is_param) in enumerate(self._groups):
+            src = _FlatOf.apply(flat, *[t for _, t in items]) if (is_param and grad) else flat
+            sizes = [t.numel() for _, t in items]
+            for i in targets:
+                key = (gi, i)
+                buf = self._replicas.get(key)
+                if buf is None or buf.device != devs[i] or buf.numel() != flat.numel():
+                    buf = self._replicas[key] = torch.empty(flat.numel(), dtype=flat.dtype, device=devs[i])
+                if is_param and grad:
+                    rep = _CopyInto.apply(src, buf)
+                else:
+                    with torch.no_grad():
+                        buf.copy_(src, non_blocking=True)
+                    rep = buf
+                self.replica_copies += 1
+                for (n, t), piece in zip(items, rep.split(sizes)):
+                    states[i][n] = piece.view_as(t)
         return states
 
     def forward(self, *inputs, **kwargs):

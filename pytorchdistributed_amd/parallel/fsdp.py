@@ -84,7 +84,8 @@ class _Unit:
         self.entries = []  # (owner module, attr name, shape, offset, numel)
         off = 0
         first = getattr(params[0][0], params[0][1])
-        self.device = first.device
+        deferred = first.is_meta
+        self.device = fsdp.init_device if deferred else first.device
         for owner, name in params:
             p = getattr(owner, name)
             self.entries.append((owner, name, tuple(p.shape), off, p.numel()))
@@ -92,13 +93,25 @@ class _Unit:
         W = fsdp.world
         self.numel = _round(max(off, 1), W * ALIGN)
         self.shard_numel = self.numel // W
-        full = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
-        for (owner, name, shape, o, n) in self.entries:
-            full[o: o + n].copy_(getattr(owner, name).detach().reshape(-1).float())
         r = fsdp.rank
+        if deferred:
+            # deferred construction: materialise THIS unit only, as views of one compute-dtype buffer, let
+            # the model initialise it (identical on every rank: per-unit seeded streams), keep this rank's
+            # shard and drop the rest — a rank never holds more than one full unit plus its shards
+            full = torch.zeros(self.numel, dtype=fsdp.param_dtype, device=self.device)
+            for (owner, name, shape, o, n) in self.entries:
+                rg = owner._parameters[name].requires_grad
+                owner._parameters[name] = tnn.Parameter(full[o: o + n].view(shape), requires_grad=rg)
+            fsdp.param_init_fn(module, index)
+            fsdp._note_init(full.numel() * full.element_size())
+        else:
+            full = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+            for (owner, name, shape, o, n) in self.entries:
+                full[o: o + n].copy_(getattr(owner, name).detach().reshape(-1).float())
         self.shard = tnn.Parameter(full[r * self.shard_numel: (r + 1) * self.shard_numel].to(fsdp.shard_dtype,
                                                                                               copy=True))
         del full
+        fsdp._shard_bytes += self.shard.numel() * self.shard.element_size()
         for (owner, name, *_rest) in self.entries:
             del owner._parameters[name]
         # world 1 with a compute-dtype shard: the shard itself is the gathered buffer (no copy, never freed)
@@ -233,13 +246,30 @@ class _Unit:
 class FullyShardedDataParallel(tnn.Module):
     def __init__(self, module: tnn.Module, process_group=None, unit_types: Sequence[type] = (),
                  param_dtype: Optional[torch.dtype] = None, reshard_after_forward: bool = True,
-                 prefetch: bool = True, shard_dtype: Optional[torch.dtype] = None):
+                 prefetch: bool = True, shard_dtype: Optional[torch.dtype] = None, param_init_fn=None,
+                 device: Optional[torch.device] = None):
         """``param_dtype``: compute dtype of the gathered parameters (default: the module's).
         ``shard_dtype``: dtype of the sharded ``nn.Parameter`` the optimizer updates (default: the
         compute dtype — the fused optimizers then keep fp32 masters themselves and write the shard in
-        the same launch; ``torch.float32`` keeps fp32 shards and casts them once per step)."""
+        the same launch; ``torch.float32`` keeps fp32 shards and casts them once per step).
+
+        Deferred initialisation (a ``module`` built on the meta device): each unit is materialised on
+        ``device`` (default: the current GPU, else the CPU) one at a time, initialised by
+        ``param_init_fn(unit_module, unit_index)`` (default: ``module.init_unit``) — which must give every
+        rank the same values (e.g. a generator seeded per unit) — and reduced to this rank's shard before
+        the next unit exists: peak construction memory is the shards plus ONE full unit, not the model."""
         super().__init__()
         self.module = module
+        self.param_init_fn = param_init_fn if param_init_fn is not None else getattr(module, "init_unit", None)
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else \
+                torch.device("cpu")
+        self.init_device = torch.device(device)
+        self.deferred = any(p.is_meta for p in module.parameters())
+        if self.deferred and self.param_init_fn is None:
+            raise ValueError("a meta-device module needs param_init_fn (or an init_unit(module, index) method)")
+        self._shard_bytes = 0
+        self.init_peak_bytes = 0  # deferred construction: max bytes held at once (one unit + the shards so far)
         self.group = process_group
         self.world = pdist.get_world_size(process_group)
         self.rank = pdist.get_rank(process_group)
@@ -286,6 +316,11 @@ class FullyShardedDataParallel(tnn.Module):
             self.root_unit = _Unit(self, module, rest, len(self.units))
             self.units.append(self.root_unit)
         self.shards = tnn.ParameterList([u.shard for u in self.units])
+        if self.deferred:
+            for mod in module.modules():  # meta buffers (none in the shipped models): zero-filled on the device
+                for bn, b in list(mod._buffers.items()):
+                    if b is not None and b.is_meta:
+                        mod._buffers[bn] = torch.zeros(b.shape, dtype=b.dtype, device=self.init_device)
         # ---- hooks on unit modules
         self._fwd_order: List[_Unit] = []
         self._order_frozen = False
@@ -320,6 +355,9 @@ class FullyShardedDataParallel(tnn.Module):
                 cap = max(u.numel for u in self.units) * torch.tensor([], dtype=self.param_dtype).element_size()
                 self.xgmi = _xgmi.XgmiAllReduce(capacity_mb=cap / 2 ** 20 + 1, device=self.units[0].device)
                 self._ipc_stream = torch.cuda.Stream(self.units[0].device)
+
+    def _note_init(self, unit_bytes: int):
+        self.init_peak_bytes = max(self.init_peak_bytes, self._shard_bytes + unit_bytes)
 
     # ------------------------------------------------------------ communication accounting
     def _count(self, t: torch.Tensor):

@@ -57,3 +57,19 @@ def test_fsdp_sharded_checkpoint_resumes_exactly(tmp_path):
     names = list(snap["MODEL_STATE"])
     st = snap["OPTIMIZER_STATE"]["state"]
     assert st[0]["exp_avg"].shape == snap["MODEL_STATE"][names[0]].shape
+
+
+def test_fsdp_deferred_init_matches_eager(tmp_path):
+    """Meta-device construction: each rank materialises one unit at a time and keeps its
+    1/world shard; peak construction memory <= the rank's shards + one unit; losses and shards after two
+    AdamW steps are bit-identical to FSDP over the eagerly built model (world 4, gloo)."""
+    world = 4
+    spawn(_workers.fsdp_deferred_init_worker, args=(world, str(tmp_path)), nprocs=world, timeout=240)
+    for r in range(world):
+        out = torch.load(tmp_path / f"{r}.pt", weights_only=True)
+        e, d = out["eager"], out["deferred"]
+        assert torch.equal(e["losses"], d["losses"]), (e["losses"], d["losses"])
+        assert all(torch.equal(a, b) for a, b in zip(e["shards"], d["shards"]))
+        assert e["peak"] == 0 < d["peak"]
+        assert d["peak"] <= d["shard_bytes"] + d["unit_max"]
+        assert d["peak"] <= d["model_bytes"] / world + d["unit_max"]

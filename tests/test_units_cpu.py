@@ -414,3 +414,17 @@ def test_data_parallel_coalesced_replicas_match_single_device():
     ref_out.square().sum().backward()
     for (n, p), (_, q) in zip(net.named_parameters(), ref.named_parameters()):
         assert torch.allclose(p.grad, q.grad, atol=1e-5), n
+    # persistent replica: a second forward refreshes the same buffer (one copy per group, no new allocation)
+    copies = dp.replica_copies
+    st2 = dp._replica_states([torch.device("cpu"), torch.device("cpu")])
+    assert st2[1]["0.weight"].data_ptr() == w0.data_ptr()
+    assert dp.replica_copies - copies == len(dp._groups)
+    # the master's parameters are views of one flat buffer; an optimizer step through them shows in the replica
+    with torch.no_grad():
+        net[0].weight.add_(1.0)
+    st3 = dp._replica_states([torch.device("cpu"), torch.device("cpu")])
+    assert torch.equal(st3[1]["0.weight"], net[0].weight)
+    # a parameter replaced after wrapping is picked up (re-flattened), not silently dropped
+    net[3].weight = tnn.Parameter(torch.zeros(3, 8))
+    st4 = dp._replica_states([torch.device("cpu"), torch.device("cpu")])
+    assert torch.equal(st4[1]["3.weight"], torch.zeros(3, 8))
