@@ -1366,6 +1366,10 @@ Tensor rope(Tensor x, Tensor cs, Tensor sn, bool inverse, c10::optional<Tensor> 
 // ------------------------------------------------------------------ xGMI one-shot all-reduce
 class XgmiComm {
  public:
+  struct Reg {  // a zero-copy registration: every rank's tensor, mapped into this process
+    void* base[pda::kXgmiMaxRanks] = {};
+    int64_t bytes = 0;
+  };
   XgmiComm(int rank, int world, int64_t capacity_bytes, int device, double timeout_s)
       : rank_(rank), world_(world), cap_(capacity_bytes), dev_(device) {
     TORCH_CHECK(world >= 1 && world <= pda::kXgmiMaxRanks && rank >= 0 && rank < world, "xgmi: bad rank/world");
@@ -1385,6 +1389,7 @@ class XgmiComm {
   }
   ~XgmiComm() {
     c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, dev_));
+    for (auto& kv : mapped_) (void)pda::xgmi_close_handle(kv.second);
     for (int r = 0; r < world_; ++r)
       if (r != rank_) {
         if (peer_data_[r]) (void)pda::xgmi_close_handle(peer_data_[r]);
@@ -1429,6 +1434,24 @@ class XgmiComm {
     auto st = stream_of(t);
     CHECK_HIP_OK(hipMemcpyAsync(data_, t.data_ptr(), (size_t)bytes, hipMemcpyDeviceToDevice, st));
     launch(t.data_ptr(), n, average ? 1.f / (float)world_ : 1.f, algo, t.scalar_type() == at::kBFloat16, st);
+  }
+  void launch_on(const Reg& reg, int64_t byte_off, void* out, int64_t n, float scale, int algo, bool bf16,
+                 hipStream_t st) {
+    pda::XgmiArgs a{};
+    for (int r = 0; r < pda::kXgmiMaxRanks; ++r) {
+      a.data[r] = reg.base[r] ? (char*)reg.base[r] + byte_off : nullptr;
+      a.flags[r] = peer_flags_[r];
+    }
+    a.out = out;
+    a.n = n;
+    a.rank = rank_;
+    a.world = world_;
+    a.scale = scale;
+    a.epoch = ++epoch_;
+    a.timeout_ticks = timeout_ticks_;
+    a.err = err_;
+    a.algo = algo;
+    CHECK_HIP_OK(pda::xgmi_allreduce(a, bf16, st));
   }
   void launch(void* out, int64_t n, float scale, int algo, bool bf16, hipStream_t st) {
     pda::XgmiArgs a{};
@@ -1482,6 +1505,106 @@ class XgmiComm {
     launch(out.data_ptr(), n, average ? 1.f / (float)world_ : 1.f, pda::kXgmiReduceScatter,
            in.scalar_type() == at::kBFloat16, st);
   }
+  // ---- zero-copy (registered) buffers: the collective reads the peers' tensors in place
+  // instead of a copy into the exchange buffer.  reg_handle(t): this rank's IPC handle of t's allocation
+  // (hipMemGetAddressRange gives the base of the caching allocator's segment) + t's byte offset in it;
+  // reg_open(blobs): maps every peer's allocation once (mappings cached per handle, shared by later
+  // registrations in the same segment) and returns a registration id.  A registered tensor must stay
+  // allocated, unmoved, for as long as collectives use it (DDP's flat gradient buffers, FSDP shards).
+  py::bytes reg_handle(Tensor t) {
+    check_gpu(t, "t");
+    TORCH_CHECK(t.is_contiguous(), "xgmi: registered tensors are contiguous");
+    c10::DeviceGuard g(t.device());
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    CHECK_HIP_OK(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)t.data_ptr()));
+    std::string h(HIP_IPC_HANDLE_SIZE + 16, '\0');
+    CHECK_HIP_OK(pda::xgmi_get_handle(base, &h[0]));
+    const int64_t off = (int64_t)((char*)t.data_ptr() - (char*)base);
+    const int64_t bytes = t.numel() * t.element_size();
+    std::memcpy(&h[HIP_IPC_HANDLE_SIZE], &off, 8);
+    std::memcpy(&h[HIP_IPC_HANDLE_SIZE + 8], &bytes, 8);
+    return py::bytes(h);
+  }
+  int reg_open(Tensor own, const std::vector<std::string>& all) {
+    TORCH_CHECK((int)all.size() == world_, "xgmi: need one registration blob per rank");
+    c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, dev_));
+    Reg reg;
+    reg.bytes = own.numel() * own.element_size();
+    for (int r = 0; r < world_; ++r) {
+      TORCH_CHECK(all[r].size() == HIP_IPC_HANDLE_SIZE + 16, "xgmi: bad registration blob");
+      int64_t off = 0, bytes = 0;
+      std::memcpy(&off, all[r].data() + HIP_IPC_HANDLE_SIZE, 8);
+      std::memcpy(&bytes, all[r].data() + HIP_IPC_HANDLE_SIZE + 8, 8);
+      TORCH_CHECK(bytes == reg.bytes, "xgmi: registered tensors differ in size across ranks");
+      if (r == rank_) {
+        reg.base[r] = own.data_ptr();
+        continue;
+      }
+      const std::string key = std::to_string(r) + ":" + all[r].substr(0, HIP_IPC_HANDLE_SIZE);
+      auto it = mapped_.find(key);
+      void* b = nullptr;
+      if (it != mapped_.end()) {
+        b = it->second;
+      } else {
+        CHECK_HIP_OK(pda::xgmi_open_handle(all[r].data(), &b));
+        mapped_[key] = b;
+      }
+      reg.base[r] = (char*)b + off;
+    }
+    regs_.push_back(reg);
+    return (int)regs_.size() - 1;
+  }
+  // in-place all-reduce of t = registration `id`'s tensor [elem_off, elem_off + numel) (two-shot / ring:
+  // both are in-place safe; one-shot reads every peer's whole input while writing its own, so it runs as
+  // two-shot here)
+  void allreduce_reg(int id, Tensor t, int64_t elem_off, bool average, int algo) {
+    TORCH_CHECK(id >= 0 && id < (int)regs_.size(), "xgmi: unknown registration");
+    TORCH_CHECK(algo == pda::kXgmiOneShot || algo == pda::kXgmiTwoShot || algo == pda::kXgmiRing, "xgmi: bad algo");
+    check_gpu(t, "t");
+    TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, "xgmi: fp32 / bf16 only");
+    const Reg& reg = regs_[id];
+    const int64_t es = t.element_size(), n = t.numel();
+    TORCH_CHECK(n % 8 == 0 && elem_off >= 0 && (elem_off + n) * es <= reg.bytes, "xgmi: slice outside the registration");
+    TORCH_CHECK((char*)reg.base[rank_] + elem_off * es == (char*)t.data_ptr(), "xgmi: t is not that slice");
+    c10::DeviceGuard g(t.device());
+    launch_on(reg, elem_off * es, t.data_ptr(), n, average ? 1.f / (float)world_ : 1.f,
+              algo == pda::kXgmiRing ? pda::kXgmiRing : pda::kXgmiTwoShot, t.scalar_type() == at::kBFloat16,
+              stream_of(t));
+  }
+  // out[world * n] = every rank's registered shard (registration `id`), pulled in place
+  void allgather_reg(int id, Tensor in, Tensor out) {
+    TORCH_CHECK(id >= 0 && id < (int)regs_.size(), "xgmi: unknown registration");
+    check_gpu(in, "in");
+    check_gpu(out, "out");
+    const Reg& reg = regs_[id];
+    TORCH_CHECK(in.data_ptr() == reg.base[rank_] && in.numel() * in.element_size() == reg.bytes,
+                "xgmi: all-gather input must be the registered tensor");
+    TORCH_CHECK(in.scalar_type() == out.scalar_type() && out.is_contiguous() && out.numel() == in.numel() * world_ &&
+                    in.numel() % 8 == 0 && (in.scalar_type() == at::kFloat || in.scalar_type() == at::kBFloat16),
+                "xgmi all-gather: out = world x shard, same fp32 / bf16 dtype");
+    c10::DeviceGuard g(in.device());
+    launch_on(reg, 0, out.data_ptr(), in.numel(), 1.f, pda::kXgmiAllGather, in.scalar_type() == at::kBFloat16,
+              stream_of(in));
+  }
+  // out[n / world] = scale * sum over ranks of chunk `rank` of every rank's registered input (in place)
+  void reduce_scatter_reg(int id, Tensor in, Tensor out, bool average) {
+    TORCH_CHECK(id >= 0 && id < (int)regs_.size(), "xgmi: unknown registration");
+    check_gpu(in, "in");
+    check_gpu(out, "out");
+    const Reg& reg = regs_[id];
+    TORCH_CHECK(in.data_ptr() == reg.base[rank_] && in.numel() * in.element_size() == reg.bytes,
+                "xgmi: reduce-scatter input must be the registered tensor");
+    const int64_t n = in.numel();
+    TORCH_CHECK(in.scalar_type() == out.scalar_type() && out.is_contiguous() && n % (8 * world_) == 0 &&
+                    out.numel() * world_ == n && (in.scalar_type() == at::kFloat || in.scalar_type() == at::kBFloat16),
+                "xgmi reduce-scatter: numel % (8 world) == 0, out = shard, same fp32 / bf16 dtype");
+    c10::DeviceGuard g(in.device());
+    launch_on(reg, 0, out.data_ptr(), n, average ? 1.f / (float)world_ : 1.f, pda::kXgmiReduceScatter,
+              in.scalar_type() == at::kBFloat16, stream_of(in));
+  }
+  int num_registrations() const { return (int)regs_.size(); }
+
   // non-blocking: the kernels store the error word into pinned host memory; 0 = no timeout so far
   int error() const { return __atomic_load_n(err_host_, __ATOMIC_ACQUIRE); }
   void reset_error() { __atomic_store_n(err_host_, 0, __ATOMIC_RELEASE); }
@@ -1500,6 +1623,8 @@ class XgmiComm {
   uint32_t epoch_ = 0;
   long long timeout_ticks_ = 0;
   bool opened_ = false;
+  std::vector<Reg> regs_;
+  std::map<std::string, void*> mapped_;  // "rank:handle" -> mapped peer allocation base (opened once)
 };
 // HIP stream at an explicit queue priority (PyTorch's stream pools only reach normal and high; the
 // weight-gradient side stream wants LOW, so the dispatcher hands a freed CU to the critical-path
@@ -1793,6 +1918,14 @@ PYBIND11_MODULE(_C, m) {
       .def("allgather", &XgmiComm::allgather, py::arg("inp"), py::arg("out"))
       .def("reduce_scatter", &XgmiComm::reduce_scatter, py::arg("inp"), py::arg("out"), py::arg("average") = false)
       .def("error", &XgmiComm::error)
+      .def("reg_handle", &XgmiComm::reg_handle)
+      .def("reg_open", &XgmiComm::reg_open)
+      .def("allreduce_reg", &XgmiComm::allreduce_reg, py::arg("id"), py::arg("t"), py::arg("elem_off"),
+           py::arg("average") = false, py::arg("algo") = 1)
+      .def("allgather_reg", &XgmiComm::allgather_reg)
+      .def("reduce_scatter_reg", &XgmiComm::reduce_scatter_reg, py::arg("id"), py::arg("inp"), py::arg("out"),
+           py::arg("average") = false)
+      .def_property_readonly("num_registrations", &XgmiComm::num_registrations)
       .def("reset_error", &XgmiComm::reset_error)
       .def_property_readonly("capacity", &XgmiComm::capacity);
   pda_rt::bind_runtime(m);

@@ -141,6 +141,18 @@ class DistributedDataParallel(tnn.Module):
                 self.xgmi = _xgmi.XgmiAllReduce(capacity_mb=cap / 2 ** 20 + 1)
                 self._xgmi_algo = _xgmi.requested_algo()
                 self._ipc_stream = torch.cuda.Stream(self.xgmi.device)
+                self._register_xgmi()
+
+    def _register_xgmi(self):
+        """Zero-copy IPC buckets (parallel/xgmi.py, PDA_XGMI_ZERO_COPY): register every flat gradient buffer
+        once per layout, so a bucket all-reduce reads the peers' buckets in place (no copy-in)."""
+        from . import xgmi as _xgmi
+
+        self._xgmi_regs = {}
+        if self.xgmi is not None and _xgmi.zero_copy():
+            for dt, g in self.groups.items():
+                if g.dtype in (torch.float32, torch.bfloat16) and g.numel % 8 == 0:
+                    self._xgmi_regs[dt] = self.xgmi.register(g.grad_buffer)
 
     # ------------------------------------------------------------------ bucket layout
     def _layout(self, order: List[int]):
@@ -215,6 +227,7 @@ class DistributedDataParallel(tnn.Module):
             cap = max(b[2] for b in self.bucket_info())
             if cap > self.xgmi.capacity:
                 self.xgmi = _xgmi.XgmiAllReduce(capacity_mb=cap / 2 ** 20 + 1)
+            self._register_xgmi()  # the re-layout allocated new flat gradient buffers
 
     def _f32_view(self, b: int) -> torch.Tensor:
         dt, start, n = self.bucket_slices[b]
@@ -285,13 +298,26 @@ class DistributedDataParallel(tnn.Module):
         # the bucket's gradients may still be in flight on the side (weight-gradient) stream as well as
         # on the current stream (ops/streams.py): the collective is ordered after both
         producers = _streams.producer_streams(t.device) if t.is_cuda else []
-        if self.xgmi is not None and self.xgmi.fits(t, self._xgmi_algo):
-            # one-shot IPC all-reduce on a side stream, ordered after the kernels that produced the bucket
+        reg = None
+        if self.xgmi is not None and t.numel() % 8 == 0:
+            from .xgmi import RCCL
+
+            reg = getattr(self, "_xgmi_regs", {}).get(self.bucket_slices[b][0])
+            if reg is not None and self.xgmi.pick(nbytes, self._xgmi_algo) == RCCL:
+                reg = None  # the node's tuning table routes this size to RCCL
+        if self.xgmi is not None and (reg is not None or self.xgmi.fits(t, self._xgmi_algo)):
+            # IPC all-reduce on a side stream, ordered after the kernels that produced the bucket; zero-copy
+            # (registered flat gradient buffer): the peers' buckets are read in place
             ticket = _watchdog.arm(f"ddp xgmi all_reduce bucket {b} ({nbytes / 2**20:.1f} MB, {t.dtype})")
             with torch.cuda.stream(self._ipc_stream), _timing.range(f"ddp.xgmi_all_reduce.b{b}"):
                 for s in producers:
                     self._ipc_stream.wait_stream(s)
-                self.xgmi(t, average=True, algo=self._xgmi_algo)
+                if reg is not None:
+                    self.xgmi.all_reduce_registered(reg, t, self.bucket_slices[b][1], average=True,
+                                                    algo=self._xgmi_algo)
+                    self._stats["zero_copy_calls"] = self._stats.get("zero_copy_calls", 0) + 1
+                else:
+                    self.xgmi(t, average=True, algo=self._xgmi_algo)
                 done = torch.cuda.Event()
                 done.record(self._ipc_stream)
             work = _EventWork(done)

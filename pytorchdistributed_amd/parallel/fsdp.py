@@ -147,6 +147,7 @@ class _Unit:
         if not self.alias:
             self.flat.untyped_storage().resize_(0)
         self.pending_ag = None
+        self.ag_reg = self.rs_reg = None  # zero-copy IPC registrations (PDA_FSDP_COMM=ipc)
         # compute-dtype copy of an fp32 shard, made by the forward gather and reused by the backward
         # re-gather of the same step.  Invalidated at every forward entry: fused optimizers update the
         # shard through raw pointers, which does not bump its autograd version counter.
@@ -214,8 +215,12 @@ class _Unit:
                 self.gathered = True
             elif self.fsdp.xgmi is not None:
                 flat = self.flat
-                self.pending_ag = self.fsdp._ipc(lambda: self.fsdp.xgmi.all_gather_into_tensor(flat, send),
-                                                 [torch.cuda.current_stream(self.device)], [send, flat],
+                reg = self.ag_reg
+                if reg is not None:  # zero-copy: the peers' shards are read in place
+                    fn = lambda: self.fsdp.xgmi.all_gather_registered(reg, flat, send)  # noqa: E731
+                else:
+                    fn = lambda: self.fsdp.xgmi.all_gather_into_tensor(flat, send)  # noqa: E731
+                self.pending_ag = self.fsdp._ipc(fn, [torch.cuda.current_stream(self.device)], [send, flat],
                                                  ("ag", self.index))
                 self.fsdp._track("xgmi all_gather", self, self.fsdp._ipc_stream)
             elif self.fsdp.ncomm is not None:
@@ -355,6 +360,15 @@ class FullyShardedDataParallel(tnn.Module):
                 cap = max(u.numel for u in self.units) * torch.tensor([], dtype=self.param_dtype).element_size()
                 self.xgmi = _xgmi.XgmiAllReduce(capacity_mb=cap / 2 ** 20 + 1, device=self.units[0].device)
                 self._ipc_stream = torch.cuda.Stream(self.units[0].device)
+                if _xgmi.zero_copy():
+                    # zero-copy: the shards (all-gather sources) and persistent unit gradient buffers
+                    # (reduce-scatter sources) are registered once; peers read them in place
+                    for u in self.units:
+                        u.transient_grad = False
+                        u.alloc_grad()
+                        u.ag_reg = (self.xgmi.register(u.shard.detach())
+                                    if u.shard.dtype == self.param_dtype and u.shard_numel % 8 == 0 else None)
+                        u.rs_reg = self.xgmi.register(u.grad_buffer) if u.numel % (8 * self.world) == 0 else None
 
     def _note_init(self, unit_bytes: int):
         self.init_peak_bytes = max(self.init_peak_bytes, self._shard_bytes + unit_bytes)
@@ -519,8 +533,11 @@ class FullyShardedDataParallel(tnn.Module):
         # collective is ordered after both streams
         producers = _streams.producer_streams(grad_full.device) if grad_full.is_cuda else []
         if self.xgmi is not None:
-            work = self._ipc(lambda: self.xgmi.reduce_scatter_tensor(out, grad_full, average=True), producers,
-                             [out, grad_full], ("rs", u.index))
+            if u.rs_reg is not None:  # zero-copy: every peer's gradient buffer read in place
+                fn = lambda: self.xgmi.reduce_scatter_registered(u.rs_reg, out, grad_full, average=True)  # noqa: E731
+            else:
+                fn = lambda: self.xgmi.reduce_scatter_tensor(out, grad_full, average=True)  # noqa: E731
+            work = self._ipc(fn, producers, [out, grad_full], ("rs", u.index))
             self._track("xgmi reduce_scatter", u, self._ipc_stream)
         elif self.ncomm is not None:
             work = self.ncomm.reduce_scatter(out, grad_full, "avg", streams=producers)

@@ -21,6 +21,13 @@ Plus the FSDP collectives (X18): :meth:`XgmiAllReduce.all_gather_into_tensor` (e
 each peer's shard over its own link) and :meth:`XgmiAllReduce.reduce_scatter_tensor` (rank r
 reduces chunk r of every peer's buffer); ``PDA_FSDP_COMM=ipc`` routes FSDP units through them.
 
+Zero-copy (``PDA_XGMI_ZERO_COPY``, default on): a tensor that lives as long as the collectives on it —
+DDP's flat gradient buffers, FSDP's shards and unit gradient buffers — is *registered* once per layout
+(:meth:`XgmiAllReduce.register`: the IPC handle of its allocation plus its offset, swapped through the
+store), and the kernels then read the peers' tensors in place: no copy into the exchange buffer, no
+capacity limit.  In-place all-reduce runs two-shot or ring (one-shot would overwrite its input while peers
+still read it).
+
 Opt-in for DDP buckets (``PDA_ALLREDUCE=ipc|oneshot|twoshot|ring``); RCCL stays the default transport.
 Single node only (peers must be IPC-reachable GPUs).
 
@@ -104,6 +111,7 @@ class XgmiAllReduce:
         store = store if store is not None else dist.distributed_c10d._get_default_store()
         tag = f"pda_xgmi/{_COUNTER[0]}"
         _COUNTER[0] += 1
+        self._store, self._tag, self._nreg = store, tag, 0
         # rank 0's tuning table is THE table: every rank must pick the same algorithm per size
         if self.rank == 0:
             table = load_table(self.world)
@@ -156,6 +164,35 @@ class XgmiAllReduce:
         self.comm.reduce_scatter(inp, out, average)
         return out
 
+    # ------------------------------------------------------------ zero-copy registrations
+    def register(self, t: torch.Tensor) -> int:
+        """Collective (every rank, same order, same size): register ``t`` for zero-copy collectives and
+        return the registration id.  ``t`` must stay allocated and unmoved while collectives use it."""
+        key = f"{self._tag}/reg{self._nreg}"
+        self._nreg += 1
+        self._store.set(f"{key}/{self.rank}", self.comm.reg_handle(t))
+        blobs = [bytes(self._store.get(f"{key}/{r}")) for r in range(self.world)]
+        return self.comm.reg_open(t, blobs)
+
+    def all_reduce_registered(self, reg: int, t: torch.Tensor, elem_offset: int, average: bool = False,
+                              algo: str = "auto") -> torch.Tensor:
+        """In-place all-reduce of ``t`` = elements ``[elem_offset, elem_offset + numel)`` of registration
+        ``reg``, reading every peer's slice in place (no copy-in).  ``ring`` runs the ring; everything
+        else two-shot."""
+        self.comm.allreduce_reg(reg, t, elem_offset, average, 2 if algo == "ring" else 1)
+        return t
+
+    def all_gather_registered(self, reg: int, out: torch.Tensor, inp: torch.Tensor) -> torch.Tensor:
+        """``out`` (world x shard) = every rank's registered ``inp`` (shard), pulled in place."""
+        self.comm.allgather_reg(reg, inp, out)
+        return out
+
+    def reduce_scatter_registered(self, reg: int, out: torch.Tensor, inp: torch.Tensor,
+                                  average: bool = False) -> torch.Tensor:
+        """``out`` (shard) = sum (mean) over ranks of chunk ``rank`` of every rank's registered ``inp``."""
+        self.comm.reduce_scatter_reg(reg, inp, out, average)
+        return out
+
     def poll(self) -> int:
         """Non-blocking: 0, or 1 + the phase of a peer barrier that timed out in a call that already
         ran.  The kernels write the error word into pinned host memory, so no device sync is needed;
@@ -186,6 +223,11 @@ def requested_algo():
     if v in ("ipc", "xgmi"):
         return "auto"
     return v if v in _ALGOS else None  # oneshot / twoshot / ring
+
+
+def zero_copy() -> bool:
+    """``PDA_XGMI_ZERO_COPY`` (default on): registered tensors, no copy into the exchange buffer."""
+    return os.environ.get("PDA_XGMI_ZERO_COPY", "1") != "0"
 
 
 def single_node() -> bool:

@@ -387,7 +387,7 @@ def xgmi_timeout_worker(rank, world, outdir):
     pd.destroy_process_group()
 
 
-def ddp_xgmi_gpu_worker(rank, world, outdir):
+def ddp_xgmi_gpu_worker(rank, world, outdir, zero_copy=True):
     """DDP with PDA_ALLREDUCE=ipc (bucket all-reduces on the xGMI IPC kernels), `world` ranks sharing
     cuda:0 (gloo only exchanges the IPC handles): bucket gradients == mean of the per-rank gradients,
     over several steps with the per-step error poll and watchdog tickets active."""
@@ -397,6 +397,7 @@ def ddp_xgmi_gpu_worker(rank, world, outdir):
     import torch.distributed as dist
 
     os.environ["PDA_ALLREDUCE"] = "ipc"
+    os.environ["PDA_XGMI_ZERO_COPY"] = "1" if zero_copy else "0"
     torch.cuda.set_device(0)
     pd.init_process_group("gloo")
     torch.manual_seed(0)
@@ -424,6 +425,8 @@ def ddp_xgmi_gpu_worker(rank, world, outdir):
     model.xgmi.check(sync=True)
     assert model.reducer.num_buckets > 1
     assert worst < 1e-4, worst
+    zc = model.comm_stats().get("zero_copy_calls", 0)
+    assert (zc > 0) == zero_copy, zc  # zero-copy: every bucket read in place from the registered flat buffer
     with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
         f.write("ok")
     pd.destroy_process_group()
@@ -1360,4 +1363,59 @@ def fsdp_deferred_init_worker(rank, world, outdir):
                      "unit_max": max(u.numel for u in fsdp.units) * 4,
                      "shard_bytes": sum(u.shard_numel for u in fsdp.units) * 4}
     torch.save(out, os.path.join(outdir, f"{rank}.pt"))
+    pd.destroy_process_group()
+
+
+def xgmi_zero_copy_worker(rank, world, outdir):
+    """Zero-copy IPC collectives: tensors registered once, then all-reduced / all-gathered /
+    reduce-scattered by kernels that read the peers' tensors in place (no copy into the exchange buffer —
+    the exchange buffer is deliberately too small for these sizes), against fp32 sums over several epochs,
+    fp32 and bf16, two-shot and ring, slices at offsets of a registered flat buffer."""
+    import pytorchdistributed_amd.distributed as pd
+    from pytorchdistributed_amd.parallel.xgmi import XgmiAllReduce
+
+    torch.cuda.set_device(0)
+    pd.init_process_group("gloo")
+    comm = XgmiAllReduce(capacity_mb=0.01, device=torch.device("cuda", 0), timeout_s=20.0)
+    for dt in (torch.float32, torch.bfloat16):
+        flat = torch.zeros(3 << 20, dtype=dt, device="cuda")  # a DDP-style flat gradient buffer
+        reg = comm.register(flat)
+        for it, (off, n) in enumerate([(0, 8), (8, 1000), (1016, 4096 * 129), (1 << 20, 1 << 20), (0, 3 << 20)]):
+            g = torch.Generator().manual_seed(10 * it + (dt == torch.bfloat16))
+            base = [torch.randn(n, generator=g) for _ in range(world)]
+            t = flat[off: off + n]
+            t.copy_(base[rank].to(dt))
+            algo = "ring" if it % 2 else "twoshot"
+            comm.all_reduce_registered(reg, t, off, average=(it % 2 == 1), algo=algo)
+            torch.cuda.synchronize()
+            comm.check()
+            ref = sum(b.to(dt).float() for b in base)
+            if it % 2 == 1:
+                ref = ref / world
+            err = ((t.float().cpu() - ref).norm() / ref.norm()).item()
+            assert err < (1e-6 if dt == torch.float32 else 1e-2), (dt, it, err)
+        # FSDP-style: a registered shard all-gathered, a registered full buffer reduce-scattered
+        shard_n = 4096 * 8
+        shard = torch.zeros(shard_n, dtype=dt, device="cuda")
+        full_g = torch.zeros(shard_n * world, dtype=dt, device="cuda")
+        rs = comm.register(full_g)
+        ag = comm.register(shard)
+        for it in range(3):
+            g = torch.Generator().manual_seed(1000 + it)
+            shards = [torch.randn(shard_n, generator=g) for _ in range(world)]
+            fulls = [torch.randn(shard_n * world, generator=g) for _ in range(world)]
+            shard.copy_(shards[rank].to(dt))
+            full_g.copy_(fulls[rank].to(dt))
+            out = torch.empty(shard_n * world, dtype=dt, device="cuda")
+            comm.all_gather_registered(ag, out, shard)
+            red = torch.empty(shard_n, dtype=dt, device="cuda")
+            comm.reduce_scatter_registered(rs, red, full_g, average=True)
+            torch.cuda.synchronize()
+            comm.check()
+            assert torch.equal(out.cpu(), torch.cat([s.to(dt) for s in shards]))
+            ref = sum(f.to(dt).float() for f in fulls)[rank * shard_n: (rank + 1) * shard_n] / world
+            err = ((red.float().cpu() - ref).norm() / ref.norm()).item()
+            assert err < (1e-6 if dt == torch.float32 else 1e-2), (dt, "rs", it, err)
+    with open(os.path.join(outdir, f"ok{rank}"), "w") as f:
+        f.write("ok")
     pd.destroy_process_group()

@@ -57,8 +57,18 @@ def test_xgmi_barrier_timeout_is_reported(tmp_path):
     assert (tmp_path / "ok0").read_text() == "raised"
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_ddp_buckets_over_xgmi_ipc(tmp_path, world):
-    spawn(_workers.ddp_xgmi_gpu_worker, args=(world, str(tmp_path)), nprocs=world, timeout=300)
+@pytest.mark.parametrize("world,zero_copy", [(2, True), (3, True), (2, False)])
+def test_ddp_buckets_over_xgmi_ipc(tmp_path, world, zero_copy):
+    spawn(_workers.ddp_xgmi_gpu_worker, args=(world, str(tmp_path), zero_copy), nprocs=world, timeout=300)
+    for r in range(world):
+        assert (tmp_path / f"ok{r}").read_text() == "ok"
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_zero_copy_registered(tmp_path, world):
+    """Zero-copy mode: registered tensors read in place by peers (no copy-in; exchange buffer smaller than
+    every message), all-reduce (two-shot / ring) on slices of a registered flat buffer, all-gather of a
+    registered shard, reduce-scatter of a registered full buffer, vs fp32 sums."""
+    spawn(_workers.xgmi_zero_copy_worker, args=(world, str(tmp_path)), nprocs=world, timeout=300)
     for r in range(world):
         assert (tmp_path / f"ok{r}").read_text() == "ok"
