@@ -77,6 +77,13 @@ def _join_side_streams(units) -> None:
         _streams.join(d)
 
 
+class _Slot:
+    """One slot of the FSDP gradient ring: the buffer and the reduce-scatter that last read it."""
+
+    def __init__(self, buf: torch.Tensor):
+        self.buf, self.work = buf, None
+
+
 class _Unit:
     def __init__(self, fsdp: "FullyShardedDataParallel", module: tnn.Module, params: List[Tuple[tnn.Module, str]],
                  index: int):
@@ -148,6 +155,8 @@ class _Unit:
             self.flat.untyped_storage().resize_(0)
         self.pending_ag = None
         self.ag_reg = self.rs_reg = None  # zero-copy IPC registrations (PDA_FSDP_COMM=ipc)
+        self.ring = False  # gathered buffer is a slot of the FSDP ring (FullyShardedDataParallel._enable_ring)
+        self.grad_slot = None  # gradient-ring slot (native RCCL path)
         # compute-dtype copy of an fp32 shard, made by the forward gather and reused by the backward
         # re-gather of the same step.  Invalidated at every forward entry: fused optimizers update the
         # shard through raw pointers, which does not bump its autograd version counter.
@@ -183,7 +192,17 @@ class _Unit:
             self.fsdp._grad_ready(self)
 
     def alloc_grad(self):
-        """(Re)allocate a released gradient buffer (zero padding) before the unit's backward writes it."""
+        """(Re)allocate a released gradient buffer (zero padding) before the unit's backward writes it.
+        Ring mode: the unit's slot of the gradient ring; the compute stream first waits for the
+        reduce-scatter of the slot's previous user (long done with 3 slots)."""
+        if self.grad_slot is not None:
+            slot = self.grad_slot
+            if slot.work is not None:
+                slot.work.wait()
+                slot.work = None
+            if self.pad_index.numel():
+                self.grad_buffer.index_fill_(0, self.pad_index, 0)
+            return
         st = self.grad_buffer.untyped_storage()
         if st.size() == 0:
             st.resize_(self.numel * self.grad_buffer.element_size())
@@ -191,6 +210,8 @@ class _Unit:
                 self.grad_buffer.index_fill_(0, self.pad_index, 0)
 
     def release_grad(self):
+        if self.grad_slot is not None:
+            return  # the ring slot stays; its next user waits for this unit's reduce-scatter
         if self.transient_grad:
             self.grad_buffer.untyped_storage().resize_(0)
 
@@ -243,6 +264,9 @@ class _Unit:
     def reshard(self):
         if self.alias:
             return
+        if self.ring:  # the slot belongs to the ring: nothing is freed, the next gather overwrites it
+            self.gathered = False
+            return
         if self.gathered:
             self.flat.untyped_storage().resize_(0)
         self.gathered = False
@@ -274,6 +298,7 @@ class FullyShardedDataParallel(tnn.Module):
         if self.deferred and self.param_init_fn is None:
             raise ValueError("a meta-device module needs param_init_fn (or an init_unit(module, index) method)")
         self._shard_bytes = 0
+        self.ring_enabled = False
         self.init_peak_bytes = 0  # deferred construction: max bytes held at once (one unit + the shards so far)
         self.group = process_group
         self.world = pdist.get_world_size(process_group)
@@ -560,6 +585,8 @@ class FullyShardedDataParallel(tnn.Module):
                     work = dist.reduce_scatter_tensor(out, grad_full, group=self.group, async_op=True)
         self._count(grad_full)
         self._pending_rs.append((u, work, out))
+        if u.grad_slot is not None:
+            u.grad_slot.work = work  # the slot's next user waits for this reduce-scatter
         if self.xgmi is not None or self.ncomm is not None:
             u.release_grad()  # record_stream on the collective's stream holds the storage until it is read
         else:
@@ -607,7 +634,50 @@ class FullyShardedDataParallel(tnn.Module):
             u.arrived = 0
             for leaf in u.leaves:
                 leaf._pda_seen = False
-        self._order_frozen = True
+        if not self._order_frozen:
+            self._order_frozen = True
+            self._enable_ring()
+
+    def _enable_ring(self):
+        """Preallocated rings for the transient unit buffers, once the first iteration has
+        recorded the forward order: the gathered parameters of the unit at forward position p live in
+        slot p % 2 of a 2-slot ring (the unit computing + the one prefetched), and its flat gradient in
+        slot p % 3 of a 3-slot ring (native RCCL path) — instead of a caching-allocator block per gather /
+        backward, which, with record_stream holding every block until the collective has run, fragmented
+        the pool (286 GiB reserved for a 190 GiB peak, one allocator retry in the timed steps at world 1).
+
+        Why fixed slots are safe: a unit's leaves (and every tensor autograd saved from them) view its
+        slot, and are only read while that unit computes — forward, or its backward after the re-gather
+        into the same slot.  Between two uses the slot carries other units, but a gather into slot s is
+        enqueued on the comm stream after every kernel already queued on the compute stream, i.e. after
+        the previous user of s (position p - 2) has finished; the prefetched unit (p +- 1) is always in the
+        other slot.  ``PDA_FSDP_RING=0`` keeps the allocator path."""
+        if os.environ.get("PDA_FSDP_RING", "1") == "0" or not self.comm_on or not self.reshard_after_forward \
+                or self.xgmi is not None:
+            return
+        order = [u for u in self._fwd_order if u is not self.root_unit]
+        units = [u for u in self.units if u is not self.root_unit]
+        if len(order) < 3 or len(order) != len(units) or len({id(u) for u in order}) != len(order) or \
+                any(u.alias for u in order):
+            return
+        dev = order[0].device
+        n = max(u.numel for u in order)
+        self._flat_slots = [torch.empty(n, dtype=self.param_dtype, device=dev) for _ in range(2)]
+        grad_ring = self.ncomm is not None
+        if grad_ring:
+            self._grad_slots = [_Slot(torch.zeros(n, dtype=self.param_dtype, device=dev)) for _ in range(3)]
+        for pos, u in enumerate(order):
+            u.flat = self._flat_slots[pos % 2][: u.numel]
+            for leaf, (_o, _n, shape, o, k) in zip(u.leaves, u.entries):
+                leaf.data = u.flat[o: o + k].view(shape)
+            u.ring = True
+            u.gathered = False
+            if grad_ring:
+                u.grad_buffer.untyped_storage().resize_(0)
+                slot = self._grad_slots[pos % 3]
+                u.grad_buffer = slot.buf[: u.numel]
+                u.grad_slot = slot
+        self.ring_enabled = True
 
     # ------------------------------------------------------------ module API
     def forward(self, *args, **kwargs):

@@ -592,7 +592,8 @@ def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl", force=False):
         os.environ["PDA_TRACK_COMM"] = "1"
         pd.init_process_group("nccl", device_id=0)
     torch.manual_seed(0)
-    cfg = config("llama3-tiny", dim=256, n_heads=2, n_kv_heads=1, ffn_dim=512)
+    # 4 blocks: enough units for the gathered / gradient rings (FSDP._enable_ring, from step 2)
+    cfg = config("llama3-tiny", dim=256, n_heads=2, n_kv_heads=1, ffn_dim=512, n_layers=4)
     ref = Llama(cfg, device="cuda", dtype=torch.bfloat16)
     model = Llama(cfg, device="cuda", dtype=torch.bfloat16)
     model.load_state_dict(ref.state_dict())
@@ -609,7 +610,7 @@ def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl", force=False):
     ropt = AdamW(ref.parameters(), lr=1e-3, weight_decay=0.1)
     g = torch.Generator().manual_seed(5)
     dbg = os.environ.get("PDA_TEST_DEBUG") == "1"
-    for step in range(2):
+    for step in range(3):
         idx = torch.randint(0, cfg.vocab_size, (world * 2, 64), generator=g).cuda()
         tgt = torch.randint(0, cfg.vocab_size, (world * 2, 64), generator=g).cuda()
         opt.zero_grad(set_to_none=True)
@@ -640,7 +641,9 @@ def fsdp_llama_gpu_worker(rank, world, outdir, comm="rccl", force=False):
               f"{fsdp.xgmi.poll() if fsdp.xgmi is not None else None}", flush=True)
     assert worst[0] < 2e-2, worst
     extra = ""
+    assert fsdp.ring_enabled == (fsdp.comm_on and fsdp.xgmi is None)
     if force:
+        assert fsdp.units[0].grad_slot is not None  # the native path also rings the gradient buffers
         st = fsdp.comm_stats()
         assert st["comm_calls"] > 0 and "exposed_comm_ms" in st, st
         # every native all-gather / reduce-scatter carried a watchdog ticket that retired by itself
@@ -1341,7 +1344,8 @@ def fsdp_deferred_init_worker(rank, world, outdir):
     pd.init_process_group("gloo")
     cfg = config("llama3-tiny", dim=64, n_heads=2, n_kv_heads=1, ffn_dim=128, n_layers=4, vocab_size=512)
     out = {}
-    for mode in ("eager", "deferred"):
+    for mode in ("eager", "deferred", "noring"):
+        os.environ["PDA_FSDP_RING"] = "0" if mode == "noring" else "1"
         model = Llama(cfg, device="meta" if mode == "deferred" else "cpu", seed=1234)
         if mode == "deferred":
             assert all(p.is_meta for p in model.parameters())
@@ -1349,7 +1353,7 @@ def fsdp_deferred_init_worker(rank, world, outdir):
         opt = torch.optim.AdamW(fsdp.parameters(), lr=1e-3)
         g = torch.Generator().manual_seed(7 + rank)
         losses = []
-        for _ in range(2):
+        for _ in range(3):  # (the gathered-buffer ring takes over from step 2)
             idx = torch.randint(0, cfg.vocab_size, (2, 32), generator=g)
             tgt = torch.randint(0, cfg.vocab_size, (2, 32), generator=g)
             opt.zero_grad()
@@ -1357,6 +1361,7 @@ def fsdp_deferred_init_worker(rank, world, outdir):
             loss.backward()
             opt.step()
             losses.append(loss.detach().clone())
+        assert fsdp.ring_enabled == (mode != "noring")
         out[mode] = {"losses": torch.stack(losses), "shards": [s.detach().clone() for s in fsdp.shards],
                      "peak": fsdp.init_peak_bytes,
                      "model_bytes": sum(u.numel for u in fsdp.units) * 4,  # fp32 model

@@ -61,8 +61,9 @@ def test_fsdp_sharded_checkpoint_resumes_exactly(tmp_path):
 
 def test_fsdp_deferred_init_matches_eager(tmp_path):
     """Meta-device construction: each rank materialises one unit at a time and keeps its
-    1/world shard; peak construction memory <= the rank's shards + one unit; losses and shards after two
-    AdamW steps are bit-identical to FSDP over the eagerly built model (world 4, gloo)."""
+    1/world shard; peak construction memory <= the rank's shards + one unit; losses and shards after three
+    AdamW steps are bit-identical to FSDP over the eagerly built model (world 4, gloo), and to the run
+    without the gathered-buffer ring (PDA_FSDP_RING=0)."""
     world = 4
     spawn(_workers.fsdp_deferred_init_worker, args=(world, str(tmp_path)), nprocs=world, timeout=240)
     for r in range(world):
@@ -70,6 +71,9 @@ def test_fsdp_deferred_init_matches_eager(tmp_path):
         e, d = out["eager"], out["deferred"]
         assert torch.equal(e["losses"], d["losses"]), (e["losses"], d["losses"])
         assert all(torch.equal(a, b) for a, b in zip(e["shards"], d["shards"]))
+        # the preallocated gathered-buffer ring (on from step 2) changes no bit against the allocator path
+        nr = out["noring"]
+        assert torch.equal(e["losses"], nr["losses"]) and all(torch.equal(a, b) for a, b in zip(e["shards"], nr["shards"]))
         assert e["peak"] == 0 < d["peak"]
         assert d["peak"] <= d["shard_bytes"] + d["unit_max"]
         assert d["peak"] <= d["model_bytes"] / world + d["unit_max"]
