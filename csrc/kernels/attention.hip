@@ -839,11 +839,208 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd3_kernel(AttnParams p) {
   }
 }
 
+// ---------------------------------------------------------------- v4 forward: fewer VALU per MFMA
+// The v3 loop issued ~5.5 VALU per MFMA (profiles/r5_attention_pmc.md: 16 % MFMA busy at D = 128) and
+// about a third of them were bookkeeping: 64-bit address arithmetic and per-row bounds compares /
+// selects of the register-staged K/V loads, 32 packed multiplies rescaling O every tile, and 32 adds of
+// the row sums.  v4 keeps v3's structure (double-buffered K/V images, one barrier per key tile) and:
+//   * loads the K/V tile through buffer descriptors rebased per tile in scalar registers: each lane's
+//     byte offsets are loop-invariant (one VALU add per load), rows past T fall outside the descriptor
+//     range and read as zero — no compare / select;
+//   * defers the O rescale (the "RESCALE_THRESHOLD" idea): the running max used for the exponent moves
+//     only when a row's max grows by more than 8 in the log2 domain (then P <= 2^8, exact in fp32 / bf16
+//     range) — a wave-uniform branch that almost every tile after the first few skips;
+//   * sums the rows on the matrix pipe: one extra MFMA per P fragment against an all-ones V^T fragment
+//     accumulates l (the lane's query row sum) — 4 MFMAs per tile instead of 32 adds + 4 lane swaps.
+template <int D>
+struct TileOff {  // a thread's byte offsets of its chunks inside a 64-row tile of A and B
+  static constexpr int CPR = D / 8, NCH = 64 * CPR / NT;
+  uint32_t a0, b0, da, db;  // chunk i: a0 + i * da
+};
+
+template <int D>
+__device__ __forceinline__ TileOff<D> tile_offsets(int64_t ars, int64_t brs) {
+  constexpr int CPR = TileOff<D>::CPR;
+  const int r = threadIdx.x / CPR, ch = threadIdx.x % CPR;  // chunk i: row r + (NT / CPR) i, same ch
+  TileOff<D> t;
+  t.a0 = (uint32_t)((r * ars + ch * 8) * 2);
+  t.b0 = (uint32_t)((r * brs + ch * 8) * 2);
+  t.da = (uint32_t)((NT / CPR) * ars * 2);
+  t.db = (uint32_t)((NT / CPR) * brs * 2);
+  return t;
+}
+
+template <int D>
+__device__ __forceinline__ void fetch_tile_buf(TileRegs<D>& tr, const TileOff<D>& to, const bf16_t* __restrict__ A,
+                                               int64_t ars, const bf16_t* __restrict__ B, int64_t brs, int row0,
+                                               int T) {
+  const int rows = T - row0;  // >= 1: rows past T are outside the descriptor range (read as zero)
+  const int na = (int)((rows - 1) * ars * 2 + 2 * D), nb = (int)((rows - 1) * brs * 2 + 2 * D);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (int64_t)row0 * ars), (short)0,
+                                                                      na, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (int64_t)row0 * brs), (short)0,
+                                                                      nb, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < TileRegs<D>::NCH; ++i) {
+    tr.a[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, to.a0 + i * to.da, 0, 0));
+    tr.b[i] = __builtin_bit_cast(u16x8, __builtin_amdgcn_raw_buffer_load_b128(rb, to.b0 + i * to.db, 0, 0));
+  }
+}
+
+// the buffer-descriptor fetch needs every [T][row stride] span to fit a 31-bit byte offset (true for
+// every training shape here: Llama-3-8B T = 4096 spans 48 MB); otherwise the pointer fetch
+__device__ __forceinline__ bool attn_buf_ok(const AttnParams& p) {
+  const int64_t lim = (int64_t)1 << 31, T = p.T;
+  return T * p.k_st * 2 < lim && T * p.v_st * 2 < lim && T * p.q_st * 2 < lim &&
+         (p.dout == nullptr || T * p.do_st * 2 < lim);
+}
+
+template <int D>
+__device__ __forceinline__ void fetch_any(TileRegs<D>& tr, const TileOff<D>& to, bool buf, const bf16_t* __restrict__ A,
+                                          int64_t ars, const bf16_t* __restrict__ B, int64_t brs, int row0, int T) {
+  if (buf) fetch_tile_buf<D>(tr, to, A, ars, B, brs, row0, T);
+  else fetch_tile<D>(tr, A, ars, B, brs, row0, T);
+}
+
+constexpr float RESCALE_LOG2 = 8.f;  // deferred-rescale threshold (log2 units): P <= 2^8
+
+template <int D, int QG>
+__global__ void __launch_bounds__(NT, 2) attn_fwd4_kernel(AttnParams p) {
+  constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2, BQW = 64 * QG;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];  // [stage][K row image | V tr image]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  const int qt = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z;  // heavy causal tiles first
+  const int hk = h / (p.Hq / p.Hkv);
+  const int T = p.T;
+  const int qbase = qt * BQW + w * 16 * QG;
+  const bf16_t* qb = p.q + b * p.q_sb + h * p.q_sh;
+  const bf16_t* kb = p.k + b * p.k_sb + hk * p.k_sh;
+  const bf16_t* vb = p.v + b * p.v_sb + hk * p.v_sh;
+  const int kv_end = p.causal ? min(T, (qt + 1) * BQW) : T;
+  const int ntiles = (kv_end + BKV - 1) / BKV;
+  const TileOff<D> to = tile_offsets<D>(p.k_st, p.v_st);
+  TileRegs<D> tr;
+  fetch_tile_buf<D>(tr, to, kb, p.k_st, vb, p.v_st, 0, T);
+  mbf16x8 qf[QG][KS];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[qg][ks] = load_frag_global(qb, p.q_st, qbase + 16 * qg + (lane & 15), T, ks, lane);
+  store_tile<D>(tr, smem, nullptr, nullptr, smem + IMG);
+  if (ntiles > 1) fetch_tile_buf<D>(tr, to, kb, p.k_st, vb, p.v_st, BKV, T);
+  __syncthreads();
+  const float c = p.scale * LOG2E;
+  mbf16x8 ones;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.0f;
+  float m[QG];      // the max the exponents are taken against (moves only past the threshold)
+  f32x4 lacc[QG];   // row sums from the matrix pipe (every element = the lane's query row sum)
+  f32x4 o[QG][DT];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    m[qg] = NEG_BIG;
+    lacc[qg] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o[qg][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int j = 0; j < ntiles; ++j) {
+    const int kv0 = j * BKV;
+    const char* Ks = smem + (j & 1) * 2 * IMG;
+    const char* Vs = Ks + IMG;
+    if (j + 1 < ntiles) {  // stage (j+1)&1 was last read in iteration j-1, before its barrier
+      char* nk = smem + ((j + 1) & 1) * 2 * IMG;
+      store_tile<D>(tr, nk, nullptr, nullptr, nk + IMG);
+      if (j + 2 < ntiles) fetch_tile_buf<D>(tr, to, kb, p.k_st, vb, p.v_st, kv0 + 2 * BKV, T);
+    }
+    if (!(p.causal && kv0 > qbase + 16 * QG - 1)) {
+      f32x4 s[QG][4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) s[qg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const mbf16x8 kf = frag_row<D>(Ks, 16 * t, ks, lane);
+#pragma unroll
+          for (int qg = 0; qg < QG; ++qg) s[qg][t] = mfma(kf, qf[qg][ks], s[qg][t]);
+        }
+      }
+      const bool need_mask = kv0 + BKV > T || (p.causal && kv0 + BKV - 1 > qbase);
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) {
+        const int qrow = qbase + 16 * qg + (lane & 15);
+        if (need_mask) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int kv = kv0 + 16 * t + 4 * g + r;
+              if (kv >= T || (p.causal && kv > qrow)) s[qg][t][r] = -INFINITY;
+            }
+        }
+        float mx = NEG_BIG;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) mx = fmaxf(mx, fmaxf(fmaxf(s[qg][t][0], s[qg][t][1]), fmaxf(s[qg][t][2], s[qg][t][3])));
+        mx = max_x16_x32(mx);
+        // deferred rescale: move the exponent's reference only when some row of the wave would see
+        // P > 2^RESCALE_LOG2 (the first tile always moves it: m starts at NEG_BIG)
+        if (__any((mx - m[qg]) * c > RESCALE_LOG2)) {
+          const float m_new = fmaxf(m[qg], mx);
+          const float alpha = fast_exp2((m[qg] - m_new) * c);
+          m[qg] = m_new;
+          lacc[qg] *= alpha;
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt) o[qg][dt] *= alpha;
+        }
+        const float mc = m[qg] * c;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[qg][t][r] = fast_exp2(fmaf(s[qg][t][r], c, -mc));
+      }
+#pragma unroll
+      for (int cc = 0; cc < 2; ++cc) {
+        mbf16x8 pf[QG];
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) {
+          pf[qg] = pack_p(s[qg][2 * cc], s[qg][2 * cc + 1]);
+          lacc[qg] = mfma(ones, pf[qg], lacc[qg]);
+        }
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          const mbf16x8 vf = frag_tr<D>(Vs, 32 * cc, 16 * dt, lane);
+#pragma unroll
+          for (int qg = 0; qg < QG; ++qg) o[qg][dt] = mfma(vf, pf[qg], o[qg][dt]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    const int qrow = qbase + 16 * qg + (lane & 15);
+    const float lsum = lacc[qg][0];
+    if (qrow >= T) continue;
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    bf16_t* ob = p.o + b * p.o_sb + (int64_t)qrow * p.o_st + h * p.o_sh;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      u16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[qg][dt][r] * inv);
+      *reinterpret_cast<u16x4*>(ob + 16 * dt + 4 * g) = v;
+    }
+    if (g == 0) p.lse[((int64_t)b * p.Hq + h) * T + qrow] = (m[qg] * c + log2f(lsum)) / LOG2E;
+  }
+}
+
 // dQ, query-stationary, prefetched K/V tiles; QG query groups of 16 rows per wave (query tile =
 // 64 * QG): every K / V fragment read from LDS feeds QG MFMAs.
 // DB: K/V images double-buffered (one barrier per key tile, as attn_fwd3_kernel) at twice the LDS.
-template <int D, int QG, bool DB = false>
-__global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
+// MINB: workgroups per CU the register budget is sized for (2: <= 256 registers per wave; 1: one wave per
+// SIMD with up to 512, the accumulators in AGPRs — the D = 128 two-group variants)
+template <int D, int QG, bool DB = false, int MINB = 2>
+__global__ void __launch_bounds__(NT, MINB) attn_bwd_dq2_kernel(AttnParams p) {
   constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2, BQW = BQ * QG;
   constexpr int STAGE = 3 * IMG;
   __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * STAGE];
@@ -879,10 +1076,12 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
   const int kv_end = p.causal ? min(T, (qt + 1) * BQW) : T;
   const int ntiles = (kv_end + BKV - 1) / BKV;
   TileRegs<D> tr;
-  fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, 0, T);
+  const bool buf = attn_buf_ok(p);
+  const TileOff<D> to = tile_offsets<D>(p.k_st, p.v_st);
+  fetch_any<D>(tr, to, buf, kb, p.k_st, vb, p.v_st, 0, T);
   if constexpr (DB) {
     store_tile<D>(tr, smem, smem + IMG, smem + 2 * IMG, nullptr);
-    if (ntiles > 1) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, BKV, T);
+    if (ntiles > 1) fetch_any<D>(tr, to, buf, kb, p.k_st, vb, p.v_st, BKV, T);
     __syncthreads();
   }
   for (int j = 0; j < ntiles; ++j) {
@@ -894,13 +1093,13 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dq2_kernel(AttnParams p) {
       if (j + 1 < ntiles) {  // the other stage was last read before the previous barrier
         char* nx = smem + ((j + 1) & 1) * STAGE;
         store_tile<D>(tr, nx, nx + IMG, nx + 2 * IMG, nullptr);
-        if (j + 2 < ntiles) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, kv0 + 2 * BKV, T);
+        if (j + 2 < ntiles) fetch_any<D>(tr, to, buf, kb, p.k_st, vb, p.v_st, kv0 + 2 * BKV, T);
       }
     } else {
       __syncthreads();
       store_tile<D>(tr, Kr, Kt, Vr, nullptr);
       __syncthreads();
-      if (j + 1 < ntiles) fetch_tile<D>(tr, kb, p.k_st, vb, p.v_st, kv0 + BKV, T);
+      if (j + 1 < ntiles) fetch_any<D>(tr, to, buf, kb, p.k_st, vb, p.v_st, kv0 + BKV, T);
     }
     // every key of this tile is in this wave's future (DB: skip the math, not the barrier)
     if (p.causal && kv0 > qbase + 16 * QG - 1) {
@@ -1012,8 +1211,8 @@ __device__ __forceinline__ void fused_dq(const AttnParams& p, const char* DSt, c
 // adds the fp32 result into p.dq_acc ([B][Hq][T][D], zeroed by the delta kernel) with no-return
 // atomics; attn_dq_convert_kernel scales it into dq.  Causal: a query tile only reads the key rows
 // below its last query, which are exactly the rows of the waves that did not skip it.
-template <int D, int KG, bool DB = false, int FQ = 0>
-__global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
+template <int D, int KG, bool DB = false, int FQ = 0, int MINB = 2>
+__global__ void __launch_bounds__(NT, MINB) attn_bwd_dkdv2_kernel(AttnParams p) {
   static_assert(!(DB && FQ), "fused dQ is single-stage");
   constexpr int KS = D / 32, DT = D / 16, IMG = BQ * D * 2, BK = BKV * KG;
   constexpr int STAGE = 4 * IMG + 2 * BQ * 4;  // Q row / Q tr / dO row / dO tr images + lse / delta
@@ -1068,15 +1267,17 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
       sl[BQ + threadIdx.x] = nd;
     }
   };
+  const bool buf = attn_buf_ok(p);
+  const TileOff<D> to = tile_offsets<D>(p.q_st, p.do_st);
   if (q_begin < T) {
-    fetch_tile<D>(tr, qb, p.q_st, dob, p.do_st, q_begin, T);
+    fetch_any<D>(tr, to, buf, qb, p.q_st, dob, p.do_st, q_begin, T);
     fetch_stats(q_begin);
   }
   if constexpr (DB) {
     if (q_begin < T) {
       put(smem);
       if (q_begin + BQ < T) {
-        fetch_tile<D>(tr, qb, p.q_st, dob, p.do_st, q_begin + BQ, T);
+        fetch_any<D>(tr, to, buf, qb, p.q_st, dob, p.do_st, q_begin + BQ, T);
         fetch_stats(q_begin + BQ);
       }
     }
@@ -1094,7 +1295,7 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
       if (q0 + BQ < T) {  // the other stage was last read before the previous barrier
         put(smem + ((j + 1) & 1) * STAGE);
         if (q0 + 2 * BQ < T) {
-          fetch_tile<D>(tr, qb, p.q_st, dob, p.do_st, q0 + 2 * BQ, T);
+          fetch_any<D>(tr, to, buf, qb, p.q_st, dob, p.do_st, q0 + 2 * BQ, T);
           fetch_stats(q0 + 2 * BQ);
         }
       }
@@ -1103,7 +1304,7 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dkdv2_kernel(AttnParams p) {
       put(st);
       __syncthreads();
       if (q0 + BQ < T) {
-        fetch_tile<D>(tr, qb, p.q_st, dob, p.do_st, q0 + BQ, T);
+        fetch_any<D>(tr, to, buf, qb, p.q_st, dob, p.do_st, q0 + BQ, T);
         fetch_stats(q0 + BQ);
       }
     }
@@ -1270,7 +1471,7 @@ int attn_fwd_groups(int D) {
 int attn_fwd_version() {
   static const int v = [] {
     const char* e = getenv("PDA_ATTN_FWD");
-    return e ? atoi(e) : 3;
+    return e ? atoi(e) : 4;
   }();
   return v;
 }
@@ -1290,6 +1491,18 @@ hipError_t attention_fwd(const AttnParams& p, hipStream_t st) {
       } else {
         if (qg == 1) attn_fwd2_kernel<64, 1><<<grid, NT, 0, st>>>(p);
         else attn_fwd2_kernel<64, 2><<<grid, NT, 0, st>>>(p);
+      }
+      return hipGetLastError();
+    }
+    // v4 (default): buffer-descriptor K/V loads need the [T][row stride] spans to fit 31-bit offsets
+    const bool v4_ok = (int64_t)p.T * p.k_st * 2 < ((int64_t)1 << 31) && (int64_t)p.T * p.v_st * 2 < ((int64_t)1 << 31);
+    if (attn_fwd_version() == 4 && v4_ok) {
+      if (p.D == 128) {
+        if (qg == 1) attn_fwd4_kernel<128, 1><<<grid, NT, 0, st>>>(p);
+        else attn_fwd4_kernel<128, 2><<<grid, NT, 0, st>>>(p);
+      } else {
+        if (qg == 1) attn_fwd4_kernel<64, 1><<<grid, NT, 0, st>>>(p);
+        else attn_fwd4_kernel<64, 2><<<grid, NT, 0, st>>>(p);
       }
       return hipGetLastError();
     }
@@ -1375,11 +1588,18 @@ hipError_t attention_bwd(const AttnParams& p, hipStream_t st) {
       const char* e = getenv("PDA_ATTN_BWD_DB");
       return e ? atoi(e) : 0;
     }();
-    if (p.D == 128) {  // (two key groups per wave would exceed the 256-VGPR budget at D = 128)
-      if (db & 1) attn_bwd_dq2_kernel<128, 1, true><<<gq, NT, 0, st>>>(p);
+    static const int g128 = [] {  // PDA_ATTN_BWD128 bit 0: dQ kernel with 2 query groups, bit 1: dK/dV
+      const char* e = getenv("PDA_ATTN_BWD128");  // kernel with 2 key groups (both at one wave per SIMD,
+      return e ? atoi(e) : 0;                      // double-buffered: half the LDS bytes per MFMA)
+    }();
+    if (p.D == 128) {  // (two groups per wave exceed the 256-register budget of 2 waves per SIMD at D = 128)
+      if (g128 & 1) attn_bwd_dq2_kernel<128, 2, true, 1><<<gq2, NT, 0, st>>>(p);
+      else if (db & 1) attn_bwd_dq2_kernel<128, 1, true><<<gq, NT, 0, st>>>(p);
       else attn_bwd_dq2_kernel<128, 1><<<gq, NT, 0, st>>>(p);
       const dim3 gk((p.T + BKV - 1) / BKV, p.Hq, p.B);
-      if (db & 2) attn_bwd_dkdv2_kernel<128, 1, true><<<gk, NT, 0, st>>>(p);
+      const dim3 gk2((p.T + 2 * BKV - 1) / (2 * BKV), p.Hq, p.B);
+      if (g128 & 2) attn_bwd_dkdv2_kernel<128, 2, true, 0, 1><<<gk2, NT, 0, st>>>(p);
+      else if (db & 2) attn_bwd_dkdv2_kernel<128, 1, true><<<gk, NT, 0, st>>>(p);
       else attn_bwd_dkdv2_kernel<128, 1><<<gk, NT, 0, st>>>(p);
     } else {
       // PDA_ATTN_BWD_G64=1: one query / key group per wave at D = 64 (140 / 159 VGPRs: 3 waves per SIMD
