@@ -904,8 +904,8 @@ __device__ __forceinline__ void fetch_any(TileRegs<D>& tr, const TileOff<D>& to,
 
 constexpr float RESCALE_LOG2 = 8.f;  // deferred-rescale threshold (log2 units): P <= 2^8
 
-template <int D, int QG>
-__global__ void __launch_bounds__(NT, 2) attn_fwd4_kernel(AttnParams p) {
+template <int D, int QG, int MINB = 2>
+__global__ void __launch_bounds__(NT, MINB) attn_fwd4_kernel(AttnParams p) {
   constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2, BQW = 64 * QG;
   __shared__ __attribute__((aligned(16))) char smem[4 * IMG];  // [stage][K row image | V tr image]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
@@ -1462,7 +1462,7 @@ int attn_fwd_groups(int D) {
     const char* e = getenv("PDA_ATTN_FWD_QG");
     return e ? atoi(e) : 0;
   }();
-  if (env == 1 || env == 2) return env;
+  if (env == 1 || env == 2 || env == 4) return env;
   (void)D;
   return 2;
 }
@@ -1482,7 +1482,10 @@ hipError_t attention_fwd(const AttnParams& p, hipStream_t st) {
   if (p.D != 64 && p.D != 128) return hipErrorInvalidValue;
   if (p.Hkv <= 0 || p.Hq % p.Hkv) return hipErrorInvalidValue;
   if (p.rope_cos == nullptr) {
-    const int qg = attn_fwd_groups(p.D);
+    // v4 (default): buffer-descriptor K/V loads need the [T][row stride] spans to fit 31-bit offsets
+    const bool v4_ok = (int64_t)p.T * p.k_st * 2 < ((int64_t)1 << 31) && (int64_t)p.T * p.v_st * 2 < ((int64_t)1 << 31);
+    int qg = attn_fwd_groups(p.D);
+    if (qg == 4 && !(attn_fwd_version() == 4 && v4_ok)) qg = 2;  // (4 groups: v4 only)
     dim3 grid((p.T + 64 * qg - 1) / (64 * qg), p.Hq, p.B);
     if (attn_fwd_version() == 2) {
       if (p.D == 128) {
@@ -1494,9 +1497,14 @@ hipError_t attention_fwd(const AttnParams& p, hipStream_t st) {
       }
       return hipGetLastError();
     }
-    // v4 (default): buffer-descriptor K/V loads need the [T][row stride] spans to fit 31-bit offsets
-    const bool v4_ok = (int64_t)p.T * p.k_st * 2 < ((int64_t)1 << 31) && (int64_t)p.T * p.v_st * 2 < ((int64_t)1 << 31);
     if (attn_fwd_version() == 4 && v4_ok) {
+      if (qg == 4) {  // PDA_ATTN_FWD_QG=4: 64 query rows per wave at one wave per SIMD (half the K/V LDS
+                      // reads per MFMA; O in AGPRs)
+        const dim3 g4((p.T + 255) / 256, p.Hq, p.B);
+        if (p.D == 128) attn_fwd4_kernel<128, 4, 1><<<g4, NT, 0, st>>>(p);
+        else attn_fwd4_kernel<64, 4, 1><<<g4, NT, 0, st>>>(p);
+        return hipGetLastError();
+      }
       if (p.D == 128) {
         if (qg == 1) attn_fwd4_kernel<128, 1><<<grid, NT, 0, st>>>(p);
         else attn_fwd4_kernel<128, 2><<<grid, NT, 0, st>>>(p);
