@@ -1861,6 +1861,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("set_gemm_pp", &pda::set_gemm_pp,
         "pipelined 256x256 kernel for plain wide GEMMs: -1 env default (PDA_GEMM_PP), 0 off, 1 on",
         pybind11::arg("on"));
+  m.def("set_splitk_fixup", &pda::set_splitk_fixup,
+        "split-K weight gradients reduced by the GEMM's last split per tile: -1 env default (PDA_SPLITK_FIXUP, "
+        "off), 0 separate reduce launch, 1 on",
+        pybind11::arg("on"));
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"), py::arg("dil"),
         py::arg("bias") = py::none(), py::arg("relu") = false, py::arg("out_f32") = false);
   m.def("split_bf16", &split_bf16, py::arg("x"), py::arg("nseg"), py::arg("lo_mask"), py::arg("stack"));

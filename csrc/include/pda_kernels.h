@@ -199,6 +199,7 @@ hipError_t fill_randint(int64_t* out, int64_t n, uint64_t seed, uint64_t offset,
 // variant >= 0 selects a wide-kernel schedule variant (bit 0 setprio, bit 1 MFMA/ds_read interleave)
 void set_gemm_paths(int wide);
 void set_gemm_pp(int on);  // -1: PDA_GEMM_PP (default on), 0 / 1: force
+void set_splitk_fixup(int on);  // -1: PDA_SPLITK_FIXUP (default off), 0 / 1: force
 int64_t gemm_slab_floats(int64_t M, int64_t N, int64_t K, bool allow_split);
 hipError_t gemm_bf16(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B, bool b_kmajor, int64_t ldb,
                      void* C, bool c_f32, int64_t ldc, int64_t M, int64_t N, int64_t K, const void* bias,

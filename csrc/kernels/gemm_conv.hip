@@ -29,6 +29,7 @@
 #include <cmath>
 
 #include <cstdlib>
+#include <mutex>
 #include <type_traits>
 
 namespace pda {
@@ -2323,17 +2324,67 @@ bool pp_conv_mode() {
   return on;
 }
 
+// PDA_SPLITK_FIXUP=1: split-K weight gradients on the pipelined tile reduce in the kernel (splitk_fixup in
+// gemm_epi.h: the last split of each tile sums the slabs) instead of the separate reduce launch.  Opt-in:
+// measured 7 % slower on GPT-2-medium and 13 % on ResNet-50 (profiles/r6_splitk_fixup_DROPPED.jsonl) —
+// every split's release fence writes its XCD's whole L2 back while the compute stream's kernels fill it,
+// and a deep split (12-48 slabs) serialises the sum on one CU per tile.
+int g_fixup_override = -1;  // set_splitk_fixup(): tests compare both paths in one process
+
+bool splitk_fixup_on() {
+  static const bool on = [] {
+    const char* e = getenv("PDA_SPLITK_FIXUP");
+    return e && e[0] == '1';
+  }();
+  return g_fixup_override >= 0 ? g_fixup_override != 0 : on;
+}
+
+// Arrival counters of the in-kernel split-K fix-up: one zeroed pool per device, handed out round-robin,
+// `tiles` counters per launch.  A launch's last arrivals re-zero their counters, so the pool is all zeros
+// between launches, and two launches share counters only 2^20 tiles of later launches apart (never while
+// both run).  Null (the caller reduces with a separate launch) when disabled, or when the pool would have
+// to be created while `st` is capturing a graph.
+int* splitk_tickets(int64_t tiles, hipStream_t st) {
+  constexpr int64_t kPool = (int64_t)1 << 20;
+  if (!splitk_fixup_on() || tiles <= 0 || tiles > kPool / 4) return nullptr;
+  static std::mutex mu;
+  static int* pool[64] = {};
+  static int64_t next[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (!pool[dev]) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    int* p = nullptr;
+    if (hipMalloc(&p, kPool * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(p, 0, kPool * sizeof(int), st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess) {
+      (void)hipFree(p);
+      return nullptr;
+    }
+    pool[dev] = p;
+  }
+  if (next[dev] + tiles > kPool) next[dev] = 0;
+  int* t = pool[dev] + next[dev];
+  next[dev] += tiles;
+  return t;
+}
+
 // returns hipErrorNotSupported when the pipelined kernel cannot take the shape (the caller falls back)
 template <class LA, class LB>
 hipError_t launch_pp_plain(const LA& la, const LB& lb, int64_t M, int64_t N, int64_t K, Epi epi, hipStream_t st,
                            int splits, float* slab, int* used_out = nullptr) {
   Epi e = epi;
-  if (splits > 1) e.slab = slab;
+  if (splits > 1) {
+    e.slab = slab;
+    // MN-major x MN-major (weight gradients): the kernel's last split of each tile reduces in place
+    if constexpr (!LA::kMajor && !LB::kMajor) e.tickets = splitk_tickets(((M + 255) / 256) * ((N + 255) / 256), st);
+  }
   int used = splits;
   const hipError_t r = gemm_pp(la.p, LA::kMajor, la.ld, lb.p, LB::kMajor, lb.ld, M, N, K, e, splits, -1, st, &used);
   if (used_out) *used_out = used;
   if (r == hipErrorInvalidValue) return hipErrorNotSupported;
-  if (r != hipSuccess || used <= 1) return r;
+  if (r != hipSuccess || used <= 1 || e.tickets) return r;
   int ll = 0;
   while (ll < 4 && (used >> ll) > 16) ++ll;
   const int64_t per_block = 256 >> ll;
@@ -2397,6 +2448,7 @@ bool dgrad_phased(int stride, int dil) { return stride == 1 || dil == 1; }
 // r3_epi_direct_DROPPED_and_transformers.jsonl)
 void set_gemm_paths(int wide) { g_wide_override = wide; }
 void set_gemm_pp(int on) { g_pp_override = on; }
+void set_splitk_fixup(int on) { g_fixup_override = on; }
 
 // slab sizing covers both the 128-tile plan and the wide tile's (possibly deeper) split
 int64_t split_slab_floats(int64_t M, int64_t N, int64_t K, const Plan& p) {

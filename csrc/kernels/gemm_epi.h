@@ -65,6 +65,10 @@ struct Epi {
   const bf16_t* bst_z2;
   const float* bst_mean2;
   float* bst_table2;
+  // in-kernel split-K fix-up (pipelined tile, splitk_fixup below): one zeroed arrival counter per tile of
+  // the launch (indexed by blockIdx.x); the last split of a tile sums the slabs and runs the epilogue, so no
+  // separate reduce launch follows.  Null: the caller reduces the slabs (splitk_reduce_kernel).
+  int* tickets;
 };
 
 // The pipelined 256 x 256 GEMM (gemm_pp.hip); gemm_conv.hip routes plain GEMMs to it.
@@ -328,11 +332,12 @@ __device__ __forceinline__ void epi_bias_cols(const Epi& epi, int64_t n0, int64_
 template <int WCOLS = 4, bool BST = true, int BSTG = PDA_BSTG>
 __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][16 / WCOLS], char* smem, int stats_off,
                                                    const Epi& epi, int64_t m0, int64_t n0, int64_t M, int64_t N, int tm,
-                                                   int split) {
+                                                   int split, bool reduced = false) {
   constexpr int JT = 16 / WCOLS, NT = 128 * WCOLS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wr = wid / WCOLS, wc = wid % WCOLS;
-  if (epi.slab || epi.c_f32) {
+  const bool to_slab = epi.slab && !reduced;  // reduced: acc is the split-K total (splitk_fixup)
+  if (to_slab || epi.c_f32) {
     // fp32 output (split-K slab partials or an fp32 C): 16-B stores straight from the accumulators
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -343,7 +348,7 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][16 / WC
         const int64_t n = n0 + wc * 16 * JT + 16 * j + 4 * (lane >> 4);
         if (n >= N) continue;
         f32x4 v = acc[i][j];
-        if (epi.slab) {
+        if (to_slab) {
           *reinterpret_cast<f32x4*>(epi.slab + (int64_t)split * M * N + m * N + n) = v;
           continue;
         }
@@ -430,6 +435,69 @@ __device__ __forceinline__ void wide_tile_epilogue(const f32x4 (&acc)[8][16 / WC
     if (BST) epi_stats_flush_all(epi, st1, st2, st3, reinterpret_cast<float*>(smem + stats_off), CPR, NT, tm, n0, N);
     else epi_stats_flush(epi, st1, st2, reinterpret_cast<float*>(smem + stats_off), CPR, NT, tm, n0, N);
   }
+}
+
+// In-kernel split-K fix-up (Epi::tickets): every split stores its fp32 partial tile to its slab and takes
+// a ticket; the tile's last arrival sums the S slabs in split order 0..S-1 (its own read back, so the
+// total is the same whichever split arrives last: bitwise run-to-run deterministic) into acc, sums the
+// [split][M] row sums of A into rowsum_out (tile column 0: the bias gradient), re-zeroes the ticket and
+// returns true; the caller then runs the ordinary epilogue on acc (wide_tile_epilogue with reduced =
+// true).  Each XCD has its own L2: the release fence before the ticket writes this split's slab back, the
+// acquire fence after it keeps the last arrival from reading stale lines.  Replaces the separate
+// splitk_reduce_kernel launch, which could only start once the whole GEMM had drained.
+template <int WCOLS = 4>
+__device__ __forceinline__ bool splitk_fixup(f32x4 (&acc)[8][16 / WCOLS], char* smem, const Epi& epi, int64_t m0,
+                                             int64_t n0, int64_t M, int64_t N) {
+  constexpr int JT = 16 / WCOLS;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WCOLS, wc = wid % WCOLS;
+  const int split = blockIdx.y, splits = gridDim.y, ticket = blockIdx.x;
+  float* own = epi.slab + (int64_t)split * M * N;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t m = m0 + wr * 128 + 16 * i + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < JT; ++j) {
+      const int64_t n = n0 + wc * 16 * JT + 16 * j + 4 * (lane >> 4);
+      if (m < M && n < N) *reinterpret_cast<f32x4*>(own + m * N + n) = acc[i][j];
+    }
+  }
+  int* flag = reinterpret_cast<int*>(smem);
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) *flag = atomicAdd(epi.tickets + ticket, 1) == splits - 1 ? 1 : 0;
+  __syncthreads();
+  const bool last = *flag != 0;
+  if (!last) return false;
+  __threadfence();
+  for (int s = 0; s < splits; ++s) {
+    const float* src = epi.slab + (int64_t)s * M * N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t m = m0 + wr * 128 + 16 * i + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < JT; ++j) {
+        const int64_t n = n0 + wc * 16 * JT + 16 * j + 4 * (lane >> 4);
+        if (m >= M || n >= N) continue;
+        const f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + m * N + n));
+        acc[i][j] = s == 0 ? t : acc[i][j] + t;
+      }
+    }
+  }
+  if (epi.rowsum_out && epi.rowsum_mode == 4 && n0 == 0) {
+    const float* rs = (const float*)epi.rowsum;
+    for (int r = tid; r < 256; r += blockDim.x) {
+      const int64_t m = m0 + r;
+      if (m >= M) continue;
+      float v = 0.f;
+      for (int s = 0; s < splits; ++s) v += __builtin_nontemporal_load(rs + (int64_t)s * M + m);
+      if (epi.rowsum_out_bf16) ((bf16_t*)epi.rowsum_out)[m] = f2bf(v);
+      else ((float*)epi.rowsum_out)[m] = v;
+    }
+  }
+  if (tid == 0) epi.tickets[ticket] = 0;
+  __syncthreads();  // every thread has read the flag before the staged epilogue reuses the LDS
+  return true;
 }
 
 // Persistent-kernel variant of the bf16 epilogue (gemm_pp.hip): the next tile's operand DMAs are in

@@ -589,7 +589,14 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
     rs_store();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    wide_tile_epilogue(acc, smem, PP_STATS_OFF, p.epi, m0, n0, p.M, p.N, tm, blockIdx.y);
+    bool reduced = false;
+    if constexpr (!AK && !BK) {  // split-K weight gradients: the in-kernel fix-up when the caller gave tickets
+      if (p.epi.tickets && p.epi.slab) {
+        if (!splitk_fixup(acc, smem, p.epi, m0, n0, p.M, p.N)) return;
+        reduced = true;
+      }
+    }
+    wide_tile_epilogue(acc, smem, PP_STATS_OFF, p.epi, m0, n0, p.M, p.N, tm, blockIdx.y, reduced);
     return;
   }
 
@@ -693,7 +700,14 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm_pp_kernel(PPArgs p) {
   // drain the (zero-filling) DMAs of the tiles past the end before the LDS becomes the staging tile
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  wide_tile_epilogue(acc, smem, PP_STATS_OFF, p.epi, m0, n0, p.M, p.N, tm, blockIdx.y);
+  bool reduced = false;
+  if constexpr (!AK && !BK) {  // split-K weight gradients: the in-kernel fix-up when the caller gave tickets
+    if (p.epi.tickets && p.epi.slab) {
+      if (!splitk_fixup(acc, smem, p.epi, m0, n0, p.M, p.N)) return;
+      reduced = true;
+    }
+  }
+  wide_tile_epilogue(acc, smem, PP_STATS_OFF, p.epi, m0, n0, p.M, p.N, tm, blockIdx.y, reduced);
 }
 
 // ---------------------------------------------------------------- persistent variant
@@ -1330,7 +1344,7 @@ hipError_t gemm_pp(const bf16_t* A, bool a_kmajor, int64_t lda, const bf16_t* B,
   a.epi.nt_store = pp_epi_nt();
   if (splits <= 1) a.epi.slab = nullptr;
   const int var = variant < 0 ? pp_default_variant() : variant;
-  if (var == 200 && !epi.rowsum && !epi.bst_z) {
+  if (var == 200 && !epi.rowsum && !epi.bst_z && !(epi.tickets && splits > 1)) {  // (no fix-up in pp4)
     if (a_kmajor && b_kmajor) return launch_pp4<true, true>(a, splits, st);
     if (a_kmajor) return launch_pp4<true, false>(a, splits, st);
     if (b_kmajor) return launch_pp4<false, true>(a, splits, st);

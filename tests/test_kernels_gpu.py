@@ -171,8 +171,42 @@ def test_gemm_pp_matches_wide_kernel_bitwise_fp32_slabs():
     assert rel_err(outs[0], outs[1]) < 1e-6
 
 
+@pytest.mark.parametrize("M,N,K,f32", [(320, 384, 8192, True), (1024, 1024, 16384, False), (264, 520, 4160, True)])
+def test_splitk_fixup_matches_reduce_launch(M, N, K, f32):
+    """Split-K weight-gradient layout (MN-major x MN-major) on the pipelined tile: the in-kernel fix-up (the
+    last split of each tile sums the slabs) against the separate reduce launch and fp32; the fix-up sums in
+    split order whoever arrives last, so repeated launches (tickets re-zeroed by each launch) are bitwise
+    identical."""
+    torch.manual_seed(31)
+    A, B = torch.randn(K, M), torch.randn(K, N)
+    Ab, Bb = bf(A), bf(B)
+    ref = A.to(torch.bfloat16).float().t() @ B.to(torch.bfloat16).float()
+    outs = {}
+    C().set_gemm_paths(2)
+    try:
+        for fix in (0, 1):
+            C().set_splitk_fixup(fix)
+            runs = []
+            for _ in range(3 if fix else 1):
+                o = torch.full((M, N), float("nan"), device=DEV, dtype=torch.float32 if f32 else torch.bfloat16)
+                for _ in range(5):  # back-to-back launches reuse the ticket pool
+                    C().gemm(Ab, False, M, Bb, False, N, o, N, M, N, K, None, False, True)
+                runs.append(o.clone())
+            outs[fix] = runs
+    finally:
+        C().set_splitk_fixup(-1)
+        C().set_gemm_paths(-1)
+    tol = 1e-5 if f32 else 1e-2
+    for fix, runs in outs.items():
+        assert torch.isfinite(runs[0].float()).all(), fix
+        assert rel_err(runs[0].float().cpu(), ref) < tol, (fix, rel_err(runs[0].float().cpu(), ref))
+    assert all(torch.equal(outs[1][0], r) for r in outs[1][1:])
+    assert rel_err(outs[0][0].float(), outs[1][0].float()) < (1e-6 if f32 else 1e-2)
+
+
+@pytest.mark.parametrize("fix", [1, 0])
 @pytest.mark.parametrize("T,Nout,Kin", [(4096, 1024, 1024), (2048, 512, 768), (3000, 296, 264), (64, 64, 64)])
-def test_gemm_wgrad_db_fused(T, Nout, Kin):
+def test_gemm_wgrad_db_fused(T, Nout, Kin, fix):
     """Linear weight gradient with the bias gradient folded in: dW = dY^T X and db = sum_t dY
     from one pipelined GEMM (split-K: fp32 atomics + cast; no split: direct bf16 store); small shapes
     that do not take the 256x256 path report False and leave db to the caller."""
@@ -181,7 +215,11 @@ def test_gemm_wgrad_db_fused(T, Nout, Kin):
     x = torch.randn(T, Kin)
     dw = torch.empty(Nout, Kin, device=DEV, dtype=torch.bfloat16)
     db = torch.full((Nout,), float("nan"), device=DEV, dtype=torch.bfloat16)
-    done = C().gemm_wgrad_db(bf(dy), bf(x), dw, db)
+    C().set_splitk_fixup(fix)  # split-K: the in-kernel fix-up (1) or the reduce launch (0)
+    try:
+        done = C().gemm_wgrad_db(bf(dy), bf(x), dw, db)
+    finally:
+        C().set_splitk_fixup(-1)
     dyb, xb = dy.to(torch.bfloat16).float(), x.to(torch.bfloat16).float()
     assert rel_err(dw.cpu(), dyb.t() @ xb) < 1e-2
     if (T, Nout, Kin) == (4096, 1024, 1024):
