@@ -217,7 +217,8 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * IMG];
   char* Ks = smem;
   char* Vs = smem + IMG;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  // w wave-uniform (readfirstlane): its tests are scalar branches, not per-lane exec masks
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int hk = h / (p.Hq / p.Hkv);
   const int T = p.T;
@@ -380,7 +381,8 @@ __global__ void __launch_bounds__(NT, 2) attn_bwd_dq_kernel(AttnParams p) {
   char* Kr = smem;
   char* Kt = smem + IMG;
   char* Vr = smem + 2 * IMG;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  // w wave-uniform (readfirstlane): its tests are scalar branches, not per-lane exec masks
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int hk = h / (p.Hq / p.Hkv);
   const int T = p.T;
@@ -460,7 +462,8 @@ __global__ void __launch_bounds__(NT, 1) attn_bwd_dkdv_kernel(AttnParams p) {
   char* Dt = smem + 3 * IMG;
   float* s_lse = reinterpret_cast<float*>(smem + 4 * IMG);
   float* s_dl = s_lse + BQ;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  // w wave-uniform (readfirstlane): its tests are scalar branches, not per-lane exec masks
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const int kt = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int T = p.T, G = p.Hq / p.Hkv;
   const int kvrow = kt * BKV + w * 16 + (lane & 15);
@@ -596,7 +599,8 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd2_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * IMG];
   char* Ks = smem;
   char* Vs = smem + IMG;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  // w wave-uniform (readfirstlane): its tests are scalar branches, not per-lane exec masks
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const int qt = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z;  // heavy causal tiles first
   const int hk = h / (p.Hq / p.Hkv);
   const int T = p.T;
@@ -719,7 +723,8 @@ template <int D, int QG>
 __global__ void __launch_bounds__(NT, 2) attn_fwd3_kernel(AttnParams p) {
   constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2, BQW = 64 * QG;
   __shared__ __attribute__((aligned(16))) char smem[4 * IMG];  // [stage][K row image | V tr image]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  // w wave-uniform (readfirstlane): its tests are scalar branches, not per-lane exec masks
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const int qt = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z;  // heavy causal tiles first
   const int hk = h / (p.Hq / p.Hkv);
   const int T = p.T;
@@ -908,7 +913,8 @@ template <int D, int QG, int MINB = 2>
 __global__ void __launch_bounds__(NT, MINB) attn_fwd4_kernel(AttnParams p) {
   constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2, BQW = 64 * QG;
   __shared__ __attribute__((aligned(16))) char smem[4 * IMG];  // [stage][K row image | V tr image]
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  // w wave-uniform (readfirstlane): its tests are scalar branches, not per-lane exec masks
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const int qt = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z;  // heavy causal tiles first
   const int hk = h / (p.Hq / p.Hkv);
   const int T = p.T;
@@ -1044,7 +1050,8 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dq2_kernel(AttnParams p) {
   constexpr int KS = D / 32, DT = D / 16, IMG = BKV * D * 2, BQW = BQ * QG;
   constexpr int STAGE = 3 * IMG;
   __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * STAGE];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  // w wave-uniform (readfirstlane): its tests are scalar branches, not per-lane exec masks
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const int qt = gridDim.x - 1 - blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int hk = h / (p.Hq / p.Hkv);
   const int T = p.T;
@@ -1123,21 +1130,33 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dq2_kernel(AttnParams p) {
       }
     }
     const bool need_mask = kv0 + BKV > T || (p.causal && kv0 + BKV - 1 > qbase) || qbase + 16 * QG > T;
+    // P, the mask (masked tiles only, branch-free selects under one wave-uniform branch), then dS
 #pragma unroll
-    for (int qg = 0; qg < QG; ++qg) {
-      const int qrow = qbase + 16 * qg + (lane & 15);
+    for (int qg = 0; qg < QG; ++qg)
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float pr = fast_exp2(fmaf(s[qg][t][r], c, -lse2[qg]));
-          if (need_mask) {
+        for (int r = 0; r < 4; ++r) s[qg][t][r] = fast_exp2(fmaf(s[qg][t][r], c, -lse2[qg]));
+    if (need_mask) {
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) {
+        const int qrow = qbase + 16 * qg + (lane & 15);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
             const int kv = kv0 + 16 * t + 4 * g + r;
-            if (qrow >= T || kv >= T || (p.causal && kv > qrow)) pr = 0.f;
+            const bool dead = (qrow >= T) | (kv >= T) | (p.causal & (kv > qrow));
+            s[qg][t][r] = dead ? 0.f : s[qg][t][r];
           }
-          s[qg][t][r] = pr * (dp[qg][t][r] - dl[qg]);
-        }
+      }
     }
+#pragma unroll
+    for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[qg][t][r] = s[qg][t][r] * (dp[qg][t][r] - dl[qg]);
     mbf16x8 sf[2][QG];
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc)
@@ -1220,6 +1239,7 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dkdv2_kernel(AttnParams p) 
   __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * STAGE + KIMG + DSIMG];
   char* const Kt = smem + STAGE;        // [BK keys][D] transposed-read image (FQ)
   char* const DSt = smem + STAGE + KIMG;  // [BK keys][BQ queries] transposed-read image of dS (FQ)
+  // (w left per-lane here: the readfirstlane form spills this kernel at 256 VGPRs)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
   const int kt = blockIdx.x, hq = blockIdx.y, b = blockIdx.z;
   const int T = p.T, G = p.Hq / p.Hkv, hk = hq / G;
@@ -1334,22 +1354,37 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dkdv2_kernel(AttnParams p) 
       }
     }
     const bool need_mask = q0 + BQ > T || kvbase + 16 * KG - 1 >= T || (p.causal && kvbase + 16 * KG - 1 > q0);
+    // P, then (one wave-uniform branch, masked tiles only) the mask as branch-free selects, then dS: a
+    // per-element masked test compiled into 32 scalar branches interleaved with the exponentials
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const f32x4 l4 = *reinterpret_cast<const f32x4*>(s_lse + 16 * t + 4 * g);  // 4 consecutive queries
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int kg = 0; kg < KG; ++kg) s[kg][t][r] = fast_exp2(fmaf(s[kg][t][r], c, -l4[r]));
+    }
+    if (need_mask) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = q0 + 16 * t + 4 * g + r;
+#pragma unroll
+          for (int kg = 0; kg < KG; ++kg) {
+            const int kvrow = kvbase + 16 * kg + (lane & 15);
+            const bool dead = (q >= T) | (kvrow >= T) | (p.causal & (kvrow > q));
+            s[kg][t][r] = dead ? 0.f : s[kg][t][r];
+          }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
       const f32x4 d4 = *reinterpret_cast<const f32x4*>(s_dl + 16 * t + 4 * g);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int q = q0 + 16 * t + 4 * g + r;
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int kg = 0; kg < KG; ++kg) {
-          const int kvrow = kvbase + 16 * kg + (lane & 15);
-          float pr = fast_exp2(fmaf(s[kg][t][r], c, -l4[r]));
-          if (need_mask && (q >= T || kvrow >= T || (p.causal && kvrow > q))) pr = 0.f;
-          s[kg][t][r] = pr;
-          dp[kg][t][r] = pr * (dp[kg][t][r] - d4[r]);  // dS
-        }
-      }
+        for (int kg = 0; kg < KG; ++kg) dp[kg][t][r] = s[kg][t][r] * (dp[kg][t][r] - d4[r]);  // dS
     }
     // pack P and dS to bf16 first: the fp32 S / dP registers are dead before the dV / dK MFMAs
     mbf16x8 pf[2][KG], sf[2][KG];

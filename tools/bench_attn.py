@@ -12,7 +12,8 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# PDA_AB_ROOT: import another build of the package (tools/ab_build.sh) for an A/B on the same box
+sys.path.insert(0, os.environ.get("PDA_AB_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pytorchdistributed_amd._native import C  # noqa: E402
 
 SHAPES = {"gpt2-medium": (16, 1024, 16, 16, 64), "llama3-8b": (1, 4096, 32, 8, 128)}
