@@ -1114,19 +1114,29 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dq2_kernel(AttnParams p) {
       continue;
     }
     f32x4 s[QG][4], dp[QG][4];
+    // key sub-tiles in pairs: four independent accumulation chains per k-step (two chains left each
+    // MFMA waiting on its predecessor's result and each fragment read waited for just in time)
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int tp = 0; tp < 4; tp += 2) {
 #pragma unroll
-      for (int qg = 0; qg < QG; ++qg) s[qg][t] = dp[qg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = tp; t < tp + 2; ++t)
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) s[qg][t] = dp[qg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const mbf16x8 kf = frag_row<D>(Kr, 16 * t, ks, lane);
-        const mbf16x8 vf = frag_row<D>(Vr, 16 * t, ks, lane);
+        mbf16x8 kf[2], vf[2];
 #pragma unroll
-        for (int qg = 0; qg < QG; ++qg) {
-          s[qg][t] = mfma(kf, qf[qg][ks], s[qg][t]);
-          dp[qg][t] = mfma(vf, df[qg][ks], dp[qg][t]);
+        for (int u = 0; u < 2; ++u) {
+          kf[u] = frag_row<D>(Kr, 16 * (tp + u), ks, lane);
+          vf[u] = frag_row<D>(Vr, 16 * (tp + u), ks, lane);
         }
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            s[qg][tp + u] = mfma(kf[u], qf[qg][ks], s[qg][tp + u]);
+            dp[qg][tp + u] = mfma(vf[u], df[qg][ks], dp[qg][tp + u]);
+          }
       }
     }
     const bool need_mask = kv0 + BKV > T || (p.causal && kv0 + BKV - 1 > qbase) || qbase + 16 * QG > T;
@@ -1239,8 +1249,9 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dkdv2_kernel(AttnParams p) 
   __shared__ __attribute__((aligned(16))) char smem[(DB ? 2 : 1) * STAGE + KIMG + DSIMG];
   char* const Kt = smem + STAGE;        // [BK keys][D] transposed-read image (FQ)
   char* const DSt = smem + STAGE + KIMG;  // [BK keys][BQ queries] transposed-read image of dS (FQ)
-  // (w left per-lane here: the readfirstlane form spills this kernel at 256 VGPRs)
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4;
+  // w wave-uniform at D = 128 (scalar branches); per-lane at D = 64, where the readfirstlane form spills
+  const int lane = threadIdx.x & 63, g = lane >> 4;
+  const int w = D == 128 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : threadIdx.x >> 6;
   const int kt = blockIdx.x, hq = blockIdx.y, b = blockIdx.z;
   const int T = p.T, G = p.Hq / p.Hkv, hk = hq / G;
   const int kvbase = kt * BK + w * 16 * KG;  // this wave's keys: kvbase + 16 kg + (lane & 15)
@@ -1338,19 +1349,29 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dkdv2_kernel(AttnParams p) 
       continue;
     }
     f32x4 s[KG][4], dp[KG][4];
+    // query sub-tiles in pairs when one key group leaves two chains per sub-tile (attn_bwd_dq2_kernel)
+    constexpr int TP = KG == 1 ? 2 : 1;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int tp = 0; tp < 4; tp += TP) {
 #pragma unroll
-      for (int kg = 0; kg < KG; ++kg) s[kg][t] = dp[kg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = tp; t < tp + TP; ++t)
+#pragma unroll
+        for (int kg = 0; kg < KG; ++kg) s[kg][t] = dp[kg][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const mbf16x8 qf = frag_row<D>(Qr, 16 * t, ks, lane);
-        const mbf16x8 df = frag_row<D>(Dr, 16 * t, ks, lane);
+        mbf16x8 qf[TP], df[TP];
 #pragma unroll
-        for (int kg = 0; kg < KG; ++kg) {
-          s[kg][t] = mfma(qf, kf[kg][ks], s[kg][t]);  // S^T: [q][kv = lane]
-          dp[kg][t] = mfma(df, vf[kg][ks], dp[kg][t]);
+        for (int u = 0; u < TP; ++u) {
+          qf[u] = frag_row<D>(Qr, 16 * (tp + u), ks, lane);
+          df[u] = frag_row<D>(Dr, 16 * (tp + u), ks, lane);
         }
+#pragma unroll
+        for (int kg = 0; kg < KG; ++kg)
+#pragma unroll
+          for (int u = 0; u < TP; ++u) {
+            s[kg][tp + u] = mfma(qf[u], kf[kg][ks], s[kg][tp + u]);  // S^T: [q][kv = lane]
+            dp[kg][tp + u] = mfma(df[u], vf[kg][ks], dp[kg][tp + u]);
+          }
       }
     }
     const bool need_mask = q0 + BQ > T || kvbase + 16 * KG - 1 >= T || (p.causal && kvbase + 16 * KG - 1 > q0);
