@@ -1140,46 +1140,47 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dq2_kernel(AttnParams p) {
       }
     }
     const bool need_mask = kv0 + BKV > T || (p.causal && kv0 + BKV - 1 > qbase) || qbase + 16 * QG > T;
-    // P, the mask (masked tiles only, branch-free selects under one wave-uniform branch), then dS
+    // per 32-key half cc: P, the mask (masked tiles only: branch-free selects under one wave-uniform
+    // branch), dS, the bf16 pack and the half's dQ MFMAs (the second half's exponentials can issue in the
+    // shadow of the first half's MFMAs)
 #pragma unroll
-    for (int qg = 0; qg < QG; ++qg)
+    for (int cc = 0; cc < 2; ++cc) {
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
+      for (int qg = 0; qg < QG; ++qg)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) s[qg][t][r] = fast_exp2(fmaf(s[qg][t][r], c, -lse2[qg]));
-    if (need_mask) {
+        for (int t = 2 * cc; t < 2 * cc + 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[qg][t][r] = fast_exp2(fmaf(s[qg][t][r], c, -lse2[qg]));
+      if (need_mask) {
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg) {
+          const int qrow = qbase + 16 * qg + (lane & 15);
+#pragma unroll
+          for (int t = 2 * cc; t < 2 * cc + 2; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int kv = kv0 + 16 * t + 4 * g + r;
+              const bool dead = (qrow >= T) | (kv >= T) | (p.causal & (kv > qrow));
+              s[qg][t][r] = dead ? 0.f : s[qg][t][r];
+            }
+        }
+      }
+      mbf16x8 sf[QG];
 #pragma unroll
       for (int qg = 0; qg < QG; ++qg) {
-        const int qrow = qbase + 16 * qg + (lane & 15);
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int t = 2 * cc; t < 2 * cc + 2; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int kv = kv0 + 16 * t + 4 * g + r;
-            const bool dead = (qrow >= T) | (kv >= T) | (p.causal & (kv > qrow));
-            s[qg][t][r] = dead ? 0.f : s[qg][t][r];
-          }
+          for (int r = 0; r < 4; ++r) s[qg][t][r] = s[qg][t][r] * (dp[qg][t][r] - dl[qg]);
+        sf[qg] = pack_p(s[qg][2 * cc], s[qg][2 * cc + 1]);
       }
-    }
-#pragma unroll
-    for (int qg = 0; qg < QG; ++qg)
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s[qg][t][r] = s[qg][t][r] * (dp[qg][t][r] - dl[qg]);
-    mbf16x8 sf[2][QG];
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc)
-#pragma unroll
-      for (int qg = 0; qg < QG; ++qg) sf[cc][qg] = pack_p(s[qg][2 * cc], s[qg][2 * cc + 1]);
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const mbf16x8 ktf = frag_tr<D>(Kt, 32 * cc, 16 * dt, lane);
 #pragma unroll
-        for (int qg = 0; qg < QG; ++qg) dq[qg][dt] = mfma(ktf, sf[cc][qg], dq[qg][dt]);
+        for (int qg = 0; qg < QG; ++qg) dq[qg][dt] = mfma(ktf, sf[qg], dq[qg][dt]);
       }
+    }
     if constexpr (DB) __syncthreads();
   }
 #pragma unroll
@@ -1375,53 +1376,52 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dkdv2_kernel(AttnParams p) 
       }
     }
     const bool need_mask = q0 + BQ > T || kvbase + 16 * KG - 1 >= T || (p.causal && kvbase + 16 * KG - 1 > q0);
-    // P, then (one wave-uniform branch, masked tiles only) the mask as branch-free selects, then dS: a
-    // per-element masked test compiled into 32 scalar branches interleaved with the exponentials
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const f32x4 l4 = *reinterpret_cast<const f32x4*>(s_lse + 16 * t + 4 * g);  // 4 consecutive queries
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int kg = 0; kg < KG; ++kg) s[kg][t][r] = fast_exp2(fmaf(s[kg][t][r], c, -l4[r]));
-    }
-    if (need_mask) {
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = q0 + 16 * t + 4 * g + r;
-#pragma unroll
-          for (int kg = 0; kg < KG; ++kg) {
-            const int kvrow = kvbase + 16 * kg + (lane & 15);
-            const bool dead = (q >= T) | (kvrow >= T) | (p.causal & (kvrow > q));
-            s[kg][t][r] = dead ? 0.f : s[kg][t][r];
-          }
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const f32x4 d4 = *reinterpret_cast<const f32x4*>(s_dl + 16 * t + 4 * g);
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int kg = 0; kg < KG; ++kg) dp[kg][t][r] = s[kg][t][r] * (dp[kg][t][r] - d4[r]);  // dS
-    }
-    // pack P and dS to bf16 first: the fp32 S / dP registers are dead before the dV / dK MFMAs
+    // Per 32-query half cc: P, the mask (masked tiles only: branch-free selects under one branch), dS,
+    // the bf16 packs and the half's dV / dK MFMAs — the second half's exponentials are independent of the
+    // first half's MFMAs, so they can issue in their shadow (a per-element masked test had compiled into
+    // 32 scalar branches interleaved with the exponentials).
     mbf16x8 pf[2][KG], sf[2][KG];
 #pragma unroll
-    for (int cc = 0; cc < 2; ++cc)
+    for (int cc = 0; cc < 2; ++cc) {
+#pragma unroll
+      for (int t = 2 * cc; t < 2 * cc + 2; ++t) {
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(s_lse + 16 * t + 4 * g);  // 4 consecutive queries
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int kg = 0; kg < KG; ++kg) s[kg][t][r] = fast_exp2(fmaf(s[kg][t][r], c, -l4[r]));
+      }
+      if (need_mask) {
+#pragma unroll
+        for (int t = 2 * cc; t < 2 * cc + 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = q0 + 16 * t + 4 * g + r;
+#pragma unroll
+            for (int kg = 0; kg < KG; ++kg) {
+              const int kvrow = kvbase + 16 * kg + (lane & 15);
+              const bool dead = (q >= T) | (kvrow >= T) | (p.causal & (kvrow > q));
+              s[kg][t][r] = dead ? 0.f : s[kg][t][r];
+            }
+          }
+      }
+#pragma unroll
+      for (int t = 2 * cc; t < 2 * cc + 2; ++t) {
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(s_dl + 16 * t + 4 * g);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int kg = 0; kg < KG; ++kg) dp[kg][t][r] = s[kg][t][r] * (dp[kg][t][r] - d4[r]);  // dS
+      }
 #pragma unroll
       for (int kg = 0; kg < KG; ++kg) {
         pf[cc][kg] = pack_p(s[kg][2 * cc], s[kg][2 * cc + 1]);
         sf[cc][kg] = pack_p(dp[kg][2 * cc], dp[kg][2 * cc + 1]);
       }
-    if constexpr (FQ) {  // dS^T -> LDS: key row kl, queries 16 t + 4 g .. +3 (one 8-byte store each)
-      const int kl = w * 16 * KG + (lane & 15);
-      const int sw = (kl >> 1) & 3;
-      char* const rowp = DSt + kl * (BQ * 2) + 8 * g;
-#pragma unroll
-      for (int cc = 0; cc < 2; ++cc)
+      if constexpr (FQ) {  // dS^T -> LDS: key row kl, queries 16 t + 4 g .. +3 (one 8-byte store each)
+        const int kl = w * 16 * KG + (lane & 15);
+        const int sw = (kl >> 1) & 3;
+        char* const rowp = DSt + kl * (BQ * 2) + 8 * g;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           char* const a = rowp + (((2 * cc + h) ^ sw) << 5);
@@ -1432,9 +1432,7 @@ __global__ void __launch_bounds__(NT, MINB) attn_bwd_dkdv2_kernel(AttnParams p) 
                 h ? s16x4{v[4], v[5], v[6], v[7]} : s16x4{v[0], v[1], v[2], v[3]};
           }
         }
-    }
-#pragma unroll
-    for (int cc = 0; cc < 2; ++cc) {
+      }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const mbf16x8 dtf = frag_tr<D>(Dt, 32 * cc, 16 * dt, lane);
