@@ -24,7 +24,7 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2
 // Block-wide merge of per-thread (max, scaled-sum) pairs plus two plain sums. Result on all threads.
 __device__ __forceinline__ void block_lse(float& m, float& s, float& a, float& b) {
   __shared__ float sm[16], ss[16], sa[16], sb[16];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(s, o, 64);

@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(kDecThreads) decode_attn_kernel(DecodeAttnPara
   constexpr int kSteps = G >= 8 ? 4 : kMaxSteps;  // G = 8: fewer rows in flight keeps 1 wave/SIMD spill-free
   constexpr int TILE = KPI * kSteps;  // rows per wave tile
   const int split = blockIdx.x, hkv = blockIdx.y, b = blockIdx.z;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int kk = lane / DCH, c = lane % DCH;
   // graph-replayable decode: the length comes from device memory (pos + 1 of this step)
   const int L = p.L_dev != nullptr ? *p.L_dev + 1 : p.L;

@@ -58,7 +58,7 @@ __global__ void __launch_bounds__(DS_NT) dgrad_stream_kernel(DSArgs a) {
   __shared__ __attribute__((aligned(16))) bf16_t patch[DS_NT / 64][ROWS * DS_PITCH];
   const Epi& e = a.epi;
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nw = blockDim.x >> 6;
   const int N = a.N;
   const int cb = (blockIdx.y * nw + wid) * 64;  // this wave's 64 columns

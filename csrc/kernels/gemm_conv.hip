@@ -552,7 +552,7 @@ __device__ __forceinline__ void tile_epilogue_bf16_impl(const f32x4 (&acc)[BM / 
                                                         int tm, float (&st1)[8], float (&st2)[8]) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   // bf16 output: stage the tile through LDS (row stride BN + 8 elements keeps both the 8-B fragment
   // writes and the 16-B row reads bank-conflict free), then write whole 16-B chunks of rows —
@@ -640,7 +640,7 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(LA la, LB lb, int64_t M, in
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int ntiles = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, ntiles);
@@ -780,7 +780,7 @@ __global__ void __launch_bounds__(NT, 2) conv3x3_halo_kernel(const bf16_t* __res
   char* band = smem;
   char* bst = smem + hg.band_px * 128;  // D weight stages
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int ntiles = gridDim.x;
   const int tile = xcd_remap(blockIdx.x, ntiles);
@@ -933,7 +933,7 @@ __global__ void __launch_bounds__(NT, 1) conv3x3_res64_kernel(const bf16_t* __re
   constexpr int TM = TMW, TN = WN / 16;
   static_assert(BM == 4 * R64_QW, "a tile is 4 image rows");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1, g = lane >> 4;
   const int per = (ntiles + (int)gridDim.x - 1) / (int)gridDim.x;
   const int t_begin = (int)blockIdx.x * per;
@@ -1077,7 +1077,7 @@ __global__ void __launch_bounds__(NT, 2) conv3x3_wgrad_kernel(const bf16_t* __re
   // one dynamic array the compiler drained the next group's DMA before this group's reads)
   __shared__ __attribute__((aligned(16))) char s_st0[WG3_STAGE];
   __shared__ __attribute__((aligned(16))) char s_st1[WG3_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tco = blockIdx.x / g.tiles_ci, tci = blockIdx.x - tco * g.tiles_ci;
   const int co0 = tco * 64, ci0 = tci * 64;
   const int W = g.W, H = g.H, W2 = W + 2;
@@ -1405,7 +1405,7 @@ __global__ void __launch_bounds__(NT, 2) conv_stem_fwd_kernel(const bf16_t* __re
   __shared__ __attribute__((aligned(16))) char s_w[STEMF_W_BYTES];
   __shared__ __attribute__((aligned(16))) char s_b0[STEMF_STAGE];
   __shared__ __attribute__((aligned(16))) char s_b1[STEMF_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1;
   const int rb = blockIdx.x * g.rps, re = min(g.rows, rb + g.rps);
   if (rb >= re) return;
@@ -1506,7 +1506,7 @@ __global__ void __launch_bounds__(NT, 2) conv_stem_wgrad_kernel(const bf16_t* __
   constexpr int DY_BYTES = 128 * 64 * 2;  // [128 px][64 co]: two [64][64] MN-major images
   __shared__ __attribute__((aligned(16))) char s_st0[STEM_STAGE];
   __shared__ __attribute__((aligned(16))) char s_st1[STEM_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int co0 = blockIdx.x * 64;
   const int rb = blockIdx.y * g.rps, re = min(g.rows, rb + g.rps);  // (stem_splits: never empty)
 
@@ -1613,7 +1613,7 @@ __global__ void __launch_bounds__(BIG_NT, 1) gemm_big_kernel(LA la, LB lb, int64
   constexpr int BM = 256, BN = 128, TM = 4, TN = 4;
   constexpr int LPT = LA::NCH + LB::NCH;  // glds per thread per K tile
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = tid >> 8, gtid = tid & 255, gwid = wid & 3;
   const int wm = wid >> 1, wn = wid & 1;
   const int ntiles = gridDim.x;
@@ -1777,7 +1777,7 @@ __global__ void __launch_bounds__(W_NT, 1) gemm_wide_kernel(LA la, LB lb, int64_
                                                            int tiles_n, int ktiles_per_split, Epi epi) {
   static_assert(LA::NCH == 2 && LB::NCH == 2, "64-row / 64-column loaders");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = tid >> 8, gtid = tid & 255, gwid = wid & 3;
   const int wr = wid >> 2, wc = wid & 3;
   const int ntiles = gridDim.x;

@@ -160,7 +160,7 @@ __global__ void __launch_bounds__(kThreads) rownorm_bwd_fused_kernel(const T* __
                                                                      int64_t rows_per_slab, int nslab) {
   static_assert(VPL <= 4, "rows kept in registers");
   __shared__ float red[kRowsPerBlock - 1][2][2048];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_slab;
   const int64_t r1 = min(rows, r0 + rows_per_slab);
   float g[VPL][8], pg[VPL][8], pb[VPL][8];

@@ -43,7 +43,7 @@ __device__ __forceinline__ mbf16x8 i8_to_bf16x8(uint32_t lo, uint32_t hi) {
 template <int MB, int kNB>
 __global__ void __launch_bounds__(kW8Threads) w8_gemm_kernel(W8GemmParams p) {
   constexpr int kW8Rows = 16 * kNB;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int r16 = lane & 15, kg = lane >> 4;
   const int ntile = blockIdx.x, split = blockIdx.y;
   const int kper = p.K / (4 * p.S);
