@@ -1839,6 +1839,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_table", &bn_bwd_table);
   m.def("set_bn_bwd_fused_max_c", &set_bn_bwd_fused_max_c);
   m.def("set_dgrad_stream", [](int64_t m) { pda::set_dgrad_stream((int)m); });
+  m.def("set_fwd_stream", [](int64_t m) { pda::set_fwd_stream((int)m); });
   m.def("set_attn_bwd_fused", [](int64_t m) { pda::attention_bwd_fused_mode() = (int)m; });
   m.def("attn_bwd_fused_mode", []() { return (int64_t)pda::attention_bwd_fused_mode(); });
   m.def("bn_bwd_fused_max_c", []() { return bn_bwd_fused_max_c(); });

@@ -247,6 +247,7 @@ hipError_t conv2d_dgrad(const bf16_t* dy, const bf16_t* w, const bf16_t* wt, voi
                         const uint8_t* addend_bits, hipStream_t st, const BnBwdStats* bst = nullptr);
 // PDA_DGRAD_STREAM at run time (-1: back to the environment's value): 0 off, 1 BN-sums dgrads, 2 all short-K
 void set_dgrad_stream(int mode);
+void set_fwd_stream(int mode);  // -1: PDA_FWD_STREAM (default 1), 0 off, 1 K in {64, 128}, 2 also K = 256
 hipError_t conv2d_wgrad(const bf16_t* dy, const bf16_t* x, void* dw, bool dw_f32, int N, int H, int W, int C,
                         int Cout, int R, int S, int P, int Q, int stride, int pad, int dil, float* slab,
                         hipStream_t st);

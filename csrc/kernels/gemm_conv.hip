@@ -2894,6 +2894,8 @@ hipError_t conv2d_fwd(const bf16_t* x, const bf16_t* w, void* y, bool y_f32, int
   }
   auto mk_b = [&](auto t) { t.p = w; t.rows = Nn; t.K = K; t.ld = K; return t; };
   if (conv_1x1_plain(R, S, stride, pad, dil)) {  // y[NHW, Cout] = x[NHW, C] w[Cout, C]^T
+    // short K (the bottleneck expansions): the streaming kernel (HBM-bound shape, fwd_stream.hip)
+    if (fwd_stream_ok(M, Nn, K, epi)) return fwd_stream(x, w, M, Nn, K, epi, st);
     auto mk_ap = [&](auto t) { t.p = x; t.rows = M; t.K = K; t.ld = C; return t; };
     return dispatch_bn<PlainK, PlainK>(M, Nn, K, p, epi, nullptr, st, mk_ap, mk_b);
   }

@@ -80,6 +80,10 @@ int pp_default_variant();
 bool dgrad_stream_ok(int64_t M, int64_t N, int64_t K, const Epi& epi);
 hipError_t dgrad_stream(const bf16_t* dy, const bf16_t* w, int64_t M, int64_t N, int64_t K, const Epi& epi,
                         hipStream_t st);
+// Streaming short-K (64 / 128 / 256) 1x1 stride-1 forward with the forward BN statistics (fwd_stream.hip)
+bool fwd_stream_ok(int64_t M, int64_t N, int64_t K, const Epi& epi);
+hipError_t fwd_stream(const bf16_t* x, const bf16_t* w, int64_t M, int64_t N, int64_t K, const Epi& epi,
+                      hipStream_t st);
 hipError_t gemm_pp_wgrad(const bf16_t* dy, const bf16_t* x, int Nimg, int H, int W, int C, int Cout, int R, int S,
                          int P, int Q, int stride, int pad, int dil, const Epi& epi, int splits, hipStream_t stream,
                          int* used_splits);

@@ -1058,3 +1058,29 @@ def test_linear_grads_land_in_flat_slots_once(monkeypatch, fused, M, K, N):
         assert b.grad.data_ptr() == fg.grad_view(1).data_ptr()
     assert rel_err(w.grad, dy.float().t() @ x.float()) < 1e-2
     assert rel_err(b.grad, dy.float().sum(0)) < 1e-2
+
+
+@pytest.mark.parametrize("M,Cin,Cout", [(640 * 56 * 56 // 64, 64, 256), (3000, 128, 512), (1000, 256, 1024), (37, 64, 64),
+                                        (4100, 128, 192)])
+def test_fwd_stream_matches_tile(M, Cin, Cout):
+    """Streaming short-K 1x1 forward (fwd_stream.hip) against the 256 x 256 tile and fp32: the same bf16
+    output (same MFMA k order), and BN sums over the stored output (ragged M, N = 64 / 192 column groups)."""
+    torch.manual_seed(41)
+    x = torch.randn(1, 1, M, Cin).to(torch.bfloat16)
+    w = (torch.randn(Cout, 1, 1, Cin) / math.sqrt(Cin)).to(torch.bfloat16)
+    shift = torch.randn(Cout) * 0.1
+    outs = {}
+    try:
+        for mode in (0, 2):
+            C().set_fwd_stream(mode)
+            table = torch.zeros(3, 2, Cout, device=DEV)
+            y = C().conv_fwd_stats(x.to(DEV), w.to(DEV), 1, 0, 1, shift.to(DEV), table)
+            outs[mode] = (y, table.sum(0))
+    finally:
+        C().set_fwd_stream(-1)
+    ref = x.float().reshape(M, Cin) @ w.float().reshape(Cout, Cin).t()
+    for mode, (y, tab) in outs.items():
+        assert rel_err(y.float().cpu().reshape(M, Cout), ref) < 1e-2, mode
+        d = y.float().cpu().reshape(M, Cout) - shift
+        assert rel_err(tab.cpu(), torch.stack([d.sum(0), (d * d).sum(0)])) < 1e-4, mode
+    assert rel_err(outs[0][0].float(), outs[2][0].float()) < 1e-3
