@@ -1299,10 +1299,13 @@ int pp_group_m() {
   return v;
 }
 
+// PDA_PP_VAR: the main-loop schedule.  10 (two MFMA phases per K tile + staggered wave groups) over 2 (staggered
+// four-phase): +1-3 % on the transformer GEMM shapes, Llama-3-8B FSDP +2.6 %, ResNet-50 +0.3-0.6 %, GPT-2 even
+// (profiles/r6_gemm_lab_transformer_fwd.jsonl, r6_pp_var10_ab.jsonl)
 int pp_default_variant() {
   static const int v = [] {
     const char* e = getenv("PDA_PP_VAR");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 10;
   }();
   return v;
 }
