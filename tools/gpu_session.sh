@@ -36,6 +36,9 @@ for step in "$@"; do
                  PDA_DIST_BACKEND=gloo run rehearse_dp4 300 python -u bench.py --gpus 4 --steps 5 --warmup 2 --batch 128 ;;
     rehearse_pp) PDA_DIST_BACKEND=gloo run rehearse_pp 400 python -u -m pytorchdistributed_amd.bench.gpt2xl_pp --gpus 4 --pp 2 --micro 4 --micro-batch 4 --steps 3 --warmup 1 ;;
     gpt2xl_pp) run gpt2xl_pp 600 python -u -m pytorchdistributed_amd.bench.gpt2xl_pp --steps 4 --warmup 2 ;;
+    gpt2xl_pp_il) run gpt2xl_pp_il 600 python -u -m pytorchdistributed_amd.bench.gpt2xl_pp --steps 4 --warmup 2 --schedule interleaved --chunks 2 ;;
+    llama_forced) PDA_FSDP_FORCE_COMM=1 run llama_forced 500 python -u -m pytorchdistributed_amd.bench.llama_fsdp --steps 4 --warmup 2 ;;
+    bench20) run bench20 300 python -u bench.py --steps 20 --warmup 5 ;;
     *) echo "[session] unknown step $step" ;;
   esac
 done
