@@ -1592,10 +1592,14 @@ int64_t attention_bwd_ws_floats(int B, int T, int Hq, int Hkv, int D, bool rope)
 // the atomics).  Measured (profiles/r5_attn_bwd_fused.jsonl): GPT-2-medium 326.1 / 321.8 k vs 315.3 /
 // 318.1 k tok/s on one box; microbench backward 0.4065 vs 0.4176 ms (atomics ~0.05 ms of it).  At
 // D = 128 the fused kernel needs 88.5 KB of LDS (one workgroup per CU): Llama-3-8B 16.9 k vs 18.6 k, off.
+// Round 6: after the branch-free masking and the paired S / dP chains the pair overtook the fused kernel at
+// D = 64 too (microbench 0.341 vs 0.379 ms, GPT-2-medium 322.5-322.7 k vs 321.4-321.5 k tok/s on one box,
+// profiles/r6_attn_bwd_pair_vs_fused.jsonl), so the default is the pair — also atomic-free, i.e.
+// run-to-run deterministic without PDA_DETERMINISTIC.
 int& attention_bwd_fused_mode() {
   static int mode = [] {
     const char* e = getenv("PDA_ATTN_BWD_FUSED");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   return mode;
 }
